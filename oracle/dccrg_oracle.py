@@ -1,0 +1,410 @@
+"""TEST INFRASTRUCTURE ONLY -- Python face of the CPU oracle.
+
+ctypes wrapper over ``oracle/_build/libdccrg_oracle.so`` (the plain-C
+restatement in ``dccrg_oracle.c``) plus pure-Python restatements of the
+reference's per-rank bookkeeping, each citing the reference file:line it
+follows.  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the checker (or the
+timed CPU baseline).  The product package ``dccrg_amd`` never imports it.
+
+Parity pinning: see ``oracle/dccrg_oracle.h`` -- the reference is unbuildable
+in this image (it needs Boost.TTI / Zoltan headers the image lacks), so this
+restatement is pinned by the reference tests' own known answers
+(``tests/golden/*.json``) and the survey's recorded reference outputs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libdccrg_oracle.so")
+
+ERROR_CELL = 0
+ERROR_INDEX = 0xFFFFFFFFFFFFFFFF
+DEFAULT_NEIGHBORHOOD_ID = -0xDCC  # dccrg.hpp:99
+
+
+def build() -> str:
+    """Compile the C restatement (gcc) into oracle/_build/."""
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        u64p = C.POINTER(C.c_uint64)
+        i32p = C.POINTER(C.c_int32)
+        u32p = C.POINTER(C.c_uint32)
+        L.dox_mapping_init.argtypes = [C.c_void_p, u64p, C.c_int32]
+        L.dox_max_possible_refinement_level.argtypes = [u64p]
+        L.dox_get_cell_from_indices.restype = C.c_uint64
+        L.dox_get_cell_from_indices.argtypes = [C.c_void_p, u64p, C.c_int]
+        L.dox_get_indices.argtypes = [C.c_void_p, C.c_uint64, u64p]
+        L.dox_get_refinement_level.argtypes = [C.c_void_p, C.c_uint64]
+        for f in ("dox_get_cell_length_in_indices", "dox_get_parent", "dox_get_child",
+                  "dox_get_level_0_parent"):
+            getattr(L, f).restype = C.c_uint64
+            getattr(L, f).argtypes = [C.c_void_p, C.c_uint64]
+        L.dox_get_all_children.argtypes = [C.c_void_p, C.c_uint64, u64p]
+        L.dox_get_siblings.argtypes = [C.c_void_p, C.c_uint64, u64p]
+        L.dox_map_ids_to_indices.argtypes = [C.c_void_p, u64p, C.c_size_t, u64p, i32p]
+        L.dox_map_indices_to_ids.argtypes = [C.c_void_p, u64p, i32p, C.c_size_t, u64p]
+        L.dox_default_neighborhood.restype = C.c_size_t
+        L.dox_default_neighborhood.argtypes = [C.c_uint, i32p]
+        L.dox_block_first_cell.restype = C.c_uint64
+        L.dox_block_first_cell.argtypes = [C.c_uint64] * 3
+        L.dox_block_owner.restype = C.c_uint64
+        L.dox_block_owner.argtypes = [C.c_uint64] * 3
+        L.dox_grid_create.restype = C.c_void_p
+        L.dox_grid_create.argtypes = [u64p, C.c_int32, C.POINTER(C.c_uint8), u64p, C.c_size_t]
+        L.dox_grid_destroy.argtypes = [C.c_void_p]
+        L.dox_grid_exists.argtypes = [C.c_void_p, C.c_uint64]
+        L.dox_grid_size.restype = C.c_size_t
+        L.dox_grid_size.argtypes = [C.c_void_p]
+        L.dox_grid_cells.restype = C.c_size_t
+        L.dox_grid_cells.argtypes = [C.c_void_p, u64p, C.c_size_t]
+        L.dox_get_existing_cell.restype = C.c_uint64
+        L.dox_get_existing_cell.argtypes = [C.c_void_p, u64p, C.c_int, C.c_int]
+        L.dox_grid_get_child.restype = C.c_uint64
+        L.dox_grid_get_child.argtypes = [C.c_void_p, C.c_uint64]
+        L.dox_update_neighbors_.argtypes = [C.c_void_p, C.c_uint64, u64p]
+        L.dox_find_neighbors_of.restype = C.c_long
+        L.dox_find_neighbors_of.argtypes = [C.c_void_p, C.c_uint64, i32p, C.c_size_t, u64p, i32p,
+                                            C.c_size_t]
+        L.dox_find_neighbors_to.restype = C.c_long
+        L.dox_find_neighbors_to.argtypes = [C.c_void_p, C.c_uint64, i32p, C.c_size_t, u64p,
+                                            C.c_size_t]
+        L.dox_get_face_neighbors_of.restype = C.c_long
+        L.dox_get_face_neighbors_of.argtypes = [C.c_void_p, C.c_uint64, u64p, i32p, C.c_size_t]
+        L.dox_gol_count.argtypes = [C.c_size_t, u64p, u32p, u32p, u32p]
+        L.dox_gol_apply.argtypes = [C.c_size_t, u32p, u32p]
+        L.dox_build_uniform_slot_lists.restype = C.c_long
+        L.dox_build_uniform_slot_lists.argtypes = [C.c_void_p, C.c_uint, u64p, u32p, C.c_size_t]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class _MappingStruct(C.Structure):
+    _fields_ = [("length", C.c_uint64 * 3), ("max_ref_lvl", C.c_int32), ("pad_", C.c_int32),
+                ("last_cell", C.c_uint64)]
+
+
+def default_neighborhood(hood_length: int) -> np.ndarray:
+    """dccrg.hpp:8017-8076 -- the default neighborhood_of items, shape (K, 3)."""
+    out = np.zeros((343, 3), dtype=np.int32)
+    n = lib().dox_default_neighborhood(hood_length, _p(out, C.c_int32))
+    return out[:n].copy()
+
+
+def neighborhood_to(items: np.ndarray) -> np.ndarray:
+    """dccrg.hpp:8070-8075: hood_to = -hood_of."""
+    return (-np.asarray(items, dtype=np.int32)).copy()
+
+
+class Mapping:
+    """dccrg_mapping.hpp:55-690 restated (scalar + batched)."""
+
+    def __init__(self, length: Sequence[int], max_ref_lvl: int = 0):
+        self._m = _MappingStruct()
+        ln = np.array(length, dtype=np.uint64)
+        if lib().dox_mapping_init(C.byref(self._m), _p(ln, C.c_uint64), int(max_ref_lvl)) != 0:
+            raise ValueError("invalid mapping parameters")
+
+    @property
+    def max_ref_lvl(self) -> int:
+        return self._m.max_ref_lvl
+
+    @property
+    def last_cell(self) -> int:
+        return self._m.last_cell
+
+    @property
+    def length(self):
+        return tuple(self._m.length)
+
+    def get_cell_from_indices(self, idx, lvl: int) -> int:
+        a = np.array(idx, dtype=np.uint64)
+        return lib().dox_get_cell_from_indices(C.byref(self._m), _p(a, C.c_uint64), int(lvl))
+
+    def get_indices(self, cell: int):
+        out = np.zeros(3, dtype=np.uint64)
+        lib().dox_get_indices(C.byref(self._m), C.c_uint64(cell), _p(out, C.c_uint64))
+        return tuple(int(v) for v in out)
+
+    def get_refinement_level(self, cell: int) -> int:
+        return lib().dox_get_refinement_level(C.byref(self._m), C.c_uint64(cell))
+
+    def get_cell_length_in_indices(self, cell: int) -> int:
+        return lib().dox_get_cell_length_in_indices(C.byref(self._m), C.c_uint64(cell))
+
+    def get_parent(self, cell: int) -> int:
+        return lib().dox_get_parent(C.byref(self._m), C.c_uint64(cell))
+
+    def get_child(self, cell: int) -> int:
+        return lib().dox_get_child(C.byref(self._m), C.c_uint64(cell))
+
+    def get_level_0_parent(self, cell: int) -> int:
+        return lib().dox_get_level_0_parent(C.byref(self._m), C.c_uint64(cell))
+
+    def get_all_children(self, cell: int):
+        out = np.zeros(8, dtype=np.uint64)
+        lib().dox_get_all_children(C.byref(self._m), C.c_uint64(cell), _p(out, C.c_uint64))
+        return [int(v) for v in out]
+
+    def get_siblings(self, cell: int):
+        out = np.zeros(8, dtype=np.uint64)
+        lib().dox_get_siblings(C.byref(self._m), C.c_uint64(cell), _p(out, C.c_uint64))
+        return [int(v) for v in out]
+
+    def ids_to_indices(self, ids: np.ndarray):
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        idx = np.zeros((ids.size, 3), dtype=np.uint64)
+        lvl = np.zeros(ids.size, dtype=np.int32)
+        lib().dox_map_ids_to_indices(C.byref(self._m), _p(ids, C.c_uint64), ids.size,
+                                     _p(idx, C.c_uint64), _p(lvl, C.c_int32))
+        return idx, lvl
+
+    def indices_to_ids(self, idx: np.ndarray, lvl: np.ndarray) -> np.ndarray:
+        idx = np.ascontiguousarray(idx, dtype=np.uint64).reshape(-1, 3)
+        lvl = np.ascontiguousarray(lvl, dtype=np.int32)
+        out = np.zeros(lvl.size, dtype=np.uint64)
+        lib().dox_map_indices_to_ids(C.byref(self._m), _p(idx, C.c_uint64), _p(lvl, C.c_int32),
+                                     lvl.size, _p(out, C.c_uint64))
+        return out
+
+
+def max_possible_refinement_level(length) -> int:
+    ln = np.array(length, dtype=np.uint64)
+    return lib().dox_max_possible_refinement_level(_p(ln, C.c_uint64))
+
+
+def block_owner(total_cells: int, comm_size: int, level0_cell: int) -> int:
+    """dccrg.hpp:8098-8145."""
+    return lib().dox_block_owner(total_cells, comm_size, level0_cell)
+
+
+def block_first_cell(total_cells: int, comm_size: int, rank: int) -> int:
+    return lib().dox_block_first_cell(total_cells, comm_size, rank)
+
+
+class Grid:
+    """The set of existing leaf cells + the reference's neighbor algorithms."""
+
+    def __init__(self, length, max_ref_lvl=0, periodic=(False, False, False), hood_length=1,
+                 leaves=None):
+        self.mapping = Mapping(length, max_ref_lvl)
+        self.length = tuple(int(v) for v in length)
+        self.periodic = tuple(bool(p) for p in periodic)
+        self.hood_length = int(hood_length)
+        ln = np.array(length, dtype=np.uint64)
+        per = np.array(periodic, dtype=np.uint8)
+        if leaves is None:
+            h = lib().dox_grid_create(_p(ln, C.c_uint64), self.mapping.max_ref_lvl,
+                                      _p(per, C.c_uint8), None, 0)
+        else:
+            lv = np.ascontiguousarray(leaves, dtype=np.uint64)
+            h = lib().dox_grid_create(_p(ln, C.c_uint64), self.mapping.max_ref_lvl,
+                                      _p(per, C.c_uint8), _p(lv, C.c_uint64), lv.size)
+        if not h:
+            raise ValueError("invalid grid")
+        self._h = h
+        self.hood_of = default_neighborhood(self.hood_length)
+        self.hood_to = neighborhood_to(self.hood_of)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().dox_grid_destroy(h)
+            self._h = None
+
+    def cells(self) -> np.ndarray:
+        n = lib().dox_grid_size(self._h)
+        out = np.zeros(n, dtype=np.uint64)
+        lib().dox_grid_cells(self._h, _p(out, C.c_uint64), n)
+        return out
+
+    def exists(self, cell: int) -> bool:
+        return bool(lib().dox_grid_exists(self._h, C.c_uint64(cell)))
+
+    def face_graph(self, cell: int):
+        out = np.zeros(6, dtype=np.uint64)
+        lib().dox_update_neighbors_(self._h, C.c_uint64(cell), _p(out, C.c_uint64))
+        return [int(v) for v in out]
+
+    def find_neighbors_of(self, cell: int, items=None) -> List[Tuple[int, Tuple[int, int, int]]]:
+        items = self.hood_of if items is None else np.ascontiguousarray(items, dtype=np.int32)
+        items = np.ascontiguousarray(items, dtype=np.int32).reshape(-1, 3)
+        cap = 8 * len(items) + 8
+        ids = np.zeros(cap, dtype=np.uint64)
+        off = np.zeros((cap, 3), dtype=np.int32)
+        n = lib().dox_find_neighbors_of(self._h, C.c_uint64(cell), _p(items, C.c_int32),
+                                        len(items), _p(ids, C.c_uint64), _p(off, C.c_int32), cap)
+        if n < 0:
+            raise RuntimeError(f"find_neighbors_of({cell}) failed: {n}")
+        return [(int(ids[i]), (int(off[i, 0]), int(off[i, 1]), int(off[i, 2]))) for i in range(n)]
+
+    def find_neighbors_to(self, cell: int, items=None) -> List[int]:
+        items = self.hood_to if items is None else np.ascontiguousarray(items, dtype=np.int32)
+        items = np.ascontiguousarray(items, dtype=np.int32).reshape(-1, 3)
+        cap = 16 * len(items) + 16
+        ids = np.zeros(cap, dtype=np.uint64)
+        n = lib().dox_find_neighbors_to(self._h, C.c_uint64(cell), _p(items, C.c_int32),
+                                        len(items), _p(ids, C.c_uint64), cap)
+        if n < 0:
+            raise RuntimeError(f"find_neighbors_to({cell}) failed: {n}")
+        return [int(v) for v in ids[:n]]
+
+    def face_neighbors_of(self, cell: int) -> List[Tuple[int, int]]:
+        ids = np.zeros(64, dtype=np.uint64)
+        dirs = np.zeros(64, dtype=np.int32)
+        n = lib().dox_get_face_neighbors_of(self._h, C.c_uint64(cell), _p(ids, C.c_uint64),
+                                            _p(dirs, C.c_int32), 64)
+        if n < 0:
+            raise RuntimeError("face neighbors failed")
+        return [(int(ids[i]), int(dirs[i])) for i in range(n)]
+
+    # ---- per-rank bookkeeping (pure Python restatements) ------------------
+    def owner(self, cell: int, comm_size: int) -> int:
+        """Owner of a cell without load balancing: children stay on the process
+        of their refinement-level-0 ancestor (dccrg.hpp:8116-8145 + refines in
+        place, no migration under DCCRG_NO_LB)."""
+        total = self.length[0] * self.length[1] * self.length[2]
+        return block_owner(total, comm_size, self.mapping.get_level_0_parent(cell))
+
+    def rank_view(self, rank: int, comm_size: int, items_of=None, items_to=None):
+        """Everything one rank derives at initialize() time.
+
+        local cells, neighbors_of / neighbors_to per local cell,
+        local/remote cells on the process boundary (dccrg.hpp:9131-9234,
+        9377-9409), per-peer sorted send/receive lists (dccrg.hpp:8729-8891).
+        """
+        items_of = self.hood_of if items_of is None else np.asarray(items_of, dtype=np.int32)
+        items_to = neighborhood_to(items_of) if items_to is None else items_to
+        local = [int(c) for c in self.cells() if self.owner(int(c), comm_size) == rank]
+        nof: Dict[int, list] = {}
+        nto: Dict[int, list] = {}
+        local_bdy, remote_bdy = set(), set()
+        send: Dict[int, set] = {}
+        recv: Dict[int, set] = {}
+        for c in local:
+            nof[c] = self.find_neighbors_of(c, items_of)
+            nto[c] = self.find_neighbors_to(c, items_to)
+            for n, _ in nof[c]:
+                p = self.owner(n, comm_size)
+                if p != rank:
+                    local_bdy.add(c)
+                    remote_bdy.add(n)
+                    recv.setdefault(p, set()).add(n)
+            for n in nto[c]:
+                p = self.owner(n, comm_size)
+                if p != rank:
+                    local_bdy.add(c)
+                    remote_bdy.add(n)
+                    send.setdefault(p, set()).add(c)
+        return {
+            "local": sorted(local),
+            "neighbors_of": nof,
+            "neighbors_to": nto,
+            "inner": sorted(set(local) - local_bdy),
+            "outer": sorted(local_bdy),
+            "remote": sorted(remote_bdy),
+            "send": {p: sorted(v) for p, v in send.items()},
+            "recv": {p: sorted(v) for p, v in recv.items()},
+        }
+
+
+def iteration_cache_lists(nof: List[Tuple[int, Tuple[int, int, int]]], nto: List[int]):
+    """Neighbor order in the iteration cache, dccrg.hpp:11570-11712.
+
+    Returns (neighbors_of_range, neighbors_to_range) where each item is
+    (id, (x, y, z)).  neighbors_of = [only_of][both], neighbors_to =
+    [both][only_to]; each group is std::set-sorted by (id, offset).
+    """
+    ids_of = sorted(set((i, o) for i, o in nof if i != ERROR_CELL))
+    ids_to = sorted(set((i, (0, 0, 0)) for i in nto if i != ERROR_CELL))
+    only_to = set(ids_to)
+    both, only_of = set(), set()
+    to_set = set(ids_to)
+    for n in ids_of:
+        tmp = (n[0], (0, 0, 0))
+        only_to.discard(tmp)
+        if tmp in to_set:
+            both.add(n)
+        else:
+            only_of.add(n)
+    only_of, both, only_to = sorted(only_of), sorted(both), sorted(only_to)
+    return only_of + both, both + only_to
+
+
+def gol_reference_run(length, periodic, hood_length, alive0: np.ndarray, steps: int):
+    """Uniform level-0 grid, game of life with the reference's rule over the
+    reference's neighbors_of lists (face-graph walk).  alive0 is indexed by
+    cell id - 1.  Returns (alive, live_neighbor_count) after ``steps``."""
+    g = Grid(length, 0, periodic, hood_length)
+    n = int(np.prod(length))
+    k = len(g.hood_of)
+    row_ptr = np.zeros(n + 1, dtype=np.uint64)
+    cap = n * k
+    slots = np.zeros(cap, dtype=np.uint32)
+    tot = lib().dox_build_uniform_slot_lists(g._h, hood_length, _p(row_ptr, C.c_uint64),
+                                             _p(slots, C.c_uint32), cap)
+    if tot < 0:
+        raise RuntimeError("slot list build failed")
+    alive = np.ascontiguousarray(alive0, dtype=np.uint32).copy()
+    count = np.zeros(n, dtype=np.uint32)
+    for _ in range(steps):
+        lib().dox_gol_count(n, _p(row_ptr, C.c_uint64), _p(slots, C.c_uint32),
+                            _p(alive, C.c_uint32), _p(count, C.c_uint32))
+        lib().dox_gol_apply(n, _p(alive, C.c_uint32), _p(count, C.c_uint32))
+    return alive, count
+
+
+class GolLists:
+    """Pre-built explicit lists for repeated stepping (cpu_baseline)."""
+
+    def __init__(self, length, periodic, hood_length):
+        self.grid = Grid(length, 0, periodic, hood_length)
+        self.n = int(np.prod(length))
+        k = len(self.grid.hood_of)
+        self.row_ptr = np.zeros(self.n + 1, dtype=np.uint64)
+        self.slots = np.zeros(self.n * k, dtype=np.uint32)
+        tot = lib().dox_build_uniform_slot_lists(self.grid._h, hood_length,
+                                                 _p(self.row_ptr, C.c_uint64),
+                                                 _p(self.slots, C.c_uint32), self.n * k)
+        if tot < 0:
+            raise RuntimeError("slot list build failed")
+
+    def step(self, alive: np.ndarray, count: np.ndarray):
+        lib().dox_gol_count(self.n, _p(self.row_ptr, C.c_uint64), _p(self.slots, C.c_uint32),
+                            _p(alive, C.c_uint32), _p(count, C.c_uint32))
+        lib().dox_gol_apply(self.n, _p(alive, C.c_uint32), _p(count, C.c_uint32))
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    """Seed function for reproducible random initial states."""
+    with np.errstate(over="ignore"):
+        z = (np.asarray(x, dtype=np.uint64) + np.uint64(0x9E3779B97F4A7C15))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def random_alive(ids: np.ndarray, p_permille: int = 200) -> np.ndarray:
+    """alive = splitmix64(id) % 1000 < p_permille (bit-exact on CPU and GPU)."""
+    return (splitmix64(ids) % np.uint64(1000) < np.uint64(p_permille)).astype(np.uint32)
