@@ -1,0 +1,120 @@
+"""ctypes binding of libdccrgx.so (include/dccrgx.h).
+
+The product path: every call goes to the HIP library; there is no CPU
+fallback.  Importing this module on a machine without the built library
+raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdccrgx.so")
+
+DCCRGX_OK = 0
+ERROR_CELL = 0
+ERROR_INDEX = 0xFFFFFFFFFFFFFFFF
+DEFAULT_NEIGHBORHOOD_ID = -0xDCC
+CELLS_LOCAL, CELLS_INNER, CELLS_OUTER, CELLS_REMOTE = 0, 1, 2, 3
+WAIT_ALL, WAIT_RECEIVES, WAIT_SENDS = 0, 1, 2
+REGION_ALL, REGION_INNER, REGION_OUTER = 0, 1, 2
+OP_LENGTH_IN_INDICES, OP_PARENT, OP_LEVEL_0_PARENT, OP_CHILD = 0, 1, 2, 3
+
+ERRORS = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "ERCCL", 5: "ERANGE", 6: "ESTATE",
+          7: "ENOTFOUND", 8: "EINTERNAL"}
+
+
+class DccrgxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"dccrgx {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Mapping_t(C.Structure):
+    _fields_ = [("length", C.c_uint64 * 3), ("max_ref_lvl", C.c_int32), ("reserved", C.c_int32)]
+
+
+class GridParams_t(C.Structure):
+    _fields_ = [("length", C.c_uint64 * 3), ("max_ref_lvl", C.c_int32),
+                ("neighborhood_length", C.c_uint32), ("periodic", C.c_uint8 * 3),
+                ("reserved", C.c_uint8 * 5)]
+
+
+class GridInfo_t(C.Structure):
+    _fields_ = [("n_local", C.c_uint64), ("first_local", C.c_uint64), ("n_slots", C.c_uint64),
+                ("layout", C.c_uint64 * 4), ("max_ref_lvl", C.c_int32), ("uniform", C.c_int32),
+                ("rank", C.c_int32), ("comm_size", C.c_int32)]
+
+
+# every symbol include/dccrgx.h declares, with its ctypes signature
+_vp = C.c_void_p
+_u64p = C.POINTER(C.c_uint64)
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+_szp = C.POINTER(C.c_size_t)
+SIGNATURES = {
+    "dccrgx_last_error": (C.c_char_p, []),
+    "dccrgx_version": (C.c_int, []),
+    "dccrgx_ctx_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
+    "dccrgx_ctx_destroy": (C.c_int, [_vp]),
+    "dccrgx_get_unique_id": (C.c_int, [C.c_char_p]),
+    "dccrgx_ctx_comm_init": (C.c_int, [_vp, C.c_char_p]),
+    "dccrgx_ctx_compute_stream": (C.c_int, [_vp, C.POINTER(_vp)]),
+    "dccrgx_ctx_synchronize": (C.c_int, [_vp]),
+    "dccrgx_max_possible_refinement_level": (C.c_int, [_u64p, _i32p]),
+    "dccrgx_last_cell": (C.c_int, [C.POINTER(Mapping_t), _u64p]),
+    "dccrgx_map_ids_to_indices": (C.c_int, [C.POINTER(Mapping_t), _vp, C.c_size_t, _vp, _vp, _vp]),
+    "dccrgx_map_indices_to_ids": (C.c_int, [C.POINTER(Mapping_t), _vp, _vp, C.c_size_t, _vp, _vp]),
+    "dccrgx_map_ids_op": (C.c_int, [C.POINTER(Mapping_t), C.c_int, _vp, C.c_size_t, _vp, _vp]),
+    "dccrgx_grid_create": (C.c_int, [_vp, C.POINTER(GridParams_t), _u64p, C.c_size_t, C.POINTER(_vp)]),
+    "dccrgx_grid_destroy": (C.c_int, [_vp]),
+    "dccrgx_grid_get_info": (C.c_int, [_vp, C.POINTER(GridInfo_t)]),
+    "dccrgx_add_neighborhood": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t]),
+    "dccrgx_remove_neighborhood": (C.c_int, [_vp, C.c_int32]),
+    "dccrgx_get_neighborhood": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t, _szp]),
+    "dccrgx_get_cells": (C.c_int, [_vp, C.c_int32, C.c_int32, _u64p, C.c_size_t, _szp]),
+    "dccrgx_neighbors_of": (C.c_int, [_vp, C.c_int32, _vp, C.c_size_t, _vp, _vp, _vp, C.c_size_t, _vp]),
+    "dccrgx_neighbors_to": (C.c_int, [_vp, C.c_int32, _vp, C.c_size_t, _vp, _vp, C.c_size_t, _vp]),
+    "dccrgx_get_peers": (C.c_int, [_vp, C.c_int32, C.c_int32, _i32p, _u64p, C.c_size_t, _szp]),
+    "dccrgx_get_peer_cells": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, _u64p, C.c_size_t, _szp]),
+    "dccrgx_field_create": (C.c_int, [_vp, C.c_uint32, _i32p]),
+    "dccrgx_field_device_ptr": (C.c_int, [_vp, C.c_int32, C.POINTER(_vp), _u64p]),
+    "dccrgx_slots_of": (C.c_int, [_vp, _vp, C.c_size_t, _vp, _vp]),
+    "dccrgx_field_write_local": (C.c_int, [_vp, C.c_int32, _vp, C.c_size_t]),
+    "dccrgx_field_read_local": (C.c_int, [_vp, C.c_int32, _vp, C.c_size_t]),
+    "dccrgx_field_read_remote": (C.c_int, [_vp, C.c_int32, C.c_int32, _vp, C.c_size_t]),
+    "dccrgx_halo_start": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t]),
+    "dccrgx_halo_wait": (C.c_int, [_vp, C.c_int32, C.c_int32]),
+    "dccrgx_halo_update": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t]),
+    "dccrgx_halo_pack_to": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t, C.c_int32, _vp, C.c_size_t, _szp]),
+    "dccrgx_halo_unpack_from": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t, C.c_int32, _vp, C.c_size_t]),
+    "dccrgx_halo_self": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t]),
+    "dccrgx_gol_compute": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "dccrgx_gol_step": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "dccrgx_field_init_hash": (C.c_int, [_vp, C.c_int32, C.c_uint32]),
+    "dccrgx_kernel_timer": (C.c_int, [_vp, C.c_int32, C.POINTER(C.c_double), _u64p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libdccrgx.so; raise if it has not been built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import "
+                              f"__graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status: int):
+    if status != DCCRGX_OK:
+        raise DccrgxError(status, lib().dccrgx_last_error().decode(errors="replace"))

@@ -1,0 +1,286 @@
+// core.hip -- errors, context, mapping parameters and the batched id<->index
+// mapping kernels (dccrg_mapping.hpp re-designed for gfx950: one lane per id,
+// magic-number 64-bit division, no loops over levels beyond a branch-free
+// compare chain).
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+
+#include "internal.hpp"
+
+namespace dccrgx {
+
+static thread_local char g_err[1024] = "";
+
+int set_error(int code, const char* fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+// dccrg_mapping.hpp:317-330 (double arithmetic, as the reference)
+int max_possible_level(const uint64_t length[3])
+{
+    const uint64_t grid_length = length[0] * length[1] * length[2];
+    int lvl = 0;
+    double current_last = 0;
+    while (current_last <= double(~uint64_t(0))) {
+        current_last += double(grid_length) * std::pow(8.0, double(lvl));
+        lvl++;
+    }
+    return lvl - 2;
+}
+
+int make_map_params(const dccrgx_mapping* m, MapParams* out)
+{
+    DX_CHECK(m && out, DCCRGX_EINVAL, "null mapping");
+    DX_CHECK(m->length[0] && m->length[1] && m->length[2], DCCRGX_EINVAL,
+             "all lengths must be > 0 (dccrg_length.hpp:97-110)");
+    const int maxp = max_possible_level(m->length);
+    int M = m->max_ref_lvl < 0 ? maxp : m->max_ref_lvl;
+    DX_CHECK(M <= maxp && M < MAX_LEVELS - 2, DCCRGX_EINVAL,
+             "maximum refinement level %d exceeds the possible %d", M, maxp);
+    MapParams p{};
+    std::memcpy(p.length, m->length, sizeof(p.length));
+    p.max_lvl = M;
+    p.nlevel0 = m->length[0] * m->length[1] * m->length[2];
+    uint64_t first = 1;
+    for (int l = 0; l < MAX_LEVELS; l++) {
+        p.first_id[l] = first;
+        if (l <= M) first += p.nlevel0 * ((uint64_t)1 << (3 * l));
+    }
+    p.last_cell = p.first_id[M + 1] - 1;  // update_last_cell, dccrg_mapping.hpp:679-687
+    p.div_lx = make_divider(m->length[0]);
+    p.div_lxly = make_divider(m->length[0] * m->length[1]);
+    *out = p;
+    return DCCRGX_OK;
+}
+
+Partition make_partition(uint64_t total, int comm_size)
+{
+    Partition P{};
+    P.total = total;
+    P.comm_size = comm_size;
+    const uint64_t cs = (uint64_t)comm_size;
+    if (total < cs) P.cpp = 1;
+    else if (total % cs > 0) P.cpp = total / cs + 1;
+    else P.cpp = total / cs;
+    P.fewer = P.cpp * cs - total;
+    P.split = P.fewer * (P.cpp - 1);
+    P.div_cpp = make_divider(P.cpp);
+    P.div_cpp1 = make_divider(P.cpp > 1 ? P.cpp - 1 : 1);
+    return P;
+}
+
+// ---------------------------------------------------------------------------
+// mapping kernels
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_ids_to_indices(MapParams p, const uint64_t* __restrict__ ids,
+                                                        size_t n, uint64_t* __restrict__ idx3,
+                                                        int32_t* __restrict__ lvl)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t o[3];
+        int l;
+        map_indices(p, ids[i], o, &l);
+        if (idx3) {
+            idx3[3 * i + 0] = o[0];
+            idx3[3 * i + 1] = o[1];
+            idx3[3 * i + 2] = o[2];
+        }
+        if (lvl) lvl[i] = l;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_indices_to_ids(MapParams p, const uint64_t* __restrict__ idx3,
+                                                        const int32_t* __restrict__ lvl, size_t n,
+                                                        uint64_t* __restrict__ ids)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t c[3] = {idx3[3 * i], idx3[3 * i + 1], idx3[3 * i + 2]};
+        ids[i] = map_cell(p, c, lvl[i]);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ids_op(MapParams p, int op, const uint64_t* __restrict__ ids,
+                                                size_t n, uint64_t* __restrict__ out)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t c = ids[i];
+        uint64_t idx[3];
+        int l;
+        const bool ok = map_indices(p, c, idx, &l);
+        uint64_t r = 0;
+        switch (op) {
+        case DCCRGX_OP_LENGTH_IN_INDICES:  // dccrg_mapping.hpp:298-311
+            r = ok ? ((uint64_t)1 << (p.max_lvl - l)) : DCCRGX_ERROR_INDEX;
+            break;
+        case DCCRGX_OP_PARENT:  // dccrg_mapping.hpp:368-384
+            r = !ok ? 0 : (l == 0 ? c : map_cell(p, idx, l - 1));
+            break;
+        case DCCRGX_OP_LEVEL_0_PARENT:  // dccrg_mapping.hpp:480-494
+            r = !ok ? 0 : (l == 0 ? c : map_cell(p, idx, 0));
+            break;
+        case DCCRGX_OP_CHILD:  // dccrg_mapping.hpp:339-356
+            r = !ok ? 0 : (l >= p.max_lvl ? c : map_cell(p, idx, l + 1));
+            break;
+        }
+        out[i] = r;
+    }
+}
+
+static unsigned grid_for(size_t n)
+{
+    size_t g = (n + 255) / 256;
+    if (g > 256 * 16) g = 256 * 16;  // grid-stride beyond 16 blocks per CU
+    if (g == 0) g = 1;
+    return (unsigned)g;
+}
+
+}  // namespace dccrgx
+
+using namespace dccrgx;
+
+extern "C" {
+
+const char* dccrgx_last_error(void) { return g_err; }
+int dccrgx_version(void) { return DCCRGX_VERSION; }
+
+int dccrgx_max_possible_refinement_level(const uint64_t length[3], int32_t* out)
+{
+    DX_CHECK(length && out, DCCRGX_EINVAL, "null argument");
+    *out = max_possible_level(length);
+    return DCCRGX_OK;
+}
+
+int dccrgx_last_cell(const dccrgx_mapping* map, uint64_t* out)
+{
+    MapParams p;
+    DX_TRY(make_map_params(map, &p));
+    *out = p.last_cell;
+    return DCCRGX_OK;
+}
+
+int dccrgx_map_ids_to_indices(const dccrgx_mapping* map, const uint64_t* ids, size_t n,
+                              uint64_t* idx3, int32_t* lvl, void* stream)
+{
+    MapParams p;
+    DX_TRY(make_map_params(map, &p));
+    if (n == 0) return DCCRGX_OK;
+    DX_CHECK(ids, DCCRGX_EINVAL, "null ids");
+    hipLaunchKernelGGL(k_ids_to_indices, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p,
+                       ids, n, idx3, lvl);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+int dccrgx_map_indices_to_ids(const dccrgx_mapping* map, const uint64_t* idx3, const int32_t* lvl,
+                              size_t n, uint64_t* ids, void* stream)
+{
+    MapParams p;
+    DX_TRY(make_map_params(map, &p));
+    if (n == 0) return DCCRGX_OK;
+    DX_CHECK(idx3 && lvl && ids, DCCRGX_EINVAL, "null argument");
+    hipLaunchKernelGGL(k_indices_to_ids, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p,
+                       idx3, lvl, n, ids);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+int dccrgx_map_ids_op(const dccrgx_mapping* map, int op, const uint64_t* ids, size_t n,
+                      uint64_t* out, void* stream)
+{
+    MapParams p;
+    DX_TRY(make_map_params(map, &p));
+    DX_CHECK(op >= 0 && op <= DCCRGX_OP_CHILD, DCCRGX_EINVAL, "unknown op %d", op);
+    if (n == 0) return DCCRGX_OK;
+    DX_CHECK(ids && out, DCCRGX_EINVAL, "null argument");
+    hipLaunchKernelGGL(k_ids_op, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, op, ids,
+                       n, out);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+int dccrgx_ctx_create(int device, int rank, int comm_size, dccrgx_ctx** out)
+{
+    DX_CHECK(out, DCCRGX_EINVAL, "null out");
+    DX_CHECK(comm_size >= 1 && rank >= 0 && rank < comm_size, DCCRGX_EINVAL,
+             "bad rank %d / comm size %d", rank, comm_size);
+    int ndev = 0;
+    DX_HIP(hipGetDeviceCount(&ndev));
+    DX_CHECK(device >= 0 && device < ndev, DCCRGX_EINVAL, "device %d of %d", device, ndev);
+    DX_HIP(hipSetDevice(device));
+    auto* c = new dccrgx_ctx();
+    c->device = device;
+    c->rank = rank;
+    c->comm_size = comm_size;
+    DX_HIP(hipStreamCreateWithFlags(&c->compute, hipStreamNonBlocking));
+    DX_HIP(hipStreamCreateWithFlags(&c->comm, hipStreamNonBlocking));
+    DX_HIP(hipEventCreateWithFlags(&c->ev_compute, hipEventDisableTiming));
+    DX_HIP(hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
+    *out = c;
+    return DCCRGX_OK;
+}
+
+int dccrgx_ctx_destroy(dccrgx_ctx* c)
+{
+    if (!c) return DCCRGX_OK;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->compute);
+    hipStreamSynchronize(c->comm);
+    if (c->has_comm) ncclCommDestroy(c->nccl);
+    hipEventDestroy(c->ev_compute);
+    hipEventDestroy(c->ev_comm);
+    hipStreamDestroy(c->compute);
+    hipStreamDestroy(c->comm);
+    delete c;
+    return DCCRGX_OK;
+}
+
+int dccrgx_get_unique_id(uint8_t uid_out[128])
+{
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    DX_RCCL(ncclGetUniqueId(&id));
+    std::memcpy(uid_out, &id, 128);
+    return DCCRGX_OK;
+}
+
+int dccrgx_ctx_comm_init(dccrgx_ctx* c, const uint8_t uid[128])
+{
+    DX_CHECK(c && uid, DCCRGX_EINVAL, "null argument");
+    DX_CHECK(!c->has_comm, DCCRGX_ESTATE, "communicator already initialised");
+    DX_HIP(hipSetDevice(c->device));
+    ncclUniqueId id;
+    std::memcpy(&id, uid, 128);
+    DX_RCCL(ncclCommInitRank(&c->nccl, c->comm_size, id, c->rank));
+    c->has_comm = true;
+    return DCCRGX_OK;
+}
+
+int dccrgx_ctx_compute_stream(dccrgx_ctx* c, void** s)
+{
+    DX_CHECK(c && s, DCCRGX_EINVAL, "null argument");
+    *s = (void*)c->compute;
+    return DCCRGX_OK;
+}
+
+int dccrgx_ctx_synchronize(dccrgx_ctx* c)
+{
+    DX_CHECK(c, DCCRGX_EINVAL, "null ctx");
+    DX_HIP(hipSetDevice(c->device));
+    DX_HIP(hipStreamSynchronize(c->comm));
+    DX_HIP(hipStreamSynchronize(c->compute));
+    return DCCRGX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,529 @@
+// gol.hip -- game-of-life stencil over a rank's slab (the user hot loop of
+// examples/game_of_life.cpp:54-79 and tests/game_of_life/scalability3d.cpp:
+// 136-165, executed on the device with the neighbor gather staged in LDS).
+//
+// Fast path (the default 26-item cube, i.e. neighborhood length 1): each
+// workgroup owns a TA x TB tile of the (A, B) plane and marches along the
+// slab axis C.  Every plane is read from HBM once into a double-buffered LDS
+// tile (+1 apron in A and B, periodic wrap in index space), the 3x3 box sum
+// of the plane is formed from LDS row sums and kept in registers, and the
+// 27-point sum of plane c is S(c-1) + S(c) + S(c+1) - centre.  HBM traffic per
+// cell: 4 B read (is_alive) + 4 B write (next is_alive) + 4 B write
+// (live_neighbor_count) = 12 B -- the algorithmic minimum.
+//
+// Any other neighborhood (face neighbors, length >= 2, user neighborhoods)
+// uses the generic item loop (one lane per cell, neighbor slots computed in
+// closed form) -- same results, not bandwidth-optimised.
+#include <algorithm>
+
+#include "grid.hpp"
+
+namespace dccrgx {
+
+struct GolArgs {
+    const uint32_t* in;
+    uint32_t* out;
+    uint32_t* cnt;
+    uint64_t LA, LB, S;
+    uint64_t lo, hi;      // local lin range
+    int64_t cbase;        // canonical slice of storage slice 0
+    int64_t s0, s1;       // storage slices to compute [s0, s1)
+    int64_t chunk;        // slices per workgroup
+    uint32_t tiles_a, tiles_b;
+    int32_t perA, perB;
+};
+
+__device__ __forceinline__ uint32_t alive_bit(uint32_t v) { return v != 0u ? 1u : 0u; }
+
+// reference rule, examples/game_of_life.cpp:68-79
+__device__ __forceinline__ uint32_t gol_rule(uint32_t count, uint32_t v)
+{
+    return count == 3u ? 1u : (count == 2u ? v : 0u);
+}
+
+// TA x TB tile, NA cells per thread along A (stride 256/ (TB/NB)), NB rows per thread
+template <int TA, int TB, int NA, int NB>
+__global__ void __launch_bounds__(256) k_gol26(GolArgs g)
+{
+    constexpr int TXA = TA / NA;           // threads along A
+    constexpr int TYB = 256 / TXA;         // threads along B
+    static_assert(TYB * NB == TB, "tile shape");
+    constexpr int WA = TA + 2, WB = TB + 2;
+    constexpr int E = WA * WB;
+    constexpr int NL = (E + 255) / 256;    // tile elements loaded per thread
+    __shared__ uint32_t tile[2][WB][WA];
+
+    const int t = threadIdx.x;
+    const int tx = t % TXA, ty = t / TXA;
+    const uint32_t tiles = g.tiles_a * g.tiles_b;
+    const uint32_t tile_id = blockIdx.x % tiles;
+    const int64_t chunk_id = blockIdx.x / tiles;
+    const int64_t a0 = (int64_t)(tile_id % g.tiles_a) * TA;
+    const int64_t b0 = (int64_t)(tile_id / g.tiles_a) * TB;
+    const int64_t c0 = g.s0 + chunk_id * g.chunk;
+    const int64_t c1 = min(g.s1, c0 + g.chunk);
+    if (c0 >= c1) return;
+
+    // global element offsets within a plane for this thread's tile loads (-1: zero)
+    int64_t goff[NL];
+#pragma unroll
+    for (int i = 0; i < NL; i++) {
+        const int e = t + 256 * i;
+        goff[i] = -1;
+        if (e < E) {
+            const int r = e / WA, q = e - r * WA;
+            int64_t a = a0 - 1 + q, b = b0 - 1 + r;
+            bool ok = true;
+            if (a < 0 || a >= (int64_t)g.LA) {
+                if (g.perA) a = ug_wrap(a, (int64_t)g.LA);
+                else ok = false;
+            }
+            if (b < 0 || b >= (int64_t)g.LB) {
+                if (g.perB) b = ug_wrap(b, (int64_t)g.LB);
+                else ok = false;
+            }
+            if (ok) goff[i] = a + (int64_t)g.LA * b;
+        }
+    }
+    uint32_t pre[NL];
+    auto fetch = [&](int64_t sc) {
+        const uint32_t* plane = g.in + (uint64_t)sc * g.S;
+#pragma unroll
+        for (int i = 0; i < NL; i++) pre[i] = goff[i] >= 0 ? plane[goff[i]] : 0u;
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+            const int e = t + 256 * i;
+            if (e < E) (&tile[buf][0][0])[e] = pre[i];
+        }
+    };
+    // 3x3 box sums of the current LDS plane for this thread's cells, and centres
+    uint32_t Sx[NB][NA], Vx[NB][NA];
+    auto boxsum = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < NA; i++) {
+            const int q = tx + TXA * i + 1;
+            uint32_t hs[NB + 2];
+#pragma unroll
+            for (int r = 0; r < NB + 2; r++) {
+                const int rr = ty * NB + r;
+                hs[r] = alive_bit(tile[buf][rr][q - 1]) + alive_bit(tile[buf][rr][q]) +
+                        alive_bit(tile[buf][rr][q + 1]);
+            }
+#pragma unroll
+            for (int k = 0; k < NB; k++) {
+                Sx[k][i] = hs[k] + hs[k + 1] + hs[k + 2];
+                Vx[k][i] = tile[buf][ty * NB + k + 1][q];
+            }
+        }
+    };
+
+    uint32_t Sp[NB][NA], Sc[NB][NA], Vc[NB][NA];
+    // prologue: planes c0-1 and c0
+    fetch(c0 - 1);
+    stash(0);
+    fetch(c0);
+    __syncthreads();
+    boxsum(0);
+#pragma unroll
+    for (int k = 0; k < NB; k++)
+#pragma unroll
+        for (int i = 0; i < NA; i++) Sp[k][i] = Sx[k][i];
+    stash(1);
+    fetch(c0 + 1);
+    __syncthreads();
+    boxsum(1);
+#pragma unroll
+    for (int k = 0; k < NB; k++)
+#pragma unroll
+        for (int i = 0; i < NA; i++) {
+            Sc[k][i] = Sx[k][i];
+            Vc[k][i] = Vx[k][i];
+        }
+    int buf = 0;
+    for (int64_t c = c0; c < c1; c++) {
+        // `pre` holds plane c+1
+        stash(buf);
+        if (c + 2 <= c1) fetch(c + 2);
+        __syncthreads();
+        boxsum(buf);
+        buf ^= 1;
+        const int64_t cg = c + g.cbase;  // canonical slice
+#pragma unroll
+        for (int k = 0; k < NB; k++) {
+            const int64_t b = b0 + ty * NB + k;
+#pragma unroll
+            for (int i = 0; i < NA; i++) {
+                const int64_t a = a0 + tx + TXA * i;
+                const uint32_t count = Sp[k][i] + Sc[k][i] + Sx[k][i] - alive_bit(Vc[k][i]);
+                if (a < (int64_t)g.LA && b < (int64_t)g.LB) {
+                    const uint64_t lin = (uint64_t)a + g.LA * ((uint64_t)b + g.LB * (uint64_t)cg);
+                    if (lin >= g.lo && lin < g.hi) {
+                        const uint64_t s = (uint64_t)c * g.S + (uint64_t)a + g.LA * (uint64_t)b;
+                        g.cnt[s] = count;
+                        g.out[s] = gol_rule(count, Vc[k][i]);
+                    }
+                }
+                Sp[k][i] = Sc[k][i];
+                Sc[k][i] = Sx[k][i];
+                Vc[k][i] = Vx[k][i];
+            }
+        }
+    }
+}
+
+// LB == 1 (2-D and 1-D grids): one row per plane; rows b-1 / b+1 are the same
+// row (periodic B) or absent.
+template <int TA, int NA>
+__global__ void __launch_bounds__(256) k_gol26_row(GolArgs g, uint32_t mult)
+{
+    constexpr int WA = TA + 2;
+    constexpr int NL = (WA + 255) / 256;
+    __shared__ uint32_t tile[2][WA];
+    const int t = threadIdx.x;
+    const uint32_t tile_id = blockIdx.x % g.tiles_a;
+    const int64_t chunk_id = blockIdx.x / g.tiles_a;
+    const int64_t a0 = (int64_t)tile_id * TA;
+    const int64_t c0 = g.s0 + chunk_id * g.chunk;
+    const int64_t c1 = min(g.s1, c0 + g.chunk);
+    if (c0 >= c1) return;
+    int64_t goff[NL];
+#pragma unroll
+    for (int i = 0; i < NL; i++) {
+        const int e = t + 256 * i;
+        goff[i] = -1;
+        if (e < WA) {
+            int64_t a = a0 - 1 + e;
+            bool ok = true;
+            if (a < 0 || a >= (int64_t)g.LA) {
+                if (g.perA) a = ug_wrap(a, (int64_t)g.LA);
+                else ok = false;
+            }
+            if (ok) goff[i] = a;
+        }
+    }
+    uint32_t pre[NL];
+    auto fetch = [&](int64_t sc) {
+        const uint32_t* plane = g.in + (uint64_t)sc * g.S;
+#pragma unroll
+        for (int i = 0; i < NL; i++) pre[i] = goff[i] >= 0 ? plane[goff[i]] : 0u;
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+            const int e = t + 256 * i;
+            if (e < WA) tile[buf][e] = pre[i];
+        }
+    };
+    uint32_t Sx[NA], Vx[NA];
+    auto rowsum = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < NA; i++) {
+            const int q = t + 256 * i + 1;
+            Sx[i] = mult * (alive_bit(tile[buf][q - 1]) + alive_bit(tile[buf][q]) +
+                            alive_bit(tile[buf][q + 1]));
+            Vx[i] = tile[buf][q];
+        }
+    };
+    uint32_t Sp[NA], Sc[NA], Vc[NA];
+    fetch(c0 - 1);
+    stash(0);
+    fetch(c0);
+    __syncthreads();
+    rowsum(0);
+#pragma unroll
+    for (int i = 0; i < NA; i++) Sp[i] = Sx[i];
+    stash(1);
+    fetch(c0 + 1);
+    __syncthreads();
+    rowsum(1);
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+        Sc[i] = Sx[i];
+        Vc[i] = Vx[i];
+    }
+    int buf = 0;
+    for (int64_t c = c0; c < c1; c++) {
+        stash(buf);
+        if (c + 2 <= c1) fetch(c + 2);
+        __syncthreads();
+        rowsum(buf);
+        buf ^= 1;
+        const int64_t cg = c + g.cbase;
+#pragma unroll
+        for (int i = 0; i < NA; i++) {
+            const int64_t a = a0 + t + 256 * i;
+            const uint32_t count = Sp[i] + Sc[i] + Sx[i] - alive_bit(Vc[i]);
+            if (a < (int64_t)g.LA) {
+                const uint64_t lin = (uint64_t)a + g.LA * (uint64_t)cg;
+                if (lin >= g.lo && lin < g.hi) {
+                    const uint64_t s = (uint64_t)c * g.S + (uint64_t)a;
+                    g.cnt[s] = count;
+                    g.out[s] = gol_rule(count, Vc[i]);
+                }
+            }
+            Sp[i] = Sc[i];
+            Sc[i] = Sx[i];
+            Vc[i] = Vx[i];
+        }
+    }
+}
+
+// generic neighborhood: one lane per local cell, closed-form neighbor slots
+__global__ void __launch_bounds__(256) k_gol_items(UGeom g, const uint32_t* __restrict__ in,
+                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ cnt,
+                                                   const int32_t* __restrict__ items, int K,
+                                                   uint64_t lin0, uint64_t n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const uint64_t soff = (uint64_t)(-g.cbase * (int64_t)g.S);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t lin = lin0 + i;
+        int64_t a, b, c;
+        ug_decompose(g, lin, a, b, c);
+        uint32_t count = 0;
+        for (int k = 0; k < K; k++) {
+            const int32_t* d = items + 3 * k;
+            int64_t a2 = a + d[0], b2 = b + d[1], c2 = c + d[2];
+            if (a2 < 0 || a2 >= (int64_t)g.LA) {
+                if (!g.perA) continue;
+                a2 = ug_wrap(a2, (int64_t)g.LA);
+            }
+            if (b2 < 0 || b2 >= (int64_t)g.LB) {
+                if (!g.perB) continue;
+                b2 = ug_wrap(b2, (int64_t)g.LB);
+            }
+            if ((c2 < 0 || c2 >= (int64_t)g.LC) && !g.perC) continue;
+            count += alive_bit(in[ug_slot(g, a2, b2, c2)]);
+        }
+        const uint64_t s = lin + soff;
+        cnt[s] = count;
+        out[s] = gol_rule(count, in[s]);
+    }
+}
+
+// deterministic synthetic initial state: alive = splitmix64(id) % 1000 < permille
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) k_init_hash(uint32_t* __restrict__ f, uint64_t lin0, uint64_t n,
+                                                   uint64_t soff, uint32_t permille)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t id = lin0 + i + 1;
+        f[lin0 + i + soff] = (splitmix64(id) % 1000u) < permille ? 1u : 0u;
+    }
+}
+
+static unsigned grid_for(uint64_t n)
+{
+    uint64_t g = (n + 255) / 256;
+    if (g > 256 * 16) g = 256 * 16;
+    if (g == 0) g = 1;
+    return (unsigned)g;
+}
+
+int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out, const Field& cnt,
+               int64_t s0, int64_t s1, hipStream_t st)
+{
+    const UGeom& u = grid->g;
+    if (s1 <= s0 || grid->n_local == 0) return DCCRGX_OK;
+    if (!h.cube1) {
+        // local lin range of the slices
+        const int64_t S = (int64_t)u.S;
+        const uint64_t l0 = std::max<int64_t>((s0 + u.cbase) * S, (int64_t)u.lo);
+        const uint64_t l1 = std::min<int64_t>((s1 + u.cbase) * S, (int64_t)u.hi);
+        if (l1 <= l0) return DCCRGX_OK;
+        hipLaunchKernelGGL(k_gol_items, dim3(grid_for(l1 - l0)), dim3(256), 0, st, u,
+                           (const uint32_t*)in.ptr, (uint32_t*)out.ptr, (uint32_t*)cnt.ptr, h.d_of_c, h.K,
+                           l0, l1 - l0);
+        DX_HIP(hipGetLastError());
+        return DCCRGX_OK;
+    }
+    GolArgs a{};
+    a.in = (const uint32_t*)in.ptr;
+    a.out = (uint32_t*)out.ptr;
+    a.cnt = (uint32_t*)cnt.ptr;
+    a.LA = u.LA;
+    a.LB = u.LB;
+    a.S = u.S;
+    a.lo = u.lo;
+    a.hi = u.hi;
+    a.cbase = u.cbase;
+    a.s0 = s0;
+    a.s1 = s1;
+    a.perA = u.perA;
+    a.perB = u.perB;
+    const int64_t nsl = s1 - s0;
+    if (u.LB == 1) {
+        constexpr int TA = 1024, NA = 4;
+        a.tiles_a = (uint32_t)((u.LA + TA - 1) / TA);
+        a.tiles_b = 1;
+        int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(nsl, (2048 + a.tiles_a - 1) / a.tiles_a));
+        a.chunk = (nsl + chunks - 1) / chunks;
+        chunks = (nsl + a.chunk - 1) / a.chunk;
+        const uint32_t mult = u.perB ? 3u : 1u;
+        hipLaunchKernelGGL((k_gol26_row<TA, NA>), dim3((unsigned)(a.tiles_a * chunks)), dim3(256), 0, st, a,
+                           mult);
+    } else {
+        constexpr int TA = 64, TB = 16, NA = 1, NB = 4;
+        a.tiles_a = (uint32_t)((u.LA + TA - 1) / TA);
+        a.tiles_b = (uint32_t)((u.LB + TB - 1) / TB);
+        const int64_t tiles = (int64_t)a.tiles_a * a.tiles_b;
+        int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(nsl, (2048 + tiles - 1) / tiles));
+        a.chunk = (nsl + chunks - 1) / chunks;
+        chunks = (nsl + a.chunk - 1) / a.chunk;
+        DX_CHECK(tiles * chunks < (int64_t)UINT32_MAX, DCCRGX_EINVAL, "grid too large for one launch");
+        hipLaunchKernelGGL((k_gol26<TA, TB, NA, NB>), dim3((unsigned)(tiles * chunks)), dim3(256), 0, st, a);
+    }
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+// explicit grids: CSR gather (explicit.hip)
+int explicit_gol(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out, const Field& cnt,
+                 int32_t region, hipStream_t st);
+
+struct TimerPool {
+    std::vector<hipEvent_t> ev;
+    size_t used = 0;
+    bool on = false;
+};
+static std::map<const dccrgx_grid*, TimerPool> g_timers;
+
+static int timed(dccrgx_grid* grid, bool begin, hipStream_t st)
+{
+    auto it = g_timers.find(grid);
+    if (it == g_timers.end() || !it->second.on) return DCCRGX_OK;
+    TimerPool& T = it->second;
+    if (T.used == T.ev.size()) {
+        hipEvent_t e;
+        DX_HIP(hipEventCreate(&e));
+        T.ev.push_back(e);
+    }
+    (void)begin;
+    DX_HIP(hipEventRecord(T.ev[T.used++], st));
+    return DCCRGX_OK;
+}
+
+static int compute_region(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out,
+                          const Field& cnt, int32_t region, hipStream_t st)
+{
+    if (!grid->uniform) return explicit_gol(grid, h, in, out, cnt, region, st);
+    const UGeom& u = grid->g;
+    const int64_t all0 = u.pad, all1 = (int64_t)u.nslices - u.pad;
+    int64_t r[2][2] = {{0, 0}, {0, 0}};
+    if (region == DCCRGX_REGION_ALL) {
+        r[0][0] = all0;
+        r[0][1] = all1;
+    } else if (region == DCCRGX_REGION_INNER) {
+        r[0][0] = h.inner_s0;
+        r[0][1] = h.inner_s1;
+    } else {
+        r[0][0] = all0;
+        r[0][1] = std::min(h.inner_s0, all1);
+        r[1][0] = std::max(h.inner_s1, all0);
+        r[1][1] = all1;
+        if (h.inner_s1 <= h.inner_s0) {  // no inner slices: everything is outer
+            r[0][1] = all1;
+            r[1][0] = r[1][1] = 0;
+        }
+    }
+    for (auto& x : r) {
+        if (x[1] <= x[0]) continue;
+        DX_TRY(timed(grid, true, st));
+        DX_TRY(gol_launch(grid, h, in, out, cnt, x[0], x[1], st));
+        DX_TRY(timed(grid, false, st));
+    }
+    return DCCRGX_OK;
+}
+
+}  // namespace dccrgx
+
+using namespace dccrgx;
+
+extern "C" {
+
+static int gol_fields(dccrgx_grid* grid, int32_t a, int32_t b, int32_t c)
+{
+    const int32_t f[3] = {a, b, c};
+    for (int i = 0; i < 3; i++) {
+        DX_CHECK(f[i] >= 0 && (size_t)f[i] < grid->fields.size(), DCCRGX_EINVAL, "bad field %d", f[i]);
+        DX_CHECK(grid->fields[f[i]].elem == 4, DCCRGX_EINVAL, "game of life fields are 4-byte");
+    }
+    DX_CHECK(a != b && a != c && b != c, DCCRGX_EINVAL, "fields must be distinct (double buffered)");
+    return DCCRGX_OK;
+}
+
+int dccrgx_gol_compute(dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t fout, int32_t fcnt,
+                       int32_t region)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    const Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    DX_TRY(gol_fields(grid, fin, fout, fcnt));
+    DX_CHECK(region >= DCCRGX_REGION_ALL && region <= DCCRGX_REGION_OUTER, DCCRGX_EINVAL, "bad region");
+    return compute_region(grid, *h, grid->fields[fin], grid->fields[fout], grid->fields[fcnt], region,
+                          grid->ctx->compute);
+}
+
+int dccrgx_gol_step(dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t fout, int32_t fcnt)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    const Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    DX_TRY(gol_fields(grid, fin, fout, fcnt));
+    // scalability3d.cpp:122-166: start halo, inner cells, wait, outer cells
+    DX_TRY(dccrgx_halo_start(grid, hood_id, &fin, 1));
+    DX_TRY(dccrgx_gol_compute(grid, hood_id, fin, fout, fcnt, DCCRGX_REGION_INNER));
+    DX_TRY(dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL));
+    DX_TRY(dccrgx_gol_compute(grid, hood_id, fin, fout, fcnt, DCCRGX_REGION_OUTER));
+    return DCCRGX_OK;
+}
+
+int dccrgx_field_init_hash(dccrgx_grid* grid, int32_t fid, uint32_t permille)
+{
+    DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    DX_CHECK(grid->fields[fid].elem == 4, DCCRGX_EINVAL, "4-byte field expected");
+    DX_CHECK(grid->uniform, DCCRGX_EINVAL, "uniform grids only");
+    if (!grid->n_local) return DCCRGX_OK;
+    const uint64_t soff = (uint64_t)(-grid->g.cbase * (int64_t)grid->g.S);
+    hipLaunchKernelGGL(k_init_hash, dim3(grid_for(grid->n_local)), dim3(256), 0, grid->ctx->compute,
+                       (uint32_t*)grid->fields[fid].ptr, grid->g.lo, grid->n_local, soff, permille);
+    DX_HIP(hipGetLastError());
+    DX_HIP(hipStreamSynchronize(grid->ctx->compute));
+    return DCCRGX_OK;
+}
+
+int dccrgx_kernel_timer(dccrgx_grid* grid, int32_t reset, double* ms, uint64_t* launches)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    TimerPool& T = g_timers[grid];
+    if (reset) {
+        DX_HIP(hipStreamSynchronize(grid->ctx->compute));
+        T.used = 0;
+        T.on = reset > 0;
+        if (ms) *ms = 0;
+        if (launches) *launches = 0;
+        return DCCRGX_OK;
+    }
+    DX_HIP(hipStreamSynchronize(grid->ctx->compute));
+    double tot = 0;
+    for (size_t i = 0; i + 1 < T.used; i += 2) {
+        float x = 0;
+        DX_HIP(hipEventElapsedTime(&x, T.ev[i], T.ev[i + 1]));
+        tot += x;
+    }
+    if (ms) *ms = tot;
+    if (launches) *launches = T.used / 2;
+    return DCCRGX_OK;
+}
+
+}  // extern "C"

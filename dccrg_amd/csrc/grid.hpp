@@ -1,0 +1,165 @@
+// grid.hpp -- dccrgx_grid internals: uniform implicit layout, neighborhoods,
+// per-peer halo plans, field pools.
+#pragma once
+
+#include "internal.hpp"
+
+namespace dccrgx {
+
+// Canonical axes (A fastest, C slowest with extent > 1 unless 1-D) so that
+// the 0-based cell index lin = a + LA*(b + LB*c) equals id - 1 for level-0
+// cells (dccrg_mapping.hpp:154-209 at level 0).  The block partition
+// (dccrg.hpp:8098-8145) then cuts the C axis into slabs: each rank stores its
+// slab plus `pad` ghost slices on both sides, addressed with an UNWRAPPED c
+// (periodic wrap of A and B is done in index space by the kernels).
+struct UGeom {
+    uint64_t LA, LB, LC, S;  // S = LA * LB (one slice)
+    uint64_t N;              // total level-0 cells
+    uint64_t lo, hi;         // local lin range [lo, hi)
+    int64_t cbase;           // canonical slice held in storage slice 0
+    uint64_t nslices;        // storage slices (local + 2 * pad)
+    Divider dA, dS;
+    Partition part;
+    int32_t perA, perB, perC;
+    int32_t rank;
+    int32_t M;               // max refinement level (offsets are in units of 2^M)
+    int32_t pad;             // ghost slices on each side
+    int32_t perm[3];         // canonical axis -> original axis
+};
+
+__host__ __device__ inline void ug_decompose(const UGeom& g, uint64_t lin, int64_t& a, int64_t& b,
+                                             int64_t& c)
+{
+    const uint64_t cc = divide(lin, g.dS);
+    const uint64_t rem = lin - cc * g.S;
+    const uint64_t bb = divide(rem, g.dA);
+    a = (int64_t)(rem - bb * g.LA);
+    b = (int64_t)bb;
+    c = (int64_t)cc;
+}
+
+__host__ __device__ inline int64_t ug_wrap(int64_t x, int64_t L)
+{
+    int64_t r = x % L;
+    return r < 0 ? r + L : r;
+}
+
+// neighbor of canonical (a,b,c) at item d: wrapped lin and unwrapped c.
+// false when the item falls outside a non-periodic grid (dropped, as the
+// reference drops it: dccrg.hpp:4670-4672)
+__host__ __device__ inline bool ug_neighbor(const UGeom& g, int64_t a, int64_t b, int64_t c,
+                                            const int32_t* d, uint64_t& nlin, int64_t& cu)
+{
+    int64_t a2 = a + d[0], b2 = b + d[1], c2 = c + d[2];
+    cu = c2;
+    if (a2 < 0 || a2 >= (int64_t)g.LA) {
+        if (!g.perA) return false;
+        a2 = ug_wrap(a2, (int64_t)g.LA);
+    }
+    if (b2 < 0 || b2 >= (int64_t)g.LB) {
+        if (!g.perB) return false;
+        b2 = ug_wrap(b2, (int64_t)g.LB);
+    }
+    if (c2 < 0 || c2 >= (int64_t)g.LC) {
+        if (!g.perC) return false;
+        c2 = ug_wrap(c2, (int64_t)g.LC);
+    }
+    nlin = (uint64_t)a2 + g.LA * ((uint64_t)b2 + g.LB * (uint64_t)c2);
+    return true;
+}
+
+__host__ __device__ inline bool ug_local(const UGeom& g, uint64_t lin) { return lin >= g.lo && lin < g.hi; }
+
+__host__ __device__ inline int ug_owner(const UGeom& g, uint64_t lin) { return part_owner(g.part, lin + 1); }
+
+// storage slot of canonical (a, b, unwrapped c)
+__host__ __device__ inline uint64_t ug_slot(const UGeom& g, int64_t a, int64_t b, int64_t cu)
+{
+    return (uint64_t)a + g.LA * ((uint64_t)b + g.LB * (uint64_t)(cu - g.cbase));
+}
+
+struct Field {
+    void* ptr = nullptr;
+    uint32_t elem = 0;
+};
+
+struct PeerPlan {
+    int peer = -1;
+    // cells this rank sends to `peer` (ascending ids) -- dccrg.hpp:8754-8850
+    std::vector<uint64_t> send_ids;
+    uint64_t* d_send_slots = nullptr;  // storage slot of each sent cell
+    bool send_direct = false;          // slots contiguous: send straight from the field
+    uint64_t send_slot0 = 0;
+    // cells this rank receives from `peer` (ascending ids) -- dccrg.hpp:8852-8891
+    std::vector<uint64_t> recv_ids;
+    bool recv_direct = false;          // one ghost slot per cell, contiguous: receive in place
+    uint64_t recv_slot0 = 0;
+    uint64_t n_unpack = 0;             // (dst slot, message index) pairs otherwise
+    uint64_t* d_unpack_dst = nullptr;
+    uint64_t* d_unpack_src = nullptr;
+    // staging (allocated on first use, grown as needed)
+    void* d_send_buf = nullptr;
+    size_t send_buf_bytes = 0;
+    void* d_recv_buf = nullptr;
+    size_t recv_buf_bytes = 0;
+};
+
+struct CopySeg {
+    uint64_t dst, src, n;  // contiguous slot run
+};
+
+struct Hood {
+    int32_t id = 0;
+    std::vector<int32_t> items;    // original (x, y, z) items, hood_of
+    std::vector<int32_t> of_c;     // canonical hood_of
+    std::vector<int32_t> to_c;     // canonical hood_to = -hood_of (dccrg.hpp:8070-8075)
+    int32_t* d_of_c = nullptr;
+    int32_t* d_to_c = nullptr;
+    int32_t K = 0;
+    bool cube1 = false;            // the full 26-item cube: fast stencil path
+    // classification, dccrg.hpp:9131-9409
+    std::vector<uint64_t> outer;   // ascending
+    std::vector<uint64_t> remote;  // ascending
+    std::vector<PeerPlan> peers;   // ascending peer rank
+    // periodic self copies into pad slots
+    std::vector<CopySeg> self_segs;  // contiguous runs (memcpy)
+    uint64_t n_self_scatter = 0;     // non-contiguous remainder (kernel)
+    uint64_t* d_self_dst = nullptr;
+    uint64_t* d_self_src = nullptr;
+    // slice ranges for the overlap split (storage slice indices, inclusive-exclusive)
+    int64_t inner_s0 = 0, inner_s1 = 0;  // fully local and only local reads
+    bool pending = false;                // halo started, not waited
+    std::vector<int32_t> pending_fields; // fields of the started halo
+};
+
+}  // namespace dccrgx
+
+struct dccrgx_grid {
+    dccrgx::Ctx* ctx = nullptr;
+    dccrgx_grid_params params{};
+    dccrgx::MapParams map{};
+    bool uniform = true;
+    dccrgx::UGeom g{};
+    uint64_t n_local = 0, first_local = 0, n_slots = 0;
+    std::vector<dccrgx::Field> fields;
+    std::map<int32_t, dccrgx::Hood> hoods;
+    // kernel timing (dccrgx_kernel_timer)
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    double timed_ms = 0;
+    uint64_t timed_launches = 0;
+};
+
+namespace dccrgx {
+Hood* find_hood(dccrgx_grid* g, int32_t id);
+const Hood* find_hood(const dccrgx_grid* g, int32_t id);
+int build_hood(dccrgx_grid* g, Hood& h);
+void free_hood(Hood& h);
+int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out,
+               const Field& cnt, int64_t s0, int64_t s1, hipStream_t st);
+// explicit (mixed refinement level) grids, explicit.hip
+int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n);
+void explicit_destroy(dccrgx_grid* grid);
+int explicit_build_hood(dccrgx_grid* grid, Hood& h);
+int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, uint64_t* ids,
+                       size_t cap, size_t* n);
+}  // namespace dccrgx

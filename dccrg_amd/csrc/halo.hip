@@ -1,0 +1,430 @@
+// halo.hip -- device SoA field pools and the remote-neighbor halo exchange.
+//
+// Replaces the reference transfer engine (dccrg.hpp:10726-11209): instead of
+// one MPI struct datatype per peer built from every boundary cell's
+// get_mpi_datatype(), each registered field is moved as one contiguous RCCL
+// message per peer (field-major, cells in ascending id order as in
+// dccrg.hpp:8822-8826).  When the per-peer cell run is contiguous in the
+// slab layout the message is sent from / received into the field itself
+// (no pack, no unpack); otherwise a gather / scatter kernel stages it.
+#include <algorithm>
+#include <cstring>
+
+#include "grid.hpp"
+
+namespace dccrgx {
+
+static unsigned grid_for(uint64_t n)
+{
+    uint64_t g = (n + 255) / 256;
+    if (g > 256 * 16) g = 256 * 16;
+    if (g == 0) g = 1;
+    return (unsigned)g;
+}
+
+// dst[i*E .. ] = src[idx[i]*E ..], elements of E bytes (E multiple of 4 or any)
+template <class T>
+__global__ void __launch_bounds__(256) k_gather(const T* __restrict__ src, const uint64_t* __restrict__ idx,
+                                                uint64_t n, uint32_t words, T* __restrict__ dst)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const uint64_t tot = n * words;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += stride) {
+        const uint64_t c = i / words, w = i - c * words;
+        dst[i] = src[idx[c] * words + w];
+    }
+}
+
+// dst[didx[i]*E ..] = src[sidx ? sidx[i] : i]
+template <class T>
+__global__ void __launch_bounds__(256) k_scatter(const T* __restrict__ src, const uint64_t* __restrict__ sidx,
+                                                 const uint64_t* __restrict__ didx, uint64_t n,
+                                                 uint32_t words, T* __restrict__ dst)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const uint64_t tot = n * words;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += stride) {
+        const uint64_t c = i / words, w = i - c * words;
+        const uint64_t s = sidx ? sidx[c] : c;
+        dst[didx[c] * words + w] = src[s * words + w];
+    }
+}
+
+static int launch_gather(const void* src, const uint64_t* idx, uint64_t n, uint32_t elem, void* dst,
+                         hipStream_t st)
+{
+    if (n == 0) return DCCRGX_OK;
+    if (elem % 4 == 0)
+        hipLaunchKernelGGL(k_gather<uint32_t>, dim3(grid_for(n * (elem / 4))), dim3(256), 0, st,
+                           (const uint32_t*)src, idx, n, elem / 4, (uint32_t*)dst);
+    else
+        hipLaunchKernelGGL(k_gather<uint8_t>, dim3(grid_for(n * elem)), dim3(256), 0, st,
+                           (const uint8_t*)src, idx, n, elem, (uint8_t*)dst);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+static int launch_scatter(const void* src, const uint64_t* sidx, const uint64_t* didx, uint64_t n,
+                          uint32_t elem, void* dst, hipStream_t st)
+{
+    if (n == 0) return DCCRGX_OK;
+    if (elem % 4 == 0)
+        hipLaunchKernelGGL(k_scatter<uint32_t>, dim3(grid_for(n * (elem / 4))), dim3(256), 0, st,
+                           (const uint32_t*)src, sidx, didx, n, elem / 4, (uint32_t*)dst);
+    else
+        hipLaunchKernelGGL(k_scatter<uint8_t>, dim3(grid_for(n * elem)), dim3(256), 0, st,
+                           (const uint8_t*)src, sidx, didx, n, elem, (uint8_t*)dst);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+static int check_fields(const dccrgx_grid* g, const int32_t* f, size_t nf, size_t* bytes_per_cell)
+{
+    DX_CHECK(f || nf == 0, DCCRGX_EINVAL, "null field list");
+    size_t b = 0;
+    for (size_t i = 0; i < nf; i++) {
+        DX_CHECK(f[i] >= 0 && (size_t)f[i] < g->fields.size(), DCCRGX_EINVAL, "bad field %d", f[i]);
+        b += g->fields[f[i]].elem;
+    }
+    if (bytes_per_cell) *bytes_per_cell = b;
+    return DCCRGX_OK;
+}
+
+static int ensure(void** p, size_t* have, size_t need)
+{
+    if (*have >= need) return DCCRGX_OK;
+    hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    DX_HIP(hipMalloc(p, need));
+    *have = need;
+    return DCCRGX_OK;
+}
+
+// periodic self copies into pad slots (stream st)
+static int self_copy(dccrgx_grid* g, const Hood& h, const int32_t* f, size_t nf, hipStream_t st)
+{
+    for (size_t i = 0; i < nf; i++) {
+        const Field& F = g->fields[f[i]];
+        for (const CopySeg& s : h.self_segs)
+            DX_HIP(hipMemcpyAsync((char*)F.ptr + s.dst * F.elem, (char*)F.ptr + s.src * F.elem,
+                                  s.n * F.elem, hipMemcpyDeviceToDevice, st));
+        DX_TRY(launch_scatter(F.ptr, h.d_self_src, h.d_self_dst, h.n_self_scatter, F.elem, F.ptr, st));
+    }
+    return DCCRGX_OK;
+}
+
+// message layout per peer: field-major, cells ascending
+static int pack_peer(dccrgx_grid* g, PeerPlan& p, const int32_t* f, size_t nf, void* dst,
+                     hipStream_t st)
+{
+    const uint64_t n = p.send_ids.size();
+    size_t off = 0;
+    for (size_t i = 0; i < nf; i++) {
+        const Field& F = g->fields[f[i]];
+        char* d = (char*)dst + off;
+        if (p.send_direct)
+            DX_HIP(hipMemcpyAsync(d, (char*)F.ptr + p.send_slot0 * F.elem, n * F.elem,
+                                  hipMemcpyDeviceToDevice, st));
+        else
+            DX_TRY(launch_gather(F.ptr, p.d_send_slots, n, F.elem, d, st));
+        off += n * F.elem;
+    }
+    return DCCRGX_OK;
+}
+
+static int unpack_peer(dccrgx_grid* g, PeerPlan& p, const int32_t* f, size_t nf, const void* src,
+                       hipStream_t st)
+{
+    const uint64_t n = p.recv_ids.size();
+    size_t off = 0;
+    for (size_t i = 0; i < nf; i++) {
+        const Field& F = g->fields[f[i]];
+        const char* s = (const char*)src + off;
+        if (p.recv_direct)
+            DX_HIP(hipMemcpyAsync((char*)F.ptr + p.recv_slot0 * F.elem, s, n * F.elem,
+                                  hipMemcpyDeviceToDevice, st));
+        else
+            DX_TRY(launch_scatter(s, p.d_unpack_src, p.d_unpack_dst, p.n_unpack, F.elem, F.ptr, st));
+        off += n * F.elem;
+    }
+    return DCCRGX_OK;
+}
+
+// remote cell lin -> first storage slot holding it (or -1)
+__host__ __device__ inline int64_t ghost_slot(const UGeom& g, uint64_t lin)
+{
+    const uint64_t c = divide(lin, g.dS);
+    const uint64_t rem = lin - c * g.S;
+    const int64_t c0 = g.cbase, c1 = g.cbase + (int64_t)g.nslices;
+    if (!g.perC) {
+        if ((int64_t)c >= c0 && (int64_t)c < c1) return (int64_t)(rem + g.S * (uint64_t)((int64_t)c - c0));
+        return -1;
+    }
+    // smallest unwrapped copy c + k*LC >= c0
+    int64_t cu = (int64_t)c;
+    const int64_t LC = (int64_t)g.LC;
+    if (cu < c0) cu += ((c0 - cu + LC - 1) / LC) * LC;
+    else cu -= ((cu - c0) / LC) * LC;
+    if (cu < c1) return (int64_t)(rem + g.S * (uint64_t)(cu - c0));
+    return -1;
+}
+
+__global__ void __launch_bounds__(256) k_slots_of(UGeom g, const uint64_t* __restrict__ ids, size_t n,
+                                                  int64_t* __restrict__ slots)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t id = ids[i];
+        int64_t s = -1;
+        if (id >= 1 && id <= g.N) {
+            const uint64_t lin = id - 1;
+            if (ug_local(g, lin)) s = (int64_t)(lin + (uint64_t)(-g.cbase * (int64_t)g.S));
+            else s = ghost_slot(g, lin);
+        }
+        slots[i] = s;
+    }
+}
+
+int explicit_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int64_t* slots,
+                      hipStream_t st);
+
+static int halo_finish(dccrgx_grid* grid, Hood& h, const int32_t* f, size_t nf)
+{
+    for (PeerPlan& p : h.peers)
+        if (!p.recv_direct && !p.recv_ids.empty())
+            DX_TRY(unpack_peer(grid, p, f, nf, p.d_recv_buf, grid->ctx->compute));
+    return DCCRGX_OK;
+}
+
+}  // namespace dccrgx
+
+using namespace dccrgx;
+
+extern "C" {
+
+int dccrgx_field_create(dccrgx_grid* grid, uint32_t elem, int32_t* fid)
+{
+    DX_CHECK(grid && fid && elem > 0, DCCRGX_EINVAL, "bad argument");
+    DX_HIP(hipSetDevice(grid->ctx->device));
+    Field F;
+    F.elem = elem;
+    const size_t bytes = std::max<uint64_t>(grid->n_slots, 1) * elem;
+    DX_HIP(hipMalloc(&F.ptr, bytes));
+    // ghost slots of cells outside the grid stay zero forever; default-constructed
+    // (value-initialised) ghosts as in allocate_copies_of_remote_neighbors, dccrg.hpp:7153-7184
+    DX_HIP(hipMemsetAsync(F.ptr, 0, bytes, grid->ctx->compute));
+    DX_HIP(hipStreamSynchronize(grid->ctx->compute));
+    grid->fields.push_back(F);
+    *fid = (int32_t)grid->fields.size() - 1;
+    return DCCRGX_OK;
+}
+
+int dccrgx_field_device_ptr(const dccrgx_grid* grid, int32_t fid, void** ptr, uint64_t* n_slots)
+{
+    DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    if (ptr) *ptr = grid->fields[fid].ptr;
+    if (n_slots) *n_slots = grid->n_slots;
+    return DCCRGX_OK;
+}
+
+int dccrgx_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int64_t* slots, void* stream)
+{
+    DX_CHECK(grid && (n == 0 || (ids && slots)), DCCRGX_EINVAL, "bad argument");
+    hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
+    if (n == 0) return DCCRGX_OK;
+    if (!grid->uniform) return explicit_slots_of(grid, ids, n, slots, st);
+    if (grid->n_local == 0) return set_error(DCCRGX_ESTATE, "rank has no cells");
+    hipLaunchKernelGGL(k_slots_of, dim3(grid_for(n)), dim3(256), 0, st, grid->g, ids, n, slots);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+// local cells occupy one contiguous slot run in both layouts
+static uint64_t local_slot0(const dccrgx_grid* grid)
+{
+    if (!grid->uniform) return 0;
+    return grid->g.lo + (uint64_t)(-grid->g.cbase * (int64_t)grid->g.S);
+}
+
+int dccrgx_field_write_local(dccrgx_grid* grid, int32_t fid, const void* host, size_t n)
+{
+    DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    DX_CHECK(n == grid->n_local && (host || !n), DCCRGX_EINVAL, "expected %llu local values",
+             (unsigned long long)grid->n_local);
+    if (!n) return DCCRGX_OK;
+    const Field& F = grid->fields[fid];
+    DX_HIP(hipMemcpyAsync((char*)F.ptr + local_slot0(grid) * F.elem, host, n * F.elem,
+                          hipMemcpyHostToDevice, grid->ctx->compute));
+    DX_HIP(hipStreamSynchronize(grid->ctx->compute));
+    return DCCRGX_OK;
+}
+
+int dccrgx_field_read_local(const dccrgx_grid* grid, int32_t fid, void* host, size_t n)
+{
+    DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    DX_CHECK(n == grid->n_local && (host || !n), DCCRGX_EINVAL, "expected %llu local values",
+             (unsigned long long)grid->n_local);
+    if (!n) return DCCRGX_OK;
+    const Field& F = grid->fields[fid];
+    DX_HIP(hipMemcpyAsync(host, (char*)F.ptr + local_slot0(grid) * F.elem, n * F.elem,
+                          hipMemcpyDeviceToHost, grid->ctx->compute));
+    DX_HIP(hipStreamSynchronize(grid->ctx->compute));
+    return DCCRGX_OK;
+}
+
+int dccrgx_field_read_remote(const dccrgx_grid* grid, int32_t hood_id, int32_t fid, void* host,
+                             size_t n)
+{
+    DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    const Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    DX_CHECK(n == h->remote.size() && (host || !n), DCCRGX_EINVAL, "expected %zu remote values",
+             h->remote.size());
+    if (!n) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    const Field& F = grid->fields[fid];
+    uint64_t* d_ids = nullptr;
+    int64_t* d_slots = nullptr;
+    void* d_out = nullptr;
+    DX_HIP(hipMalloc(&d_ids, n * 8));
+    DX_HIP(hipMalloc(&d_slots, n * 8));
+    DX_HIP(hipMalloc(&d_out, n * F.elem));
+    DX_HIP(hipMemcpyAsync(d_ids, h->remote.data(), n * 8, hipMemcpyHostToDevice, st));
+    DX_TRY(dccrgx_slots_of(grid, d_ids, n, d_slots, st));
+    DX_TRY(launch_gather(F.ptr, (const uint64_t*)d_slots, n, F.elem, d_out, st));
+    DX_HIP(hipMemcpyAsync(host, d_out, n * F.elem, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_ids);
+    hipFree(d_slots);
+    hipFree(d_out);
+    return DCCRGX_OK;
+}
+
+int dccrgx_halo_self(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size_t nf)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    DX_TRY(check_fields(grid, f, nf, nullptr));
+    return self_copy(grid, *h, f, nf, grid->ctx->compute);
+}
+
+int dccrgx_halo_start(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size_t nf)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    Hood* h = find_hood(grid, hood_id);
+    // the reference returns false for unknown ids (dccrg.hpp:5055-5060)
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    DX_CHECK(!h->pending, DCCRGX_ESTATE, "halo of neighborhood %d already started", hood_id);
+    size_t bpc = 0;
+    DX_TRY(check_fields(grid, f, nf, &bpc));
+    Ctx* c = grid->ctx;
+    DX_TRY(self_copy(grid, *h, f, nf, c->compute));
+    bool any = false;
+    for (const PeerPlan& p : h->peers) any |= !p.send_ids.empty() || !p.recv_ids.empty();
+    if (!any) return DCCRGX_OK;
+    DX_CHECK(c->has_comm, DCCRGX_ESTATE,
+             "rank %d has remote neighbors but no RCCL communicator (dccrgx_ctx_comm_init)", c->rank);
+    // the comm stream starts after everything queued so far on the compute stream
+    DX_HIP(hipEventRecord(c->ev_compute, c->compute));
+    DX_HIP(hipStreamWaitEvent(c->comm, c->ev_compute, 0));
+    for (PeerPlan& p : h->peers) {
+        if (!p.send_direct && !p.send_ids.empty()) {
+            DX_TRY(ensure(&p.d_send_buf, &p.send_buf_bytes, p.send_ids.size() * bpc));
+            DX_TRY(pack_peer(grid, p, f, nf, p.d_send_buf, c->comm));
+        }
+        if (!p.recv_direct && !p.recv_ids.empty())
+            DX_TRY(ensure(&p.d_recv_buf, &p.recv_buf_bytes, p.recv_ids.size() * bpc));
+    }
+    // grouped point-to-point: one message per field per peer (xGMI links are
+    // point-to-point; z-slab peers are the ring neighbours)
+    DX_RCCL(ncclGroupStart());
+    for (PeerPlan& p : h->peers) {
+        size_t soff = 0, roff = 0;
+        for (size_t i = 0; i < nf; i++) {
+            const Field& F = grid->fields[f[i]];
+            const size_t sb = p.send_ids.size() * F.elem, rb = p.recv_ids.size() * F.elem;
+            if (sb) {
+                const void* src = p.send_direct ? (const char*)F.ptr + p.send_slot0 * F.elem
+                                                : (const char*)p.d_send_buf + soff;
+                DX_RCCL(ncclSend(src, sb, ncclUint8, p.peer, c->nccl, c->comm));
+            }
+            if (rb) {
+                void* dst = p.recv_direct ? (char*)F.ptr + p.recv_slot0 * F.elem
+                                          : (char*)p.d_recv_buf + roff;
+                DX_RCCL(ncclRecv(dst, rb, ncclUint8, p.peer, c->nccl, c->comm));
+            }
+            soff += sb;
+            roff += rb;
+        }
+    }
+    DX_RCCL(ncclGroupEnd());
+    DX_HIP(hipEventRecord(c->ev_comm, c->comm));
+    h->pending = true;
+    h->pending_fields.assign(f, f + nf);
+    return DCCRGX_OK;
+}
+
+int dccrgx_halo_wait(dccrgx_grid* grid, int32_t hood_id, int32_t which)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    DX_CHECK(which >= DCCRGX_WAIT_ALL && which <= DCCRGX_WAIT_SENDS, DCCRGX_EINVAL, "bad selector");
+    if (!h->pending) return DCCRGX_OK;
+    Ctx* c = grid->ctx;
+    // sends and receives of one RCCL group complete together: any wait
+    // completes both (dccrg.hpp:5307-5413 semantics are preserved: after a
+    // receive wait the ghosts are current, after a send wait the sent cells
+    // may be modified)
+    DX_HIP(hipStreamWaitEvent(c->compute, c->ev_comm, 0));
+    h->pending = false;
+    return halo_finish(grid, *h, h->pending_fields.data(), h->pending_fields.size());
+}
+
+int dccrgx_halo_update(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size_t nf)
+{
+    DX_TRY(dccrgx_halo_start(grid, hood_id, f, nf));
+    return dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL);
+}
+
+int dccrgx_halo_pack_to(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size_t nf, int32_t peer,
+                        void* dst, size_t cap, size_t* bytes)
+{
+    DX_CHECK(grid && bytes, DCCRGX_EINVAL, "null argument");
+    Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    size_t bpc = 0;
+    DX_TRY(check_fields(grid, f, nf, &bpc));
+    *bytes = 0;
+    for (PeerPlan& p : h->peers) {
+        if (p.peer != peer) continue;
+        *bytes = p.send_ids.size() * bpc;
+        DX_CHECK(cap >= *bytes, DCCRGX_ERANGE, "capacity %zu < %zu", cap, *bytes);
+        DX_TRY(pack_peer(grid, p, f, nf, dst, grid->ctx->compute));
+    }
+    return DCCRGX_OK;
+}
+
+int dccrgx_halo_unpack_from(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size_t nf,
+                            int32_t peer, const void* src, size_t bytes)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null argument");
+    Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    size_t bpc = 0;
+    DX_TRY(check_fields(grid, f, nf, &bpc));
+    for (PeerPlan& p : h->peers) {
+        if (p.peer != peer) continue;
+        DX_CHECK(bytes == p.recv_ids.size() * bpc, DCCRGX_EINVAL, "message is %zu bytes, expected %zu",
+                 bytes, p.recv_ids.size() * bpc);
+        DX_TRY(unpack_peer(grid, p, f, nf, src, grid->ctx->compute));
+        return DCCRGX_OK;
+    }
+    DX_CHECK(bytes == 0, DCCRGX_EINVAL, "no receives from peer %d", peer);
+    return DCCRGX_OK;
+}
+
+}  // extern "C"
+

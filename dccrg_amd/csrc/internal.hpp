@@ -1,0 +1,209 @@
+// internal.hpp -- shared internals of libdccrgx.so (MI355X / gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dccrgx.h"
+
+namespace dccrgx {
+
+// ---------------------------------------------------------------------------
+// errors: thread-local message, status codes from dccrgx.h
+// ---------------------------------------------------------------------------
+int set_error(int code, const char* fmt, ...);
+
+#define DX_HIP(expr)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return ::dccrgx::set_error(DCCRGX_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, \
+                                       #expr, hipGetErrorString(e_));                   \
+    } while (0)
+
+#define DX_RCCL(expr)                                                                    \
+    do {                                                                                 \
+        ncclResult_t r_ = (expr);                                                        \
+        if (r_ != ncclSuccess)                                                           \
+            return ::dccrgx::set_error(DCCRGX_ERCCL, "%s:%d %s: %s", __FILE__, __LINE__, \
+                                       #expr, ncclGetErrorString(r_));                   \
+    } while (0)
+
+#define DX_TRY(expr)                       \
+    do {                                   \
+        int s_ = (expr);                   \
+        if (s_ != DCCRGX_OK) return s_;    \
+    } while (0)
+
+#define DX_CHECK(cond, code, ...)                                     \
+    do {                                                              \
+        if (!(cond)) return ::dccrgx::set_error((code), __VA_ARGS__); \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// 64-bit division by an invariant divisor (Granlund-Montgomery, "unsigned
+// division by invariant integers using multiplication", fig. 4.1): 64-bit
+// integer division is a long emulated sequence on CDNA, a mul-hi is 4 muls.
+// ---------------------------------------------------------------------------
+struct Divider {
+    uint64_t m;      // magic
+    uint32_t sh1;    // min(L, 1)
+    uint32_t sh2;    // max(L - 1, 0)
+};
+
+inline Divider make_divider(uint64_t d)
+{
+    Divider r{};
+    if (d == 0) d = 1;  // never divided by; keep well defined
+    int L = 0;
+    while (L < 64 && ((unsigned __int128)1 << L) < d) L++;  // L = ceil(log2 d)
+    const unsigned __int128 twoL = (unsigned __int128)1 << L;
+    const unsigned __int128 num = (twoL - d) << 64;
+    r.m = (uint64_t)(num / d) + 1;
+    r.sh1 = L < 1 ? L : 1;
+    r.sh2 = L > 1 ? L - 1 : 0;
+    return r;
+}
+
+__host__ __device__ inline uint64_t mulhi64(uint64_t a, uint64_t b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+__host__ __device__ inline uint64_t divide(uint64_t n, const Divider& d)
+{
+    const uint64_t t1 = mulhi64(d.m, n);
+    return (t1 + ((n - t1) >> d.sh1)) >> d.sh2;
+}
+
+// ---------------------------------------------------------------------------
+// Mapping parameters (dccrg_mapping.hpp) in a form kernels take by value.
+// ---------------------------------------------------------------------------
+constexpr int MAX_LEVELS = 24;  // > maximum possible refinement level (21) + 2
+
+struct MapParams {
+    uint64_t length[3];
+    uint64_t first_id[MAX_LEVELS];  // first id of each level (level l .. l+1 boundary)
+    uint64_t last_cell;
+    uint64_t nlevel0;
+    Divider div_lx;    // / length[0]
+    Divider div_lxly;  // / (length[0]*length[1])
+    int32_t max_lvl;
+    int32_t pad_;
+};
+
+int make_map_params(const dccrgx_mapping* m, MapParams* out);
+int max_possible_level(const uint64_t length[3]);
+
+// Mapping::get_refinement_level, dccrg_mapping.hpp:262-290
+__host__ __device__ inline int map_level(const MapParams& p, uint64_t cell)
+{
+    if (cell == 0 || cell > p.last_cell) return -1;
+    int l = 0;
+#pragma unroll
+    for (int k = 1; k < MAX_LEVELS; k++)
+        l += (k <= p.max_lvl && cell >= p.first_id[k]) ? 1 : 0;
+    return l;
+}
+
+// Mapping::get_indices, dccrg_mapping.hpp:218-254 (bit-exact; 2 magic divisions)
+__host__ __device__ inline bool map_indices(const MapParams& p, uint64_t cell, uint64_t out[3],
+                                            int* lvl_out)
+{
+    const int l = map_level(p, cell);
+    if (lvl_out) *lvl_out = l;
+    if (l < 0) {
+        out[0] = out[1] = out[2] = DCCRGX_ERROR_INDEX;
+        return false;
+    }
+    const uint64_t r = cell - p.first_id[l];
+    const uint64_t t = divide(r >> l, p.div_lx);          // r / (Lx 2^l)
+    const uint64_t z = divide(r >> (2 * l), p.div_lxly);  // r / (Lx Ly 4^l)
+    const uint64_t x = r - t * (p.length[0] << l);
+    const uint64_t y = t - z * (p.length[1] << l);
+    const int s = p.max_lvl - l;
+    out[0] = x << s;
+    out[1] = y << s;
+    out[2] = z << s;
+    return true;
+}
+
+// Mapping::get_cell_from_indices, dccrg_mapping.hpp:154-209
+__host__ __device__ inline uint64_t map_cell(const MapParams& p, const uint64_t idx[3], int lvl)
+{
+    const int M = p.max_lvl;
+    if (idx[0] >= (p.length[0] << M)) return 0;
+    if (idx[1] >= (p.length[1] << M)) return 0;
+    if (idx[2] >= (p.length[2] << M)) return 0;
+    if (lvl < 0 || lvl > M) return 0;
+    const int s = M - lvl;
+    const uint64_t lx = p.length[0] << lvl, ly = p.length[1] << lvl;
+    return p.first_id[lvl] + (idx[0] >> s) + (idx[1] >> s) * lx + (idx[2] >> s) * lx * ly;
+}
+
+__host__ __device__ inline uint64_t map_len_in_indices(const MapParams& p, uint64_t cell)
+{
+    const int l = map_level(p, cell);
+    if (l < 0) return DCCRGX_ERROR_INDEX;
+    return (uint64_t)1 << (p.max_lvl - l);
+}
+
+// ---------------------------------------------------------------------------
+// block partition, dccrg.hpp:8098-8145 (non-SFC)
+// ---------------------------------------------------------------------------
+struct Partition {
+    uint64_t total;   // level-0 cells
+    uint64_t cpp;     // cells_per_process
+    uint64_t fewer;   // processes with cpp-1 cells
+    uint64_t split;   // first 0-based index owned by a "cpp" process = fewer*(cpp-1)
+    Divider div_cpp, div_cpp1;
+    int32_t comm_size;
+    int32_t pad_;
+};
+
+Partition make_partition(uint64_t total, int comm_size);
+
+__host__ __device__ inline int part_owner(const Partition& P, uint64_t level0_id)
+{
+    const uint64_t i = level0_id - 1;
+    if (i < P.split) return (int)divide(i, P.div_cpp1);  // cpp-1 > 0 here
+    return (int)(P.fewer + divide(i - P.split, P.div_cpp));
+}
+
+inline uint64_t part_first(const Partition& P, int rank)  // 1-based first id
+{
+    const uint64_t r = (uint64_t)rank;
+    if (r <= P.fewer) return 1 + r * (P.cpp - 1);
+    return 1 + P.split + (r - P.fewer) * P.cpp;
+}
+
+inline uint64_t part_count(const Partition& P, int rank)
+{
+    return (uint64_t)rank < P.fewer ? P.cpp - 1 : P.cpp;
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+struct Ctx {
+    int device = 0, rank = 0, comm_size = 1;
+    hipStream_t compute = nullptr, comm = nullptr;
+    hipEvent_t ev_compute = nullptr, ev_comm = nullptr;
+    ncclComm_t nccl = nullptr;
+    bool has_comm = false;
+};
+
+}  // namespace dccrgx
+
+struct dccrgx_ctx : dccrgx::Ctx {};

@@ -1,0 +1,177 @@
+// nbr.hip -- neighbor lists of arbitrary cells as device CSR (uniform grids).
+//
+// get_neighbors_of (dccrg.hpp:836-883, built by find_neighbors_of :4375-4716):
+// for a single-level grid the face-graph walk of the reference always ends on
+// the cell at the item's window, so the list is closed form: one entry per
+// item in neighborhood order, dropped outside non-periodic boundaries,
+// offset = item * 2^max_ref_lvl (geometric, not wrapped: dccrg.hpp:7408-7430).
+// get_neighbors_to (find_neighbors_to :4744-4897): unique cells found with
+// hood_to = -hood_of, ascending here (the reference: unordered_map order).
+#include <algorithm>
+#include <cstring>
+
+#include "grid.hpp"
+
+namespace dccrgx {
+
+static unsigned grid_for(uint64_t n)
+{
+    uint64_t g = (n + 255) / 256;
+    if (g > 256 * 16) g = 256 * 16;
+    if (g == 0) g = 1;
+    return (unsigned)g;
+}
+
+// pass 1 (ids == nullptr): per-cell counts into row[i + 1]; pass 2: fill
+__global__ void __launch_bounds__(256) k_uniform_nbrs(UGeom g, const int32_t* __restrict__ items, int K,
+                                                      const uint64_t* __restrict__ cells, size_t n,
+                                                      uint64_t* __restrict__ row, uint64_t* __restrict__ ids,
+                                                      int32_t* __restrict__ off3, int32_t* __restrict__ err,
+                                                      int32_t sx, int32_t sy, int32_t sz)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t id = cells[i];
+        if (id < 1 || id > g.N) {
+            atomicOr(err, 1);
+            if (!ids) row[i + 1] = 0;
+            continue;
+        }
+        int64_t a, b, c;
+        ug_decompose(g, id - 1, a, b, c);
+        uint64_t w = ids ? row[i] : 0;
+        for (int k = 0; k < K; k++) {
+            uint64_t nlin;
+            int64_t cu;
+            if (!ug_neighbor(g, a, b, c, items + 3 * k, nlin, cu)) continue;
+            if (ids) {
+                ids[w] = nlin + 1;
+                if (off3) {
+                    // canonical item back to x, y, z (perm maps canonical -> original)
+                    int32_t o[3];
+                    for (int d = 0; d < 3; d++) o[g.perm[d]] = items[3 * k + d];
+                    off3[3 * w + 0] = o[0] * sx;
+                    off3[3 * w + 1] = o[1] * sy;
+                    off3[3 * w + 2] = o[2] * sz;
+                }
+            }
+            w++;
+        }
+        if (!ids) row[i + 1] = w;
+    }
+}
+
+int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n,
+                          uint64_t* row, uint64_t* ids, int32_t* off3, size_t cap, hipStream_t st);
+int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n,
+                          uint64_t* row, uint64_t* ids, size_t cap, hipStream_t st);
+
+// exclusive scan of row[1..n] counts in place on the host (API, not hot path)
+static int scan_rows(uint64_t* row, size_t n, hipStream_t st, uint64_t* total)
+{
+    std::vector<uint64_t> h(n + 1);
+    DX_HIP(hipMemcpyAsync(h.data(), row, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    h[0] = 0;
+    for (size_t i = 0; i < n; i++) h[i + 1] += h[i];
+    DX_HIP(hipMemcpyAsync(row, h.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    *total = h[n];
+    return DCCRGX_OK;
+}
+
+}  // namespace dccrgx
+
+using namespace dccrgx;
+
+extern "C" {
+
+int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells, size_t n,
+                        uint64_t* row, uint64_t* ids, int32_t* off3, size_t cap, void* stream)
+{
+    DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    const Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
+    if (!grid->uniform) return explicit_neighbors_of(grid, *h, cells, n, row, ids, off3, cap, st);
+    const UGeom& g = grid->g;
+    int32_t* d_err = nullptr;
+    DX_HIP(hipMalloc(&d_err, 4));
+    DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
+    DX_HIP(hipMemsetAsync(row, 0, 8, st));
+    const int32_t sc = 1 << grid->map.max_lvl;  // offsets in indices of the finest level
+    if (n)
+        hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells,
+                           n, row, (uint64_t*)nullptr, (int32_t*)nullptr, d_err, sc, sc, sc);
+    DX_HIP(hipGetLastError());
+    uint64_t total = 0;
+    DX_TRY(scan_rows(row, n, st, &total));
+    int32_t err = 0;
+    DX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_err);
+    DX_CHECK(!err, DCCRGX_ENOTFOUND, "cell outside the grid");
+    if (!ids) return DCCRGX_OK;
+    DX_CHECK(cap >= total, DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total);
+    if (n)
+        hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells,
+                           n, row, ids, off3, d_err, sc, sc, sc);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+int dccrgx_neighbors_to(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells, size_t n,
+                        uint64_t* row, uint64_t* ids, size_t cap, void* stream)
+{
+    DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    const Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
+    if (!grid->uniform) return explicit_neighbors_to(grid, *h, cells, n, row, ids, cap, st);
+    // candidates with hood_to on the device, unique + sort per cell on the host
+    const UGeom& g = grid->g;
+    int32_t* d_err = nullptr;
+    uint64_t *d_row = nullptr, *d_ids = nullptr;
+    DX_HIP(hipMalloc(&d_err, 4));
+    DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
+    DX_HIP(hipMalloc(&d_row, (n + 1) * 8));
+    DX_HIP(hipMemsetAsync(d_row, 0, 8, st));
+    if (n)
+        hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_to_c, h->K, cells, n,
+                           d_row, (uint64_t*)nullptr, (int32_t*)nullptr, d_err, 1, 1, 1);
+    uint64_t total = 0;
+    DX_TRY(scan_rows(d_row, n, st, &total));
+    DX_HIP(hipMalloc(&d_ids, std::max<uint64_t>(total, 1) * 8));
+    if (n)
+        hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_to_c, h->K, cells, n,
+                           d_row, d_ids, (int32_t*)nullptr, d_err, 1, 1, 1);
+    DX_HIP(hipGetLastError());
+    std::vector<uint64_t> hr(n + 1), hi(total);
+    int32_t err = 0;
+    DX_HIP(hipMemcpyAsync(hr.data(), d_row, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (total) DX_HIP(hipMemcpyAsync(hi.data(), d_ids, total * 8, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_err);
+    hipFree(d_row);
+    hipFree(d_ids);
+    DX_CHECK(!err, DCCRGX_ENOTFOUND, "cell outside the grid");
+    std::vector<uint64_t> orow(n + 1, 0), oids;
+    oids.reserve(total);
+    for (size_t i = 0; i < n; i++) {
+        std::vector<uint64_t> v(hi.begin() + hr[i], hi.begin() + hr[i + 1]);
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        oids.insert(oids.end(), v.begin(), v.end());
+        orow[i + 1] = oids.size();
+    }
+    DX_HIP(hipMemcpyAsync(row, orow.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    if (ids) {
+        DX_CHECK(cap >= oids.size(), DCCRGX_ERANGE, "capacity %zu < %zu", cap, oids.size());
+        if (!oids.empty())
+            DX_HIP(hipMemcpyAsync(ids, oids.data(), oids.size() * 8, hipMemcpyHostToDevice, st));
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    return DCCRGX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,408 @@
+"""Host-side mirror of the reference interface on this path.
+
+``Dccrg`` keeps the names, argument meaning and error behaviour of
+``dccrg::Dccrg<Cell_Data, Geometry>`` (dccrg.hpp:151-7186) for the hot path:
+chained configuration setters, ``initialize``, ``local_cells`` /
+``inner_cells`` / ``outer_cells`` / ``remote_cells``, ``get_neighbors_of`` /
+``get_neighbors_to``, ``add_neighborhood``, the per-peer send / receive lists
+and ``update_copies_of_remote_neighbors`` / ``start_`` / ``wait_`` halo calls.
+Cell data lives on the device as structure-of-arrays fields (one per
+``Cell_Data`` member); the user stencil runs as a device kernel.
+
+Everything here calls libdccrgx.so; no computation happens in Python.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _capi as X
+from ._capi import check, lib
+
+DEFAULT_NEIGHBORHOOD_ID = X.DEFAULT_NEIGHBORHOOD_ID
+
+
+def _u64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+class Context:
+    """Device, compute + communication streams, RCCL communicator."""
+
+    def __init__(self, device: int = 0, rank: int = 0, comm_size: int = 1):
+        h = C.c_void_p()
+        check(lib().dccrgx_ctx_create(device, rank, comm_size, C.byref(h)))
+        self._h = h
+        self.device, self.rank, self.comm_size = device, rank, comm_size
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        check(lib().dccrgx_get_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, uid: bytes):
+        assert len(uid) == 128
+        check(lib().dccrgx_ctx_comm_init(self._h, uid))
+
+    def synchronize(self):
+        check(lib().dccrgx_ctx_synchronize(self._h))
+
+    @property
+    def stream(self) -> int:
+        s = C.c_void_p()
+        check(lib().dccrgx_ctx_compute_stream(self._h, C.byref(s)))
+        return s.value or 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().dccrgx_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Mapping:
+    """dccrg::Mapping (dccrg_mapping.hpp:55-690) with batched device calls.
+
+    Batched methods take / return torch CUDA tensors (device memory plumbing);
+    scalar conveniences round-trip one element through the device.
+    """
+
+    def __init__(self, length: Sequence[int], max_ref_lvl: int = 0):
+        self._m = X.Mapping_t((C.c_uint64 * 3)(*[int(v) for v in length]), int(max_ref_lvl), 0)
+        if max_ref_lvl < 0:
+            out = C.c_int32()
+            check(lib().dccrgx_max_possible_refinement_level(self._m.length, C.byref(out)))
+            self._m.max_ref_lvl = out.value
+        last = C.c_uint64()
+        check(lib().dccrgx_last_cell(C.byref(self._m), C.byref(last)))
+        self.last_cell = last.value
+        self.length = tuple(int(v) for v in length)
+
+    @property
+    def max_ref_lvl(self) -> int:
+        return self._m.max_ref_lvl
+
+    def get_maximum_refinement_level(self) -> int:
+        return self._m.max_ref_lvl
+
+    def get_last_cell(self) -> int:
+        return self.last_cell
+
+    def ids_to_indices(self, ids, stream: int = 0):
+        import torch
+        n = ids.numel()
+        idx = torch.empty((n, 3), dtype=torch.int64, device=ids.device)
+        lvl = torch.empty(n, dtype=torch.int32, device=ids.device)
+        check(lib().dccrgx_map_ids_to_indices(C.byref(self._m), ids.data_ptr(), n, idx.data_ptr(),
+                                              lvl.data_ptr(), stream or None))
+        return idx, lvl
+
+    def indices_to_ids(self, idx, lvl, stream: int = 0):
+        import torch
+        n = lvl.numel()
+        ids = torch.empty(n, dtype=torch.int64, device=lvl.device)
+        check(lib().dccrgx_map_indices_to_ids(C.byref(self._m), idx.data_ptr(), lvl.data_ptr(), n,
+                                              ids.data_ptr(), stream or None))
+        return ids
+
+    def ids_op(self, op: int, ids, stream: int = 0):
+        import torch
+        out = torch.empty_like(ids)
+        check(lib().dccrgx_map_ids_op(C.byref(self._m), op, ids.data_ptr(), ids.numel(),
+                                      out.data_ptr(), stream or None))
+        return out
+
+
+class Dccrg:
+    """dccrg::Dccrg for the hot path (dccrg.hpp:151-7186)."""
+
+    def __init__(self):
+        self._length = (1, 1, 1)
+        self._max_ref_lvl = 0
+        self._periodic = (False, False, False)
+        self._hood_length = 1
+        self._h = None
+        self.ctx: Optional[Context] = None
+        self._fields: Dict[str, Tuple[int, np.dtype]] = {}
+
+    # ---- chained configuration (dccrg.hpp:8242-8361) ---------------------
+    def set_initial_length(self, length):
+        if any(int(v) == 0 for v in length):
+            raise ValueError("all lengths must be > 0 (dccrg.hpp:8244-8254)")
+        self._length = tuple(int(v) for v in length)
+        return self
+
+    def set_maximum_refinement_level(self, lvl: int):
+        self._max_ref_lvl = int(lvl)
+        return self
+
+    def set_periodic(self, x: bool, y: bool, z: bool):
+        self._periodic = (bool(x), bool(y), bool(z))
+        return self
+
+    def set_neighborhood_length(self, n: int):
+        self._hood_length = int(n)
+        return self
+
+    def set_load_balancing_method(self, method: str):
+        # Zoltan stays on the host (north star); the partition is the
+        # reference's own non-Zoltan block partition (dccrg.hpp:8098-8145).
+        self._lb_method = method
+        return self
+
+    def initialize(self, ctx: Context, leaves: Optional[Sequence[int]] = None):
+        """dccrg.hpp:485-562.  leaves: existing cells of a mixed-level grid."""
+        self.ctx = ctx
+        p = X.GridParams_t()
+        p.length = (C.c_uint64 * 3)(*self._length)
+        p.max_ref_lvl = self._max_ref_lvl
+        p.neighborhood_length = self._hood_length
+        p.periodic = (C.c_uint8 * 3)(*[1 if v else 0 for v in self._periodic])
+        h = C.c_void_p()
+        if leaves is None:
+            check(lib().dccrgx_grid_create(ctx._h, C.byref(p), None, 0, C.byref(h)))
+        else:
+            lv = _u64(leaves)
+            check(lib().dccrgx_grid_create(ctx._h, C.byref(p), lv.ctypes.data_as(X._u64p), lv.size,
+                                           C.byref(h)))
+        self._h = h
+        info = X.GridInfo_t()
+        check(lib().dccrgx_grid_get_info(self._h, C.byref(info)))
+        self.info = info
+        self.mapping = Mapping(self._length, info.max_ref_lvl)
+        return self
+
+    def balance_load(self, use_zoltan: bool = True):
+        # without Zoltan the reference's balance_load is a no-op (dccrg.hpp:1048-1062)
+        return self
+
+    def close(self):
+        if self._h:
+            lib().dccrgx_grid_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- queries ------------------------------------------------------------
+    def get_rank(self) -> int:
+        return self.ctx.rank
+
+    def get_comm_size(self) -> int:
+        return self.ctx.comm_size
+
+    def get_maximum_refinement_level(self) -> int:
+        return self.info.max_ref_lvl
+
+    @property
+    def n_local(self) -> int:
+        return self.info.n_local
+
+    def _cells(self, which: int, hood: int) -> np.ndarray:
+        n = C.c_size_t()
+        st = lib().dccrgx_get_cells(self._h, hood, which, None, 0, C.byref(n))
+        if st not in (X.DCCRGX_OK, 5):
+            check(st)
+        out = np.zeros(n.value, dtype=np.uint64)
+        check(lib().dccrgx_get_cells(self._h, hood, which, out.ctypes.data_as(X._u64p), n.value,
+                                     C.byref(n)))
+        return out
+
+    def local_cells(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> np.ndarray:
+        return self._cells(X.CELLS_LOCAL, hood)
+
+    def inner_cells(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> np.ndarray:
+        return self._cells(X.CELLS_INNER, hood)
+
+    def outer_cells(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> np.ndarray:
+        return self._cells(X.CELLS_OUTER, hood)
+
+    def remote_cells(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> np.ndarray:
+        return self._cells(X.CELLS_REMOTE, hood)
+
+    def neighbors_of(self, cells: np.ndarray, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        """Batched get_neighbors_of: (row_ptr, ids, offsets[x,y,z]) as numpy."""
+        import torch
+        dev = torch.device("cuda", self.ctx.device)
+        c = torch.from_numpy(_u64(cells).view(np.int64)).to(dev)
+        n = c.numel()
+        row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
+        check(lib().dccrgx_neighbors_of(self._h, hood, c.data_ptr(), n, row.data_ptr(), None, None, 0,
+                                        None))
+        self.ctx.synchronize()
+        total = int(row[-1].item())
+        ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
+        off = torch.zeros((max(total, 1), 3), dtype=torch.int32, device=dev)
+        check(lib().dccrgx_neighbors_of(self._h, hood, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
+                                        off.data_ptr(), total, None))
+        self.ctx.synchronize()
+        return (row.cpu().numpy().astype(np.uint64), ids[:total].cpu().numpy().view(np.uint64),
+                off[:total].cpu().numpy())
+
+    def neighbors_to(self, cells: np.ndarray, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        import torch
+        dev = torch.device("cuda", self.ctx.device)
+        c = torch.from_numpy(_u64(cells).view(np.int64)).to(dev)
+        n = c.numel()
+        row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
+        check(lib().dccrgx_neighbors_to(self._h, hood, c.data_ptr(), n, row.data_ptr(), None, 0, None))
+        self.ctx.synchronize()
+        total = int(row[-1].item())
+        ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
+        check(lib().dccrgx_neighbors_to(self._h, hood, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
+                                        total, None))
+        self.ctx.synchronize()
+        return row.cpu().numpy().astype(np.uint64), ids[:total].cpu().numpy().view(np.uint64)
+
+    def get_neighbors_of(self, cell: int, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        """dccrg.hpp:836-883 for one cell: [(id, (x, y, z)), ...] in reference order."""
+        row, ids, off = self.neighbors_of(np.array([cell]), hood)
+        return [(int(i), tuple(int(v) for v in o)) for i, o in zip(ids, off)]
+
+    def get_neighbors_to(self, cell: int, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        row, ids = self.neighbors_to(np.array([cell]), hood)
+        return [int(i) for i in ids]
+
+    def add_neighborhood(self, hood_id: int, items) -> bool:
+        """dccrg.hpp:6491-6663: False where the reference returns false."""
+        it = np.ascontiguousarray(items, dtype=np.int32).reshape(-1, 3)
+        st = lib().dccrgx_add_neighborhood(self._h, hood_id, it.ctypes.data_as(X._i32p), len(it))
+        if st == 1:  # EINVAL
+            return False
+        check(st)
+        return True
+
+    def remove_neighborhood(self, hood_id: int):
+        check(lib().dccrgx_remove_neighborhood(self._h, hood_id))
+        return self
+
+    def _peer_lists(self, send: int, hood: int) -> Dict[int, List[int]]:
+        n = C.c_size_t()
+        st = lib().dccrgx_get_peers(self._h, hood, send, None, None, 0, C.byref(n))
+        if st not in (X.DCCRGX_OK, 5):
+            check(st)
+        peers = np.zeros(n.value, dtype=np.int32)
+        counts = np.zeros(n.value, dtype=np.uint64)
+        check(lib().dccrgx_get_peers(self._h, hood, send, peers.ctypes.data_as(X._i32p),
+                                     counts.ctypes.data_as(X._u64p), n.value, C.byref(n)))
+        out = {}
+        for p, k in zip(peers, counts):
+            ids = np.zeros(int(k), dtype=np.uint64)
+            m = C.c_size_t()
+            check(lib().dccrgx_get_peer_cells(self._h, hood, send, int(p), ids.ctypes.data_as(X._u64p),
+                                              int(k), C.byref(m)))
+            out[int(p)] = ids.tolist()
+        return out
+
+    def get_cells_to_send(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> Dict[int, List[int]]:
+        """dccrg.hpp:7008-7020: per receiving process, ascending cell ids."""
+        return self._peer_lists(1, hood)
+
+    def get_cells_to_receive(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> Dict[int, List[int]]:
+        return self._peer_lists(0, hood)
+
+    # ---- cell data ------------------------------------------------------------
+    def add_field(self, name: str, dtype=np.uint32) -> int:
+        dt = np.dtype(dtype)
+        fid = C.c_int32()
+        check(lib().dccrgx_field_create(self._h, dt.itemsize, C.byref(fid)))
+        self._fields[name] = (fid.value, dt)
+        return fid.value
+
+    def field_id(self, name: str) -> int:
+        return self._fields[name][0]
+
+    def write_local(self, name: str, values: np.ndarray):
+        fid, dt = self._fields[name]
+        v = np.ascontiguousarray(values, dtype=dt)
+        check(lib().dccrgx_field_write_local(self._h, fid, v.ctypes.data, v.size))
+
+    def read_local(self, name: str) -> np.ndarray:
+        fid, dt = self._fields[name]
+        out = np.zeros(self.info.n_local, dtype=dt)
+        check(lib().dccrgx_field_read_local(self._h, fid, out.ctypes.data, out.size))
+        return out
+
+    def read_remote(self, name: str, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> np.ndarray:
+        fid, dt = self._fields[name]
+        n = len(self.remote_cells(hood))
+        out = np.zeros(n, dtype=dt)
+        check(lib().dccrgx_field_read_remote(self._h, hood, fid, out.ctypes.data, n))
+        return out
+
+    def _fids(self, names) -> np.ndarray:
+        if names is None:
+            names = list(self._fields)
+        return np.array([self._fields[n][0] for n in names], dtype=np.int32)
+
+    # ---- halo (dccrg.hpp:978-1014, 5046-5413) --------------------------------
+    def update_copies_of_remote_neighbors(self, hood: int = DEFAULT_NEIGHBORHOOD_ID, fields=None):
+        f = self._fids(fields)
+        check(lib().dccrgx_halo_update(self._h, hood, f.ctypes.data_as(X._i32p), f.size))
+        self.ctx.synchronize()
+        # quirk kept: with the default id the reference returns false (dccrg.hpp:1001-1003)
+        return hood != DEFAULT_NEIGHBORHOOD_ID
+
+    def start_remote_neighbor_copy_updates(self, hood: int = DEFAULT_NEIGHBORHOOD_ID, fields=None):
+        f = self._fids(fields)
+        check(lib().dccrgx_halo_start(self._h, hood, f.ctypes.data_as(X._i32p), f.size))
+        return True
+
+    def wait_remote_neighbor_copy_updates(self, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        check(lib().dccrgx_halo_wait(self._h, hood, X.WAIT_ALL))
+        return True
+
+    def wait_remote_neighbor_copy_update_receives(self, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        check(lib().dccrgx_halo_wait(self._h, hood, X.WAIT_RECEIVES))
+        return True
+
+    def wait_remote_neighbor_copy_update_sends(self, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        check(lib().dccrgx_halo_wait(self._h, hood, X.WAIT_SENDS))
+        return True
+
+    def pack_to(self, peer: int, dst_ptr: int, cap: int, hood: int = DEFAULT_NEIGHBORHOOD_ID,
+                fields=None) -> int:
+        f = self._fids(fields)
+        n = C.c_size_t()
+        check(lib().dccrgx_halo_pack_to(self._h, hood, f.ctypes.data_as(X._i32p), f.size, peer, dst_ptr,
+                                        cap, C.byref(n)))
+        return n.value
+
+    def unpack_from(self, peer: int, src_ptr: int, nbytes: int, hood: int = DEFAULT_NEIGHBORHOOD_ID,
+                    fields=None):
+        f = self._fids(fields)
+        check(lib().dccrgx_halo_unpack_from(self._h, hood, f.ctypes.data_as(X._i32p), f.size, peer,
+                                            src_ptr, nbytes))
+
+    def halo_self(self, hood: int = DEFAULT_NEIGHBORHOOD_ID, fields=None):
+        f = self._fids(fields)
+        check(lib().dccrgx_halo_self(self._h, hood, f.ctypes.data_as(X._i32p), f.size))
+
+    # ---- game of life stencil ----------------------------------------------
+    def gol_compute(self, fin: str, fout: str, fcnt: str, region: int = X.REGION_ALL,
+                    hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        check(lib().dccrgx_gol_compute(self._h, hood, self.field_id(fin), self.field_id(fout),
+                                       self.field_id(fcnt), region))
+
+    def gol_step(self, fin: str, fout: str, fcnt: str, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        check(lib().dccrgx_gol_step(self._h, hood, self.field_id(fin), self.field_id(fout),
+                                    self.field_id(fcnt)))
+
+    def kernel_timer(self, reset: int = 0):
+        ms = C.c_double()
+        n = C.c_uint64()
+        check(lib().dccrgx_kernel_timer(self._h, reset, C.byref(ms), C.byref(n)))
+        return ms.value, n.value

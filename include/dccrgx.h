@@ -1,0 +1,237 @@
+/*
+ * dccrgx.h -- C-ABI of the MI355X-native dccrg hot path (libdccrgx.so).
+ *
+ * The reference (ykempf/dccrg) is a header-only C++ template library with no
+ * FFI; its drop-in boundary is the public member-function surface of
+ * dccrg::Dccrg<Cell_Data, Geometry> plus dccrg::Mapping.  Each export below
+ * names the reference interface it replaces (file:line in the reference
+ * tree).  The C++ facade include/dccrg_amd.hpp re-implements those member
+ * functions on top of these exports; INTEGRATION.md shows the wiring.
+ *
+ * Conventions:
+ *  - every function returns int status, DCCRGX_OK == 0; no exception crosses
+ *    the ABI; dccrgx_last_error() returns a thread-local message;
+ *  - plain pointers and sizes only; "_dev" pointers are HIP device memory,
+ *    "_host" pointers are host memory; streams are hipStream_t passed as void*
+ *    (NULL = the context's compute stream);
+ *  - thread-compatible, not thread-safe: one context per host thread;
+ *  - device memory of a grid is owned by the grid (SoA field pools).
+ */
+#ifndef DCCRGX_H
+#define DCCRGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCCRGX_VERSION 1
+
+enum {
+    DCCRGX_OK = 0,
+    DCCRGX_EINVAL = 1,      /* bad argument (reference: std::invalid_argument / false) */
+    DCCRGX_ENOMEM = 2,      /* device or host allocation failed */
+    DCCRGX_EHIP = 3,        /* HIP runtime error */
+    DCCRGX_ERCCL = 4,       /* RCCL error */
+    DCCRGX_ERANGE = 5,      /* output capacity too small; *n holds the needed size */
+    DCCRGX_ESTATE = 6,      /* call not valid in the current state */
+    DCCRGX_ENOTFOUND = 7,   /* unknown cell / neighborhood id (reference: nullptr / false) */
+    DCCRGX_EINTERNAL = 8    /* inconsistent structure (reference: std::runtime_error) */
+};
+
+/* dccrg_mapping.hpp:38-41 */
+#define DCCRGX_ERROR_CELL ((uint64_t)0)
+#define DCCRGX_ERROR_INDEX ((uint64_t)0xFFFFFFFFFFFFFFFFull)
+/* dccrg.hpp:99 default_neighborhood_id */
+#define DCCRGX_DEFAULT_NEIGHBORHOOD_ID (-0xdcc)
+
+/* cell classes, dccrg.hpp:7594-7718 (inner/outer/local/remote/all_cells) */
+enum { DCCRGX_CELLS_LOCAL = 0, DCCRGX_CELLS_INNER = 1, DCCRGX_CELLS_OUTER = 2,
+       DCCRGX_CELLS_REMOTE = 3 };
+
+/* halo wait selectors, dccrg.hpp:5307-5413 */
+enum { DCCRGX_WAIT_ALL = 0, DCCRGX_WAIT_RECEIVES = 1, DCCRGX_WAIT_SENDS = 2 };
+
+const char* dccrgx_last_error(void);
+int dccrgx_version(void);
+
+/* ------------------------------------------------------------------------ *
+ * Context: device, compute + communication streams, RCCL communicator.
+ * Replaces Dccrg::initialize_mpi (dccrg.hpp:7738-7803): MPI stays only for
+ * bootstrap; the data path communicator is RCCL over xGMI.
+ * ------------------------------------------------------------------------ */
+typedef struct dccrgx_ctx dccrgx_ctx;
+
+int dccrgx_ctx_create(int device, int rank, int comm_size, dccrgx_ctx** out);
+int dccrgx_ctx_destroy(dccrgx_ctx* ctx);
+/* 128-byte ncclUniqueId; rank 0 creates it, the host bootstrap broadcasts it */
+int dccrgx_get_unique_id(uint8_t uid_out[128]);
+int dccrgx_ctx_comm_init(dccrgx_ctx* ctx, const uint8_t uid[128]);
+int dccrgx_ctx_compute_stream(dccrgx_ctx* ctx, void** hip_stream_out);
+int dccrgx_ctx_synchronize(dccrgx_ctx* ctx);
+
+/* ------------------------------------------------------------------------ *
+ * Batched cell-id mapping (bit-exact with dccrg::Mapping).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+    uint64_t length[3];   /* Grid_Length, dccrg_length.hpp:34-142 */
+    int32_t max_ref_lvl;  /* Mapping::max_refinement_level, dccrg_mapping.hpp:664 */
+    int32_t reserved;
+} dccrgx_mapping;
+
+/* Mapping::get_maximum_possible_refinement_level, dccrg_mapping.hpp:317-330 */
+int dccrgx_max_possible_refinement_level(const uint64_t length[3], int32_t* out);
+/* Mapping::get_last_cell / update_last_cell, dccrg_mapping.hpp:500-503, 679-687 */
+int dccrgx_last_cell(const dccrgx_mapping* map, uint64_t* out);
+/* Mapping::get_indices (dccrg_mapping.hpp:218-254) and get_refinement_level
+ * (dccrg_mapping.hpp:262-290) for n ids: idx3_dev[3*i..3*i+2], lvl_dev[i];
+ * either output may be NULL. */
+int dccrgx_map_ids_to_indices(const dccrgx_mapping* map, const uint64_t* ids_dev, size_t n,
+                              uint64_t* idx3_dev, int32_t* lvl_dev, void* stream);
+/* Mapping::get_cell_from_indices, dccrg_mapping.hpp:154-209 */
+int dccrgx_map_indices_to_ids(const dccrgx_mapping* map, const uint64_t* idx3_dev,
+                              const int32_t* lvl_dev, size_t n, uint64_t* ids_dev, void* stream);
+/* Octree relations, dccrg_mapping.hpp:298-494: op selects the function */
+enum { DCCRGX_OP_LENGTH_IN_INDICES = 0, DCCRGX_OP_PARENT = 1, DCCRGX_OP_LEVEL_0_PARENT = 2,
+       DCCRGX_OP_CHILD = 3 };
+int dccrgx_map_ids_op(const dccrgx_mapping* map, int op, const uint64_t* ids_dev, size_t n,
+                      uint64_t* out_dev, void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * Grid: one dccrg grid on this rank.  Replaces Dccrg::initialize
+ * (dccrg.hpp:485-562): level-0 creation + block partition (:8089-8145),
+ * neighborhoods (:8017-8076), neighbor lists (:8371-8420), boundary
+ * classification (:9131-9409), send/receive lists (:8729-8891) and ghost
+ * allocation (:7153-7184) -- all built on the device.
+ * ------------------------------------------------------------------------ */
+typedef struct dccrgx_grid dccrgx_grid;
+
+typedef struct {
+    uint64_t length[3];            /* set_initial_length, dccrg.hpp:8242 */
+    int32_t max_ref_lvl;           /* set_maximum_refinement_level (<0: max possible), :8276 */
+    uint32_t neighborhood_length;  /* set_neighborhood_length, :8328 */
+    uint8_t periodic[3];           /* set_periodic, :8305 */
+    uint8_t reserved[5];
+} dccrgx_grid_params;
+
+typedef struct {
+    uint64_t n_local;        /* cells owned by this rank */
+    uint64_t first_local;    /* uniform grids: first owned id (0 if none) */
+    uint64_t n_slots;        /* slots per field (local + ghost/pad) */
+    uint64_t layout[4];      /* uniform: LA, LB, slices in storage, pad slices */
+    int32_t max_ref_lvl;     /* effective maximum refinement level */
+    int32_t uniform;         /* 1: implicit uniform level-0 grid */
+    int32_t rank, comm_size;
+} dccrgx_grid_info;
+
+/* leaves_host == NULL: every refinement-level-0 cell exists (implicit uniform
+ * grid, arbitrarily large).  Otherwise the replicated set of existing leaf
+ * cells (mixed refinement levels); each cell is owned by the rank owning its
+ * level-0 parent under the block partition. */
+int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* params,
+                       const uint64_t* leaves_host, size_t n_leaves, dccrgx_grid** out);
+int dccrgx_grid_destroy(dccrgx_grid* grid);
+int dccrgx_grid_get_info(const dccrgx_grid* grid, dccrgx_grid_info* out);
+
+/* Dccrg::add_neighborhood / remove_neighborhood, dccrg.hpp:6491-6711
+ * (validation as :6573-6618: returns DCCRGX_EINVAL when the reference returns false) */
+int dccrgx_add_neighborhood(dccrgx_grid* grid, int32_t hood_id, const int32_t* items3,
+                            size_t n_items);
+int dccrgx_remove_neighborhood(dccrgx_grid* grid, int32_t hood_id);
+/* the neighborhood items (3 ints each) */
+int dccrgx_get_neighborhood(const dccrgx_grid* grid, int32_t hood_id, int32_t* items3_out,
+                            size_t cap, size_t* n);
+
+/* local/inner/outer/remote cells (dccrg.hpp:7594-7718), ascending ids, host
+ * output.  DCCRGX_ERANGE with *n = needed size if cap is too small. */
+int dccrgx_get_cells(const dccrgx_grid* grid, int32_t hood_id, int32_t which, uint64_t* ids_host,
+                     size_t cap, size_t* n);
+/* Dccrg::get_neighbors_of (dccrg.hpp:836-883 / find_neighbors_of :4375-4716)
+ * for n cells in one batch, computed on the device: CSR in reference list
+ * order.  row_ptr_dev has n+1 entries; call with ids_dev == NULL to size. */
+int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells_dev,
+                        size_t n, uint64_t* row_ptr_dev, uint64_t* ids_dev, int32_t* off3_dev,
+                        size_t cap, void* stream);
+/* Dccrg::get_neighbors_to (dccrg.hpp:900-943 / find_neighbors_to :4744-4897),
+ * unique ids per cell in ascending order (the reference: unordered). */
+int dccrgx_neighbors_to(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells_dev,
+                        size_t n, uint64_t* row_ptr_dev, uint64_t* ids_dev, size_t cap,
+                        void* stream);
+/* per-peer ascending send / receive lists (dccrg.hpp:7008-7046, :8729-8891) */
+int dccrgx_get_peers(const dccrgx_grid* grid, int32_t hood_id, int32_t send, int32_t* peers_host,
+                     uint64_t* counts_host, size_t cap, size_t* n_peers);
+int dccrgx_get_peer_cells(const dccrgx_grid* grid, int32_t hood_id, int32_t send, int32_t peer,
+                          uint64_t* ids_host, size_t cap, size_t* n);
+
+/* ------------------------------------------------------------------------ *
+ * Cell data: device SoA field pools (replace Dccrg::cell_data /
+ * remote_neighbors unordered_maps, dccrg.hpp:7238, 7330).
+ * ------------------------------------------------------------------------ */
+int dccrgx_field_create(dccrgx_grid* grid, uint32_t elem_bytes, int32_t* field_id_out);
+int dccrgx_field_device_ptr(const dccrgx_grid* grid, int32_t field_id, void** ptr_out,
+                            uint64_t* n_slots_out);
+/* slot of each cell id in every field (-1: no slot on this rank) */
+int dccrgx_slots_of(const dccrgx_grid* grid, const uint64_t* ids_dev, size_t n, int64_t* slots_dev,
+                    void* stream);
+/* copy local cells' values (ascending id order) between host and device */
+int dccrgx_field_write_local(dccrgx_grid* grid, int32_t field_id, const void* host, size_t n_local);
+int dccrgx_field_read_local(const dccrgx_grid* grid, int32_t field_id, void* host, size_t n_local);
+/* ghost copies of the remote cells of a neighborhood (ascending id order) */
+int dccrgx_field_read_remote(const dccrgx_grid* grid, int32_t hood_id, int32_t field_id,
+                             void* host, size_t n_remote);
+
+/* ------------------------------------------------------------------------ *
+ * Remote-neighbor halo exchange.  Replaces update_copies_of_remote_neighbors
+ * (dccrg.hpp:978-1014), start_remote_neighbor_copy_updates (:5046-5078),
+ * start_..._receives/_sends (:5091-5298), wait_remote_neighbor_copy_updates
+ * (:5307-5338), wait_..._sends/_receives (:5347-5413) and the transfer engine
+ * (:10726-11209).  Payload = the listed fields of each cell (the MPI datatype
+ * of get_mpi_datatype, dccrg_get_cell_datatype.hpp:48-339, becomes a field
+ * list); per peer the cells go in ascending id order as in the reference.
+ * ------------------------------------------------------------------------ */
+int dccrgx_halo_start(dccrgx_grid* grid, int32_t hood_id, const int32_t* field_ids,
+                      size_t n_fields);
+int dccrgx_halo_wait(dccrgx_grid* grid, int32_t hood_id, int32_t which);
+/* start + wait(ALL) */
+int dccrgx_halo_update(dccrgx_grid* grid, int32_t hood_id, const int32_t* field_ids,
+                       size_t n_fields);
+/* Transport-free halo for several ranks driven from ONE process (tests on a
+ * single GPU): pack this rank's sends to peer into dst_dev (field-major,
+ * ascending ids) / unpack a peer's message into the ghost slots. */
+int dccrgx_halo_pack_to(dccrgx_grid* grid, int32_t hood_id, const int32_t* field_ids,
+                        size_t n_fields, int32_t peer, void* dst_dev, size_t cap_bytes,
+                        size_t* bytes_out);
+int dccrgx_halo_unpack_from(dccrgx_grid* grid, int32_t hood_id, const int32_t* field_ids,
+                            size_t n_fields, int32_t peer, const void* src_dev, size_t bytes);
+/* periodic self-copies into the ghost/pad slots (part of halo_start) */
+int dccrgx_halo_self(dccrgx_grid* grid, int32_t hood_id, const int32_t* field_ids,
+                     size_t n_fields);
+
+/* ------------------------------------------------------------------------ *
+ * Stencils over local cells.  Game of life as in examples/game_of_life.cpp:
+ * 54-79 / tests/game_of_life/scalability3d.cpp:136-165: count live
+ * neighbors_of (u32 is_alive > 0), then B3/S23 (count == 3 -> 1, count != 2
+ * -> 0).  Double-buffered: alive_in -> (alive_out, count).
+ * ------------------------------------------------------------------------ */
+enum { DCCRGX_REGION_ALL = 0, DCCRGX_REGION_INNER = 1, DCCRGX_REGION_OUTER = 2 };
+int dccrgx_gol_compute(dccrgx_grid* grid, int32_t hood_id, int32_t f_alive_in,
+                       int32_t f_alive_out, int32_t f_count, int32_t region);
+/* one full step: halo start, inner cells, halo wait, outer cells (the
+ * overlap pattern of scalability3d.cpp:122-166); swaps nothing */
+int dccrgx_gol_step(dccrgx_grid* grid, int32_t hood_id, int32_t f_alive_in, int32_t f_alive_out,
+                    int32_t f_count);
+/* synthetic initial state of a 4-byte field on local cells: 1 where
+ * splitmix64(id) % 1000 < permille, else 0 (replaces the rand() loops of
+ * tests/game_of_life/scalability3d.cpp:106-114 with an order-independent,
+ * reproducible generator) */
+int dccrgx_field_init_hash(dccrgx_grid* grid, int32_t field_id, uint32_t permille);
+/* time the last dccrgx_gol_compute kernels (HIP events on the compute
+ * stream): total ms and launch count since the last reset */
+int dccrgx_kernel_timer(dccrgx_grid* grid, int32_t reset, double* ms_out, uint64_t* launches_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCCRGX_H */

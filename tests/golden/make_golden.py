@@ -127,17 +127,17 @@ def neighbor_list_length_cases():
         {"id": None, "items": None, "nof": 124, "nto": 124, "src": ":72-91"},
         {"id": 1, "items": [[-2, -2, -2]], "nof": 1, "nto": 1, "src": ":95-125"},
         {"id": 2, "items": [[-2, -2, -2], [2, 2, 2]], "nof": 2, "nto": 2, "src": ":127-160"},
-        {"id": 3, "items": [[i, j, 0] for j in range(-2, 3) for i in range(-2, 3)
+        {"id": -3, "items": [[i, j, 0] for j in range(-2, 3) for i in range(-2, 3)
                             if not (i == 0 and j == 0)], "nof": 24, "nto": 24, "src": ":162-200"},
-        {"id": 4, "items": [[0, j, k] for k in range(-2, 3) for j in range(-2, 3)
+        {"id": -4, "items": [[0, j, k] for k in range(-2, 3) for j in range(-2, 3)
                             if not (j == 0 and k == 0)], "nof": 24, "nto": 24, "src": ":203-241"},
-        {"id": 5, "items": [[i, j, k] for k in range(-2, 3) for j in range(-2, 3)
+        {"id": 0, "items": [[i, j, k] for k in range(-2, 3) for j in range(-2, 3)
                             for i in range(-2, 3) if not (i == 0 and j == 0 and k == 0)],
          "nof": 124, "nto": 124, "src": ":244-283"},
     ]
     rejected = [
         {"id": 5, "items": [[-1, 2, -3]], "why": "item beyond neighborhood length", "src": ":286-296"},
-        {"id": 0, "items": [[1, 2, -2]], "why": "existing neighborhood id", "src": ":298-308"},
+        {"id": 0, "items": [[1, 2, -2]], "why": "existing neighborhood id (0 added at :248)", "src": ":298-308"},
     ]
     return {"length": [10, 10, 10], "periodic": [1, 1, 1], "hood_length": 2, "hoods": hoods,
             "rejected": rejected, "src": "tests/user_neighborhood/neighbor_list_length.cpp"}
