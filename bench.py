@@ -151,7 +151,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "k_gol26<64,16,1,4>",
+            "kernel": "dccrgx::k_gol26v<8, 4, true>",
             "kernel_ms_per_step": kern_ms / args.steps,
             "launches_per_step": launches / max(args.steps, 1),
             "bytes_per_cell": BYTES_PER_CELL,

@@ -15,6 +15,7 @@
 // uses the generic item loop (one lane per cell, neighbor slots computed in
 // closed form) -- same results, not bandwidth-optimised.
 #include <algorithm>
+#include <cstdlib>
 
 #include "grid.hpp"
 
@@ -169,6 +170,229 @@ __global__ void __launch_bounds__(256) k_gol26(GolArgs g)
                 Sc[k][i] = Sx[k][i];
                 Vc[k][i] = Vx[k][i];
             }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Vectorised 26-neighbor stencil (LA % 4 == 0).  Tile = 256 cells along A x
+// 16 rows along B; a workgroup is 4 waves, wave w owns tile rows 4w..4w+3,
+// lane l owns cells 4l..4l+3 of each of its rows (one dwordx4 per row per
+// plane, loaded once from HBM).  Alive bits of a plane are published to LDS
+// packed 4 cells per u32 (one byte each); each lane forms its 3-wide row sums
+// with byte-SWAR from its own word and its neighbours' edge bytes, the
+// 3x3 plane sums by adding packed rows, and the 27-point sum across the
+// planes c-1, c, c+1 held in registers.  Counts <= 27 never carry across
+// bytes.  Raw centre values stay in registers for the B3/S23 rule.
+// ---------------------------------------------------------------------------
+struct Gol4Args {
+    const uint32_t* in;
+    uint32_t* out;
+    uint32_t* cnt;
+    uint64_t LA, LB, S;
+    uint64_t lo, hi;
+    int64_t cbase;
+    int64_t s0, s1;
+    int64_t chunk;
+    uint32_t tiles_a, tiles_b;
+    uint32_t nwg;
+    int32_t perA, perB;
+};
+
+__device__ __forceinline__ uint32_t pack_bits(uint4 v)
+{
+    return (v.x != 0u ? 1u : 0u) | (v.y != 0u ? 0x100u : 0u) | (v.z != 0u ? 0x10000u : 0u) |
+           (v.w != 0u ? 0x1000000u : 0u);
+}
+
+template <int NW, int RW, bool NT = false>
+__global__ void __launch_bounds__(64 * NW) k_gol26v(Gol4Args g)
+{
+    constexpr int TA = 256, TB = NW * RW;
+    static_assert(NW >= 2, "apron rows are loaded by the first and last wave");
+    __shared__ uint32_t P[2][TB + 2][64];
+    __shared__ uint32_t EL[2][TB + 2], ER[2][TB + 2];
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // XCD-aware remap (bijective): workgroups b and b+8 share an XCD; give each
+    // XCD a contiguous run of tiles so vertically adjacent tiles (which share
+    // apron rows) are served from the same L2.
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, q8 = g.nwg >> 3, r8 = g.nwg & 7;
+    const uint32_t wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const uint32_t tiles = g.tiles_a * g.tiles_b;
+    const uint32_t tile_id = wgid % tiles;
+    const int64_t chunk_id = wgid / tiles;
+    const int64_t a0 = (int64_t)(tile_id % g.tiles_a) * TA;
+    const int64_t b0 = (int64_t)(tile_id / g.tiles_a) * TB;
+    const int64_t c0 = g.s0 + chunk_id * g.chunk;
+    const int64_t c1 = min(g.s1, c0 + g.chunk);
+    if (c0 >= c1) return;
+
+    const int64_t LA = (int64_t)g.LA, LB = (int64_t)g.LB;
+    auto wrapA = [&](int64_t a) -> int64_t {  // -1: outside a non-periodic grid
+        if (a >= 0 && a < LA) return a;
+        return g.perA ? ug_wrap(a, LA) : -1;
+    };
+    auto wrapB = [&](int64_t b) -> int64_t {
+        if (b >= 0 && b < LB) return b;
+        return g.perB ? ug_wrap(b, LB) : -1;
+    };
+    // my vector column and rows (tile rows 1+RW*w+k), plus the apron row of the
+    // first / last wave.  In-plane offsets are 32-bit (plane < 2^31 cells) so the
+    // loads use a scalar plane base + one VGPR offset; invalid cells (outside a
+    // non-periodic grid) load offset 0 and are masked to zero.
+    const int64_t av = wrapA(a0 + 4 * lane);
+    uint32_t roff[RW + 1], eoff[RW + 1];
+    uint32_t rmask = 0, emask = 0;
+#pragma unroll
+    for (int k = 0; k < RW; k++) {
+        const int64_t b = wrapB(b0 + RW * w + k);
+        const bool ok = av >= 0 && b >= 0;
+        roff[k] = ok ? (uint32_t)(av + LA * b) : 0u;
+        rmask |= ok ? (1u << k) : 0u;
+    }
+    const int xrow = w == 0 ? 0 : (w == NW - 1 ? TB + 1 : -1);  // extra tile row of this wave
+    {
+        const int64_t b = xrow < 0 ? -1 : wrapB(b0 - 1 + xrow);
+        const bool ok = av >= 0 && b >= 0;
+        roff[RW] = ok ? (uint32_t)(av + LA * b) : 0u;
+        rmask |= ok ? (1u << RW) : 0u;
+    }
+    // apron columns: lane 0 the left one, lane 63 the right one, for my rows (+ extra row)
+    {
+        const int64_t ae = lane == 0 ? wrapA(a0 - 1) : (lane == 63 ? wrapA(a0 + TA) : -1);
+#pragma unroll
+        for (int k = 0; k <= RW; k++) {
+            const int64_t b = k < RW ? wrapB(b0 + RW * w + k) : (xrow < 0 ? -1 : wrapB(b0 - 1 + xrow));
+            const bool ok = ae >= 0 && b >= 0;
+            eoff[k] = ok ? (uint32_t)(ae + LA * b) : 0u;
+            emask |= ok ? (1u << k) : 0u;
+        }
+    }
+
+    uint4 F[RW + 1];       // fetched plane (own rows + extra row)
+    uint32_t FE[RW + 1];   // fetched apron scalars
+    auto fetch = [&](int64_t sc) {
+        const uint32_t* __restrict__ plane = g.in + (uint64_t)sc * g.S;
+#pragma unroll
+        for (int k = 0; k <= RW; k++) {
+            if (k == RW && xrow < 0) {
+                F[k] = make_uint4(0, 0, 0, 0);
+            } else {
+                const uint4 v = *reinterpret_cast<const uint4*>(plane + roff[k]);
+                F[k] = (rmask >> k) & 1u ? v : make_uint4(0, 0, 0, 0);
+            }
+        }
+        if (emask) {
+#pragma unroll
+            for (int k = 0; k <= RW; k++) FE[k] = (emask >> k) & 1u ? plane[eoff[k]] : 0u;
+        } else {
+#pragma unroll
+            for (int k = 0; k <= RW; k++) FE[k] = 0u;
+        }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int k = 0; k < RW; k++) P[buf][1 + RW * w + k][lane] = pack_bits(F[k]);
+        if (xrow >= 0) P[buf][xrow][lane] = pack_bits(F[RW]);
+        if (lane == 0 || lane == 63) {
+            uint32_t(*E)[TB + 2] = lane == 0 ? EL : ER;
+#pragma unroll
+            for (int k = 0; k < RW; k++) E[buf][1 + RW * w + k] = FE[k] != 0u ? 1u : 0u;
+            if (xrow >= 0) E[buf][xrow] = FE[RW] != 0u ? 1u : 0u;
+        }
+    };
+    uint32_t Sx[RW], Bx[RW];
+    auto plane_sums = [&](int buf) {
+        uint32_t h[RW + 2];
+        const int ll = lane > 0 ? lane - 1 : 0, lr = lane < 63 ? lane + 1 : 63;
+#pragma unroll
+        for (int q = 0; q < RW + 2; q++) {
+            const int rr = RW * w + q;
+            const uint32_t m = P[buf][rr][lane];
+            const uint32_t lft = lane > 0 ? (P[buf][rr][ll] >> 24) : EL[buf][rr];
+            const uint32_t rgt = lane < 63 ? (P[buf][rr][lr] & 0xffu) : ER[buf][rr];
+            h[q] = m + ((m << 8) | lft) + ((m >> 8) | (rgt << 24));
+            if (q >= 1 && q <= RW) Bx[q - 1] = m;
+        }
+#pragma unroll
+        for (int k = 0; k < RW; k++) Sx[k] = h[k] + h[k + 1] + h[k + 2];
+    };
+
+    uint32_t Sp[RW], Sc[RW], Bc[RW];
+    uint4 Vc[RW], Vn[RW];
+    fetch(c0 - 1);
+    stash(0);
+    fetch(c0);
+    __syncthreads();
+    plane_sums(0);
+#pragma unroll
+    for (int k = 0; k < RW; k++) Sp[k] = Sx[k];
+    stash(1);
+#pragma unroll
+    for (int k = 0; k < RW; k++) Vc[k] = F[k];
+    fetch(c0 + 1);
+    __syncthreads();
+    plane_sums(1);
+#pragma unroll
+    for (int k = 0; k < RW; k++) {
+        Sc[k] = Sx[k];
+        Bc[k] = Bx[k];
+    }
+    int buf = 0;
+    const uint64_t ua = (uint64_t)(a0 + 4 * lane);
+    const bool a_ok = (int64_t)ua < LA;
+    for (int64_t c = c0; c < c1; c++) {
+        stash(buf);
+#pragma unroll
+        for (int k = 0; k < RW; k++) Vn[k] = F[k];
+        if (c + 2 <= c1) fetch(c + 2);
+        __syncthreads();
+        plane_sums(buf);
+        buf ^= 1;
+        // plane c: canonical linear index of its first cell, storage offset
+        const uint64_t plin = g.S * (uint64_t)(c + g.cbase);
+        const bool full = plin >= g.lo && plin + g.S <= g.hi;  // wave-uniform
+        uint32_t* pcnt = g.cnt + (uint64_t)c * g.S;
+        uint32_t* pout = g.out + (uint64_t)c * g.S;
+#pragma unroll
+        for (int k = 0; k < RW; k++) {
+            const uint32_t cnt4 = Sp[k] + Sc[k] + Sx[k] - Bc[k];
+            const int64_t b = b0 + RW * w + k;
+            if (a_ok && b < LB) {
+                const uint32_t n0 = cnt4 & 0xffu, n1 = (cnt4 >> 8) & 0xffu, n2 = (cnt4 >> 16) & 0xffu,
+                               n3 = cnt4 >> 24;
+                const uint4 v = Vc[k];
+                const uint4 nc = make_uint4(n0, n1, n2, n3);
+                const uint4 nv = make_uint4(gol_rule(n0, v.x), gol_rule(n1, v.y), gol_rule(n2, v.z),
+                                            gol_rule(n3, v.w));
+                const uint32_t p = (uint32_t)ua + (uint32_t)LA * (uint32_t)b;
+                if (full) {
+                    if (NT) {
+                        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                        const u32x4 xc = {nc.x, nc.y, nc.z, nc.w}, xv = {nv.x, nv.y, nv.z, nv.w};
+                        __builtin_nontemporal_store(xc, reinterpret_cast<u32x4*>(pcnt + p));
+                        __builtin_nontemporal_store(xv, reinterpret_cast<u32x4*>(pout + p));
+                    } else {
+                        *reinterpret_cast<uint4*>(pcnt + p) = nc;
+                        *reinterpret_cast<uint4*>(pout + p) = nv;
+                    }
+                } else {
+                    const uint32_t ncs[4] = {nc.x, nc.y, nc.z, nc.w}, nvs[4] = {nv.x, nv.y, nv.z, nv.w};
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const uint64_t lin = plin + p + j;
+                        if (lin >= g.lo && lin < g.hi) {
+                            pcnt[p + j] = ncs[j];
+                            pout[p + j] = nvs[j];
+                        }
+                    }
+                }
+            }
+            Sp[k] = Sc[k];
+            Sc[k] = Sx[k];
+            Bc[k] = Bx[k];
+            Vc[k] = Vn[k];
         }
     }
 }
@@ -330,6 +554,18 @@ static unsigned grid_for(uint64_t n)
     return (unsigned)g;
 }
 
+static bool getenv_flag(const char* name)
+{
+    const char* v = getenv(name);
+    return v && *v && *v != '0';
+}
+
+static int64_t getenv_int(const char* name, int64_t dflt)
+{
+    const char* v = getenv(name);
+    return (v && *v) ? atoll(v) : dflt;
+}
+
 int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out, const Field& cnt,
                int64_t s0, int64_t s1, hipStream_t st)
 {
@@ -372,6 +608,56 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
         const uint32_t mult = u.perB ? 3u : 1u;
         hipLaunchKernelGGL((k_gol26_row<TA, NA>), dim3((unsigned)(a.tiles_a * chunks)), dim3(256), 0, st, a,
                            mult);
+    } else if (u.LA % 4 == 0 && u.S < (1ull << 31) && !getenv_flag("DCCRGX_GOL_SCALAR")) {
+        Gol4Args v{};
+        v.in = a.in;
+        v.out = a.out;
+        v.cnt = a.cnt;
+        v.LA = u.LA;
+        v.LB = u.LB;
+        v.S = u.S;
+        v.lo = u.lo;
+        v.hi = u.hi;
+        v.cbase = u.cbase;
+        v.s0 = s0;
+        v.s1 = s1;
+        v.perA = u.perA;
+        v.perB = u.perB;
+        // variant: waves per workgroup x rows per wave (tile = 256 x NW*RW)
+        // 8 x 4 with non-temporal stores measured fastest on MI355X
+        // (tools/gol_sweep.py; profiles/r1_summary.md)
+        int64_t var = getenv_int("DCCRGX_GOL_VARIANT", 841);
+        if (var != 44 && var != 42 && var != 81 && var != 162 && var != 82 && var != 84 &&
+            var != 1621)
+            var = 841;
+        const int64_t shape = var >= 1000 ? var / 10 : (var == 841 ? 84 : var);  // drop the NT digit
+        const int NW = (int)(shape / 10), RW = (int)(shape % 10);
+        const int TB = NW * RW;
+        v.tiles_a = (uint32_t)((u.LA + 255) / 256);
+        v.tiles_b = (uint32_t)((u.LB + TB - 1) / TB);
+        const int64_t tiles = (int64_t)v.tiles_a * v.tiles_b;
+        // slices per workgroup: enough workgroups to fill 256 CUs several times
+        int64_t chunk = getenv_int("DCCRGX_GOL_CHUNK", 0);
+        if (chunk <= 0) {
+            const int64_t want = getenv_int("DCCRGX_GOL_WGS", 8192);
+            int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(nsl, (want + tiles - 1) / tiles));
+            chunk = (nsl + chunks - 1) / chunks;
+        }
+        v.chunk = chunk;
+        const int64_t chunks = (nsl + chunk - 1) / chunk;
+        DX_CHECK(tiles * chunks < (int64_t)UINT32_MAX, DCCRGX_EINVAL, "grid too large for one launch");
+        v.nwg = (uint32_t)(tiles * chunks);
+        switch (var) {
+        case 44: hipLaunchKernelGGL((k_gol26v<4, 4>), dim3(v.nwg), dim3(256), 0, st, v); break;
+        case 42: hipLaunchKernelGGL((k_gol26v<4, 2>), dim3(v.nwg), dim3(256), 0, st, v); break;
+        case 81: hipLaunchKernelGGL((k_gol26v<8, 1>), dim3(v.nwg), dim3(512), 0, st, v); break;
+        case 162: hipLaunchKernelGGL((k_gol26v<16, 2>), dim3(v.nwg), dim3(1024), 0, st, v); break;
+        case 82: hipLaunchKernelGGL((k_gol26v<8, 2>), dim3(v.nwg), dim3(512), 0, st, v); break;
+        case 84: hipLaunchKernelGGL((k_gol26v<8, 4>), dim3(v.nwg), dim3(512), 0, st, v); break;
+        case 1621: hipLaunchKernelGGL((k_gol26v<16, 2, true>), dim3(v.nwg), dim3(1024), 0, st, v); break;
+        case 841:
+        default: hipLaunchKernelGGL((k_gol26v<8, 4, true>), dim3(v.nwg), dim3(512), 0, st, v); break;
+        }
     } else {
         constexpr int TA = 64, TB = 16, NA = 1, NB = 4;
         a.tiles_a = (uint32_t)((u.LA + TA - 1) / TA);

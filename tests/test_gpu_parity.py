@@ -259,6 +259,32 @@ def test_gol_bit_exact(length, periodic, hood, P):
         assert np.array_equal(c, ref_n), mode
 
 
+VEC_CASES = [
+    ((12, 20, 9), (True, True, True), 1),
+    ((264, 20, 5), (False, False, False), 1),
+    ((8, 40, 6), (True, False, True), 3),
+    ((520, 33, 4), (True, True, False), 2),
+    ((4, 4, 7), (False, True, True), 1),
+]
+
+
+@pytest.mark.parametrize("variant", ["82", "44", "42", "84", "81", "162", "841", "1621", "scalar"])
+@pytest.mark.parametrize("length,periodic,P", VEC_CASES)
+def test_gol_kernel_variants_bit_exact(monkeypatch, variant, length, periodic, P):
+    """Every build of the 26-neighbor stencil (tile shapes, scalar fallback)
+    against the oracle, including partial slabs and tile overhangs."""
+    if variant == "scalar":
+        monkeypatch.setenv("DCCRGX_GOL_SCALAR", "1")
+    else:
+        monkeypatch.setenv("DCCRGX_GOL_VARIANT", variant)
+        monkeypatch.setenv("DCCRGX_GOL_CHUNK", "3")
+    n = int(np.prod(length))
+    a0 = O.random_alive(np.arange(1, n + 1, dtype=np.uint64), 350)
+    ref_a, ref_n = O.gol_reference_run(length, periodic, 1, a0, 4)
+    a, c = gol_gpu(length, periodic, 1, a0, 4, P, "split" if P > 1 else "step")
+    assert np.array_equal(a, ref_a) and np.array_equal(c, ref_n)
+
+
 def test_gol_kat_15x15():
     k = GOLD["gol_kat"]
     n = int(np.prod(k["length"]))
