@@ -1,36 +1,745 @@
-// explicit.hip -- grids with mixed refinement levels (placeholder until the
-// device hash + CSR neighbor build lands).
+// explicit.hip -- grids with mixed refinement levels.
+//
+// The set of existing leaf cells is replicated on every rank (as the
+// reference's cell_process, dccrg.hpp:7311) in a device open-addressing hash
+// (64-bit id -> global leaf index).  Neighbor lists are built on the device
+// for every leaf, in closed form instead of the reference's face-graph walk
+// (dccrg.hpp:4375-4716): for item h of a cell at level l (length L in
+// indices) the window is the level-l cell at idx + h*L (periodic wrap in
+// index space, dropped outside a non-periodic grid); it is covered by
+//   - that cell itself                  -> one entry, offset h*L
+//   - its parent at level l-1           -> one entry, offset h*L - (window mod 2L)
+//   - its 8 children at level l+1       -> 8 entries x-fastest, offset h*L + d*L/2
+// which is exactly where the walk ends on a 2:1-balanced grid (the
+// reference's own assumption, dccrg.hpp:4736-4737).  neighbors_to
+// (dccrg.hpp:4744-4897) is the transpose of neighbors_of on such grids; it
+// is built by transposing the device CSR.  Storage slot of a cell = its
+// global leaf index (fields are sized for all leaves).
+#include <algorithm>
+#include <cstring>
+#include <set>
+
 #include "grid.hpp"
 
 namespace dccrgx {
 
-int explicit_create(dccrgx_grid*, const uint64_t*, size_t)
+struct Explicit {
+    uint64_t n = 0;                 // global leaves
+    std::vector<uint64_t> leaves;   // ascending
+    uint64_t* d_leaves = nullptr;
+    uint64_t* d_keys = nullptr;     // hash keys (0 = empty)
+    uint32_t* d_vals = nullptr;     // global index
+    uint64_t mask = 0;
+    Partition part;                 // over level-0 cells
+    std::vector<uint64_t> local;    // ascending local ids
+    std::vector<uint32_t> local_g;  // their global indices
+    uint32_t* d_local_g = nullptr;
+    struct HoodLists {
+        std::vector<uint64_t> h_nof_row, h_nto_row;
+        std::vector<uint32_t> h_nof_g, h_nto_g;
+        std::vector<uint32_t> inner_pos, outer_pos;  // positions in `local`
+        uint32_t* d_inner_pos = nullptr;
+        uint32_t* d_outer_pos = nullptr;
+        uint32_t* d_all_pos = nullptr;
+    };
+    std::map<int32_t, HoodLists> hl;
+};
+
+struct ExView {
+    MapParams mp;
+    const uint64_t* keys;
+    const uint32_t* vals;
+    uint64_t mask;
+    int32_t per[3];
+};
+
+__host__ __device__ inline uint64_t hmix(uint64_t x)
 {
-    return set_error(DCCRGX_EINVAL, "mixed-level grids are not supported yet");
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
 }
-void explicit_destroy(dccrgx_grid*) {}
-int explicit_build_hood(dccrgx_grid*, Hood&) { return set_error(DCCRGX_EINVAL, "unsupported"); }
-int explicit_get_cells(const dccrgx_grid*, const Hood&, int32_t, uint64_t*, size_t, size_t*)
+
+__device__ inline int64_t ex_find(const ExView& v, uint64_t id)
 {
-    return set_error(DCCRGX_EINVAL, "unsupported");
+    if (id == 0) return -1;
+    uint64_t h = hmix(id) & v.mask;
+    for (;;) {
+        const uint64_t k = v.keys[h];
+        if (k == id) return (int64_t)v.vals[h];
+        if (k == 0) return -1;
+        h = (h + 1) & v.mask;
+    }
 }
-int explicit_slots_of(const dccrgx_grid*, const uint64_t*, size_t, int64_t*, hipStream_t)
+
+__global__ void __launch_bounds__(256) k_hash_insert(const uint64_t* __restrict__ ids, size_t n,
+                                                     unsigned long long* keys, uint32_t* vals, uint64_t mask)
 {
-    return set_error(DCCRGX_EINVAL, "unsupported");
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const unsigned long long id = ids[i];
+        uint64_t h = hmix(id) & mask;
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&keys[h], 0ull, id);
+            if (prev == 0ull || prev == id) {
+                vals[h] = (uint32_t)i;
+                break;
+            }
+            h = (h + 1) & mask;
+        }
+    }
 }
-int explicit_neighbors_of(const dccrgx_grid*, const Hood&, const uint64_t*, size_t, uint64_t*, uint64_t*,
-                          int32_t*, size_t, hipStream_t)
+
+// neighbors_of of `cells` (pass 1: counts in row[i+1]; pass 2: fill from row[i])
+__global__ void __launch_bounds__(256) k_ex_nof(ExView v, const int32_t* __restrict__ items, int K,
+                                                const uint64_t* __restrict__ cells, size_t n,
+                                                uint64_t* __restrict__ row, uint64_t* __restrict__ ids,
+                                                int32_t* __restrict__ off, uint32_t* __restrict__ gidx,
+                                                int32_t* __restrict__ err)
 {
-    return set_error(DCCRGX_EINVAL, "unsupported");
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const MapParams& p = v.mp;
+    const int M = p.max_lvl;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t c = cells[i];
+        uint64_t w = ids ? row[i] : 0;
+        uint64_t idx[3];
+        int l;
+        if (ex_find(v, c) < 0 || !map_indices(p, c, idx, &l)) {
+            atomicOr(err, 1);
+            if (!ids) row[i + 1] = 0;
+            continue;
+        }
+        const int64_t L = (int64_t)1 << (M - l);
+        auto emit = [&](uint64_t id, int64_t g, int64_t ox, int64_t oy, int64_t oz) {
+            if (ids) {
+                ids[w] = id;
+                if (gidx) gidx[w] = (uint32_t)g;
+                if (off) {
+                    off[3 * w + 0] = (int32_t)ox;
+                    off[3 * w + 1] = (int32_t)oy;
+                    off[3 * w + 2] = (int32_t)oz;
+                }
+            }
+            w++;
+        };
+        for (int k = 0; k < K; k++) {
+            const int32_t* h = items + 3 * k;
+            uint64_t wi[3];
+            bool ok = true;
+            for (int d = 0; d < 3; d++) {
+                const int64_t G = (int64_t)(p.length[d] << M);
+                int64_t x = (int64_t)idx[d] + (int64_t)h[d] * L;
+                if (x < 0 || x >= G) {
+                    if (!v.per[d]) {
+                        ok = false;
+                        break;
+                    }
+                    x %= G;
+                    if (x < 0) x += G;
+                }
+                wi[d] = (uint64_t)x;
+            }
+            if (!ok) continue;  // outside a non-periodic grid: dropped (dccrg.hpp:4670-4672)
+            const uint64_t W = map_cell(p, wi, l);
+            int64_t g = ex_find(v, W);
+            if (g >= 0) {
+                emit(W, g, h[0] * L, h[1] * L, h[2] * L);
+                continue;
+            }
+            if (l > 0) {
+                const uint64_t P = map_cell(p, wi, l - 1);
+                g = ex_find(v, P);
+                if (g >= 0) {
+                    const int64_t L2 = 2 * L;
+                    emit(P, g, h[0] * L - (int64_t)(wi[0] % L2), h[1] * L - (int64_t)(wi[1] % L2),
+                         h[2] * L - (int64_t)(wi[2] % L2));
+                    continue;
+                }
+            }
+            if (l < M) {
+                const int64_t hl = L / 2;
+                bool all = true;
+                for (int dz = 0; dz < 2; dz++)
+                    for (int dy = 0; dy < 2; dy++)
+                        for (int dx = 0; dx < 2; dx++) {
+                            const uint64_t ci[3] = {wi[0] + dx * hl, wi[1] + dy * hl, wi[2] + dz * hl};
+                            const uint64_t ch = map_cell(p, ci, l + 1);
+                            const int64_t gc = ex_find(v, ch);
+                            all &= gc >= 0;
+                            emit(ch, gc, h[0] * L + dx * hl, h[1] * L + dy * hl, h[2] * L + dz * hl);
+                        }
+                if (all) continue;
+            }
+            atomicOr(err, 2);  // level difference > 1: outside the reference's assumptions
+        }
+        if (!ids) row[i + 1] = w;
+    }
 }
-int explicit_neighbors_to(const dccrgx_grid*, const Hood&, const uint64_t*, size_t, uint64_t*, uint64_t*,
-                          size_t, hipStream_t)
+
+// transpose helpers: rows = global leaves
+__global__ void __launch_bounds__(256) k_tr_count(const uint64_t* __restrict__ row, const uint32_t* __restrict__ tgt,
+                                                  uint64_t n, uint32_t* __restrict__ cnt)
 {
-    return set_error(DCCRGX_EINVAL, "unsupported");
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += stride)
+        for (uint64_t e = row[s]; e < row[s + 1]; e++) atomicAdd(&cnt[tgt[e]], 1u);
 }
-int explicit_gol(dccrgx_grid*, const Hood&, const Field&, const Field&, const Field&, int32_t, hipStream_t)
+
+__global__ void __launch_bounds__(256) k_tr_scatter(const uint64_t* __restrict__ row, const uint32_t* __restrict__ tgt,
+                                                    uint64_t n, const uint64_t* __restrict__ trow,
+                                                    uint32_t* __restrict__ cursor, uint32_t* __restrict__ out)
 {
-    return set_error(DCCRGX_EINVAL, "unsupported");
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += stride)
+        for (uint64_t e = row[s]; e < row[s + 1]; e++) {
+            const uint32_t t = tgt[e];
+            out[trow[t] + atomicAdd(&cursor[t], 1u)] = (uint32_t)s;
+        }
+}
+
+// per row: insertion sort + unique in place; unique count -> ucnt
+__global__ void __launch_bounds__(256) k_sort_unique_rows(const uint64_t* __restrict__ row, uint64_t n,
+                                                          uint32_t* __restrict__ v, uint32_t* __restrict__ ucnt)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
+        uint32_t* a = v + row[r];
+        const uint64_t m = row[r + 1] - row[r];
+        for (uint64_t i = 1; i < m; i++) {
+            const uint32_t x = a[i];
+            uint64_t j = i;
+            while (j > 0 && a[j - 1] > x) {
+                a[j] = a[j - 1];
+                j--;
+            }
+            a[j] = x;
+        }
+        uint64_t u = 0;
+        for (uint64_t i = 0; i < m; i++)
+            if (u == 0 || a[i] != a[u - 1]) a[u++] = a[i];
+        ucnt[r] = (uint32_t)u;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_copy_rows(const uint64_t* __restrict__ srow, const uint32_t* __restrict__ sv,
+                                                   const uint64_t* __restrict__ drow, uint64_t n,
+                                                   uint32_t* __restrict__ dv)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride)
+        for (uint64_t i = 0; i < drow[r + 1] - drow[r]; i++) dv[drow[r] + i] = sv[srow[r] + i];
+}
+
+// stencil rows for local cells: unique (leaf, offset) pairs of neighbors_of
+struct Pair {
+    uint32_t g;
+    int32_t x, y, z;
+};
+__device__ inline bool pair_less(const Pair& a, const Pair& b)
+{
+    if (a.g != b.g) return a.g < b.g;
+    if (a.x != b.x) return a.x < b.x;
+    if (a.y != b.y) return a.y < b.y;
+    return a.z < b.z;
+}
+__device__ inline bool pair_eq(const Pair& a, const Pair& b)
+{
+    return a.g == b.g && a.x == b.x && a.y == b.y && a.z == b.z;
+}
+
+__global__ void __launch_bounds__(256) k_stencil_rows(const uint64_t* __restrict__ nof_row,
+                                                      const uint32_t* __restrict__ nof_g,
+                                                      const int32_t* __restrict__ nof_off,
+                                                      const uint32_t* __restrict__ local_g, uint64_t nl,
+                                                      const uint64_t* __restrict__ tmp_row, Pair* __restrict__ tmp,
+                                                      uint32_t* __restrict__ ucnt)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
+        const uint32_t r = local_g[i];
+        Pair* a = tmp + tmp_row[i];
+        const uint64_t m = nof_row[r + 1] - nof_row[r];
+        for (uint64_t e = 0; e < m; e++) {
+            const uint64_t s = nof_row[r] + e;
+            Pair x{nof_g[s], nof_off[3 * s], nof_off[3 * s + 1], nof_off[3 * s + 2]};
+            uint64_t j = e;
+            while (j > 0 && pair_less(x, a[j - 1])) {
+                a[j] = a[j - 1];
+                j--;
+            }
+            a[j] = x;
+        }
+        uint64_t u = 0;
+        for (uint64_t e = 0; e < m; e++)
+            if (u == 0 || !pair_eq(a[e], a[u - 1])) a[u++] = a[e];
+        ucnt[i] = (uint32_t)u;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_stencil_slots(const uint64_t* __restrict__ tmp_row, const Pair* __restrict__ tmp,
+                                                       const uint64_t* __restrict__ st_row, uint64_t nl,
+                                                       uint32_t* __restrict__ st_slot)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride)
+        for (uint64_t e = 0; e < st_row[i + 1] - st_row[i]; e++) st_slot[st_row[i] + e] = tmp[tmp_row[i] + e].g;
+}
+
+__global__ void __launch_bounds__(256) k_ex_gol(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                uint32_t* __restrict__ cnt, const uint64_t* __restrict__ st_row,
+                                                const uint32_t* __restrict__ st_slot,
+                                                const uint32_t* __restrict__ local_g,
+                                                const uint32_t* __restrict__ pos, uint64_t n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t q = pos[i];
+        uint32_t c = 0;
+        for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) c += in[st_slot[e]] != 0u ? 1u : 0u;
+        const uint32_t s = local_g[q];
+        cnt[s] = c;
+        out[s] = c == 3u ? 1u : (c == 2u ? in[s] : 0u);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ex_slots(ExView v, const uint64_t* __restrict__ ids, size_t n,
+                                                  int64_t* __restrict__ slots)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) slots[i] = ex_find(v, ids[i]);
+}
+
+static unsigned grid_for(uint64_t n)
+{
+    uint64_t g = (n + 255) / 256;
+    if (g > 256 * 16) g = 256 * 16;
+    if (g == 0) g = 1;
+    return (unsigned)g;
+}
+
+static ExView view(const dccrgx_grid* grid)
+{
+    ExView v{};
+    v.mp = grid->map;
+    v.keys = grid->ex->d_keys;
+    v.vals = grid->ex->d_vals;
+    v.mask = grid->ex->mask;
+    for (int d = 0; d < 3; d++) v.per[d] = grid->params.periodic[d] ? 1 : 0;
+    return v;
+}
+
+static int scan_counts_u32(const uint32_t* d_cnt, uint64_t n, std::vector<uint64_t>& row, hipStream_t st)
+{
+    std::vector<uint32_t> h(n);
+    if (n) DX_HIP(hipMemcpyAsync(h.data(), d_cnt, n * 4, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    row.assign(n + 1, 0);
+    for (uint64_t i = 0; i < n; i++) row[i + 1] = row[i] + h[i];
+    return DCCRGX_OK;
+}
+
+template <class T>
+static int upload(const std::vector<T>& v, T** d, hipStream_t st)
+{
+    *d = nullptr;
+    DX_HIP(hipMalloc(d, std::max<size_t>(v.size(), 1) * sizeof(T)));
+    if (!v.empty()) DX_HIP(hipMemcpyAsync(*d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
+    return DCCRGX_OK;
+}
+
+// neighbors_of for a device array of cells: row (n+1, device) + optional outputs
+static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n, uint64_t* row,
+                      uint64_t** ids, int32_t** off, uint32_t** gidx, uint64_t* total, hipStream_t st)
+{
+    const ExView v = view(grid);
+    int32_t* d_err = nullptr;
+    DX_HIP(hipMalloc(&d_err, 4));
+    DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
+    DX_HIP(hipMemsetAsync(row, 0, 8, st));
+    if (n)
+        hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(n)), dim3(256), 0, st, v, h.d_of_c, h.K, cells, n, row,
+                           (uint64_t*)nullptr, (int32_t*)nullptr, (uint32_t*)nullptr, d_err);
+    DX_HIP(hipGetLastError());
+    std::vector<uint64_t> hr(n + 1);
+    DX_HIP(hipMemcpyAsync(hr.data(), row, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    hr[0] = 0;
+    for (size_t i = 0; i < n; i++) hr[i + 1] += hr[i];
+    DX_HIP(hipMemcpyAsync(row, hr.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    *total = hr[n];
+    int32_t err = 0;
+    DX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    if (err) {
+        hipFree(d_err);
+        return set_error(err & 1 ? DCCRGX_ENOTFOUND : DCCRGX_EINTERNAL,
+                         err & 1 ? "cell does not exist" : "neighbor more than one level apart");
+    }
+    if (ids) {
+        uint64_t t = std::max<uint64_t>(*total, 1);
+        DX_HIP(hipMalloc(ids, t * 8));
+        DX_HIP(hipMalloc(off, t * 12));
+        DX_HIP(hipMalloc(gidx, t * 4));
+        if (n)
+            hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(n)), dim3(256), 0, st, v, h.d_of_c, h.K, cells, n, row,
+                               *ids, *off, *gidx, d_err);
+        DX_HIP(hipGetLastError());
+    }
+    hipFree(d_err);
+    return DCCRGX_OK;
+}
+
+int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
+{
+    Ctx* ctx = grid->ctx;
+    hipStream_t st = ctx->compute;
+    DX_CHECK(n > 0 && n < (1ull << 32), DCCRGX_EINVAL, "leaf count %zu", n);
+    auto* E = new Explicit();
+    grid->ex = E;
+    E->leaves.assign(leaves, leaves + n);
+    std::sort(E->leaves.begin(), E->leaves.end());
+    E->leaves.erase(std::unique(E->leaves.begin(), E->leaves.end()), E->leaves.end());
+    for (uint64_t c : E->leaves)
+        DX_CHECK(map_level(grid->map, c) >= 0, DCCRGX_EINVAL, "invalid cell %llu", (unsigned long long)c);
+    E->n = E->leaves.size();
+    uint64_t cap = 16;
+    while (cap < 2 * E->n) cap <<= 1;
+    E->mask = cap - 1;
+    DX_TRY(upload(E->leaves, &E->d_leaves, st));
+    DX_HIP(hipMalloc(&E->d_keys, cap * 8));
+    DX_HIP(hipMalloc(&E->d_vals, cap * 4));
+    DX_HIP(hipMemsetAsync(E->d_keys, 0, cap * 8, st));
+    hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(E->n)), dim3(256), 0, st, E->d_leaves, E->n,
+                       (unsigned long long*)E->d_keys, E->d_vals, E->mask);
+    DX_HIP(hipGetLastError());
+    // ownership: the process of the level-0 ancestor (no load balancing)
+    E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
+    for (uint64_t i = 0; i < E->n; i++) {
+        uint64_t idx[3];
+        int l;
+        map_indices(grid->map, E->leaves[i], idx, &l);
+        const uint64_t l0 = map_cell(grid->map, idx, 0);
+        if (part_owner(E->part, l0) == ctx->rank) {
+            E->local.push_back(E->leaves[i]);
+            E->local_g.push_back((uint32_t)i);
+        }
+    }
+    DX_TRY(upload(E->local_g, &E->d_local_g, st));
+    grid->n_local = E->local.size();
+    grid->first_local = E->local.empty() ? 0 : E->local[0];
+    grid->n_slots = E->n;
+    Hood h;
+    h.id = DCCRGX_DEFAULT_NEIGHBORHOOD_ID;
+    // default items, dccrg.hpp:8017-8076
+    const uint32_t hl = grid->params.neighborhood_length;
+    if (hl == 0) {
+        const int32_t f[6][3] = {{0, 0, -1}, {0, -1, 0}, {-1, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+        for (auto& it : f) h.items.insert(h.items.end(), it, it + 3);
+    } else {
+        const int hh = (int)hl;
+        for (int z = -hh; z <= hh; z++)
+            for (int y = -hh; y <= hh; y++)
+                for (int x = -hh; x <= hh; x++)
+                    if (x || y || z) h.items.insert(h.items.end(), {x, y, z});
+    }
+    grid->hoods[h.id] = h;
+    return explicit_build_hood(grid, grid->hoods[h.id]);
+}
+
+void explicit_destroy(dccrgx_grid* grid)
+{
+    Explicit* E = grid->ex;
+    if (!E) return;
+    hipFree(E->d_leaves);
+    hipFree(E->d_keys);
+    hipFree(E->d_vals);
+    hipFree(E->d_local_g);
+    for (auto& kv : E->hl) {
+        hipFree(kv.second.d_inner_pos);
+        hipFree(kv.second.d_outer_pos);
+        hipFree(kv.second.d_all_pos);
+    }
+    delete E;
+    grid->ex = nullptr;
+}
+
+int explicit_build_hood(dccrgx_grid* grid, Hood& h)
+{
+    Explicit* E = grid->ex;
+    Ctx* ctx = grid->ctx;
+    hipStream_t st = ctx->compute;
+    free_hood(h);
+    h.K = (int32_t)(h.items.size() / 3);
+    h.of_c = h.items;  // explicit grids use the original axes
+    h.to_c.resize(h.items.size());
+    for (size_t i = 0; i < h.items.size(); i++) h.to_c[i] = -h.items[i];
+    DX_TRY(upload(h.of_c, &h.d_of_c, st));
+    DX_TRY(upload(h.to_c, &h.d_to_c, st));
+    h.outer.clear();
+    h.remote.clear();
+    const uint64_t N = E->n;
+    h.n_rows = N;
+    // neighbors_of of every leaf (the reference also builds all of them)
+    DX_HIP(hipMalloc(&h.d_nof_row, (N + 1) * 8));
+    uint64_t tot = 0;
+    DX_TRY(nof_device(grid, h, E->d_leaves, N, h.d_nof_row, &h.d_nof_id, &h.d_nof_off, &h.d_nof_g, &tot, st));
+    // neighbors_to = transpose (rows: leaves)
+    uint32_t *d_cnt = nullptr, *d_cur = nullptr, *d_tmp = nullptr, *d_ucnt = nullptr;
+    DX_HIP(hipMalloc(&d_cnt, N * 4));
+    DX_HIP(hipMalloc(&d_cur, N * 4));
+    DX_HIP(hipMemsetAsync(d_cnt, 0, N * 4, st));
+    DX_HIP(hipMemsetAsync(d_cur, 0, N * 4, st));
+    hipLaunchKernelGGL(k_tr_count, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_cnt);
+    std::vector<uint64_t> trow;
+    DX_TRY(scan_counts_u32(d_cnt, N, trow, st));
+    uint64_t* d_trow = nullptr;
+    DX_TRY(upload(trow, &d_trow, st));
+    DX_HIP(hipMalloc(&d_tmp, std::max<uint64_t>(trow[N], 1) * 4));
+    hipLaunchKernelGGL(k_tr_scatter, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_trow,
+                       d_cur, d_tmp);
+    DX_HIP(hipMalloc(&d_ucnt, N * 4));
+    hipLaunchKernelGGL(k_sort_unique_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, N, d_tmp, d_ucnt);
+    DX_HIP(hipGetLastError());
+    std::vector<uint64_t> nto_row;
+    DX_TRY(scan_counts_u32(d_ucnt, N, nto_row, st));
+    DX_TRY(upload(nto_row, &h.d_nto_row, st));
+    DX_HIP(hipMalloc(&h.d_nto_g, std::max<uint64_t>(nto_row[N], 1) * 4));
+    hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, d_tmp, h.d_nto_row, N, h.d_nto_g);
+    DX_HIP(hipGetLastError());
+    hipFree(d_cnt);
+    hipFree(d_cur);
+    hipFree(d_tmp);
+    hipFree(d_ucnt);
+    hipFree(d_trow);
+
+    // stencil rows of local cells (iteration-cache neighbors_of: unique pairs)
+    const uint64_t nl = E->local.size();
+    std::vector<uint64_t> nof_row(N + 1);
+    DX_HIP(hipMemcpyAsync(nof_row.data(), h.d_nof_row, (N + 1) * 8, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    std::vector<uint64_t> tmp_row(nl + 1, 0);
+    for (uint64_t i = 0; i < nl; i++) {
+        const uint32_t r = E->local_g[i];
+        tmp_row[i + 1] = tmp_row[i] + (nof_row[r + 1] - nof_row[r]);
+    }
+    uint64_t* d_tmp_row = nullptr;
+    Pair* d_pairs = nullptr;
+    uint32_t* d_pc = nullptr;
+    DX_TRY(upload(tmp_row, &d_tmp_row, st));
+    DX_HIP(hipMalloc(&d_pairs, std::max<uint64_t>(tmp_row[nl], 1) * sizeof(Pair)));
+    DX_HIP(hipMalloc(&d_pc, std::max<uint64_t>(nl, 1) * 4));
+    if (nl)
+        hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
+                           h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
+    std::vector<uint64_t> st_row;
+    DX_TRY(scan_counts_u32(d_pc, nl, st_row, st));
+    DX_TRY(upload(st_row, &h.d_st_row, st));
+    DX_HIP(hipMalloc(&h.d_st_slot, std::max<uint64_t>(st_row[nl], 1) * 4));
+    if (nl)
+        hipLaunchKernelGGL(k_stencil_slots, dim3(grid_for(nl)), dim3(256), 0, st, d_tmp_row, d_pairs, h.d_st_row, nl,
+                           h.d_st_slot);
+    DX_HIP(hipGetLastError());
+    hipFree(d_tmp_row);
+    hipFree(d_pairs);
+    hipFree(d_pc);
+
+    // per-rank bookkeeping from the device lists (dccrg.hpp:9131-9234, 8729-8891)
+    Explicit::HoodLists& L = E->hl[h.id];
+    for (uint32_t* p : {L.d_inner_pos, L.d_outer_pos, L.d_all_pos}) hipFree(p);
+    L = Explicit::HoodLists{};
+    L.h_nof_row = nof_row;
+    L.h_nof_g.resize(nof_row[N]);
+    L.h_nto_row = nto_row;
+    L.h_nto_g.resize(nto_row[N]);
+    if (nof_row[N]) DX_HIP(hipMemcpyAsync(L.h_nof_g.data(), h.d_nof_g, nof_row[N] * 4, hipMemcpyDeviceToHost, st));
+    if (nto_row[N]) DX_HIP(hipMemcpyAsync(L.h_nto_g.data(), h.d_nto_g, nto_row[N] * 4, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    auto owner_of = [&](uint32_t g) {
+        uint64_t idx[3];
+        int l;
+        map_indices(grid->map, E->leaves[g], idx, &l);
+        return part_owner(E->part, map_cell(grid->map, idx, 0));
+    };
+    std::vector<int> owner(N);
+    for (uint64_t g = 0; g < N; g++) owner[g] = owner_of((uint32_t)g);
+    const int me = ctx->rank;
+    std::set<uint64_t> remote;
+    std::map<int, std::set<uint64_t>> send, recv;
+    for (uint64_t i = 0; i < nl; i++) {
+        const uint32_t r = E->local_g[i];
+        bool outer = false;
+        for (uint64_t e = nof_row[r]; e < nof_row[r + 1]; e++) {
+            const uint32_t t = L.h_nof_g[e];
+            if (owner[t] != me) {
+                outer = true;
+                remote.insert(E->leaves[t]);
+                recv[owner[t]].insert(E->leaves[t]);
+            }
+        }
+        for (uint64_t e = nto_row[r]; e < nto_row[r + 1]; e++) {
+            const uint32_t t = L.h_nto_g[e];
+            if (owner[t] != me) {
+                outer = true;
+                remote.insert(E->leaves[t]);
+                send[owner[t]].insert(E->local[i]);
+            }
+        }
+        (outer ? L.outer_pos : L.inner_pos).push_back((uint32_t)i);
+        if (outer) h.outer.push_back(E->local[i]);
+    }
+    h.remote.assign(remote.begin(), remote.end());
+    std::set<int> peers;
+    for (auto& kv : send) peers.insert(kv.first);
+    for (auto& kv : recv) peers.insert(kv.first);
+    auto gidx_of = [&](uint64_t id) {
+        return (uint64_t)(std::lower_bound(E->leaves.begin(), E->leaves.end(), id) - E->leaves.begin());
+    };
+    for (int p : peers) {
+        PeerPlan pp;
+        pp.peer = p;
+        pp.send_ids.assign(send[p].begin(), send[p].end());
+        pp.recv_ids.assign(recv[p].begin(), recv[p].end());
+        std::vector<uint64_t> ss, rd;
+        for (uint64_t c : pp.send_ids) ss.push_back(gidx_of(c));
+        for (uint64_t c : pp.recv_ids) rd.push_back(gidx_of(c));
+        if (!ss.empty()) DX_TRY(upload(ss, &pp.d_send_slots, st));
+        if (!rd.empty()) DX_TRY(upload(rd, &pp.d_unpack_dst, st));
+        pp.n_unpack = rd.size();
+        h.peers.push_back(std::move(pp));
+    }
+    std::vector<uint32_t> all(nl);
+    for (uint64_t i = 0; i < nl; i++) all[i] = (uint32_t)i;
+    DX_TRY(upload(L.inner_pos, &L.d_inner_pos, st));
+    DX_TRY(upload(L.outer_pos, &L.d_outer_pos, st));
+    DX_TRY(upload(all, &L.d_all_pos, st));
+    DX_HIP(hipStreamSynchronize(st));
+    return DCCRGX_OK;
+}
+
+int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, uint64_t* ids, size_t cap,
+                       size_t* n)
+{
+    const Explicit* E = grid->ex;
+    const std::vector<uint64_t>* v = nullptr;
+    std::vector<uint64_t> inner;
+    switch (which) {
+    case DCCRGX_CELLS_LOCAL: v = &E->local; break;
+    case DCCRGX_CELLS_OUTER: v = &h.outer; break;
+    case DCCRGX_CELLS_REMOTE: v = &h.remote; break;
+    case DCCRGX_CELLS_INNER: {
+        const auto& L = E->hl.at(h.id);
+        for (uint32_t p : L.inner_pos) inner.push_back(E->local[p]);
+        v = &inner;
+        break;
+    }
+    default: return set_error(DCCRGX_EINVAL, "unknown cell class %d", which);
+    }
+    *n = v->size();
+    DX_CHECK(cap >= *n && (ids || !*n), DCCRGX_ERANGE, "capacity");
+    std::copy(v->begin(), v->end(), ids);
+    return DCCRGX_OK;
+}
+
+int explicit_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int64_t* slots, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_ex_slots, dim3(grid_for(n)), dim3(256), 0, st, view(grid), ids, n, slots);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n, uint64_t* row,
+                          uint64_t* ids, int32_t* off3, size_t cap, hipStream_t st)
+{
+    dccrgx_grid* g = const_cast<dccrgx_grid*>(grid);
+    uint64_t total = 0;
+    uint64_t* t_ids = nullptr;
+    int32_t* t_off = nullptr;
+    uint32_t* t_g = nullptr;
+    DX_TRY(nof_device(g, h, cells, n, row, ids ? &t_ids : nullptr, &t_off, &t_g, &total, st));
+    if (!ids) return DCCRGX_OK;
+    int s = DCCRGX_OK;
+    if (cap < total) s = set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total);
+    else if (total) {
+        DX_HIP(hipMemcpyAsync(ids, t_ids, total * 8, hipMemcpyDeviceToDevice, st));
+        if (off3) DX_HIP(hipMemcpyAsync(off3, t_off, total * 12, hipMemcpyDeviceToDevice, st));
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(t_ids);
+    hipFree(t_off);
+    hipFree(t_g);
+    return s;
+}
+
+int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n, uint64_t* row,
+                          uint64_t* ids, size_t cap, hipStream_t st)
+{
+    const Explicit* E = grid->ex;
+    const auto& L = E->hl.at(h.id);
+    std::vector<uint64_t> hc(n);
+    if (n) DX_HIP(hipMemcpyAsync(hc.data(), cells, n * 8, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    std::vector<uint64_t> orow(n + 1, 0), oids;
+    for (size_t i = 0; i < n; i++) {
+        auto it = std::lower_bound(E->leaves.begin(), E->leaves.end(), hc[i]);
+        DX_CHECK(it != E->leaves.end() && *it == hc[i], DCCRGX_ENOTFOUND, "cell %llu does not exist",
+                 (unsigned long long)hc[i]);
+        const uint64_t g = (uint64_t)(it - E->leaves.begin());
+        for (uint64_t e = L.h_nto_row[g]; e < L.h_nto_row[g + 1]; e++) oids.push_back(E->leaves[L.h_nto_g[e]]);
+        orow[i + 1] = oids.size();
+    }
+    DX_HIP(hipMemcpyAsync(row, orow.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    if (ids) {
+        DX_CHECK(cap >= oids.size(), DCCRGX_ERANGE, "capacity %zu < %zu", cap, oids.size());
+        if (!oids.empty()) DX_HIP(hipMemcpyAsync(ids, oids.data(), oids.size() * 8, hipMemcpyHostToDevice, st));
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    return DCCRGX_OK;
+}
+
+int explicit_gol(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out, const Field& cnt,
+                 int32_t region, hipStream_t st)
+{
+    const Explicit* E = grid->ex;
+    const auto& L = E->hl.at(h.id);
+    const uint32_t* pos = region == DCCRGX_REGION_INNER ? L.d_inner_pos
+                          : region == DCCRGX_REGION_OUTER ? L.d_outer_pos : L.d_all_pos;
+    const uint64_t n = region == DCCRGX_REGION_INNER ? L.inner_pos.size()
+                       : region == DCCRGX_REGION_OUTER ? L.outer_pos.size() : E->local.size();
+    if (!n) return DCCRGX_OK;
+    hipLaunchKernelGGL(k_ex_gol, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)in.ptr, (uint32_t*)out.ptr,
+                       (uint32_t*)cnt.ptr, h.d_st_row, h.d_st_slot, E->d_local_g, pos, n);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+// local values in ascending id order <-> slots (global leaf index)
+int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device)
+{
+    const Explicit* E = grid->ex;
+    hipStream_t st = grid->ctx->compute;
+    const uint64_t n = E->local.size();
+    if (!n) return DCCRGX_OK;
+    void* d_buf = nullptr;
+    uint64_t* d_idx = nullptr;
+    std::vector<uint64_t> idx(E->local_g.begin(), E->local_g.end());
+    DX_TRY(upload(idx, &d_idx, st));
+    DX_HIP(hipMalloc(&d_buf, n * F.elem));
+    int s = DCCRGX_OK;
+    if (to_device) {
+        DX_HIP(hipMemcpyAsync(d_buf, host, n * F.elem, hipMemcpyHostToDevice, st));
+        s = launch_scatter_ext(d_buf, nullptr, d_idx, n, F.elem, F.ptr, st);
+    } else {
+        s = launch_gather_ext(F.ptr, d_idx, n, F.elem, d_buf, st);
+        if (s == DCCRGX_OK) DX_HIP(hipMemcpyAsync(host, d_buf, n * F.elem, hipMemcpyDeviceToHost, st));
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_buf);
+    hipFree(d_idx);
+    return s;
 }
 
 }  // namespace dccrgx

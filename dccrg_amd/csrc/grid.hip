@@ -286,6 +286,13 @@ void free_hood(Hood& h)
     h.d_of_c = h.d_to_c = nullptr;
     h.d_self_dst = h.d_self_src = nullptr;
     h.peers.clear();
+    for (void* p : {(void*)h.d_nof_row, (void*)h.d_nof_id, (void*)h.d_nof_off, (void*)h.d_nof_g,
+                    (void*)h.d_nto_row, (void*)h.d_nto_g, (void*)h.d_st_row, (void*)h.d_st_slot})
+        hipFree(p);
+    h.d_nof_row = h.d_nof_id = h.d_nto_row = h.d_st_row = nullptr;
+    h.d_nof_off = nullptr;
+    h.d_nof_g = h.d_nto_g = h.d_st_slot = nullptr;
+    h.n_rows = 0;
 }
 
 Hood* find_hood(dccrgx_grid* g, int32_t id)

@@ -104,6 +104,8 @@ struct PeerPlan {
     size_t recv_buf_bytes = 0;
 };
 
+struct Explicit;  // explicit.hip
+
 struct CopySeg {
     uint64_t dst, src, n;  // contiguous slot run
 };
@@ -130,6 +132,19 @@ struct Hood {
     int64_t inner_s0 = 0, inner_s1 = 0;  // fully local and only local reads
     bool pending = false;                // halo started, not waited
     std::vector<int32_t> pending_fields; // fields of the started halo
+    // explicit (mixed-level) grids: device CSR over ALL leaves (global index
+    // rows), as the reference keeps lists for every cell (dccrg.hpp:8371-8397)
+    uint64_t n_rows = 0;
+    uint64_t* d_nof_row = nullptr;   // neighbors_of, reference list order
+    uint64_t* d_nof_id = nullptr;
+    int32_t* d_nof_off = nullptr;    // x, y, z offsets in indices
+    uint32_t* d_nof_g = nullptr;     // global leaf index of each entry
+    uint64_t* d_nto_row = nullptr;   // neighbors_to, ascending
+    uint32_t* d_nto_g = nullptr;
+    // stencil rows of local cells: iteration-cache neighbors_of (unique
+    // (id, offset) pairs, dccrg.hpp:11570-11712) as storage slots
+    uint64_t* d_st_row = nullptr;
+    uint32_t* d_st_slot = nullptr;
 };
 
 }  // namespace dccrgx
@@ -143,6 +158,8 @@ struct dccrgx_grid {
     uint64_t n_local = 0, first_local = 0, n_slots = 0;
     std::vector<dccrgx::Field> fields;
     std::map<int32_t, dccrgx::Hood> hoods;
+    // explicit grids (explicit.hip)
+    dccrgx::Explicit* ex = nullptr;
     // kernel timing (dccrgx_kernel_timer)
     hipEvent_t t0 = nullptr, t1 = nullptr;
     double timed_ms = 0;
@@ -162,4 +179,9 @@ void explicit_destroy(dccrgx_grid* grid);
 int explicit_build_hood(dccrgx_grid* grid, Hood& h);
 int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, uint64_t* ids,
                        size_t cap, size_t* n);
+int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device);
+int launch_gather_ext(const void* src, const uint64_t* idx, uint64_t n, uint32_t elem, void* dst,
+                      hipStream_t st);
+int launch_scatter_ext(const void* src, const uint64_t* sidx, const uint64_t* didx, uint64_t n,
+                       uint32_t elem, void* dst, hipStream_t st);
 }  // namespace dccrgx

@@ -78,6 +78,18 @@ static int launch_scatter(const void* src, const uint64_t* sidx, const uint64_t*
     return DCCRGX_OK;
 }
 
+int launch_gather_ext(const void* src, const uint64_t* idx, uint64_t n, uint32_t elem, void* dst,
+                      hipStream_t st)
+{
+    return launch_gather(src, idx, n, elem, dst, st);
+}
+
+int launch_scatter_ext(const void* src, const uint64_t* sidx, const uint64_t* didx, uint64_t n,
+                       uint32_t elem, void* dst, hipStream_t st)
+{
+    return launch_scatter(src, sidx, didx, n, elem, dst, st);
+}
+
 static int check_fields(const dccrgx_grid* g, const int32_t* f, size_t nf, size_t* bytes_per_cell)
 {
     DX_CHECK(f || nf == 0, DCCRGX_EINVAL, "null field list");
@@ -254,6 +266,7 @@ int dccrgx_field_write_local(dccrgx_grid* grid, int32_t fid, const void* host, s
              (unsigned long long)grid->n_local);
     if (!n) return DCCRGX_OK;
     const Field& F = grid->fields[fid];
+    if (!grid->uniform) return explicit_local_copy(grid, F, const_cast<void*>(host), true);
     DX_HIP(hipMemcpyAsync((char*)F.ptr + local_slot0(grid) * F.elem, host, n * F.elem,
                           hipMemcpyHostToDevice, grid->ctx->compute));
     DX_HIP(hipStreamSynchronize(grid->ctx->compute));
@@ -267,6 +280,7 @@ int dccrgx_field_read_local(const dccrgx_grid* grid, int32_t fid, void* host, si
              (unsigned long long)grid->n_local);
     if (!n) return DCCRGX_OK;
     const Field& F = grid->fields[fid];
+    if (!grid->uniform) return explicit_local_copy(grid, F, host, false);
     DX_HIP(hipMemcpyAsync(host, (char*)F.ptr + local_slot0(grid) * F.elem, n * F.elem,
                           hipMemcpyDeviceToHost, grid->ctx->compute));
     DX_HIP(hipStreamSynchronize(grid->ctx->compute));

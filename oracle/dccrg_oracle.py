@@ -408,3 +408,25 @@ def splitmix64(x: np.ndarray) -> np.ndarray:
 def random_alive(ids: np.ndarray, p_permille: int = 200) -> np.ndarray:
     """alive = splitmix64(id) % 1000 < p_permille (bit-exact on CPU and GPU)."""
     return (splitmix64(ids) % np.uint64(1000) < np.uint64(p_permille)).astype(np.uint32)
+
+
+def random_balanced_leaves(length, max_ref_lvl, periodic, hood_length, n_refines, seed):
+    """Random 2:1-balanced leaf set (test input generator): a cell of level l
+    is refined only when every cell in its neighbors_of and neighbors_to has
+    level >= l, which keeps neighbors within one level (the assumption of
+    dccrg.hpp:4736-4737, enforced in the reference by induce_refines)."""
+    rng = np.random.default_rng(seed)
+    m = Mapping(length, max_ref_lvl)
+    cells = set(range(1, int(np.prod(length)) + 1))
+    for _ in range(n_refines):
+        g = Grid(length, max_ref_lvl, periodic, hood_length, sorted(cells))
+        cand = sorted(c for c in cells if m.get_refinement_level(c) < m.max_ref_lvl)
+        if not cand:
+            break
+        c = int(cand[int(rng.integers(len(cand)))])
+        lvl = m.get_refinement_level(c)
+        if all(m.get_refinement_level(n) >= lvl for n, _ in g.find_neighbors_of(c)) and \
+                all(m.get_refinement_level(n) >= lvl for n in g.find_neighbors_to(c)):
+            cells.discard(c)
+            cells |= set(m.get_all_children(c))
+    return sorted(cells)

@@ -1,0 +1,201 @@
+"""GPU parity for grids with mixed refinement levels (explicit leaf sets):
+device hash + closed-form neighbor CSR vs the oracle's face-graph walk
+(dccrg.hpp:4375-4716) and find_neighbors_to (dccrg.hpp:4744-4897), per-rank
+classification and send/receive lists, halo ghosts and the game-of-life
+stencil over the iteration-cache neighbor lists."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import dccrg_amd as D  # noqa: E402
+from dccrg_amd import _capi as X  # noqa: E402
+from oracle import dccrg_oracle as O  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kats.json")))
+
+CASES = [  # length, max_ref_lvl, periodic, hood, refines, seed
+    ((3, 3, 1), 1, (False, False, False), 1, 0, 0),
+    ((4, 1, 1), 1, (True, False, False), 1, 0, 1),
+    ((3, 3, 1), 1, (True, True, False), 1, 10, 2),
+    ((4, 3, 2), 2, (False, False, False), 0, 20, 3),
+    ((2, 2, 2), 2, (True, True, True), 1, 25, 4),
+    ((5, 1, 1), 2, (True, False, True), 2, 20, 5),
+    ((3, 4, 3), 1, (True, False, False), 1, 30, 6),
+    ((4, 4, 1), 2, (False, True, False), 1, 30, 7),
+    ((3, 3, 3), 2, (True, True, True), 2, 15, 8),
+]
+
+
+def leaves_for(case):
+    length, M, per, hood, nref, seed = case
+    if nref == 0:
+        # the survey's fixed cases: 3x3x1 with cell 5 refined, 4x1x1 with cell 1 refined
+        m = O.Mapping(length, M)
+        c = 5 if length == (3, 3, 1) else 1
+        cells = set(range(1, int(np.prod(length)) + 1)) - {c}
+        return sorted(cells | set(m.get_all_children(c)))
+    return O.random_balanced_leaves(length, M, per, hood, nref, seed)
+
+
+def make(case, leaves, rank=0, size=1):
+    length, M, per, hood = case[:4]
+    c = D.Context(0, rank, size)
+    g = (D.Dccrg().set_initial_length(length).set_maximum_refinement_level(M).set_periodic(*per)
+         .set_neighborhood_length(hood).initialize(c, leaves=leaves))
+    g._keep = c
+    return g
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_explicit_neighbor_lists(case):
+    leaves = leaves_for(case)
+    length, M, per, hood = case[:4]
+    og = O.Grid(length, M, per, hood, leaves)
+    g = make(case, leaves)
+    cells = np.array(leaves, dtype=np.uint64)
+    row, ids, off = g.neighbors_of(cells)
+    for i, c in enumerate(leaves):
+        want = og.find_neighbors_of(c)
+        got = [(int(ids[k]), tuple(int(v) for v in off[k])) for k in range(int(row[i]), int(row[i + 1]))]
+        assert got == want, (c, got, want)
+    row, ids = g.neighbors_to(cells)
+    for i, c in enumerate(leaves):
+        assert [int(v) for v in ids[int(row[i]):int(row[i + 1])]] == og.find_neighbors_to(c), c
+
+
+@pytest.mark.parametrize("P", [2, 3, 5])
+@pytest.mark.parametrize("case", CASES[2:7])
+def test_explicit_rank_structures(case, P):
+    leaves = leaves_for(case)
+    length, M, per, hood = case[:4]
+    og = O.Grid(length, M, per, hood, leaves)
+    for r in range(P):
+        ref = og.rank_view(r, P)
+        g = make(case, leaves, r, P)
+        assert g.local_cells().tolist() == ref["local"]
+        assert g.outer_cells().tolist() == ref["outer"]
+        assert g.inner_cells().tolist() == ref["inner"]
+        assert g.remote_cells().tolist() == ref["remote"]
+        assert g.get_cells_to_send() == ref["send"]
+        assert g.get_cells_to_receive() == ref["recv"]
+
+
+def loopback(grids, fields):
+    msgs = {}
+    for r, g in enumerate(grids):
+        for p in g.get_cells_to_send():
+            buf = torch.empty(1 << 20, dtype=torch.uint8, device=DEV)
+            torch.cuda.synchronize()
+            msgs[(r, p)] = (buf, g.pack_to(p, buf.data_ptr(), buf.numel(), fields=fields))
+            g.ctx.synchronize()
+    for r, g in enumerate(grids):
+        for p in g.get_cells_to_receive():
+            buf, n = msgs[(p, r)]
+            g.unpack_from(p, buf.data_ptr(), n, fields=fields)
+        g.ctx.synchronize()
+
+
+@pytest.mark.parametrize("case", CASES[2:])
+def test_explicit_halo_ids(case):
+    """examples/basic_cell_data.cpp:27-53 on refined grids: ghosts == ids."""
+    leaves = leaves_for(case)
+    P = 3
+    grids = [make(case, leaves, r, P) for r in range(P)]
+    for g in grids:
+        g.add_field("id", np.uint64)
+        g.write_local("id", g.local_cells())
+    loopback(grids, ["id"])
+    for g in grids:
+        recv = set(c for v in g.get_cells_to_receive().values() for c in v)
+        for c, v in zip(g.remote_cells(), g.read_remote("id")):
+            if int(c) in recv:
+                assert int(v) == int(c)
+        assert np.array_equal(g.read_local("id"), g.local_cells())
+
+
+def gol_cache_reference(og, leaves, alive, steps):
+    """examples/game_of_life.cpp:54-79 over the iteration-cache neighbors_of
+    (unique (id, offset) pairs, dccrg.hpp:11570-11712)."""
+    pos = {c: i for i, c in enumerate(leaves)}
+    rows = []
+    for c in leaves:
+        lof, _ = O.iteration_cache_lists(og.find_neighbors_of(c), og.find_neighbors_to(c))
+        rows.append([pos[i] for i, _ in lof])
+    a = alive.copy()
+    cnt = np.zeros_like(a)
+    for _ in range(steps):
+        cnt = np.array([sum(1 for j in r if a[j]) for r in rows], dtype=np.uint32)
+        a = np.where(cnt == 3, 1, np.where(cnt == 2, a, 0)).astype(np.uint32)
+    return a, cnt
+
+
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("case", CASES[2:])
+def test_explicit_gol(case, P):
+    leaves = leaves_for(case)
+    length, M, per, hood = case[:4]
+    og = O.Grid(length, M, per, hood, leaves)
+    a0 = O.random_alive(np.array(leaves, dtype=np.uint64), 400)
+    steps = 4
+    ref_a, ref_n = gol_cache_reference(og, leaves, a0, steps)
+    grids = [make(case, leaves, r, P) for r in range(P)]
+    pos = {c: i for i, c in enumerate(leaves)}
+    for g in grids:
+        for f in ("a", "b", "n"):
+            g.add_field(f, np.uint32)
+        g.write_local("a", a0[[pos[int(c)] for c in g.local_cells()]])
+    cur, nxt = "a", "b"
+    for _ in range(steps):
+        if P == 1:
+            grids[0].gol_step(cur, nxt, "n")
+        else:
+            loopback(grids, [cur])
+            for g in grids:
+                g.gol_compute(cur, nxt, "n", X.REGION_INNER)
+                g.gol_compute(cur, nxt, "n", X.REGION_OUTER)
+        cur, nxt = nxt, cur
+    for g in grids:
+        idx = [pos[int(c)] for c in g.local_cells()]
+        assert np.array_equal(g.read_local(cur), ref_a[idx])
+        assert np.array_equal(g.read_local("n"), ref_n[idx])
+
+
+def test_explicit_user_neighborhood():
+    case = CASES[8]
+    leaves = leaves_for(case)
+    length, M, per, hood = case[:4]
+    og = O.Grid(length, M, per, hood, leaves)
+    g = make(case, leaves)
+    items = [[-2, 0, 1], [1, 1, 1], [0, -1, 0], [2, -2, 2]]
+    assert g.add_neighborhood(3, items)
+    cells = np.array(leaves, dtype=np.uint64)
+    row, ids, off = g.neighbors_of(cells, 3)
+    it = np.array(items, dtype=np.int32)
+    for i, c in enumerate(leaves):
+        want = og.find_neighbors_of(c, it)
+        got = [(int(ids[k]), tuple(int(v) for v in off[k])) for k in range(int(row[i]), int(row[i + 1]))]
+        assert got == want
+    assert not g.add_neighborhood(4, [[3, 0, 0]])
+
+
+def test_survey_facts_on_device():
+    for f in GOLD["survey_facts"]:
+        length, M = tuple(f["length"]), f["max_ref_lvl"]
+        m = O.Mapping(length, M)
+        cells = set(range(1, int(np.prod(length)) + 1))
+        for c in f["refine"]:
+            cells.discard(c)
+            cells |= set(m.get_all_children(c))
+        case = (length, M, tuple(bool(p) for p in f["periodic"]), f["hood_length"], 0, 0)
+        g = make(case, sorted(cells))
+        nof = g.get_neighbors_of(f["cell"])
+        if "offsets" in f:
+            assert [list(o) for i, o in nof if i == f["neighbor"]] == f["offsets"]
+        if "axis_sequence" in f:
+            assert [[i, o[0]] for i, o in nof if o[1] == 0 and o[2] == 0] == f["axis_sequence"]
