@@ -67,6 +67,14 @@ SIGNATURES = {
     "dccrgx_map_ids_to_indices": (C.c_int, [C.POINTER(Mapping_t), _vp, C.c_size_t, _vp, _vp, _vp]),
     "dccrgx_map_indices_to_ids": (C.c_int, [C.POINTER(Mapping_t), _vp, _vp, C.c_size_t, _vp, _vp]),
     "dccrgx_map_ids_op": (C.c_int, [C.POINTER(Mapping_t), C.c_int, _vp, C.c_size_t, _vp, _vp]),
+    "dccrgx_map_host_indices": (C.c_int, [C.POINTER(Mapping_t), C.c_uint64, _u64p, _i32p]),
+    "dccrgx_map_host_cell": (C.c_int, [C.POINTER(Mapping_t), _u64p, C.c_int32, _u64p]),
+    "dccrgx_map_host_op": (C.c_int, [C.POINTER(Mapping_t), C.c_int, C.c_uint64, _u64p]),
+    "dccrgx_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "dccrgx_neighbors_of_host": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _u64p, _u64p, _i32p, C.c_size_t]),
+    "dccrgx_neighbors_to_host": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _u64p, _u64p, C.c_size_t]),
+    "dccrgx_exchange_start": (C.c_int, [_vp, C.c_int32, C.POINTER(_vp), _u64p, C.POINTER(_vp), _u64p]),
+    "dccrgx_exchange_wait": (C.c_int, [_vp, C.c_int32]),
     "dccrgx_grid_create": (C.c_int, [_vp, C.POINTER(GridParams_t), _u64p, C.c_size_t, C.POINTER(_vp)]),
     "dccrgx_grid_destroy": (C.c_int, [_vp]),
     "dccrgx_grid_get_info": (C.c_int, [_vp, C.POINTER(GridInfo_t)]),

@@ -207,6 +207,50 @@ int dccrgx_map_ids_op(const dccrgx_mapping* map, int op, const uint64_t* ids, si
     return DCCRGX_OK;
 }
 
+int dccrgx_map_host_indices(const dccrgx_mapping* map, uint64_t cell, uint64_t idx3[3], int32_t* lvl)
+{
+    MapParams p;
+    DX_TRY(make_map_params(map, &p));
+    DX_CHECK(idx3, DCCRGX_EINVAL, "null output");
+    int l;
+    map_indices(p, cell, idx3, &l);
+    if (lvl) *lvl = l;
+    return DCCRGX_OK;
+}
+
+int dccrgx_map_host_cell(const dccrgx_mapping* map, const uint64_t idx3[3], int32_t lvl, uint64_t* cell)
+{
+    MapParams p;
+    DX_TRY(make_map_params(map, &p));
+    DX_CHECK(idx3 && cell, DCCRGX_EINVAL, "null argument");
+    *cell = map_cell(p, idx3, lvl);
+    return DCCRGX_OK;
+}
+
+int dccrgx_map_host_op(const dccrgx_mapping* map, int op, uint64_t c, uint64_t* out)
+{
+    MapParams p;
+    DX_TRY(make_map_params(map, &p));
+    DX_CHECK(out && op >= 0 && op <= DCCRGX_OP_CHILD, DCCRGX_EINVAL, "bad argument");
+    uint64_t idx[3];
+    int l;
+    const bool ok = map_indices(p, c, idx, &l);
+    switch (op) {
+    case DCCRGX_OP_LENGTH_IN_INDICES: *out = ok ? ((uint64_t)1 << (p.max_lvl - l)) : DCCRGX_ERROR_INDEX; break;
+    case DCCRGX_OP_PARENT: *out = !ok ? 0 : (l == 0 ? c : map_cell(p, idx, l - 1)); break;
+    case DCCRGX_OP_LEVEL_0_PARENT: *out = !ok ? 0 : (l == 0 ? c : map_cell(p, idx, 0)); break;
+    default: *out = !ok ? 0 : (l >= p.max_lvl ? c : map_cell(p, idx, l + 1)); break;
+    }
+    return DCCRGX_OK;
+}
+
+int dccrgx_device_count(int* n)
+{
+    DX_CHECK(n, DCCRGX_EINVAL, "null output");
+    DX_HIP(hipGetDeviceCount(n));
+    return DCCRGX_OK;
+}
+
 // ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------

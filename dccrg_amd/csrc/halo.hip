@@ -403,6 +403,64 @@ int dccrgx_halo_update(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, siz
     return dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL);
 }
 
+int dccrgx_exchange_start(dccrgx_grid* grid, int32_t hood_id, const void* const* send_host,
+                          const uint64_t* send_bytes, void* const* recv_host, const uint64_t* recv_bytes)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    DX_CHECK(!h->pending, DCCRGX_ESTATE, "transfer of neighborhood %d already started", hood_id);
+    Ctx* c = grid->ctx;
+    size_t si = 0, ri = 0;
+    bool any = false;
+    struct Msg { PeerPlan* p; size_t sb, rb; const void* sh; void* rh; };
+    std::vector<Msg> msgs;
+    for (PeerPlan& p : h->peers) {
+        Msg m{&p, 0, 0, nullptr, nullptr};
+        if (!p.send_ids.empty()) {
+            m.sb = send_bytes[si];
+            m.sh = send_host[si++];
+        }
+        if (!p.recv_ids.empty()) {
+            m.rb = recv_bytes[ri];
+            m.rh = recv_host[ri++];
+        }
+        any |= m.sb || m.rb;
+        msgs.push_back(m);
+    }
+    if (!any) return DCCRGX_OK;
+    DX_CHECK(c->has_comm, DCCRGX_ESTATE, "rank %d has remote neighbors but no RCCL communicator", c->rank);
+    for (Msg& m : msgs) {
+        if (m.sb) {
+            DX_TRY(ensure(&m.p->d_send_buf, &m.p->send_buf_bytes, m.sb));
+            DX_HIP(hipMemcpyAsync(m.p->d_send_buf, m.sh, m.sb, hipMemcpyHostToDevice, c->comm));
+        }
+        if (m.rb) DX_TRY(ensure(&m.p->d_recv_buf, &m.p->recv_buf_bytes, m.rb));
+    }
+    DX_RCCL(ncclGroupStart());
+    for (Msg& m : msgs) {
+        if (m.sb) DX_RCCL(ncclSend(m.p->d_send_buf, m.sb, ncclUint8, m.p->peer, c->nccl, c->comm));
+        if (m.rb) DX_RCCL(ncclRecv(m.p->d_recv_buf, m.rb, ncclUint8, m.p->peer, c->nccl, c->comm));
+    }
+    DX_RCCL(ncclGroupEnd());
+    for (Msg& m : msgs)
+        if (m.rb) DX_HIP(hipMemcpyAsync(m.rh, m.p->d_recv_buf, m.rb, hipMemcpyDeviceToHost, c->comm));
+    h->pending = true;
+    h->pending_fields.clear();
+    return DCCRGX_OK;
+}
+
+int dccrgx_exchange_wait(dccrgx_grid* grid, int32_t hood_id)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    if (!h->pending) return DCCRGX_OK;
+    DX_HIP(hipStreamSynchronize(grid->ctx->comm));
+    h->pending = false;
+    return DCCRGX_OK;
+}
+
 int dccrgx_halo_pack_to(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size_t nf, int32_t peer,
                         void* dst, size_t cap, size_t* bytes)
 {

@@ -174,4 +174,72 @@ int dccrgx_neighbors_to(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     return DCCRGX_OK;
 }
 
+int dccrgx_neighbors_of_host(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells, size_t n,
+                             uint64_t* row, uint64_t* ids, int32_t* off3, size_t cap)
+{
+    DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    hipStream_t st = grid->ctx->compute;
+    uint64_t *d_cells = nullptr, *d_row = nullptr, *d_ids = nullptr;
+    int32_t* d_off = nullptr;
+    DX_HIP(hipMalloc(&d_cells, std::max<size_t>(n, 1) * 8));
+    DX_HIP(hipMalloc(&d_row, (n + 1) * 8));
+    if (n) DX_HIP(hipMemcpyAsync(d_cells, cells, n * 8, hipMemcpyHostToDevice, st));
+    int s = dccrgx_neighbors_of(grid, hood_id, d_cells, n, d_row, nullptr, nullptr, 0, st);
+    if (s == DCCRGX_OK) {
+        DX_HIP(hipMemcpyAsync(row, d_row, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+        DX_HIP(hipStreamSynchronize(st));
+        const uint64_t total = row[n];
+        if (ids) {
+            if (cap < total) {
+                s = set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total);
+            } else {
+                DX_HIP(hipMalloc(&d_ids, std::max<uint64_t>(total, 1) * 8));
+                DX_HIP(hipMalloc(&d_off, std::max<uint64_t>(total, 1) * 12));
+                s = dccrgx_neighbors_of(grid, hood_id, d_cells, n, d_row, d_ids, d_off, total, st);
+                if (s == DCCRGX_OK && total) {
+                    DX_HIP(hipMemcpyAsync(ids, d_ids, total * 8, hipMemcpyDeviceToHost, st));
+                    if (off3) DX_HIP(hipMemcpyAsync(off3, d_off, total * 12, hipMemcpyDeviceToHost, st));
+                }
+            }
+        }
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_cells);
+    hipFree(d_row);
+    hipFree(d_ids);
+    hipFree(d_off);
+    return s;
+}
+
+int dccrgx_neighbors_to_host(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells, size_t n,
+                             uint64_t* row, uint64_t* ids, size_t cap)
+{
+    DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    hipStream_t st = grid->ctx->compute;
+    uint64_t *d_cells = nullptr, *d_row = nullptr, *d_ids = nullptr;
+    DX_HIP(hipMalloc(&d_cells, std::max<size_t>(n, 1) * 8));
+    DX_HIP(hipMalloc(&d_row, (n + 1) * 8));
+    if (n) DX_HIP(hipMemcpyAsync(d_cells, cells, n * 8, hipMemcpyHostToDevice, st));
+    int s = dccrgx_neighbors_to(grid, hood_id, d_cells, n, d_row, nullptr, 0, st);
+    if (s == DCCRGX_OK) {
+        DX_HIP(hipMemcpyAsync(row, d_row, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+        DX_HIP(hipStreamSynchronize(st));
+        const uint64_t total = row[n];
+        if (ids) {
+            if (cap < total) {
+                s = set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total);
+            } else {
+                DX_HIP(hipMalloc(&d_ids, std::max<uint64_t>(total, 1) * 8));
+                s = dccrgx_neighbors_to(grid, hood_id, d_cells, n, d_row, d_ids, total, st);
+                if (s == DCCRGX_OK && total) DX_HIP(hipMemcpyAsync(ids, d_ids, total * 8, hipMemcpyDeviceToHost, st));
+            }
+        }
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_cells);
+    hipFree(d_row);
+    hipFree(d_ids);
+    return s;
+}
+
 }  // extern "C"

@@ -1,0 +1,700 @@
+/*
+ * dccrg_amd.hpp -- C++ drop-in facade of dccrg::Dccrg / dccrg::Mapping for the
+ * hot path, implemented over the C-ABI of libdccrgx.so (include/dccrgx.h).
+ *
+ * Kept from the reference interface (dccrg.hpp:151-7186, dccrg_mapping.hpp):
+ * chained setters, initialize(MPI_Comm), local/inner/outer/remote/all_cells()
+ * with Cells_Item{id, data, neighbors_of, neighbors_to, all_neighbors} and
+ * Neighbors_Item{id, data, x, y, z}, operator[], get_neighbors_of/_to,
+ * add/remove_neighborhood, the per-peer send/receive lists and the halo
+ * calls (update_copies_of_remote_neighbors, start_/wait_...), and Mapping's
+ * id <-> index functions.  Cell data of arbitrary Cell_Data types stays on
+ * the host as in the reference (pointers from operator[] are stable); its
+ * halo bytes are produced with MPI_Pack from get_mpi_datatype() exactly as
+ * the reference's struct datatypes describe them and moved per peer with
+ * RCCL.  Neighbor lists, classification and send/receive lists are built on
+ * the GPU.  The device-speed path (SoA fields + device stencils) is the C-ABI
+ * itself (dccrgx_field_*, dccrgx_gol_*), reachable via device_grid().
+ *
+ * MPI is used for bootstrap only (rank, size, broadcasting the RCCL id).
+ * Load balancing (Zoltan) and refinement are not part of this path:
+ * balance_load() keeps the reference's non-Zoltan block partition.
+ */
+#ifndef DCCRG_AMD_HPP
+#define DCCRG_AMD_HPP
+
+#include <mpi.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdint>
+#include <map>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <type_traits>
+#include <unordered_map>
+#include <unordered_set>
+#include <utility>
+#include <vector>
+
+#include "dccrgx.h"
+
+namespace dccrg {
+
+static const uint64_t error_cell = DCCRGX_ERROR_CELL;    // dccrg_mapping.hpp:38
+static const uint64_t error_index = DCCRGX_ERROR_INDEX;  // dccrg_mapping.hpp:41
+static const int default_neighborhood_id = DCCRGX_DEFAULT_NEIGHBORHOOD_ID;  // dccrg.hpp:99
+
+template <unsigned N> struct Types;
+template <> struct Types<3> {  // dccrg_types.hpp:34-86
+    typedef std::array<uint64_t, 3> indices_t;
+    typedef std::array<int, 3> neighborhood_item_t;
+};
+
+namespace detail {
+
+inline void check(int status, const char* what)
+{
+    if (status != DCCRGX_OK) throw std::runtime_error(std::string(what) + ": " + dccrgx_last_error());
+}
+
+// MPI datatype of builtin cell data (dccrg_get_cell_datatype.hpp:226-281)
+template <class T> inline MPI_Datatype builtin_type();
+template <> inline MPI_Datatype builtin_type<char>() { return MPI_CHAR; }
+template <> inline MPI_Datatype builtin_type<signed char>() { return MPI_SIGNED_CHAR; }
+template <> inline MPI_Datatype builtin_type<unsigned char>() { return MPI_UNSIGNED_CHAR; }
+template <> inline MPI_Datatype builtin_type<short>() { return MPI_SHORT; }
+template <> inline MPI_Datatype builtin_type<unsigned short>() { return MPI_UNSIGNED_SHORT; }
+template <> inline MPI_Datatype builtin_type<int>() { return MPI_INT; }
+template <> inline MPI_Datatype builtin_type<unsigned>() { return MPI_UNSIGNED; }
+template <> inline MPI_Datatype builtin_type<long>() { return MPI_LONG; }
+template <> inline MPI_Datatype builtin_type<unsigned long>() { return MPI_UNSIGNED_LONG; }
+template <> inline MPI_Datatype builtin_type<long long>() { return MPI_LONG_LONG; }
+template <> inline MPI_Datatype builtin_type<unsigned long long>() { return MPI_UNSIGNED_LONG_LONG; }
+template <> inline MPI_Datatype builtin_type<float>() { return MPI_FLOAT; }
+template <> inline MPI_Datatype builtin_type<double>() { return MPI_DOUBLE; }
+template <> inline MPI_Datatype builtin_type<long double>() { return MPI_LONG_DOUBLE; }
+
+template <class C, class = void> struct has_gmd5 : std::false_type {};
+template <class C>
+struct has_gmd5<C, decltype(void(std::declval<C&>().get_mpi_datatype(uint64_t(), int(), int(), bool(), int())))>
+    : std::true_type {};
+template <class C, class = void> struct has_gmd0 : std::false_type {};
+template <class C>
+struct has_gmd0<C, decltype(void(std::declval<C&>().get_mpi_datatype()))> : std::true_type {};
+template <class T> struct is_std_array : std::false_type {};
+template <class T, size_t N> struct is_std_array<std::array<T, N>> : std::true_type {};
+
+// the (address, count, datatype) a cell puts on the wire, dccrg_get_cell_datatype.hpp:48-339
+template <class C>
+std::tuple<void*, int, MPI_Datatype> cell_datatype(C& c, uint64_t id, int sender, int receiver, bool receiving,
+                                                   int hood)
+{
+    if constexpr (has_gmd5<C>::value) {
+        return c.get_mpi_datatype(id, sender, receiver, receiving, hood);
+    } else if constexpr (has_gmd0<C>::value) {
+        (void)id, (void)sender, (void)receiver, (void)receiving, (void)hood;
+        return c.get_mpi_datatype();
+    } else if constexpr (std::is_arithmetic<C>::value) {
+        return std::make_tuple((void*)&c, 1, builtin_type<C>());
+    } else {
+        static_assert(is_std_array<C>::value, "Cell_Data needs get_mpi_datatype() or must be a builtin / std::array");
+        return std::make_tuple((void*)c.data(), (int)c.size(), builtin_type<typename C::value_type>());
+    }
+}
+
+// dccrg_mpi_support.hpp:66-95
+inline bool is_named(MPI_Datatype t)
+{
+    int ni = 0, na = 0, nd = 0, comb = 0;
+    MPI_Type_get_envelope(t, &ni, &na, &nd, &comb);
+    return comb == MPI_COMBINER_NAMED;
+}
+
+}  // namespace detail
+
+class Grid_Length {  // dccrg_length.hpp:34-142
+public:
+    typedef std::array<uint64_t, 3> type;
+    const type& get() const { return l_; }
+    type l_{{1, 1, 1}};
+};
+
+class Grid_Topology {  // dccrg_topology.hpp:38-217
+public:
+    bool is_periodic(size_t d) const { return d < 3 && p_[d]; }
+    bool set_periodicity(size_t d, bool v)
+    {
+        if (d > 2) return false;
+        p_[d] = v;
+        return true;
+    }
+    std::array<bool, 3> p_{{false, false, false}};
+};
+
+// dccrg_mapping.hpp:55-690 (host-side scalar calls of libdccrgx)
+class Mapping {
+public:
+    Grid_Length length;
+
+    bool set_length(const Grid_Length::type& l)
+    {
+        if (!l[0] || !l[1] || !l[2]) return false;
+        length.l_ = l;
+        return true;
+    }
+    bool set_maximum_refinement_level(int lvl)
+    {
+        int maxp = 0;
+        detail::check(dccrgx_max_possible_refinement_level(length.l_.data(), &maxp), "max level");
+        if (lvl > maxp) return false;
+        max_lvl_ = lvl < 0 ? maxp : lvl;
+        return true;
+    }
+    const int& get_maximum_refinement_level() const { return max_lvl_; }
+    int get_maximum_possible_refinement_level() const
+    {
+        int maxp = 0;
+        detail::check(dccrgx_max_possible_refinement_level(length.l_.data(), &maxp), "max level");
+        return maxp;
+    }
+    uint64_t get_last_cell() const
+    {
+        uint64_t v = 0;
+        const dccrgx_mapping m = raw();
+        detail::check(dccrgx_last_cell(&m, &v), "last cell");
+        return v;
+    }
+    uint64_t get_cell_from_indices(const Types<3>::indices_t& idx, int lvl) const
+    {
+        uint64_t v = 0;
+        const dccrgx_mapping m = raw();
+        detail::check(dccrgx_map_host_cell(&m, idx.data(), lvl, &v), "get_cell_from_indices");
+        return v;
+    }
+    Types<3>::indices_t get_indices(uint64_t cell) const
+    {
+        Types<3>::indices_t out;
+        const dccrgx_mapping m = raw();
+        detail::check(dccrgx_map_host_indices(&m, cell, out.data(), nullptr), "get_indices");
+        return out;
+    }
+    int get_refinement_level(uint64_t cell) const
+    {
+        Types<3>::indices_t out;
+        int32_t l = -1;
+        const dccrgx_mapping m = raw();
+        detail::check(dccrgx_map_host_indices(&m, cell, out.data(), &l), "get_refinement_level");
+        return l;
+    }
+    uint64_t get_cell_length_in_indices(uint64_t c) const { return op(DCCRGX_OP_LENGTH_IN_INDICES, c); }
+    uint64_t get_parent(uint64_t c) const { return op(DCCRGX_OP_PARENT, c); }
+    uint64_t get_level_0_parent(uint64_t c) const { return op(DCCRGX_OP_LEVEL_0_PARENT, c); }
+    uint64_t get_child(uint64_t c) const { return op(DCCRGX_OP_CHILD, c); }
+    // dccrg_mapping.hpp:392-442, x fastest then y then z
+    std::array<uint64_t, 8> get_all_children(uint64_t cell) const
+    {
+        std::array<uint64_t, 8> ch;
+        ch.fill(error_cell);
+        const int l = get_refinement_level(cell);
+        if (cell == error_cell || l < 0 || l >= max_lvl_) return ch;
+        const auto idx = get_indices(cell);
+        const uint64_t off = uint64_t(1) << (max_lvl_ - l - 1);
+        size_t i = 0;
+        for (uint64_t z = 0; z < 2 * off; z += off)
+            for (uint64_t y = 0; y < 2 * off; y += off)
+                for (uint64_t x = 0; x < 2 * off; x += off)
+                    ch[i++] = get_cell_from_indices({{idx[0] + x, idx[1] + y, idx[2] + z}}, l + 1);
+        return ch;
+    }
+    std::array<uint64_t, 8> get_siblings(uint64_t cell) const  // dccrg_mapping.hpp:450-471
+    {
+        std::array<uint64_t, 8> s;
+        s.fill(error_cell);
+        const int l = get_refinement_level(cell);
+        if (l < 0) return s;
+        if (l == 0) {
+            s[0] = cell;
+            return s;
+        }
+        return get_all_children(get_parent(cell));
+    }
+    dccrgx_mapping raw() const
+    {
+        dccrgx_mapping m{};
+        for (int d = 0; d < 3; d++) m.length[d] = length.l_[d];
+        m.max_ref_lvl = max_lvl_;
+        return m;
+    }
+
+private:
+    uint64_t op(int o, uint64_t c) const
+    {
+        uint64_t v = 0;
+        const dccrgx_mapping m = raw();
+        detail::check(dccrgx_map_host_op(&m, o, c, &v), "mapping");
+        return v;
+    }
+    int max_lvl_ = 0;
+};
+
+struct No_Geometry {  // dccrg_no_geometry.hpp (nothing on the hot path)
+    struct Parameters {};
+    bool set(const Parameters&) { return true; }
+};
+
+template <class Cell_Data, class Geometry = No_Geometry>
+class Dccrg {
+public:
+    typedef std::vector<std::pair<uint64_t, std::array<int, 3>>> neighbor_list_t;
+
+    // dccrg.hpp:7394-7401
+    template <class T> struct Iterator_Storage {
+        typename std::vector<T>::const_iterator begin_, end_;
+        typename std::vector<T>::const_iterator begin() const { return begin_; }
+        typename std::vector<T>::const_iterator cbegin() const { return begin_; }
+        typename std::vector<T>::const_iterator end() const { return end_; }
+        typename std::vector<T>::const_iterator cend() const { return end_; }
+    };
+    struct Neighbors_Item {  // dccrg.hpp:7404-7456
+        uint64_t id;
+        Cell_Data* data;
+        int x, y, z;
+    };
+    struct Cells_Item {  // dccrg.hpp:7480-7518
+        uint64_t id = error_cell;
+        Cell_Data* data = nullptr;
+        Iterator_Storage<Neighbors_Item> neighbors_of, neighbors_to, all_neighbors;
+    };
+
+    Mapping mapping;
+    Grid_Topology topology;
+    Geometry geometry;
+
+    Dccrg() = default;
+    Dccrg(const Dccrg&) = delete;
+    ~Dccrg()
+    {
+        if (grid_) dccrgx_grid_destroy(grid_);
+        if (ctx_) dccrgx_ctx_destroy(ctx_);
+        if (comm_ != MPI_COMM_NULL) {
+            int fin = 0;
+            MPI_Finalized(&fin);
+            if (!fin) MPI_Comm_free(&comm_);
+        }
+    }
+
+    // ---- configuration (dccrg.hpp:8242-8361) ------------------------------
+    Dccrg& set_initial_length(const std::array<uint64_t, 3>& l)
+    {
+        if (initialized_) throw std::invalid_argument("set_initial_length after initialize");
+        if (!mapping.set_length(l)) throw std::invalid_argument("all lengths must be > 0");
+        return *this;
+    }
+    Dccrg& set_maximum_refinement_level(int lvl)
+    {
+        if (initialized_) throw std::invalid_argument("set_maximum_refinement_level after initialize");
+        if (!mapping.set_maximum_refinement_level(lvl)) throw std::invalid_argument("refinement level too large");
+        return *this;
+    }
+    Dccrg& set_periodic(bool x, bool y, bool z)
+    {
+        if (initialized_) throw std::invalid_argument("set_periodic after initialize");
+        topology.set_periodicity(0, x);
+        topology.set_periodicity(1, y);
+        topology.set_periodicity(2, z);
+        return *this;
+    }
+    Dccrg& set_neighborhood_length(unsigned n)
+    {
+        if (initialized_) throw std::invalid_argument("set_neighborhood_length after initialize");
+        hood_length_ = n;
+        return *this;
+    }
+    Dccrg& set_load_balancing_method(const std::string&) { return *this; }
+    bool set_geometry(const typename Geometry::Parameters& p) { return geometry.set(p); }
+    Dccrg& balance_load(bool = true) { return *this; }  // block partition kept (dccrg.hpp:1048-1062)
+
+    // dccrg.hpp:485-562
+    Dccrg& initialize(const MPI_Comm& comm, uint64_t = 1)
+    {
+        if (initialized_) throw std::invalid_argument("already initialized");
+        MPI_Comm_dup(comm, &comm_);
+        MPI_Comm_rank(comm_, &rank_);
+        MPI_Comm_size(comm_, &size_);
+        MPI_Comm node;
+        MPI_Comm_split_type(comm_, MPI_COMM_TYPE_SHARED, rank_, MPI_INFO_NULL, &node);
+        int node_rank = 0, ndev = 0;
+        MPI_Comm_rank(node, &node_rank);
+        MPI_Comm_free(&node);
+        detail::check(dccrgx_device_count(&ndev), "device count");
+        if (ndev < 1) throw std::runtime_error("no GPU");
+        detail::check(dccrgx_ctx_create(node_rank % ndev, rank_, size_, &ctx_), "context");
+        if (size_ > 1) {
+            uint8_t uid[128] = {0};
+            if (rank_ == 0) detail::check(dccrgx_get_unique_id(uid), "unique id");
+            MPI_Bcast(uid, 128, MPI_BYTE, 0, comm_);
+            detail::check(dccrgx_ctx_comm_init(ctx_, uid), "RCCL communicator");
+        }
+        dccrgx_grid_params p{};
+        for (int d = 0; d < 3; d++) {
+            p.length[d] = mapping.length.get()[d];
+            p.periodic[d] = topology.is_periodic(d) ? 1 : 0;
+        }
+        p.max_ref_lvl = mapping.get_maximum_refinement_level();
+        p.neighborhood_length = hood_length_;
+        detail::check(dccrgx_grid_create(ctx_, &p, nullptr, 0, &grid_), "grid");
+        for (uint64_t c : query_cells(default_neighborhood_id, DCCRGX_CELLS_LOCAL)) cell_data_[c];
+        initialized_ = true;
+        build_hood(default_neighborhood_id);
+        return *this;
+    }
+
+    // ---- queries ------------------------------------------------------------
+    int get_rank() const { return rank_; }
+    int get_comm_size() const { return size_; }
+    MPI_Comm get_communicator() const { return comm_; }
+    int get_maximum_refinement_level() const { return mapping.get_maximum_refinement_level(); }
+    unsigned get_neighborhood_length() const { return hood_length_; }
+    const Grid_Length& length() const { return mapping.length; }
+
+    // dccrg.hpp:768-781: local cells, then copies of remote neighbors
+    Cell_Data* operator[](uint64_t cell) const
+    {
+        auto it = cell_data_.find(cell);
+        if (it != cell_data_.end()) return const_cast<Cell_Data*>(&it->second);
+        auto jt = remote_data_.find(cell);
+        if (jt != remote_data_.end()) return const_cast<Cell_Data*>(&jt->second);
+        return nullptr;
+    }
+    bool is_local(uint64_t cell) const { return cell_data_.count(cell) > 0; }
+
+    std::vector<uint64_t> get_cells() const  // local cells, ascending
+    {
+        return query_cells(default_neighborhood_id, DCCRGX_CELLS_LOCAL);
+    }
+
+    const Iterator_Storage<Cells_Item>& local_cells(int hood = default_neighborhood_id) const { return hs(hood).local; }
+    const Iterator_Storage<Cells_Item>& inner_cells(int hood = default_neighborhood_id) const { return hs(hood).inner; }
+    const Iterator_Storage<Cells_Item>& outer_cells(int hood = default_neighborhood_id) const { return hs(hood).outer; }
+    const Iterator_Storage<Cells_Item>& remote_cells(int hood = default_neighborhood_id) const { return hs(hood).remote; }
+    const Iterator_Storage<Cells_Item>& all_cells(int hood = default_neighborhood_id) const { return hs(hood).all; }
+
+    // dccrg.hpp:836-883 / 900-943
+    const neighbor_list_t* get_neighbors_of(uint64_t cell, int hood = default_neighborhood_id) const
+    {
+        auto h = hoods_.find(hood);
+        if (h == hoods_.end()) return nullptr;
+        auto it = h->second.nof.find(cell);
+        return it == h->second.nof.end() ? nullptr : &it->second;
+    }
+    const neighbor_list_t* get_neighbors_to(uint64_t cell, int hood = default_neighborhood_id) const
+    {
+        auto h = hoods_.find(hood);
+        if (h == hoods_.end()) return nullptr;
+        auto it = h->second.nto.find(cell);
+        return it == h->second.nto.end() ? nullptr : &it->second;
+    }
+
+    // dccrg.hpp:7008-7046: per process, ascending ids with tags 1..N
+    const std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>& get_cells_to_send() const
+    {
+        return hs(default_neighborhood_id).send_tagged;
+    }
+    const std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>& get_cells_to_receive() const
+    {
+        return hs(default_neighborhood_id).recv_tagged;
+    }
+    uint64_t get_number_of_update_send_cells(int hood = default_neighborhood_id) const
+    {
+        uint64_t n = 0;
+        for (auto& kv : hs(hood).send) n += kv.second.size();
+        return n;
+    }
+    uint64_t get_number_of_update_receive_cells(int hood = default_neighborhood_id) const
+    {
+        uint64_t n = 0;
+        for (auto& kv : hs(hood).recv) n += kv.second.size();
+        return n;
+    }
+    std::unordered_set<uint64_t> get_remote_cells_on_process_boundary(int hood = default_neighborhood_id) const
+    {
+        const auto& r = hs(hood).remote_ids;
+        return std::unordered_set<uint64_t>(r.begin(), r.end());
+    }
+
+    // dccrg.hpp:6491-6711
+    bool add_neighborhood(int id, const std::vector<Types<3>::neighborhood_item_t>& items)
+    {
+        std::vector<int32_t> flat;
+        for (const auto& it : items) flat.insert(flat.end(), it.begin(), it.end());
+        const int s = dccrgx_add_neighborhood(grid_, id, flat.data(), items.size());
+        if (s == DCCRGX_EINVAL) return false;
+        detail::check(s, "add_neighborhood");
+        build_hood(id);
+        return true;
+    }
+    Dccrg& remove_neighborhood(int id)
+    {
+        if (id == default_neighborhood_id) return *this;
+        detail::check(dccrgx_remove_neighborhood(grid_, id), "remove_neighborhood");
+        hoods_.erase(id);
+        return *this;
+    }
+
+    // ---- halo ---------------------------------------------------------------
+    // dccrg.hpp:978-1014 (returns false for the default id like the reference,
+    // dccrg.hpp:1001-1003, but still transfers)
+    bool update_copies_of_remote_neighbors(int hood = default_neighborhood_id)
+    {
+        if (!start_remote_neighbor_copy_updates(hood)) return false;
+        wait_remote_neighbor_copy_updates(hood);
+        return hood != default_neighborhood_id;
+    }
+    bool start_remote_neighbor_copy_updates(int hood = default_neighborhood_id)  // :5046-5078
+    {
+        auto h = hoods_.find(hood);
+        if (h == hoods_.end()) return false;
+        HoodState& S = h->second;
+        S.sbuf.clear();
+        S.rbuf.clear();
+        std::vector<const void*> sp;
+        std::vector<void*> rp;
+        std::vector<uint64_t> sb, rb;
+        for (auto& kv : S.send) {
+            std::vector<char> buf;
+            for (uint64_t c : kv.second) pack(c, *(*this)[c], rank_, kv.first, false, hood, buf);
+            S.sbuf.push_back(std::move(buf));
+        }
+        for (auto& kv : S.recv) {
+            int total = 0;
+            for (uint64_t c : kv.second) total += pack_size(c, *(*this)[c], kv.first, rank_, true, hood);
+            S.rbuf.emplace_back((size_t)total);
+        }
+        for (auto& b : S.sbuf) {
+            sp.push_back(b.data());
+            sb.push_back(b.size());
+        }
+        for (auto& b : S.rbuf) {
+            rp.push_back(b.data());
+            rb.push_back(b.size());
+        }
+        detail::check(dccrgx_exchange_start(grid_, hood, sp.data(), sb.data(), rp.data(), rb.data()),
+                      "start_remote_neighbor_copy_updates");
+        S.pending = true;
+        return true;
+    }
+    bool start_remote_neighbor_copy_receives(int hood = default_neighborhood_id)
+    {
+        return start_remote_neighbor_copy_updates(hood);
+    }
+    bool start_remote_neighbor_copy_sends(int hood = default_neighborhood_id) { return hoods_.count(hood) > 0; }
+    bool wait_remote_neighbor_copy_updates(int hood = default_neighborhood_id)  // :5307-5338
+    {
+        auto h = hoods_.find(hood);
+        if (h == hoods_.end()) return false;
+        HoodState& S = h->second;
+        if (!S.pending) return true;
+        detail::check(dccrgx_exchange_wait(grid_, hood), "wait_remote_neighbor_copy_updates");
+        size_t i = 0;
+        for (auto& kv : S.recv) {
+            int pos = 0;
+            for (uint64_t c : kv.second) unpack(c, *(*this)[c], kv.first, rank_, hood, S.rbuf[i], pos);
+            i++;
+        }
+        S.pending = false;
+        return true;
+    }
+    bool wait_remote_neighbor_copy_update_receives(int hood = default_neighborhood_id)
+    {
+        return wait_remote_neighbor_copy_updates(hood);
+    }
+    bool wait_remote_neighbor_copy_update_sends(int hood = default_neighborhood_id)
+    {
+        return wait_remote_neighbor_copy_updates(hood);
+    }
+
+    // device fast path
+    dccrgx_grid* device_grid() const { return grid_; }
+    dccrgx_ctx* device_context() const { return ctx_; }
+
+private:
+    struct HoodState {
+        std::vector<Cells_Item> cells;
+        std::vector<Neighbors_Item> neighbors;
+        Iterator_Storage<Cells_Item> inner, outer, local, remote, all;
+        std::unordered_map<uint64_t, neighbor_list_t> nof, nto;
+        std::map<int, std::vector<uint64_t>> send, recv;
+        std::unordered_map<int, std::vector<std::pair<uint64_t, int>>> send_tagged, recv_tagged;
+        std::vector<uint64_t> remote_ids;
+        std::vector<std::vector<char>> sbuf, rbuf;
+        bool pending = false;
+    };
+
+    const HoodState& hs(int hood) const
+    {
+        auto it = hoods_.find(hood);
+        if (it == hoods_.end()) throw std::invalid_argument("unknown neighborhood id " + std::to_string(hood));
+        return it->second;
+    }
+
+    std::vector<uint64_t> query_cells(int hood, int which) const
+    {
+        size_t n = 0;
+        int s = dccrgx_get_cells(grid_, hood, which, nullptr, 0, &n);
+        if (s != DCCRGX_OK && s != DCCRGX_ERANGE) detail::check(s, "get_cells");
+        std::vector<uint64_t> v(n);
+        detail::check(dccrgx_get_cells(grid_, hood, which, v.data(), n, &n), "get_cells");
+        return v;
+    }
+
+    std::map<int, std::vector<uint64_t>> peer_lists(int hood, int send) const
+    {
+        size_t n = 0;
+        int s = dccrgx_get_peers(grid_, hood, send, nullptr, nullptr, 0, &n);
+        if (s != DCCRGX_OK && s != DCCRGX_ERANGE) detail::check(s, "get_peers");
+        std::vector<int32_t> peers(n);
+        std::vector<uint64_t> counts(n);
+        detail::check(dccrgx_get_peers(grid_, hood, send, peers.data(), counts.data(), n, &n), "get_peers");
+        std::map<int, std::vector<uint64_t>> out;
+        for (size_t i = 0; i < n; i++) {
+            std::vector<uint64_t> ids(counts[i]);
+            size_t m = 0;
+            detail::check(dccrgx_get_peer_cells(grid_, hood, send, peers[i], ids.data(), ids.size(), &m),
+                          "get_peer_cells");
+            out[peers[i]] = std::move(ids);
+        }
+        return out;
+    }
+
+    // the iteration cache, dccrg.hpp:11453-11767: inner, outer, remote cells;
+    // neighbors per cell as std::set-ordered [only_of][both][only_to]
+    void build_hood(int hood)
+    {
+        HoodState S;
+        const auto inner = query_cells(hood, DCCRGX_CELLS_INNER);
+        const auto outer = query_cells(hood, DCCRGX_CELLS_OUTER);
+        S.remote_ids = query_cells(hood, DCCRGX_CELLS_REMOTE);
+        for (uint64_t c : S.remote_ids) remote_data_.emplace(c, Cell_Data{});  // :7153-7184
+        std::vector<uint64_t> order;
+        order.insert(order.end(), inner.begin(), inner.end());
+        order.insert(order.end(), outer.begin(), outer.end());
+        order.insert(order.end(), S.remote_ids.begin(), S.remote_ids.end());
+        const size_t n = order.size();
+        std::vector<uint64_t> row(n + 1), trow(n + 1);
+        detail::check(dccrgx_neighbors_of_host(grid_, hood, order.data(), n, row.data(), nullptr, nullptr, 0),
+                      "neighbors_of");
+        std::vector<uint64_t> ids(row[n]);
+        std::vector<int32_t> off(3 * row[n]);
+        detail::check(dccrgx_neighbors_of_host(grid_, hood, order.data(), n, row.data(), ids.data(), off.data(),
+                                               ids.size()),
+                      "neighbors_of");
+        detail::check(dccrgx_neighbors_to_host(grid_, hood, order.data(), n, trow.data(), nullptr, 0),
+                      "neighbors_to");
+        std::vector<uint64_t> tids(trow[n]);
+        detail::check(dccrgx_neighbors_to_host(grid_, hood, order.data(), n, trow.data(), tids.data(), tids.size()),
+                      "neighbors_to");
+        typedef std::pair<uint64_t, std::array<int, 3>> item;
+        std::vector<std::array<size_t, 4>> ranges(n);
+        for (size_t i = 0; i < n; i++) {
+            neighbor_list_t nof, nto;
+            for (uint64_t k = row[i]; k < row[i + 1]; k++)
+                nof.push_back({ids[k], {{off[3 * k], off[3 * k + 1], off[3 * k + 2]}}});
+            for (uint64_t k = trow[i]; k < trow[i + 1]; k++) nto.push_back({tids[k], {{0, 0, 0}}});
+            std::set<item> ids_of(nof.begin(), nof.end()), ids_to(nto.begin(), nto.end());
+            std::set<item> only_of, both, only_to = ids_to;
+            for (const item& x : ids_of) {
+                item t{x.first, {{0, 0, 0}}};
+                only_to.erase(t);
+                if (ids_to.count(t)) both.insert(x);
+                else only_of.insert(x);
+            }
+            ranges[i][0] = S.neighbors.size();
+            for (const auto* group : {&only_of, &both, &only_to})
+                for (const item& x : *group)
+                    S.neighbors.push_back(Neighbors_Item{x.first, (*this)[x.first], x.second[0], x.second[1],
+                                                         x.second[2]});
+            ranges[i][1] = ranges[i][0] + only_of.size();
+            ranges[i][2] = ranges[i][1] + both.size();
+            ranges[i][3] = ranges[i][2] + only_to.size();
+            S.nof[order[i]] = std::move(nof);
+            S.nto[order[i]] = std::move(nto);
+            Cells_Item ci;
+            ci.id = order[i];
+            ci.data = (*this)[order[i]];
+            S.cells.push_back(ci);
+        }
+        auto b = S.neighbors.cbegin();
+        for (size_t i = 0; i < n; i++) {
+            S.cells[i].neighbors_of = {b + ranges[i][0], b + ranges[i][2]};
+            S.cells[i].neighbors_to = {b + ranges[i][1], b + ranges[i][3]};
+            S.cells[i].all_neighbors = {b + ranges[i][0], b + ranges[i][3]};
+        }
+        auto cb = S.cells.cbegin();
+        const size_t ni = inner.size(), no = outer.size();
+        S.inner = {cb, cb + ni};
+        S.outer = {cb + ni, cb + ni + no};
+        S.local = {cb, cb + ni + no};
+        S.remote = {cb + ni + no, S.cells.cend()};
+        S.all = {cb, S.cells.cend()};
+        S.send = peer_lists(hood, 1);
+        S.recv = peer_lists(hood, 0);
+        for (auto pr : {std::make_pair(&S.send, &S.send_tagged), std::make_pair(&S.recv, &S.recv_tagged)}) {
+            for (auto& kv : *pr.first) {
+                auto& v = (*pr.second)[kv.first];
+                for (size_t i = 0; i < kv.second.size(); i++) v.push_back({kv.second[i], (int)i + 1});
+            }
+        }
+        hoods_[hood] = std::move(S);
+    }
+
+    int pack_size(uint64_t id, Cell_Data& c, int sender, int receiver, bool receiving, int hood)
+    {
+        auto d = detail::cell_datatype(c, id, sender, receiver, receiving, hood);
+        MPI_Datatype t = std::get<2>(d);
+        const bool named = detail::is_named(t);
+        if (!named) MPI_Type_commit(&t);
+        int sz = 0;
+        MPI_Pack_size(std::get<1>(d), t, comm_, &sz);
+        if (!named) MPI_Type_free(&t);
+        return sz;
+    }
+    void pack(uint64_t id, Cell_Data& c, int sender, int receiver, bool receiving, int hood, std::vector<char>& buf)
+    {
+        auto d = detail::cell_datatype(c, id, sender, receiver, receiving, hood);
+        MPI_Datatype t = std::get<2>(d);
+        const bool named = detail::is_named(t);
+        if (!named) MPI_Type_commit(&t);
+        int sz = 0;
+        MPI_Pack_size(std::get<1>(d), t, comm_, &sz);
+        int pos = (int)buf.size();
+        buf.resize(buf.size() + sz);
+        MPI_Pack(std::get<0>(d), std::get<1>(d), t, buf.data(), (int)buf.size(), &pos, comm_);
+        buf.resize(pos);
+        if (!named) MPI_Type_free(&t);
+    }
+    void unpack(uint64_t id, Cell_Data& c, int sender, int receiver, int hood, std::vector<char>& buf, int& pos)
+    {
+        auto d = detail::cell_datatype(c, id, sender, receiver, true, hood);
+        MPI_Datatype t = std::get<2>(d);
+        const bool named = detail::is_named(t);
+        if (!named) MPI_Type_commit(&t);
+        MPI_Unpack(buf.data(), (int)buf.size(), &pos, std::get<0>(d), std::get<1>(d), t, comm_);
+        if (!named) MPI_Type_free(&t);
+    }
+
+    std::unordered_map<uint64_t, Cell_Data> cell_data_, remote_data_;
+    std::map<int, HoodState> hoods_;
+    dccrgx_ctx* ctx_ = nullptr;
+    dccrgx_grid* grid_ = nullptr;
+    MPI_Comm comm_ = MPI_COMM_NULL;
+    int rank_ = 0, size_ = 1;
+    unsigned hood_length_ = 1;
+    bool initialized_ = false;
+};
+
+}  // namespace dccrg
+
+#endif  // DCCRG_AMD_HPP

@@ -99,6 +99,15 @@ enum { DCCRGX_OP_LENGTH_IN_INDICES = 0, DCCRGX_OP_PARENT = 1, DCCRGX_OP_LEVEL_0_
 int dccrgx_map_ids_op(const dccrgx_mapping* map, int op, const uint64_t* ids_dev, size_t n,
                       uint64_t* out_dev, void* stream);
 
+/* Scalar host-side forms of the same functions (no device involved), for
+ * host code that calls Mapping per cell (tests/game_of_life/solve.hpp:48-51) */
+int dccrgx_map_host_indices(const dccrgx_mapping* map, uint64_t cell, uint64_t idx3_out[3],
+                            int32_t* lvl_out);
+int dccrgx_map_host_cell(const dccrgx_mapping* map, const uint64_t idx3[3], int32_t lvl,
+                         uint64_t* cell_out);
+int dccrgx_map_host_op(const dccrgx_mapping* map, int op, uint64_t cell, uint64_t* out);
+int dccrgx_device_count(int* n_out);
+
 /* ------------------------------------------------------------------------ *
  * Grid: one dccrg grid on this rank.  Replaces Dccrg::initialize
  * (dccrg.hpp:485-562): level-0 creation + block partition (:8089-8145),
@@ -159,6 +168,12 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
 int dccrgx_neighbors_to(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells_dev,
                         size_t n, uint64_t* row_ptr_dev, uint64_t* ids_dev, size_t cap,
                         void* stream);
+/* host-pointer forms of the two batched queries (same results) */
+int dccrgx_neighbors_of_host(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells_host,
+                             size_t n, uint64_t* row_host, uint64_t* ids_host, int32_t* off3_host,
+                             size_t cap);
+int dccrgx_neighbors_to_host(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells_host,
+                             size_t n, uint64_t* row_host, uint64_t* ids_host, size_t cap);
 /* per-peer ascending send / receive lists (dccrg.hpp:7008-7046, :8729-8891) */
 int dccrgx_get_peers(const dccrgx_grid* grid, int32_t hood_id, int32_t send, int32_t* peers_host,
                      uint64_t* counts_host, size_t cap, size_t* n_peers);
@@ -205,6 +220,16 @@ int dccrgx_halo_pack_to(dccrgx_grid* grid, int32_t hood_id, const int32_t* field
                         size_t* bytes_out);
 int dccrgx_halo_unpack_from(dccrgx_grid* grid, int32_t hood_id, const int32_t* field_ids,
                             size_t n_fields, int32_t peer, const void* src_dev, size_t bytes);
+/* Byte transport for host-resident cell data (the C++ facade's drop-in path
+ * for arbitrary Cell_Data / MPI datatypes, dccrg.hpp:10726-11209): one
+ * message per peer, the peers in dccrgx_get_peers order (send=1 for
+ * send_host / send_bytes, send=0 for recv_host / recv_bytes), moved with
+ * grouped RCCL send/recv through device staging on the communication
+ * stream.  Host buffers must stay valid until dccrgx_exchange_wait. */
+int dccrgx_exchange_start(dccrgx_grid* grid, int32_t hood_id, const void* const* send_host,
+                          const uint64_t* send_bytes, void* const* recv_host,
+                          const uint64_t* recv_bytes);
+int dccrgx_exchange_wait(dccrgx_grid* grid, int32_t hood_id);
 /* periodic self-copies into the ghost/pad slots (part of halo_start) */
 int dccrgx_halo_self(dccrgx_grid* grid, int32_t hood_id, const int32_t* field_ids,
                      size_t n_fields);

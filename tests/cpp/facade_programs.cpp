@@ -1,0 +1,177 @@
+// User programs written against the dccrg interface (include/dccrg_amd.hpp),
+// the way the reference's examples and tests use it.  Modes:
+//   blinker          examples/simple_game_of_life.cpp semantics (aborts on error)
+//   scal3d LX LY LZ STEPS PX PY PZ
+//                    tests/game_of_life/scalability3d.cpp loop (start, inner,
+//                    wait, outer, rule); prints "alive <id>" lines
+//   halo             examples/basic_cell_data.cpp (Dccrg<int>, ghosts == ids)
+//   mapping          prints Mapping results for a list of ids
+//   lists            prints the iteration-cache neighbor lists of every cell
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "dccrg_amd.hpp"
+
+struct game_of_life_cell {
+    unsigned int is_alive = 0, live_neighbor_count = 0;
+    std::tuple<void*, int, MPI_Datatype> get_mpi_datatype()
+    {
+        return std::make_tuple((void*)&(this->is_alive), 1, MPI_UNSIGNED);
+    }
+};
+
+static uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static int blinker()
+{
+    dccrg::Dccrg<game_of_life_cell> grid;
+    grid.set_initial_length({10, 10, 1})
+        .set_maximum_refinement_level(0)
+        .set_neighborhood_length(1)
+        .set_load_balancing_method("RCB")
+        .initialize(MPI_COMM_WORLD);
+    grid.balance_load();
+    for (const auto& cell : grid.local_cells()) {
+        cell.data->live_neighbor_count = 0;
+        cell.data->is_alive = (cell.id == 54 || cell.id == 55 || cell.id == 56) ? 1 : 0;
+    }
+    for (int turn = 0; turn < 100; turn++) {
+        grid.update_copies_of_remote_neighbors();
+        for (const auto& cell : grid.local_cells()) {
+            cell.data->live_neighbor_count = 0;
+            for (const auto& neighbor : cell.neighbors_of)
+                if (neighbor.data->is_alive > 0) cell.data->live_neighbor_count++;
+        }
+        for (const auto& cell : grid.local_cells()) {
+            if (cell.data->live_neighbor_count == 3) cell.data->is_alive = 1;
+            else if (cell.data->live_neighbor_count != 2) cell.data->is_alive = 0;
+        }
+        for (const auto& cell : grid.local_cells()) {
+            const bool even = turn % 2 == 0;
+            if (cell.id == 55 && !cell.data->is_alive) abort();
+            if ((cell.id == 54 || cell.id == 56) && (cell.data->is_alive != (even ? 0u : 1u))) abort();
+            if ((cell.id == 45 || cell.id == 65) && (cell.data->is_alive != (even ? 1u : 0u))) abort();
+        }
+    }
+    printf("PASS blinker\n");
+    return 0;
+}
+
+static int scal3d(int argc, char** argv)
+{
+    const uint64_t L[3] = {strtoull(argv[2], 0, 10), strtoull(argv[3], 0, 10), strtoull(argv[4], 0, 10)};
+    const int steps = atoi(argv[5]);
+    dccrg::Dccrg<game_of_life_cell> grid;
+    grid.set_initial_length({L[0], L[1], L[2]})
+        .set_neighborhood_length(1)
+        .set_maximum_refinement_level(0)
+        .set_periodic(atoi(argv[6]), atoi(argv[7]), atoi(argv[8]))
+        .initialize(MPI_COMM_WORLD)
+        .balance_load();
+    for (const auto& cell : grid.local_cells()) {
+        cell.data->live_neighbor_count = 0;
+        cell.data->is_alive = splitmix64(cell.id) % 1000 < 200;
+    }
+    for (int step = 0; step < steps; step++) {
+        grid.start_remote_neighbor_copy_updates();
+        for (const auto& cell : grid.inner_cells()) {
+            cell.data->live_neighbor_count = 0;
+            for (const auto& neighbor : cell.neighbors_of)
+                if (neighbor.data->is_alive) cell.data->live_neighbor_count++;
+        }
+        grid.wait_remote_neighbor_copy_updates();
+        for (const auto& cell : grid.outer_cells()) {
+            cell.data->live_neighbor_count = 0;
+            for (const auto& neighbor : cell.neighbors_of)
+                if (neighbor.data->is_alive) cell.data->live_neighbor_count++;
+        }
+        for (const auto& cell : grid.local_cells()) {
+            if (cell.data->live_neighbor_count == 3) cell.data->is_alive = true;
+            else if (cell.data->live_neighbor_count != 2) cell.data->is_alive = false;
+        }
+    }
+    for (const auto& cell : grid.local_cells())
+        if (cell.data->is_alive) printf("alive %llu %u\n", (unsigned long long)cell.id, cell.data->live_neighbor_count);
+    return 0;
+}
+
+static int halo()
+{
+    dccrg::Dccrg<int> grid;
+    grid.set_initial_length({7, 13, 11})
+        .set_maximum_refinement_level(1)
+        .set_neighborhood_length(2)
+        .set_load_balancing_method("RANDOM")
+        .set_periodic(true, true, true)
+        .initialize(MPI_COMM_WORLD)
+        .balance_load();
+    for (const auto& cell : grid.local_cells()) *cell.data = (int)cell.id;
+    grid.update_copies_of_remote_neighbors();
+    size_t checked = 0;
+    for (const auto& cell : grid.local_cells())
+        for (const auto& neighbor : cell.neighbors_of) {
+            if (*neighbor.data != (int)neighbor.id) abort();
+            checked++;
+        }
+    printf("PASS halo %zu\n", checked);
+    return 0;
+}
+
+static int mapping()
+{
+    dccrg::Dccrg<int> grid;
+    grid.set_initial_length({100, 200, 300}).set_maximum_refinement_level(13);
+    const auto& m = grid.mapping;
+    const uint64_t ids[] = {1, 2, 100, 6000000, 6000001, 48000001, 123456789, 9000000000ull, m.get_last_cell(),
+                            m.get_last_cell() + 1, 0};
+    for (uint64_t id : ids) {
+        const auto idx = m.get_indices(id);
+        printf("%llu %d %llu %llu %llu %llu %llu %llu\n", (unsigned long long)id, m.get_refinement_level(id),
+               (unsigned long long)idx[0], (unsigned long long)idx[1], (unsigned long long)idx[2],
+               (unsigned long long)m.get_parent(id), (unsigned long long)m.get_level_0_parent(id),
+               (unsigned long long)m.get_cell_length_in_indices(id));
+    }
+    return 0;
+}
+
+static int lists(int argc, char** argv)
+{
+    dccrg::Dccrg<int> grid;
+    grid.set_initial_length({strtoull(argv[2], 0, 10), strtoull(argv[3], 0, 10), strtoull(argv[4], 0, 10)})
+        .set_neighborhood_length(atoi(argv[8]))
+        .set_maximum_refinement_level(0)
+        .set_periodic(atoi(argv[5]), atoi(argv[6]), atoi(argv[7]))
+        .initialize(MPI_COMM_WORLD);
+    for (const auto& cell : grid.local_cells()) {
+        printf("cell %llu of", (unsigned long long)cell.id);
+        for (const auto& n : cell.neighbors_of) printf(" %llu:%d,%d,%d", (unsigned long long)n.id, n.x, n.y, n.z);
+        printf(" to");
+        for (const auto& n : cell.neighbors_to) printf(" %llu:%d,%d,%d", (unsigned long long)n.id, n.x, n.y, n.z);
+        printf("\n");
+    }
+    return 0;
+}
+
+int main(int argc, char** argv)
+{
+    if (MPI_Init(&argc, &argv) != MPI_SUCCESS) abort();
+    int rc = 1;
+    {
+        const std::string mode = argc > 1 ? argv[1] : "blinker";
+        if (mode == "blinker") rc = blinker();
+        else if (mode == "scal3d") rc = scal3d(argc, argv);
+        else if (mode == "halo") rc = halo();
+        else if (mode == "mapping") rc = mapping();
+        else if (mode == "lists") rc = lists(argc, argv);
+    }
+    MPI_Finalize();
+    return rc;
+}

@@ -1,0 +1,99 @@
+"""The C++ drop-in facade (include/dccrg_amd.hpp): user programs written the
+way the reference's examples use dccrg::Dccrg, compiled against the facade
+and run on the GPU; results compared with the oracle."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import dccrg_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "build", "facade_programs")
+MPI_INC, MPI_LIB = "/opt/conda/include", "/opt/conda/lib"
+
+
+def compile_facade(out=BIN):
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"), "-I", MPI_INC,
+           os.path.join(ROOT, "tests", "cpp", "facade_programs.cpp"), "-o", out,
+           os.path.join(ROOT, "dccrg_amd", "libdccrgx.so"), os.path.join(MPI_LIB, "libmpi.so"),
+           f"-Wl,-rpath,{os.path.join(ROOT, 'dccrg_amd')}:{MPI_LIB}"]
+    subprocess.check_call(cmd)
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(MPI_INC, "mpi.h")), reason="MPI headers absent")
+def test_facade_compiles(tmp_path):
+    compile_facade(str(tmp_path / "facade_programs"))
+
+
+def run(*args):
+    if not os.path.exists(BIN):
+        compile_facade()
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = "/usr/lib/x86_64-linux-gnu:" + MPI_LIB
+    r = subprocess.run([BIN, *[str(a) for a in args]], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+@pytest.mark.gpu
+def test_facade_blinker():
+    assert "PASS blinker" in run("blinker")
+
+
+@pytest.mark.gpu
+def test_facade_halo():
+    assert "PASS halo" in run("halo")
+
+
+@pytest.mark.gpu
+def test_facade_mapping_matches_oracle():
+    om = O.Mapping((100, 200, 300), 13)
+    for line in run("mapping").strip().splitlines():
+        v = [int(x) for x in line.split()]
+        cid = v[0]
+        assert v[1] == om.get_refinement_level(cid)
+        assert tuple(v[2:5]) == om.get_indices(cid)
+        assert v[5] == om.get_parent(cid) and v[6] == om.get_level_0_parent(cid)
+        assert v[7] == om.get_cell_length_in_indices(cid)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims,per", [((12, 10, 9), (0, 0, 1)), ((9, 7, 1), (1, 1, 0))])
+def test_facade_scalability_loop(dims, per):
+    steps = 5
+    out = run("scal3d", *dims, steps, *per)
+    got = {}
+    for line in out.strip().splitlines():
+        _, cid, cnt = line.split()
+        got[int(cid)] = int(cnt)
+    n = int(np.prod(dims))
+    a0 = O.random_alive(np.arange(1, n + 1, dtype=np.uint64), 200)
+    ra, rc = O.gol_reference_run(dims, tuple(bool(p) for p in per), 1, a0, steps)
+    want = {int(i) + 1: int(rc[i]) for i in np.nonzero(ra)[0]}
+    assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims,per,hood", [((4, 3, 2), (1, 0, 1), 1), ((3, 1, 1), (1, 0, 0), 2),
+                                           ((5, 4, 1), (0, 0, 0), 0)])
+def test_facade_iteration_cache_order(dims, per, hood):
+    """neighbors_of = [only_of][both], neighbors_to = [both][only_to] (dccrg.hpp:11570-11712)."""
+    og = O.Grid(dims, 0, tuple(bool(p) for p in per), hood)
+    for line in run("lists", *dims, *per, hood).strip().splitlines():
+        head, rest = line.split(" of", 1)
+        cid = int(head.split()[1])
+        of_part, to_part = rest.split(" to", 1)
+
+        def parse(s):
+            out = []
+            for tok in s.split():
+                i, o = tok.split(":")
+                out.append((int(i), tuple(int(x) for x in o.split(","))))
+            return out
+        lof, lto = O.iteration_cache_lists(og.find_neighbors_of(cid), og.find_neighbors_to(cid))
+        assert parse(of_part) == lof
+        assert parse(to_part) == lto
