@@ -50,6 +50,22 @@ def cpu_baseline(seconds: float = 10.0):
                       f"face-graph-walk neighbor lists"}
 
 
+def pmc_traffic(kernel: str, cells_per_launch: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of the
+    same kernel and launch size (tools/summarize_prof.py; FETCH_SIZE and
+    WRITE_SIZE in separate passes, gfx950 corrections applied), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=os.path.getmtime):
+        try:
+            s = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in s.get("kernel", "") and s.get("cells_per_launch") == cells_per_launch:
+            best = (s["traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -158,6 +174,11 @@ def main():
         },
         "init_s": t_init,
     }
+    if launches == args.steps:  # one stencil launch per step (no remote halo split)
+        t = pmc_traffic("k_gol26v<8, 4, true>", n_local)
+        if t:
+            line["roofline"]["traffic"] = t[0]
+            line["roofline"]["traffic_source"] = t[1]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -397,6 +397,111 @@ __global__ void __launch_bounds__(64 * NW) k_gol26v(Gol4Args g)
     }
 }
 
+// Vectorised LB == 1 kernel (2-D grids, LA % 4 == 0): a workgroup owns 256*NW
+// cells of a row and marches along C (the y rows); lane = 4 cells (dwordx4),
+// packed-byte row sums as in k_gol26v; rows b-1 / b+1 are the row itself
+// (periodic B: mult = 3) or absent (mult = 1).
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_gol26_rowv(Gol4Args g, uint32_t mult)
+{
+    constexpr int NT = 64 * NW, TA = 4 * NT;
+    __shared__ uint32_t P[2][NT];
+    __shared__ uint32_t E[2][2];
+    const int t = threadIdx.x;
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, q8 = g.nwg >> 3, r8 = g.nwg & 7;
+    const uint32_t wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const uint32_t tile_id = wgid % g.tiles_a;
+    const int64_t chunk_id = wgid / g.tiles_a;
+    const int64_t a0 = (int64_t)tile_id * TA;
+    const int64_t c0 = g.s0 + chunk_id * g.chunk;
+    const int64_t c1 = min(g.s1, c0 + g.chunk);
+    if (c0 >= c1) return;
+    const int64_t LA = (int64_t)g.LA;
+    auto wrapA = [&](int64_t a) -> int64_t {
+        if (a >= 0 && a < LA) return a;
+        return g.perA ? ug_wrap(a, LA) : -1;
+    };
+    const int64_t av = wrapA(a0 + 4 * t);
+    const bool vok = av >= 0;
+    const uint32_t voff = vok ? (uint32_t)av : 0u;
+    const int64_t ae = t == 0 ? wrapA(a0 - 1) : (t == NT - 1 ? wrapA(a0 + TA) : -1);
+    const bool eok = ae >= 0;
+    const uint32_t eoff = eok ? (uint32_t)ae : 0u;
+    uint4 F;
+    uint32_t FE;
+    auto fetch = [&](int64_t sc) {
+        const uint32_t* __restrict__ plane = g.in + (uint64_t)sc * g.S;
+        const uint4 v = *reinterpret_cast<const uint4*>(plane + voff);
+        F = vok ? v : make_uint4(0, 0, 0, 0);
+        FE = eok ? plane[eoff] : 0u;
+    };
+    auto stash = [&](int buf) {
+        P[buf][t] = pack_bits(F);
+        if (t == 0) E[buf][0] = FE != 0u ? 1u : 0u;
+        if (t == NT - 1) E[buf][1] = FE != 0u ? 1u : 0u;
+    };
+    uint32_t Sx, Bx;
+    auto sums = [&](int buf) {
+        const uint32_t m = P[buf][t];
+        const uint32_t lft = t > 0 ? (P[buf][t - 1] >> 24) : E[buf][0];
+        const uint32_t rgt = t < NT - 1 ? (P[buf][t + 1] & 0xffu) : E[buf][1];
+        Sx = mult * (m + ((m << 8) | lft) + ((m >> 8) | (rgt << 24)));
+        Bx = m;
+    };
+    uint32_t Sp, Sc, Bc;
+    uint4 Vc, Vn;
+    fetch(c0 - 1);
+    stash(0);
+    fetch(c0);
+    __syncthreads();
+    sums(0);
+    Sp = Sx;
+    stash(1);
+    Vc = F;
+    fetch(c0 + 1);
+    __syncthreads();
+    sums(1);
+    Sc = Sx;
+    Bc = Bx;
+    int buf = 0;
+    const bool a_ok = a0 + 4 * t < LA;
+    for (int64_t c = c0; c < c1; c++) {
+        stash(buf);
+        Vn = F;
+        if (c + 2 <= c1) fetch(c + 2);
+        __syncthreads();
+        sums(buf);
+        buf ^= 1;
+        const uint32_t cnt4 = Sp + Sc + Sx - Bc;
+        if (a_ok) {
+            const uint32_t n0 = cnt4 & 0xffu, n1 = (cnt4 >> 8) & 0xffu, n2 = (cnt4 >> 16) & 0xffu, n3 = cnt4 >> 24;
+            const uint4 nc = make_uint4(n0, n1, n2, n3);
+            const uint4 nv = make_uint4(gol_rule(n0, Vc.x), gol_rule(n1, Vc.y), gol_rule(n2, Vc.z),
+                                        gol_rule(n3, Vc.w));
+            const uint64_t plin = g.S * (uint64_t)(c + g.cbase);
+            const uint32_t p = (uint32_t)(a0 + 4 * t);
+            uint32_t* pcnt = g.cnt + (uint64_t)c * g.S;
+            uint32_t* pout = g.out + (uint64_t)c * g.S;
+            if (plin >= g.lo && plin + g.S <= g.hi) {
+                *reinterpret_cast<uint4*>(pcnt + p) = nc;
+                *reinterpret_cast<uint4*>(pout + p) = nv;
+            } else {
+                const uint32_t ncs[4] = {nc.x, nc.y, nc.z, nc.w}, nvs[4] = {nv.x, nv.y, nv.z, nv.w};
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (plin + p + j >= g.lo && plin + p + j < g.hi) {
+                        pcnt[p + j] = ncs[j];
+                        pout[p + j] = nvs[j];
+                    }
+            }
+        }
+        Sp = Sc;
+        Sc = Sx;
+        Bc = Bx;
+        Vc = Vn;
+    }
+}
+
 // LB == 1 (2-D and 1-D grids): one row per plane; rows b-1 / b+1 are the same
 // row (periodic B) or absent.
 template <int TA, int NA>
@@ -598,7 +703,35 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
     a.perA = u.perA;
     a.perB = u.perB;
     const int64_t nsl = s1 - s0;
-    if (u.LB == 1) {
+    if (u.LB == 1 && u.LA % 4 == 0 && u.S < (1ull << 31) && !getenv_flag("DCCRGX_GOL_SCALAR")) {
+        Gol4Args v{};
+        v.in = a.in;
+        v.out = a.out;
+        v.cnt = a.cnt;
+        v.LA = u.LA;
+        v.LB = 1;
+        v.S = u.S;
+        v.lo = u.lo;
+        v.hi = u.hi;
+        v.cbase = u.cbase;
+        v.s0 = s0;
+        v.s1 = s1;
+        v.perA = u.perA;
+        v.perB = u.perB;
+        constexpr int NW = 4, TA = 256 * NW;
+        v.tiles_a = (uint32_t)((u.LA + TA - 1) / TA);
+        v.tiles_b = 1;
+        int64_t chunk = getenv_int("DCCRGX_GOL_CHUNK", 0);
+        if (chunk <= 0) {
+            const int64_t want = getenv_int("DCCRGX_GOL_WGS", 8192);
+            int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(nsl, (want + v.tiles_a - 1) / v.tiles_a));
+            chunk = (nsl + chunks - 1) / chunks;
+        }
+        v.chunk = chunk;
+        const int64_t chunks = (nsl + chunk - 1) / chunk;
+        v.nwg = (uint32_t)(v.tiles_a * chunks);
+        hipLaunchKernelGGL((k_gol26_rowv<NW>), dim3(v.nwg), dim3(64 * NW), 0, st, v, u.perB ? 3u : 1u);
+    } else if (u.LB == 1) {
         constexpr int TA = 1024, NA = 4;
         a.tiles_a = (uint32_t)((u.LA + TA - 1) / TA);
         a.tiles_b = 1;

@@ -265,6 +265,9 @@ VEC_CASES = [
     ((8, 40, 6), (True, False, True), 3),
     ((520, 33, 4), (True, True, False), 2),
     ((4, 4, 7), (False, True, True), 1),
+    ((264, 20, 1), (True, False, False), 1),   # 2-D: vectorised row kernel
+    ((1032, 9, 1), (False, True, True), 2),
+    ((8, 1, 1), (True, False, False), 1),
 ]
 
 

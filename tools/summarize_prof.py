@@ -1,0 +1,48 @@
+"""Summarise a rocprofv3 run of bench.py into profiles/<tag>_summary.json.
+
+Inputs (from tools/gpu_r1f.sh): <dir>/trace/run_kernel_stats.csv (kernel
+trace + stats), <dir>/fetch/run_counter_collection.csv (--pmc FETCH_SIZE) and
+<dir>/write/run_counter_collection.csv (--pmc WRITE_SIZE), each a separate
+pass.  HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half of the bytes of a
+wide coalesced streaming read, so it is doubled; WRITE_SIZE is exact for
+16-B-per-lane streaming stores.
+"""
+import csv
+import json
+import statistics
+import sys
+
+KERNEL = "k_gol26v"
+
+
+def main(prof_dir, tag, cells_per_launch):
+    stats = list(csv.DictReader(open(f"{prof_dir}/trace/run_kernel_stats.csv")))
+    k = [r for r in stats if KERNEL in r["Name"]][0]
+    fetch = [float(r["Counter_Value"]) for r in csv.DictReader(open(f"{prof_dir}/fetch/run_counter_collection.csv"))
+             if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
+    write = [float(r["Counter_Value"]) for r in csv.DictReader(open(f"{prof_dir}/write/run_counter_collection.csv"))
+             if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "WRITE_SIZE"]
+    fetch_b = 2 * statistics.median(fetch) * 1024
+    write_b = statistics.median(write) * 1024
+    alg = 12 * cells_per_launch
+    avg_ns = float(k["AverageNs"])
+    out = {
+        "kernel": k["Name"],
+        "calls": int(k["Calls"]),
+        "average_ns": avg_ns,
+        "cells_per_launch": cells_per_launch,
+        "algorithmic_bytes_per_launch": alg,
+        "achieved_GBs": alg / avg_ns,
+        "fetch_bytes_per_launch": fetch_b,
+        "write_bytes_per_launch": write_b,
+        "traffic_bytes_per_launch": fetch_b + write_b,
+        "traffic_over_algorithmic": (fetch_b + write_b) / alg,
+        "note": "FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> bytes; separate --pmc passes",
+    }
+    json.dump(out, open(f"profiles/{tag}_summary.json", "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 2048 ** 3)
