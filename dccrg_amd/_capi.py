@@ -47,6 +47,11 @@ class GridInfo_t(C.Structure):
                 ("rank", C.c_int32), ("comm_size", C.c_int32)]
 
 
+class AdvectFields_t(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("density", "flux", "vx", "vy", "vz",
+                                         "length_x", "length_y", "length_z")]
+
+
 # every symbol include/dccrgx.h declares, with its ctypes signature
 _vp = C.c_void_p
 _u64p = C.POINTER(C.c_uint64)
@@ -102,6 +107,10 @@ SIGNATURES = {
     "dccrgx_gol_step": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "dccrgx_field_init_hash": (C.c_int, [_vp, C.c_int32, C.c_uint32]),
     "dccrgx_kernel_timer": (C.c_int, [_vp, C.c_int32, C.POINTER(C.c_double), _u64p]),
+    "dccrgx_advect_fluxes": (C.c_int, [_vp, C.c_int32, C.POINTER(AdvectFields_t), C.c_double, C.c_int32]),
+    "dccrgx_advect_apply": (C.c_int, [_vp, C.POINTER(AdvectFields_t)]),
+    "dccrgx_advect_max_time_step": (C.c_int, [_vp, C.POINTER(AdvectFields_t), C.POINTER(C.c_double)]),
+    "dccrgx_advect_step": (C.c_int, [_vp, C.c_int32, C.POINTER(AdvectFields_t), C.c_double]),
 }
 
 _lib = None

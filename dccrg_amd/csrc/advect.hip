@@ -1,0 +1,343 @@
+// advect.hip -- the advection solver of tests/advection/solve.hpp on the device.
+//
+// The reference loops over inner (or outer) cells and, for every face
+// neighbor in the iteration cache, computes one upwind flux and adds it to
+// BOTH cells (solve.hpp:224-230), skipping the negative direction of
+// local-local pairs so each face is solved once (:125-128).  On the GPU that
+// scatter would need atomics on doubles; instead every local cell gathers
+// the fluxes of all of its own faces (both directions).  Per face the flux is
+// the same expression evaluated in the same order (contraction off), so each
+// face value is bit-identical to the reference's; only the order in which a
+// cell's face fluxes are summed differs (fp64, checked at 1e-12 relative).
+//
+// Fields are SoA f64 (one field per Cell::data member, cell.hpp:34-44), so
+// the per-step halo moves only density -- the reference's
+// transfer_all_data = false datatype (cell.hpp:47-57).
+#include <cfloat>
+#include <cstring>
+
+#include "grid.hpp"
+
+namespace dccrgx {
+
+namespace {
+
+struct AdvPtrs {
+    const double* rho;
+    double* flux;
+    const double* v[3];
+    const double* l[3];
+};
+
+unsigned grid_for(uint64_t n)
+{
+    uint64_t g = (n + 255) / 256;
+    if (g > 256 * 64) g = 256 * 64;
+    if (g == 0) g = 1;
+    return (unsigned)g;
+}
+
+// flux of one face, solve.hpp:134-221; dir = +-1, +-2, +-3 (x, y, z).
+// Returns the contribution to the cell's flux: -flux / V for dir > 0,
+// +flux / V for dir < 0 (:224-230).
+__device__ inline double face_term(const AdvPtrs& p, uint64_t c, uint64_t n, int dir, double dt, double vol_c)
+{
+#pragma clang fp contract(off)
+    const int ax = (dir > 0 ? dir : -dir) - 1;
+    const int a1 = ax == 0 ? 1 : 0, a2 = ax == 2 ? 1 : 2;  // the other two axes, ascending
+    const double area_c = p.l[a1][c] * p.l[a2][c], area_n = p.l[a1][n] * p.l[a2][n];
+    const double min_area = area_c < area_n ? area_c : area_n;
+    const double lc = p.l[ax][c], ln = p.l[ax][n];
+    const double v = (lc * p.v[ax][n] + ln * p.v[ax][c]) / (lc + ln);
+    const double rho_c = p.rho[c], rho_n = p.rho[n];
+    double f;
+    if (dir > 0) f = (v >= 0 ? rho_c : rho_n) * dt * v * min_area;
+    else f = (v >= 0 ? rho_n : rho_c) * dt * v * min_area;
+    return dir > 0 ? -(f / vol_c) : f / vol_c;
+}
+
+// face classification of one cache entry, solve.hpp:73-99
+__device__ inline int face_dir(int64_t cl, int64_t nl, const int32_t* off)
+{
+    int overlaps = 0, direction = 0;
+    for (int d = 0; d < 3; d++) {
+        const int64_t o = off[d];
+        if (o < cl && o > -nl) overlaps++;
+        else if (o == cl) direction = d + 1;
+        else if (o == -nl) direction = -(d + 1);
+    }
+    // overlaps > 2 would be a neighbor overlapping the cell itself, which a
+    // valid leaf set cannot produce (the reference aborts, :101-116)
+    return overlaps == 2 ? direction : 0;
+}
+
+// explicit (mixed-level) grids: gather over the iteration-cache stencil rows
+__global__ void __launch_bounds__(256) k_ex_advect(AdvPtrs p, double dt, const uint64_t* __restrict__ st_row,
+                                                   const uint32_t* __restrict__ st_slot,
+                                                   const int32_t* __restrict__ st_off,
+                                                   const uint32_t* __restrict__ local_g,
+                                                   const uint8_t* __restrict__ level, int M,
+                                                   const uint32_t* __restrict__ pos, uint64_t n)
+{
+#pragma clang fp contract(off)
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t q = pos[i];
+        const uint32_t c = local_g[q];
+        const int64_t cl = 1ll << (M - level[c]);
+        const double vol = p.l[0][c] * p.l[1][c] * p.l[2][c];
+        double acc = p.flux[c];
+        for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) {
+            const uint32_t nb = st_slot[e];
+            const int dir = face_dir(cl, 1ll << (M - level[nb]), st_off + 3 * e);
+            if (dir) acc += face_term(p, c, nb, dir, dt, vol);
+        }
+        p.flux[c] = acc;
+    }
+}
+
+// uniform grids: the face neighbors present in the neighborhood (mask bit
+// 2k / 2k+1 = canonical axis k, -1 / +1), addressed in the slab layout
+__global__ void __launch_bounds__(256) k_u_advect(UGeom g, AdvPtrs p, double dt, uint32_t mask, uint64_t lin0,
+                                                  uint64_t n)
+{
+#pragma clang fp contract(off)
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const uint64_t soff = (uint64_t)(-g.cbase * (int64_t)g.S);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t lin = lin0 + i;
+        int64_t a, b, c;
+        ug_decompose(g, lin, a, b, c);
+        const uint64_t s = lin + soff;
+        const double vol = p.l[0][s] * p.l[1][s] * p.l[2][s];
+        double acc = p.flux[s];
+        for (int k = 0; k < 3; k++)
+            for (int sg = 0; sg < 2; sg++) {
+                if (!(mask >> (2 * k + sg) & 1)) continue;
+                int32_t d[3] = {0, 0, 0};
+                d[k] = sg ? 1 : -1;
+                int64_t a2 = a + d[0], b2 = b + d[1], c2 = c + d[2];
+                if (a2 < 0 || a2 >= (int64_t)g.LA) {
+                    if (!g.perA) continue;
+                    a2 = ug_wrap(a2, (int64_t)g.LA);
+                }
+                if (b2 < 0 || b2 >= (int64_t)g.LB) {
+                    if (!g.perB) continue;
+                    b2 = ug_wrap(b2, (int64_t)g.LB);
+                }
+                if ((c2 < 0 || c2 >= (int64_t)g.LC) && !g.perC) continue;
+                const int dir = (sg ? 1 : -1) * (g.perm[k] + 1);
+                acc += face_term(p, s, ug_slot(g, a2, b2, c2), dir, dt, vol);
+            }
+        p.flux[s] = acc;
+    }
+}
+
+// apply_fluxes, solve.hpp:283-293
+__global__ void __launch_bounds__(256) k_apply_slots(double* __restrict__ rho, double* __restrict__ flux,
+                                                     uint64_t s0, uint64_t n, const uint32_t* __restrict__ slots)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t s = slots ? slots[i] : s0 + i;
+        rho[s] += flux[s];
+        flux[s] = 0;
+    }
+}
+
+// order-preserving map of doubles onto uint64 for atomicMin
+__device__ inline unsigned long long dkey(double x)
+{
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__host__ inline double dunkey(unsigned long long k)
+{
+    const unsigned long long b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    double x;
+    memcpy(&x, &b, 8);
+    return x;
+}
+
+// max_time_step, solve.hpp:302-320 (local part)
+__global__ void __launch_bounds__(256) k_max_dt(AdvPtrs p, uint64_t s0, uint64_t n,
+                                                const uint32_t* __restrict__ slots,
+                                                unsigned long long* __restrict__ out)
+{
+    __shared__ unsigned long long red[256];
+    unsigned long long m = dkey(DBL_MAX);
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t s = slots ? slots[i] : s0 + i;
+        for (int d = 0; d < 3; d++) {
+            const double t = p.l[d][s] / fabs(p.v[d][s]);
+            if (isnormal(t)) {
+                const unsigned long long k = dkey(t);
+                m = k < m ? k : m;
+            }
+        }
+    }
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] = min(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMin(out, red[0]);
+}
+
+int adv_ptrs(const dccrgx_grid* grid, const dccrgx_advect_fields* f, AdvPtrs* p)
+{
+    DX_CHECK(f, DCCRGX_EINVAL, "null field set");
+    const int32_t ids[8] = {f->density, f->flux, f->vx, f->vy, f->vz, f->length_x, f->length_y, f->length_z};
+    for (int i = 0; i < 8; i++) {
+        DX_CHECK(ids[i] >= 0 && (size_t)ids[i] < grid->fields.size(), DCCRGX_EINVAL, "bad field %d", ids[i]);
+        DX_CHECK(grid->fields[ids[i]].elem == 8, DCCRGX_EINVAL, "advection fields are f64 (field %d)", ids[i]);
+    }
+    DX_CHECK(f->density != f->flux, DCCRGX_EINVAL, "density and flux must be distinct fields");
+    auto P = [&](int32_t id) { return (double*)grid->fields[id].ptr; };
+    p->rho = P(f->density);
+    p->flux = P(f->flux);
+    p->v[0] = P(f->vx);
+    p->v[1] = P(f->vy);
+    p->v[2] = P(f->vz);
+    p->l[0] = P(f->length_x);
+    p->l[1] = P(f->length_y);
+    p->l[2] = P(f->length_z);
+    for (int i = 2; i < 8; i++) DX_CHECK(ids[i] != f->flux, DCCRGX_EINVAL, "flux aliases an input field");
+    return DCCRGX_OK;
+}
+
+// face items of a uniform grid's neighborhood, in canonical axes
+uint32_t face_mask(const Hood& h)
+{
+    uint32_t m = 0;
+    for (int32_t k = 0; k < h.K; k++) {
+        const int32_t* d = &h.of_c[3 * k];
+        const int nz = (d[0] != 0) + (d[1] != 0) + (d[2] != 0);
+        if (nz != 1) continue;
+        for (int ax = 0; ax < 3; ax++) {
+            if (d[ax] == -1) m |= 1u << (2 * ax);
+            if (d[ax] == 1) m |= 1u << (2 * ax + 1);
+        }
+    }
+    return m;
+}
+
+// local storage runs of a uniform grid: [s0, s0 + n)
+void uniform_local_run(const dccrgx_grid* grid, uint64_t* s0, uint64_t* n)
+{
+    const UGeom& u = grid->g;
+    *s0 = u.lo + (uint64_t)(-u.cbase * (int64_t)u.S);
+    *n = u.hi - u.lo;
+}
+
+}  // namespace
+
+}  // namespace dccrgx
+
+using namespace dccrgx;
+
+extern "C" {
+
+int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt,
+                         int32_t region)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    const Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    DX_CHECK(region >= DCCRGX_REGION_ALL && region <= DCCRGX_REGION_OUTER, DCCRGX_EINVAL, "bad region");
+    AdvPtrs p;
+    DX_TRY(adv_ptrs(grid, f, &p));
+    if (!grid->n_local) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    if (!grid->uniform) {
+        ExRegion R;
+        DX_TRY(explicit_region(grid, *h, region, &R));
+        if (!R.n) return DCCRGX_OK;
+        hipLaunchKernelGGL(k_ex_advect, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, h->d_st_row, h->d_st_slot,
+                           h->d_st_off, R.local_g, R.level, grid->map.max_lvl, R.pos, R.n);
+        DX_HIP(hipGetLastError());
+        return DCCRGX_OK;
+    }
+    const UGeom& u = grid->g;
+    const uint32_t mask = face_mask(*h);
+    if (!mask) return DCCRGX_OK;
+    int64_t r[2][2];
+    region_slices(grid, *h, region, r);
+    const int64_t S = (int64_t)u.S;
+    for (auto& x : r) {
+        if (x[1] <= x[0]) continue;
+        const uint64_t l0 = std::max<int64_t>((x[0] + u.cbase) * S, (int64_t)u.lo);
+        const uint64_t l1 = std::min<int64_t>((x[1] + u.cbase) * S, (int64_t)u.hi);
+        if (l1 <= l0) continue;
+        hipLaunchKernelGGL(k_u_advect, dim3(grid_for(l1 - l0)), dim3(256), 0, st, u, p, dt, mask, l0, l1 - l0);
+        DX_HIP(hipGetLastError());
+    }
+    return DCCRGX_OK;
+}
+
+int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    AdvPtrs p;
+    DX_TRY(adv_ptrs(grid, f, &p));
+    if (!grid->n_local) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    uint64_t s0 = 0, n = grid->n_local;
+    const uint32_t* slots = nullptr;
+    if (grid->uniform) uniform_local_run(grid, &s0, &n);
+    else {
+        ExRegion R;
+        DX_TRY(explicit_region(grid, grid->hoods.begin()->second, DCCRGX_REGION_ALL, &R));
+        slots = R.local_g;
+    }
+    hipLaunchKernelGGL(k_apply_slots, dim3(grid_for(n)), dim3(256), 0, st, (double*)p.rho, p.flux, s0, n, slots);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f, double* local_min)
+{
+    DX_CHECK(grid && local_min, DCCRGX_EINVAL, "null argument");
+    AdvPtrs p;
+    DX_TRY(adv_ptrs(grid, f, &p));
+    *local_min = DBL_MAX;
+    if (!grid->n_local) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    uint64_t s0 = 0, n = grid->n_local;
+    const uint32_t* slots = nullptr;
+    if (grid->uniform) uniform_local_run(grid, &s0, &n);
+    else {
+        ExRegion R;
+        DX_TRY(explicit_region(grid, grid->hoods.begin()->second, DCCRGX_REGION_ALL, &R));
+        slots = R.local_g;
+    }
+    unsigned long long* d = nullptr;
+    DX_HIP(hipMalloc((void**)&d, 8));
+    const unsigned long long init = 0xffffffffffffffffull;  // above every key
+    DX_HIP(hipMemcpyAsync(d, &init, 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_max_dt, dim3(std::min<unsigned>(grid_for(n), 1024)), dim3(256), 0, st, p, s0, n, slots, d);
+    DX_HIP(hipGetLastError());
+    unsigned long long k = 0;
+    DX_HIP(hipMemcpyAsync(&k, d, 8, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d);
+    if (k != init) *local_min = dunkey(k);
+    return DCCRGX_OK;
+}
+
+int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt)
+{
+    DX_CHECK(grid && f, DCCRGX_EINVAL, "null argument");
+    // 2d.cpp:321-390: start density halo, inner fluxes, wait, outer fluxes, apply
+    const int32_t fd = f->density;
+    DX_TRY(dccrgx_halo_start(grid, hood_id, &fd, 1));
+    DX_TRY(dccrgx_advect_fluxes(grid, hood_id, f, dt, DCCRGX_REGION_INNER));
+    DX_TRY(dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL));
+    DX_TRY(dccrgx_advect_fluxes(grid, hood_id, f, dt, DCCRGX_REGION_OUTER));
+    return dccrgx_advect_apply(grid, f);
+}
+
+}  // extern "C"

@@ -34,6 +34,7 @@ struct Explicit {
     std::vector<uint64_t> local;    // ascending local ids
     std::vector<uint32_t> local_g;  // their global indices
     uint32_t* d_local_g = nullptr;
+    uint8_t* d_level = nullptr;     // refinement level of each leaf (global index)
     struct HoodLists {
         std::vector<uint64_t> h_nof_row, h_nto_row;
         std::vector<uint32_t> h_nof_g, h_nto_g;
@@ -282,11 +283,18 @@ __global__ void __launch_bounds__(256) k_stencil_rows(const uint64_t* __restrict
 
 __global__ void __launch_bounds__(256) k_stencil_slots(const uint64_t* __restrict__ tmp_row, const Pair* __restrict__ tmp,
                                                        const uint64_t* __restrict__ st_row, uint64_t nl,
-                                                       uint32_t* __restrict__ st_slot)
+                                                       uint32_t* __restrict__ st_slot, int32_t* __restrict__ st_off)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride)
-        for (uint64_t e = 0; e < st_row[i + 1] - st_row[i]; e++) st_slot[st_row[i] + e] = tmp[tmp_row[i] + e].g;
+        for (uint64_t e = 0; e < st_row[i + 1] - st_row[i]; e++) {
+            const Pair& p = tmp[tmp_row[i] + e];
+            const uint64_t o = st_row[i] + e;
+            st_slot[o] = p.g;
+            st_off[3 * o + 0] = p.x;
+            st_off[3 * o + 1] = p.y;
+            st_off[3 * o + 2] = p.z;
+        }
 }
 
 __global__ void __launch_bounds__(256) k_ex_gol(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
@@ -403,9 +411,15 @@ int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     E->leaves.assign(leaves, leaves + n);
     std::sort(E->leaves.begin(), E->leaves.end());
     E->leaves.erase(std::unique(E->leaves.begin(), E->leaves.end()), E->leaves.end());
-    for (uint64_t c : E->leaves)
-        DX_CHECK(map_level(grid->map, c) >= 0, DCCRGX_EINVAL, "invalid cell %llu", (unsigned long long)c);
+    std::vector<uint8_t> level;
+    level.reserve(E->leaves.size());
+    for (uint64_t c : E->leaves) {
+        const int l = map_level(grid->map, c);
+        DX_CHECK(l >= 0, DCCRGX_EINVAL, "invalid cell %llu", (unsigned long long)c);
+        level.push_back((uint8_t)l);
+    }
     E->n = E->leaves.size();
+    DX_TRY(upload(level, &E->d_level, st));
     uint64_t cap = 16;
     while (cap < 2 * E->n) cap <<= 1;
     E->mask = cap - 1;
@@ -458,6 +472,7 @@ void explicit_destroy(dccrgx_grid* grid)
     hipFree(E->d_keys);
     hipFree(E->d_vals);
     hipFree(E->d_local_g);
+    hipFree(E->d_level);
     for (auto& kv : E->hl) {
         hipFree(kv.second.d_inner_pos);
         hipFree(kv.second.d_outer_pos);
@@ -539,9 +554,10 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     DX_TRY(scan_counts_u32(d_pc, nl, st_row, st));
     DX_TRY(upload(st_row, &h.d_st_row, st));
     DX_HIP(hipMalloc(&h.d_st_slot, std::max<uint64_t>(st_row[nl], 1) * 4));
+    DX_HIP(hipMalloc(&h.d_st_off, std::max<uint64_t>(st_row[nl], 1) * 12));
     if (nl)
         hipLaunchKernelGGL(k_stencil_slots, dim3(grid_for(nl)), dim3(256), 0, st, d_tmp_row, d_pairs, h.d_st_row, nl,
-                           h.d_st_slot);
+                           h.d_st_slot, h.d_st_off);
     DX_HIP(hipGetLastError());
     hipFree(d_tmp_row);
     hipFree(d_pairs);
@@ -700,18 +716,29 @@ int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t
     return DCCRGX_OK;
 }
 
+int explicit_region(const dccrgx_grid* grid, const Hood& h, int32_t region, ExRegion* out)
+{
+    const Explicit* E = grid->ex;
+    const auto it = E->hl.find(h.id);
+    DX_CHECK(it != E->hl.end(), DCCRGX_EINTERNAL, "no lists for neighborhood %d", h.id);
+    const auto& L = it->second;
+    out->pos = region == DCCRGX_REGION_INNER ? L.d_inner_pos
+               : region == DCCRGX_REGION_OUTER ? L.d_outer_pos : L.d_all_pos;
+    out->n = region == DCCRGX_REGION_INNER ? L.inner_pos.size()
+             : region == DCCRGX_REGION_OUTER ? L.outer_pos.size() : E->local.size();
+    out->local_g = E->d_local_g;
+    out->level = E->d_level;
+    return DCCRGX_OK;
+}
+
 int explicit_gol(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out, const Field& cnt,
                  int32_t region, hipStream_t st)
 {
-    const Explicit* E = grid->ex;
-    const auto& L = E->hl.at(h.id);
-    const uint32_t* pos = region == DCCRGX_REGION_INNER ? L.d_inner_pos
-                          : region == DCCRGX_REGION_OUTER ? L.d_outer_pos : L.d_all_pos;
-    const uint64_t n = region == DCCRGX_REGION_INNER ? L.inner_pos.size()
-                       : region == DCCRGX_REGION_OUTER ? L.outer_pos.size() : E->local.size();
-    if (!n) return DCCRGX_OK;
-    hipLaunchKernelGGL(k_ex_gol, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)in.ptr, (uint32_t*)out.ptr,
-                       (uint32_t*)cnt.ptr, h.d_st_row, h.d_st_slot, E->d_local_g, pos, n);
+    ExRegion R;
+    DX_TRY(explicit_region(grid, h, region, &R));
+    if (!R.n) return DCCRGX_OK;
+    hipLaunchKernelGGL(k_ex_gol, dim3(grid_for(R.n)), dim3(256), 0, st, (const uint32_t*)in.ptr,
+                       (uint32_t*)out.ptr, (uint32_t*)cnt.ptr, h.d_st_row, h.d_st_slot, R.local_g, R.pos, R.n);
     DX_HIP(hipGetLastError());
     return DCCRGX_OK;
 }

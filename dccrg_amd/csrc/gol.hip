@@ -832,13 +832,11 @@ static int timed(dccrgx_grid* grid, bool begin, hipStream_t st)
     return DCCRGX_OK;
 }
 
-static int compute_region(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out,
-                          const Field& cnt, int32_t region, hipStream_t st)
+void region_slices(const dccrgx_grid* grid, const Hood& h, int32_t region, int64_t r[2][2])
 {
-    if (!grid->uniform) return explicit_gol(grid, h, in, out, cnt, region, st);
     const UGeom& u = grid->g;
     const int64_t all0 = u.pad, all1 = (int64_t)u.nslices - u.pad;
-    int64_t r[2][2] = {{0, 0}, {0, 0}};
+    r[0][0] = r[0][1] = r[1][0] = r[1][1] = 0;
     if (region == DCCRGX_REGION_ALL) {
         r[0][0] = all0;
         r[0][1] = all1;
@@ -855,6 +853,14 @@ static int compute_region(dccrgx_grid* grid, const Hood& h, const Field& in, con
             r[1][0] = r[1][1] = 0;
         }
     }
+}
+
+static int compute_region(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out,
+                          const Field& cnt, int32_t region, hipStream_t st)
+{
+    if (!grid->uniform) return explicit_gol(grid, h, in, out, cnt, region, st);
+    int64_t r[2][2];
+    region_slices(grid, h, region, r);
     for (auto& x : r) {
         if (x[1] <= x[0]) continue;
         DX_TRY(timed(grid, true, st));

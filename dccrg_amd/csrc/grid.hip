@@ -287,8 +287,10 @@ void free_hood(Hood& h)
     h.d_self_dst = h.d_self_src = nullptr;
     h.peers.clear();
     for (void* p : {(void*)h.d_nof_row, (void*)h.d_nof_id, (void*)h.d_nof_off, (void*)h.d_nof_g,
-                    (void*)h.d_nto_row, (void*)h.d_nto_g, (void*)h.d_st_row, (void*)h.d_st_slot})
+                    (void*)h.d_nto_row, (void*)h.d_nto_g, (void*)h.d_st_row, (void*)h.d_st_slot,
+                    (void*)h.d_st_off})
         hipFree(p);
+    h.d_st_off = nullptr;
     h.d_nof_row = h.d_nof_id = h.d_nto_row = h.d_st_row = nullptr;
     h.d_nof_off = nullptr;
     h.d_nof_g = h.d_nto_g = h.d_st_slot = nullptr;

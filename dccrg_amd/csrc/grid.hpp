@@ -145,6 +145,7 @@ struct Hood {
     // (id, offset) pairs, dccrg.hpp:11570-11712) as storage slots
     uint64_t* d_st_row = nullptr;
     uint32_t* d_st_slot = nullptr;
+    int32_t* d_st_off = nullptr;     // x, y, z offset of each stencil entry
 };
 
 }  // namespace dccrgx
@@ -173,6 +174,17 @@ int build_hood(dccrgx_grid* g, Hood& h);
 void free_hood(Hood& h);
 int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out,
                const Field& cnt, int64_t s0, int64_t s1, hipStream_t st);
+// uniform grids: storage slice ranges [r[i][0], r[i][1]) of a region
+// (DCCRGX_REGION_*; outer cells may form two runs), gol.hip
+void region_slices(const dccrgx_grid* grid, const Hood& h, int32_t region, int64_t r[2][2]);
+// explicit grids: local cells of a region as positions into the local list
+struct ExRegion {
+    const uint32_t* pos = nullptr;      // positions in the local cell list
+    uint64_t n = 0;
+    const uint32_t* local_g = nullptr;  // local position -> storage slot
+    const uint8_t* level = nullptr;     // storage slot -> refinement level
+};
+int explicit_region(const dccrgx_grid* grid, const Hood& h, int32_t region, ExRegion* out);
 // explicit (mixed refinement level) grids, explicit.hip
 int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n);
 void explicit_destroy(dccrgx_grid* grid);

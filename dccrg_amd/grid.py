@@ -401,6 +401,42 @@ class Dccrg:
         check(lib().dccrgx_gol_step(self._h, hood, self.field_id(fin), self.field_id(fout),
                                     self.field_id(fcnt)))
 
+    # ---- advection, tests/advection/solve.hpp ------------------------------
+    ADVECT_FIELDS = ("density", "flux", "vx", "vy", "vz", "length_x", "length_y", "length_z")
+
+    def _advect_fields(self, names=None):
+        """names: mapping from the Cell::data members (cell.hpp:34-44) to
+        field names; default: fields named after the members."""
+        names = names or {}
+        return X.AdvectFields_t(*[self.field_id(names.get(m, m)) for m in self.ADVECT_FIELDS])
+
+    def add_advection_fields(self):
+        for m in self.ADVECT_FIELDS:
+            self.add_field(m, np.float64)
+
+    def calculate_fluxes(self, dt: float, solve_inner: bool, hood: int = DEFAULT_NEIGHBORHOOD_ID,
+                         names=None, region=None):
+        """solve.hpp:44-247: inner cells (solve_inner) or outer cells."""
+        f = self._advect_fields(names)
+        if region is None:
+            region = X.REGION_INNER if solve_inner else X.REGION_OUTER
+        check(lib().dccrgx_advect_fluxes(self._h, hood, C.byref(f), dt, region))
+
+    def apply_fluxes(self, names=None):
+        f = self._advect_fields(names)
+        check(lib().dccrgx_advect_apply(self._h, C.byref(f)))
+
+    def max_time_step(self, names=None) -> float:
+        """Local part of solve.hpp:302-332 (reduce with MIN across ranks)."""
+        f = self._advect_fields(names)
+        out = C.c_double()
+        check(lib().dccrgx_advect_max_time_step(self._h, C.byref(f), C.byref(out)))
+        return out.value
+
+    def advect_step(self, dt: float, hood: int = DEFAULT_NEIGHBORHOOD_ID, names=None):
+        f = self._advect_fields(names)
+        check(lib().dccrgx_advect_step(self._h, hood, C.byref(f), dt))
+
     def kernel_timer(self, reset: int = 0):
         ms = C.c_double()
         n = C.c_uint64()

@@ -256,6 +256,34 @@ int dccrgx_field_init_hash(dccrgx_grid* grid, int32_t field_id, uint32_t permill
  * stream): total ms and launch count since the last reset */
 int dccrgx_kernel_timer(dccrgx_grid* grid, int32_t reset, double* ms_out, uint64_t* launches_out);
 
+/* ------------------------------------------------------------------------ *
+ * Advection, tests/advection/solve.hpp.  The reference's Cell::data members
+ * (cell.hpp:34-44) as separate f64 fields; only `density` changes per step,
+ * so the per-step halo moves only that field (transfer_all_data = false,
+ * cell.hpp:47-57).  Velocities and lengths of remote neighbors must have
+ * been exchanged once (initialize.hpp:60).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+    int32_t density, flux, vx, vy, vz, length_x, length_y, length_z;
+} dccrgx_advect_fields;
+/* calculate_fluxes(dt, solve_inner, grid, hood), solve.hpp:44-247: adds to
+ * `flux` of every local cell of `region` the upwind fluxes through all of
+ * its faces found in the neighborhood's neighbors_of (faces detected from
+ * offsets and lengths in indices, :73-120).  Gather form: each cell sums its
+ * own faces (both directions) instead of scattering into its neighbors;
+ * per-face values equal the reference's. */
+int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
+                         double dt, int32_t region);
+/* apply_fluxes, solve.hpp:283-293: density += flux, flux = 0 (local cells) */
+int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f);
+/* max_time_step, solve.hpp:302-320, this rank's part: min over local cells
+ * and axes of length / |v| where that is a normal number (DBL_MAX if none).
+ * The caller reduces with MIN across ranks (:322-332). */
+int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f, double* local_min);
+/* one step of tests/advection/2d.cpp:321-390: density halo start, inner
+ * fluxes, halo wait, outer fluxes, apply */
+int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,7 @@
  */
 #include "dccrg_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -733,4 +734,102 @@ long dox_build_uniform_slot_lists(const dox_grid* g, unsigned hood_length, uint6
     free(ids);
     free(off);
     return (long)n;
+}
+
+/* ---- Advection (tests/advection/solve.hpp) ---------------------------- */
+
+/* calculate_fluxes, solve.hpp:44-247, for the cells iter_slot[0..n_iter),
+ * each with its iteration-cache neighbors_of row (slots + offsets).  Face
+ * detection :73-120, local pairs solved once in the positive direction
+ * :125-128, min_area :134-157, interpolated velocity :165-171, upwind flux
+ * :173-221, accumulation into BOTH cells :224-230 (into ghost copies too;
+ * the reference discards those).  Returns the number of overlaps > 2 pairs
+ * (the reference aborts, :101-116). */
+long dox_advect_fluxes(size_t n_iter, const uint32_t* iter_slot, const uint64_t* row_ptr,
+                       const uint32_t* nbr_slot, const int32_t* nbr_off, const uint8_t* is_local,
+                       const uint64_t* len_idx, const double* density, const double* vx,
+                       const double* vy, const double* vz, const double* lx, const double* ly,
+                       const double* lz, double* flux, double dt)
+{
+    long bad = 0;
+    for (size_t i = 0; i < n_iter; i++) {
+        const uint32_t c = iter_slot[i];
+        const double cell_density = density[c], cell_volume = lx[c] * ly[c] * lz[c];
+        const int64_t cl = (int64_t)len_idx[c];
+        for (uint64_t e = row_ptr[i]; e < row_ptr[i + 1]; e++) {
+            const uint32_t nb = nbr_slot[e];
+            const int64_t nl = (int64_t)len_idx[nb];
+            int overlaps = 0, direction = 0;
+            for (int d = 0; d < 3; d++) {
+                const int64_t o = nbr_off[3 * e + d];
+                if (o < cl && o > -nl) overlaps++;
+                else if (o == cl) direction = d + 1;
+                else if (o == -nl) direction = -(d + 1);
+            }
+            if (overlaps < 2) continue;
+            if (overlaps > 2) {
+                bad++;
+                continue;
+            }
+            if (direction == 0) continue;
+            if (is_local[nb] && direction < 0) continue;
+            const double neighbor_density = density[nb], neighbor_volume = lx[nb] * ly[nb] * lz[nb];
+            double min_area = -1;
+            switch (direction) {
+            case -1: case 1: {
+                const double a = ly[c] * lz[c], b = ly[nb] * lz[nb];
+                min_area = a < b ? a : b;
+                break;
+            }
+            case -2: case 2: {
+                const double a = lx[c] * lz[c], b = lx[nb] * lz[nb];
+                min_area = a < b ? a : b;
+                break;
+            }
+            default: {
+                const double a = lx[c] * ly[c], b = lx[nb] * ly[nb];
+                min_area = a < b ? a : b;
+                break;
+            }
+            }
+            const double v_x = (lx[c] * vx[nb] + lx[nb] * vx[c]) / (lx[c] + lx[nb]);
+            const double v_y = (ly[c] * vy[nb] + ly[nb] * vy[c]) / (ly[c] + ly[nb]);
+            const double v_z = (lz[c] * vz[nb] + lz[nb] * vz[c]) / (lz[c] + lz[nb]);
+            const double v = direction == 1 || direction == -1 ? v_x : direction == 2 || direction == -2 ? v_y : v_z;
+            double f;
+            if (direction > 0) f = (v >= 0 ? cell_density : neighbor_density) * dt * v * min_area;
+            else f = (v >= 0 ? neighbor_density : cell_density) * dt * v * min_area;
+            if (direction > 0) {
+                flux[c] -= f / cell_volume;
+                flux[nb] += f / neighbor_volume;
+            } else {
+                flux[c] += f / cell_volume;
+                flux[nb] -= f / neighbor_volume;
+            }
+        }
+    }
+    return bad;
+}
+
+/* apply_fluxes, solve.hpp:283-293 */
+void dox_advect_apply(size_t n, const uint32_t* slot, double* density, double* flux)
+{
+    for (size_t i = 0; i < n; i++) {
+        density[slot[i]] += flux[slot[i]];
+        flux[slot[i]] = 0;
+    }
+}
+
+/* max_time_step, solve.hpp:302-332, local part (before MPI_Allreduce MIN) */
+double dox_advect_max_time_step(size_t n, const uint32_t* slot, const double* vx, const double* vy,
+                                const double* vz, const double* lx, const double* ly, const double* lz)
+{
+    double m = DBL_MAX;
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t c = slot[i];
+        const double s[3] = {lx[c] / fabs(vx[c]), ly[c] / fabs(vy[c]), lz[c] / fabs(vz[c])};
+        for (int d = 0; d < 3; d++)
+            if (isnormal(s[d]) && s[d] < m) m = s[d];
+    }
+    return m;
 }

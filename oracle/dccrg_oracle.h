@@ -103,6 +103,17 @@ void dox_gol_apply(size_t n_cells, uint32_t* alive, const uint32_t* count);
 long dox_build_uniform_slot_lists(const dox_grid* g, unsigned hood_length, uint64_t* row_ptr,
                                   uint32_t* nbr_slot, size_t cap);
 
+/* ---- Advection, tests/advection/solve.hpp.  All per-cell arrays are
+ * slot-indexed; len_idx = get_cell_length_in_indices; is_local per slot. */
+long dox_advect_fluxes(size_t n_iter, const uint32_t* iter_slot, const uint64_t* row_ptr,
+                       const uint32_t* nbr_slot, const int32_t* nbr_off, const uint8_t* is_local,
+                       const uint64_t* len_idx, const double* density, const double* vx,
+                       const double* vy, const double* vz, const double* lx, const double* ly,
+                       const double* lz, double* flux, double dt);
+void dox_advect_apply(size_t n, const uint32_t* slot, double* density, double* flux);
+double dox_advect_max_time_step(size_t n, const uint32_t* slot, const double* vx, const double* vy,
+                                const double* vz, const double* lx, const double* ly, const double* lz);
+
 #ifdef __cplusplus
 }
 #endif

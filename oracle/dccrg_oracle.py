@@ -92,6 +92,13 @@ def lib():
         L.dox_gol_apply.argtypes = [C.c_size_t, u32p, u32p]
         L.dox_build_uniform_slot_lists.restype = C.c_long
         L.dox_build_uniform_slot_lists.argtypes = [C.c_void_p, C.c_uint, u64p, u32p, C.c_size_t]
+        f64p = C.POINTER(C.c_double)
+        L.dox_advect_fluxes.restype = C.c_long
+        L.dox_advect_fluxes.argtypes = [C.c_size_t, u32p, u64p, u32p, i32p, C.POINTER(C.c_uint8), u64p] + \
+            [f64p] * 8 + [C.c_double]
+        L.dox_advect_apply.argtypes = [C.c_size_t, u32p, f64p, f64p]
+        L.dox_advect_max_time_step.restype = C.c_double
+        L.dox_advect_max_time_step.argtypes = [C.c_size_t, u32p] + [f64p] * 6
         _lib = L
     return _lib
 
@@ -430,3 +437,90 @@ def random_balanced_leaves(length, max_ref_lvl, periodic, hood_length, n_refines
             cells.discard(c)
             cells |= set(m.get_all_children(c))
     return sorted(cells)
+
+
+# ---- advection (tests/advection) --------------------------------------------
+def advection_initial_state(mapping: Mapping, cells: Sequence[int], level0_length=None):
+    """tests/advection/initialize.hpp:27-65 on a Cartesian geometry starting
+    at 0 with level-0 cell length ``level0_length`` (default 1 / length per
+    axis): hump density, solid-body velocities (solve.hpp:335-345), cell
+    lengths.  Returns slot-ordered (density, vx, vy, vz, lx, ly, lz)."""
+    L = mapping.length
+    l0 = np.array(level0_length if level0_length is not None else [1.0 / x for x in L])
+    M = mapping.max_ref_lvl
+    cells = np.asarray(cells, dtype=np.uint64)
+    idx, lvl = mapping.ids_to_indices(cells)
+    unit = l0 / float(2 ** M)
+    ln = l0[None, :] / (2.0 ** lvl.astype(np.float64))[:, None]
+    center = idx.astype(np.float64) * unit[None, :] + ln / 2
+    r = np.minimum(np.sqrt((center[:, 0] - 0.25) ** 2 + (center[:, 1] - 0.5) ** 2), 0.15) / 0.15
+    density = 0.25 * (1 + np.cos(np.pi * r))
+    vx = -center[:, 1] + 0.5
+    vy = center[:, 0] - 0.5
+    vz = np.zeros(len(cells))
+    return [np.ascontiguousarray(a, dtype=np.float64)
+            for a in (density, vx, vy, vz, ln[:, 0], ln[:, 1], ln[:, 2])]
+
+
+class AdvectionLists:
+    """The reference advection solver (solve.hpp:44-332) on every rank of a
+    block-partitioned grid, over the iteration-cache neighbor lists
+    (dccrg.hpp:11570-11712).  Slots = positions in ``cells`` (ascending)."""
+
+    def __init__(self, grid: "Grid", comm_size: int = 1, items=None):
+        self.cells = [int(c) for c in grid.cells()]
+        pos = {c: i for i, c in enumerate(self.cells)}
+        m = grid.mapping
+        n = len(self.cells)
+        self.n = n
+        self.len_idx = np.array([m.get_cell_length_in_indices(c) for c in self.cells], dtype=np.uint64)
+        self.ranks = []
+        for r in range(comm_size):
+            v = grid.rank_view(r, comm_size, items)
+            is_local = np.zeros(n, dtype=np.uint8)
+            local = np.array([pos[c] for c in v["local"]], dtype=np.uint32)
+            is_local[local] = 1
+            order = v["inner"] + v["outer"]  # 2d.cpp:331 then :339
+            row = [0]
+            slots, offs = [], []
+            for c in order:
+                lof, _ = iteration_cache_lists(v["neighbors_of"][c], v["neighbors_to"][c])
+                for i, o in lof:
+                    slots.append(pos[i])
+                    offs.extend(o)
+                row.append(len(slots))
+            self.ranks.append({
+                "iter": np.array([pos[c] for c in order], dtype=np.uint32),
+                "row": np.array(row, dtype=np.uint64),
+                "slots": np.array(slots or [0], dtype=np.uint32),
+                "offs": np.array(offs or [0, 0, 0], dtype=np.int32),
+                "is_local": is_local,
+                "local": local,
+            })
+
+    def step(self, state, dt: float):
+        """One 2d.cpp:321-390 step on every rank; returns the new density."""
+        rho, vx, vy, vz, lx, ly, lz = state
+        new = rho.copy()
+        f64 = C.c_double
+        for R in self.ranks:
+            flux = np.zeros(self.n)
+            bad = lib().dox_advect_fluxes(
+                len(R["iter"]), _p(R["iter"], C.c_uint32), _p(R["row"], C.c_uint64),
+                _p(R["slots"], C.c_uint32), _p(R["offs"], C.c_int32), _p(R["is_local"], C.c_uint8),
+                _p(self.len_idx, C.c_uint64), _p(rho, f64), _p(vx, f64), _p(vy, f64), _p(vz, f64),
+                _p(lx, f64), _p(ly, f64), _p(lz, f64), _p(flux, f64), dt)
+            if bad:
+                raise RuntimeError("overlapping neighbor (solve.hpp:101-116 aborts)")
+            mine = rho.copy()
+            lib().dox_advect_apply(len(R["local"]), _p(R["local"], C.c_uint32), _p(mine, f64), _p(flux, f64))
+            new[R["local"]] = mine[R["local"]]
+        return new
+
+    def max_time_step(self, state) -> float:
+        """solve.hpp:302-332 including the MIN reduction over ranks."""
+        _, vx, vy, vz, lx, ly, lz = state
+        f64 = C.c_double
+        return min(lib().dox_advect_max_time_step(len(R["local"]), _p(R["local"], C.c_uint32), _p(vx, f64),
+                                                  _p(vy, f64), _p(vz, f64), _p(lx, f64), _p(ly, f64),
+                                                  _p(lz, f64)) for R in self.ranks)
