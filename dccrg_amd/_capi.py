@@ -52,6 +52,19 @@ class AdvectFields_t(C.Structure):
                                          "length_x", "length_y", "length_z")]
 
 
+class PoissonParams_t(C.Structure):
+    _fields_ = [("max_iterations", C.c_uint32), ("min_iterations", C.c_uint32), ("stop_residual", C.c_double),
+                ("p_of_norm", C.c_double), ("stop_after_residual_increase", C.c_double)]
+
+
+class PoissonFields_t(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("rhs", "solution", "length_x", "length_y", "length_z")]
+
+
+POISSON_MEMBERS = ("type", "p0", "p1", "r0", "r1", "A_dot_p0", "best_solution", "scaling_factor",
+                   "f_x_pos", "f_x_neg", "f_y_pos", "f_y_neg", "f_z_pos", "f_z_neg")
+
+
 # every symbol include/dccrgx.h declares, with its ctypes signature
 _vp = C.c_void_p
 _u64p = C.POINTER(C.c_uint64)
@@ -78,6 +91,8 @@ SIGNATURES = {
     "dccrgx_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "dccrgx_neighbors_of_host": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _u64p, _u64p, _i32p, C.c_size_t]),
     "dccrgx_neighbors_to_host": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _u64p, _u64p, C.c_size_t]),
+    "dccrgx_face_neighbors_of": (C.c_int, [_vp, _vp, C.c_size_t, _vp, _vp, _vp, C.c_size_t, _vp]),
+    "dccrgx_face_neighbors_of_host": (C.c_int, [_vp, _u64p, C.c_size_t, _u64p, _u64p, _i32p, C.c_size_t]),
     "dccrgx_exchange_start": (C.c_int, [_vp, C.c_int32, C.POINTER(_vp), _u64p, C.POINTER(_vp), _u64p]),
     "dccrgx_exchange_wait": (C.c_int, [_vp, C.c_int32]),
     "dccrgx_grid_create": (C.c_int, [_vp, C.POINTER(GridParams_t), _u64p, C.c_size_t, C.POINTER(_vp)]),
@@ -111,6 +126,12 @@ SIGNATURES = {
     "dccrgx_advect_apply": (C.c_int, [_vp, C.POINTER(AdvectFields_t)]),
     "dccrgx_advect_max_time_step": (C.c_int, [_vp, C.POINTER(AdvectFields_t), C.POINTER(C.c_double)]),
     "dccrgx_advect_step": (C.c_int, [_vp, C.c_int32, C.POINTER(AdvectFields_t), C.c_double]),
+    "dccrgx_poisson_create": (C.c_int, [_vp, C.POINTER(PoissonParams_t), C.POINTER(PoissonFields_t),
+                                        C.POINTER(_vp)]),
+    "dccrgx_poisson_destroy": (C.c_int, [_vp]),
+    "dccrgx_poisson_field": (C.c_int, [_vp, C.c_int32, _i32p]),
+    "dccrgx_poisson_solve": (C.c_int, [_vp, _u64p, C.c_size_t, _u64p, C.c_size_t, C.c_int32,
+                                       C.POINTER(C.c_uint32), C.POINTER(C.c_double)]),
 }
 
 _lib = None

@@ -19,6 +19,7 @@
 #include <cstring>
 #include <set>
 
+#include "face.hpp"
 #include "grid.hpp"
 
 namespace dccrgx {
@@ -714,6 +715,20 @@ int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t
     }
     DX_HIP(hipStreamSynchronize(st));
     return DCCRGX_OK;
+}
+
+namespace {
+struct ExExists {
+    ExView v;
+    __device__ bool operator()(uint64_t c) const { return ex_find(v, c) >= 0; }
+};
+}  // namespace
+
+int explicit_face_neighbors(const dccrgx_grid* grid, const uint64_t* cells, size_t n, uint64_t* row,
+                            uint64_t* ids, int32_t* dirs, size_t cap, hipStream_t st)
+{
+    return face_neighbors_launch(grid->map, grid->params.periodic, ExExists{view(grid)}, cells, n, row, ids, dirs,
+                                 cap, st);
 }
 
 int explicit_region(const dccrgx_grid* grid, const Hood& h, int32_t region, ExRegion* out)

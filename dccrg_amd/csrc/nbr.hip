@@ -10,9 +10,21 @@
 #include <algorithm>
 #include <cstring>
 
+#include "face.hpp"
 #include "grid.hpp"
 
 namespace dccrgx {
+
+int explicit_face_neighbors(const dccrgx_grid* grid, const uint64_t* cells, size_t n, uint64_t* row,
+                            uint64_t* ids, int32_t* dirs, size_t cap, hipStream_t st);
+
+namespace {
+// a single-level grid: exactly the level-0 ids exist
+struct UniformExists {
+    MapParams mp;
+    __host__ __device__ bool operator()(uint64_t c) const { return map_level(mp, c) == 0; }
+};
+}  // namespace
 
 static unsigned grid_for(uint64_t n)
 {
@@ -117,6 +129,45 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
                            n, row, ids, off3, d_err, sc, sc, sc);
     DX_HIP(hipGetLastError());
     return DCCRGX_OK;
+}
+
+int dccrgx_face_neighbors_of(const dccrgx_grid* grid, const uint64_t* cells, size_t n, uint64_t* row,
+                             uint64_t* ids, int32_t* dirs, size_t cap, void* stream)
+{
+    DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
+    if (!grid->uniform) return explicit_face_neighbors(grid, cells, n, row, ids, dirs, cap, st);
+    return face_neighbors_launch(grid->map, grid->params.periodic, UniformExists{grid->map}, cells, n, row, ids,
+                                 dirs, cap, st);
+}
+
+int dccrgx_face_neighbors_of_host(const dccrgx_grid* grid, const uint64_t* cells, size_t n, uint64_t* row,
+                                  uint64_t* ids, int32_t* dirs, size_t cap)
+{
+    DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    hipStream_t st = grid->ctx->compute;
+    uint64_t *d_cells = nullptr, *d_row = nullptr, *d_ids = nullptr;
+    int32_t* d_dirs = nullptr;
+    DX_HIP(hipMalloc(&d_cells, std::max<size_t>(n, 1) * 8));
+    DX_HIP(hipMalloc(&d_row, (n + 1) * 8));
+    DX_HIP(hipMalloc(&d_ids, std::max<size_t>(cap, 1) * 8));
+    DX_HIP(hipMalloc(&d_dirs, std::max<size_t>(cap, 1) * 4));
+    if (n) DX_HIP(hipMemcpyAsync(d_cells, cells, n * 8, hipMemcpyHostToDevice, st));
+    int s = dccrgx_face_neighbors_of(grid, d_cells, n, d_row, ids ? d_ids : nullptr, d_dirs, cap, st);
+    if (s == DCCRGX_OK || s == DCCRGX_ERANGE) {
+        DX_HIP(hipMemcpyAsync(row, d_row, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+        DX_HIP(hipStreamSynchronize(st));
+        if (s == DCCRGX_OK && ids && row[n]) {
+            DX_HIP(hipMemcpyAsync(ids, d_ids, row[n] * 8, hipMemcpyDeviceToHost, st));
+            if (dirs) DX_HIP(hipMemcpyAsync(dirs, d_dirs, row[n] * 4, hipMemcpyDeviceToHost, st));
+        }
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_cells);
+    hipFree(d_row);
+    hipFree(d_ids);
+    hipFree(d_dirs);
+    return s;
 }
 
 int dccrgx_neighbors_to(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells, size_t n,

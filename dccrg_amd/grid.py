@@ -272,6 +272,29 @@ class Dccrg:
         row, ids, off = self.neighbors_of(np.array([cell]), hood)
         return [(int(i), tuple(int(v) for v in o)) for i, o in zip(ids, off)]
 
+    def face_neighbors_of(self, cells: np.ndarray):
+        """Batched get_face_neighbors_of (dccrg.hpp:2828-2955) on the device:
+        (row_ptr, ids, dirs) as numpy."""
+        import torch
+        dev = torch.device("cuda", self.ctx.device)
+        c = torch.from_numpy(_u64(cells).view(np.int64)).to(dev)
+        n = c.numel()
+        row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        cap = 24 * max(n, 1)
+        ids = torch.zeros(cap, dtype=torch.int64, device=dev)
+        dirs = torch.zeros(cap, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)
+        check(lib().dccrgx_face_neighbors_of(self._h, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
+                                             dirs.data_ptr(), cap, None))
+        total = int(row[-1].item())
+        return (row.cpu().numpy().astype(np.uint64), ids[:total].cpu().numpy().view(np.uint64),
+                dirs[:total].cpu().numpy())
+
+    def get_face_neighbors_of(self, cell: int):
+        """dccrg.hpp:2828-2955 for one cell: [(id, direction), ...]."""
+        _, ids, dirs = self.face_neighbors_of(np.array([cell]))
+        return [(int(i), int(d)) for i, d in zip(ids, dirs)]
+
     def get_neighbors_to(self, cell: int, hood: int = DEFAULT_NEIGHBORHOOD_ID):
         row, ids = self.neighbors_to(np.array([cell]), hood)
         return [int(i) for i in ids]

@@ -163,6 +163,16 @@ int dccrgx_get_cells(const dccrgx_grid* grid, int32_t hood_id, int32_t which, ui
 int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells_dev,
                         size_t n, uint64_t* row_ptr_dev, uint64_t* ids_dev, int32_t* off3_dev,
                         size_t cap, void* stream);
+/* Dccrg::get_face_neighbors_of (dccrg.hpp:2828-2955) for n cells: the face
+ * graph (update_neighbors_, :9463-9597) neighbor in -x,+x,-y,+y,-z,+z order
+ * plus, for a smaller neighbor, its 3 siblings sharing the face; dirs_dev
+ * gets -1/+1/-2/+2/-3/+3.  CSR like dccrgx_neighbors_of (<= 24 per cell);
+ * DCCRGX_ENOTFOUND if a cell is not an existing leaf (the reference aborts). */
+int dccrgx_face_neighbors_of(const dccrgx_grid* grid, const uint64_t* cells_dev, size_t n,
+                             uint64_t* row_ptr_dev, uint64_t* ids_dev, int32_t* dirs_dev, size_t cap,
+                             void* stream);
+int dccrgx_face_neighbors_of_host(const dccrgx_grid* grid, const uint64_t* cells, size_t n,
+                                  uint64_t* row_ptr, uint64_t* ids, int32_t* dirs, size_t cap);
 /* Dccrg::get_neighbors_to (dccrg.hpp:900-943 / find_neighbors_to :4744-4897),
  * unique ids per cell in ascending order (the reference: unordered). */
 int dccrgx_neighbors_to(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells_dev,
@@ -283,6 +293,44 @@ int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f
 /* one step of tests/advection/2d.cpp:321-390: density halo start, inner
  * fluxes, halo wait, outer fluxes, apply */
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt);
+
+/* ------------------------------------------------------------------------ *
+ * Poisson, tests/poisson/poisson_solve.hpp: Poisson_Solve (BiCG over face
+ * neighbors, 1/4 weight per smaller face neighbor) with its cell data in the
+ * grid's f64 fields.  The solver adds 14 internal fields (Poisson_Cell
+ * members, :44-83).  On several ranks the halos and the scalar reductions go
+ * over the context's RCCL communicator.
+ * ------------------------------------------------------------------------ */
+typedef struct dccrgx_poisson dccrgx_poisson;
+/* Poisson_Solve(max_iterations, min_iterations, stop_residual, p_of_norm,
+ * stop_after_residual_increase, verbose), :147-195 (defaults 1000, 0,
+ * 1e-15, 2, 10 with params == NULL) */
+typedef struct {
+    uint32_t max_iterations, min_iterations;
+    double stop_residual, p_of_norm, stop_after_residual_increase;
+} dccrgx_poisson_params;
+/* user fields: rhs and solution (Poisson_Cell::rhs/solution) and the cell
+ * lengths (the geometry's get_length, used by set_scaling_factor :704-821) */
+typedef struct {
+    int32_t rhs, solution, length_x, length_y, length_z;
+} dccrgx_poisson_fields;
+enum {
+    DCCRGX_POISSON_TYPE = 0, DCCRGX_POISSON_P0, DCCRGX_POISSON_P1, DCCRGX_POISSON_R0, DCCRGX_POISSON_R1,
+    DCCRGX_POISSON_A_DOT_P0, DCCRGX_POISSON_BEST_SOLUTION, DCCRGX_POISSON_SCALING_FACTOR,
+    DCCRGX_POISSON_F_X_POS, DCCRGX_POISSON_F_X_NEG, DCCRGX_POISSON_F_Y_POS, DCCRGX_POISSON_F_Y_NEG,
+    DCCRGX_POISSON_F_Z_POS, DCCRGX_POISSON_F_Z_NEG
+};
+int dccrgx_poisson_create(dccrgx_grid* grid, const dccrgx_poisson_params* params,
+                          const dccrgx_poisson_fields* fields, dccrgx_poisson** out);
+int dccrgx_poisson_destroy(dccrgx_poisson* solver);
+/* field id of an internal member (DCCRGX_POISSON_*) */
+int dccrgx_poisson_field(const dccrgx_poisson* solver, int32_t which, int32_t* field_id);
+/* Poisson_Solve::solve(cells, grid, cells_to_skip, cache_is_up_to_date),
+ * :251-522: cells/skip are host id lists (non-local ids are ignored).
+ * Outputs the iteration count and the minimum residual reached. */
+int dccrgx_poisson_solve(dccrgx_poisson* solver, const uint64_t* cells, size_t n_cells,
+                         const uint64_t* cells_to_skip, size_t n_skip, int32_t cache_is_up_to_date,
+                         uint32_t* iterations, double* residual_min);
 
 #ifdef __cplusplus
 }

@@ -833,3 +833,128 @@ double dox_advect_max_time_step(size_t n, const uint32_t* slot, const double* vx
     }
     return m;
 }
+
+/* ---- Poisson, tests/poisson/poisson_solve.hpp ------------------------- */
+
+/* multiplier of a cell's own factor for a neighbor in direction dir (and the
+ * transposed one, taken from the neighbor), poisson_solve.hpp:290-330,
+ * :430-470; f holds f_x_pos, f_x_neg, f_y_pos, f_y_neg, f_z_pos, f_z_neg */
+static int pf_index(int dir) { return dir > 0 ? 2 * (dir - 1) : 2 * (-dir - 1) + 1; }
+
+/* Poisson_Solve::solve iterations (poisson_solve.hpp:251-522) and
+ * initialize_solver (:976-1056) over the cached cell_info (:892-971).  Rank
+ * r's cell_info entries are [rank_begin[r], rank_begin[r+1]); per-rank
+ * partial sums are added in rank order (MPI_Allreduce SUM).  Ghost copies
+ * are the owners' values (every read happens right after the exchange the
+ * reference does).  nb_code = (dir + 3) | ((rel + 1) << 4). */
+long dox_poisson_solve(size_t n_info, const uint32_t* info_slot, int P, const size_t* rank_begin,
+                       const uint64_t* row, const uint32_t* nb_slot, const int32_t* nb_code,
+                       const double* type, const double* rhs, double* solution, double* best,
+                       double* p0, double* p1, double* r0, double* r1, double* adp0, const double* sf,
+                       const double* f /* 6 per slot */, unsigned max_iterations, unsigned min_iterations,
+                       double stop_residual, double p_of_norm, double stop_after_residual_increase,
+                       double* residual_min_out)
+{
+    double part[256];
+    if (P > 256) return -1;
+#define ALLREDUCE(expr_, cond_, out_)                                                            \
+    do {                                                                                         \
+        double tot_ = 0;                                                                         \
+        for (int r_ = 0; r_ < P; r_++) {                                                         \
+            part[r_] = 0;                                                                        \
+            for (size_t i = rank_begin[r_]; i < rank_begin[r_ + 1]; i++) {                       \
+                const uint32_t c = info_slot[i];                                                 \
+                (void)c;                                                                         \
+                if (cond_) part[r_] += (expr_);                                                  \
+            }                                                                                    \
+        }                                                                                        \
+        for (int r_ = 0; r_ < P; r_++) tot_ += part[r_];                                         \
+        out_ = tot_;                                                                             \
+    } while (0)
+    /* initialize_solver: r0 = rhs - A . solution; p0 = p1 = r1 = r0 */
+    for (size_t i = 0; i < n_info; i++) {
+        const uint32_t c = info_slot[i];
+        if (type[c] != 0) continue;
+        r0[c] = rhs[c] - sf[c] * solution[c];
+        for (uint64_t e = row[i]; e < row[i + 1]; e++) {
+            const int dir = (nb_code[e] & 15) - 3, rel = (nb_code[e] >> 4) - 1;
+            double m = f[6 * c + pf_index(dir)];
+            if (rel > 0) m /= 4.0;
+            r0[c] -= m * solution[nb_slot[e]];
+        }
+        p0[c] = p1[c] = r1[c] = r0[c];
+    }
+    double dot_r_g;
+    ALLREDUCE(r0[c] * r1[c], type[c] == 0, dot_r_g);
+    double residual_min = DBL_MAX;
+    size_t iteration = 0;
+    do {
+        iteration++;
+        for (size_t i = 0; i < n_info; i++) {  /* A . p0 */
+            const uint32_t c = info_slot[i];
+            if (type[c] != 0) continue;
+            adp0[c] = sf[c] * p0[c];
+            for (uint64_t e = row[i]; e < row[i + 1]; e++) {
+                const int dir = (nb_code[e] & 15) - 3, rel = (nb_code[e] >> 4) - 1;
+                double m = f[6 * c + pf_index(dir)];
+                if (rel > 0) m /= 4.0;
+                adp0[c] += m * p0[nb_slot[e]];
+            }
+        }
+        double dot_p_g;
+        ALLREDUCE(p1[c] * adp0[c], type[c] == 0, dot_p_g);
+        if (dot_p_g == 0) break;
+        const double alpha = dot_r_g / dot_p_g;
+        for (size_t i = 0; i < n_info; i++) {
+            const uint32_t c = info_slot[i];
+            if (type[c] == 0) solution[c] += alpha * p0[c];
+        }
+        double residual; /* get_residual, :684-697 (all cell_info cells) */
+        ALLREDUCE(pow(fabs(r0[c]), p_of_norm), 1, residual);
+        residual = pow(residual, 1.0 / p_of_norm);
+        if (residual_min > residual) {
+            residual_min = residual;
+            for (size_t i = 0; i < n_info; i++) {
+                const uint32_t c = info_slot[i];
+                if (type[c] == 0) best[c] = solution[c];
+            }
+        }
+        if (residual <= stop_residual && iteration >= min_iterations) break;
+        if (residual >= stop_after_residual_increase * residual_min && iteration >= min_iterations) break;
+        for (size_t i = 0; i < n_info; i++) {
+            const uint32_t c = info_slot[i];
+            if (type[c] == 0) r0[c] -= alpha * adp0[c];
+        }
+        for (size_t i = 0; i < n_info; i++) {  /* r1 -= alpha * transpose(A) . p1 */
+            const uint32_t c = info_slot[i];
+            if (type[c] != 0) continue;
+            double a = sf[c] * p1[c];
+            for (uint64_t e = row[i]; e < row[i + 1]; e++) {
+                const int dir = (nb_code[e] & 15) - 3, rel = (nb_code[e] >> 4) - 1;
+                const uint32_t nb = nb_slot[e];
+                double m = f[6 * nb + pf_index(-dir)];
+                if (rel > 0) m /= 4.0;
+                a += m * p1[nb];
+            }
+            r1[c] -= alpha * a;
+        }
+        if (dot_r_g == 0) break;
+        const double old = dot_r_g;
+        ALLREDUCE(r0[c] * r1[c], type[c] == 0, dot_r_g);
+        const double beta = dot_r_g / old;
+        for (size_t i = 0; i < n_info; i++) {
+            const uint32_t c = info_slot[i];
+            if (type[c] == 0) {
+                p0[c] = r0[c] + beta * p0[c];
+                p1[c] = r1[c] + beta * p1[c];
+            }
+        }
+    } while (iteration < max_iterations);
+#undef ALLREDUCE
+    for (size_t i = 0; i < n_info; i++) {
+        const uint32_t c = info_slot[i];
+        if (type[c] == 0) solution[c] = best[c];
+    }
+    *residual_min_out = residual_min;
+    return (long)iteration;
+}

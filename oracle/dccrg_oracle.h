@@ -114,6 +114,16 @@ void dox_advect_apply(size_t n, const uint32_t* slot, double* density, double* f
 double dox_advect_max_time_step(size_t n, const uint32_t* slot, const double* vx, const double* vy,
                                 const double* vz, const double* lx, const double* ly, const double* lz);
 
+/* ---- Poisson BiCG, tests/poisson/poisson_solve.hpp:251-522 + 976-1056.
+ * Returns the iteration count; nb_code = (dir + 3) | ((rel + 1) << 4). */
+long dox_poisson_solve(size_t n_info, const uint32_t* info_slot, int P, const size_t* rank_begin,
+                       const uint64_t* row, const uint32_t* nb_slot, const int32_t* nb_code,
+                       const double* type, const double* rhs, double* solution, double* best,
+                       double* p0, double* p1, double* r0, double* r1, double* adp0, const double* sf,
+                       const double* f, unsigned max_iterations, unsigned min_iterations,
+                       double stop_residual, double p_of_norm, double stop_after_residual_increase,
+                       double* residual_min_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -99,6 +99,9 @@ def lib():
         L.dox_advect_apply.argtypes = [C.c_size_t, u32p, f64p, f64p]
         L.dox_advect_max_time_step.restype = C.c_double
         L.dox_advect_max_time_step.argtypes = [C.c_size_t, u32p] + [f64p] * 6
+        L.dox_poisson_solve.restype = C.c_long
+        L.dox_poisson_solve.argtypes = [C.c_size_t, u32p, C.c_int, C.POINTER(C.c_size_t), u64p, u32p, i32p] + \
+            [f64p] * 11 + [C.c_uint, C.c_uint, C.c_double, C.c_double, C.c_double, f64p]
         _lib = L
     return _lib
 
@@ -524,3 +527,125 @@ class AdvectionLists:
         return min(lib().dox_advect_max_time_step(len(R["local"]), _p(R["local"], C.c_uint32), _p(vx, f64),
                                                   _p(vy, f64), _p(vz, f64), _p(lx, f64), _p(ly, f64),
                                                   _p(lz, f64)) for R in self.ranks)
+
+
+# ---- Poisson (tests/poisson/poisson_solve.hpp) -------------------------------
+POISSON_SOLVE, POISSON_BOUNDARY, POISSON_SKIP = 0.0, 1.0, 2.0  # :160-165
+
+
+class PoissonSystem:
+    """Poisson_Solve's cached system (cache_system_info, poisson_solve.hpp:
+    827-971, set_scaling_factor :704-821) on every rank of a block-partitioned
+    grid, and solve() via the C restatement.  Slots = positions in
+    ``grid.cells()``.  ``lengths`` = (lx, ly, lz) slot arrays (the geometry's
+    get_length).  Cell order within a rank: ascending id (the reference's
+    get_cells() order is its hash order; only sums' order depends on it)."""
+
+    def __init__(self, grid: "Grid", comm_size: int, lengths, solve_cells=None, skip_cells=()):
+        self.cells = [int(c) for c in grid.cells()]
+        pos = {c: i for i, c in enumerate(self.cells)}
+        n = len(self.cells)
+        m = grid.mapping
+        solve = set(self.cells if solve_cells is None else solve_cells)
+        skip = set(skip_cells) - solve
+        owner = [grid.owner(c, comm_size) for c in self.cells]
+        self.type = np.full(n, POISSON_BOUNDARY)
+        for c in skip:
+            self.type[pos[c]] = POISSON_SKIP
+        for c in solve:
+            self.type[pos[c]] = POISSON_SOLVE
+        lx, ly, lz = (np.asarray(a, dtype=np.float64) for a in lengths)
+        self.f = np.zeros((n, 6))
+        self.sf = np.zeros(n)
+        info, row, nb, code, rank_begin = [], [0], [], [], [0]
+        for r in range(comm_size):
+            for c in self.cells:
+                i = pos[c]
+                if owner[i] != r or self.type[i] == POISSON_SKIP:
+                    continue
+                lvl = m.get_refinement_level(c)
+                kept = []
+                for nbr, d in grid.face_neighbors_of(c):
+                    j = pos[nbr]
+                    if self.type[j] == POISSON_SKIP:
+                        continue
+                    if self.type[i] == POISSON_BOUNDARY and self.type[j] == POISSON_BOUNDARY:
+                        continue
+                    nl = m.get_refinement_level(nbr)
+                    rel = 1 if nl > lvl else (-1 if nl < lvl else 0)
+                    kept.append((j, d, rel))
+                if not kept:
+                    self.type[i] = POISSON_SKIP
+                    continue
+                self._scaling(i, kept, lx, ly, lz)
+                info.append(i)
+                for j, d, rel in kept:
+                    nb.append(j)
+                    code.append((d + 3) | ((rel + 1) << 4))
+                row.append(len(nb))
+            rank_begin.append(len(info))
+        self.info = np.array(info, dtype=np.uint32)
+        self.row = np.array(row, dtype=np.uint64)
+        self.nb = np.array(nb or [0], dtype=np.uint32)
+        self.code = np.array(code or [0], dtype=np.int32)
+        self.rank_begin = np.array(rank_begin, dtype=np.uintp)
+        self.P = comm_size
+
+    def _scaling(self, i, kept, lx, ly, lz):
+        """set_scaling_factor, poisson_solve.hpp:704-821."""
+        hx, hy, hz = lx[i] / 2.0, ly[i] / 2.0, lz[i] / 2.0
+        pos_x, neg_x = +2 * hx, -2 * hx
+        pos_y, neg_y = +2 * hy, -2 * hy
+        pos_z, neg_z = +2 * hz, -2 * hz
+        for j, d, _ in kept:
+            nx, ny, nz = lx[j] / 2.0, ly[j] / 2.0, lz[j] / 2.0
+            if d == 1:
+                pos_x = hx + nx
+            elif d == -1:
+                neg_x = -1.0 * (hx + nx)
+            elif d == 2:
+                pos_y = hy + ny
+            elif d == -2:
+                neg_y = -1.0 * (hy + ny)
+            elif d == 3:
+                pos_z = hz + nz
+            else:
+                neg_z = -1.0 * (hz + nz)
+        tx, ty, tz = pos_x - neg_x, pos_y - neg_y, pos_z - neg_z
+        f = [0.0] * 6
+        for _, d, _ in kept:
+            if d == 1:
+                f[0] = +2.0 / (pos_x * tx)
+            elif d == -1:
+                f[1] = -2.0 / (neg_x * tx)
+            elif d == 2:
+                f[2] = +2.0 / (pos_y * ty)
+            elif d == -2:
+                f[3] = -2.0 / (neg_y * ty)
+            elif d == 3:
+                f[4] = +2.0 / (pos_z * tz)
+            else:
+                f[5] = -2.0 / (neg_z * tz)
+        self.f[i] = f
+        self.sf[i] = -f[0] - f[1] - f[2] - f[3] - f[4] - f[5]
+
+    def solve(self, rhs, solution, max_iterations=1000, min_iterations=0, stop_residual=1e-15,
+              p_of_norm=2.0, stop_after_residual_increase=10.0):
+        """Poisson_Solve::solve (:251-522).  Returns (solution, iterations,
+        minimum residual); ``solution`` holds the initial guess."""
+        n = len(self.cells)
+        f64 = C.c_double
+        sol = np.ascontiguousarray(solution, dtype=np.float64).copy()
+        rhs = np.ascontiguousarray(rhs, dtype=np.float64)
+        work = [np.zeros(n) for _ in range(7)]  # best, p0, p1, r0, r1, adp0
+        res = C.c_double()
+        f = np.ascontiguousarray(self.f)
+        it = lib().dox_poisson_solve(
+            len(self.info), _p(self.info, C.c_uint32), self.P,
+            self.rank_begin.ctypes.data_as(C.POINTER(C.c_size_t)), _p(self.row, C.c_uint64),
+            _p(self.nb, C.c_uint32), _p(self.code, C.c_int32), _p(self.type, f64), _p(rhs, f64), _p(sol, f64),
+            *[_p(w, f64) for w in work[:6]], _p(self.sf, f64), _p(f, f64), max_iterations, min_iterations,
+            stop_residual, p_of_norm, stop_after_residual_increase, C.byref(res))
+        if it < 0:
+            raise RuntimeError("dox_poisson_solve failed")
+        return sol, int(it), res.value
