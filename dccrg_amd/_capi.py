@@ -112,6 +112,11 @@ SIGNATURES = {
     "dccrgx_field_write_local": (C.c_int, [_vp, C.c_int32, _vp, C.c_size_t]),
     "dccrgx_field_read_local": (C.c_int, [_vp, C.c_int32, _vp, C.c_size_t]),
     "dccrgx_field_read_remote": (C.c_int, [_vp, C.c_int32, C.c_int32, _vp, C.c_size_t]),
+    "dccrgx_field_create_variable": (C.c_int, [_vp, C.c_uint32, _i32p]),
+    "dccrgx_field_resize": (C.c_int, [_vp, C.c_int32, _u64p, C.POINTER(C.c_uint32), C.c_size_t]),
+    "dccrgx_field_get_counts": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, C.POINTER(C.c_uint32)]),
+    "dccrgx_field_write_cells": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _vp, C.c_size_t]),
+    "dccrgx_field_read_cells": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _vp, C.c_size_t, _szp]),
     "dccrgx_halo_start": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t]),
     "dccrgx_halo_wait": (C.c_int, [_vp, C.c_int32, C.c_int32]),
     "dccrgx_halo_update": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t]),

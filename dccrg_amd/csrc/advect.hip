@@ -193,7 +193,8 @@ int adv_ptrs(const dccrgx_grid* grid, const dccrgx_advect_fields* f, AdvPtrs* p)
     const int32_t ids[8] = {f->density, f->flux, f->vx, f->vy, f->vz, f->length_x, f->length_y, f->length_z};
     for (int i = 0; i < 8; i++) {
         DX_CHECK(ids[i] >= 0 && (size_t)ids[i] < grid->fields.size(), DCCRGX_EINVAL, "bad field %d", ids[i]);
-        DX_CHECK(grid->fields[ids[i]].elem == 8, DCCRGX_EINVAL, "advection fields are f64 (field %d)", ids[i]);
+        DX_CHECK(grid->fields[ids[i]].elem == 8 && !grid->fields[ids[i]].variable, DCCRGX_EINVAL,
+                 "advection fields are f64 (field %d)", ids[i]);
     }
     DX_CHECK(f->density != f->flux, DCCRGX_EINVAL, "density and flux must be distinct fields");
     auto P = [&](int32_t id) { return (double*)grid->fields[id].ptr; };

@@ -626,6 +626,10 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
         if (!ss.empty()) DX_TRY(upload(ss, &pp.d_send_slots, st));
         if (!rd.empty()) DX_TRY(upload(rd, &pp.d_unpack_dst, st));
         pp.n_unpack = rd.size();
+        pp.h_send_slots = ss;
+        pp.h_unpack_dst = rd;
+        pp.h_unpack_src.resize(rd.size());
+        for (size_t i = 0; i < rd.size(); i++) pp.h_unpack_src[i] = i;
         h.peers.push_back(std::move(pp));
     }
     std::vector<uint32_t> all(nl);
@@ -659,6 +663,13 @@ int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, ui
     DX_CHECK(cap >= *n && (ids || !*n), DCCRGX_ERANGE, "capacity");
     std::copy(v->begin(), v->end(), ids);
     return DCCRGX_OK;
+}
+
+int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id)
+{
+    const auto& L = grid->ex->leaves;
+    auto it = std::lower_bound(L.begin(), L.end(), id);
+    return (it != L.end() && *it == id) ? (int64_t)(it - L.begin()) : -1;
 }
 
 int explicit_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int64_t* slots, hipStream_t st)

@@ -881,7 +881,8 @@ static int gol_fields(dccrgx_grid* grid, int32_t a, int32_t b, int32_t c)
     const int32_t f[3] = {a, b, c};
     for (int i = 0; i < 3; i++) {
         DX_CHECK(f[i] >= 0 && (size_t)f[i] < grid->fields.size(), DCCRGX_EINVAL, "bad field %d", f[i]);
-        DX_CHECK(grid->fields[f[i]].elem == 4, DCCRGX_EINVAL, "game of life fields are 4-byte");
+        DX_CHECK(grid->fields[f[i]].elem == 4 && !grid->fields[f[i]].variable, DCCRGX_EINVAL,
+                 "game of life fields are 4-byte");
     }
     DX_CHECK(a != b && a != c && b != c, DCCRGX_EINVAL, "fields must be distinct (double buffered)");
     return DCCRGX_OK;

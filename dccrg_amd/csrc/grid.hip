@@ -432,6 +432,7 @@ int build_hood(dccrgx_grid* grid, Hood& h)
             if (slots[i] != slots[0] + i) pp.send_direct = false;
         pp.send_slot0 = slots[0];
         if (!pp.send_direct) DX_TRY(upload(slots, &pp.d_send_slots, st));
+        pp.h_send_slots = std::move(slots);
     }
 
     // pad plan over all non-local storage slots
@@ -494,6 +495,12 @@ int build_hood(dccrgx_grid* grid, Hood& h)
             if (u[i].first != i || u[i].second != u[0].second + i) pp.recv_direct = false;
         DX_CHECK(pp.recv_ids.empty() || !u.empty(), DCCRGX_EINTERNAL,
                  "received cells of peer %d have no ghost slot", pp.peer);
+        pp.h_unpack_dst.clear();
+        pp.h_unpack_src.clear();
+        for (auto& e : u) {
+            pp.h_unpack_src.push_back(e.first);
+            pp.h_unpack_dst.push_back(e.second);
+        }
         if (pp.recv_direct) {
             pp.recv_slot0 = u[0].second;
         } else {
@@ -507,6 +514,7 @@ int build_hood(dccrgx_grid* grid, Hood& h)
             DX_TRY(upload(src, &pp.d_unpack_src, st));
         }
     }
+    h.h_self = self;
     // self copies: contiguous runs become memcpys when there are few of them
     std::vector<CopySeg> segs;
     for (auto& e : self) {

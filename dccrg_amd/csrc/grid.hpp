@@ -81,6 +81,13 @@ __host__ __device__ inline uint64_t ug_slot(const UGeom& g, int64_t a, int64_t b
 struct Field {
     void* ptr = nullptr;
     uint32_t elem = 0;
+    // variable-size cell data (tests/variable_data_size): `ptr` is a pool,
+    // slot s holds count[s] elements at byte offset off[s] (host mirrors;
+    // message sizes are computed from them)
+    bool variable = false;
+    std::vector<uint32_t> count;
+    std::vector<uint64_t> off;
+    size_t pool_bytes = 0;
 };
 
 struct PeerPlan {
@@ -97,6 +104,11 @@ struct PeerPlan {
     uint64_t n_unpack = 0;             // (dst slot, message index) pairs otherwise
     uint64_t* d_unpack_dst = nullptr;
     uint64_t* d_unpack_src = nullptr;
+    // host copies of the plans (variable-size fields build byte segments
+    // from them): slot of each sent cell; (dst slot, message index) of every
+    // ghost slot filled from this peer, direct receives included
+    std::vector<uint64_t> h_send_slots;
+    std::vector<uint64_t> h_unpack_dst, h_unpack_src;
     // staging (allocated on first use, grown as needed)
     void* d_send_buf = nullptr;
     size_t send_buf_bytes = 0;
@@ -128,6 +140,7 @@ struct Hood {
     uint64_t n_self_scatter = 0;     // non-contiguous remainder (kernel)
     uint64_t* d_self_dst = nullptr;
     uint64_t* d_self_src = nullptr;
+    std::vector<std::pair<uint64_t, uint64_t>> h_self;  // all (dst, src) self copies
     // slice ranges for the overlap split (storage slice indices, inclusive-exclusive)
     int64_t inner_s0 = 0, inner_s1 = 0;  // fully local and only local reads
     bool pending = false;                // halo started, not waited

@@ -102,6 +102,75 @@ static int check_fields(const dccrgx_grid* g, const int32_t* f, size_t nf, size_
     return DCCRGX_OK;
 }
 
+// ---- variable-size fields: byte segments ------------------------------------
+struct Seg {
+    uint64_t src, dst, len;  // byte offsets and length
+};
+
+// one wavefront per segment; 4-byte words when the segment allows it
+__global__ void __launch_bounds__(256) k_seg_copy(const Seg* __restrict__ segs, uint64_t n,
+                                                  const char* __restrict__ src, char* __restrict__ dst)
+{
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+    const uint64_t lane = threadIdx.x % 64;
+    const uint64_t waves = (uint64_t)gridDim.x * blockDim.x / 64;
+    for (uint64_t k = wave; k < n; k += waves) {
+        const Seg s = segs[k];
+        if (((s.src | s.dst | s.len) & 3) == 0) {
+            const uint32_t* a = (const uint32_t*)(src + s.src);
+            uint32_t* b = (uint32_t*)(dst + s.dst);
+            for (uint64_t i = lane; i < s.len / 4; i += 64) b[i] = a[i];
+        } else {
+            for (uint64_t i = lane; i < s.len; i += 64) dst[s.dst + i] = src[s.src + i];
+        }
+    }
+}
+
+static int seg_copy(const std::vector<Seg>& segs, const void* src, void* dst, hipStream_t st)
+{
+    if (segs.empty()) return DCCRGX_OK;
+    Seg* d = nullptr;
+    DX_HIP(hipMalloc(&d, segs.size() * sizeof(Seg)));
+    DX_HIP(hipMemcpyAsync(d, segs.data(), segs.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
+    const uint64_t blocks = std::min<uint64_t>((segs.size() + 3) / 4, 4096);
+    hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)blocks), dim3(256), 0, st, d, (uint64_t)segs.size(),
+                       (const char*)src, (char*)dst);
+    DX_HIP(hipGetLastError());
+    DX_HIP(hipStreamSynchronize(st));  // variable-size exchanges are not the bandwidth path
+    hipFree(d);
+    return DCCRGX_OK;
+}
+
+// first ghost slot of each message cell of peer p
+static std::vector<int64_t> first_dst(const PeerPlan& p)
+{
+    std::vector<int64_t> first(p.recv_ids.size(), -1);
+    for (size_t k = 0; k < p.h_unpack_src.size(); k++)
+        if (first[p.h_unpack_src[k]] < 0) first[p.h_unpack_src[k]] = (int64_t)p.h_unpack_dst[k];
+    return first;
+}
+
+// bytes field F contributes to the message to (send) or from (recv) peer p
+static size_t field_bytes(const Field& F, const PeerPlan& p, bool send)
+{
+    if (!F.variable) return (send ? p.send_ids.size() : p.recv_ids.size()) * F.elem;
+    size_t b = 0;
+    if (send) {
+        for (uint64_t s : p.h_send_slots) b += (size_t)F.count[s] * F.elem;
+    } else {
+        for (int64_t s : first_dst(p))
+            if (s >= 0) b += (size_t)F.count[s] * F.elem;
+    }
+    return b;
+}
+
+static size_t message_bytes(const dccrgx_grid* g, const PeerPlan& p, const int32_t* f, size_t nf, bool send)
+{
+    size_t b = 0;
+    for (size_t i = 0; i < nf; i++) b += field_bytes(g->fields[f[i]], p, send);
+    return b;
+}
+
 static int ensure(void** p, size_t* have, size_t need)
 {
     if (*have >= need) return DCCRGX_OK;
@@ -118,6 +187,14 @@ static int self_copy(dccrgx_grid* g, const Hood& h, const int32_t* f, size_t nf,
 {
     for (size_t i = 0; i < nf; i++) {
         const Field& F = g->fields[f[i]];
+        if (F.variable) {
+            std::vector<Seg> segs;
+            for (auto& e : h.h_self)
+                if (F.count[e.second])
+                    segs.push_back({F.off[e.second], F.off[e.first], (uint64_t)F.count[e.second] * F.elem});
+            DX_TRY(seg_copy(segs, F.ptr, F.ptr, st));
+            continue;
+        }
         for (const CopySeg& s : h.self_segs)
             DX_HIP(hipMemcpyAsync((char*)F.ptr + s.dst * F.elem, (char*)F.ptr + s.src * F.elem,
                                   s.n * F.elem, hipMemcpyDeviceToDevice, st));
@@ -135,6 +212,18 @@ static int pack_peer(dccrgx_grid* g, PeerPlan& p, const int32_t* f, size_t nf, v
     for (size_t i = 0; i < nf; i++) {
         const Field& F = g->fields[f[i]];
         char* d = (char*)dst + off;
+        if (F.variable) {  // cells ascending, each its count[] elements
+            std::vector<Seg> segs;
+            uint64_t o = 0;
+            for (uint64_t s : p.h_send_slots) {
+                const uint64_t len = (uint64_t)F.count[s] * F.elem;
+                if (len) segs.push_back({F.off[s], off + o, len});
+                o += len;
+            }
+            DX_TRY(seg_copy(segs, F.ptr, dst, st));
+            off += o;
+            continue;
+        }
         if (p.send_direct)
             DX_HIP(hipMemcpyAsync(d, (char*)F.ptr + p.send_slot0 * F.elem, n * F.elem,
                                   hipMemcpyDeviceToDevice, st));
@@ -153,6 +242,21 @@ static int unpack_peer(dccrgx_grid* g, PeerPlan& p, const int32_t* f, size_t nf,
     for (size_t i = 0; i < nf; i++) {
         const Field& F = g->fields[f[i]];
         const char* s = (const char*)src + off;
+        if (F.variable) {  // message cell j has the count of its ghost slots (pre-sized by the caller)
+            const std::vector<int64_t> first = first_dst(p);
+            std::vector<uint64_t> pre(n + 1, 0);
+            for (uint64_t j = 0; j < n; j++)
+                pre[j + 1] = pre[j] + (first[j] >= 0 ? (uint64_t)F.count[first[j]] * F.elem : 0);
+            std::vector<Seg> segs;
+            for (size_t k = 0; k < p.h_unpack_dst.size(); k++) {
+                const uint64_t d = p.h_unpack_dst[k], j = p.h_unpack_src[k];
+                const uint64_t len = std::min<uint64_t>((uint64_t)F.count[d] * F.elem, pre[j + 1] - pre[j]);
+                if (len) segs.push_back({off + pre[j], F.off[d], len});
+            }
+            DX_TRY(seg_copy(segs, src, F.ptr, st));
+            off += pre[n];
+            continue;
+        }
         if (p.recv_direct)
             DX_HIP(hipMemcpyAsync((char*)F.ptr + p.recv_slot0 * F.elem, s, n * F.elem,
                                   hipMemcpyDeviceToDevice, st));
@@ -200,11 +304,50 @@ __global__ void __launch_bounds__(256) k_slots_of(UGeom g, const uint64_t* __res
 
 int explicit_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int64_t* slots,
                       hipStream_t st);
+int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id);
+
+// every storage slot holding cell `id` (a uniform grid's periodic images in
+// the pad slices included), ascending
+static void slots_holding(const dccrgx_grid* grid, uint64_t id, std::vector<uint64_t>& out)
+{
+    out.clear();
+    if (!grid->uniform) {
+        const int64_t s = explicit_host_slot(grid, id);
+        if (s >= 0) out.push_back((uint64_t)s);
+        return;
+    }
+    const UGeom& g = grid->g;
+    if (id < 1 || id > g.N) return;
+    const uint64_t lin = id - 1, c = lin / g.S, rem = lin - c * g.S;
+    const int64_t c0 = g.cbase, c1 = g.cbase + (int64_t)g.nslices, LC = (int64_t)g.LC;
+    int64_t cu = (int64_t)c;
+    if (g.perC) {
+        if (cu < c0) cu += ((c0 - cu + LC - 1) / LC) * LC;
+        else cu -= ((cu - c0) / LC) * LC;
+    }
+    for (; cu < c1; cu += LC) {
+        if (cu >= c0) out.push_back(rem + g.S * (uint64_t)(cu - c0));
+        if (!g.perC) break;
+    }
+}
+
+// the slot read and written for a cell: its own slot if local, else its
+// first ghost copy; -1 if this rank stores no copy
+static int64_t primary_slot(const dccrgx_grid* grid, uint64_t id)
+{
+    if (!grid->uniform) return explicit_host_slot(grid, id);
+    const UGeom& g = grid->g;
+    if (id < 1 || id > g.N) return -1;
+    if (ug_local(g, id - 1)) return (int64_t)(id - 1 + (uint64_t)(-g.cbase * (int64_t)g.S));
+    return ghost_slot(g, id - 1);
+}
 
 static int halo_finish(dccrgx_grid* grid, Hood& h, const int32_t* f, size_t nf)
 {
+    bool var = false;
+    for (size_t i = 0; i < nf; i++) var |= grid->fields[f[i]].variable;
     for (PeerPlan& p : h.peers)
-        if (!p.recv_direct && !p.recv_ids.empty())
+        if ((var || !p.recv_direct) && !p.recv_ids.empty())
             DX_TRY(unpack_peer(grid, p, f, nf, p.d_recv_buf, grid->ctx->compute));
     return DCCRGX_OK;
 }
@@ -262,6 +405,7 @@ static uint64_t local_slot0(const dccrgx_grid* grid)
 int dccrgx_field_write_local(dccrgx_grid* grid, int32_t fid, const void* host, size_t n)
 {
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    DX_CHECK(!grid->fields[fid].variable, DCCRGX_EINVAL, "variable-size field: use dccrgx_field_write_cells");
     DX_CHECK(n == grid->n_local && (host || !n), DCCRGX_EINVAL, "expected %llu local values",
              (unsigned long long)grid->n_local);
     if (!n) return DCCRGX_OK;
@@ -276,6 +420,7 @@ int dccrgx_field_write_local(dccrgx_grid* grid, int32_t fid, const void* host, s
 int dccrgx_field_read_local(const dccrgx_grid* grid, int32_t fid, void* host, size_t n)
 {
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    DX_CHECK(!grid->fields[fid].variable, DCCRGX_EINVAL, "variable-size field: use dccrgx_field_read_cells");
     DX_CHECK(n == grid->n_local && (host || !n), DCCRGX_EINVAL, "expected %llu local values",
              (unsigned long long)grid->n_local);
     if (!n) return DCCRGX_OK;
@@ -291,6 +436,7 @@ int dccrgx_field_read_remote(const dccrgx_grid* grid, int32_t hood_id, int32_t f
                              size_t n)
 {
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    DX_CHECK(!grid->fields[fid].variable, DCCRGX_EINVAL, "variable-size field: use dccrgx_field_read_cells");
     const Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     DX_CHECK(n == h->remote.size() && (host || !n), DCCRGX_EINVAL, "expected %zu remote values",
@@ -343,13 +489,15 @@ int dccrgx_halo_start(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size
     // the comm stream starts after everything queued so far on the compute stream
     DX_HIP(hipEventRecord(c->ev_compute, c->compute));
     DX_HIP(hipStreamWaitEvent(c->comm, c->ev_compute, 0));
+    bool var = false;
+    for (size_t i = 0; i < nf; i++) var |= grid->fields[f[i]].variable;
     for (PeerPlan& p : h->peers) {
-        if (!p.send_direct && !p.send_ids.empty()) {
-            DX_TRY(ensure(&p.d_send_buf, &p.send_buf_bytes, p.send_ids.size() * bpc));
+        if ((var || !p.send_direct) && !p.send_ids.empty()) {
+            DX_TRY(ensure(&p.d_send_buf, &p.send_buf_bytes, std::max<size_t>(message_bytes(grid, p, f, nf, true), 1)));
             DX_TRY(pack_peer(grid, p, f, nf, p.d_send_buf, c->comm));
         }
-        if (!p.recv_direct && !p.recv_ids.empty())
-            DX_TRY(ensure(&p.d_recv_buf, &p.recv_buf_bytes, p.recv_ids.size() * bpc));
+        if ((var || !p.recv_direct) && !p.recv_ids.empty())
+            DX_TRY(ensure(&p.d_recv_buf, &p.recv_buf_bytes, std::max<size_t>(message_bytes(grid, p, f, nf, false), 1)));
     }
     // grouped point-to-point: one message per field per peer (xGMI links are
     // point-to-point; z-slab peers are the ring neighbours)
@@ -358,15 +506,15 @@ int dccrgx_halo_start(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size
         size_t soff = 0, roff = 0;
         for (size_t i = 0; i < nf; i++) {
             const Field& F = grid->fields[f[i]];
-            const size_t sb = p.send_ids.size() * F.elem, rb = p.recv_ids.size() * F.elem;
+            const size_t sb = field_bytes(F, p, true), rb = field_bytes(F, p, false);
             if (sb) {
-                const void* src = p.send_direct ? (const char*)F.ptr + p.send_slot0 * F.elem
-                                                : (const char*)p.d_send_buf + soff;
+                const void* src = p.send_direct && !var ? (const char*)F.ptr + p.send_slot0 * F.elem
+                                                        : (const char*)p.d_send_buf + soff;
                 DX_RCCL(ncclSend(src, sb, ncclUint8, p.peer, c->nccl, c->comm));
             }
             if (rb) {
-                void* dst = p.recv_direct ? (char*)F.ptr + p.recv_slot0 * F.elem
-                                          : (char*)p.d_recv_buf + roff;
+                void* dst = p.recv_direct && !var ? (char*)F.ptr + p.recv_slot0 * F.elem
+                                                  : (char*)p.d_recv_buf + roff;
                 DX_RCCL(ncclRecv(dst, rb, ncclUint8, p.peer, c->nccl, c->comm));
             }
             soff += sb;
@@ -472,7 +620,7 @@ int dccrgx_halo_pack_to(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, si
     *bytes = 0;
     for (PeerPlan& p : h->peers) {
         if (p.peer != peer) continue;
-        *bytes = p.send_ids.size() * bpc;
+        *bytes = message_bytes(grid, p, f, nf, true);
         DX_CHECK(cap >= *bytes, DCCRGX_ERANGE, "capacity %zu < %zu", cap, *bytes);
         DX_TRY(pack_peer(grid, p, f, nf, dst, grid->ctx->compute));
     }
@@ -489,13 +637,146 @@ int dccrgx_halo_unpack_from(dccrgx_grid* grid, int32_t hood_id, const int32_t* f
     DX_TRY(check_fields(grid, f, nf, &bpc));
     for (PeerPlan& p : h->peers) {
         if (p.peer != peer) continue;
-        DX_CHECK(bytes == p.recv_ids.size() * bpc, DCCRGX_EINVAL, "message is %zu bytes, expected %zu",
-                 bytes, p.recv_ids.size() * bpc);
+        const size_t want = message_bytes(grid, p, f, nf, false);
+        DX_CHECK(bytes == want, DCCRGX_EINVAL, "message is %zu bytes, expected %zu", bytes, want);
         DX_TRY(unpack_peer(grid, p, f, nf, src, grid->ctx->compute));
         return DCCRGX_OK;
     }
     DX_CHECK(bytes == 0, DCCRGX_EINVAL, "no receives from peer %d", peer);
     return DCCRGX_OK;
+}
+
+// ---- variable-size cell data and cell-addressed access -----------------------
+
+int dccrgx_field_create_variable(dccrgx_grid* grid, uint32_t elem, int32_t* fid)
+{
+    DX_CHECK(grid && fid && elem > 0, DCCRGX_EINVAL, "bad argument");
+    Field F;
+    F.elem = elem;
+    F.variable = true;
+    F.count.assign(grid->n_slots, 0);
+    F.off.assign(grid->n_slots, 0);
+    F.pool_bytes = 0;
+    DX_HIP(hipMalloc(&F.ptr, 16));
+    grid->fields.push_back(std::move(F));
+    *fid = (int32_t)grid->fields.size() - 1;
+    return DCCRGX_OK;
+}
+
+int dccrgx_field_resize(dccrgx_grid* grid, int32_t fid, const uint64_t* ids, const uint32_t* counts, size_t n)
+{
+    DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    DX_CHECK((ids && counts) || !n, DCCRGX_EINVAL, "null argument");
+    Field& F = grid->fields[fid];
+    DX_CHECK(F.variable, DCCRGX_EINVAL, "field %d has a fixed size per cell", fid);
+    std::vector<uint32_t> cnt = F.count;
+    std::vector<uint64_t> s;
+    for (size_t i = 0; i < n; i++) {
+        slots_holding(grid, ids[i], s);
+        DX_CHECK(!s.empty(), DCCRGX_ENOTFOUND, "cell %llu is neither local nor a ghost here",
+                 (unsigned long long)ids[i]);
+        for (uint64_t x : s) cnt[x] = counts[i];
+    }
+    std::vector<uint64_t> off(cnt.size());
+    uint64_t tot = 0;
+    for (size_t k = 0; k < cnt.size(); k++) {
+        off[k] = tot;
+        tot += (uint64_t)cnt[k] * F.elem;
+        tot = (tot + 7) & ~7ull;  // 8-byte aligned cells
+    }
+    hipStream_t st = grid->ctx->compute;
+    void* pool = nullptr;
+    DX_HIP(hipMalloc(&pool, std::max<uint64_t>(tot, 16)));
+    DX_HIP(hipMemsetAsync(pool, 0, std::max<uint64_t>(tot, 16), st));  // new elements value-initialised
+    std::vector<Seg> keep;
+    for (size_t k = 0; k < cnt.size(); k++) {
+        const uint64_t len = (uint64_t)std::min(cnt[k], F.count[k]) * F.elem;
+        if (len) keep.push_back({F.off[k], off[k], len});
+    }
+    DX_TRY(seg_copy(keep, F.ptr, pool, st));
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(F.ptr);
+    F.ptr = pool;
+    F.pool_bytes = tot;
+    F.count.swap(cnt);
+    F.off.swap(off);
+    return DCCRGX_OK;
+}
+
+int dccrgx_field_get_counts(const dccrgx_grid* grid, int32_t fid, const uint64_t* ids, size_t n, uint32_t* counts)
+{
+    DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    DX_CHECK((ids && counts) || !n, DCCRGX_EINVAL, "null argument");
+    const Field& F = grid->fields[fid];
+    for (size_t i = 0; i < n; i++) {
+        const int64_t s = primary_slot(grid, ids[i]);
+        DX_CHECK(s >= 0, DCCRGX_ENOTFOUND, "cell %llu is neither local nor a ghost here", (unsigned long long)ids[i]);
+        counts[i] = F.variable ? F.count[s] : 1;
+    }
+    return DCCRGX_OK;
+}
+
+// segments between a packed host-order buffer and the cells' storage
+static int cell_segments(const dccrgx_grid* grid, const Field& F, const uint64_t* ids, size_t n, bool to_cells,
+                         std::vector<Seg>& segs, uint64_t* total)
+{
+    uint64_t o = 0;
+    for (size_t i = 0; i < n; i++) {
+        const int64_t s = primary_slot(grid, ids[i]);
+        DX_CHECK(s >= 0, DCCRGX_ENOTFOUND, "cell %llu is neither local nor a ghost here", (unsigned long long)ids[i]);
+        const uint64_t len = F.variable ? (uint64_t)F.count[s] * F.elem : F.elem;
+        const uint64_t at = F.variable ? F.off[s] : (uint64_t)s * F.elem;
+        if (len) segs.push_back(to_cells ? Seg{o, at, len} : Seg{at, o, len});
+        o += len;
+    }
+    *total = o;
+    return DCCRGX_OK;
+}
+
+int dccrgx_field_write_cells(dccrgx_grid* grid, int32_t fid, const uint64_t* ids, size_t n, const void* data,
+                             size_t bytes)
+{
+    DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    DX_CHECK(ids || !n, DCCRGX_EINVAL, "null argument");
+    const Field& F = grid->fields[fid];
+    std::vector<Seg> segs;
+    uint64_t tot = 0;
+    DX_TRY(cell_segments(grid, F, ids, n, true, segs, &tot));
+    DX_CHECK(bytes == tot && (data || !tot), DCCRGX_EINVAL, "%zu bytes given, the cells hold %llu", bytes,
+             (unsigned long long)tot);
+    if (!tot) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    void* d = nullptr;
+    DX_HIP(hipMalloc(&d, tot));
+    DX_HIP(hipMemcpyAsync(d, data, tot, hipMemcpyHostToDevice, st));
+    const int s = seg_copy(segs, d, F.ptr, st);
+    hipFree(d);
+    return s;
+}
+
+int dccrgx_field_read_cells(const dccrgx_grid* grid, int32_t fid, const uint64_t* ids, size_t n, void* data,
+                            size_t cap, size_t* bytes)
+{
+    DX_CHECK(grid && bytes && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad argument");
+    DX_CHECK(ids || !n, DCCRGX_EINVAL, "null argument");
+    const Field& F = grid->fields[fid];
+    std::vector<Seg> segs;
+    uint64_t tot = 0;
+    DX_TRY(cell_segments(grid, F, ids, n, false, segs, &tot));
+    *bytes = tot;
+    if (!data) return DCCRGX_OK;  // size query
+    DX_CHECK(cap >= tot, DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)tot);
+    if (!tot) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    void* d = nullptr;
+    DX_HIP(hipMalloc(&d, tot));
+    int s = seg_copy(segs, F.ptr, d, st);
+    if (s == DCCRGX_OK) {
+        DX_HIP(hipMemcpyAsync(data, d, tot, hipMemcpyDeviceToHost, st));
+        DX_HIP(hipStreamSynchronize(st));
+    }
+    hipFree(d);
+    return s;
 }
 
 }  // extern "C"

@@ -718,7 +718,8 @@ int dccrgx_poisson_create(dccrgx_grid* grid, const dccrgx_poisson_params* prm, c
     const int32_t uf[5] = {f->rhs, f->solution, f->length_x, f->length_y, f->length_z};
     for (int32_t id : uf) {
         DX_CHECK(id >= 0 && (size_t)id < grid->fields.size(), DCCRGX_EINVAL, "bad field %d", id);
-        DX_CHECK(grid->fields[id].elem == 8, DCCRGX_EINVAL, "Poisson fields are f64 (field %d)", id);
+        DX_CHECK(grid->fields[id].elem == 8 && !grid->fields[id].variable, DCCRGX_EINVAL,
+                 "Poisson fields are f64 (field %d)", id);
     }
     DX_CHECK(f->rhs != f->solution, DCCRGX_EINVAL, "rhs and solution must be distinct fields");
     auto* P = new dccrgx_poisson();

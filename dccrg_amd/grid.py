@@ -345,6 +345,54 @@ class Dccrg:
         self._fields[name] = (fid.value, dt)
         return fid.value
 
+    def add_variable_field(self, name: str, dtype=np.int32) -> int:
+        """A field with a per-cell number of elements (tests/variable_data_size)."""
+        dt = np.dtype(dtype)
+        fid = C.c_int32()
+        check(lib().dccrgx_field_create_variable(self._h, dt.itemsize, C.byref(fid)))
+        self._fields[name] = (fid.value, dt)
+        return fid.value
+
+    def resize(self, name: str, cells, counts):
+        """Element counts of local cells or ghosts (std::vector::resize)."""
+        fid, _ = self._fields[name]
+        c = _u64(cells)
+        n = np.ascontiguousarray(np.broadcast_to(np.asarray(counts, dtype=np.uint32), c.shape))
+        check(lib().dccrgx_field_resize(self._h, fid, c.ctypes.data_as(X._u64p),
+                                        n.ctypes.data_as(C.POINTER(C.c_uint32)), c.size))
+
+    def get_counts(self, name: str, cells) -> np.ndarray:
+        fid, _ = self._fields[name]
+        c = _u64(cells)
+        out = np.zeros(c.size, dtype=np.uint32)
+        check(lib().dccrgx_field_get_counts(self._h, fid, c.ctypes.data_as(X._u64p), c.size,
+                                            out.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return out
+
+    def write_cells(self, name: str, cells, values):
+        """values: one array per cell, or the cells' elements concatenated."""
+        fid, dt = self._fields[name]
+        c = _u64(cells)
+        if isinstance(values, (list, tuple)):
+            values = np.concatenate([np.asarray(v, dtype=dt).ravel() for v in values]) if values else \
+                np.zeros(0, dtype=dt)
+        v = np.ascontiguousarray(values, dtype=dt)
+        check(lib().dccrgx_field_write_cells(self._h, fid, c.ctypes.data_as(X._u64p), c.size, v.ctypes.data,
+                                             v.nbytes))
+
+    def read_cells(self, name: str, cells):
+        """One array per cell (operator[] on local cells and ghosts)."""
+        fid, dt = self._fields[name]
+        c = _u64(cells)
+        nbytes = C.c_size_t()
+        check(lib().dccrgx_field_read_cells(self._h, fid, c.ctypes.data_as(X._u64p), c.size, None, 0,
+                                            C.byref(nbytes)))
+        buf = np.zeros(nbytes.value // dt.itemsize, dtype=dt)
+        check(lib().dccrgx_field_read_cells(self._h, fid, c.ctypes.data_as(X._u64p), c.size, buf.ctypes.data,
+                                            buf.nbytes, C.byref(nbytes)))
+        counts = self.get_counts(name, c)
+        return np.split(buf, np.cumsum(counts)[:-1]) if c.size else []
+
     def field_id(self, name: str) -> int:
         return self._fields[name][0]
 

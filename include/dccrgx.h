@@ -245,6 +245,29 @@ int dccrgx_halo_self(dccrgx_grid* grid, int32_t hood_id, const int32_t* field_id
                      size_t n_fields);
 
 /* ------------------------------------------------------------------------ *
+ * Variable-size cell data (tests/variable_data_size: a Cell_Data whose
+ * get_mpi_datatype describes a per-cell number of elements).  A variable
+ * field holds count[cell] elements of elem_bytes per cell, zero-initialised
+ * on resize like std::vector::resize.  As in the reference, the receiver
+ * sizes its ghost copies before a halo (variable_neighbour_data.cpp:95-102);
+ * messages carry each cell's elements in ascending id order.
+ * ------------------------------------------------------------------------ */
+int dccrgx_field_create_variable(dccrgx_grid* grid, uint32_t elem_bytes, int32_t* field_id);
+/* set the element counts of cells this rank stores (local cells or ghosts;
+ * all storage copies of a cell follow); keeps the leading elements */
+int dccrgx_field_resize(dccrgx_grid* grid, int32_t field_id, const uint64_t* ids,
+                        const uint32_t* counts, size_t n);
+int dccrgx_field_get_counts(const dccrgx_grid* grid, int32_t field_id, const uint64_t* ids, size_t n,
+                            uint32_t* counts);
+/* cell-addressed access for any field (operator[], dccrg.hpp:768-781): the
+ * cells' elements concatenated in the given order, host buffers; a ghost is
+ * read from its first copy.  read with data == NULL returns the size. */
+int dccrgx_field_write_cells(dccrgx_grid* grid, int32_t field_id, const uint64_t* ids, size_t n,
+                             const void* data, size_t bytes);
+int dccrgx_field_read_cells(const dccrgx_grid* grid, int32_t field_id, const uint64_t* ids, size_t n,
+                            void* data, size_t cap, size_t* bytes);
+
+/* ------------------------------------------------------------------------ *
  * Stencils over local cells.  Game of life as in examples/game_of_life.cpp:
  * 54-79 / tests/game_of_life/scalability3d.cpp:136-165: count live
  * neighbors_of (u32 is_alive > 0), then B3/S23 (count == 3 -> 1, count != 2
