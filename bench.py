@@ -31,9 +31,10 @@ BYTES_PER_CELL = 12    # read is_alive 4 + write is_alive 4 + write live_neighbo
 
 def cpu_baseline(seconds: float = 10.0):
     """The oracle's port of the reference hot loop (explicit neighbor lists,
-    examples/game_of_life.cpp:54-79), one host core, on a bounded sample."""
+    examples/game_of_life.cpp:54-79) on the host cores OpenMP is given
+    (OMP_NUM_THREADS; 16 on the GPU box), on a bounded sample."""
     from oracle import dccrg_oracle as O
-    L = (96, 96, 96)
+    L = (128, 128, 128)
     n = L[0] * L[1] * L[2]
     lists = O.GolLists(L, (False, False, True), 1)
     alive = O.random_alive(np.arange(1, n + 1, dtype=np.uint64), 200)
@@ -44,7 +45,8 @@ def cpu_baseline(seconds: float = 10.0):
         lists.step(alive, count)
         steps += 1
     dt = time.perf_counter() - t0
-    return {"value": steps * n / dt, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+    return {"value": steps * n / dt, "unit": "cell-updates/s", "cores": int(O.lib().dox_num_threads()),
+            "kind": "port",
             "sample": f"{L[0]}x{L[1]}x{L[2]} uniform grid, hood 1, periodic z, {steps} steps "
                       f"({dt:.1f} s) of oracle/dccrg_oracle.c dox_gol_count+apply over "
                       f"face-graph-walk neighbor lists"}
@@ -66,6 +68,199 @@ def pmc_traffic(kernel: str, cells_per_launch: int):
     return best
 
 
+def advection_leaves(n=400, r1=0.2, r2=0.12, centre=(0.25, 0.5)):
+    """configs[2]: tests/advection's 2-D grid (n x n x 1, max_ref_lvl 2) with
+    the region around the density hump refined once (r < r1) and twice
+    (r < r2) -- a static snapshot of what 2d.cpp's adaptation produces
+    (AMR itself is out of scope).  Nested disks far apart keep the grid
+    2:1 balanced under the reference's induce rule."""
+    N0 = n * n
+    first = [1, 1 + N0, 1 + N0 + 8 * N0]
+    i, j = np.meshgrid(np.arange(n), np.arange(n), indexing="xy")
+    i, j = i.ravel(), j.ravel()
+    r0 = np.hypot((i + 0.5) / n - centre[0], (j + 0.5) / n - centre[1])
+    out = [first[0] + i[r0 >= r1] + n * j[r0 >= r1]]
+    # level 1: children of refined level-0 cells (x fastest, y, z)
+    ri, rj = i[r0 < r1], j[r0 < r1]
+    d = np.array([(dx, dy, dz) for dz in (0, 1) for dy in (0, 1) for dx in (0, 1)])
+    x1 = (2 * ri[:, None] + d[None, :, 0]).ravel()
+    y1 = (2 * rj[:, None] + d[None, :, 1]).ravel()
+    z1 = np.broadcast_to(d[None, :, 2], (len(ri), 8)).ravel()
+    r_1 = np.hypot((x1 + 0.5) / (2 * n) - centre[0], (y1 + 0.5) / (2 * n) - centre[1])
+    keep = r_1 >= r2
+    out.append(first[1] + x1[keep] + 2 * n * y1[keep] + 4 * N0 * z1[keep])
+    x2 = (2 * x1[~keep][:, None] + d[None, :, 0]).ravel()
+    y2 = (2 * y1[~keep][:, None] + d[None, :, 1]).ravel()
+    z2 = (2 * z1[~keep][:, None] + d[None, :, 2]).ravel()
+    out.append(first[2] + x2 + 4 * n * y2 + 16 * N0 * z2)
+    return np.sort(np.concatenate(out)).astype(np.uint64)
+
+
+def poisson3d_leaves():
+    """tests/poisson/poisson3d.cpp:158-178's grid: 8^3, the 2x2x2 block around
+    (pi, pi/2, 4 pi) refined, the 24 level-0 cells face-adjacent to it refined
+    by the reference's induce rule (dccrg.hpp:9730-9800), and the 8 level-1
+    cells touching the centre refined again: 792 leaves (max_ref_lvl 2).
+    tests/test_bench_inputs.py checks this against the oracle's construction.
+    Returns (ids, indices in level-2 units, levels)."""
+    N0 = 512
+    first = [1, 1 + N0, 1 + 9 * N0]
+    blk = {(x, y, z) for x in (3, 4) for y in (3, 4) for z in (3, 4)}
+    ref0 = set(blk)
+    for (x, y, z) in blk:
+        for d in ((1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)):
+            ref0.add(((x + d[0]) % 8, (y + d[1]) % 8, (z + d[2]) % 8))
+    ids, idx, lvl = [], [], []
+    for z in range(8):
+        for y in range(8):
+            for x in range(8):
+                if (x, y, z) not in ref0:
+                    ids.append(first[0] + x + 8 * y + 64 * z)
+                    idx.append((4 * x, 4 * y, 4 * z))
+                    lvl.append(0)
+                    continue
+                for dz in (0, 1):
+                    for dy in (0, 1):
+                        for dx in (0, 1):
+                            x1, y1, z1 = 2 * x + dx, 2 * y + dy, 2 * z + dz
+                            if (x1 in (7, 8) and y1 in (7, 8) and z1 in (7, 8)):
+                                for ez in (0, 1):
+                                    for ey in (0, 1):
+                                        for ex in (0, 1):
+                                            x2, y2, z2 = 2 * x1 + ex, 2 * y1 + ey, 2 * z1 + ez
+                                            ids.append(first[2] + x2 + 32 * y2 + 1024 * z2)
+                                            idx.append((x2, y2, z2))
+                                            lvl.append(2)
+                            else:
+                                ids.append(first[1] + x1 + 16 * y1 + 256 * z1)
+                                idx.append((2 * x1, 2 * y1, 2 * z1))
+                                lvl.append(1)
+    order = np.argsort(ids)
+    return (np.array(ids, dtype=np.uint64)[order], np.array(idx, dtype=np.float64)[order],
+            np.array(lvl)[order])
+
+
+def secondary(ctx, torch, D):
+    """One line per other BASELINE config (N = 1 only): the 2-D game of life
+    (configs[1]), advection on a 2-level refined grid (configs[2]), the
+    Poisson solve of configs[4] and the mapping kernel."""
+    out = {}
+    dev = torch.device("cuda", ctx.device)
+    # configs[1]: 16384^2, hood 1, periodic x y (scalability.cpp:85)
+    n = 16384
+    g = (D.Dccrg().set_initial_length((n, n, 1)).set_neighborhood_length(1)
+         .set_maximum_refinement_level(0).set_periodic(True, True, False).initialize(ctx))
+    for f in ("a", "b", "c"):
+        g.add_field(f, np.uint32)
+    D.lib().dccrgx_field_init_hash(g._h, g.field_id("a"), 200)
+    cur, nxt = "a", "b"
+    g.gol_step(cur, nxt, "c")
+    ctx.synchronize()
+    steps = 50
+    g.kernel_timer(reset=1)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.gol_step(cur, nxt, "c")
+        cur, nxt = nxt, cur
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    kms, _ = g.kernel_timer(reset=0)
+    g.kernel_timer(reset=-1)
+    ach = BYTES_PER_CELL * n * n * steps / (kms * 1e-3) / 1e9
+    out["gol2d"] = {"workload": "configs[1] 2-D game of life 16384x16384, hood 1, periodic x,y",
+                    "value": n * n * steps / dt, "unit": "cell-updates/s", "steps": steps,
+                    "kernel": "k_gol26_rowv<4>", "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS}
+    g.close()
+
+    # configs[2]: advection, 400x400x1 with 2 refinement levels (static)
+    leaves = advection_leaves()
+    g = (D.Dccrg().set_initial_length((400, 400, 1)).set_maximum_refinement_level(2)
+         .set_periodic(True, True, False).set_neighborhood_length(0).initialize(ctx, leaves=leaves))
+    g.add_advection_fields()
+    idx = np.zeros((len(leaves), 3), dtype=np.int64)
+    lv = np.zeros(len(leaves), dtype=np.int32)
+    m = D.Mapping((400, 400, 1), 2)
+    ids_t = torch.from_numpy(leaves.view(np.int64)).to(dev)
+    it, lt = m.ids_to_indices(ids_t)
+    torch.cuda.synchronize(dev)
+    idx, lv = it.cpu().numpy(), lt.cpu().numpy()
+    ln = (1.0 / 400) / (2.0 ** lv)
+    ctr = (idx + 0.5 * (2 ** (2 - lv))[:, None]) / (400 * 4)
+    rr = np.minimum(np.hypot(ctr[:, 0] - 0.25, ctr[:, 1] - 0.5), 0.15) / 0.15
+    vals = {"density": 0.25 * (1 + np.cos(np.pi * rr)), "vx": -ctr[:, 1] + 0.5, "vy": ctr[:, 0] - 0.5,
+            "vz": np.zeros(len(leaves)), "length_x": ln, "length_y": ln, "length_z": 1.0 / (2.0 ** lv)}
+    for k, v in vals.items():
+        g.write_local(k, v)
+    g.update_copies_of_remote_neighbors(fields=list(vals))
+    dt_adv = 0.5 * g.max_time_step()
+    g.advect_step(dt_adv)
+    ctx.synchronize()
+    steps = 50
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.advect_step(dt_adv)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    nl = len(leaves)
+    out["advection"] = {"workload": "configs[2] tests/advection 400x400x1, max_ref_lvl 2, static refined "
+                                    f"hump region, {nl} leaf cells, neighborhood 0, fp64",
+                        "value": nl * steps / dt, "unit": "cell-steps/s", "steps": steps,
+                        "achieved_GBs": 72 * nl * steps / dt / 1e9,
+                        "frac": 72 * nl * steps / dt / 1e9 / HBM_PEAK_GBS, "bytes_per_cell_step": 72}
+    g.close()
+
+    # configs[4] (Poisson part): poisson3d's 792-leaf grid on one GPU
+    pl, pidx, plv = poisson3d_leaves()
+    L0 = np.array([2 * np.pi / 8, np.pi / 8, 8 * np.pi / 8])
+    g = (D.Dccrg().set_initial_length((8, 8, 8)).set_maximum_refinement_level(2)
+         .set_periodic(True, True, True).set_neighborhood_length(0).initialize(ctx, leaves=pl))
+    for f in ("rhs", "solution", "length_x", "length_y", "length_z"):
+        g.add_field(f, np.float64)
+    pln = L0[None, :] / (2.0 ** plv)[:, None]
+    pc = pidx * (L0 / 4)[None, :] + pln / 2
+    g.write_local("rhs", -(81.0 / 16.0) * np.sin(pc[:, 0]) * np.cos(2 * pc[:, 1]) * np.sin(pc[:, 2] / 4))
+    for k, a in enumerate(("length_x", "length_y", "length_z")):
+        g.write_local(a, pln[:, k])
+    s = D.PoissonSolve(g)
+    g.write_local("solution", np.zeros(len(pl)))
+    s.solve(pl)
+    reps = 20
+    t0 = time.perf_counter()
+    its = 0
+    for _ in range(reps):
+        g.write_local("solution", np.zeros(len(pl)))
+        it_, _ = s.solve(pl, cache_is_up_to_date=True)
+        its += it_
+    dt = time.perf_counter() - t0
+    out["poisson"] = {"workload": "configs[4] tests/poisson/poisson3d 8^3 refined twice (792 leaves), BiCG, "
+                                  "1 GPU", "solve_ms": dt * 1e3 / reps, "iterations_per_s": its / dt,
+                      "iterations_per_solve": its / reps,
+                      "note": "792 cells: launch-latency bound, not bandwidth"}
+    s.close()
+    g.close()
+
+    # mapping kernel: ids -> indices + level, 2048^3 grid at max level 10
+    m = D.Mapping((2048, 2048, 2048), 10)
+    nid = 1 << 26
+    gen = torch.Generator(device=dev).manual_seed(1)
+    ids = torch.randint(1, 1 << 62, (nid,), device=dev, dtype=torch.int64, generator=gen)
+    m.ids_to_indices(ids)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    e0.record()
+    for _ in range(reps):
+        m.ids_to_indices(ids)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    out["mapping"] = {"workload": "Mapping::get_indices + get_refinement_level on 2^26 random ids, 2048^3 "
+                                  "grid, max_ref_lvl 10", "value": nid / (ms * 1e-3), "unit": "ids/s",
+                      "achieved_GBs": 36 * nid / (ms * 1e-3) / 1e9,
+                      "frac": 36 * nid / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_id": 36}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -73,6 +268,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=2048, help="cells per axis per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the other configs' lines (N = 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -179,11 +375,13 @@ def main():
         if t:
             line["roofline"]["traffic"] = t[0]
             line["roofline"]["traffic_source"] = t[1]
+    grid.close()
+    if rank == 0 and world == 1 and not args.no_secondary:
+        line["secondary"] = secondary(ctx, torch, D)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(line), flush=True)
-    grid.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -96,6 +96,83 @@ __global__ void __launch_bounds__(256) k_ex_advect(AdvPtrs p, double dt, const u
     }
 }
 
+// face lists of local cells from the stencil rows: pass 1 (o_row == null)
+// writes the first 6 faces column-major and counts the rest into o_cnt;
+// pass 2 writes the rest at o_row
+__global__ void __launch_bounds__(256) k_face_build(const uint64_t* __restrict__ st_row,
+                                                    const uint32_t* __restrict__ st_slot,
+                                                    const int32_t* __restrict__ st_off,
+                                                    const uint32_t* __restrict__ local_g,
+                                                    const uint8_t* __restrict__ level, int M, uint64_t n,
+                                                    uint32_t* __restrict__ ell_slot, int8_t* __restrict__ ell_dir,
+                                                    uint32_t* __restrict__ o_cnt, const uint64_t* __restrict__ o_row,
+                                                    uint32_t* __restrict__ o_slot, int8_t* __restrict__ o_dir)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        const int64_t cl = 1ll << (M - level[local_g[q]]);
+        uint32_t k = 0;
+        for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) {
+            const uint32_t nb = st_slot[e];
+            const int dir = face_dir(cl, 1ll << (M - level[nb]), st_off + 3 * e);
+            if (!dir) continue;
+            if (k < 6) {
+                if (!o_row) {
+                    ell_slot[k * n + q] = nb;
+                    ell_dir[k * n + q] = (int8_t)dir;
+                }
+            } else if (o_row) {
+                o_slot[o_row[q] + k - 6] = nb;
+                o_dir[o_row[q] + k - 6] = (int8_t)dir;
+            }
+            k++;
+        }
+        if (!o_row) {
+            for (uint32_t j = k; j < 6; j++) ell_slot[j * n + q] = 0xffffffffu;
+            o_cnt[q] = k > 6 ? k - 6 : 0;
+        }
+    }
+}
+
+// explicit grids over the face lists: the 6 column-major faces are
+// independent loads (issued together), the overflow is rare
+struct FaceView {  // trivially copyable kernel argument
+    uint64_t n;
+    const uint32_t* ell_slot;
+    const int8_t* ell_dir;
+    const uint64_t* o_row;
+    const uint32_t* o_slot;
+    const int8_t* o_dir;
+    bool overflow;
+};
+
+__global__ void __launch_bounds__(256) k_ex_advect_faces(AdvPtrs p, double dt, FaceView fc,
+                                                         const uint32_t* __restrict__ local_g,
+                                                         const uint32_t* __restrict__ pos, uint64_t n)
+{
+#pragma clang fp contract(off)
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t q = pos[i];
+        const uint32_t c = local_g[q];
+        const double vol = p.l[0][c] * p.l[1][c] * p.l[2][c];
+        double acc = p.flux[c];
+        uint32_t s[6];
+        int8_t d[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            s[k] = fc.ell_slot[k * fc.n + q];
+            d[k] = fc.ell_dir[k * fc.n + q];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++)
+            if (s[k] != 0xffffffffu) acc += face_term(p, c, s[k], d[k], dt, vol);
+        if (fc.overflow)
+            for (uint64_t e = fc.o_row[q]; e < fc.o_row[q + 1]; e++) acc += face_term(p, c, fc.o_slot[e], fc.o_dir[e], dt, vol);
+        p.flux[c] = acc;
+    }
+}
+
 // uniform grids: the face neighbors present in the neighborhood (mask bit
 // 2k / 2k+1 = canonical axis k, -1 / +1), addressed in the slab layout
 __global__ void __launch_bounds__(256) k_u_advect(UGeom g, AdvPtrs p, double dt, uint32_t mask, uint64_t lin0,
@@ -234,7 +311,53 @@ void uniform_local_run(const dccrgx_grid* grid, uint64_t* s0, uint64_t* n)
     *n = u.hi - u.lo;
 }
 
+// build the face lists of a neighborhood's local cells (explicit grids)
+int build_faces(const dccrgx_grid* grid, Hood& h)
+{
+    ExRegion R;
+    DX_TRY(explicit_region(grid, h, DCCRGX_REGION_ALL, &R));
+    hipStream_t st = grid->ctx->compute;
+    auto fc = std::make_shared<FaceCache>();
+    const uint64_t n = R.n;
+    fc->n = n;
+    const size_t m = std::max<uint64_t>(n, 1);
+    DX_HIP(hipMalloc(&fc->ell_slot, 6 * m * 4));
+    DX_HIP(hipMalloc(&fc->ell_dir, 6 * m));
+    DX_HIP(hipMalloc(&fc->o_row, (m + 1) * 8));
+    uint32_t* d_cnt = nullptr;
+    DX_HIP(hipMalloc(&d_cnt, m * 4));
+    const int M = grid->map.max_lvl;
+    if (n)
+        hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
+                           R.local_g, R.level, M, n, fc->ell_slot, fc->ell_dir, d_cnt, (const uint64_t*)nullptr,
+                           (uint32_t*)nullptr, (int8_t*)nullptr);
+    DX_HIP(hipGetLastError());
+    std::vector<uint32_t> cnt(n);
+    if (n) DX_HIP(hipMemcpyAsync(cnt.data(), d_cnt, n * 4, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_cnt);
+    std::vector<uint64_t> row(n + 1, 0);
+    for (uint64_t q = 0; q < n; q++) row[q + 1] = row[q] + cnt[q];
+    fc->overflow = row[n] > 0;
+    DX_HIP(hipMemcpyAsync(fc->o_row, row.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    DX_HIP(hipMalloc(&fc->o_slot, std::max<uint64_t>(row[n], 1) * 4));
+    DX_HIP(hipMalloc(&fc->o_dir, std::max<uint64_t>(row[n], 1)));
+    if (fc->overflow)
+        hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
+                           R.local_g, R.level, M, n, fc->ell_slot, fc->ell_dir, (uint32_t*)nullptr, fc->o_row,
+                           fc->o_slot, fc->o_dir);
+    DX_HIP(hipGetLastError());
+    DX_HIP(hipStreamSynchronize(st));
+    h.faces = fc;
+    return DCCRGX_OK;
+}
+
 }  // namespace
+
+FaceCache::~FaceCache()
+{
+    for (void* q : {(void*)ell_slot, (void*)ell_dir, (void*)o_row, (void*)o_slot, (void*)o_dir}) hipFree(q);
+}
 
 }  // namespace dccrgx
 
@@ -257,8 +380,17 @@ int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect
         ExRegion R;
         DX_TRY(explicit_region(grid, *h, region, &R));
         if (!R.n) return DCCRGX_OK;
-        hipLaunchKernelGGL(k_ex_advect, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, h->d_st_row, h->d_st_slot,
-                           h->d_st_off, R.local_g, R.level, grid->map.max_lvl, R.pos, R.n);
+        Hood* hm = find_hood(grid, hood_id);
+        if (!hm->faces) DX_TRY(build_faces(grid, *hm));
+        if (getenv("DCCRGX_ADVECT_ROWS"))  // the plain stencil-row gather (comparison path)
+            hipLaunchKernelGGL(k_ex_advect, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, h->d_st_row,
+                               h->d_st_slot, h->d_st_off, R.local_g, R.level, grid->map.max_lvl, R.pos, R.n);
+        else {
+            const FaceCache& F = *hm->faces;
+            const FaceView fv{F.n, F.ell_slot, F.ell_dir, F.o_row, F.o_slot, F.o_dir, F.overflow};
+            hipLaunchKernelGGL(k_ex_advect_faces, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, fv, R.local_g,
+                               R.pos, R.n);
+        }
         DX_HIP(hipGetLastError());
         return DCCRGX_OK;
     }

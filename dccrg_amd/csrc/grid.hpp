@@ -122,6 +122,22 @@ struct CopySeg {
     uint64_t dst, src, n;  // contiguous slot run
 };
 
+// explicit grids: the face neighbors among a neighborhood's stencil rows,
+// per local cell (built on first use by the advection solver, advect.hip).
+// The first 6 faces of a cell are stored column-major ([k][local position],
+// slot or UINT32_MAX) so a wavefront's loads of face k are independent and
+// coalesced; faces beyond 6 (next to finer cells) go to a CSR overflow.
+struct FaceCache {
+    uint64_t n = 0;
+    uint32_t* ell_slot = nullptr;
+    int8_t* ell_dir = nullptr;
+    uint64_t* o_row = nullptr;
+    uint32_t* o_slot = nullptr;
+    int8_t* o_dir = nullptr;
+    bool overflow = false;
+    ~FaceCache();
+};
+
 struct Hood {
     int32_t id = 0;
     std::vector<int32_t> items;    // original (x, y, z) items, hood_of
@@ -159,6 +175,7 @@ struct Hood {
     uint64_t* d_st_row = nullptr;
     uint32_t* d_st_slot = nullptr;
     int32_t* d_st_off = nullptr;     // x, y, z offset of each stencil entry
+    std::shared_ptr<FaceCache> faces;  // advection face lists (explicit grids)
 };
 
 }  // namespace dccrgx

@@ -110,10 +110,10 @@ int max_possible_level(const uint64_t length[3]);
 __host__ __device__ inline int map_level(const MapParams& p, uint64_t cell)
 {
     if (cell == 0 || cell > p.last_cell) return -1;
+    // levels are contiguous id ranges: count the level starts <= cell
+    // (uniform trip count max_lvl; first_id lives in scalar registers)
     int l = 0;
-#pragma unroll
-    for (int k = 1; k < MAX_LEVELS; k++)
-        l += (k <= p.max_lvl && cell >= p.first_id[k]) ? 1 : 0;
+    for (int k = 1; k <= p.max_lvl; k++) l += cell >= p.first_id[k] ? 1 : 0;
     return l;
 }
 

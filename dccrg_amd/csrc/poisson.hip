@@ -375,6 +375,102 @@ __global__ void k_control(PState* S, int phase, double pnorm, double stop_residu
     control(S, phase, S->red, pnorm, stop_residual, increase, min_it, max_it);
 }
 
+// One workgroup runs the whole iteration loop (one rank, no periodic self
+// copies, small systems): the same per-cell arithmetic and control as the
+// multi-kernel path, block-wide reductions, no launch per phase.
+constexpr int SB = 1024;
+
+__device__ double solo_sum(double v, double* red)
+{
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int w = SB / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    const double r = red[0];
+    __syncthreads();
+    return r;
+}
+
+__global__ void __launch_bounds__(SB) k_solo(PPtrs p, PSys s, PState* S, double pnorm, double stop_residual,
+                                            double increase, uint32_t min_it, uint32_t max_it)
+{
+#pragma clang fp contract(off)
+    __shared__ double red[SB];
+    __shared__ PState T;
+    if (threadIdx.x == 0) T = *S;
+    __syncthreads();
+    for (;;) {
+        // A . p0 and p1 . (A . p0)
+        double acc = 0;
+        for (uint64_t i = threadIdx.x; i < s.n; i += SB) {
+            const uint64_t c = s.slot[i];
+            if (p.type[c] != SOLVE) continue;
+            double a = p.sf[c] * p.p0[c];
+            for (uint64_t e = s.row[i]; e < s.row[i + 1]; e++) {
+                const int code = s.code[e];
+                double m = p.f[fidx((code & 15) - 3)][c];
+                if ((code >> 4) - 1 > 0) m /= 4.0;
+                a += m * p.p0[s.nb[e]];
+            }
+            p.adp0[c] = a;
+            acc += p.p1[c] * a;
+        }
+        double v = solo_sum(acc, red);
+        if (threadIdx.x == 0) control(&T, PH_ALPHA, v, pnorm, stop_residual, increase, min_it, max_it);
+        __syncthreads();
+        if (T.done) break;
+        // solution update and |r0|^p
+        acc = 0;
+        for (uint64_t i = threadIdx.x; i < s.n; i += SB) {
+            const uint64_t c = s.slot[i];
+            if (p.type[c] == SOLVE) p.sol[c] += T.alpha * p.p0[c];
+            acc += pw(fabs(p.r0[c]), pnorm);
+        }
+        v = solo_sum(acc, red);
+        if (threadIdx.x == 0) control(&T, PH_RES, v, pnorm, stop_residual, increase, min_it, max_it);
+        __syncthreads();
+        // best solution, r0 and r1, r0 . r1
+        acc = 0;
+        for (uint64_t i = threadIdx.x; i < s.n; i += SB) {
+            const uint64_t c = s.slot[i];
+            if (p.type[c] != SOLVE) continue;
+            if (T.save) p.best[c] = p.sol[c];
+            if (T.halt) continue;
+            const double r0 = p.r0[c] - T.alpha * p.adp0[c];
+            double a = p.sf[c] * p.p1[c];
+            for (uint64_t e = s.row[i]; e < s.row[i + 1]; e++) {
+                const int code = s.code[e];
+                const uint64_t nb = s.nb[e];
+                double m = p.f[fidx(-((code & 15) - 3))][nb];
+                if ((code >> 4) - 1 > 0) m /= 4.0;
+                a += m * p.p1[nb];
+            }
+            const double r1 = p.r1[c] - T.alpha * a;
+            p.r0[c] = r0;
+            p.r1[c] = r1;
+            acc += r0 * r1;
+        }
+        v = solo_sum(acc, red);
+        if (threadIdx.x == 0) control(&T, PH_BETA, v, pnorm, stop_residual, increase, min_it, max_it);
+        __syncthreads();
+        if (T.done) break;
+        for (uint64_t i = threadIdx.x; i < s.n; i += SB) {
+            const uint64_t c = s.slot[i];
+            if (p.type[c] != SOLVE) continue;
+            p.p0[c] = p.r0[c] + T.beta * p.p0[c];
+            p.p1[c] = p.r1[c] + T.beta * p.p1[c];
+        }
+        __syncthreads();  // p0, p1 of neighbors are read by the next A . p0
+        if (T.end) {
+            if (threadIdx.x == 0) T.done = 1;
+            break;
+        }
+    }
+    if (threadIdx.x == 0) *S = T;
+}
+
 __global__ void __launch_bounds__(256) k_rel(const uint64_t* __restrict__ cells, const uint64_t* __restrict__ row,
                                              const uint64_t* __restrict__ ids, uint64_t n, MapParams mp,
                                              int8_t* __restrict__ rel)
@@ -773,8 +869,18 @@ int dccrgx_poisson_solve(dccrgx_poisson* P, const uint64_t* cells, size_t n, con
     DX_TRY(reduce(P, PH_INIT));
     const double pn = P->prm.p_of_norm;
     PState hs{};
+    const Hood* dh = find_hood(P->grid, DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
+    const bool solo = P->grid->ctx->comm_size == 1 && dh && dh->h_self.empty() && P->n_info <= (1u << 16) &&
+                      !getenv("DCCRGX_POISSON_MULTI");
+    if (solo) {
+        const dccrgx_poisson_params& q = P->prm;
+        hipLaunchKernelGGL(k_solo, dim3(1), dim3(SB), 0, st, p, s, P->d_state, pn, q.stop_residual,
+                           q.stop_after_residual_increase, q.min_iterations, q.max_iterations);
+        DX_HIP(hipGetLastError());
+        DX_HIP(hipMemcpyAsync(&hs, P->d_state, sizeof(PState), hipMemcpyDeviceToHost, st));
+    }
     uint32_t batch = 4;
-    for (;;) {
+    for (; !solo;) {
         for (uint32_t k = 0; k < batch; k++) {
             DX_TRY(halo(P, {P->fid[F_P0], P->fid[F_P1]}));  // SOLVING, :279-281
             hipLaunchKernelGGL(k_adp0, dim3(RG), dim3(RB), 0, st, p, s, (const PState*)P->d_state, P->d_part);

@@ -10,6 +10,9 @@
 #include "dccrg_oracle.h"
 
 #include <float.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -694,7 +697,9 @@ long dox_get_face_neighbors_of(const dox_grid* g, uint64_t cell, uint64_t* out_i
 void dox_gol_count(size_t n_cells, const uint64_t* row_ptr, const uint32_t* nbr_slot,
                    const uint32_t* alive, uint32_t* count)
 {
-    /* examples/game_of_life.cpp:54-66: live_neighbor_count = #alive neighbors_of */
+    /* examples/game_of_life.cpp:54-66: live_neighbor_count = #alive neighbors_of
+     * (cells are independent: host threads split them, results unchanged) */
+#pragma omp parallel for schedule(static)
     for (size_t c = 0; c < n_cells; c++) {
         uint32_t cnt = 0;
         for (uint64_t k = row_ptr[c]; k < row_ptr[c + 1]; k++)
@@ -706,10 +711,20 @@ void dox_gol_count(size_t n_cells, const uint64_t* row_ptr, const uint32_t* nbr_
 void dox_gol_apply(size_t n_cells, uint32_t* alive, const uint32_t* count)
 {
     /* examples/game_of_life.cpp:68-79 (B3/S23) */
+#pragma omp parallel for schedule(static)
     for (size_t c = 0; c < n_cells; c++) {
         if (count[c] == 3) alive[c] = 1;
         else if (count[c] != 2) alive[c] = 0;
     }
+}
+
+int dox_num_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
 }
 
 long dox_build_uniform_slot_lists(const dox_grid* g, unsigned hood_length, uint64_t* row_ptr,

@@ -1,7 +1,9 @@
 /*
  * dccrg_oracle.h -- TEST INFRASTRUCTURE ONLY.
  *
- * A plain-C, single-threaded restatement of the reference algorithms on the
+ * A plain-C restatement (single-threaded except the game-of-life loops, which
+ * split independent cells over OpenMP threads for the CPU baseline) of the
+ * reference algorithms on the
  * dccrg hot path (ykempf/dccrg, mounted read-only at /root/reference during
  * development).  Every function cites the reference file:line it follows.
  *
@@ -97,6 +99,8 @@ long dox_get_face_neighbors_of(const dox_grid* g, uint64_t cell, uint64_t* out_i
 void dox_gol_count(size_t n_cells, const uint64_t* row_ptr, const uint32_t* nbr_slot,
                    const uint32_t* alive, uint32_t* count);
 void dox_gol_apply(size_t n_cells, uint32_t* alive, const uint32_t* count);
+/* host threads the two loops above use (OpenMP; OMP_NUM_THREADS) */
+int dox_num_threads(void);
 
 /* Build neighbors_of slot lists for ALL cells of a uniform level-0 grid using
  * the face-graph walk; slot = id - 1.  Returns total entries (row_ptr has n+1). */

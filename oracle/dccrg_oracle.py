@@ -90,6 +90,7 @@ def lib():
         L.dox_get_face_neighbors_of.argtypes = [C.c_void_p, C.c_uint64, u64p, i32p, C.c_size_t]
         L.dox_gol_count.argtypes = [C.c_size_t, u64p, u32p, u32p, u32p]
         L.dox_gol_apply.argtypes = [C.c_size_t, u32p, u32p]
+        L.dox_num_threads.restype = C.c_int
         L.dox_build_uniform_slot_lists.restype = C.c_long
         L.dox_build_uniform_slot_lists.argtypes = [C.c_void_p, C.c_uint, u64p, u32p, C.c_size_t]
         f64p = C.POINTER(C.c_double)

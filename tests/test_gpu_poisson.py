@@ -16,6 +16,17 @@ from test_oracle_poisson import L0, error_norm, poisson3d_leaves, solution_value
 TOL = 1e-12
 
 
+@pytest.fixture(params=["solo", "multi"])
+def path(request, monkeypatch):
+    """Both iteration drivers: one workgroup for small single-rank systems,
+    and the batched multi-kernel path used across ranks."""
+    if request.param == "multi":
+        monkeypatch.setenv("DCCRGX_POISSON_MULTI", "1")
+    else:
+        monkeypatch.delenv("DCCRGX_POISSON_MULTI", raising=False)
+    return request.param
+
+
 def geometry(length, M, cells, l0):
     m = O.Mapping(length, M)
     idx, lvl = m.ids_to_indices(np.asarray(cells, dtype=np.uint64))
@@ -81,7 +92,7 @@ def test_poisson_factors_bit_exact(name):
 
 @pytest.mark.parametrize("iters", [1, 2, 5, 12])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_poisson_fixed_iterations(name, iters):
+def test_poisson_fixed_iterations(name, iters, path):
     g, sysm, cells, rhs, guess, solve, skip = build(name)
     s = D.PoissonSolve(g, max_iterations=iters)
     g.write_local("solution", guess)
@@ -94,7 +105,7 @@ def test_poisson_fixed_iterations(name, iters):
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_poisson_full_solve(name):
+def test_poisson_full_solve(name, path):
     g, sysm, cells, rhs, guess, solve, skip = build(name)
     s = D.PoissonSolve(g)
     g.write_local("solution", guess)
@@ -110,7 +121,7 @@ def test_poisson_full_solve(name):
         assert np.abs(got - ref).max() <= 1e-9 * scale
 
 
-def test_poisson_cache_reuse():
+def test_poisson_cache_reuse(path):
     """cache_is_up_to_date = true skips cache_system_info (:263-265)."""
     g, sysm, cells, rhs, guess, solve, skip = build("plane_open")
     s = D.PoissonSolve(g, max_iterations=3)
