@@ -146,6 +146,32 @@ struct FaceView {  // trivially copyable kernel argument
     bool overflow;
 };
 
+__device__ inline double sel3(int k, double x0, double x1, double x2) { return k == 0 ? x0 : (k == 1 ? x1 : x2); }
+
+// face_term over values already in registers (same expression, same order)
+__device__ inline double face_term_v(int dir, double dt, double vol_c, const double lc3[3], const double vc3[3],
+                                     double rho_c, double ln0, double ln1, double ln2, double vn, double rho_n)
+{
+#pragma clang fp contract(off)
+    const int ax = (dir > 0 ? dir : -dir) - 1;
+    const int a1 = ax == 0 ? 1 : 0, a2 = ax == 2 ? 1 : 2;
+    const double area_c = lc3[a1] * lc3[a2];
+    const double area_n = sel3(a1, ln0, ln1, ln2) * sel3(a2, ln0, ln1, ln2);
+    const double min_area = area_c < area_n ? area_c : area_n;
+    const double lc = lc3[ax], ln = sel3(ax, ln0, ln1, ln2);
+    const double v = (lc * vn + ln * vc3[ax]) / (lc + ln);
+    double f;
+    if (dir > 0) f = (v >= 0 ? rho_c : rho_n) * dt * v * min_area;
+    else f = (v >= 0 ? rho_n : rho_c) * dt * v * min_area;
+    return dir > 0 ? -(f / vol_c) : f / vol_c;
+}
+
+// explicit grids over the face lists: the 6 column-major faces are
+// independent loads, and every neighbour value of all 6 faces is gathered
+// unconditionally (an absent face reads the cell itself and is masked out)
+// so the ~30 gathers of a cell are in flight together instead of one face's
+// loads waiting behind the previous face's branch.  The overflow (faces
+// next to finer cells beyond the first 6) is rare.
 __global__ void __launch_bounds__(256) k_ex_advect_faces(AdvPtrs p, double dt, FaceView fc,
                                                          const uint32_t* __restrict__ local_g,
                                                          const uint32_t* __restrict__ pos, uint64_t n)
@@ -153,10 +179,8 @@ __global__ void __launch_bounds__(256) k_ex_advect_faces(AdvPtrs p, double dt, F
 #pragma clang fp contract(off)
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t q = pos[i];
+        const uint32_t q = pos ? pos[i] : (uint32_t)i;
         const uint32_t c = local_g[q];
-        const double vol = p.l[0][c] * p.l[1][c] * p.l[2][c];
-        double acc = p.flux[c];
         uint32_t s[6];
         int8_t d[6];
 #pragma unroll
@@ -164,9 +188,27 @@ __global__ void __launch_bounds__(256) k_ex_advect_faces(AdvPtrs p, double dt, F
             s[k] = fc.ell_slot[k * fc.n + q];
             d[k] = fc.ell_dir[k * fc.n + q];
         }
+        const double lc3[3] = {p.l[0][c], p.l[1][c], p.l[2][c]};
+        const double vc3[3] = {p.v[0][c], p.v[1][c], p.v[2][c]};
+        const double rho_c = p.rho[c];
+        double acc = p.flux[c];
+        double ln0[6], ln1[6], ln2[6], vn[6], rn[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const uint32_t nb = s[k] != 0xffffffffu ? s[k] : c;
+            const int ax = d[k] > 0 ? d[k] - 1 : (d[k] < 0 ? -d[k] - 1 : 0);
+            const double* vp = ax == 0 ? p.v[0] : (ax == 1 ? p.v[1] : p.v[2]);
+            ln0[k] = p.l[0][nb];
+            ln1[k] = p.l[1][nb];
+            ln2[k] = p.l[2][nb];
+            vn[k] = vp[nb];
+            rn[k] = p.rho[nb];
+        }
+        const double vol = lc3[0] * lc3[1] * lc3[2];
 #pragma unroll
         for (int k = 0; k < 6; k++)
-            if (s[k] != 0xffffffffu) acc += face_term(p, c, s[k], d[k], dt, vol);
+            if (s[k] != 0xffffffffu)
+                acc += face_term_v(d[k], dt, vol, lc3, vc3, rho_c, ln0[k], ln1[k], ln2[k], vn[k], rn[k]);
         if (fc.overflow)
             for (uint64_t e = fc.o_row[q]; e < fc.o_row[q + 1]; e++) acc += face_term(p, c, fc.o_slot[e], fc.o_dir[e], dt, vol);
         p.flux[c] = acc;
@@ -389,7 +431,7 @@ int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect
             const FaceCache& F = *hm->faces;
             const FaceView fv{F.n, F.ell_slot, F.ell_dir, F.o_row, F.o_slot, F.o_dir, F.overflow};
             hipLaunchKernelGGL(k_ex_advect_faces, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, fv, R.local_g,
-                               R.pos, R.n);
+                               region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos, R.n);
         }
         DX_HIP(hipGetLastError());
         return DCCRGX_OK;
@@ -466,7 +508,16 @@ int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_f
     DX_CHECK(grid && f, DCCRGX_EINVAL, "null argument");
     // 2d.cpp:321-390: start density halo, inner fluxes, wait, outer fluxes, apply
     const int32_t fd = f->density;
+    const Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    bool remote = false;
+    for (const PeerPlan& pp : h->peers) remote |= !pp.send_ids.empty() || !pp.recv_ids.empty();
     DX_TRY(dccrgx_halo_start(grid, hood_id, &fd, 1));
+    if (!remote) {  // nothing to overlap: one launch over every local cell
+        DX_TRY(dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL));
+        DX_TRY(dccrgx_advect_fluxes(grid, hood_id, f, dt, DCCRGX_REGION_ALL));
+        return dccrgx_advect_apply(grid, f);
+    }
     DX_TRY(dccrgx_advect_fluxes(grid, hood_id, f, dt, DCCRGX_REGION_INNER));
     DX_TRY(dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL));
     DX_TRY(dccrgx_advect_fluxes(grid, hood_id, f, dt, DCCRGX_REGION_OUTER));

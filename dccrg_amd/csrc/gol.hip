@@ -401,7 +401,7 @@ __global__ void __launch_bounds__(64 * NW) k_gol26v(Gol4Args g)
 // cells of a row and marches along C (the y rows); lane = 4 cells (dwordx4),
 // packed-byte row sums as in k_gol26v; rows b-1 / b+1 are the row itself
 // (periodic B: mult = 3) or absent (mult = 1).
-template <int NW>
+template <int NW, bool NTS = false>
 __global__ void __launch_bounds__(64 * NW) k_gol26_rowv(Gol4Args g, uint32_t mult)
 {
     constexpr int NT = 64 * NW, TA = 4 * NT;
@@ -483,8 +483,15 @@ __global__ void __launch_bounds__(64 * NW) k_gol26_rowv(Gol4Args g, uint32_t mul
             uint32_t* pcnt = g.cnt + (uint64_t)c * g.S;
             uint32_t* pout = g.out + (uint64_t)c * g.S;
             if (plin >= g.lo && plin + g.S <= g.hi) {
-                *reinterpret_cast<uint4*>(pcnt + p) = nc;
-                *reinterpret_cast<uint4*>(pout + p) = nv;
+                if (NTS) {
+                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 xc = {nc.x, nc.y, nc.z, nc.w}, xv = {nv.x, nv.y, nv.z, nv.w};
+                    __builtin_nontemporal_store(xc, reinterpret_cast<u32x4*>(pcnt + p));
+                    __builtin_nontemporal_store(xv, reinterpret_cast<u32x4*>(pout + p));
+                } else {
+                    *reinterpret_cast<uint4*>(pcnt + p) = nc;
+                    *reinterpret_cast<uint4*>(pout + p) = nv;
+                }
             } else {
                 const uint32_t ncs[4] = {nc.x, nc.y, nc.z, nc.w}, nvs[4] = {nv.x, nv.y, nv.z, nv.w};
 #pragma unroll
@@ -499,6 +506,110 @@ __global__ void __launch_bounds__(64 * NW) k_gol26_rowv(Gol4Args g, uint32_t mul
         Sc = Sx;
         Bc = Bx;
         Vc = Vn;
+    }
+}
+
+// Wave-independent LB == 1 kernel (2-D grids, LA % 4 == 0): each wave owns a
+// 256-cell strip of a row and marches along C on its own -- no LDS tile and
+// no barrier.  The horizontal neighbours of a lane's 4 packed cells come from
+// the adjacent lanes by cross-lane shuffles; lanes 0 and 63 fetch the strip's
+// two apron cells.  Rows are fetched G at a time, G rows ahead of the ones
+// being finished, so every wave keeps G dwordx4 loads in flight (the barrier
+// per row of k_gol26_rowv capped its memory-level parallelism at one row).
+template <int G>
+__global__ void __launch_bounds__(256) k_gol2d_wave(Gol4Args g, uint32_t mult)
+{
+    constexpr int NW = 4;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, q8 = g.nwg >> 3, r8 = g.nwg & 7;
+    const uint32_t wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const uint32_t tile_id = wgid % g.tiles_a;
+    const int64_t chunk_id = wgid / g.tiles_a;
+    const int64_t a0 = ((int64_t)tile_id * NW + w) * 256;
+    const int64_t c0 = g.s0 + chunk_id * g.chunk;
+    const int64_t c1 = min(g.s1, c0 + g.chunk);
+    const int64_t LA = (int64_t)g.LA;
+    if (c0 >= c1 || a0 >= LA) return;  // wave-uniform
+    auto wrapA = [&](int64_t a) -> int64_t {
+        if (a >= 0 && a < LA) return a;
+        return g.perA ? ug_wrap(a, LA) : -1;
+    };
+    const int64_t av = wrapA(a0 + 4 * lane);
+    const bool vok = av >= 0;
+    const uint32_t voff = vok ? (uint32_t)av : 0u;
+    const int64_t ae = lane == 0 ? wrapA(a0 - 1) : (lane == 63 ? wrapA(a0 + 256) : -1);
+    const bool eok = ae >= 0;
+    const uint32_t eoff = eok ? (uint32_t)ae : 0u;
+
+    uint4 F[G];
+    uint32_t FE[G];
+    auto fetch_row = [&](int64_t sc, uint4& v, uint32_t& e) {
+        const uint32_t* __restrict__ plane = g.in + (uint64_t)sc * g.S;
+        const uint4 x = *reinterpret_cast<const uint4*>(plane + voff);
+        v = vok ? x : make_uint4(0, 0, 0, 0);
+        e = eok ? plane[eoff] : 0u;
+    };
+    // packed 3-wide row sum of a row (4 cells per lane, one byte each)
+    auto hsum = [&](uint32_t m, uint32_t e) -> uint32_t {
+        const uint32_t up = __shfl_up(m, 1), dn = __shfl_down(m, 1);
+        const uint32_t lft = lane > 0 ? (up >> 24) : (e != 0u ? 1u : 0u);
+        const uint32_t rgt = lane < 63 ? (dn & 0xffu) : (e != 0u ? 1u : 0u);
+        return mult * (m + ((m << 8) | lft) + ((m >> 8) | (rgt << 24)));
+    };
+    uint4 Vc;
+    uint32_t Hp, Hc, Bc;
+    {
+        uint4 v;
+        uint32_t e;
+        fetch_row(c0 - 1, v, e);
+        Hp = hsum(pack_bits(v), e);
+        fetch_row(c0, Vc, e);
+        Bc = pack_bits(Vc);
+        Hc = hsum(Bc, e);
+    }
+#pragma unroll
+    for (int j = 0; j < G; j++)
+        if (c0 + 1 + j <= c1) fetch_row(c0 + 1 + j, F[j], FE[j]);
+    const bool a_ok = a0 + 4 * lane < LA;
+    const uint32_t p = (uint32_t)(a0 + 4 * lane);
+    for (int64_t c = c0; c < c1; c += G) {
+#pragma unroll
+        for (int j = 0; j < G; j++) {
+            const int64_t r = c + j;  // output row
+            const uint32_t Bn = pack_bits(F[j]);
+            const uint32_t Hn = hsum(Bn, FE[j]);
+            const uint32_t cnt4 = Hp + Hc + Hn - Bc;
+            if (a_ok && r < c1) {
+                const uint32_t n0 = cnt4 & 0xffu, n1 = (cnt4 >> 8) & 0xffu, n2 = (cnt4 >> 16) & 0xffu,
+                               n3 = cnt4 >> 24;
+                const uint4 nc = make_uint4(n0, n1, n2, n3);
+                const uint4 nv = make_uint4(gol_rule(n0, Vc.x), gol_rule(n1, Vc.y), gol_rule(n2, Vc.z),
+                                            gol_rule(n3, Vc.w));
+                const uint64_t plin = g.S * (uint64_t)(r + g.cbase);
+                uint32_t* pcnt = g.cnt + (uint64_t)r * g.S;
+                uint32_t* pout = g.out + (uint64_t)r * g.S;
+                if (plin >= g.lo && plin + g.S <= g.hi) {
+                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 xc = {nc.x, nc.y, nc.z, nc.w}, xv = {nv.x, nv.y, nv.z, nv.w};
+                    __builtin_nontemporal_store(xc, reinterpret_cast<u32x4*>(pcnt + p));
+                    __builtin_nontemporal_store(xv, reinterpret_cast<u32x4*>(pout + p));
+                } else {
+                    const uint32_t ncs[4] = {nc.x, nc.y, nc.z, nc.w}, nvs[4] = {nv.x, nv.y, nv.z, nv.w};
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        if (plin + p + q >= g.lo && plin + p + q < g.hi) {
+                            pcnt[p + q] = ncs[q];
+                            pout[p + q] = nvs[q];
+                        }
+                }
+            }
+            Hp = Hc;
+            Hc = Hn;
+            Bc = Bn;
+            Vc = F[j];
+            // refill the slot just consumed: row c+G+1+j, G rows ahead
+            if (c + G + 1 + j <= c1) fetch_row(c + G + 1 + j, F[j], FE[j]);
+        }
     }
 }
 
@@ -719,6 +830,9 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
         v.perA = u.perA;
         v.perB = u.perB;
         constexpr int NW = 4, TA = 256 * NW;
+        // 0: k_gol26_rowv, 1: k_gol26_rowv with non-temporal stores, 4/8/16: k_gol2d_wave<G>
+        // (tools/gol2d_sweep.py)
+        const int64_t var2 = getenv_int("DCCRGX_GOL2D_VARIANT", 0);
         v.tiles_a = (uint32_t)((u.LA + TA - 1) / TA);
         v.tiles_b = 1;
         int64_t chunk = getenv_int("DCCRGX_GOL_CHUNK", 0);
@@ -729,8 +843,16 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
         }
         v.chunk = chunk;
         const int64_t chunks = (nsl + chunk - 1) / chunk;
+        DX_CHECK((int64_t)v.tiles_a * chunks < (int64_t)UINT32_MAX, DCCRGX_EINVAL, "grid too large for one launch");
         v.nwg = (uint32_t)(v.tiles_a * chunks);
-        hipLaunchKernelGGL((k_gol26_rowv<NW>), dim3(v.nwg), dim3(64 * NW), 0, st, v, u.perB ? 3u : 1u);
+        const uint32_t mult = u.perB ? 3u : 1u;
+        switch (var2) {
+        case 1: hipLaunchKernelGGL((k_gol26_rowv<NW, true>), dim3(v.nwg), dim3(64 * NW), 0, st, v, mult); break;
+        case 4: hipLaunchKernelGGL((k_gol2d_wave<4>), dim3(v.nwg), dim3(256), 0, st, v, mult); break;
+        case 16: hipLaunchKernelGGL((k_gol2d_wave<16>), dim3(v.nwg), dim3(256), 0, st, v, mult); break;
+        case 8: hipLaunchKernelGGL((k_gol2d_wave<8>), dim3(v.nwg), dim3(256), 0, st, v, mult); break;
+        default: hipLaunchKernelGGL((k_gol26_rowv<NW>), dim3(v.nwg), dim3(64 * NW), 0, st, v, mult); break;
+        }
     } else if (u.LB == 1) {
         constexpr int TA = 1024, NA = 4;
         a.tiles_a = (uint32_t)((u.LA + TA - 1) / TA);

@@ -288,6 +288,34 @@ def test_gol_kernel_variants_bit_exact(monkeypatch, variant, length, periodic, P
     assert np.array_equal(a, ref_a) and np.array_equal(c, ref_n)
 
 
+VEC2D_CASES = [
+    ((264, 20, 1), (True, False, False), 1),
+    ((264, 20, 1), (True, True, False), 1),
+    ((1028, 37, 1), (True, True, False), 1),   # strip overhang with periodic wrap
+    ((1028, 37, 1), (False, False, False), 3),
+    ((1032, 9, 1), (False, True, True), 2),
+    ((520, 61, 1), (True, True, True), 2),
+    ((8, 1, 1), (True, False, False), 1),
+    ((2048, 40, 1), (False, True, False), 4),
+]
+
+
+@pytest.mark.parametrize("variant", ["0", "1", "4", "8", "16"])
+@pytest.mark.parametrize("chunk", ["0", "3", "11"])
+@pytest.mark.parametrize("length,periodic,P", VEC2D_CASES)
+def test_gol2d_kernel_variants_bit_exact(monkeypatch, variant, chunk, length, periodic, P):
+    """The 2-D (LB == 1) builds: the LDS row kernel (0) and the wave-independent
+    kernel with G rows in flight, over chunk lengths that are and are not
+    multiples of G, partial slabs, strip overhangs and periodic wraps."""
+    monkeypatch.setenv("DCCRGX_GOL2D_VARIANT", variant)
+    monkeypatch.setenv("DCCRGX_GOL_CHUNK", chunk)
+    n = int(np.prod(length))
+    a0 = O.random_alive(np.arange(1, n + 1, dtype=np.uint64), 350)
+    ref_a, ref_n = O.gol_reference_run(length, periodic, 1, a0, 4)
+    a, c = gol_gpu(length, periodic, 1, a0, 4, P, "split" if P > 1 else "step")
+    assert np.array_equal(a, ref_a) and np.array_equal(c, ref_n)
+
+
 def test_gol_kat_15x15():
     k = GOLD["gol_kat"]
     n = int(np.prod(k["length"]))
