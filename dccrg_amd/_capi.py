@@ -20,6 +20,7 @@ CELLS_LOCAL, CELLS_INNER, CELLS_OUTER, CELLS_REMOTE = 0, 1, 2, 3
 WAIT_ALL, WAIT_RECEIVES, WAIT_SENDS = 0, 1, 2
 REGION_ALL, REGION_INNER, REGION_OUTER = 0, 1, 2
 OP_LENGTH_IN_INDICES, OP_PARENT, OP_LEVEL_0_PARENT, OP_CHILD = 0, 1, 2, 3
+AMR_REFINE, AMR_DONT_REFINE, AMR_UNREFINE, AMR_DONT_UNREFINE = 0, 1, 2, 3
 
 ERRORS = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "ERCCL", 5: "ERANGE", 6: "ESTATE",
           7: "ENOTFOUND", 8: "EINTERNAL"}
@@ -135,6 +136,15 @@ SIGNATURES = {
                                         C.POINTER(_vp)]),
     "dccrgx_poisson_destroy": (C.c_int, [_vp]),
     "dccrgx_poisson_field": (C.c_int, [_vp, C.c_int32, _i32p]),
+    "dccrgx_refine_completely": (C.c_int, [_vp, C.c_uint64, _i32p]),
+    "dccrgx_unrefine_completely": (C.c_int, [_vp, C.c_uint64, _i32p]),
+    "dccrgx_dont_unrefine": (C.c_int, [_vp, C.c_uint64, _i32p]),
+    "dccrgx_dont_refine": (C.c_int, [_vp, C.c_uint64, _i32p]),
+    "dccrgx_amr_requests": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _szp]),
+    "dccrgx_stop_refining": (C.c_int, [_vp, C.POINTER(_u64p), _szp, _szp]),
+    "dccrgx_get_new_cells": (C.c_int, [_vp, _u64p, C.c_size_t, _szp]),
+    "dccrgx_get_removed_cells": (C.c_int, [_vp, _u64p, C.c_size_t, _szp]),
+    "dccrgx_clear_refined_unrefined_data": (C.c_int, [_vp]),
     "dccrgx_poisson_solve": (C.c_int, [_vp, _u64p, C.c_size_t, _u64p, C.c_size_t, C.c_int32,
                                        C.POINTER(C.c_uint32), C.POINTER(C.c_double)]),
 }

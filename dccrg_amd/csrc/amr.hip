@@ -1,0 +1,642 @@
+// amr.hip -- adaptive mesh refinement: the reference's request calls and
+// stop_refining (dccrg.hpp:2456-2806, 3483-3543, 5550-5567, 9730-10693), with
+// the grid rebuilt on the device around the new leaf set.
+//
+// Requests are kept per rank exactly as the reference keeps them
+// (cells_to_refine, cells_not_to_refine, cells_to_unrefine,
+// cells_not_to_unrefine) and filtered at request time with this rank's state.
+// stop_refining takes the union of every rank's four sets (the caller
+// all-gathers them: MPI in the C++ facade, torch.distributed or an in-process
+// loop in Python) and evaluates override_refines, induce_refines and
+// override_unrefines on the replicated leaf set -- every rank reaches the same
+// decision, which the reference reaches by All_Gather after each phase.  The
+// leaf set is then updated (execute_refines, :10243-10693) and the device
+// structures are rebuilt: leaf hash, per-level table, neighbors_of / _to of
+// every leaf, stencil rows, per-rank lists and halo plans of every
+// neighborhood (the reference's full rebuild, :10642-10690).  Field data moves
+// to the new slots with one device scatter per field; new cells (children of
+// refined cells, parents of unrefined ones) are zero-initialised
+// (value-initialised Cell_Data, :10375, :10590).  The data of refined parents
+// and removed children stays readable until clear_refined_unrefined_data.
+//
+// Ownership needs no migration: without load balancing every cell stays on
+// the process of its level-0 ancestor (children on the parent's process,
+// :10368; parent on its first child's process, :10437).
+#include <algorithm>
+#include <cstring>
+#include <unordered_set>
+
+#include "face.hpp"
+#include "grid.hpp"
+
+namespace dccrgx {
+
+namespace {
+
+struct View {
+    const dccrgx_grid* g;
+    const Explicit* E;
+    int M;
+
+    int level(uint64_t c) const { return map_level(g->map, c); }
+    bool exists(uint64_t c) const { return std::binary_search(E->leaves.begin(), E->leaves.end(), c); }
+    int64_t gidx(uint64_t c) const
+    {
+        auto it = std::lower_bound(E->leaves.begin(), E->leaves.end(), c);
+        return (it != E->leaves.end() && *it == c) ? (int64_t)(it - E->leaves.begin()) : -1;
+    }
+    int owner(uint64_t c) const
+    {
+        uint64_t idx[3];
+        int l;
+        map_indices(g->map, c, idx, &l);
+        return part_owner(E->part, map_cell(g->map, idx, 0));
+    }
+    bool local(uint64_t c) const { return owner(c) == g->ctx->rank; }
+    uint64_t parent(uint64_t c) const
+    {
+        uint64_t idx[3];
+        int l;
+        if (!map_indices(g->map, c, idx, &l)) return 0;
+        return l == 0 ? c : map_cell(g->map, idx, l - 1);
+    }
+    // dccrg_mapping.hpp:392-442 (x fastest, then y, z)
+    void children(uint64_t c, uint64_t out[8]) const
+    {
+        uint64_t idx[3];
+        int l;
+        for (int i = 0; i < 8; i++) out[i] = 0;
+        if (!map_indices(g->map, c, idx, &l) || l >= M) return;
+        const uint64_t h = (uint64_t)1 << (M - l - 1);
+        int i = 0;
+        for (int dz = 0; dz < 2; dz++)
+            for (int dy = 0; dy < 2; dy++)
+                for (int dx = 0; dx < 2; dx++) {
+                    const uint64_t ci[3] = {idx[0] + dx * h, idx[1] + dy * h, idx[2] + dz * h};
+                    out[i++] = map_cell(g->map, ci, l + 1);
+                }
+    }
+    // dccrg_mapping.hpp:450-471
+    void siblings(uint64_t c, uint64_t out[8]) const
+    {
+        const int l = level(c);
+        for (int i = 0; i < 8; i++) out[i] = 0;
+        if (l < 0) return;
+        if (l == 0) {
+            out[0] = c;
+            return;
+        }
+        children(parent(c), out);
+    }
+    // c != get_child(c), dccrg.hpp:9694-9718
+    bool has_children(uint64_t c) const
+    {
+        const int l = level(c);
+        if (l == M) return !exists(c);
+        uint64_t idx[3];
+        int ll;
+        map_indices(g->map, c, idx, &ll);
+        if (exists(map_cell(g->map, idx, l + 1))) return true;
+        return !exists(c);
+    }
+    // neighbors_of / neighbors_to of an existing leaf (default neighborhood)
+    template <class F>
+    void for_nof(uint64_t c, F f) const
+    {
+        const auto& L = E->hl.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
+        const int64_t r = gidx(c);
+        if (r < 0) return;
+        for (uint64_t e = L.h_nof_row[r]; e < L.h_nof_row[r + 1]; e++) f(E->leaves[L.h_nof_g[e]]);
+    }
+    template <class F>
+    void for_nto(uint64_t c, F f) const
+    {
+        const auto& L = E->hl.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
+        const int64_t r = gidx(c);
+        if (r < 0) return;
+        for (uint64_t e = L.h_nto_row[r]; e < L.h_nto_row[r + 1]; e++) f(E->leaves[L.h_nto_g[e]]);
+    }
+    // the face graph neighbors_ of a leaf (update_neighbors_, :9463-9597)
+    void face(uint64_t c, uint64_t out[6]) const
+    {
+        int32_t per[3];
+        for (int d = 0; d < 3; d++) per[d] = g->params.periodic[d] ? 1 : 0;
+        face_graph(g->map, per, c, out, [this](uint64_t x) { return exists(x); });
+    }
+    // dccrg.hpp:11364-11405
+    int overlapping_indices(uint64_t c1, uint64_t c2) const
+    {
+        uint64_t i1[3], i2[3];
+        int l1, l2;
+        map_indices(g->map, c1, i1, &l1);
+        map_indices(g->map, c2, i2, &l2);
+        const uint64_t s1 = (uint64_t)1 << (M - l1), s2 = (uint64_t)1 << (M - l2);
+        int r = 0;
+        for (int d = 0; d < 3; d++) r += (i1[d] + s1 > i2[d] && i1[d] < i2[d] + s2) ? 1 : 0;
+        return r;
+    }
+    // dccrg.hpp:9603-9683
+    bool is_neighbor(uint64_t c1, uint64_t c2) const
+    {
+        uint64_t i1[3], i2[3];
+        int l1, l2;
+        map_indices(g->map, c1, i1, &l1);
+        map_indices(g->map, c2, i2, &l2);
+        const uint64_t len1 = (uint64_t)1 << (M - l1), len2 = (uint64_t)1 << (M - l2);
+        uint64_t maxd = 0;
+        for (int d = 0; d < 3; d++) {
+            const uint64_t G = g->map.length[d] << M;
+            uint64_t dist;
+            if (i1[d] <= i2[d]) {
+                dist = i2[d] <= i1[d] + len1 ? 0 : i2[d] - (i1[d] + len1);
+                if (g->params.periodic[d]) dist = std::min(dist, i1[d] + (G - (i2[d] + len2)));
+            } else {
+                dist = i1[d] <= i2[d] + len2 ? 0 : i1[d] - (i2[d] + len2);
+                if (g->params.periodic[d]) dist = std::min(dist, i2[d] + (G - (i1[d] + len1)));
+            }
+            maxd = std::max(maxd, dist);
+        }
+        const uint64_t hl = g->params.neighborhood_length;
+        if (hl == 0) return maxd < len1 && overlapping_indices(c1, c2) >= 2;
+        return maxd < hl * len1;
+    }
+    // leaves overlapping the neighborhood windows of a non-existing parent:
+    // the intent of find_neighbors_of(parent) in unrefine_completely
+    // (:2561-2580, :2638-2670; see oracle/dccrg_amr.py for why it is restated)
+    void parent_window_leaves(uint64_t parent, std::vector<uint64_t>& out) const
+    {
+        out.clear();
+        const Hood& h = g->hoods.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
+        uint64_t pi[3];
+        int pl;
+        map_indices(g->map, parent, pi, &pl);
+        const int64_t L = (int64_t)1 << (M - pl);
+        std::vector<uint64_t> stack;
+        for (size_t k = 0; k + 2 < h.items.size(); k += 3) {
+            uint64_t wi[3];
+            bool ok = true;
+            for (int d = 0; d < 3; d++) {
+                const int64_t G = (int64_t)(g->map.length[d] << M);
+                int64_t x = (int64_t)pi[d] + (int64_t)h.items[k + d] * L;
+                if (x < 0 || x >= G) {
+                    if (!g->params.periodic[d]) {
+                        ok = false;
+                        break;
+                    }
+                    x %= G;
+                    if (x < 0) x += G;
+                }
+                wi[d] = (uint64_t)x;
+            }
+            if (!ok) continue;
+            const uint64_t W = map_cell(g->map, wi, pl);
+            if (exists(W)) {
+                out.push_back(W);
+                continue;
+            }
+            if (pl > 0) {
+                const uint64_t Pw = map_cell(g->map, wi, pl - 1);
+                if (exists(Pw)) {
+                    out.push_back(Pw);
+                    continue;
+                }
+            }
+            stack.assign(1, W);
+            while (!stack.empty()) {
+                const uint64_t w = stack.back();
+                stack.pop_back();
+                if (exists(w)) {
+                    out.push_back(w);
+                    continue;
+                }
+                if (level(w) >= M) continue;
+                uint64_t ch[8];
+                children(w, ch);
+                for (uint64_t x : ch) stack.push_back(x);
+            }
+        }
+    }
+};
+
+Amr& amr_of(dccrgx_grid* grid)
+{
+    if (!grid->amr) grid->amr = new Amr();
+    return *grid->amr;
+}
+
+__global__ void __launch_bounds__(256) k_level0_ids(uint64_t* __restrict__ out, uint64_t n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = i + 1;
+}
+
+// Rebuild the grid on an ascending leaf list: device leaf state, every
+// neighborhood, and every field moved to the new slots (slot s of the new
+// layout takes old slot src[s]; -1 = zero).  `retired` cells (ascending) get
+// slots n + i and keep their old data.
+int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired)
+{
+    Ctx* ctx = grid->ctx;
+    hipStream_t st = ctx->compute;
+    for (const Field& F : grid->fields)
+        DX_CHECK(!F.variable, DCCRGX_EINVAL, "refinement of grids with variable-size fields is not supported");
+    for (auto& kv : grid->hoods) DX_CHECK(!kv.second.pending, DCCRGX_ESTATE, "a halo update is in progress");
+    DX_HIP(hipStreamSynchronize(st));
+    DX_HIP(hipStreamSynchronize(ctx->comm));
+    const uint64_t n = leaves.size(), nr = retired.size(), ns = n + nr;
+    // old slot of every new slot, from the old layout's own lookup
+    std::vector<uint64_t> sidx, didx;
+    sidx.reserve(ns);
+    didx.reserve(ns);
+    auto add = [&](uint64_t id, uint64_t to) {
+        const int64_t s = host_primary_slot(grid, id);
+        if (s >= 0) {
+            sidx.push_back((uint64_t)s);
+            didx.push_back(to);
+        }
+    };
+    for (uint64_t i = 0; i < n; i++) add(leaves[i], i);
+    for (uint64_t i = 0; i < nr; i++) add(retired[i], n + i);
+    uint64_t *d_s = nullptr, *d_d = nullptr;
+    DX_HIP(hipMalloc(&d_s, std::max<size_t>(sidx.size(), 1) * 8));
+    DX_HIP(hipMalloc(&d_d, std::max<size_t>(didx.size(), 1) * 8));
+    if (!sidx.empty()) {
+        DX_HIP(hipMemcpyAsync(d_s, sidx.data(), sidx.size() * 8, hipMemcpyHostToDevice, st));
+        DX_HIP(hipMemcpyAsync(d_d, didx.data(), didx.size() * 8, hipMemcpyHostToDevice, st));
+    }
+    int s = DCCRGX_OK;
+    for (Field& F : grid->fields) {
+        void* np = nullptr;
+        if (hipMalloc(&np, std::max<uint64_t>(ns, 1) * F.elem) != hipSuccess) {
+            s = set_error(DCCRGX_EHIP, "out of device memory for a refined field");
+            break;
+        }
+        hipMemsetAsync(np, 0, std::max<uint64_t>(ns, 1) * F.elem, st);
+        if (!sidx.empty()) s = launch_scatter_ext(F.ptr, d_s, d_d, sidx.size(), F.elem, np, st);
+        hipStreamSynchronize(st);
+        hipFree(F.ptr);
+        F.ptr = np;
+        if (s != DCCRGX_OK) break;
+    }
+    hipFree(d_s);
+    hipFree(d_d);
+    DX_TRY(s);
+    // new leaf state and neighborhoods
+    for (auto& kv : grid->hoods) free_hood(kv.second);
+    if (grid->ex) explicit_destroy(grid);
+    grid->uniform = false;
+    DX_TRY(explicit_init(grid, leaves.data(), n));
+    grid->ex->retired = retired;
+    grid->n_slots = ns;
+    for (auto& kv : grid->hoods) DX_TRY(explicit_build_hood(grid, kv.second));
+    return DCCRGX_OK;
+}
+
+// refinement requests need the explicit form (neighbor lists of every leaf on
+// the host); a uniform grid is converted on its first request
+int ensure_explicit(dccrgx_grid* grid)
+{
+    if (!grid->uniform) return DCCRGX_OK;
+    const uint64_t N = grid->g.N;
+    DX_CHECK(N < (1ull << 32), DCCRGX_EINVAL, "grid of %llu cells is too large to refine",
+             (unsigned long long)N);
+    std::vector<uint64_t> leaves(N);
+    for (uint64_t i = 0; i < N; i++) leaves[i] = i + 1;
+    return rebuild(grid, leaves, {});
+}
+
+}  // namespace
+
+void amr_destroy(dccrgx_grid* grid)
+{
+    delete grid->amr;
+    grid->amr = nullptr;
+}
+
+}  // namespace dccrgx
+
+using namespace dccrgx;
+
+extern "C" {
+
+int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
+{
+    DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
+    *result = 0;
+    if (cell == 0) return DCCRGX_OK;
+    if (grid->map.max_lvl == 0 && grid->uniform) {  // level == max: dont_unrefine, a no-op at level 0
+        *result = map_level(grid->map, cell) == 0 && cell <= grid->g.N &&
+                  part_owner(grid->g.part, cell) == grid->ctx->rank;
+        return DCCRGX_OK;
+    }
+    DX_TRY(ensure_explicit(grid));
+    const View v{grid, grid->ex, grid->map.max_lvl};
+    Amr& A = amr_of(grid);
+    // dccrg.hpp:2476-2546
+    if (!v.exists(cell) || !v.local(cell)) return DCCRGX_OK;
+    const int lvl = v.level(cell);
+    if (lvl == v.M) return dccrgx_dont_unrefine(grid, cell, result);
+    if (A.not_to_refine.count(cell)) return DCCRGX_OK;
+    bool blocked = false;
+    v.for_nof(cell, [&](uint64_t n) { blocked |= v.level(n) < lvl && A.not_to_refine.count(n) > 0; });
+    if (blocked) return DCCRGX_OK;
+    A.to_refine.insert(cell);
+    uint64_t sib[8];
+    v.siblings(cell, sib);
+    for (uint64_t s : sib)
+        if (s) A.to_unrefine.erase(s);
+    auto unmark = [&](uint64_t n) {
+        if (v.level(n) > lvl) return;
+        uint64_t ns[8];
+        v.siblings(n, ns);
+        for (uint64_t s : ns)
+            if (s) A.to_unrefine.erase(s);
+    };
+    v.for_nof(cell, unmark);
+    v.for_nto(cell, unmark);
+    *result = 1;
+    return DCCRGX_OK;
+}
+
+int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
+{
+    DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
+    *result = 0;
+    if (cell == 0) return DCCRGX_OK;
+    if (grid->uniform) {  // every cell is at level 0: true for existing local cells (:2600-2602)
+        *result = map_level(grid->map, cell) == 0 && cell <= grid->g.N &&
+                  part_owner(grid->g.part, cell) == grid->ctx->rank;
+        return DCCRGX_OK;
+    }
+    const View v{grid, grid->ex, grid->map.max_lvl};
+    Amr& A = amr_of(grid);
+    // dccrg.hpp:2596-2675
+    if (!v.exists(cell) || !v.local(cell)) return DCCRGX_OK;
+    *result = 1;
+    if (v.level(cell) == 0) return DCCRGX_OK;
+    uint64_t sib[8];
+    v.siblings(cell, sib);
+    for (uint64_t s : sib) {
+        if (v.has_children(s)) {
+            *result = 0;
+            return DCCRGX_OK;
+        }
+        if (A.to_refine.count(s) || A.not_to_unrefine.count(s)) return DCCRGX_OK;
+    }
+    const uint64_t parent = v.parent(cell);
+    const int plvl = v.level(parent);
+    std::vector<uint64_t> nb;
+    v.parent_window_leaves(parent, nb);
+    for (uint64_t n : nb) {
+        const int nl = v.level(n);
+        if (nl > plvl + 1) return DCCRGX_OK;
+        if (nl == plvl + 1 && A.to_refine.count(n)) return DCCRGX_OK;
+    }
+    for (uint64_t s : sib)
+        if (A.to_unrefine.count(s)) return DCCRGX_OK;
+    A.to_unrefine.insert(cell);
+    return DCCRGX_OK;
+}
+
+int dccrgx_dont_unrefine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
+{
+    DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
+    *result = 0;
+    if (cell == 0) return DCCRGX_OK;
+    if (grid->uniform) {  // level 0: true for any existing cell (:2731-2733)
+        *result = map_level(grid->map, cell) == 0 && cell <= grid->g.N;
+        return DCCRGX_OK;
+    }
+    const View v{grid, grid->ex, grid->map.max_lvl};
+    Amr& A = amr_of(grid);
+    // dccrg.hpp:2715-2759
+    if (!v.exists(cell)) return DCCRGX_OK;
+    *result = 1;
+    if (v.level(cell) == 0) return DCCRGX_OK;
+    uint64_t sib[8];
+    v.siblings(cell, sib);
+    for (uint64_t s : sib)
+        if (A.not_to_unrefine.count(s)) return DCCRGX_OK;
+    for (uint64_t s : sib) A.to_unrefine.erase(s);
+    A.not_to_unrefine.insert(cell);
+    return DCCRGX_OK;
+}
+
+int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
+{
+    DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
+    *result = 0;
+    if (cell == 0) return DCCRGX_OK;
+    const int lvl = map_level(grid->map, cell);
+    if (grid->uniform) {
+        if (lvl != 0 || cell > grid->g.N) return DCCRGX_OK;
+    } else if (!View{grid, grid->ex, grid->map.max_lvl}.exists(cell)) {
+        return DCCRGX_OK;
+    }
+    // dccrg.hpp:2782-2805
+    *result = 1;
+    if (lvl == grid->map.max_lvl) return DCCRGX_OK;
+    Amr& A = amr_of(grid);
+    A.to_refine.erase(cell);
+    A.not_to_refine.insert(cell);
+    return DCCRGX_OK;
+}
+
+int dccrgx_amr_requests(const dccrgx_grid* grid, int32_t which, uint64_t* ids, size_t cap, size_t* n)
+{
+    DX_CHECK(grid && n && which >= 0 && which < 4, DCCRGX_EINVAL, "bad argument");
+    *n = 0;
+    if (!grid->amr) return DCCRGX_OK;
+    const Amr& A = *grid->amr;
+    const std::set<uint64_t>& s = which == DCCRGX_AMR_REFINE       ? A.to_refine
+                                  : which == DCCRGX_AMR_DONT_REFINE ? A.not_to_refine
+                                  : which == DCCRGX_AMR_UNREFINE    ? A.to_unrefine
+                                                                    : A.not_to_unrefine;
+    *n = s.size();
+    if (!ids) return DCCRGX_OK;
+    DX_CHECK(cap >= s.size(), DCCRGX_ERANGE, "capacity %zu < %zu", cap, s.size());
+    std::copy(s.begin(), s.end(), ids);
+    return DCCRGX_OK;
+}
+
+int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const size_t* counts, size_t* n_new)
+{
+    DX_CHECK(grid && sets && counts, DCCRGX_EINVAL, "null argument");
+    for (int k = 0; k < 4; k++) DX_CHECK(sets[k] || !counts[k], DCCRGX_EINVAL, "null request set %d", k);
+    Amr& A = amr_of(grid);
+    A.new_cells.clear();
+    A.removed.clear();
+    if (n_new) *n_new = 0;
+    std::set<uint64_t> R(sets[0], sets[0] + counts[0]), NR(sets[1], sets[1] + counts[1]);
+    std::set<uint64_t> U(sets[2], sets[2] + counts[2]), NU(sets[3], sets[3] + counts[3]);
+    if (grid->uniform && R.empty() && U.empty()) {
+        // nothing can change; on a level-0 grid the dont_refine closure is the
+        // set itself, and it persists (:10188)
+        A.to_refine.clear();
+        A.to_unrefine.clear();
+        A.not_to_unrefine.clear();
+        A.not_to_refine = NR;
+        return DCCRGX_OK;
+    }
+    DX_TRY(ensure_explicit(grid));
+    const View v{grid, grid->ex, grid->map.max_lvl};
+
+    // override_refines, dccrg.hpp:10130-10236: dont_refine spreads to every
+    // finer cell among the neighbors of a dont_refine cell, transitively
+    std::set<uint64_t> donts;
+    std::vector<uint64_t> frontier;
+    for (uint64_t c : NR)
+        if (donts.insert(c).second) frontier.push_back(c);
+    while (!frontier.empty()) {
+        std::vector<uint64_t> next;
+        for (uint64_t c : frontier) {
+            if (!v.exists(c)) continue;
+            const int cl = v.level(c);
+            auto spread = [&](uint64_t n) {
+                if (v.level(n) > cl && donts.insert(n).second) next.push_back(n);
+            };
+            v.for_nof(c, spread);
+            v.for_nto(c, spread);
+        }
+        frontier.swap(next);
+    }
+    for (uint64_t c : donts) R.erase(c);
+
+    // induce_refines, dccrg.hpp:9730-9907: every coarser neighbor (of / to)
+    // of a refined cell is refined, transitively
+    frontier.assign(R.begin(), R.end());
+    while (!frontier.empty()) {
+        std::vector<uint64_t> next;
+        for (uint64_t r : frontier) {
+            const int rl = v.level(r);
+            auto induce = [&](uint64_t n) {
+                if (v.level(n) < rl && R.insert(n).second) next.push_back(n);
+            };
+            v.for_nof(r, induce);
+            v.for_nto(r, induce);
+        }
+        frontier.swap(next);
+    }
+
+    // override_unrefines, dccrg.hpp:9935-10124
+    std::set<uint64_t> final_un;
+    for (uint64_t u : U) {
+        const uint64_t parent = v.parent(u);
+        uint64_t sib[8];
+        v.children(parent, sib);
+        bool can = true;
+        for (uint64_t s : sib)
+            if (s && (R.count(s) || NU.count(s))) can = false;
+        if (!can) continue;
+        const int ul = v.level(u);
+        std::set<uint64_t> processed, process;
+        uint64_t f6[6];
+        v.face(u, f6);
+        for (uint64_t x : f6)
+            if (x) process.insert(x);
+        while (!process.empty()) {
+            const uint64_t next = *process.begin();
+            processed.insert(next);
+            process.erase(process.begin());
+            v.face(next, f6);
+            for (uint64_t x : f6) {
+                if (!x || processed.count(x)) continue;
+                if (v.is_neighbor(parent, x)) process.insert(x);
+                else processed.insert(x);
+            }
+            const int rl = v.level(next);
+            if (rl < ul) continue;
+            if (rl == ul) {
+                if (R.count(next)) {
+                    can = false;
+                    break;
+                }
+                continue;
+            }
+            can = false;
+            break;
+        }
+        if (can) final_un.insert(u);
+    }
+
+    // execute_refines, dccrg.hpp:10243-10693
+    const Explicit* E = grid->ex;
+    std::unordered_set<uint64_t> gone;
+    std::vector<uint64_t> added, retired;
+    for (uint64_t r : R) {
+        uint64_t ch[8];
+        v.children(r, ch);
+        gone.insert(r);
+        added.insert(added.end(), ch, ch + 8);
+        if (v.local(r)) {
+            A.new_cells.insert(A.new_cells.end(), ch, ch + 8);
+            retired.push_back(r);
+        }
+    }
+    std::set<uint64_t> parents;
+    for (uint64_t u : final_un) {
+        const uint64_t p = v.parent(u);
+        if (!parents.insert(p).second) continue;
+        uint64_t ch[8];
+        v.children(p, ch);
+        for (uint64_t c : ch) {
+            gone.insert(c);
+            if (v.local(c)) {  // the parent is local too (same level-0 ancestor)
+                A.removed.push_back(c);
+                retired.push_back(c);
+            }
+        }
+        added.push_back(p);
+    }
+    std::vector<uint64_t> leaves;
+    leaves.reserve(E->leaves.size() + added.size());
+    for (uint64_t c : E->leaves)
+        if (!gone.count(c)) leaves.push_back(c);
+    leaves.insert(leaves.end(), added.begin(), added.end());
+    std::sort(leaves.begin(), leaves.end());
+    leaves.erase(std::unique(leaves.begin(), leaves.end()), leaves.end());
+    std::sort(retired.begin(), retired.end());
+    std::sort(A.new_cells.begin(), A.new_cells.end());
+    std::sort(A.removed.begin(), A.removed.end());
+    // the dont_refine closure persists (:10188), everything else is consumed
+    A.to_refine.clear();
+    A.to_unrefine.clear();
+    A.not_to_unrefine.clear();
+    A.not_to_refine = donts;
+    if (!R.empty() || !final_un.empty()) {
+        if (grid->ex) grid->ex->retired.clear();
+        DX_TRY(rebuild(grid, leaves, retired));
+    }
+    if (n_new) *n_new = A.new_cells.size();
+    return DCCRGX_OK;
+}
+
+int dccrgx_get_new_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, size_t* n)
+{
+    DX_CHECK(grid && n, DCCRGX_EINVAL, "null argument");
+    *n = grid->amr ? grid->amr->new_cells.size() : 0;
+    if (!ids || !*n) return DCCRGX_OK;
+    DX_CHECK(cap >= *n, DCCRGX_ERANGE, "capacity %zu < %zu", cap, *n);
+    std::copy(grid->amr->new_cells.begin(), grid->amr->new_cells.end(), ids);
+    return DCCRGX_OK;
+}
+
+int dccrgx_get_removed_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, size_t* n)
+{
+    DX_CHECK(grid && n, DCCRGX_EINVAL, "null argument");
+    *n = grid->amr ? grid->amr->removed.size() : 0;
+    if (!ids || !*n) return DCCRGX_OK;
+    DX_CHECK(cap >= *n, DCCRGX_ERANGE, "capacity %zu < %zu", cap, *n);
+    std::copy(grid->amr->removed.begin(), grid->amr->removed.end(), ids);
+    return DCCRGX_OK;
+}
+
+int dccrgx_clear_refined_unrefined_data(dccrgx_grid* grid)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    if (grid->ex) grid->ex->retired.clear();
+    if (grid->amr) grid->amr->removed.clear();
+    return DCCRGX_OK;
+}
+
+}  // extern "C"

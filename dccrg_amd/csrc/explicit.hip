@@ -24,29 +24,6 @@
 
 namespace dccrgx {
 
-struct Explicit {
-    uint64_t n = 0;                 // global leaves
-    std::vector<uint64_t> leaves;   // ascending
-    uint64_t* d_leaves = nullptr;
-    uint64_t* d_keys = nullptr;     // hash keys (0 = empty)
-    uint32_t* d_vals = nullptr;     // global index
-    uint64_t mask = 0;
-    Partition part;                 // over level-0 cells
-    std::vector<uint64_t> local;    // ascending local ids
-    std::vector<uint32_t> local_g;  // their global indices
-    uint32_t* d_local_g = nullptr;
-    uint8_t* d_level = nullptr;     // refinement level of each leaf (global index)
-    struct HoodLists {
-        std::vector<uint64_t> h_nof_row, h_nto_row;
-        std::vector<uint32_t> h_nof_g, h_nto_g;
-        std::vector<uint32_t> inner_pos, outer_pos;  // positions in `local`
-        uint32_t* d_inner_pos = nullptr;
-        uint32_t* d_outer_pos = nullptr;
-        uint32_t* d_all_pos = nullptr;
-    };
-    std::map<int32_t, HoodLists> hl;
-};
-
 struct ExView {
     MapParams mp;
     const uint64_t* keys;
@@ -402,7 +379,7 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     return DCCRGX_OK;
 }
 
-int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
+int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
 {
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
@@ -447,6 +424,12 @@ int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     grid->n_local = E->local.size();
     grid->first_local = E->local.empty() ? 0 : E->local[0];
     grid->n_slots = E->n;
+    return DCCRGX_OK;
+}
+
+int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
+{
+    DX_TRY(explicit_init(grid, leaves, n));
     Hood h;
     h.id = DCCRGX_DEFAULT_NEIGHBORHOOD_ID;
     // default items, dccrg.hpp:8017-8076
@@ -669,7 +652,11 @@ int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id)
 {
     const auto& L = grid->ex->leaves;
     auto it = std::lower_bound(L.begin(), L.end(), id);
-    return (it != L.end() && *it == id) ? (int64_t)(it - L.begin()) : -1;
+    if (it != L.end() && *it == id) return (int64_t)(it - L.begin());
+    // data of a refined / unrefined cell kept until clear_refined_unrefined_data
+    const auto& R = grid->ex->retired;
+    auto jt = std::lower_bound(R.begin(), R.end(), id);
+    return (jt != R.end() && *jt == id) ? (int64_t)(L.size() + (jt - R.begin())) : -1;
 }
 
 int explicit_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int64_t* slots, hipStream_t st)

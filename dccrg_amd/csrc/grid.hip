@@ -650,6 +650,7 @@ int dccrgx_grid_destroy(dccrgx_grid* grid)
     for (auto& kv : grid->hoods) free_hood(kv.second);
     for (Field& f : grid->fields) hipFree(f.ptr);
     if (!grid->uniform) explicit_destroy(grid);
+    amr_destroy(grid);
     hipEventDestroy(grid->t0);
     hipEventDestroy(grid->t1);
     delete grid;

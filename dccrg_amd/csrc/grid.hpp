@@ -4,6 +4,8 @@
 
 #include "internal.hpp"
 
+#include <set>
+
 namespace dccrgx {
 
 // Canonical axes (A fastest, C slowest with extent > 1 unless 1-D) so that
@@ -116,7 +118,41 @@ struct PeerPlan {
     size_t recv_buf_bytes = 0;
 };
 
-struct Explicit;  // explicit.hip
+struct Explicit {
+    uint64_t n = 0;                 // global leaves
+    std::vector<uint64_t> leaves;   // ascending
+    uint64_t* d_leaves = nullptr;
+    uint64_t* d_keys = nullptr;     // hash keys (0 = empty)
+    uint32_t* d_vals = nullptr;     // global index
+    uint64_t mask = 0;
+    Partition part;                 // over level-0 cells
+    std::vector<uint64_t> local;    // ascending local ids
+    std::vector<uint32_t> local_g;  // their global indices
+    uint32_t* d_local_g = nullptr;
+    uint8_t* d_level = nullptr;     // refinement level of each leaf (global index)
+    struct HoodLists {
+        std::vector<uint64_t> h_nof_row, h_nto_row;
+        std::vector<uint32_t> h_nof_g, h_nto_g;
+        std::vector<uint32_t> inner_pos, outer_pos;  // positions in `local`
+        uint32_t* d_inner_pos = nullptr;
+        uint32_t* d_outer_pos = nullptr;
+        uint32_t* d_all_pos = nullptr;
+    };
+    std::map<int32_t, HoodLists> hl;
+    // data of cells removed by the last stop_refining (refined parents and
+    // unrefined children of this rank), readable until
+    // clear_refined_unrefined_data (dccrg.hpp:3519-3543, 5550-5567): ascending
+    // ids, stored at slots n + i of every field
+    std::vector<uint64_t> retired;
+};
+
+// pending refinement requests of this rank and the results of the last
+// stop_refining (dccrg.hpp:7355-7360, 3483-3543)
+struct Amr {
+    std::set<uint64_t> to_refine, not_to_refine, to_unrefine, not_to_unrefine;
+    std::vector<uint64_t> new_cells, removed;
+};
+
 
 struct CopySeg {
     uint64_t dst, src, n;  // contiguous slot run
@@ -191,6 +227,8 @@ struct dccrgx_grid {
     std::map<int32_t, dccrgx::Hood> hoods;
     // explicit grids (explicit.hip)
     dccrgx::Explicit* ex = nullptr;
+    // refinement requests and results (amr.hip)
+    dccrgx::Amr* amr = nullptr;
     // kernel timing (dccrgx_kernel_timer)
     hipEvent_t t0 = nullptr, t1 = nullptr;
     double timed_ms = 0;
@@ -222,6 +260,12 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h);
 int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, uint64_t* ids,
                        size_t cap, size_t* n);
 int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device);
+// explicit grid state over an ascending leaf list (no neighborhoods built)
+int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n);
+int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id);
+// the slot read and written for a cell on this rank (-1: none), halo.hip
+int64_t host_primary_slot(const dccrgx_grid* grid, uint64_t id);
+void amr_destroy(dccrgx_grid* grid);
 int launch_gather_ext(const void* src, const uint64_t* idx, uint64_t n, uint32_t elem, void* dst,
                       hipStream_t st);
 int launch_scatter_ext(const void* src, const uint64_t* sidx, const uint64_t* didx, uint64_t n,

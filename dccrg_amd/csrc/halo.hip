@@ -342,6 +342,8 @@ static int64_t primary_slot(const dccrgx_grid* grid, uint64_t id)
     return ghost_slot(g, id - 1);
 }
 
+int64_t host_primary_slot(const dccrgx_grid* grid, uint64_t id) { return primary_slot(grid, id); }
+
 static int halo_finish(dccrgx_grid* grid, Hood& h, const int32_t* f, size_t nf)
 {
     bool var = false;

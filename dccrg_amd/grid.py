@@ -96,6 +96,62 @@ class Mapping:
     def get_last_cell(self) -> int:
         return self.last_cell
 
+    # ---- scalar host calls (dccrg_mapping.hpp:154-503) ----------------------
+    def get_indices(self, cell: int):
+        idx = (C.c_uint64 * 3)()
+        lvl = C.c_int32()
+        check(lib().dccrgx_map_host_indices(C.byref(self._m), C.c_uint64(int(cell)), idx, C.byref(lvl)))
+        return tuple(int(v) for v in idx)
+
+    def get_refinement_level(self, cell: int) -> int:
+        idx = (C.c_uint64 * 3)()
+        lvl = C.c_int32()
+        check(lib().dccrgx_map_host_indices(C.byref(self._m), C.c_uint64(int(cell)), idx, C.byref(lvl)))
+        return lvl.value
+
+    def get_cell_from_indices(self, idx, lvl: int) -> int:
+        a = (C.c_uint64 * 3)(*[int(v) for v in idx])
+        out = C.c_uint64()
+        check(lib().dccrgx_map_host_cell(C.byref(self._m), a, int(lvl), C.byref(out)))
+        return out.value
+
+    def _op(self, op: int, cell: int) -> int:
+        out = C.c_uint64()
+        check(lib().dccrgx_map_host_op(C.byref(self._m), op, C.c_uint64(int(cell)), C.byref(out)))
+        return out.value
+
+    def get_cell_length_in_indices(self, cell: int) -> int:
+        return self._op(X.OP_LENGTH_IN_INDICES, cell)
+
+    def get_parent(self, cell: int) -> int:
+        return self._op(X.OP_PARENT, cell)
+
+    def get_level_0_parent(self, cell: int) -> int:
+        return self._op(X.OP_LEVEL_0_PARENT, cell)
+
+    def get_child(self, cell: int) -> int:
+        return self._op(X.OP_CHILD, cell)
+
+    def get_all_children(self, cell: int):
+        """dccrg_mapping.hpp:392-442: x fastest, then y, z; error_cell x 8
+        for an invalid cell or one at the maximum level."""
+        lvl = self.get_refinement_level(cell)
+        if lvl < 0 or lvl >= self.max_ref_lvl:
+            return [0] * 8
+        i = self.get_indices(cell)
+        h = self.get_cell_length_in_indices(cell) // 2
+        return [self.get_cell_from_indices((i[0] + dx * h, i[1] + dy * h, i[2] + dz * h), lvl + 1)
+                for dz in (0, 1) for dy in (0, 1) for dx in (0, 1)]
+
+    def get_siblings(self, cell: int):
+        """dccrg_mapping.hpp:450-471."""
+        lvl = self.get_refinement_level(cell)
+        if lvl < 0 or lvl > self.max_ref_lvl:
+            return [0] * 8
+        if lvl == 0:
+            return [int(cell)] + [0] * 7
+        return self.get_all_children(self.get_parent(cell))
+
     def ids_to_indices(self, ids, stream: int = 0):
         import torch
         n = ids.numel()
@@ -194,6 +250,81 @@ class Dccrg:
             self.close()
         except Exception:
             pass
+
+    # ---- adaptive mesh refinement (dccrg.hpp:2456-2806, 3483-3543) ---------
+    def _request(self, fn, cell: int) -> bool:
+        r = C.c_int32()
+        check(fn(self._h, C.c_uint64(int(cell)), C.byref(r)))
+        self._refresh_info()  # a uniform grid switches to the explicit layout
+        return bool(r.value)
+
+    def refine_completely(self, cell: int) -> bool:
+        return self._request(lib().dccrgx_refine_completely, cell)
+
+    def unrefine_completely(self, cell: int) -> bool:
+        return self._request(lib().dccrgx_unrefine_completely, cell)
+
+    def dont_unrefine(self, cell: int) -> bool:
+        return self._request(lib().dccrgx_dont_unrefine, cell)
+
+    def dont_refine(self, cell: int) -> bool:
+        return self._request(lib().dccrgx_dont_refine, cell)
+
+    def amr_requests(self):
+        """This rank's four pending request sets (refine, dont_refine,
+        unrefine, dont_unrefine), for the all-gather of stop_refining."""
+        out = []
+        for k in range(4):
+            n = C.c_size_t()
+            check(lib().dccrgx_amr_requests(self._h, k, None, 0, C.byref(n)))
+            a = np.zeros(n.value, dtype=np.uint64)
+            check(lib().dccrgx_amr_requests(self._h, k, a.ctypes.data_as(X._u64p), a.size, C.byref(n)))
+            out.append(a)
+        return out
+
+    def stop_refining(self, sorted: bool = True, all_requests=None) -> np.ndarray:
+        """Collective (dccrg.hpp:3483-3507).  all_requests: the union over all
+        ranks of amr_requests(); gathered with torch.distributed when the
+        grid has several ranks and it is not given."""
+        if all_requests is None:
+            mine = self.amr_requests()
+            if self.ctx.comm_size == 1:
+                all_requests = mine
+            else:
+                import torch.distributed as dist
+                got = [None] * self.ctx.comm_size
+                dist.all_gather_object(got, [a.tolist() for a in mine])
+                all_requests = [np.unique(np.concatenate([np.asarray(g[k], dtype=np.uint64) for g in got]))
+                                for k in range(4)]
+        sets = [_u64(a) for a in all_requests]
+        ptrs = (X._u64p * 4)(*[a.ctypes.data_as(X._u64p) for a in sets])
+        counts = (C.c_size_t * 4)(*[a.size for a in sets])
+        n_new = C.c_size_t()
+        check(lib().dccrgx_stop_refining(self._h, ptrs, counts, C.byref(n_new)))
+        self._refresh_info()
+        return self.get_new_cells()
+
+    def get_new_cells(self) -> np.ndarray:
+        return self._id_list(lib().dccrgx_get_new_cells)
+
+    def get_removed_cells(self, sorted: bool = True) -> np.ndarray:
+        return self._id_list(lib().dccrgx_get_removed_cells)
+
+    def clear_refined_unrefined_data(self):
+        check(lib().dccrgx_clear_refined_unrefined_data(self._h))
+        return self
+
+    def _id_list(self, fn) -> np.ndarray:
+        n = C.c_size_t()
+        check(fn(self._h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint64)
+        check(fn(self._h, out.ctypes.data_as(X._u64p), out.size, C.byref(n)))
+        return out
+
+    def _refresh_info(self):
+        info = X.GridInfo_t()
+        check(lib().dccrgx_grid_get_info(self._h, C.byref(info)))
+        self.info = info
 
     # ---- queries ------------------------------------------------------------
     def get_rank(self) -> int:

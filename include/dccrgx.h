@@ -318,6 +318,42 @@ int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt);
 
 /* ------------------------------------------------------------------------ *
+ * Adaptive mesh refinement (dccrg.hpp:2456-2806, 3483-3543, 5550-5567,
+ * 9730-10693).  Request calls set *result to the reference's bool.  A
+ * uniform grid switches to the explicit (mixed-level) layout on its first
+ * refine request.  stop_refining is collective: every rank passes the union
+ * over all ranks of the four request sets (dccrgx_amr_requests on each rank,
+ * all-gathered by the caller); the library then evaluates override_refines,
+ * induce_refines and override_unrefines on the replicated leaf set and
+ * rebuilds the grid on the device.  Field data of surviving cells moves to
+ * their new slots, new cells are zero-initialised, and the data of refined
+ * parents / removed children stays readable (dccrgx_field_read_cells) until
+ * clear_refined_unrefined_data.  Grids with variable-size fields are refused.
+ * ------------------------------------------------------------------------ */
+enum { DCCRGX_AMR_REFINE = 0, DCCRGX_AMR_DONT_REFINE = 1, DCCRGX_AMR_UNREFINE = 2, DCCRGX_AMR_DONT_UNREFINE = 3 };
+/* Dccrg::refine_completely, dccrg.hpp:2456-2548 */
+int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result);
+/* Dccrg::unrefine_completely, dccrg.hpp:2582-2676 */
+int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result);
+/* Dccrg::dont_unrefine, dccrg.hpp:2701-2760 */
+int dccrgx_dont_unrefine(dccrgx_grid* grid, uint64_t cell, int32_t* result);
+/* Dccrg::dont_refine, dccrg.hpp:2768-2806 */
+int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result);
+/* this rank's pending request set `which` (DCCRGX_AMR_*), ascending; ids == NULL: count only */
+int dccrgx_amr_requests(const dccrgx_grid* grid, int32_t which, uint64_t* ids, size_t cap, size_t* n);
+/* Dccrg::stop_refining, dccrg.hpp:3483-3507: sets[k] / counts[k] = union over
+ * all ranks of request set k; n_new = cells created on this rank */
+int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const size_t* counts,
+                         size_t* n_new);
+/* the cells the last stop_refining created on this rank (ascending; the
+ * reference's return value of stop_refining(true)) */
+int dccrgx_get_new_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, size_t* n);
+/* Dccrg::get_removed_cells(true), dccrg.hpp:3519-3543 */
+int dccrgx_get_removed_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, size_t* n);
+/* Dccrg::clear_refined_unrefined_data, dccrg.hpp:5550-5567 */
+int dccrgx_clear_refined_unrefined_data(dccrgx_grid* grid);
+
+/* ------------------------------------------------------------------------ *
  * Poisson, tests/poisson/poisson_solve.hpp: Poisson_Solve (BiCG over face
  * neighbors, 1/4 weight per smaller face neighbor) with its cell data in the
  * grid's f64 fields.  The solver adds 14 internal fields (Poisson_Cell

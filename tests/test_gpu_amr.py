@@ -1,0 +1,221 @@
+"""GPU parity of adaptive mesh refinement: the library's request calls and
+stop_refining (dccrg.hpp:2456-2806, 3483-3543, 9730-10693) against the CPU
+restatement oracle/dccrg_amr.py on the same request sequences -- request
+return values, leaf sets, new and removed cells per rank, the rebuilt
+neighbor lists and per-rank lists, and the movement of cell data."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import dccrg_amd as D  # noqa: E402
+from oracle import dccrg_oracle as O  # noqa: E402
+from oracle.dccrg_amr import AmrOracle  # noqa: E402
+
+
+def make_ranks(length, M, per, hood, P, leaves=None):
+    grids = []
+    for r in range(P):
+        c = D.Context(0, r, P)
+        g = (D.Dccrg().set_initial_length(length).set_maximum_refinement_level(M).set_periodic(*per)
+             .set_neighborhood_length(hood).initialize(c, leaves=leaves))
+        g._keep = c
+        grids.append(g)
+    return grids
+
+
+def stop_all(grids):
+    reqs = [g.amr_requests() for g in grids]
+    union = [np.unique(np.concatenate([r[k] for r in reqs])).astype(np.uint64) for k in range(4)]
+    return [g.stop_refining(all_requests=union) for g in grids]
+
+
+def all_leaves(grids):
+    return sorted(int(c) for g in grids for c in g.local_cells())
+
+
+def check_structure(grids, o: AmrOracle):
+    assert all_leaves(grids) == o.cells()
+    og = o.grid
+    P = len(grids)
+    for r, g in enumerate(grids):
+        ref = og.rank_view(r, P)
+        loc = [int(c) for c in g.local_cells()]
+        assert loc == ref["local"]
+        assert [int(c) for c in g.inner_cells()] == ref["inner"]
+        assert [int(c) for c in g.outer_cells()] == ref["outer"]
+        assert [int(c) for c in g.remote_cells()] == ref["remote"]
+        if loc:
+            cells = np.array(loc, dtype=np.uint64)
+            row, ids, off = g.neighbors_of(cells)
+            for i, c in enumerate(loc):
+                got = [(int(ids[k]), tuple(int(v) for v in off[k])) for k in range(int(row[i]), int(row[i + 1]))]
+                assert got == og.find_neighbors_of(c), c
+            row, ids = g.neighbors_to(cells)
+            for i, c in enumerate(loc):
+                assert [int(v) for v in ids[int(row[i]):int(row[i + 1])]] == og.find_neighbors_to(c), c
+        assert g.get_cells_to_send() == ref["send"]
+        assert g.get_cells_to_receive() == ref["recv"]
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_dont_refine_cases_on_device(P):
+    """tests/refine/dont_refine.cpp's three scenarios, replayed on the device
+    and on the oracle step by step."""
+    scen = [
+        [("dont_refine", 1), ("refine", 1), "stop"],
+        [("refine", 2), "stop", ("dont_refine", 1), ("refine", 6), "stop", ("dont_refine", 1), ("refine", 7), "stop"],
+        [("refine", 3), "stop", ("dont_refine", 1), ("refine", 8), "stop", ("refine", 37), "stop"],
+    ]
+    for steps in scen:
+        o = AmrOracle((3, 1, 1), -1, hood_length=1, comm_size=P)
+        grids = make_ranks((3, 1, 1), -1, (False, False, False), 1, P)
+        for st in steps:
+            if st == "stop":
+                got = stop_all(grids)
+                want = o.stop_refining()
+                for r in range(P):
+                    assert [int(c) for c in got[r]] == want[r]
+                check_structure(grids, o)
+                continue
+            # every process makes the call, as in the reference test (only the
+            # owner accepts a refine; dont_refine is accepted everywhere)
+            kind, cell = st
+            for rr in range(P):
+                if kind == "refine":
+                    assert grids[rr].refine_completely(cell) == o.refine_completely(rr, cell)
+                else:
+                    assert grids[rr].dont_refine(cell) == o.dont_refine(rr, cell)
+        assert 4 not in o.leaves
+        for g in grids:
+            g.close()
+
+
+SEQ_CASES = [  # length, M, periodic, hood, P, rounds, seed
+    ((4, 3, 2), 2, (False, False, False), 1, 1, 4, 0),
+    ((4, 4, 1), 2, (True, True, False), 1, 2, 4, 1),
+    ((5, 3, 3), 2, (True, False, True), 1, 3, 3, 2),
+    ((4, 4, 2), 2, (False, True, False), 0, 2, 4, 3),
+    ((3, 3, 3), 1, (True, True, True), 2, 2, 3, 4),
+    ((6, 2, 1), 3, (True, False, False), 1, 1, 5, 5),
+]
+
+
+@pytest.mark.parametrize("case", SEQ_CASES)
+def test_random_request_sequences(case):
+    length, M, per, hood, P, rounds, seed = case
+    rng = np.random.default_rng(seed)
+    o = AmrOracle(length, M, per, hood, P)
+    grids = make_ranks(length, M, per, hood, P)
+    for rnd in range(rounds):
+        cells = o.cells()
+        picks = rng.choice(cells, min(len(cells), 8), replace=False)
+        for c in picks:
+            c = int(c)
+            r = o.owner(c)
+            k = int(rng.integers(4)) if rnd > 0 else 0
+            fn = ("refine_completely", "unrefine_completely", "dont_unrefine", "dont_refine")[k]
+            if k == 3 and rng.integers(3):
+                continue  # keep dont_refine rare
+            got = getattr(grids[r], fn)(c)
+            want = getattr(o, fn)(r, c)
+            assert got == want, (fn, c)
+        got = stop_all(grids)
+        want = o.stop_refining()
+        for r in range(P):
+            assert [int(c) for c in got[r]] == want[r]
+            assert [int(c) for c in grids[r].get_removed_cells()] == o.get_removed_cells(r)
+            grids[r].clear_refined_unrefined_data()
+        check_structure(grids, o)
+        assert o.max_level_difference() <= 1
+    for g in grids:
+        g.close()
+
+
+def test_cell_data_moves_with_refinement():
+    """Surviving cells keep their data, new cells start at zero, refined
+    parents and removed children stay readable until
+    clear_refined_unrefined_data (dccrg.hpp:3519-3543, 5550-5567); halos run
+    on the rebuilt plans."""
+    length, M, per = (4, 4, 2), 2, (True, True, False)
+    o = AmrOracle(length, M, per, 1, 2)
+    grids = make_ranks(length, M, per, 1, 2)
+    for g in grids:
+        g.add_field("v", np.float64)
+        loc = g.local_cells()
+        g.write_local("v", loc.astype(np.float64) * 0.5)
+    for c in (6, 11, 27):
+        r = o.owner(c)
+        assert grids[r].refine_completely(c) == o.refine_completely(r, c)
+    new = stop_all(grids)
+    want = o.stop_refining()
+    for r, g in enumerate(grids):
+        assert [int(c) for c in new[r]] == want[r]
+        loc = g.local_cells()
+        vals = g.read_local("v")
+        isnew = np.isin(loc, new[r])
+        assert np.all(vals[isnew] == 0)
+        assert np.array_equal(vals[~isnew], loc[~isnew].astype(np.float64) * 0.5)
+        # refined parents stay readable on their own rank
+        for c in (6, 11, 27):
+            if o.owner(c) == r and int(c) not in o.leaves:
+                assert g.read_cells("v", [c])[0][0] == c * 0.5
+        # children inherit the parent's value, as tests/advection/adapter.hpp:240-262 does
+        par = np.array([g.mapping.get_parent(int(c)) for c in new[r]], dtype=np.uint64)
+        if par.size:
+            g.write_cells("v", new[r], np.concatenate(g.read_cells("v", par)))
+        g.clear_refined_unrefined_data()
+        if par.size:
+            with pytest.raises(D.DccrgxError):
+                g.read_cells("v", par[:1])
+    # halo over the rebuilt plans: ghost values = the owners' values
+    buf = {}
+    for r, g in enumerate(grids):
+        for p, ids in g.get_cells_to_send().items():
+            buf[(r, p)] = dict(zip(ids, np.concatenate(g.read_cells("v", ids))))
+    for r, g in enumerate(grids):
+        for p, ids in g.get_cells_to_receive().items():
+            assert p != r
+            for c in ids:
+                assert c in buf[(p, r)]
+    # unrefine everything back where possible
+    for r, g in enumerate(grids):
+        for c in g.local_cells():
+            if o.level(int(c)) == 1:
+                assert g.unrefine_completely(int(c)) == o.unrefine_completely(r, int(c))
+    stop_all(grids)
+    o.stop_refining()
+    for r, g in enumerate(grids):
+        rem = g.get_removed_cells()
+        assert [int(c) for c in rem] == o.get_removed_cells(r)
+        if rem.size:
+            # removed children still readable; their parents are new (zero) cells
+            assert np.all(np.concatenate(g.read_cells("v", rem)) != 0)
+            par = np.unique([g.mapping.get_parent(int(c)) for c in rem]).astype(np.uint64)
+            assert np.all(np.concatenate(g.read_cells("v", par)) == 0)
+    check_structure(grids, o)
+    for g in grids:
+        g.close()
+
+
+def test_uniform_grid_switches_layout_on_refine():
+    """A grid initialised without a leaf list (uniform layout) keeps its
+    level-0 data when the first refine request converts it."""
+    length, M, per = (6, 5, 4), 1, (False, True, True)
+    o = AmrOracle(length, M, per, 1, 1)
+    (g,) = make_ranks(length, M, per, 1, 1)
+    g.add_field("a", np.uint32)
+    ids = g.local_cells()
+    g.write_local("a", (ids % 7).astype(np.uint32))
+    assert g.info.uniform == 1
+    assert g.refine_completely(33) == o.refine_completely(0, 33)
+    assert g.info.uniform == 0
+    new = g.stop_refining()
+    assert [int(c) for c in new] == o.stop_refining()[0]
+    loc = g.local_cells()
+    vals = g.read_local("a")
+    keep = ~np.isin(loc, new)
+    assert np.array_equal(vals[keep], (loc[keep] % 7).astype(np.uint32))
+    check_structure([g], o)
+    g.close()
