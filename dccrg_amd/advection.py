@@ -1,0 +1,164 @@
+"""The advection test program of the reference (tests/advection/2d.cpp with
+initialize.hpp, solve.hpp and adapter.hpp) over the device grid: the
+per-step solver and the neighbor-difference adaptation run as HIP kernels
+(dccrgx_advect_step, dccrgx_advect_adapt_marks); the refinement decisions
+and the data handed to new cells follow adapter.hpp on the host, as the
+reference does.
+
+Geometry: tests/advection/2d.cpp:200-250 for direction 'z' -- a Cartesian
+geometry starting at 0 with level-0 cell length 1 / cells along every axis
+(z included, :241-243).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Tuple
+
+import numpy as np
+
+from . import _capi as X
+from ._capi import check, lib
+from .grid import Dccrg
+
+
+class CartesianGeometry:
+    """Cartesian_Geometry (dccrg_cartesian_geometry.hpp) for the cell
+    centers and lengths the advection program needs."""
+
+    def __init__(self, grid: Dccrg, start=(0.0, 0.0, 0.0), level_0_cell_length=None):
+        self.grid = grid
+        self.start = np.asarray(start, dtype=np.float64)
+        n = np.asarray(grid._length, dtype=np.float64)
+        self.l0 = np.asarray(level_0_cell_length if level_0_cell_length is not None else 1.0 / n,
+                             dtype=np.float64)
+
+    def centers_and_lengths(self, cells: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        m = self.grid.mapping
+        M = m.max_ref_lvl
+        idx = np.array([m.get_indices(int(c)) for c in cells], dtype=np.float64).reshape(-1, 3)
+        lvl = np.array([m.get_refinement_level(int(c)) for c in cells], dtype=np.float64)
+        ln = self.l0[None, :] / (2.0 ** lvl)[:, None]
+        center = self.start[None, :] + idx * (self.l0 / 2.0 ** M)[None, :] + ln / 2
+        return center, ln
+
+
+def geometry_2d(grid: Dccrg) -> CartesianGeometry:
+    """2d.cpp:238-243 (direction 'z'): start 0, level-0 cell length
+    GRID_END / cells = 1 / cells along x, y and z."""
+    cells = grid._length[0]
+    return CartesianGeometry(grid, (0.0, 0.0, 0.0), [1.0 / cells] * 3)
+
+
+def get_vx(y):  # solve.hpp:336-338
+    return -y + 0.5
+
+
+def get_vy(x):  # solve.hpp:340-342
+    return x - 0.5
+
+
+ALL = ("density", "flux", "vx", "vy", "vz", "length_x", "length_y", "length_z")
+
+
+def initialize(grid: Dccrg, geom: CartesianGeometry):
+    """initialize.hpp:27-65: hump density, solid-body velocities, lengths."""
+    cells = grid.local_cells()
+    center, ln = geom.centers_and_lengths(cells)
+    r = np.minimum(np.sqrt((center[:, 0] - 0.25) ** 2 + (center[:, 1] - 0.5) ** 2), 0.15) / 0.15
+    grid.write_local("density", 0.25 * (1 + np.cos(np.pi * r)))
+    grid.write_local("flux", np.zeros(cells.size))
+    _velocities_lengths(grid, geom, cells, center, ln)
+    grid.update_copies_of_remote_neighbors(fields=list(ALL))
+
+
+def _velocities_lengths(grid, geom, cells, center=None, ln=None):
+    if center is None:
+        center, ln = geom.centers_and_lengths(cells)
+    grid.write_local("vx", get_vx(center[:, 1]))
+    grid.write_local("vy", get_vy(center[:, 0]))
+    grid.write_local("vz", np.zeros(cells.size))
+    grid.write_local("length_x", ln[:, 0])
+    grid.write_local("length_y", ln[:, 1])
+    grid.write_local("length_z", ln[:, 2])
+
+
+def check_for_adaptation(grid: Dccrg, diff_increase: float, diff_threshold: float,
+                         unrefine_sensitivity: float):
+    """adapter.hpp:43-176.  The differences and categories come from the
+    device; the sibling rules of :120-175 are applied per sibling group (their
+    effect does not depend on the order the reference visits cells in).
+    Returns (cells_to_refine, cells_not_to_unrefine, cells_to_unrefine)."""
+    empty = np.zeros(0, dtype=np.uint64)
+    if grid.get_maximum_refinement_level() == 0:
+        return empty, empty, empty
+    n = grid.n_local
+    marks = np.zeros(n, dtype=np.int8)
+    f = grid._advect_fields()
+    check(lib().dccrgx_advect_adapt_marks(grid._h, X.DEFAULT_NEIGHBORHOOD_ID, C.byref(f), diff_increase,
+                                          diff_threshold, unrefine_sensitivity,
+                                          marks.ctypes.data_as(C.POINTER(C.c_int8)), None))
+    grid._refresh_info()
+    cells = grid.local_cells()
+    m = grid.mapping
+    lvl = np.array([m.get_refinement_level(int(c)) for c in cells])
+    group = np.array([m.get_parent(int(c)) if l > 0 else int(c) for c, l in zip(cells, lvl)], dtype=np.uint64)
+    refine = cells[marks == 2]
+    # per sibling group: any refine blocks keep/unrefine marks; any keep (level > 0)
+    # blocks unrefine marks (:126-174)
+    g_ref = set(group[marks == 2].tolist())
+    g_keep = set(group[(marks == 1) & (lvl > 0)].tolist())
+    keep = np.array([c for c, g, mk, l in zip(cells, group, marks, lvl)
+                     if mk == 1 and l > 0 and g not in g_ref], dtype=np.uint64)
+    # one dont_unrefine per group is what the reference leaves behind (:146-155)
+    if keep.size:
+        gk = np.array([m.get_parent(int(c)) for c in keep], dtype=np.uint64)
+        _, first = np.unique(gk, return_index=True)
+        keep = keep[np.sort(first)]
+    unref = np.array([c for c, g, mk, l in zip(cells, group, marks, lvl)
+                      if mk == 0 and l > 0 and g not in g_ref and g not in g_keep], dtype=np.uint64)
+    return refine.astype(np.uint64), keep, unref
+
+
+def _request(grid: Dccrg, kind: int, ids: np.ndarray):
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    check(lib().dccrgx_amr_request_cells(grid._h, kind, ids.ctypes.data_as(X._u64p), ids.size, None))
+
+
+def adapt_grid(grid: Dccrg, geom: CartesianGeometry, to_refine, not_to_unrefine, to_unrefine,
+               all_requests=None) -> Tuple[int, int]:
+    """adapter.hpp:184-319.  Returns (created, removed) cell counts."""
+    if grid.get_maximum_refinement_level() == 0:
+        return 0, 0
+    _request(grid, X.AMR_REFINE, to_refine)
+    _request(grid, X.AMR_DONT_UNREFINE, not_to_unrefine)
+    _request(grid, X.AMR_UNREFINE, to_unrefine)
+    grid._refresh_info()
+    new = grid.stop_refining(all_requests=all_requests)
+    m = grid.mapping
+    # new cells: the parent's density, zero flux (:236-262)
+    if new.size:
+        par = np.array([m.get_parent(int(c)) for c in new], dtype=np.uint64)
+        rho = np.concatenate(grid.read_cells("density", par))
+        grid.write_cells("density", new, rho)
+        grid.write_cells("flux", new, np.zeros(new.size))
+    # parents of removed cells: the mean of their children (:264-299)
+    removed = grid.get_removed_cells()
+    if removed.size:
+        par = np.array([m.get_parent(int(c)) for c in removed], dtype=np.uint64)
+        rho = np.concatenate(grid.read_cells("density", removed))
+        up, inv = np.unique(par, return_inverse=True)
+        acc = np.zeros(up.size)
+        for i in range(removed.size):  # parent += child / 8 in order (:291-298)
+            acc[inv[i]] += rho[i] / 8
+        grid.write_cells("density", up, acc)
+        grid.write_cells("flux", up, np.zeros(up.size))
+    grid.clear_refined_unrefined_data()
+    # velocities and lengths of every local cell (:303-313)
+    _velocities_lengths(grid, geom, grid.local_cells())
+    grid.update_copies_of_remote_neighbors(fields=list(ALL))
+    return int(new.size), int(removed.size)
+
+
+def max_time_step(grid: Dccrg) -> float:
+    """solve.hpp:302-332 on one rank (the caller reduces with MIN)."""
+    return grid.max_time_step()

@@ -215,6 +215,62 @@ __global__ void __launch_bounds__(256) k_ex_advect_faces(AdvPtrs p, double dt, F
     }
 }
 
+// check_for_adaptation, tests/advection/adapter.hpp:66-103: max relative
+// density difference over the adapter's face neighbors, maximised into both
+// cells of a pair when the neighbor is local (atomic max on the bit pattern
+// of a non-negative double)
+__global__ void __launch_bounds__(256) k_adapt_diff(const double* __restrict__ rho, const uint64_t* __restrict__ st_row,
+                                                    const uint32_t* __restrict__ st_slot,
+                                                    const int32_t* __restrict__ st_off,
+                                                    const uint32_t* __restrict__ local_g,
+                                                    const uint8_t* __restrict__ level, int M, uint64_t n,
+                                                    const uint8_t* __restrict__ slot_local, double thr,
+                                                    unsigned long long* __restrict__ maxd)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        const uint32_t c = local_g[q];
+        const int64_t lc = 1ll << (M - level[c]);
+        const double rc = rho[c];
+        for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) {
+            const uint32_t nb = st_slot[e];
+            const int64_t ln = 1ll << (M - level[nb]);
+            const int64_t x = st_off[3 * e], y = st_off[3 * e + 1], z = st_off[3 * e + 2];
+            const bool face = ((x == lc || x == -ln) && y == 0 && z == 0) || ((y == lc || y == -ln) && x == 0 && z == 0) ||
+                              ((z == lc || z == -ln) && x == 0 && y == 0);
+            if (!face) continue;
+            const double rn = rho[nb];
+            const double diff = fabs(rc - rn) / ((rc < rn ? rc : rn) + thr);
+            const unsigned long long k = (unsigned long long)__double_as_longlong(diff);
+            atomicMax(&maxd[c], k);
+            if (slot_local[nb]) atomicMax(&maxd[nb], k);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_adapt_marks(const unsigned long long* __restrict__ maxd,
+                                                     const uint32_t* __restrict__ local_g,
+                                                     const uint8_t* __restrict__ level, uint64_t n, double inc,
+                                                     double sens, int8_t* __restrict__ marks, double* __restrict__ out)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        const uint32_t c = local_g[q];
+        const double diff = __longlong_as_double((long long)maxd[c]);
+        // adapter.hpp:114-118
+        const double refine_diff = (level[c] + 1) * inc, unrefine_diff = sens * refine_diff;
+        marks[q] = diff > refine_diff ? 2 : (diff >= unrefine_diff ? 1 : 0);
+        out[q] = diff;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_flag_slots(const uint32_t* __restrict__ local_g, uint64_t n,
+                                                    uint8_t* __restrict__ flag)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) flag[local_g[q]] = 1;
+}
+
 // uniform grids: the face neighbors present in the neighborhood (mask bit
 // 2k / 2k+1 = canonical axis k, -1 / +1), addressed in the slab layout
 __global__ void __launch_bounds__(256) k_u_advect(UGeom g, AdvPtrs p, double dt, uint32_t mask, uint64_t lin0,
@@ -500,6 +556,49 @@ int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f
     DX_HIP(hipStreamSynchronize(st));
     hipFree(d);
     if (k != init) *local_min = dunkey(k);
+    return DCCRGX_OK;
+}
+
+int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
+                              double diff_increase, double diff_threshold, double unrefine_sensitivity,
+                              int8_t* marks_out, double* max_diff_out)
+{
+    DX_CHECK(grid && f && (marks_out || !grid->n_local), DCCRGX_EINVAL, "null argument");
+    DX_TRY(amr_ensure_explicit(grid));
+    const Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    AdvPtrs p;
+    DX_TRY(adv_ptrs(grid, f, &p));
+    const uint64_t n = grid->n_local;
+    if (!n) return DCCRGX_OK;
+    ExRegion R;
+    DX_TRY(explicit_region(grid, *h, DCCRGX_REGION_ALL, &R));
+    hipStream_t st = grid->ctx->compute;
+    unsigned long long* d_max = nullptr;
+    uint8_t* d_flag = nullptr;
+    int8_t* d_marks = nullptr;
+    double* d_diff = nullptr;
+    const uint64_t ns = grid->n_slots;
+    DX_HIP(hipMalloc(&d_max, ns * 8));
+    DX_HIP(hipMalloc(&d_flag, ns));
+    DX_HIP(hipMalloc(&d_marks, n));
+    DX_HIP(hipMalloc(&d_diff, n * 8));
+    DX_HIP(hipMemsetAsync(d_max, 0, ns * 8, st));  // max_diff = 0 (:62-64)
+    DX_HIP(hipMemsetAsync(d_flag, 0, ns, st));
+    hipLaunchKernelGGL(k_flag_slots, dim3(grid_for(n)), dim3(256), 0, st, R.local_g, n, d_flag);
+    hipLaunchKernelGGL(k_adapt_diff, dim3(grid_for(n)), dim3(256), 0, st, p.rho, h->d_st_row, h->d_st_slot,
+                       h->d_st_off, R.local_g, R.level, grid->map.max_lvl, n, (const uint8_t*)d_flag,
+                       diff_threshold, d_max);
+    hipLaunchKernelGGL(k_adapt_marks, dim3(grid_for(n)), dim3(256), 0, st, (const unsigned long long*)d_max,
+                       R.local_g, R.level, n, diff_increase, unrefine_sensitivity, d_marks, d_diff);
+    DX_HIP(hipGetLastError());
+    DX_HIP(hipMemcpyAsync(marks_out, d_marks, n, hipMemcpyDeviceToHost, st));
+    if (max_diff_out) DX_HIP(hipMemcpyAsync(max_diff_out, d_diff, n * 8, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_max);
+    hipFree(d_flag);
+    hipFree(d_marks);
+    hipFree(d_diff);
     return DCCRGX_OK;
 }
 

@@ -281,8 +281,15 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     hipFree(d_s);
     hipFree(d_d);
     DX_TRY(s);
-    // new leaf state and neighborhoods
-    for (auto& kv : grid->hoods) free_hood(kv.second);
+    // new leaf state and neighborhoods: every plan of the old layout goes
+    // (uniform grids keep periodic self-copy segments and slab ranges)
+    for (auto& kv : grid->hoods) {
+        free_hood(kv.second);
+        Hood fresh;
+        fresh.id = kv.second.id;
+        fresh.items = kv.second.items;
+        kv.second = std::move(fresh);
+    }
     if (grid->ex) explicit_destroy(grid);
     grid->uniform = false;
     DX_TRY(explicit_init(grid, leaves.data(), n));
@@ -306,6 +313,8 @@ int ensure_explicit(dccrgx_grid* grid)
 }
 
 }  // namespace
+
+int amr_ensure_explicit(dccrgx_grid* grid) { return ensure_explicit(grid); }
 
 void amr_destroy(dccrgx_grid* grid)
 {
@@ -439,6 +448,22 @@ int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
     Amr& A = amr_of(grid);
     A.to_refine.erase(cell);
     A.not_to_refine.insert(cell);
+    return DCCRGX_OK;
+}
+
+int dccrgx_amr_request_cells(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results)
+{
+    DX_CHECK(grid && (ids || !n) && kind >= 0 && kind < 4, DCCRGX_EINVAL, "bad argument");
+    for (size_t i = 0; i < n; i++) {
+        int32_t r = 0;
+        switch (kind) {
+        case DCCRGX_AMR_REFINE: DX_TRY(dccrgx_refine_completely(grid, ids[i], &r)); break;
+        case DCCRGX_AMR_DONT_REFINE: DX_TRY(dccrgx_dont_refine(grid, ids[i], &r)); break;
+        case DCCRGX_AMR_UNREFINE: DX_TRY(dccrgx_unrefine_completely(grid, ids[i], &r)); break;
+        default: DX_TRY(dccrgx_dont_unrefine(grid, ids[i], &r)); break;
+        }
+        if (results) results[i] = r;
+    }
     return DCCRGX_OK;
 }
 

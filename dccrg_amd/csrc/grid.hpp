@@ -266,6 +266,8 @@ int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id);
 // the slot read and written for a cell on this rank (-1: none), halo.hip
 int64_t host_primary_slot(const dccrgx_grid* grid, uint64_t id);
 void amr_destroy(dccrgx_grid* grid);
+// switch a uniform grid to the explicit layout (amr.hip)
+int amr_ensure_explicit(dccrgx_grid* grid);
 int launch_gather_ext(const void* src, const uint64_t* idx, uint64_t n, uint32_t elem, void* dst,
                       hipStream_t st);
 int launch_scatter_ext(const void* src, const uint64_t* sidx, const uint64_t* didx, uint64_t n,

@@ -313,6 +313,18 @@ int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f);
  * and axes of length / |v| where that is a normal number (DBL_MAX if none).
  * The caller reduces with MIN across ranks (:322-332). */
 int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f, double* local_min);
+/* check_for_adaptation, tests/advection/adapter.hpp:43-176, device part: for
+ * every local cell (ascending ids) the maximum relative density difference
+ * |a - b| / (min(a, b) + diff_threshold) over the neighbors_of entries the
+ * adapter counts as face neighbors (offset == own length or == -neighbor
+ * length along one axis, 0 along the others, :70-90), taken over both cells
+ * of each pair when the neighbor is local (:98-101); and the decision
+ * category: 2 refine (diff > (level + 1) * diff_increase), 1 keep (diff >=
+ * unrefine_sensitivity * that), 0 unrefine.  Switches a uniform grid to the
+ * explicit layout.  max_diff_out optional. */
+int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
+                              double diff_increase, double diff_threshold, double unrefine_sensitivity,
+                              int8_t* marks_out, double* max_diff_out);
 /* one step of tests/advection/2d.cpp:321-390: density halo start, inner
  * fluxes, halo wait, outer fluxes, apply */
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt);
@@ -339,6 +351,8 @@ int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result
 int dccrgx_dont_unrefine(dccrgx_grid* grid, uint64_t cell, int32_t* result);
 /* Dccrg::dont_refine, dccrg.hpp:2768-2806 */
 int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result);
+/* the request call of `kind` (DCCRGX_AMR_*) for each id in order; results optional */
+int dccrgx_amr_request_cells(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results);
 /* this rank's pending request set `which` (DCCRGX_AMR_*), ascending; ids == NULL: count only */
 int dccrgx_amr_requests(const dccrgx_grid* grid, int32_t which, uint64_t* ids, size_t cap, size_t* n);
 /* Dccrg::stop_refining, dccrg.hpp:3483-3507: sets[k] / counts[k] = union over

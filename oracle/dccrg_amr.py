@@ -439,3 +439,152 @@ class AmrOracle:
             for n in self.nof(c):
                 worst = max(worst, abs(self.level(c) - self.level(n)))
         return worst
+
+
+# ---- the advection program with adaptation (tests/advection/2d.cpp) --------
+class AdvectionAmrOracle:
+    """tests/advection/2d.cpp:170-390 on the CPU: initialize.hpp, the
+    pre-refinement loop (:260-290), then per step the solver (solve.hpp via
+    oracle.dccrg_oracle.AdvectionLists), check_for_adaptation on the
+    pre-apply densities, apply_fluxes and adapt_grid (adapter.hpp:184-319),
+    every rank simulated.  Geometry: start 0, level-0 cell length 1 / cells
+    along every axis (2d.cpp:238-243)."""
+
+    def __init__(self, cells: int, max_ref_lvl: int, comm_size: int = 1, relative_diff=0.025,
+                 diff_threshold=0.25, unrefine_sensitivity=0.5, cfl=0.5):
+        from oracle.dccrg_oracle import AdvectionLists  # noqa: F401
+        self.o = AmrOracle((cells, cells, 1), max_ref_lvl, (True, True, False), 0, comm_size)
+        self.l0 = np.array([1.0 / cells] * 3)
+        self.params = (relative_diff, diff_threshold, unrefine_sensitivity)
+        self.cfl = cfl
+        self.state: Dict[int, List[float]] = {}  # cell -> [rho, flux, vx, vy, vz, lx, ly, lz]
+        self._init_state()
+        for _ in range(self.o.M):
+            sets = self.check_for_adaptation()
+            self.adapt(sets)
+            self._init_state()
+        self.dt = self.max_time_step()
+
+    def _geom(self, c):
+        m = self.o.mapping
+        idx = np.array(m.get_indices(c), dtype=np.float64)
+        ln = self.l0 / 2.0 ** self.o.level(c)
+        return idx * (self.l0 / 2.0 ** self.o.M) + ln / 2, ln
+
+    def _init_state(self):
+        """initialize.hpp:27-65."""
+        self.state = {}
+        for c in self.o.cells():
+            ctr, ln = self._geom(c)
+            r = min(np.sqrt((ctr[0] - 0.25) ** 2 + (ctr[1] - 0.5) ** 2), 0.15) / 0.15
+            self.state[c] = [0.25 * (1 + np.cos(np.pi * r)), 0.0, -ctr[1] + 0.5, ctr[0] - 0.5, 0.0,
+                             ln[0], ln[1], ln[2]]
+
+    def _lists(self):
+        from oracle.dccrg_oracle import AdvectionLists
+        return AdvectionLists(self.o.grid, self.o.P)
+
+    def arrays(self):
+        """cells ascending, and the state columns rho, flux, vx, vy, vz, lx,
+        ly, lz as contiguous arrays (the C restatement takes raw pointers)"""
+        cells = self.o.cells()
+        a = np.array([self.state[c] for c in cells])
+        return cells, [np.ascontiguousarray(a[:, k]) for k in range(8)]
+
+    def max_time_step(self) -> float:
+        cells, a = self.arrays()
+        lists = self._lists()
+        return lists.max_time_step([a[0], a[2], a[3], a[4], a[5], a[6], a[7]])
+
+    def check_for_adaptation(self):
+        """adapter.hpp:43-176, per rank, cells visited in ascending order."""
+        from oracle.dccrg_oracle import iteration_cache_lists
+        o = self.o
+        rel, thr, sens = self.params
+        inc = rel / o.M
+        sets = []
+        for r in range(o.P):
+            local = [c for c in o.cells() if o.owner(c) == r]
+            maxd = {c: 0.0 for c in local}
+            for c in local:
+                lc = o.mapping.get_cell_length_in_indices(c)
+                nof = o.grid.find_neighbors_of(c)
+                nto = o.grid.find_neighbors_to(c)
+                lof, _ = iteration_cache_lists(nof, nto)
+                for n, off in lof:
+                    ln = o.mapping.get_cell_length_in_indices(n)
+                    x, y, z = off
+                    face = ((x == lc or x == -ln) and y == 0 and z == 0) or \
+                           ((y == lc or y == -ln) and x == 0 and z == 0) or \
+                           ((z == lc or z == -ln) and x == 0 and y == 0)
+                    if not face:
+                        continue
+                    a, b = self.state[c][0], self.state[n][0]
+                    diff = abs(a - b) / (min(a, b) + thr)
+                    maxd[c] = max(diff, maxd[c])
+                    if o.owner(n) == r:
+                        maxd[n] = max(diff, maxd[n])
+            to_ref, keep, unref = set(), set(), set()
+            for c in local:
+                lvl = o.level(c)
+                refine_diff = (lvl + 1) * inc
+                unrefine_diff = sens * refine_diff
+                sibs = o.siblings(c)
+                diff = maxd[c]
+                if diff > refine_diff:
+                    to_ref.add(c)
+                    for s in sibs:
+                        unref.discard(s)
+                        keep.discard(s)
+                elif diff >= unrefine_diff:
+                    dont = not any(s in to_ref or s in keep for s in sibs)
+                    if dont and lvl > 0:
+                        keep.add(c)
+                        for s in sibs:
+                            unref.discard(s)
+                else:
+                    un = not any(s in to_ref or s in keep for s in sibs)
+                    if un and lvl > 0:
+                        unref.add(c)
+            sets.append((sorted(to_ref), sorted(keep), sorted(unref)))
+        return sets
+
+    def adapt(self, sets):
+        """adapter.hpp:184-319 on every rank, then one stop_refining."""
+        o = self.o
+        for r, (to_ref, keep, unref) in enumerate(sets):
+            for c in to_ref:
+                o.refine_completely(r, c)
+            for c in keep:
+                o.dont_unrefine(r, c)
+            for c in unref:
+                o.unrefine_completely(r, c)
+        old = self.state
+        new = o.stop_refining()
+        st = {c: old[c] for c in o.cells() if c in old}
+        for r in range(o.P):
+            for c in new[r]:
+                p = o.mapping.get_parent(c)
+                st[c] = [old[p][0], 0.0] + [0.0] * 6
+            rem = o.get_removed_cells(r)
+            parents = sorted(set(o.mapping.get_parent(c) for c in rem))
+            for p in parents:
+                st[p] = [0.0, 0.0] + [0.0] * 6
+            for c in rem:
+                st[o.mapping.get_parent(c)][0] += old[c][0] / 8
+        for c in o.cells():  # velocities and lengths (:303-313)
+            ctr, ln = self._geom(c)
+            st[c][2:] = [-ctr[1] + 0.5, ctr[0] - 0.5, 0.0, ln[0], ln[1], ln[2]]
+        self.state = st
+
+    def step(self):
+        """2d.cpp:321-444 with adapt_n = 1."""
+        cells, a = self.arrays()
+        sets = self.check_for_adaptation()
+        lists = self._lists()
+        rho = lists.step([a[0], a[2], a[3], a[4], a[5], a[6], a[7]], self.cfl * self.dt)
+        for i, c in enumerate(cells):
+            self.state[c][0] = rho[i]
+            self.state[c][1] = 0.0
+        self.adapt(sets)
+        self.dt = self.max_time_step()

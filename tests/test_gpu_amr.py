@@ -219,3 +219,46 @@ def test_uniform_grid_switches_layout_on_refine():
     assert np.array_equal(vals[keep], (loc[keep] % 7).astype(np.uint32))
     check_structure([g], o)
     g.close()
+
+
+@pytest.mark.parametrize("cells,M,steps", [(16, 2, 5), (12, 1, 4)])
+def test_adaptive_advection_matches_oracle(cells, M, steps):
+    """tests/advection/2d.cpp with adaptation every step (adapt_n = 1):
+    pre-refinement, then solve / check_for_adaptation / apply / adapt_grid.
+    Leaf sets equal the oracle's after every step; densities within 1e-12
+    relative (fp64, the north star's bound); time steps equal."""
+    from dccrg_amd import advection as A
+    from oracle.dccrg_amr import AdvectionAmrOracle
+    rel, thr, sens, cfl = 0.025, 0.25, 0.5, 0.5
+    ref = AdvectionAmrOracle(cells, M, 1, rel, thr, sens, cfl)
+    ctx = D.Context(0, 0, 1)
+    g = (D.Dccrg().set_initial_length((cells, cells, 1)).set_maximum_refinement_level(M)
+         .set_periodic(True, True, False).set_neighborhood_length(0).initialize(ctx))
+    g.add_advection_fields()
+    geom = A.geometry_2d(g)
+    A.initialize(g, geom)
+    for _ in range(M):
+        sets = A.check_for_adaptation(g, rel / M, thr, sens)
+        A.adapt_grid(g, geom, *sets)
+        A.initialize(g, geom)
+
+    def compare(tag):
+        rc, ra = ref.arrays()
+        assert [int(c) for c in g.local_cells()] == rc, tag
+        rho = g.read_local("density")
+        assert np.max(np.abs(rho - ra[0])) <= 1e-12 * np.max(np.abs(ra[0])), tag
+
+    compare("prerefined")
+    dt = g.max_time_step()
+    assert abs(dt - ref.dt) <= 1e-15 * ref.dt
+    for s in range(steps):
+        g.update_copies_of_remote_neighbors(fields=["density"])
+        sets = A.check_for_adaptation(g, rel / M, thr, sens)
+        g.advect_step(cfl * dt)
+        A.adapt_grid(g, geom, *sets)
+        dt = g.max_time_step()
+        ref.step()
+        compare(f"step {s}")
+        assert abs(dt - ref.dt) <= 1e-15 * ref.dt
+    g.close()
+    ctx.close()
