@@ -68,34 +68,6 @@ def pmc_traffic(kernel: str, cells_per_launch: int):
     return best
 
 
-def advection_leaves(n=400, r1=0.2, r2=0.12, centre=(0.25, 0.5)):
-    """configs[2]: tests/advection's 2-D grid (n x n x 1, max_ref_lvl 2) with
-    the region around the density hump refined once (r < r1) and twice
-    (r < r2) -- a static snapshot of what 2d.cpp's adaptation produces
-    (AMR itself is out of scope).  Nested disks far apart keep the grid
-    2:1 balanced under the reference's induce rule."""
-    N0 = n * n
-    first = [1, 1 + N0, 1 + N0 + 8 * N0]
-    i, j = np.meshgrid(np.arange(n), np.arange(n), indexing="xy")
-    i, j = i.ravel(), j.ravel()
-    r0 = np.hypot((i + 0.5) / n - centre[0], (j + 0.5) / n - centre[1])
-    out = [first[0] + i[r0 >= r1] + n * j[r0 >= r1]]
-    # level 1: children of refined level-0 cells (x fastest, y, z)
-    ri, rj = i[r0 < r1], j[r0 < r1]
-    d = np.array([(dx, dy, dz) for dz in (0, 1) for dy in (0, 1) for dx in (0, 1)])
-    x1 = (2 * ri[:, None] + d[None, :, 0]).ravel()
-    y1 = (2 * rj[:, None] + d[None, :, 1]).ravel()
-    z1 = np.broadcast_to(d[None, :, 2], (len(ri), 8)).ravel()
-    r_1 = np.hypot((x1 + 0.5) / (2 * n) - centre[0], (y1 + 0.5) / (2 * n) - centre[1])
-    keep = r_1 >= r2
-    out.append(first[1] + x1[keep] + 2 * n * y1[keep] + 4 * N0 * z1[keep])
-    x2 = (2 * x1[~keep][:, None] + d[None, :, 0]).ravel()
-    y2 = (2 * y1[~keep][:, None] + d[None, :, 1]).ravel()
-    z2 = (2 * z1[~keep][:, None] + d[None, :, 2]).ravel()
-    out.append(first[2] + x2 + 4 * n * y2 + 16 * N0 * z2)
-    return np.sort(np.concatenate(out)).astype(np.uint64)
-
-
 def poisson3d_leaves():
     """tests/poisson/poisson3d.cpp:158-178's grid: 8^3, the 2x2x2 block around
     (pi, pi/2, 4 pi) refined, the 24 level-0 cells face-adjacent to it refined
@@ -172,41 +144,59 @@ def secondary(ctx, torch, D):
                     "kernel": "k_gol26_rowv<4>", "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS}
     g.close()
 
-    # configs[2]: advection, 400x400x1 with 2 refinement levels (static)
-    leaves = advection_leaves()
-    g = (D.Dccrg().set_initial_length((400, 400, 1)).set_maximum_refinement_level(2)
-         .set_periodic(True, True, False).set_neighborhood_length(0).initialize(ctx, leaves=leaves))
+    # configs[2]: tests/advection/2d.cpp, 400x400x1, max_ref_lvl 2, hood 0:
+    # the program's own pre-refinement, then (a) the solver alone on that
+    # mixed-level grid and (b) the full loop with adaptation every step
+    # (adapt_n = 1: solve, check_for_adaptation, apply, adapt_grid, dt)
+    from dccrg_amd import advection as A
+    rel, thr, sens, cfl, M = 0.025, 0.25, 0.5, 0.5, 2
+    t0 = time.perf_counter()
+    g = (D.Dccrg().set_initial_length((400, 400, 1)).set_maximum_refinement_level(M)
+         .set_periodic(True, True, False).set_neighborhood_length(0).initialize(ctx))
     g.add_advection_fields()
-    idx = np.zeros((len(leaves), 3), dtype=np.int64)
-    lv = np.zeros(len(leaves), dtype=np.int32)
-    m = D.Mapping((400, 400, 1), 2)
-    ids_t = torch.from_numpy(leaves.view(np.int64)).to(dev)
-    it, lt = m.ids_to_indices(ids_t)
-    torch.cuda.synchronize(dev)
-    idx, lv = it.cpu().numpy(), lt.cpu().numpy()
-    ln = (1.0 / 400) / (2.0 ** lv)
-    ctr = (idx + 0.5 * (2 ** (2 - lv))[:, None]) / (400 * 4)
-    rr = np.minimum(np.hypot(ctr[:, 0] - 0.25, ctr[:, 1] - 0.5), 0.15) / 0.15
-    vals = {"density": 0.25 * (1 + np.cos(np.pi * rr)), "vx": -ctr[:, 1] + 0.5, "vy": ctr[:, 0] - 0.5,
-            "vz": np.zeros(len(leaves)), "length_x": ln, "length_y": ln, "length_z": 1.0 / (2.0 ** lv)}
-    for k, v in vals.items():
-        g.write_local(k, v)
-    g.update_copies_of_remote_neighbors(fields=list(vals))
-    dt_adv = 0.5 * g.max_time_step()
-    g.advect_step(dt_adv)
+    geom = A.geometry_2d(g)
+    A.initialize(g, geom)
+    for _ in range(M):
+        A.adapt_grid(g, geom, *A.check_for_adaptation(g, rel / M, thr, sens))
+        A.initialize(g, geom)
+    t_pre = time.perf_counter() - t0
+    nl = g.n_local
+    dt_adv = g.max_time_step()
+    g.advect_step(cfl * dt_adv)
     ctx.synchronize()
     steps = 50
     t0 = time.perf_counter()
     for _ in range(steps):
-        g.advect_step(dt_adv)
+        g.advect_step(cfl * dt_adv)
     ctx.synchronize()
     dt = time.perf_counter() - t0
-    nl = len(leaves)
-    out["advection"] = {"workload": "configs[2] tests/advection 400x400x1, max_ref_lvl 2, static refined "
-                                    f"hump region, {nl} leaf cells, neighborhood 0, fp64",
+    out["advection"] = {"workload": "configs[2] tests/advection/2d.cpp 400x400x1, max_ref_lvl 2, neighborhood 0, "
+                                    f"fp64: solver steps on the pre-refined grid ({nl} leaf cells)",
                         "value": nl * steps / dt, "unit": "cell-steps/s", "steps": steps,
                         "achieved_GBs": 72 * nl * steps / dt / 1e9,
-                        "frac": 72 * nl * steps / dt / 1e9 / HBM_PEAK_GBS, "bytes_per_cell_step": 72}
+                        "frac": 72 * nl * steps / dt / 1e9 / HBM_PEAK_GBS, "bytes_per_cell_step": 72,
+                        "prerefine_s": t_pre}
+    # (b) adaptive loop
+    g.update_copies_of_remote_neighbors(fields=list(A.ALL))
+    steps, cells_steps = 5, 0
+    t_adapt = 0.0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        cells_steps += g.n_local
+        g.update_copies_of_remote_neighbors(fields=["density"])
+        sets = A.check_for_adaptation(g, rel / M, thr, sens)
+        g.advect_step(cfl * dt_adv)
+        ta = time.perf_counter()
+        A.adapt_grid(g, geom, *sets)
+        dt_adv = g.max_time_step()
+        t_adapt += time.perf_counter() - ta
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    out["advection_adaptive"] = {"workload": "configs[2] tests/advection/2d.cpp loop with adapt_n = 1 "
+                                             "(refine/unrefine and device rebuild every step)",
+                                 "value": cells_steps / dt, "unit": "cell-steps/s", "steps": steps,
+                                 "ms_per_step": dt * 1e3 / steps, "adapt_ms_per_step": t_adapt * 1e3 / steps,
+                                 "leaf_cells_end": g.n_local}
     g.close()
 
     # configs[4] (Poisson part): poisson3d's 792-leaf grid on one GPU

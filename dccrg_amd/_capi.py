@@ -90,6 +90,8 @@ SIGNATURES = {
     "dccrgx_map_host_cell": (C.c_int, [C.POINTER(Mapping_t), _u64p, C.c_int32, _u64p]),
     "dccrgx_map_host_op": (C.c_int, [C.POINTER(Mapping_t), C.c_int, C.c_uint64, _u64p]),
     "dccrgx_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "dccrgx_map_host_ids_to_indices": (C.c_int, [C.POINTER(Mapping_t), _u64p, C.c_size_t, _u64p, _i32p]),
+    "dccrgx_map_host_ids_op": (C.c_int, [C.POINTER(Mapping_t), C.c_int, _u64p, C.c_size_t, _u64p]),
     "dccrgx_neighbors_of_host": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _u64p, _u64p, _i32p, C.c_size_t]),
     "dccrgx_neighbors_to_host": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _u64p, _u64p, C.c_size_t]),
     "dccrgx_face_neighbors_of": (C.c_int, [_vp, _vp, C.c_size_t, _vp, _vp, _vp, C.c_size_t, _vp]),

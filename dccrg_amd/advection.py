@@ -35,9 +35,9 @@ class CartesianGeometry:
     def centers_and_lengths(self, cells: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
         m = self.grid.mapping
         M = m.max_ref_lvl
-        idx = np.array([m.get_indices(int(c)) for c in cells], dtype=np.float64).reshape(-1, 3)
-        lvl = np.array([m.get_refinement_level(int(c)) for c in cells], dtype=np.float64)
-        ln = self.l0[None, :] / (2.0 ** lvl)[:, None]
+        idx, lvl = m.levels_and_indices(cells)
+        idx = idx.astype(np.float64)
+        ln = self.l0[None, :] / (2.0 ** lvl.astype(np.float64))[:, None]
         center = self.start[None, :] + idx * (self.l0 / 2.0 ** M)[None, :] + ln / 2
         return center, ln
 
@@ -100,23 +100,21 @@ def check_for_adaptation(grid: Dccrg, diff_increase: float, diff_threshold: floa
     grid._refresh_info()
     cells = grid.local_cells()
     m = grid.mapping
-    lvl = np.array([m.get_refinement_level(int(c)) for c in cells])
-    group = np.array([m.get_parent(int(c)) if l > 0 else int(c) for c, l in zip(cells, lvl)], dtype=np.uint64)
+    _, lvl = m.levels_and_indices(cells)
+    group = m.parents(cells)  # level-0 cells are their own group
     refine = cells[marks == 2]
     # per sibling group: any refine blocks keep/unrefine marks; any keep (level > 0)
     # blocks unrefine marks (:126-174)
-    g_ref = set(group[marks == 2].tolist())
-    g_keep = set(group[(marks == 1) & (lvl > 0)].tolist())
-    keep = np.array([c for c, g, mk, l in zip(cells, group, marks, lvl)
-                     if mk == 1 and l > 0 and g not in g_ref], dtype=np.uint64)
+    g_ref = np.isin(group, group[marks == 2])
+    g_keep = np.isin(group, group[(marks == 1) & (lvl > 0)])
+    kmask = (marks == 1) & (lvl > 0) & ~g_ref
+    keep = cells[kmask]
     # one dont_unrefine per group is what the reference leaves behind (:146-155)
     if keep.size:
-        gk = np.array([m.get_parent(int(c)) for c in keep], dtype=np.uint64)
-        _, first = np.unique(gk, return_index=True)
+        _, first = np.unique(group[kmask], return_index=True)
         keep = keep[np.sort(first)]
-    unref = np.array([c for c, g, mk, l in zip(cells, group, marks, lvl)
-                      if mk == 0 and l > 0 and g not in g_ref and g not in g_keep], dtype=np.uint64)
-    return refine.astype(np.uint64), keep, unref
+    unref = cells[(marks == 0) & (lvl > 0) & ~g_ref & ~g_keep]
+    return refine.astype(np.uint64), keep.astype(np.uint64), unref.astype(np.uint64)
 
 
 def _request(grid: Dccrg, kind: int, ids: np.ndarray):
@@ -137,19 +135,18 @@ def adapt_grid(grid: Dccrg, geom: CartesianGeometry, to_refine, not_to_unrefine,
     m = grid.mapping
     # new cells: the parent's density, zero flux (:236-262)
     if new.size:
-        par = np.array([m.get_parent(int(c)) for c in new], dtype=np.uint64)
+        par = m.parents(new)
         rho = np.concatenate(grid.read_cells("density", par))
         grid.write_cells("density", new, rho)
         grid.write_cells("flux", new, np.zeros(new.size))
     # parents of removed cells: the mean of their children (:264-299)
     removed = grid.get_removed_cells()
     if removed.size:
-        par = np.array([m.get_parent(int(c)) for c in removed], dtype=np.uint64)
+        par = m.parents(removed)
         rho = np.concatenate(grid.read_cells("density", removed))
         up, inv = np.unique(par, return_inverse=True)
         acc = np.zeros(up.size)
-        for i in range(removed.size):  # parent += child / 8 in order (:291-298)
-            acc[inv[i]] += rho[i] / 8
+        np.add.at(acc, inv, rho / 8)  # parent += child / 8, children in order (:291-298)
         grid.write_cells("density", up, acc)
         grid.write_cells("flux", up, np.zeros(up.size))
     grid.clear_refined_unrefined_data()

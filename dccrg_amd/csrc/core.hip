@@ -284,6 +284,33 @@ int dccrgx_map_host_op(const dccrgx_mapping* map, int op, uint64_t c, uint64_t* 
     return DCCRGX_OK;
 }
 
+int dccrgx_map_host_ids_to_indices(const dccrgx_mapping* map, const uint64_t* ids, size_t n, uint64_t* idx3,
+                                   int32_t* lvl)
+{
+    MapParams p;
+    DX_TRY(make_map_params(map, &p));
+    DX_CHECK(ids || !n, DCCRGX_EINVAL, "null argument");
+    for (size_t i = 0; i < n; i++) {
+        uint64_t o[3];
+        int l;
+        map_indices(p, ids[i], o, &l);
+        if (idx3) {
+            idx3[3 * i] = o[0];
+            idx3[3 * i + 1] = o[1];
+            idx3[3 * i + 2] = o[2];
+        }
+        if (lvl) lvl[i] = l;
+    }
+    return DCCRGX_OK;
+}
+
+int dccrgx_map_host_ids_op(const dccrgx_mapping* map, int op, const uint64_t* ids, size_t n, uint64_t* out)
+{
+    DX_CHECK(ids || !n, DCCRGX_EINVAL, "null argument");
+    for (size_t i = 0; i < n; i++) DX_TRY(dccrgx_map_host_op(map, op, ids[i], out + i));
+    return DCCRGX_OK;
+}
+
 int dccrgx_device_count(int* n)
 {
     DX_CHECK(n, DCCRGX_EINVAL, "null output");

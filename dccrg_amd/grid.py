@@ -132,6 +132,26 @@ class Mapping:
     def get_child(self, cell: int) -> int:
         return self._op(X.OP_CHILD, cell)
 
+    # ---- host arrays (numpy in, numpy out) --------------------------------
+    def levels_and_indices(self, cells):
+        """(indices (n, 3) uint64 in max-level units, levels int32) of an array of ids."""
+        c = np.ascontiguousarray(cells, dtype=np.uint64)
+        idx = np.zeros((c.size, 3), dtype=np.uint64)
+        lvl = np.zeros(c.size, dtype=np.int32)
+        check(lib().dccrgx_map_host_ids_to_indices(C.byref(self._m), c.ctypes.data_as(X._u64p), c.size,
+                                                   idx.ctypes.data_as(X._u64p), lvl.ctypes.data_as(X._i32p)))
+        return idx, lvl
+
+    def ids_op_host(self, op: int, cells) -> np.ndarray:
+        c = np.ascontiguousarray(cells, dtype=np.uint64)
+        out = np.zeros(c.size, dtype=np.uint64)
+        check(lib().dccrgx_map_host_ids_op(C.byref(self._m), op, c.ctypes.data_as(X._u64p), c.size,
+                                           out.ctypes.data_as(X._u64p)))
+        return out
+
+    def parents(self, cells) -> np.ndarray:
+        return self.ids_op_host(X.OP_PARENT, cells)
+
     def get_all_children(self, cell: int):
         """dccrg_mapping.hpp:392-442: x fastest, then y, z; error_cell x 8
         for an invalid cell or one at the maximum level."""

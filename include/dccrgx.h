@@ -106,6 +106,10 @@ int dccrgx_map_host_indices(const dccrgx_mapping* map, uint64_t cell, uint64_t i
 int dccrgx_map_host_cell(const dccrgx_mapping* map, const uint64_t idx3[3], int32_t lvl,
                          uint64_t* cell_out);
 int dccrgx_map_host_op(const dccrgx_mapping* map, int op, uint64_t cell, uint64_t* out);
+/* host loops of the two above over an array (host memory) */
+int dccrgx_map_host_ids_to_indices(const dccrgx_mapping* map, const uint64_t* ids, size_t n,
+                                   uint64_t* idx3_out, int32_t* lvl_out);
+int dccrgx_map_host_ids_op(const dccrgx_mapping* map, int op, const uint64_t* ids, size_t n, uint64_t* out);
 int dccrgx_device_count(int* n_out);
 
 /* ------------------------------------------------------------------------ *
