@@ -60,15 +60,18 @@ def get_vy(x):  # solve.hpp:340-342
 ALL = ("density", "flux", "vx", "vy", "vz", "length_x", "length_y", "length_z")
 
 
-def initialize(grid: Dccrg, geom: CartesianGeometry):
-    """initialize.hpp:27-65: hump density, solid-body velocities, lengths."""
+def initialize(grid: Dccrg, geom: CartesianGeometry, update: bool = True):
+    """initialize.hpp:27-65: hump density, solid-body velocities, lengths.
+    update=False leaves the final ghost update (:60) to the caller (ranks
+    driven in one process exchange through pack / unpack)."""
     cells = grid.local_cells()
     center, ln = geom.centers_and_lengths(cells)
     r = np.minimum(np.sqrt((center[:, 0] - 0.25) ** 2 + (center[:, 1] - 0.5) ** 2), 0.15) / 0.15
     grid.write_local("density", 0.25 * (1 + np.cos(np.pi * r)))
     grid.write_local("flux", np.zeros(cells.size))
     _velocities_lengths(grid, geom, cells, center, ln)
-    grid.update_copies_of_remote_neighbors(fields=list(ALL))
+    if update:
+        grid.update_copies_of_remote_neighbors(fields=list(ALL))
 
 
 def _velocities_lengths(grid, geom, cells, center=None, ln=None):
@@ -127,10 +130,29 @@ def adapt_grid(grid: Dccrg, geom: CartesianGeometry, to_refine, not_to_unrefine,
     """adapter.hpp:184-319.  Returns (created, removed) cell counts."""
     if grid.get_maximum_refinement_level() == 0:
         return 0, 0
+    request_adaptation(grid, to_refine, not_to_unrefine, to_unrefine)
+    return finish_adaptation(grid, geom, all_requests)
+
+
+def request_adaptation(grid: Dccrg, to_refine, not_to_unrefine, to_unrefine):
+    """adapter.hpp:197-213: this rank's requests (before the collective
+    stop_refining)."""
+    if grid.get_maximum_refinement_level() == 0:
+        return
     _request(grid, X.AMR_REFINE, to_refine)
     _request(grid, X.AMR_DONT_UNREFINE, not_to_unrefine)
     _request(grid, X.AMR_UNREFINE, to_unrefine)
     grid._refresh_info()
+
+
+def finish_adaptation(grid: Dccrg, geom: CartesianGeometry, all_requests=None,
+                      update: bool = True) -> Tuple[int, int]:
+    """adapter.hpp:215-319: stop_refining (all_requests: the union of every
+    rank's requests, see Dccrg.stop_refining), data of new cells and of the
+    parents of removed cells, velocities and lengths, ghost update (skipped
+    with update=False)."""
+    if grid.get_maximum_refinement_level() == 0:
+        return 0, 0
     new = grid.stop_refining(all_requests=all_requests)
     m = grid.mapping
     # new cells: the parent's density, zero flux (:236-262)
@@ -152,7 +174,8 @@ def adapt_grid(grid: Dccrg, geom: CartesianGeometry, to_refine, not_to_unrefine,
     grid.clear_refined_unrefined_data()
     # velocities and lengths of every local cell (:303-313)
     _velocities_lengths(grid, geom, grid.local_cells())
-    grid.update_copies_of_remote_neighbors(fields=list(ALL))
+    if update:
+        grid.update_copies_of_remote_neighbors(fields=list(ALL))
     return int(new.size), int(removed.size)
 
 

@@ -241,6 +241,9 @@ __global__ void __launch_bounds__(256) k_adapt_diff(const double* __restrict__ r
             if (!face) continue;
             const double rn = rho[nb];
             const double diff = fabs(rc - rn) / ((rc < rn ? rc : rn) + thr);
+            // the bit pattern orders like the value only for diff >= 0; a
+            // non-positive diff never raises the reference's max from 0
+            if (!(diff > 0.0)) continue;
             const unsigned long long k = (unsigned long long)__double_as_longlong(diff);
             atomicMax(&maxd[c], k);
             if (slot_local[nb]) atomicMax(&maxd[nb], k);
@@ -427,7 +430,7 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
     const int M = grid->map.max_lvl;
     if (n)
         hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
-                           R.local_g, R.level, M, n, fc->ell_slot, fc->ell_dir, d_cnt, (const uint64_t*)nullptr,
+                           R.local_slot, R.level, M, n, fc->ell_slot, fc->ell_dir, d_cnt, (const uint64_t*)nullptr,
                            (uint32_t*)nullptr, (int8_t*)nullptr);
     DX_HIP(hipGetLastError());
     std::vector<uint32_t> cnt(n);
@@ -442,7 +445,7 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
     DX_HIP(hipMalloc(&fc->o_dir, std::max<uint64_t>(row[n], 1)));
     if (fc->overflow)
         hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
-                           R.local_g, R.level, M, n, fc->ell_slot, fc->ell_dir, (uint32_t*)nullptr, fc->o_row,
+                           R.local_slot, R.level, M, n, fc->ell_slot, fc->ell_dir, (uint32_t*)nullptr, fc->o_row,
                            fc->o_slot, fc->o_dir);
     DX_HIP(hipGetLastError());
     DX_HIP(hipStreamSynchronize(st));
@@ -482,11 +485,11 @@ int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect
         if (!hm->faces) DX_TRY(build_faces(grid, *hm));
         if (getenv("DCCRGX_ADVECT_ROWS"))  // the plain stencil-row gather (comparison path)
             hipLaunchKernelGGL(k_ex_advect, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, h->d_st_row,
-                               h->d_st_slot, h->d_st_off, R.local_g, R.level, grid->map.max_lvl, R.pos, R.n);
+                               h->d_st_slot, h->d_st_off, R.local_slot, R.level, grid->map.max_lvl, R.pos, R.n);
         else {
             const FaceCache& F = *hm->faces;
             const FaceView fv{F.n, F.ell_slot, F.ell_dir, F.o_row, F.o_slot, F.o_dir, F.overflow};
-            hipLaunchKernelGGL(k_ex_advect_faces, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, fv, R.local_g,
+            hipLaunchKernelGGL(k_ex_advect_faces, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, fv, R.local_slot,
                                region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos, R.n);
         }
         DX_HIP(hipGetLastError());
@@ -522,7 +525,7 @@ int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f)
     else {
         ExRegion R;
         DX_TRY(explicit_region(grid, grid->hoods.begin()->second, DCCRGX_REGION_ALL, &R));
-        slots = R.local_g;
+        slots = R.local_slot;
     }
     hipLaunchKernelGGL(k_apply_slots, dim3(grid_for(n)), dim3(256), 0, st, (double*)p.rho, p.flux, s0, n, slots);
     DX_HIP(hipGetLastError());
@@ -543,7 +546,7 @@ int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f
     else {
         ExRegion R;
         DX_TRY(explicit_region(grid, grid->hoods.begin()->second, DCCRGX_REGION_ALL, &R));
-        slots = R.local_g;
+        slots = R.local_slot;
     }
     unsigned long long* d = nullptr;
     DX_HIP(hipMalloc((void**)&d, 8));
@@ -585,12 +588,12 @@ int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_a
     DX_HIP(hipMalloc(&d_diff, n * 8));
     DX_HIP(hipMemsetAsync(d_max, 0, ns * 8, st));  // max_diff = 0 (:62-64)
     DX_HIP(hipMemsetAsync(d_flag, 0, ns, st));
-    hipLaunchKernelGGL(k_flag_slots, dim3(grid_for(n)), dim3(256), 0, st, R.local_g, n, d_flag);
+    hipLaunchKernelGGL(k_flag_slots, dim3(grid_for(n)), dim3(256), 0, st, R.local_slot, n, d_flag);
     hipLaunchKernelGGL(k_adapt_diff, dim3(grid_for(n)), dim3(256), 0, st, p.rho, h->d_st_row, h->d_st_slot,
-                       h->d_st_off, R.local_g, R.level, grid->map.max_lvl, n, (const uint8_t*)d_flag,
+                       h->d_st_off, R.local_slot, R.level, grid->map.max_lvl, n, (const uint8_t*)d_flag,
                        diff_threshold, d_max);
     hipLaunchKernelGGL(k_adapt_marks, dim3(grid_for(n)), dim3(256), 0, st, (const unsigned long long*)d_max,
-                       R.local_g, R.level, n, diff_increase, unrefine_sensitivity, d_marks, d_diff);
+                       R.local_slot, R.level, n, diff_increase, unrefine_sensitivity, d_marks, d_diff);
     DX_HIP(hipGetLastError());
     DX_HIP(hipMemcpyAsync(marks_out, d_marks, n, hipMemcpyDeviceToHost, st));
     if (max_diff_out) DX_HIP(hipMemcpyAsync(max_diff_out, d_diff, n * 8, hipMemcpyDeviceToHost, st));

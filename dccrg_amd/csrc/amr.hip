@@ -231,9 +231,11 @@ __global__ void __launch_bounds__(256) k_level0_ids(uint64_t* __restrict__ out, 
 }
 
 // Rebuild the grid on an ascending leaf list: device leaf state, every
-// neighborhood, and every field moved to the new slots (slot s of the new
-// layout takes old slot src[s]; -1 = zero).  `retired` cells (ascending) get
-// slots n + i and keep their old data.
+// neighborhood (which defines the ghost slots), and every field moved to the
+// new slots.  `retired` cells (ascending, local) get slots after the ghosts
+// and keep their old data.  Transactional: the new state and every new field
+// array are built first; on any failure they are freed and the old grid is
+// left exactly as it was.
 int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired)
 {
     Ctx* ctx = grid->ctx;
@@ -243,59 +245,123 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     for (auto& kv : grid->hoods) DX_CHECK(!kv.second.pending, DCCRGX_ESTATE, "a halo update is in progress");
     DX_HIP(hipStreamSynchronize(st));
     DX_HIP(hipStreamSynchronize(ctx->comm));
-    const uint64_t n = leaves.size(), nr = retired.size(), ns = n + nr;
-    // old slot of every new slot, from the old layout's own lookup
-    std::vector<uint64_t> sidx, didx;
-    sidx.reserve(ns);
-    didx.reserve(ns);
-    auto add = [&](uint64_t id, uint64_t to) {
-        const int64_t s = host_primary_slot(grid, id);
-        if (s >= 0) {
-            sidx.push_back((uint64_t)s);
-            didx.push_back(to);
-        }
-    };
-    for (uint64_t i = 0; i < n; i++) add(leaves[i], i);
-    for (uint64_t i = 0; i < nr; i++) add(retired[i], n + i);
-    uint64_t *d_s = nullptr, *d_d = nullptr;
-    DX_HIP(hipMalloc(&d_s, std::max<size_t>(sidx.size(), 1) * 8));
-    DX_HIP(hipMalloc(&d_d, std::max<size_t>(didx.size(), 1) * 8));
-    if (!sidx.empty()) {
-        DX_HIP(hipMemcpyAsync(d_s, sidx.data(), sidx.size() * 8, hipMemcpyHostToDevice, st));
-        DX_HIP(hipMemcpyAsync(d_d, didx.data(), didx.size() * 8, hipMemcpyHostToDevice, st));
-    }
-    int s = DCCRGX_OK;
-    for (Field& F : grid->fields) {
-        void* np = nullptr;
-        if (hipMalloc(&np, std::max<uint64_t>(ns, 1) * F.elem) != hipSuccess) {
-            s = set_error(DCCRGX_EHIP, "out of device memory for a refined field");
-            break;
-        }
-        hipMemsetAsync(np, 0, std::max<uint64_t>(ns, 1) * F.elem, st);
-        if (!sidx.empty()) s = launch_scatter_ext(F.ptr, d_s, d_d, sidx.size(), F.elem, np, st);
-        hipStreamSynchronize(st);
-        hipFree(F.ptr);
-        F.ptr = np;
-        if (s != DCCRGX_OK) break;
-    }
-    hipFree(d_s);
-    hipFree(d_d);
-    DX_TRY(s);
-    // new leaf state and neighborhoods: every plan of the old layout goes
-    // (uniform grids keep periodic self-copy segments and slab ranges)
-    for (auto& kv : grid->hoods) {
-        free_hood(kv.second);
+
+    // the old layout, kept aside for lookups and for a rollback
+    dccrgx_grid old;
+    old.ctx = ctx;
+    old.params = grid->params;
+    old.map = grid->map;
+    old.uniform = grid->uniform;
+    old.g = grid->g;
+    old.ex = grid->ex;
+    old.n_local = grid->n_local;
+    old.first_local = grid->first_local;
+    old.n_slots = grid->n_slots;
+    std::map<int32_t, Hood> old_hoods;
+    old_hoods.swap(grid->hoods);
+    for (auto& kv : old_hoods) {
         Hood fresh;
         fresh.id = kv.second.id;
         fresh.items = kv.second.items;
-        kv.second = std::move(fresh);
+        grid->hoods[kv.first] = std::move(fresh);
     }
-    if (grid->ex) explicit_destroy(grid);
+    std::vector<void*> np(grid->fields.size(), nullptr);
+    auto rollback = [&](int code) {
+        for (void* q : np) hipFree(q);
+        for (auto& kv : grid->hoods) free_hood(kv.second);
+        grid->hoods.swap(old_hoods);
+        explicit_free(grid->ex);
+        grid->ex = old.ex;
+        grid->uniform = old.uniform;
+        grid->n_local = old.n_local;
+        grid->first_local = old.first_local;
+        grid->n_slots = old.n_slots;
+        return code;
+    };
+
+    // the new leaf state and neighborhoods (fields untouched meanwhile)
+    grid->ex = nullptr;
     grid->uniform = false;
-    DX_TRY(explicit_init(grid, leaves.data(), n));
-    grid->ex->retired = retired;
-    grid->n_slots = ns;
-    for (auto& kv : grid->hoods) DX_TRY(explicit_build_hood(grid, kv.second));
+    int s = explicit_init(grid, leaves.data(), leaves.size());
+    if (s == DCCRGX_OK) grid->ex->defer_fields = true;
+    for (auto it = grid->hoods.begin(); s == DCCRGX_OK && it != grid->hoods.end(); ++it)
+        s = explicit_build_hood(grid, it->second);
+    if (s == DCCRGX_OK) s = explicit_add_slots(grid, retired);
+    if (s != DCCRGX_OK) return rollback(s);
+    Explicit* E = grid->ex;
+    E->defer_fields = false;
+    E->retired = retired;
+    const uint64_t ns = E->slot_ids.size();
+
+    // old slot of every new slot, from the old layout's own lookup
+    std::vector<uint64_t> sidx, didx;
+    for (uint64_t k = 0; k < ns; k++) {
+        const int64_t o = host_primary_slot(&old, E->slot_ids[k]);
+        if (o >= 0) {
+            sidx.push_back((uint64_t)o);
+            didx.push_back(k);
+        }
+    }
+    uint64_t *d_s = nullptr, *d_d = nullptr;
+    auto fail = [&](int code) {
+        hipFree(d_s);
+        hipFree(d_d);
+        return rollback(code);
+    };
+    if (hipMalloc(&d_s, std::max<size_t>(sidx.size(), 1) * 8) != hipSuccess ||
+        hipMalloc(&d_d, std::max<size_t>(didx.size(), 1) * 8) != hipSuccess)
+        return fail(set_error(DCCRGX_ENOMEM, "out of device memory for the rebuild plan"));
+    if (!sidx.empty() &&
+        (hipMemcpyAsync(d_s, sidx.data(), sidx.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+         hipMemcpyAsync(d_d, didx.data(), didx.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess))
+        return fail(set_error(DCCRGX_EHIP, "uploading the rebuild plan failed"));
+    for (size_t i = 0; i < grid->fields.size(); i++) {
+        const Field& F = grid->fields[i];
+        const size_t bytes = std::max<uint64_t>(ns, 1) * F.elem;
+        if (hipMalloc(&np[i], bytes) != hipSuccess) {
+            np[i] = nullptr;
+            return fail(set_error(DCCRGX_ENOMEM, "out of device memory for a refined field (%zu bytes)", bytes));
+        }
+        // new cells are value-initialised (dccrg.hpp:10375, 10590)
+        if (hipMemsetAsync(np[i], 0, bytes, st) != hipSuccess)
+            return fail(set_error(DCCRGX_EHIP, "clearing a refined field failed"));
+    }
+    for (size_t i = 0; i < grid->fields.size(); i++) {
+        const Field& F = grid->fields[i];
+        if (!sidx.empty() && launch_scatter_ext(F.ptr, d_s, d_d, sidx.size(), F.elem, np[i], st) != DCCRGX_OK)
+            return fail(DCCRGX_EHIP);
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(set_error(DCCRGX_EHIP, "moving field data failed"));
+    hipFree(d_s);
+    hipFree(d_d);
+    // commit
+    for (size_t i = 0; i < grid->fields.size(); i++) {
+        hipFree(grid->fields[i].ptr);
+        grid->fields[i].ptr = np[i];
+    }
+    for (auto& kv : old_hoods) free_hood(kv.second);
+    explicit_free(old.ex);
+    old.ex = nullptr;
+    return DCCRGX_OK;
+}
+
+// an estimate of the device memory the explicit form of the current grid
+// needs (replicated leaf ids, hash, slot map, every leaf's neighbor lists),
+// checked before a uniform grid is converted
+static int check_explicit_memory(const dccrgx_grid* grid, uint64_t N)
+{
+    uint64_t cap = 16;
+    while (cap < 2 * N) cap <<= 1;
+    double need = (double)N * (8 + 4 + 4 + 1) + (double)cap * 12;
+    for (const auto& kv : grid->hoods) {
+        const double K = (double)(kv.second.items.size() / 3);
+        need += (double)N * (16 + K * (8 + 12 + 4 + 4));  // rows, neighbors_of (+ transpose)
+    }
+    size_t free_b = 0, total_b = 0;
+    DX_HIP(hipMemGetInfo(&free_b, &total_b));
+    DX_CHECK(need < 0.9 * (double)free_b, DCCRGX_ENOMEM,
+             "refining a uniform grid of %llu cells needs ~%.1f GB of replicated leaf state and neighbor lists; "
+             "%.1f GB free", (unsigned long long)N, need / 1e9, free_b / 1e9);
     return DCCRGX_OK;
 }
 
@@ -307,6 +373,7 @@ int ensure_explicit(dccrgx_grid* grid)
     const uint64_t N = grid->g.N;
     DX_CHECK(N < (1ull << 32), DCCRGX_EINVAL, "grid of %llu cells is too large to refine",
              (unsigned long long)N);
+    DX_TRY(check_explicit_memory(grid, N));
     std::vector<uint64_t> leaves(N);
     for (uint64_t i = 0; i < N; i++) leaves[i] = i + 1;
     return rebuild(grid, leaves, {});
@@ -338,7 +405,20 @@ int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
                   part_owner(grid->g.part, cell) == grid->ctx->rank;
         return DCCRGX_OK;
     }
-    DX_TRY(ensure_explicit(grid));
+    if (grid->uniform) {
+        // dccrg.hpp:2476-2546 on a grid of level-0 cells: no coarser neighbor
+        // can block, no sibling or neighbor is marked for unrefinement.  The
+        // layout switch waits for the collective stop_refining, so every rank
+        // switches together.
+        if (map_level(grid->map, cell) != 0 || cell > grid->g.N ||
+            part_owner(grid->g.part, cell) != grid->ctx->rank)
+            return DCCRGX_OK;
+        Amr& A = amr_of(grid);
+        if (A.not_to_refine.count(cell)) return DCCRGX_OK;
+        A.to_refine.insert(cell);
+        *result = 1;
+        return DCCRGX_OK;
+    }
     const View v{grid, grid->ex, grid->map.max_lvl};
     Amr& A = amr_of(grid);
     // dccrg.hpp:2476-2546
@@ -629,7 +709,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     A.not_to_unrefine.clear();
     A.not_to_refine = donts;
     if (!R.empty() || !final_un.empty()) {
-        if (grid->ex) grid->ex->retired.clear();
+        if (grid->ex) explicit_clear_retired(grid->ex);
         DX_TRY(rebuild(grid, leaves, retired));
     }
     if (n_new) *n_new = A.new_cells.size();
@@ -659,7 +739,7 @@ int dccrgx_get_removed_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap,
 int dccrgx_clear_refined_unrefined_data(dccrgx_grid* grid)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
-    if (grid->ex) grid->ex->retired.clear();
+    if (grid->ex) explicit_clear_retired(grid->ex);
     if (grid->amr) grid->amr->removed.clear();
     return DCCRGX_OK;
 }

@@ -13,8 +13,9 @@
 // which is exactly where the walk ends on a 2:1-balanced grid (the
 // reference's own assumption, dccrg.hpp:4736-4737).  neighbors_to
 // (dccrg.hpp:4744-4897) is the transpose of neighbors_of on such grids; it
-// is built by transposing the device CSR.  Storage slot of a cell = its
-// global leaf index (fields are sized for all leaves).
+// is built by transposing the device CSR.  Only the leaf ids and the lists
+// are replicated; field storage is per rank: local cells, then ghosts, then
+// retired cells (grid.hpp, Explicit).
 #include <algorithm>
 #include <cstring>
 #include <set>
@@ -261,6 +262,7 @@ __global__ void __launch_bounds__(256) k_stencil_rows(const uint64_t* __restrict
 
 __global__ void __launch_bounds__(256) k_stencil_slots(const uint64_t* __restrict__ tmp_row, const Pair* __restrict__ tmp,
                                                        const uint64_t* __restrict__ st_row, uint64_t nl,
+                                                       const uint32_t* __restrict__ slot_of_g,
                                                        uint32_t* __restrict__ st_slot, int32_t* __restrict__ st_off)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -268,7 +270,7 @@ __global__ void __launch_bounds__(256) k_stencil_slots(const uint64_t* __restric
         for (uint64_t e = 0; e < st_row[i + 1] - st_row[i]; e++) {
             const Pair& p = tmp[tmp_row[i] + e];
             const uint64_t o = st_row[i] + e;
-            st_slot[o] = p.g;
+            st_slot[o] = slot_of_g[p.g];
             st_off[3 * o + 0] = p.x;
             st_off[3 * o + 1] = p.y;
             st_off[3 * o + 2] = p.z;
@@ -278,7 +280,7 @@ __global__ void __launch_bounds__(256) k_stencil_slots(const uint64_t* __restric
 __global__ void __launch_bounds__(256) k_ex_gol(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ cnt, const uint64_t* __restrict__ st_row,
                                                 const uint32_t* __restrict__ st_slot,
-                                                const uint32_t* __restrict__ local_g,
+                                                const uint32_t* __restrict__ local_slot,
                                                 const uint32_t* __restrict__ pos, uint64_t n)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -286,17 +288,22 @@ __global__ void __launch_bounds__(256) k_ex_gol(const uint32_t* __restrict__ in,
         const uint32_t q = pos[i];
         uint32_t c = 0;
         for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) c += in[st_slot[e]] != 0u ? 1u : 0u;
-        const uint32_t s = local_g[q];
+        const uint32_t s = local_slot[q];
         cnt[s] = c;
         out[s] = c == 3u ? 1u : (c == 2u ? in[s] : 0u);
     }
 }
 
-__global__ void __launch_bounds__(256) k_ex_slots(ExView v, const uint64_t* __restrict__ ids, size_t n,
+__global__ void __launch_bounds__(256) k_ex_slots(ExView v, const uint32_t* __restrict__ slot_of_g,
+                                                  const uint64_t* __restrict__ ids, size_t n,
                                                   int64_t* __restrict__ slots)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) slots[i] = ex_find(v, ids[i]);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t g = ex_find(v, ids[i]);
+        const uint32_t s = g < 0 ? NO_SLOT : slot_of_g[g];
+        slots[i] = s == NO_SLOT ? -1 : (int64_t)s;
+    }
 }
 
 static unsigned grid_for(uint64_t n)
@@ -379,6 +386,8 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     return DCCRGX_OK;
 }
 
+static int sync_slots(dccrgx_grid* grid);
+
 int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
 {
     Ctx* ctx = grid->ctx;
@@ -389,15 +398,9 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     E->leaves.assign(leaves, leaves + n);
     std::sort(E->leaves.begin(), E->leaves.end());
     E->leaves.erase(std::unique(E->leaves.begin(), E->leaves.end()), E->leaves.end());
-    std::vector<uint8_t> level;
-    level.reserve(E->leaves.size());
-    for (uint64_t c : E->leaves) {
-        const int l = map_level(grid->map, c);
-        DX_CHECK(l >= 0, DCCRGX_EINVAL, "invalid cell %llu", (unsigned long long)c);
-        level.push_back((uint8_t)l);
-    }
+    for (uint64_t c : E->leaves)
+        DX_CHECK(map_level(grid->map, c) >= 0, DCCRGX_EINVAL, "invalid cell %llu", (unsigned long long)c);
     E->n = E->leaves.size();
-    DX_TRY(upload(level, &E->d_level, st));
     uint64_t cap = 16;
     while (cap < 2 * E->n) cap <<= 1;
     E->mask = cap - 1;
@@ -423,8 +426,103 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     DX_TRY(upload(E->local_g, &E->d_local_g, st));
     grid->n_local = E->local.size();
     grid->first_local = E->local.empty() ? 0 : E->local[0];
-    grid->n_slots = E->n;
+    // storage: the local cells first (ghosts are added by the neighborhoods)
+    E->slot_ids = E->local;
+    E->slot_of_g.assign(E->n, NO_SLOT);
+    for (uint64_t i = 0; i < E->local.size(); i++) E->slot_of_g[E->local_g[i]] = (uint32_t)i;
+    std::vector<uint32_t> ident(E->local.size());
+    for (uint64_t i = 0; i < ident.size(); i++) ident[i] = (uint32_t)i;
+    DX_TRY(upload(ident, &E->d_local_slot, st));
+    DX_TRY(sync_slots(grid));
     return DCCRGX_OK;
+}
+
+// device copies of the slot map and per-slot levels; n_slots
+static int sync_slots(dccrgx_grid* grid)
+{
+    Explicit* E = grid->ex;
+    hipStream_t st = grid->ctx->compute;
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(E->d_slot_of_g);
+    hipFree(E->d_level);
+    E->d_slot_of_g = nullptr;
+    E->d_level = nullptr;
+    std::vector<uint8_t> level(E->slot_ids.size());
+    for (size_t s = 0; s < level.size(); s++) level[s] = (uint8_t)map_level(grid->map, E->slot_ids[s]);
+    DX_TRY(upload(E->slot_of_g, &E->d_slot_of_g, st));
+    DX_TRY(upload(level, &E->d_level, st));
+    DX_HIP(hipStreamSynchronize(st));
+    grid->n_slots = E->slot_ids.size();
+    return DCCRGX_OK;
+}
+
+// every field grows to `ns` slots (new slots zero, value-initialised ghosts
+// as allocate_copies_of_remote_neighbors, dccrg.hpp:7153-7184); all new
+// arrays are allocated before any pointer is swapped
+static int grow_fields(dccrgx_grid* grid, uint64_t old_ns, uint64_t ns)
+{
+    hipStream_t st = grid->ctx->compute;
+    std::vector<void*> np(grid->fields.size(), nullptr);
+    int s = DCCRGX_OK;
+    for (size_t i = 0; i < grid->fields.size() && s == DCCRGX_OK; i++) {
+        const Field& F = grid->fields[i];
+        if (F.variable) continue;
+        if (hipMalloc(&np[i], std::max<uint64_t>(ns, 1) * F.elem) != hipSuccess) {
+            np[i] = nullptr;
+            s = set_error(DCCRGX_ENOMEM, "out of device memory for %llu ghost slots", (unsigned long long)ns);
+            break;
+        }
+        if (hipMemsetAsync(np[i], 0, std::max<uint64_t>(ns, 1) * F.elem, st) != hipSuccess ||
+            (old_ns && hipMemcpyAsync(np[i], F.ptr, old_ns * F.elem, hipMemcpyDeviceToDevice, st) != hipSuccess))
+            s = set_error(DCCRGX_EHIP, "growing field %zu failed", i);
+    }
+    if (s == DCCRGX_OK && hipStreamSynchronize(st) != hipSuccess) s = set_error(DCCRGX_EHIP, "growing fields failed");
+    if (s != DCCRGX_OK) {
+        for (void* q : np) hipFree(q);
+        return s;
+    }
+    for (size_t i = 0; i < grid->fields.size(); i++) {
+        Field& F = grid->fields[i];
+        if (F.variable) {  // new slots hold zero elements
+            F.count.resize(ns, 0);
+            F.off.resize(ns, F.pool_bytes);
+            continue;
+        }
+        hipFree(F.ptr);
+        F.ptr = np[i];
+    }
+    return DCCRGX_OK;
+}
+
+int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
+{
+    Explicit* E = grid->ex;
+    const uint64_t old_ns = E->slot_ids.size();
+    for (uint64_t c : ids) {
+        if (std::binary_search(E->local.begin(), E->local.end(), c) || E->extra.count(c)) continue;
+        const uint32_t s = (uint32_t)E->slot_ids.size();
+        E->slot_ids.push_back(c);
+        E->extra[c] = s;
+        auto it = std::lower_bound(E->leaves.begin(), E->leaves.end(), c);
+        if (it != E->leaves.end() && *it == c) E->slot_of_g[it - E->leaves.begin()] = s;
+    }
+    const uint64_t ns = E->slot_ids.size();
+    DX_CHECK(ns < NO_SLOT, DCCRGX_EINVAL, "%llu storage slots on one rank", (unsigned long long)ns);
+    if (ns == old_ns) return DCCRGX_OK;
+    if (!E->defer_fields) {
+        const int s = grow_fields(grid, old_ns, ns);
+        if (s != DCCRGX_OK) {  // undo the new slots
+            for (uint64_t k = old_ns; k < ns; k++) {
+                const uint64_t c = E->slot_ids[k];
+                E->extra.erase(c);
+                auto it = std::lower_bound(E->leaves.begin(), E->leaves.end(), c);
+                if (it != E->leaves.end() && *it == c) E->slot_of_g[it - E->leaves.begin()] = NO_SLOT;
+            }
+            E->slot_ids.resize(old_ns);
+            return s;
+        }
+    }
+    return sync_slots(grid);
 }
 
 int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
@@ -448,21 +546,31 @@ int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     return explicit_build_hood(grid, grid->hoods[h.id]);
 }
 
-void explicit_destroy(dccrgx_grid* grid)
+void explicit_free(Explicit* E)
 {
-    Explicit* E = grid->ex;
     if (!E) return;
-    hipFree(E->d_leaves);
-    hipFree(E->d_keys);
-    hipFree(E->d_vals);
-    hipFree(E->d_local_g);
-    hipFree(E->d_level);
+    for (void* q : {(void*)E->d_leaves, (void*)E->d_keys, (void*)E->d_vals, (void*)E->d_local_g,
+                    (void*)E->d_level, (void*)E->d_slot_of_g, (void*)E->d_local_slot})
+        hipFree(q);
     for (auto& kv : E->hl) {
         hipFree(kv.second.d_inner_pos);
         hipFree(kv.second.d_outer_pos);
         hipFree(kv.second.d_all_pos);
     }
     delete E;
+}
+
+// retired cells' data is no longer addressable (their slots are reused by
+// the next rebuild)
+void explicit_clear_retired(Explicit* E)
+{
+    for (uint64_t c : E->retired) E->extra.erase(c);
+    E->retired.clear();
+}
+
+void explicit_destroy(dccrgx_grid* grid)
+{
+    explicit_free(grid->ex);
     grid->ex = nullptr;
 }
 
@@ -515,46 +623,18 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     hipFree(d_ucnt);
     hipFree(d_trow);
 
-    // stencil rows of local cells (iteration-cache neighbors_of: unique pairs)
+    // per-rank bookkeeping from the device lists (dccrg.hpp:9131-9234, 8729-8891)
     const uint64_t nl = E->local.size();
     std::vector<uint64_t> nof_row(N + 1);
     DX_HIP(hipMemcpyAsync(nof_row.data(), h.d_nof_row, (N + 1) * 8, hipMemcpyDeviceToHost, st));
-    DX_HIP(hipStreamSynchronize(st));
-    std::vector<uint64_t> tmp_row(nl + 1, 0);
-    for (uint64_t i = 0; i < nl; i++) {
-        const uint32_t r = E->local_g[i];
-        tmp_row[i + 1] = tmp_row[i] + (nof_row[r + 1] - nof_row[r]);
-    }
-    uint64_t* d_tmp_row = nullptr;
-    Pair* d_pairs = nullptr;
-    uint32_t* d_pc = nullptr;
-    DX_TRY(upload(tmp_row, &d_tmp_row, st));
-    DX_HIP(hipMalloc(&d_pairs, std::max<uint64_t>(tmp_row[nl], 1) * sizeof(Pair)));
-    DX_HIP(hipMalloc(&d_pc, std::max<uint64_t>(nl, 1) * 4));
-    if (nl)
-        hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
-                           h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
-    std::vector<uint64_t> st_row;
-    DX_TRY(scan_counts_u32(d_pc, nl, st_row, st));
-    DX_TRY(upload(st_row, &h.d_st_row, st));
-    DX_HIP(hipMalloc(&h.d_st_slot, std::max<uint64_t>(st_row[nl], 1) * 4));
-    DX_HIP(hipMalloc(&h.d_st_off, std::max<uint64_t>(st_row[nl], 1) * 12));
-    if (nl)
-        hipLaunchKernelGGL(k_stencil_slots, dim3(grid_for(nl)), dim3(256), 0, st, d_tmp_row, d_pairs, h.d_st_row, nl,
-                           h.d_st_slot, h.d_st_off);
-    DX_HIP(hipGetLastError());
-    hipFree(d_tmp_row);
-    hipFree(d_pairs);
-    hipFree(d_pc);
-
-    // per-rank bookkeeping from the device lists (dccrg.hpp:9131-9234, 8729-8891)
     Explicit::HoodLists& L = E->hl[h.id];
     for (uint32_t* p : {L.d_inner_pos, L.d_outer_pos, L.d_all_pos}) hipFree(p);
     L = Explicit::HoodLists{};
-    L.h_nof_row = nof_row;
-    L.h_nof_g.resize(nof_row[N]);
     L.h_nto_row = nto_row;
     L.h_nto_g.resize(nto_row[N]);
+    DX_HIP(hipStreamSynchronize(st));
+    L.h_nof_row = nof_row;
+    L.h_nof_g.resize(nof_row[N]);
     if (nof_row[N]) DX_HIP(hipMemcpyAsync(L.h_nof_g.data(), h.d_nof_g, nof_row[N] * 4, hipMemcpyDeviceToHost, st));
     if (nto_row[N]) DX_HIP(hipMemcpyAsync(L.h_nto_g.data(), h.d_nto_g, nto_row[N] * 4, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
@@ -592,11 +672,44 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
         if (outer) h.outer.push_back(E->local[i]);
     }
     h.remote.assign(remote.begin(), remote.end());
+    // ghost slots for this neighborhood's remote neighbors
+    DX_TRY(explicit_add_slots(grid, h.remote));
+
+    // stencil rows of local cells (iteration-cache neighbors_of: unique pairs)
+    std::vector<uint64_t> tmp_row(nl + 1, 0);
+    for (uint64_t i = 0; i < nl; i++) {
+        const uint32_t r = E->local_g[i];
+        tmp_row[i + 1] = tmp_row[i] + (nof_row[r + 1] - nof_row[r]);
+    }
+    uint64_t* d_tmp_row = nullptr;
+    Pair* d_pairs = nullptr;
+    uint32_t* d_pc = nullptr;
+    DX_TRY(upload(tmp_row, &d_tmp_row, st));
+    DX_HIP(hipMalloc(&d_pairs, std::max<uint64_t>(tmp_row[nl], 1) * sizeof(Pair)));
+    DX_HIP(hipMalloc(&d_pc, std::max<uint64_t>(nl, 1) * 4));
+    if (nl)
+        hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
+                           h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
+    std::vector<uint64_t> st_row;
+    DX_TRY(scan_counts_u32(d_pc, nl, st_row, st));
+    DX_TRY(upload(st_row, &h.d_st_row, st));
+    DX_HIP(hipMalloc(&h.d_st_slot, std::max<uint64_t>(st_row[nl], 1) * 4));
+    DX_HIP(hipMalloc(&h.d_st_off, std::max<uint64_t>(st_row[nl], 1) * 12));
+    if (nl)
+        hipLaunchKernelGGL(k_stencil_slots, dim3(grid_for(nl)), dim3(256), 0, st, d_tmp_row, d_pairs, h.d_st_row, nl,
+                           E->d_slot_of_g, h.d_st_slot, h.d_st_off);
+    DX_HIP(hipGetLastError());
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_tmp_row);
+    hipFree(d_pairs);
+    hipFree(d_pc);
+
+    // per-peer plans: send from local slots, receive into ghost slots
     std::set<int> peers;
     for (auto& kv : send) peers.insert(kv.first);
     for (auto& kv : recv) peers.insert(kv.first);
-    auto gidx_of = [&](uint64_t id) {
-        return (uint64_t)(std::lower_bound(E->leaves.begin(), E->leaves.end(), id) - E->leaves.begin());
+    auto local_pos = [&](uint64_t id) {
+        return (uint64_t)(std::lower_bound(E->local.begin(), E->local.end(), id) - E->local.begin());
     };
     for (int p : peers) {
         PeerPlan pp;
@@ -604,8 +717,8 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
         pp.send_ids.assign(send[p].begin(), send[p].end());
         pp.recv_ids.assign(recv[p].begin(), recv[p].end());
         std::vector<uint64_t> ss, rd;
-        for (uint64_t c : pp.send_ids) ss.push_back(gidx_of(c));
-        for (uint64_t c : pp.recv_ids) rd.push_back(gidx_of(c));
+        for (uint64_t c : pp.send_ids) ss.push_back(local_pos(c));
+        for (uint64_t c : pp.recv_ids) rd.push_back(E->extra.at(c));
         if (!ss.empty()) DX_TRY(upload(ss, &pp.d_send_slots, st));
         if (!rd.empty()) DX_TRY(upload(rd, &pp.d_unpack_dst, st));
         pp.n_unpack = rd.size();
@@ -650,18 +763,19 @@ int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, ui
 
 int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id)
 {
-    const auto& L = grid->ex->leaves;
-    auto it = std::lower_bound(L.begin(), L.end(), id);
-    if (it != L.end() && *it == id) return (int64_t)(it - L.begin());
-    // data of a refined / unrefined cell kept until clear_refined_unrefined_data
-    const auto& R = grid->ex->retired;
-    auto jt = std::lower_bound(R.begin(), R.end(), id);
-    return (jt != R.end() && *jt == id) ? (int64_t)(L.size() + (jt - R.begin())) : -1;
+    const Explicit* E = grid->ex;
+    auto it = std::lower_bound(E->local.begin(), E->local.end(), id);
+    if (it != E->local.end() && *it == id) return (int64_t)(it - E->local.begin());
+    // ghosts, and data of refined / unrefined cells kept until
+    // clear_refined_unrefined_data
+    auto jt = E->extra.find(id);
+    return jt != E->extra.end() ? (int64_t)jt->second : -1;
 }
 
 int explicit_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int64_t* slots, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_ex_slots, dim3(grid_for(n)), dim3(256), 0, st, view(grid), ids, n, slots);
+    hipLaunchKernelGGL(k_ex_slots, dim3(grid_for(n)), dim3(256), 0, st, view(grid), grid->ex->d_slot_of_g, ids, n,
+                       slots);
     DX_HIP(hipGetLastError());
     return DCCRGX_OK;
 }
@@ -739,7 +853,7 @@ int explicit_region(const dccrgx_grid* grid, const Hood& h, int32_t region, ExRe
                : region == DCCRGX_REGION_OUTER ? L.d_outer_pos : L.d_all_pos;
     out->n = region == DCCRGX_REGION_INNER ? L.inner_pos.size()
              : region == DCCRGX_REGION_OUTER ? L.outer_pos.size() : E->local.size();
-    out->local_g = E->d_local_g;
+    out->local_slot = E->d_local_slot;
     out->level = E->d_level;
     return DCCRGX_OK;
 }
@@ -751,35 +865,21 @@ int explicit_gol(dccrgx_grid* grid, const Hood& h, const Field& in, const Field&
     DX_TRY(explicit_region(grid, h, region, &R));
     if (!R.n) return DCCRGX_OK;
     hipLaunchKernelGGL(k_ex_gol, dim3(grid_for(R.n)), dim3(256), 0, st, (const uint32_t*)in.ptr,
-                       (uint32_t*)out.ptr, (uint32_t*)cnt.ptr, h.d_st_row, h.d_st_slot, R.local_g, R.pos, R.n);
+                       (uint32_t*)out.ptr, (uint32_t*)cnt.ptr, h.d_st_row, h.d_st_slot, R.local_slot, R.pos, R.n);
     DX_HIP(hipGetLastError());
     return DCCRGX_OK;
 }
 
-// local values in ascending id order <-> slots (global leaf index)
+// local values in ascending id order <-> slots [0, nl)
 int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device)
 {
-    const Explicit* E = grid->ex;
-    hipStream_t st = grid->ctx->compute;
-    const uint64_t n = E->local.size();
+    const uint64_t n = grid->ex->local.size();
     if (!n) return DCCRGX_OK;
-    void* d_buf = nullptr;
-    uint64_t* d_idx = nullptr;
-    std::vector<uint64_t> idx(E->local_g.begin(), E->local_g.end());
-    DX_TRY(upload(idx, &d_idx, st));
-    DX_HIP(hipMalloc(&d_buf, n * F.elem));
-    int s = DCCRGX_OK;
-    if (to_device) {
-        DX_HIP(hipMemcpyAsync(d_buf, host, n * F.elem, hipMemcpyHostToDevice, st));
-        s = launch_scatter_ext(d_buf, nullptr, d_idx, n, F.elem, F.ptr, st);
-    } else {
-        s = launch_gather_ext(F.ptr, d_idx, n, F.elem, d_buf, st);
-        if (s == DCCRGX_OK) DX_HIP(hipMemcpyAsync(host, d_buf, n * F.elem, hipMemcpyDeviceToHost, st));
-    }
+    hipStream_t st = grid->ctx->compute;
+    if (to_device) DX_HIP(hipMemcpyAsync(F.ptr, host, n * F.elem, hipMemcpyHostToDevice, st));
+    else DX_HIP(hipMemcpyAsync(host, F.ptr, n * F.elem, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_buf);
-    hipFree(d_idx);
-    return s;
+    return DCCRGX_OK;
 }
 
 }  // namespace dccrgx

@@ -5,6 +5,7 @@
 #include "internal.hpp"
 
 #include <set>
+#include <unordered_map>
 
 namespace dccrgx {
 
@@ -129,7 +130,18 @@ struct Explicit {
     std::vector<uint64_t> local;    // ascending local ids
     std::vector<uint32_t> local_g;  // their global indices
     uint32_t* d_local_g = nullptr;
-    uint8_t* d_level = nullptr;     // refinement level of each leaf (global index)
+    // Storage (per rank, not replicated): slots [0, nl) hold the local cells
+    // in ascending id order, then ghost copies of remote neighbors (of every
+    // neighborhood), then the data of retired cells.  Fields are sized for
+    // these slots only, as the reference stores data only for local cells and
+    // remote neighbors (dccrg.hpp:7238, 7330).
+    std::vector<uint64_t> slot_ids;                 // id held by each slot
+    std::unordered_map<uint64_t, uint32_t> extra;   // ghost / retired id -> slot
+    std::vector<uint32_t> slot_of_g;                // global leaf index -> slot (NO_SLOT)
+    uint32_t* d_slot_of_g = nullptr;
+    uint32_t* d_local_slot = nullptr;               // local position -> slot (identity)
+    uint8_t* d_level = nullptr;                     // refinement level of each slot
+    bool defer_fields = false;                      // rebuild(): fields are moved afterwards
     struct HoodLists {
         std::vector<uint64_t> h_nof_row, h_nto_row;
         std::vector<uint32_t> h_nof_g, h_nto_g;
@@ -142,7 +154,7 @@ struct Explicit {
     // data of cells removed by the last stop_refining (refined parents and
     // unrefined children of this rank), readable until
     // clear_refined_unrefined_data (dccrg.hpp:3519-3543, 5550-5567): ascending
-    // ids, stored at slots n + i of every field
+    // ids, stored in slots after the ghosts
     std::vector<uint64_t> retired;
 };
 
@@ -247,15 +259,21 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
 void region_slices(const dccrgx_grid* grid, const Hood& h, int32_t region, int64_t r[2][2]);
 // explicit grids: local cells of a region as positions into the local list
 struct ExRegion {
-    const uint32_t* pos = nullptr;      // positions in the local cell list
+    const uint32_t* pos = nullptr;         // positions in the local cell list
     uint64_t n = 0;
-    const uint32_t* local_g = nullptr;  // local position -> storage slot
-    const uint8_t* level = nullptr;     // storage slot -> refinement level
+    const uint32_t* local_slot = nullptr;  // local position -> storage slot
+    const uint8_t* level = nullptr;        // storage slot -> refinement level
 };
+constexpr uint32_t NO_SLOT = 0xffffffffu;
 int explicit_region(const dccrgx_grid* grid, const Hood& h, int32_t region, ExRegion* out);
 // explicit (mixed refinement level) grids, explicit.hip
 int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n);
 void explicit_destroy(dccrgx_grid* grid);
+void explicit_free(Explicit* E);
+void explicit_clear_retired(Explicit* E);
+// explicit grids: give `ids` (leaves or retired cells) storage slots if they
+// have none, growing every field unless a rebuild defers that
+int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids);
 int explicit_build_hood(dccrgx_grid* grid, Hood& h);
 int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, uint64_t* ids,
                        size_t cap, size_t* n);

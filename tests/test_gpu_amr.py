@@ -210,8 +210,9 @@ def test_uniform_grid_switches_layout_on_refine():
     g.write_local("a", (ids % 7).astype(np.uint32))
     assert g.info.uniform == 1
     assert g.refine_completely(33) == o.refine_completely(0, 33)
-    assert g.info.uniform == 0
+    assert g.info.uniform == 1  # the switch waits for the collective stop_refining
     new = g.stop_refining()
+    assert g.info.uniform == 0
     assert [int(c) for c in new] == o.stop_refining()[0]
     loc = g.local_cells()
     vals = g.read_local("a")
@@ -262,3 +263,132 @@ def test_adaptive_advection_matches_oracle(cells, M, steps):
         assert abs(dt - ref.dt) <= 1e-15 * ref.dt
     g.close()
     ctx.close()
+
+
+def test_layout_switch_is_collective():
+    """A request for a remote or non-existent cell switches nothing; ranks
+    switch together inside stop_refining, also when only one rank asked."""
+    length, M, per = (6, 5, 4), 1, (False, True, True)
+    o = AmrOracle(length, M, per, 1, 2)
+    grids = make_ranks(length, M, per, 1, 2)
+    remote = int(grids[1].local_cells()[0])
+    assert not grids[0].refine_completely(remote)
+    assert not grids[0].refine_completely(10 ** 9)
+    assert all(g.info.uniform == 1 for g in grids)
+    new = stop_all(grids)
+    assert all(g.info.uniform == 1 for g in grids) and all(n.size == 0 for n in new)
+    assert grids[1].refine_completely(remote) == o.refine_completely(1, remote)
+    assert grids[0].info.uniform == 1
+    new = stop_all(grids)
+    want = o.stop_refining()
+    assert all(g.info.uniform == 0 for g in grids)
+    for r in range(2):
+        assert [int(c) for c in new[r]] == want[r]
+    check_structure(grids, o)
+    for g in grids:
+        g.close()
+
+
+def test_explicit_storage_is_per_rank():
+    """Fields of a refined grid hold the rank's local cells, its ghosts and
+    retired cells only -- not the whole grid (the reference stores data
+    only for local cells and copies of remote neighbors)."""
+    length, M, per = (8, 8, 8), 1, (True, True, True)
+    P = 4
+    grids = make_ranks(length, M, per, 1, P)
+    for g in grids:
+        g.add_field("a", np.float64)
+    r0 = int(grids[0].local_cells()[3])
+    grids[0].refine_completely(r0)
+    stop_all(grids)
+    total = sum(g.n_local for g in grids)
+    for g in grids:
+        nghost = len(g.remote_cells())
+        retired = 1 if g is grids[0] else 0
+        assert g.info.n_slots == g.n_local + nghost + retired
+        assert g.info.n_slots < total
+    # a user neighborhood lies inside the default one (dccrg.hpp:6573-6618),
+    # so its ghosts already have slots; data stays put
+    for g in grids:
+        vals = g.local_cells().astype(np.float64)
+        g.write_local("a", vals)
+        items = [(1, 1, 1), (-1, -1, -1), (0, 0, 1)]
+        assert g.add_neighborhood(7, items)
+        assert np.array_equal(g.read_local("a"), vals)
+        ghosts = set(int(c) for c in g.remote_cells()) | set(int(c) for c in g.remote_cells(7))
+        g._refresh_info()
+        assert g.info.n_slots == g.n_local + len(ghosts) + (1 if g is grids[0] else 0)
+    for g in grids:
+        g.close()
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_adaptive_advection_multirank(P):
+    """tests/advection/2d.cpp with adapt_n = 1 on P ranks (driven in one
+    process; ghosts move through the same pack / unpack plans the RCCL path
+    uses).  Per-rank leaf sets and densities match the oracle's P-rank run
+    (check_for_adaptation depends on which neighbors are local)."""
+    from dccrg_amd import advection as A
+    from oracle.dccrg_amr import AdvectionAmrOracle
+    from test_gpu_explicit import loopback
+    cells, M, steps = 16, 2, 4
+    rel, thr, sens, cfl = 0.025, 0.25, 0.5, 0.5
+    ref = AdvectionAmrOracle(cells, M, P, rel, thr, sens, cfl)
+    grids = []
+    for r in range(P):
+        c = D.Context(0, r, P)
+        g = (D.Dccrg().set_initial_length((cells, cells, 1)).set_maximum_refinement_level(M)
+             .set_periodic(True, True, False).set_neighborhood_length(0).initialize(c))
+        g._keep = c
+        g.add_advection_fields()
+        grids.append(g)
+    geoms = [A.geometry_2d(g) for g in grids]
+
+    def init_all():
+        for g, geom in zip(grids, geoms):
+            A.initialize(g, geom, update=False)
+        loopback(grids, list(A.ALL))
+
+    def adapt_all(sets):
+        for g, s in zip(grids, sets):
+            A.request_adaptation(g, *s)
+        reqs = [g.amr_requests() for g in grids]
+        union = [np.unique(np.concatenate([q[k] for q in reqs])).astype(np.uint64) for k in range(4)]
+        for g, geom in zip(grids, geoms):
+            A.finish_adaptation(g, geom, all_requests=union, update=False)
+        loopback(grids, list(A.ALL))
+
+    init_all()
+    for _ in range(M):
+        adapt_all([A.check_for_adaptation(g, rel / M, thr, sens) for g in grids])
+        init_all()
+
+    def compare(tag):
+        rc, ra = ref.arrays()
+        pos = {c: i for i, c in enumerate(rc)}
+        assert sorted(int(c) for g in grids for c in g.local_cells()) == rc, tag
+        scale = np.max(np.abs(ra[0]))
+        for r, g in enumerate(grids):
+            loc = [int(c) for c in g.local_cells()]
+            assert loc == [c for c in rc if ref.o.owner(c) == r], tag
+            rho = g.read_local("density")
+            want = ra[0][[pos[c] for c in loc]]
+            assert np.max(np.abs(rho - want), initial=0.0) <= 1e-12 * scale, tag
+
+    compare("prerefined")
+    dt = min(g.max_time_step() for g in grids)
+    assert abs(dt - ref.dt) <= 1e-15 * ref.dt
+    for s in range(steps):
+        loopback(grids, ["density"])
+        sets = [A.check_for_adaptation(g, rel / M, thr, sens) for g in grids]
+        for g in grids:
+            g.calculate_fluxes(cfl * dt, True)
+            g.calculate_fluxes(cfl * dt, False)
+            g.apply_fluxes()
+        adapt_all(sets)
+        dt = min(g.max_time_step() for g in grids)
+        ref.step()
+        compare(f"step {s}")
+        assert abs(dt - ref.dt) <= 1e-15 * ref.dt
+    for g in grids:
+        g.close()
