@@ -16,9 +16,20 @@
  * the GPU.  The device-speed path (SoA fields + device stencils) is the C-ABI
  * itself (dccrgx_field_*, dccrgx_gol_*), reachable via device_grid().
  *
- * MPI is used for bootstrap only (rank, size, broadcasting the RCCL id).
- * Load balancing (Zoltan) and refinement are not part of this path:
- * balance_load() keeps the reference's non-Zoltan block partition.
+ * Adaptive refinement: refine_completely / unrefine_completely /
+ * dont_refine / dont_unrefine record this rank's requests in libdccrgx;
+ * stop_refining() all-gathers the four request sets with MPI_Allgatherv and
+ * hands their union to dccrgx_stop_refining, which makes the reference's
+ * decisions (override / induce / execute, dccrg.hpp:9730-10693) and rebuilds
+ * the device structures; the facade then moves host cell data exactly as the
+ * reference does (refined parents and removed children stay readable through
+ * operator[] until clear_refined_unrefined_data, new cells are
+ * value-initialised) and rebuilds its iteration caches.
+ *
+ * MPI is used for bootstrap (rank, size, broadcasting the RCCL id) and for
+ * the all-gather of refinement requests.  Load balancing (Zoltan) is not part
+ * of this path: balance_load() keeps the reference's non-Zoltan block
+ * partition.
  */
 #ifndef DCCRG_AMD_HPP
 #define DCCRG_AMD_HPP
@@ -360,15 +371,88 @@ public:
     unsigned get_neighborhood_length() const { return hood_length_; }
     const Grid_Length& length() const { return mapping.length; }
 
-    // dccrg.hpp:768-781: local cells, then copies of remote neighbors
+    // dccrg.hpp:768-781: local cells, copies of remote neighbors, then data
+    // of refined / unrefined cells (until clear_refined_unrefined_data)
     Cell_Data* operator[](uint64_t cell) const
     {
-        auto it = cell_data_.find(cell);
-        if (it != cell_data_.end()) return const_cast<Cell_Data*>(&it->second);
-        auto jt = remote_data_.find(cell);
-        if (jt != remote_data_.end()) return const_cast<Cell_Data*>(&jt->second);
+        for (const auto* m : {&cell_data_, &remote_data_, &refined_data_, &unrefined_data_}) {
+            auto it = m->find(cell);
+            if (it != m->end()) return const_cast<Cell_Data*>(&it->second);
+        }
         return nullptr;
     }
+
+    // ---- adaptive mesh refinement (dccrg.hpp:2456-2806, 3483-3543, 5550-5567)
+    bool refine_completely(uint64_t cell) { return request(dccrgx_refine_completely, cell); }
+    bool unrefine_completely(uint64_t cell) { return request(dccrgx_unrefine_completely, cell); }
+    bool dont_refine(uint64_t cell) { return request(dccrgx_dont_refine, cell); }
+    bool dont_unrefine(uint64_t cell) { return request(dccrgx_dont_unrefine, cell); }
+
+    // collective; returns the cells created on this rank
+    std::vector<uint64_t> stop_refining(bool sorted = false)
+    {
+        std::vector<uint64_t> sets[4];
+        for (int k = 0; k < 4; k++) {
+            size_t n = 0;
+            detail::check(dccrgx_amr_requests(grid_, k, nullptr, 0, &n), "amr_requests");
+            std::vector<uint64_t> mine(n);
+            detail::check(dccrgx_amr_requests(grid_, k, mine.data(), n, &n), "amr_requests");
+            int cnt = (int)n;
+            std::vector<int> counts(size_), displs(size_, 0);
+            MPI_Allgather(&cnt, 1, MPI_INT, counts.data(), 1, MPI_INT, comm_);
+            for (int r = 1; r < size_; r++) displs[r] = displs[r - 1] + counts[r - 1];
+            sets[k].resize((size_t)displs[size_ - 1] + counts[size_ - 1]);
+            MPI_Allgatherv(mine.data(), cnt, MPI_UINT64_T, sets[k].data(), counts.data(), displs.data(),
+                           MPI_UINT64_T, comm_);
+            std::sort(sets[k].begin(), sets[k].end());
+            sets[k].erase(std::unique(sets[k].begin(), sets[k].end()), sets[k].end());
+        }
+        const uint64_t* ptrs[4] = {sets[0].data(), sets[1].data(), sets[2].data(), sets[3].data()};
+        const size_t counts[4] = {sets[0].size(), sets[1].size(), sets[2].size(), sets[3].size()};
+        size_t n_new = 0;
+        detail::check(dccrgx_stop_refining(grid_, ptrs, counts, &n_new), "stop_refining");
+        std::vector<uint64_t> created = id_list(dccrgx_get_new_cells);
+        // data moves as execute_refines moves it (dccrg.hpp:10266-10267,
+        // 10354-10375, 10526-10590): previous refined/unrefined data dropped,
+        // local cells that stopped being leaves kept aside, new cells
+        // value-initialised
+        refined_data_.clear();
+        unrefined_data_.clear();
+        const std::vector<uint64_t> removed = id_list(dccrgx_get_removed_cells);
+        const std::unordered_set<uint64_t> removed_set(removed.begin(), removed.end());
+        const std::vector<uint64_t> local = get_cells();
+        const std::unordered_set<uint64_t> now(local.begin(), local.end());
+        for (auto it = cell_data_.begin(); it != cell_data_.end();) {
+            if (now.count(it->first)) {
+                ++it;
+                continue;
+            }
+            (removed_set.count(it->first) ? unrefined_data_ : refined_data_)[it->first] = std::move(it->second);
+            it = cell_data_.erase(it);
+        }
+        for (uint64_t c : local) cell_data_[c];
+        remote_data_.clear();
+        std::vector<int> ids;
+        for (auto& kv : hoods_) ids.push_back(kv.first);
+        hoods_.clear();
+        for (int id : ids) build_hood(id);
+        if (sorted) std::sort(created.begin(), created.end());
+        return created;
+    }
+    std::vector<uint64_t> get_removed_cells(bool sorted = false) const
+    {
+        std::vector<uint64_t> v;
+        for (auto& kv : unrefined_data_) v.push_back(kv.first);
+        if (sorted) std::sort(v.begin(), v.end());
+        return v;
+    }
+    void clear_refined_unrefined_data()
+    {
+        detail::check(dccrgx_clear_refined_unrefined_data(grid_), "clear_refined_unrefined_data");
+        refined_data_.clear();
+        unrefined_data_.clear();
+    }
+    int get_refinement_level(uint64_t cell) const { return mapping.get_refinement_level(cell); }
     bool is_local(uint64_t cell) const { return cell_data_.count(cell) > 0; }
 
     std::vector<uint64_t> get_cells() const  // local cells, ascending
@@ -540,6 +624,22 @@ private:
         return it->second;
     }
 
+    bool request(int (*fn)(dccrgx_grid*, uint64_t, int32_t*), uint64_t cell)
+    {
+        int32_t r = 0;
+        detail::check(fn(grid_, cell, &r), "refinement request");
+        return r != 0;
+    }
+
+    std::vector<uint64_t> id_list(int (*fn)(const dccrgx_grid*, uint64_t*, size_t, size_t*)) const
+    {
+        size_t n = 0;
+        detail::check(fn(grid_, nullptr, 0, &n), "cell list");
+        std::vector<uint64_t> v(n);
+        detail::check(fn(grid_, v.data(), n, &n), "cell list");
+        return v;
+    }
+
     std::vector<uint64_t> query_cells(int hood, int which) const
     {
         size_t n = 0;
@@ -685,7 +785,7 @@ private:
         if (!named) MPI_Type_free(&t);
     }
 
-    std::unordered_map<uint64_t, Cell_Data> cell_data_, remote_data_;
+    std::unordered_map<uint64_t, Cell_Data> cell_data_, remote_data_, refined_data_, unrefined_data_;
     std::map<int, HoodState> hoods_;
     dccrgx_ctx* ctx_ = nullptr;
     dccrgx_grid* grid_ = nullptr;

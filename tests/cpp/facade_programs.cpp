@@ -7,6 +7,9 @@
 //   halo             examples/basic_cell_data.cpp (Dccrg<int>, ghosts == ids)
 //   mapping          prints Mapping results for a list of ids
 //   lists            prints the iteration-cache neighbor lists of every cell
+//   amr CELL...      refines CELLs (6x5x4, max level 1, hood 1, periodic y z),
+//                    checks the data movement, prints new cells and the
+//                    rebuilt iteration-cache lists; then unrefines them back
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -160,6 +163,62 @@ static int lists(int argc, char** argv)
     return 0;
 }
 
+static void print_lists(dccrg::Dccrg<uint64_t>& grid)
+{
+    for (const auto& cell : grid.local_cells()) {
+        printf("cell %llu of", (unsigned long long)cell.id);
+        for (const auto& n : cell.neighbors_of) printf(" %llu:%d,%d,%d", (unsigned long long)n.id, n.x, n.y, n.z);
+        printf(" to");
+        for (const auto& n : cell.neighbors_to) printf(" %llu:%d,%d,%d", (unsigned long long)n.id, n.x, n.y, n.z);
+        printf("\n");
+    }
+}
+
+static int amr(int argc, char** argv)
+{
+    dccrg::Dccrg<uint64_t> grid;
+    grid.set_initial_length({6, 5, 4})
+        .set_neighborhood_length(1)
+        .set_maximum_refinement_level(1)
+        .set_periodic(false, true, true)
+        .initialize(MPI_COMM_WORLD);
+    for (const auto& cell : grid.local_cells()) *cell.data = cell.id;
+    std::vector<uint64_t> asked;
+    for (int i = 2; i < argc; i++) {
+        const uint64_t c = strtoull(argv[i], 0, 10);
+        if (!grid.refine_completely(c)) abort();
+        asked.push_back(c);
+    }
+    const auto created = grid.stop_refining(true);
+    printf("new");
+    for (uint64_t c : created) printf(" %llu", (unsigned long long)c);
+    printf("\n");
+    // refined parents keep their data until clear_refined_unrefined_data
+    for (uint64_t c : asked)
+        if (!grid[c] || *grid[c] != c) abort();
+    for (uint64_t c : created) {
+        if (!grid[c] || *grid[c] != 0) abort();  // value-initialised
+        *grid[c] = *grid[grid.mapping.get_parent(c)];
+    }
+    grid.clear_refined_unrefined_data();
+    for (uint64_t c : asked)
+        if (grid[c]) abort();
+    grid.update_copies_of_remote_neighbors();
+    print_lists(grid);
+    // unrefine back: the children's data stays readable, parents are new
+    for (uint64_t c : created) grid.unrefine_completely(c);
+    // execute_refines returns only the children of refined cells (dccrg.hpp:10374)
+    if (!grid.stop_refining(true).empty()) abort();
+    for (uint64_t c : asked)
+        if (!grid.is_local(c) || *grid[c] != 0) abort();  // parents are new, value-initialised
+    const auto removed = grid.get_removed_cells(true);
+    if (removed.size() != created.size()) abort();
+    for (uint64_t c : removed)
+        if (!grid[c] || *grid[c] != grid.mapping.get_parent(c)) abort();
+    printf("PASS amr\n");
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     if (MPI_Init(&argc, &argv) != MPI_SUCCESS) abort();
@@ -171,6 +230,7 @@ int main(int argc, char** argv)
         else if (mode == "halo") rc = halo();
         else if (mode == "mapping") rc = mapping();
         else if (mode == "lists") rc = lists(argc, argv);
+        else if (mode == "amr") rc = amr(argc, argv);
     }
     MPI_Finalize();
     return rc;

@@ -30,7 +30,9 @@ def test_facade_compiles(tmp_path):
 
 
 def run(*args):
-    if not os.path.exists(BIN):
+    srcs = [os.path.join(ROOT, "tests", "cpp", "facade_programs.cpp"), os.path.join(ROOT, "include", "dccrg_amd.hpp"),
+            os.path.join(ROOT, "include", "dccrgx.h")]
+    if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(f) for f in srcs):
         compile_facade()
     env = dict(os.environ)
     env["LD_LIBRARY_PATH"] = "/usr/lib/x86_64-linux-gnu:" + MPI_LIB
@@ -97,3 +99,41 @@ def test_facade_iteration_cache_order(dims, per, hood):
         lof, lto = O.iteration_cache_lists(og.find_neighbors_of(cid), og.find_neighbors_to(cid))
         assert parse(of_part) == lof
         assert parse(to_part) == lto
+
+
+@pytest.mark.gpu
+def test_facade_amr_matches_oracle():
+    """refine_completely / stop_refining / unrefine_completely through the
+    facade: new cells and the rebuilt iteration-cache lists equal the
+    oracle's, data moves as execute_refines moves it (checked in the
+    program), and unrefining restores the parents."""
+    from oracle.dccrg_amr import AmrOracle
+    asked = [33, 8]
+    o = AmrOracle((6, 5, 4), 1, (False, True, True), 1, 1)
+    for c in asked:
+        assert o.refine_completely(0, c)
+    want_new = sorted(o.stop_refining()[0])
+    out = run("amr", *asked)
+    assert "PASS amr" in out, out
+    lines = out.strip().splitlines()
+    assert [int(x) for x in lines[0].split()[1:]] == want_new
+    og = o.grid
+    n_cells = 0
+    for line in lines[1:]:
+        if not line.startswith("cell "):
+            continue
+        n_cells += 1
+        head, rest = line.split(" of", 1)
+        cid = int(head.split()[1])
+        of_part, to_part = rest.split(" to", 1)
+
+        def parse(s):
+            out = []
+            for tok in s.split():
+                i, off = tok.split(":")
+                out.append((int(i), tuple(int(x) for x in off.split(","))))
+            return out
+        lof, lto = O.iteration_cache_lists(og.find_neighbors_of(cid), og.find_neighbors_to(cid))
+        assert parse(of_part) == lof, cid
+        assert parse(to_part) == lto, cid
+    assert n_cells == len(o.cells())
