@@ -79,6 +79,7 @@ SIGNATURES = {
     "dccrgx_ctx_destroy": (C.c_int, [_vp]),
     "dccrgx_get_unique_id": (C.c_int, [C.c_char_p]),
     "dccrgx_ctx_comm_init": (C.c_int, [_vp, C.c_char_p]),
+    "dccrgx_ctx_route_self_through_rccl": (C.c_int, [_vp, C.c_int32]),
     "dccrgx_ctx_compute_stream": (C.c_int, [_vp, C.POINTER(_vp)]),
     "dccrgx_ctx_synchronize": (C.c_int, [_vp]),
     "dccrgx_max_possible_refinement_level": (C.c_int, [_u64p, _i32p]),

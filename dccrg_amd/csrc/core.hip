@@ -366,6 +366,13 @@ int dccrgx_get_unique_id(uint8_t uid_out[128])
     return DCCRGX_OK;
 }
 
+int dccrgx_ctx_route_self_through_rccl(dccrgx_ctx* c, int32_t on)
+{
+    DX_CHECK(c, DCCRGX_EINVAL, "null context");
+    c->self_peer = on != 0;
+    return DCCRGX_OK;
+}
+
 int dccrgx_ctx_comm_init(dccrgx_ctx* c, const uint8_t uid[128])
 {
     DX_CHECK(c && uid, DCCRGX_EINVAL, "null argument");

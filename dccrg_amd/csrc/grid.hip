@@ -515,6 +515,51 @@ int build_hood(dccrgx_grid* grid, Hood& h)
             DX_TRY(upload(src, &pp.d_unpack_src, st));
         }
     }
+    if (ctx->self_peer && ctx->has_comm && !self.empty()) {
+        // own periodic images as messages to this rank (test mode): one
+        // peer plan, cells ascending, read from their local slots
+        const uint64_t off = (uint64_t)(-g.cbase * (int64_t)g.S);
+        PeerPlan pp;
+        pp.peer = g.rank;
+        for (auto& e : self) pp.send_ids.push_back(e.second - off + 1);
+        std::sort(pp.send_ids.begin(), pp.send_ids.end());
+        pp.send_ids.erase(std::unique(pp.send_ids.begin(), pp.send_ids.end()), pp.send_ids.end());
+        pp.recv_ids = pp.send_ids;
+        std::vector<uint64_t> slots(pp.send_ids.size());
+        for (size_t i = 0; i < slots.size(); i++) slots[i] = pp.send_ids[i] - 1 + off;
+        pp.send_direct = true;
+        for (size_t i = 1; i < slots.size(); i++)
+            if (slots[i] != slots[0] + i) pp.send_direct = false;
+        pp.send_slot0 = slots[0];
+        if (!pp.send_direct) DX_TRY(upload(slots, &pp.d_send_slots, st));
+        std::vector<std::pair<uint64_t, uint64_t>> u;  // (message index, dst)
+        for (auto& e : self) {
+            const uint64_t id = e.second - off + 1;
+            u.push_back({(uint64_t)(std::lower_bound(pp.send_ids.begin(), pp.send_ids.end(), id) -
+                                    pp.send_ids.begin()),
+                         e.first});
+        }
+        std::stable_sort(u.begin(), u.end());
+        pp.recv_direct = u.size() == pp.recv_ids.size();
+        for (size_t i = 0; i < u.size() && pp.recv_direct; i++)
+            if (u[i].first != i || u[i].second != u[0].second + i) pp.recv_direct = false;
+        for (auto& e : u) {
+            pp.h_unpack_src.push_back(e.first);
+            pp.h_unpack_dst.push_back(e.second);
+        }
+        if (pp.recv_direct) {
+            pp.recv_slot0 = u[0].second;
+        } else {
+            pp.n_unpack = u.size();
+            DX_TRY(upload(pp.h_unpack_dst, &pp.d_unpack_dst, st));
+            DX_TRY(upload(pp.h_unpack_src, &pp.d_unpack_src, st));
+        }
+        pp.h_send_slots = std::move(slots);
+        auto at = std::lower_bound(h.peers.begin(), h.peers.end(), pp.peer,
+                                   [](const PeerPlan& a, int p) { return a.peer < p; });
+        h.peers.insert(at, std::move(pp));
+        self.clear();
+    }
     h.h_self = self;
     // self copies: contiguous runs become memcpys when there are few of them
     std::vector<CopySeg> segs;

@@ -202,6 +202,11 @@ struct Ctx {
     hipEvent_t ev_compute = nullptr, ev_comm = nullptr;
     ncclComm_t nccl = nullptr;
     bool has_comm = false;
+    // test mode (dccrgx_ctx_route_self_through_rccl): a rank's own periodic
+    // images travel as RCCL send/recv to itself instead of device copies, so
+    // the multi-rank halo path (pack, grouped send/recv, unpack, inner/outer
+    // overlap) runs on one GPU through the real communicator
+    bool self_peer = false;
 };
 
 }  // namespace dccrgx

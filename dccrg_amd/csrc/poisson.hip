@@ -569,11 +569,15 @@ int halo(dccrgx_poisson* P, std::initializer_list<int32_t> fields)
     return dccrgx_halo_wait(P->grid, DCCRGX_DEFAULT_NEIGHBORHOOD_ID, DCCRGX_WAIT_ALL);
 }
 
+// the cross-rank reductions run (several ranks, or the one-GPU test mode
+// that drives the multi-rank path through a 1-rank communicator)
+bool multi_rank(const Ctx* c) { return c->comm_size > 1 || (c->self_peer && c->has_comm); }
+
 // across ranks: SUM of S->red (MPI_Allreduce in the reference)
 int allreduce(dccrgx_poisson* P)
 {
     Ctx* c = P->grid->ctx;
-    if (c->comm_size == 1) return DCCRGX_OK;
+    if (!multi_rank(c)) return DCCRGX_OK;
     DX_CHECK(c->has_comm, DCCRGX_ESTATE, "Poisson solve on %d ranks needs the RCCL communicator", c->comm_size);
     double* red = &P->d_state->red;
     DX_RCCL(ncclAllReduce(red, red, 1, ncclFloat64, ncclSum, c->nccl, c->compute));
@@ -585,7 +589,7 @@ int reduce(dccrgx_poisson* P, int phase)
 {
     hipStream_t st = P->grid->ctx->compute;
     const dccrgx_poisson_params& q = P->prm;
-    const bool multi = P->grid->ctx->comm_size > 1;
+    const bool multi = multi_rank(P->grid->ctx);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(RB), 0, st, P->d_part, RG, P->d_state, multi ? (int)PH_NONE : phase,
                        q.p_of_norm, q.stop_residual, q.stop_after_residual_increase, q.min_iterations,
                        q.max_iterations);
@@ -870,7 +874,7 @@ int dccrgx_poisson_solve(dccrgx_poisson* P, const uint64_t* cells, size_t n, con
     const double pn = P->prm.p_of_norm;
     PState hs{};
     const Hood* dh = find_hood(P->grid, DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
-    const bool solo = P->grid->ctx->comm_size == 1 && dh && dh->h_self.empty() && P->n_info <= (1u << 16) &&
+    const bool solo = !multi_rank(P->grid->ctx) && dh && dh->h_self.empty() && P->n_info <= (1u << 16) &&
                       !getenv("DCCRGX_POISSON_MULTI");
     if (solo) {
         const dccrgx_poisson_params& q = P->prm;

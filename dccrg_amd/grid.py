@@ -47,6 +47,12 @@ class Context:
         assert len(uid) == 128
         check(lib().dccrgx_ctx_comm_init(self._h, uid))
 
+    def route_self_through_rccl(self, on: bool = True):
+        """Test mode: grids created afterwards send this rank's own periodic
+        images through RCCL send/recv to itself (needs comm_init), so the
+        multi-rank halo path runs on one GPU."""
+        check(lib().dccrgx_ctx_route_self_through_rccl(self._h, 1 if on else 0))
+
     def synchronize(self):
         check(lib().dccrgx_ctx_synchronize(self._h))
 

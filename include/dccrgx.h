@@ -69,6 +69,11 @@ int dccrgx_ctx_destroy(dccrgx_ctx* ctx);
 /* 128-byte ncclUniqueId; rank 0 creates it, the host bootstrap broadcasts it */
 int dccrgx_get_unique_id(uint8_t uid_out[128]);
 int dccrgx_ctx_comm_init(dccrgx_ctx* ctx, const uint8_t uid[128]);
+/* Test mode, no reference counterpart: grids created afterwards on this
+ * context send a rank's own periodic images through RCCL send/recv to itself
+ * (a peer plan with peer == rank) instead of device copies, so the whole
+ * multi-rank halo path runs on a single GPU.  Needs dccrgx_ctx_comm_init. */
+int dccrgx_ctx_route_self_through_rccl(dccrgx_ctx* ctx, int32_t on);
 int dccrgx_ctx_compute_stream(dccrgx_ctx* ctx, void** hip_stream_out);
 int dccrgx_ctx_synchronize(dccrgx_ctx* ctx);
 

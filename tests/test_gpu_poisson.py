@@ -3,6 +3,8 @@ the oracle's restatement: the cached geometric factors bit-exact (same
 operation order), BiCG iterates at fixed iteration counts within 1e-12 of
 max|x| (fp64; only the dot products' summation order differs), and full
 solves to the same converged solution."""
+import os
+
 import numpy as np
 import pytest
 
@@ -16,15 +18,27 @@ from test_oracle_poisson import L0, error_norm, poisson3d_leaves, solution_value
 TOL = 1e-12
 
 
-@pytest.fixture(params=["solo", "multi"])
+@pytest.fixture(params=["solo", "multi", "rccl"])
 def path(request, monkeypatch):
-    """Both iteration drivers: one workgroup for small single-rank systems,
-    and the batched multi-kernel path used across ranks."""
+    """Every iteration driver: one workgroup for small single-rank systems,
+    the batched multi-kernel path used across ranks, and that path through a
+    real RCCL communicator (ncclAllReduce of every scalar, periodic images
+    as RCCL messages to the rank itself)."""
+    monkeypatch.delenv("DCCRGX_POISSON_MULTI", raising=False)
+    monkeypatch.delenv("DCCRGX_TEST_RCCL", raising=False)
     if request.param == "multi":
         monkeypatch.setenv("DCCRGX_POISSON_MULTI", "1")
-    else:
-        monkeypatch.delenv("DCCRGX_POISSON_MULTI", raising=False)
+    elif request.param == "rccl":
+        monkeypatch.setenv("DCCRGX_TEST_RCCL", "1")
     return request.param
+
+
+def make_context():
+    c = D.Context(0, 0, 1)
+    if os.environ.get("DCCRGX_TEST_RCCL"):
+        c.comm_init(D.Context.unique_id())
+        c.route_self_through_rccl(True)
+    return c
 
 
 def geometry(length, M, cells, l0):
@@ -62,7 +76,7 @@ def build(name):
         rhs = np.sin(3 * ctr[:, 0]) * np.cos(ctr[:, 1]) + 0.1 * ctr[:, 2]
         guess = ctr[:, 0] * 0.3 - ctr[:, 1] * 0.1
     sysm = O.PoissonSystem(og, 1, (ln[:, 0], ln[:, 1], ln[:, 2]), solve_cells=solve, skip_cells=skip)
-    c = D.Context(0, 0, 1)
+    c = make_context()
     g = (D.Dccrg().set_initial_length(length).set_maximum_refinement_level(M).set_periodic(*per)
          .set_neighborhood_length(0).initialize(c, leaves=leaves))
     g._keep = c
