@@ -118,6 +118,42 @@ def secondary(ctx, torch, D):
     Poisson solve of configs[4] and the mapping kernel."""
     out = {}
     dev = torch.device("cuda", ctx.device)
+    # the N > 1 step structure on one GPU: the 2048^3 slab's periodic images
+    # travel as RCCL send/recv to the rank itself (pack, grouped send/recv,
+    # unpack) while the inner slices run, then the outer slices
+    rc = D.Context(ctx.device, 0, 1)
+    rc.comm_init(D.Context.unique_id())
+    rc.route_self_through_rccl(True)
+    n = 2048
+    g = (D.Dccrg().set_initial_length((n, n, n)).set_neighborhood_length(1)
+         .set_maximum_refinement_level(0).set_periodic(False, False, True).initialize(rc))
+    for f in ("a", "b", "c"):
+        g.add_field(f, np.uint32)
+    D.lib().dccrgx_field_init_hash(g._h, g.field_id("a"), 200)
+    cur, nxt = "a", "b"
+    for _ in range(2):
+        g.gol_step(cur, nxt, "c")
+        cur, nxt = nxt, cur
+    rc.synchronize()
+    steps = 10
+    g.kernel_timer(reset=1)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.gol_step(cur, nxt, "c")
+        cur, nxt = nxt, cur
+    rc.synchronize()
+    dt = time.perf_counter() - t0
+    kms, launches = g.kernel_timer(reset=0)
+    g.kernel_timer(reset=-1)
+    out["gol3d_rccl_halo"] = {
+        "workload": "headline grid with the multi-GPU step structure on one GPU: periodic-z images sent "
+                    "through RCCL to the rank itself (2 x 16 MiB per step), inner slices overlapped, "
+                    "then outer slices",
+        "value": n ** 3 * steps / dt, "unit": "cell-updates/s", "steps": steps,
+        "ms_per_step": dt * 1e3 / steps, "kernel_ms_per_step": kms / steps,
+        "launches_per_step": launches / steps}
+    g.close()
+    rc.close()
     # configs[1]: 16384^2, hood 1, periodic x y (scalability.cpp:85)
     n = 16384
     g = (D.Dccrg().set_initial_length((n, n, 1)).set_neighborhood_length(1)
