@@ -48,6 +48,11 @@ class GridInfo_t(C.Structure):
                 ("rank", C.c_int32), ("comm_size", C.c_int32)]
 
 
+class FileInfo_t(C.Structure):
+    _fields_ = [("params", GridParams_t), ("geometry_bytes", C.c_uint64), ("total_cells", C.c_uint64),
+                ("list_offset", C.c_uint64)]
+
+
 class AdvectFields_t(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("density", "flux", "vx", "vy", "vz",
                                          "length_x", "length_y", "length_z")]
@@ -153,6 +158,15 @@ SIGNATURES = {
     "dccrgx_clear_refined_unrefined_data": (C.c_int, [_vp]),
     "dccrgx_poisson_solve": (C.c_int, [_vp, _u64p, C.c_size_t, _u64p, C.c_size_t, C.c_int32,
                                        C.POINTER(C.c_uint32), C.POINTER(C.c_double)]),
+    "dccrgx_file_preamble_bytes": (C.c_uint64, [C.c_size_t]),
+    "dccrgx_save_sizes": (C.c_int, [_vp, _i32p, C.c_size_t, _u64p, _u64p]),
+    "dccrgx_save_grid_data": (C.c_int, [_vp, C.c_char_p, C.c_uint64, _vp, C.c_size_t, _vp, C.c_size_t, C.c_uint64,
+                                        C.c_uint64, C.c_uint64, _i32p, C.c_size_t]),
+    "dccrgx_file_read_info": (C.c_int, [C.c_char_p, C.c_uint64, _vp, C.c_size_t, C.POINTER(FileInfo_t), _vp,
+                                        C.c_size_t]),
+    "dccrgx_grid_load": (C.c_int, [_vp, C.c_char_p, C.POINTER(FileInfo_t), C.POINTER(_vp)]),
+    "dccrgx_load_cell_data": (C.c_int, [_vp, _i32p, C.c_size_t]),
+    "dccrgx_finish_loading_grid_data": (C.c_int, [_vp]),
 }
 
 _lib = None

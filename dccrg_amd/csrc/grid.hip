@@ -696,6 +696,7 @@ int dccrgx_grid_destroy(dccrgx_grid* grid)
     for (Field& f : grid->fields) hipFree(f.ptr);
     if (!grid->uniform) explicit_destroy(grid);
     amr_destroy(grid);
+    load_state_free(grid);
     hipEventDestroy(grid->t0);
     hipEventDestroy(grid->t1);
     delete grid;

@@ -160,6 +160,8 @@ struct Explicit {
 
 // pending refinement requests of this rank and the results of the last
 // stop_refining (dccrg.hpp:7355-7360, 3483-3543)
+struct LoadState;
+
 struct Amr {
     std::set<uint64_t> to_refine, not_to_refine, to_unrefine, not_to_unrefine;
     std::vector<uint64_t> new_cells, removed;
@@ -241,6 +243,8 @@ struct dccrgx_grid {
     dccrgx::Explicit* ex = nullptr;
     // refinement requests and results (amr.hip)
     dccrgx::Amr* amr = nullptr;
+    // grid data file being loaded (checkpoint.hip)
+    dccrgx::LoadState* load = nullptr;
     // kernel timing (dccrgx_kernel_timer)
     hipEvent_t t0 = nullptr, t1 = nullptr;
     double timed_ms = 0;
@@ -284,6 +288,7 @@ int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id);
 // the slot read and written for a cell on this rank (-1: none), halo.hip
 int64_t host_primary_slot(const dccrgx_grid* grid, uint64_t id);
 void amr_destroy(dccrgx_grid* grid);
+void load_state_free(dccrgx_grid* grid);
 // switch a uniform grid to the explicit layout (amr.hip)
 int amr_ensure_explicit(dccrgx_grid* grid);
 int launch_gather_ext(const void* src, const uint64_t* idx, uint64_t n, uint32_t elem, void* dst,

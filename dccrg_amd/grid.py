@@ -14,6 +14,7 @@ Everything here calls libdccrgx.so; no computation happens in Python.
 from __future__ import annotations
 
 import ctypes as C
+import struct
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -26,6 +27,16 @@ DEFAULT_NEIGHBORHOOD_ID = X.DEFAULT_NEIGHBORHOOD_ID
 
 def _u64(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+def no_geometry() -> bytes:
+    """No_Geometry's file data (dccrg_no_geometry.hpp:486-549): its id."""
+    return struct.pack("<i", 0)
+
+
+def cartesian_geometry(start, level_0_cell_length) -> bytes:
+    """Cartesian_Geometry's file data (dccrg_cartesian_geometry.hpp:620-812)."""
+    return struct.pack("<i3d3d", 1, *[float(v) for v in start], *[float(v) for v in level_0_cell_length])
 
 
 class Context:
@@ -575,6 +586,84 @@ class Dccrg:
         if names is None:
             names = list(self._fields)
         return np.array([self._fields[n][0] for n in names], dtype=np.int32)
+
+    # ---- grid data files (dccrg.hpp:1109-2427) -------------------------------
+    def save_sizes(self, fields) -> Tuple[int, int]:
+        """This rank's (cells, data bytes) for a save of `fields`."""
+        f = self._fids(fields)
+        n, b = C.c_uint64(), C.c_uint64()
+        check(lib().dccrgx_save_sizes(self._h, f.ctypes.data_as(X._i32p), f.size, C.byref(n), C.byref(b)))
+        return n.value, b.value
+
+    def save_grid_data(self, name: str, offset: int = 0, header: bytes = b"", fields=None,
+                       geometry: Optional[bytes] = None, all_sizes=None) -> bool:
+        """Dccrg::save_grid_data (dccrg.hpp:1109-1712).  A cell's data is
+        `fields` in order (the members its get_mpi_datatype() would list).
+        geometry: the stored geometry blob (no_geometry() by default).
+        all_sizes: every rank's save_sizes() in rank order; all-gathered with
+        torch.distributed when the grid has several ranks and it is not given."""
+        f = self._fids(fields)
+        geometry = no_geometry() if geometry is None else bytes(geometry)
+        mine = self.save_sizes(fields)
+        if all_sizes is None:
+            if self.ctx.comm_size == 1:
+                all_sizes = [mine]
+            else:
+                import torch.distributed as dist
+                all_sizes = [None] * self.ctx.comm_size
+                dist.all_gather_object(all_sizes, mine)
+        r = self.ctx.rank
+        assert tuple(all_sizes[r]) == tuple(mine), "all_sizes does not match this rank's share"
+        total = sum(int(n) for n, _ in all_sizes)
+        cb = sum(int(n) for n, _ in all_sizes[:r])
+        bb = sum(int(b) for _, b in all_sizes[:r])
+        hb = bytes(header)
+        check(lib().dccrgx_save_grid_data(self._h, name.encode(), offset, hb, len(hb), geometry, len(geometry),
+                                          total, cb, bb, f.ctypes.data_as(X._i32p), f.size))
+        return True
+
+    @staticmethod
+    def read_file_info(name: str, offset: int = 0, header_bytes: int = 0):
+        """(file info, header bytes, geometry blob) of a grid data file."""
+        info = X.FileInfo_t()
+        hdr = C.create_string_buffer(max(header_bytes, 1))
+        check(lib().dccrgx_file_read_info(name.encode(), offset, hdr, header_bytes, C.byref(info), None, 0))
+        geo = C.create_string_buffer(int(info.geometry_bytes))
+        check(lib().dccrgx_file_read_info(name.encode(), offset, hdr, header_bytes, C.byref(info), geo,
+                                          info.geometry_bytes))
+        return info, hdr.raw[:header_bytes], geo.raw
+
+    @classmethod
+    def start_loading_grid_data(cls, ctx: "Context", name: str, offset: int = 0, header_bytes: int = 0):
+        """Dccrg::start_loading_grid_data (dccrg.hpp:1815-2105): a grid of the
+        file's cells on `ctx`.  Returns (grid, header bytes, geometry blob);
+        add fields, then continue_loading_grid_data(fields), then
+        finish_loading_grid_data()."""
+        info, hdr, geo = cls.read_file_info(name, offset, header_bytes)
+        g = cls()
+        p = info.params
+        g._length = tuple(int(v) for v in p.length)
+        g._max_ref_lvl = int(p.max_ref_lvl)
+        g._periodic = tuple(bool(v) for v in p.periodic)
+        g._hood_length = int(p.neighborhood_length)
+        g.ctx = ctx
+        h = C.c_void_p()
+        check(lib().dccrgx_grid_load(ctx._h, name.encode(), C.byref(info), C.byref(h)))
+        g._h = h
+        g._refresh_info()
+        g.mapping = Mapping(g._length, g.info.max_ref_lvl)
+        return g, hdr, geo
+
+    def continue_loading_grid_data(self, fields):
+        """dccrg.hpp:2134-2390: the next bytes of every local cell's record
+        into `fields` (variable fields sized beforehand)."""
+        f = self._fids(fields)
+        check(lib().dccrgx_load_cell_data(self._h, f.ctypes.data_as(X._i32p), f.size))
+        return True
+
+    def finish_loading_grid_data(self):
+        check(lib().dccrgx_finish_loading_grid_data(self._h))
+        return True
 
     # ---- halo (dccrg.hpp:978-1014, 5046-5413) --------------------------------
     def update_copies_of_remote_neighbors(self, hood: int = DEFAULT_NEIGHBORHOOD_ID, fields=None):

@@ -341,8 +341,8 @@ int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_f
 /* ------------------------------------------------------------------------ *
  * Adaptive mesh refinement (dccrg.hpp:2456-2806, 3483-3543, 5550-5567,
  * 9730-10693).  Request calls set *result to the reference's bool.  A
- * uniform grid switches to the explicit (mixed-level) layout on its first
- * refine request.  stop_refining is collective: every rank passes the union
+ * uniform grid switches to the explicit (mixed-level) layout inside the first
+ * stop_refining that changes the grid (on every rank together).  stop_refining is collective: every rank passes the union
  * over all ranks of the four request sets (dccrgx_amr_requests on each rank,
  * all-gathered by the caller); the library then evaluates override_refines,
  * induce_refines and override_unrefines on the replicated leaf set and
@@ -413,6 +413,58 @@ int dccrgx_poisson_field(const dccrgx_poisson* solver, int32_t which, int32_t* f
 int dccrgx_poisson_solve(dccrgx_poisson* solver, const uint64_t* cells, size_t n_cells,
                          const uint64_t* cells_to_skip, size_t n_skip, int32_t cache_is_up_to_date,
                          uint32_t* iterations, double* residual_min);
+
+/* ------------------------------------------------------------------------ *
+ * Grid data files: save_grid_data / load_grid_data (dccrg.hpp:1109-2427),
+ * byte-compatible with the reference's layout:
+ *   [offset bytes][user header][u64 0x1234567890abcdef][u64 length[3]]
+ *   [i32 max_ref_lvl][u32 neighborhood_length][u8 periodic[3]][geometry]
+ *   [u64 total cells][(u64 id, u64 absolute offset of its data) x total]
+ *   [cell data]
+ * rank by rank, each rank's cells in its local order (ascending ids).  A
+ * cell's data is the bytes of the given fields in order, no padding -- the
+ * packed form of the struct datatype its get_mpi_datatype() would return.
+ * Geometry blobs: i32 id (0 No_Geometry; 1 Cartesian + f64 start[3] + f64
+ * level_0_cell_length[3]; 2 Stretched + u64 n[3] + coordinates).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+    dccrgx_grid_params params;  /* mapping, neighborhood length, topology */
+    uint64_t geometry_bytes;    /* Geometry::data_size() of the stored geometry */
+    uint64_t total_cells;
+    uint64_t list_offset;       /* absolute offset of the (id, offset) list */
+} dccrgx_file_info;
+/* bytes between the user header and the cell list */
+uint64_t dccrgx_file_preamble_bytes(size_t geometry_bytes);
+/* this rank's share of a save: local cells and their data bytes */
+int dccrgx_save_sizes(const dccrgx_grid* grid, const int32_t* fields, size_t nf, uint64_t* n_cells,
+                      uint64_t* n_bytes);
+/* Dccrg::save_grid_data, dccrg.hpp:1109-1712.  Every rank calls it with the
+ * same header / geometry / total_cells and its own exclusive prefix sums of
+ * dccrgx_save_sizes over lower ranks (cells_before, bytes_before; the
+ * caller's all-gather replaces the reference's MPI_Allgather :1490-1530).
+ * Rank 0 writes header and preamble; every rank writes its list entries and
+ * its cell data (one contiguous range).  The file is not truncated
+ * (MPI_MODE_CREATE | MPI_MODE_WRONLY). */
+int dccrgx_save_grid_data(const dccrgx_grid* grid, const char* path, uint64_t offset, const void* header,
+                          size_t header_bytes, const void* geometry, size_t geometry_bytes, uint64_t total_cells,
+                          uint64_t cells_before, uint64_t bytes_before, const int32_t* fields, size_t nf);
+/* start_loading_grid_data, first half (dccrg.hpp:1815-2000): header bytes,
+ * endianness check, mapping, neighborhood length, topology, geometry (copied
+ * out if `geometry` is given) and the cell count */
+int dccrgx_file_read_info(const char* path, uint64_t offset, void* header, size_t header_bytes,
+                          dccrgx_file_info* info, void* geometry, size_t geometry_cap);
+/* start_loading_grid_data, second half (:2002-2105): the grid of the file's
+ * cells on this context (each rank gets the cells whose level-0 ancestor it
+ * owns, cell_overlaps_local :3603-3622); a file of every level-0 cell gives
+ * a uniform grid.  Fields are created afterwards, then loaded: */
+int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* info, dccrgx_grid** out);
+/* continue_loading_grid_data, :2134-2390: reads the next bytes of every
+ * local cell's record into the given fields (variable-size fields take
+ * count * elem bytes: size them first, e.g. from a count read by an earlier
+ * call) and advances each cell's file offset past them */
+int dccrgx_load_cell_data(dccrgx_grid* grid, const int32_t* fields, size_t nf);
+/* finish_loading_grid_data, :2402-2426 */
+int dccrgx_finish_loading_grid_data(dccrgx_grid* grid);
 
 #ifdef __cplusplus
 }
