@@ -167,6 +167,9 @@ SIGNATURES = {
     "dccrgx_grid_load": (C.c_int, [_vp, C.c_char_p, C.POINTER(FileInfo_t), C.POINTER(_vp)]),
     "dccrgx_load_cell_data": (C.c_int, [_vp, _i32p, C.c_size_t]),
     "dccrgx_finish_loading_grid_data": (C.c_int, [_vp]),
+    "dccrgx_save_grid_data_host": (C.c_int, [_vp, C.c_char_p, C.c_uint64, _vp, C.c_size_t, _vp, C.c_size_t,
+                                             C.c_uint64, C.c_uint64, C.c_uint64, _u64p, _vp, C.c_size_t]),
+    "dccrgx_load_cell_records_host": (C.c_int, [_vp, _u64p, _vp, C.c_size_t]),
 }
 
 _lib = None

@@ -17,6 +17,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <cstring>
 
 #include "grid.hpp"
@@ -296,20 +297,20 @@ int dccrgx_save_sizes(const dccrgx_grid* grid, const int32_t* fields, size_t nf,
     return DCCRGX_OK;
 }
 
-int dccrgx_save_grid_data(const dccrgx_grid* grid, const char* path, uint64_t offset, const void* header,
-                          size_t header_bytes, const void* geometry, size_t geometry_bytes, uint64_t total_cells,
-                          uint64_t cells_before, uint64_t bytes_before, const int32_t* fields, size_t nf)
+}  // extern "C"
+
+namespace dccrgx {
+namespace {
+
+// save_grid_data's header, preamble (rank 0) and this rank's cell list;
+// rec(i) = record bytes of local cell i.  Returns the file offset of the
+// rank's first record.
+template <class Rec>
+int write_head_and_list(const dccrgx_grid* grid, int fd, uint64_t offset, const void* header, size_t header_bytes,
+                        const void* geometry, size_t geometry_bytes, uint64_t total_cells, uint64_t cells_before,
+                        uint64_t bytes_before, Rec rec, uint64_t* data_start_out)
 {
-    DX_CHECK(grid && path && (header || !header_bytes) && geometry && geometry_bytes >= 4, DCCRGX_EINVAL,
-             "null argument");
-    FDesc d;
-    bool var = false;
-    DX_TRY(fdesc(grid, fields, nf, &d, &var));
     DX_CHECK(cells_before + grid->n_local <= total_cells, DCCRGX_EINVAL, "cell counts inconsistent");
-    Fd fd;
-    // MPI_MODE_CREATE | MPI_MODE_WRONLY: no truncation (:1146-1152)
-    fd.fd = open(path, O_WRONLY | O_CREAT, 0644);
-    DX_CHECK(fd.fd >= 0, DCCRGX_EINVAL, "couldn't open file %s", path);
     const uint64_t pre = offset + header_bytes + dccrgx_file_preamble_bytes(geometry_bytes);
     if (grid->ctx->rank == 0) {
         // rank 0: header, endianness check, mapping, neighborhood length,
@@ -332,28 +333,53 @@ int dccrgx_save_grid_data(const dccrgx_grid* grid, const char* path, uint64_t of
         std::memcpy(p, geometry, geometry_bytes);
         p += geometry_bytes;
         std::memcpy(p, &total_cells, 8);
-        DX_TRY(pwrite_all(fd.fd, b.data(), b.size(), offset));
+        DX_TRY(pwrite_all(fd, b.data(), b.size(), offset));
     }
     const uint64_t n = grid->n_local;
     const uint64_t list_start = pre + 16 * cells_before;
     const uint64_t data_start = pre + 16 * total_cells + bytes_before;
-    const uint64_t s0 = local_s0(grid);
     // cell list: (id, absolute offset of its data) (:1540-1575)
-    {
-        const uint64_t chunk = 1ull << 20;
-        std::vector<uint64_t> pairs;
-        uint64_t at = data_start;
-        for (uint64_t i0 = 0; i0 < n; i0 += chunk) {
-            const uint64_t i1 = std::min(n, i0 + chunk);
-            pairs.resize(2 * (i1 - i0));
-            for (uint64_t i = i0; i < i1; i++) {
-                pairs[2 * (i - i0)] = local_id(grid, i);
-                pairs[2 * (i - i0) + 1] = at;
-                at += var ? record_bytes(grid, fields, nf, s0, i) : d.rec;
-            }
-            DX_TRY(pwrite_all(fd.fd, pairs.data(), pairs.size() * 8, list_start + 16 * i0));
+    const uint64_t chunk = 1ull << 20;
+    std::vector<uint64_t> pairs;
+    uint64_t at = data_start;
+    for (uint64_t i0 = 0; i0 < n; i0 += chunk) {
+        const uint64_t i1 = std::min(n, i0 + chunk);
+        pairs.resize(2 * (i1 - i0));
+        for (uint64_t i = i0; i < i1; i++) {
+            pairs[2 * (i - i0)] = local_id(grid, i);
+            pairs[2 * (i - i0) + 1] = at;
+            at += rec(i);
         }
+        DX_TRY(pwrite_all(fd, pairs.data(), pairs.size() * 8, list_start + 16 * i0));
     }
+    *data_start_out = data_start;
+    return DCCRGX_OK;
+}
+
+}  // namespace
+}  // namespace dccrgx
+
+extern "C" {
+
+int dccrgx_save_grid_data(const dccrgx_grid* grid, const char* path, uint64_t offset, const void* header,
+                          size_t header_bytes, const void* geometry, size_t geometry_bytes, uint64_t total_cells,
+                          uint64_t cells_before, uint64_t bytes_before, const int32_t* fields, size_t nf)
+{
+    DX_CHECK(grid && path && (header || !header_bytes) && geometry && geometry_bytes >= 4, DCCRGX_EINVAL,
+             "null argument");
+    FDesc d;
+    bool var = false;
+    DX_TRY(fdesc(grid, fields, nf, &d, &var));
+    Fd fd;
+    // MPI_MODE_CREATE | MPI_MODE_WRONLY: no truncation (:1146-1152)
+    fd.fd = open(path, O_WRONLY | O_CREAT, 0644);
+    DX_CHECK(fd.fd >= 0, DCCRGX_EINVAL, "couldn't open file %s", path);
+    const uint64_t n = grid->n_local;
+    const uint64_t s0 = local_s0(grid);
+    uint64_t data_start = 0;
+    DX_TRY(write_head_and_list(
+        grid, fd.fd, offset, header, header_bytes, geometry, geometry_bytes, total_cells, cells_before, bytes_before,
+        [&](uint64_t i) { return var ? record_bytes(grid, fields, nf, s0, i) : (uint64_t)d.rec; }, &data_start));
     // cell data: records packed on the device, chunk by chunk
     hipStream_t st = grid->ctx->compute;
     Staging S;
@@ -617,6 +643,65 @@ int dccrgx_finish_loading_grid_data(dccrgx_grid* grid)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     load_state_free(grid);
+    return DCCRGX_OK;
+}
+
+int dccrgx_save_grid_data_host(const dccrgx_grid* grid, const char* path, uint64_t offset, const void* header,
+                               size_t header_bytes, const void* geometry, size_t geometry_bytes, uint64_t total_cells,
+                               uint64_t cells_before, uint64_t bytes_before, const uint64_t* record_bytes,
+                               const void* records, size_t bytes)
+{
+    DX_CHECK(grid && path && (header || !header_bytes) && geometry && geometry_bytes >= 4 &&
+                 (record_bytes || !grid->n_local) && (records || !bytes),
+             DCCRGX_EINVAL, "null argument");
+    uint64_t tot = 0;
+    for (uint64_t i = 0; i < grid->n_local; i++) tot += record_bytes[i];
+    DX_CHECK(tot == bytes, DCCRGX_EINVAL, "records hold %zu bytes, their sizes add up to %llu", bytes,
+             (unsigned long long)tot);
+    Fd fd;
+    fd.fd = open(path, O_WRONLY | O_CREAT, 0644);
+    DX_CHECK(fd.fd >= 0, DCCRGX_EINVAL, "couldn't open file %s", path);
+    uint64_t data_start = 0;
+    DX_TRY(write_head_and_list(grid, fd.fd, offset, header, header_bytes, geometry, geometry_bytes, total_cells,
+                               cells_before, bytes_before, [&](uint64_t i) { return record_bytes[i]; }, &data_start));
+    if (bytes) DX_TRY(pwrite_all(fd.fd, records, bytes, data_start));
+    return DCCRGX_OK;
+}
+
+int dccrgx_load_cell_records_host(dccrgx_grid* grid, const uint64_t* record_bytes, void* out, size_t bytes)
+{
+    DX_CHECK(grid && (record_bytes || !grid->n_local) && (out || !bytes), DCCRGX_EINVAL, "null argument");
+    DX_CHECK(grid->load, DCCRGX_ESTATE, "the grid was not loaded from a file (or loading finished)");
+    LoadState& L = *grid->load;
+    const uint64_t n = grid->n_local;
+    uint64_t tot = 0;
+    for (uint64_t i = 0; i < n; i++) tot += record_bytes[i];
+    DX_CHECK(tot == bytes, DCCRGX_EINVAL, "buffer holds %zu bytes, the records %llu", bytes, (unsigned long long)tot);
+    Fd fd;
+    fd.fd = open(L.path.c_str(), O_RDONLY);
+    DX_CHECK(fd.fd >= 0, DCCRGX_ENOTFOUND, "couldn't open file %s", L.path.c_str());
+    if (L.affine) {
+        const uint64_t d0 = L.disp[0];
+        L.disp.resize(n);
+        for (uint64_t i = 0; i < n; i++) L.disp[i] = d0 + i * L.stride;
+        L.affine = false;
+    }
+    std::vector<std::array<uint64_t, 3>> cells;  // (file offset, buffer offset, length), merged where contiguous
+    uint64_t at = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (record_bytes[i]) cells.push_back({L.disp[i], at, record_bytes[i]});
+        at += record_bytes[i];
+        L.disp[i] += record_bytes[i];
+    }
+    std::sort(cells.begin(), cells.end());
+    std::vector<std::array<uint64_t, 3>> runs;
+    for (auto& c : cells) {
+        if (!runs.empty() && runs.back()[0] + runs.back()[2] == c[0] && runs.back()[1] + runs.back()[2] == c[1])
+            runs.back()[2] += c[2];
+        else
+            runs.push_back(c);
+    }
+    for (auto& r : runs) DX_TRY(pread_all(fd.fd, (char*)out + r[1], r[2], r[0]));
     return DCCRGX_OK;
 }
 

@@ -39,6 +39,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdint>
+#include <cstdio>
 #include <map>
 #include <set>
 #include <stdexcept>
@@ -332,6 +333,125 @@ public:
     Dccrg& initialize(const MPI_Comm& comm, uint64_t = 1)
     {
         if (initialized_) throw std::invalid_argument("already initialized");
+        init_comm(comm);
+        dccrgx_grid_params p{};
+        for (int d = 0; d < 3; d++) {
+            p.length[d] = mapping.length.get()[d];
+            p.periodic[d] = topology.is_periodic(d) ? 1 : 0;
+        }
+        p.max_ref_lvl = mapping.get_maximum_refinement_level();
+        p.neighborhood_length = hood_length_;
+        detail::check(dccrgx_grid_create(ctx_, &p, nullptr, 0, &grid_), "grid");
+        for (uint64_t c : query_cells(default_neighborhood_id, DCCRGX_CELLS_LOCAL)) cell_data_[c];
+        initialized_ = true;
+        build_hood(default_neighborhood_id);
+        return *this;
+    }
+
+    // ---- grid data files (dccrg.hpp:1109-2427) -------------------------------
+    // save_grid_data: the header's packed bytes (rank 0), then the layout of
+    // include/dccrgx.h; every cell's record is the packed form of its
+    // get_mpi_datatype(id, rank, -1, false, -1) (:1324-1340).  Collective.
+    bool save_grid_data(const std::string& name, MPI_Offset offset, std::tuple<void*, int, MPI_Datatype> header)
+    {
+        const std::vector<char> hb = pack_header(header);
+        const std::vector<uint64_t> ids = get_cells();
+        std::vector<uint64_t> sizes;
+        std::vector<char> recs;
+        for (uint64_t c : ids) {
+            const size_t before = recs.size();
+            pack(c, cell_data_.at(c), rank_, -1, false, -1, recs);
+            sizes.push_back(recs.size() - before);
+        }
+        uint64_t mine[2] = {ids.size(), recs.size()};
+        std::vector<uint64_t> all(2 * size_);
+        MPI_Allgather(mine, 2, MPI_UINT64_T, all.data(), 2, MPI_UINT64_T, comm_);
+        uint64_t total = 0, cells_before = 0, bytes_before = 0;
+        for (int r = 0; r < size_; r++) {
+            total += all[2 * r];
+            if (r < rank_) {
+                cells_before += all[2 * r];
+                bytes_before += all[2 * r + 1];
+            }
+        }
+        const int32_t geometry_id = 0;  // No_Geometry::geometry_id, dccrg_no_geometry.hpp:55
+        const int s = dccrgx_save_grid_data_host(grid_, name.c_str(), (uint64_t)offset, hb.data(), hb.size(),
+                                                 &geometry_id, 4, total, cells_before, bytes_before, sizes.data(),
+                                                 recs.data(), recs.size());
+        int ok = s == DCCRGX_OK, all_ok = 0;
+        if (!ok) std::fprintf(stderr, "save_grid_data: %s\n", dccrgx_last_error());
+        MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_MIN, comm_);
+        return all_ok != 0;
+    }
+    bool load_grid_data(const std::string& name, MPI_Offset offset, std::tuple<void*, int, MPI_Datatype> header,
+                        const MPI_Comm& comm, const char* load_balancing_method, uint64_t sfc_caching_batches = 1,
+                        uint64_t number_of_cells = ~uint64_t(0))
+    {
+        return start_loading_grid_data(name, offset, header, comm, load_balancing_method, sfc_caching_batches,
+                                       number_of_cells) &&
+               continue_loading_grid_data() && finish_loading_grid_data();
+    }
+    // dccrg.hpp:1815-2105: creates the grid of the file's cells (instead of initialize())
+    bool start_loading_grid_data(const std::string& name, MPI_Offset offset,
+                                 std::tuple<void*, int, MPI_Datatype> header, const MPI_Comm& comm, const char*,
+                                 uint64_t = 1, uint64_t = ~uint64_t(0))
+    {
+        if (initialized_) throw std::invalid_argument("already initialized");
+        init_comm(comm);
+        std::vector<char> hb(pack_header(header).size());
+        dccrgx_file_info info{};
+        if (dccrgx_file_read_info(name.c_str(), (uint64_t)offset, hb.data(), hb.size(), &info, nullptr, 0) !=
+            DCCRGX_OK) {
+            std::fprintf(stderr, "start_loading_grid_data: %s\n", dccrgx_last_error());
+            return false;
+        }
+        int pos = 0;
+        MPI_Datatype t = std::get<2>(header);
+        const bool named = detail::is_named(t);
+        if (!named) MPI_Type_commit(&t);
+        if (!hb.empty()) MPI_Unpack(hb.data(), (int)hb.size(), &pos, std::get<0>(header), std::get<1>(header), t, comm_);
+        if (!named) MPI_Type_free(&t);
+        mapping.set_length({{info.params.length[0], info.params.length[1], info.params.length[2]}});
+        mapping.set_maximum_refinement_level(info.params.max_ref_lvl);
+        for (int d = 0; d < 3; d++) topology.set_periodicity(d, info.params.periodic[d] != 0);
+        hood_length_ = info.params.neighborhood_length;
+        if (dccrgx_grid_load(ctx_, name.c_str(), &info, &grid_) != DCCRGX_OK) {
+            std::fprintf(stderr, "start_loading_grid_data: %s\n", dccrgx_last_error());
+            return false;
+        }
+        for (uint64_t c : query_cells(default_neighborhood_id, DCCRGX_CELLS_LOCAL)) cell_data_[c];
+        initialized_ = true;
+        build_hood(default_neighborhood_id);
+        return true;
+    }
+    // dccrg.hpp:2134-2390: each local cell's next bytes, as its
+    // get_mpi_datatype(id, -1, rank, true, -1) describes them
+    bool continue_loading_grid_data()
+    {
+        const std::vector<uint64_t> ids = get_cells();
+        std::vector<uint64_t> sizes;
+        uint64_t tot = 0;
+        for (uint64_t c : ids) {
+            sizes.push_back((uint64_t)pack_size(c, cell_data_.at(c), -1, rank_, true, -1));
+            tot += sizes.back();
+        }
+        std::vector<char> buf(tot);
+        if (dccrgx_load_cell_records_host(grid_, sizes.data(), buf.data(), buf.size()) != DCCRGX_OK) {
+            std::fprintf(stderr, "continue_loading_grid_data: %s\n", dccrgx_last_error());
+            return false;
+        }
+        int pos = 0;
+        for (uint64_t c : ids) unpack(c, cell_data_.at(c), -1, rank_, -1, buf, pos);
+        return true;
+    }
+    bool finish_loading_grid_data()  // dccrg.hpp:2402-2426
+    {
+        return dccrgx_finish_loading_grid_data(grid_) == DCCRGX_OK;
+    }
+
+private:
+    void init_comm(const MPI_Comm& comm)
+    {
         MPI_Comm_dup(comm, &comm_);
         MPI_Comm_rank(comm_, &rank_);
         MPI_Comm_size(comm_, &size_);
@@ -349,20 +469,23 @@ public:
             MPI_Bcast(uid, 128, MPI_BYTE, 0, comm_);
             detail::check(dccrgx_ctx_comm_init(ctx_, uid), "RCCL communicator");
         }
-        dccrgx_grid_params p{};
-        for (int d = 0; d < 3; d++) {
-            p.length[d] = mapping.length.get()[d];
-            p.periodic[d] = topology.is_periodic(d) ? 1 : 0;
-        }
-        p.max_ref_lvl = mapping.get_maximum_refinement_level();
-        p.neighborhood_length = hood_length_;
-        detail::check(dccrgx_grid_create(ctx_, &p, nullptr, 0, &grid_), "grid");
-        for (uint64_t c : query_cells(default_neighborhood_id, DCCRGX_CELLS_LOCAL)) cell_data_[c];
-        initialized_ = true;
-        build_hood(default_neighborhood_id);
-        return *this;
+    }
+    std::vector<char> pack_header(std::tuple<void*, int, MPI_Datatype> header) const
+    {
+        MPI_Datatype t = std::get<2>(header);
+        const bool named = detail::is_named(t);
+        if (!named) MPI_Type_commit(&t);
+        int sz = 0;
+        MPI_Pack_size(std::get<1>(header), t, comm_, &sz);
+        std::vector<char> b(sz);
+        int pos = 0;
+        if (sz) MPI_Pack(std::get<0>(header), std::get<1>(header), t, b.data(), sz, &pos, comm_);
+        b.resize(pos);
+        if (!named) MPI_Type_free(&t);
+        return b;
     }
 
+public:
     // ---- queries ------------------------------------------------------------
     int get_rank() const { return rank_; }
     int get_comm_size() const { return size_; }

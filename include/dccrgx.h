@@ -465,6 +465,14 @@ int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* 
 int dccrgx_load_cell_data(dccrgx_grid* grid, const int32_t* fields, size_t nf);
 /* finish_loading_grid_data, :2402-2426 */
 int dccrgx_finish_loading_grid_data(dccrgx_grid* grid);
+/* Host-side cell data (the C++ facade keeps Cell_Data on the host): the
+ * same save with the local cells' packed records (ascending ids, sizes per
+ * cell) given by the caller, and the same continue-load into a host buffer. */
+int dccrgx_save_grid_data_host(const dccrgx_grid* grid, const char* path, uint64_t offset, const void* header,
+                               size_t header_bytes, const void* geometry, size_t geometry_bytes, uint64_t total_cells,
+                               uint64_t cells_before, uint64_t bytes_before, const uint64_t* record_bytes,
+                               const void* records, size_t bytes);
+int dccrgx_load_cell_records_host(dccrgx_grid* grid, const uint64_t* record_bytes, void* out, size_t bytes);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,9 @@
 //   halo             examples/basic_cell_data.cpp (Dccrg<int>, ghosts == ids)
 //   mapping          prints Mapping results for a list of ids
 //   lists            prints the iteration-cache neighbor lists of every cell
+//   restart FILE     tests/restart/restart_test.cpp's property: a 15x15 game
+//                    saved at step 5 (header = step), loaded into a new grid
+//                    and continued equals the uninterrupted game at step 10
 //   amr CELL...      refines CELLs (6x5x4, max level 1, hood 1, periodic y z),
 //                    checks the data movement, prints new cells and the
 //                    rebuilt iteration-cache lists; then unrefines them back
@@ -163,6 +166,49 @@ static int lists(int argc, char** argv)
     return 0;
 }
 
+template <class Grid> static void gol_turn(Grid& grid)
+{
+    grid.update_copies_of_remote_neighbors();
+    for (const auto& cell : grid.local_cells()) {
+        cell.data->live_neighbor_count = 0;
+        for (const auto& neighbor : cell.neighbors_of)
+            if (neighbor.data->is_alive) cell.data->live_neighbor_count++;
+    }
+    for (const auto& cell : grid.local_cells()) {
+        if (cell.data->live_neighbor_count == 3) cell.data->is_alive = 1;
+        else if (cell.data->live_neighbor_count != 2) cell.data->is_alive = 0;
+    }
+}
+
+static int restart(int argc, char** argv)
+{
+    const std::string name = argc > 2 ? argv[2] : "gol_5.dc";
+    dccrg::Dccrg<game_of_life_cell> ref, grid;
+    for (auto* g : {&ref, &grid}) {
+        g->set_initial_length({15, 15, 1}).set_neighborhood_length(1).set_maximum_refinement_level(-1)
+            .initialize(MPI_COMM_WORLD);
+        for (const auto& cell : g->local_cells()) cell.data->is_alive = splitmix64(cell.id) % 3 == 0;
+    }
+    for (int s = 0; s < 5; s++) gol_turn(grid);
+    uint64_t step = 5;
+    if (!grid.save_grid_data(name, 0, std::make_tuple((void*)&step, 1, MPI_UINT64_T))) abort();
+    dccrg::Dccrg<game_of_life_cell> loaded;
+    uint64_t read_step = 0;
+    if (!loaded.load_grid_data(name, 0, std::make_tuple((void*)&read_step, 1, MPI_UINT64_T), MPI_COMM_WORLD, "RCB"))
+        abort();
+    if (read_step != 5) abort();
+    if (loaded.get_maximum_refinement_level() != grid.get_maximum_refinement_level()) abort();
+    for (int s = 0; s < 5; s++) gol_turn(loaded);
+    for (int s = 0; s < 10; s++) gol_turn(ref);
+    size_t n = 0;
+    for (const auto& cell : ref.local_cells()) {
+        if (!loaded[cell.id] || loaded[cell.id]->is_alive != cell.data->is_alive) abort();
+        n++;
+    }
+    printf("PASS restart %zu\n", n);
+    return 0;
+}
+
 static void print_lists(dccrg::Dccrg<uint64_t>& grid)
 {
     for (const auto& cell : grid.local_cells()) {
@@ -231,6 +277,7 @@ int main(int argc, char** argv)
         else if (mode == "mapping") rc = mapping();
         else if (mode == "lists") rc = lists(argc, argv);
         else if (mode == "amr") rc = amr(argc, argv);
+        else if (mode == "restart") rc = restart(argc, argv);
     }
     MPI_Finalize();
     return rc;

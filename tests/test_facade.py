@@ -137,3 +137,22 @@ def test_facade_amr_matches_oracle():
         assert parse(of_part) == lof, cid
         assert parse(to_part) == lto, cid
     assert n_cells == len(o.cells())
+
+
+@pytest.mark.gpu
+def test_facade_restart(tmp_path):
+    """save_grid_data / load_grid_data through the facade: the resumed game
+    equals the uninterrupted one (checked in the program), and the file is
+    the reference layout: header = step, No_Geometry, one u32 is_alive per
+    cell (the cell's get_mpi_datatype()), cells ascending."""
+    import struct
+    from oracle import dccrg_checkpoint as K
+    path = str(tmp_path / "gol_5.dc")
+    out = run("restart", path)
+    assert "PASS restart 225" in out, out
+    buf = open(path, "rb").read()
+    got = K.read_grid_data(buf, 0, 8)
+    assert struct.unpack("<Q", got["header"])[0] == 5
+    assert got["length"] == (15, 15, 1) and got["geometry"] == K.no_geometry()
+    assert got["order"] == list(range(1, 226))
+    assert all(len(b) == 4 and struct.unpack("<I", b)[0] in (0, 1) for b in got["cells"].values())
