@@ -170,6 +170,10 @@ SIGNATURES = {
     "dccrgx_save_grid_data_host": (C.c_int, [_vp, C.c_char_p, C.c_uint64, _vp, C.c_size_t, _vp, C.c_size_t,
                                              C.c_uint64, C.c_uint64, C.c_uint64, _u64p, _vp, C.c_size_t]),
     "dccrgx_load_cell_records_host": (C.c_int, [_vp, _u64p, _vp, C.c_size_t]),
+    "dccrgx_advect_set_geometry": (C.c_int, [_vp, C.POINTER(AdvectFields_t), C.POINTER(C.c_double),
+                                             C.POINTER(C.c_double)]),
+    "dccrgx_amr_copy_from_parents": (C.c_int, [_vp, _i32p, C.c_size_t]),
+    "dccrgx_amr_average_children": (C.c_int, [_vp, _i32p, C.c_size_t]),
 }
 
 _lib = None

@@ -69,20 +69,19 @@ def initialize(grid: Dccrg, geom: CartesianGeometry, update: bool = True):
     r = np.minimum(np.sqrt((center[:, 0] - 0.25) ** 2 + (center[:, 1] - 0.5) ** 2), 0.15) / 0.15
     grid.write_local("density", 0.25 * (1 + np.cos(np.pi * r)))
     grid.write_local("flux", np.zeros(cells.size))
-    _velocities_lengths(grid, geom, cells, center, ln)
+    _velocities_lengths(grid, geom)
     if update:
         grid.update_copies_of_remote_neighbors(fields=list(ALL))
 
 
-def _velocities_lengths(grid, geom, cells, center=None, ln=None):
-    if center is None:
-        center, ln = geom.centers_and_lengths(cells)
-    grid.write_local("vx", get_vx(center[:, 1]))
-    grid.write_local("vy", get_vy(center[:, 0]))
-    grid.write_local("vz", np.zeros(cells.size))
-    grid.write_local("length_x", ln[:, 0])
-    grid.write_local("length_y", ln[:, 1])
-    grid.write_local("length_z", ln[:, 2])
+def _velocities_lengths(grid, geom, cells=None, center=None, ln=None):
+    """adapter.hpp:304-314 / initialize.hpp:50-58 on the device
+    (dccrgx_advect_set_geometry: get_center / get_length of every local cell
+    from its id, then the solid-body velocities)."""
+    f = grid._advect_fields()
+    start = (C.c_double * 3)(*[float(v) for v in geom.start])
+    l0 = (C.c_double * 3)(*[float(v) for v in geom.l0])
+    check(lib().dccrgx_advect_set_geometry(grid._h, C.byref(f), start, l0))
 
 
 def check_for_adaptation(grid: Dccrg, diff_increase: float, diff_threshold: float,
@@ -154,26 +153,17 @@ def finish_adaptation(grid: Dccrg, geom: CartesianGeometry, all_requests=None,
     if grid.get_maximum_refinement_level() == 0:
         return 0, 0
     new = grid.stop_refining(all_requests=all_requests)
-    m = grid.mapping
-    # new cells: the parent's density, zero flux (:236-262)
-    if new.size:
-        par = m.parents(new)
-        rho = np.concatenate(grid.read_cells("density", par))
-        grid.write_cells("density", new, rho)
-        grid.write_cells("flux", new, np.zeros(new.size))
-    # parents of removed cells: the mean of their children (:264-299)
     removed = grid.get_removed_cells()
-    if removed.size:
-        par = m.parents(removed)
-        rho = np.concatenate(grid.read_cells("density", removed))
-        up, inv = np.unique(par, return_inverse=True)
-        acc = np.zeros(up.size)
-        np.add.at(acc, inv, rho / 8)  # parent += child / 8, children in order (:291-298)
-        grid.write_cells("density", up, acc)
-        grid.write_cells("flux", up, np.zeros(up.size))
+    # new cells are value-initialised by the rebuild (flux = 0); they take the
+    # parent's density (:229-251).  Parents of removed cells: 0, then
+    # += child / 8 over the children in ascending order (:253-300).  Both on
+    # the device, from the retired cells' data.
+    fd = np.array([grid.field_id("density")], dtype=np.int32)
+    check(lib().dccrgx_amr_copy_from_parents(grid._h, fd.ctypes.data_as(X._i32p), fd.size))
+    check(lib().dccrgx_amr_average_children(grid._h, fd.ctypes.data_as(X._i32p), fd.size))
     grid.clear_refined_unrefined_data()
     # velocities and lengths of every local cell (:303-313)
-    _velocities_lengths(grid, geom, grid.local_cells())
+    _velocities_lengths(grid, geom)
     if update:
         grid.update_copies_of_remote_neighbors(fields=list(ALL))
     return int(new.size), int(removed.size)

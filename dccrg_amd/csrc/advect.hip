@@ -365,6 +365,62 @@ __global__ void __launch_bounds__(256) k_max_dt(AdvPtrs p, uint64_t s0, uint64_t
     if (threadIdx.x == 0) atomicMin(out, red[0]);
 }
 
+// velocities and lengths of local cells from their ids (tests/advection/
+// adapter.hpp:304-314, initialize.hpp:50-58): Cartesian_Geometry get_length
+// and get_center (dccrg_cartesian_geometry.hpp:284-364), solve.hpp:336-342
+struct GeoParams {
+    double start[3], l0[3];
+};
+
+__global__ void __launch_bounds__(256) k_advect_geometry(MapParams mp, GeoParams gp, AdvPtrs p, uint64_t n,
+                                                         uint64_t first_id, uint64_t s0,
+                                                         const uint64_t* __restrict__ leaves,
+                                                         const uint32_t* __restrict__ local_g)
+{
+#pragma clang fp contract(off)
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const double maxs = (double)((uint64_t)1 << mp.max_lvl);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t id = leaves ? leaves[local_g[i]] : first_id + i;
+        const uint64_t s = s0 + i;
+        uint64_t idx[3];
+        int l = 0;
+        map_indices(mp, id, idx, &l);
+        const double scale = 1.0 / (double)((uint64_t)1 << l);
+        double len[3], ctr[3];
+        for (int d = 0; d < 3; d++) {
+            len[d] = gp.l0[d] * scale;
+            ctr[d] = gp.start[d] + (double)idx[d] * gp.l0[d] / maxs + len[d] / 2;
+        }
+        double* v0 = (double*)p.v[0];
+        double* v1 = (double*)p.v[1];
+        double* v2 = (double*)p.v[2];
+        v0[s] = -ctr[1] + 0.5;
+        v1[s] = ctr[0] - 0.5;
+        v2[s] = 0;
+        ((double*)p.l[0])[s] = len[0];
+        ((double*)p.l[1])[s] = len[1];
+        ((double*)p.l[2])[s] = len[2];
+    }
+}
+
+// parents of removed cells: 0, then += child / 8 for each child in
+// ascending id order (adapter.hpp:265-300)
+__global__ void __launch_bounds__(256) k_average_children(double* __restrict__ f, const uint64_t* __restrict__ parent,
+                                                          const uint64_t* __restrict__ children, uint64_t n)
+{
+#pragma clang fp contract(off)
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        double acc = 0;
+        for (int k = 0; k < 8; k++) {
+            const uint64_t c = children[8 * i + k];
+            if (c != ~0ull) acc += f[c] / 8;
+        }
+        f[parent[i]] = acc;
+    }
+}
+
 int adv_ptrs(const dccrgx_grid* grid, const dccrgx_advect_fields* f, AdvPtrs* p)
 {
     DX_CHECK(f, DCCRGX_EINVAL, "null field set");
@@ -603,6 +659,114 @@ int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_a
     hipFree(d_marks);
     hipFree(d_diff);
     return DCCRGX_OK;
+}
+
+int dccrgx_advect_set_geometry(dccrgx_grid* grid, const dccrgx_advect_fields* f, const double start[3],
+                               const double level_0_cell_length[3])
+{
+    DX_CHECK(grid && f && start && level_0_cell_length, DCCRGX_EINVAL, "null argument");
+    AdvPtrs p;
+    DX_TRY(adv_ptrs(grid, f, &p));
+    const uint64_t n = grid->n_local;
+    if (!n) return DCCRGX_OK;
+    GeoParams gp;
+    for (int d = 0; d < 3; d++) {
+        gp.start[d] = start[d];
+        gp.l0[d] = level_0_cell_length[d];
+    }
+    uint64_t s0 = 0, nn = n;
+    if (grid->uniform) uniform_local_run(grid, &s0, &nn);
+    hipLaunchKernelGGL(k_advect_geometry, dim3(grid_for(n)), dim3(256), 0, grid->ctx->compute, grid->map, gp, p, n,
+                       grid->first_local, s0, grid->uniform ? (const uint64_t*)nullptr : grid->ex->d_leaves,
+                       grid->uniform ? (const uint32_t*)nullptr : grid->ex->d_local_g);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_t nf)
+{
+    DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
+    if (!grid->amr || grid->amr->new_cells.empty()) return DCCRGX_OK;
+    std::vector<uint64_t> src, dst;
+    for (uint64_t c : grid->amr->new_cells) {
+        uint64_t idx[3];
+        int l;
+        map_indices(grid->map, c, idx, &l);
+        const uint64_t par = l > 0 ? map_cell(grid->map, idx, l - 1) : c;
+        const int64_t a = host_primary_slot(grid, c), b = host_primary_slot(grid, par);
+        DX_CHECK(a >= 0 && b >= 0, DCCRGX_ENOTFOUND, "no data for new cell %llu or its parent",
+                 (unsigned long long)c);
+        dst.push_back((uint64_t)a);
+        src.push_back((uint64_t)b);
+    }
+    hipStream_t st = grid->ctx->compute;
+    uint64_t *d_src = nullptr, *d_dst = nullptr;
+    DX_HIP(hipMalloc(&d_src, src.size() * 8));
+    DX_HIP(hipMalloc(&d_dst, dst.size() * 8));
+    DX_HIP(hipMemcpyAsync(d_src, src.data(), src.size() * 8, hipMemcpyHostToDevice, st));
+    DX_HIP(hipMemcpyAsync(d_dst, dst.data(), dst.size() * 8, hipMemcpyHostToDevice, st));
+    int s = DCCRGX_OK;
+    for (size_t k = 0; k < nf && s == DCCRGX_OK; k++) {
+        if (fields[k] < 0 || (size_t)fields[k] >= grid->fields.size() || grid->fields[fields[k]].variable) {
+            s = set_error(DCCRGX_EINVAL, "bad field %d", fields[k]);
+            break;
+        }
+        const Field& F = grid->fields[fields[k]];
+        s = launch_scatter_ext(F.ptr, d_src, d_dst, src.size(), F.elem, F.ptr, st);
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_src);
+    hipFree(d_dst);
+    return s;
+}
+
+int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf)
+{
+    DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
+    if (!grid->amr || grid->amr->removed.empty()) return DCCRGX_OK;
+    // parent slot -> its removed children's slots, children in ascending id
+    // order (removed is ascending; siblings of one parent interleave with
+    // other parents' children, so group explicitly)
+    std::map<uint64_t, std::vector<uint64_t>> groups;
+    for (uint64_t c : grid->amr->removed) {
+        uint64_t idx[3];
+        int l;
+        map_indices(grid->map, c, idx, &l);
+        const uint64_t par = map_cell(grid->map, idx, l - 1);
+        const int64_t ps = host_primary_slot(grid, par), cs = host_primary_slot(grid, c);
+        DX_CHECK(ps >= 0 && cs >= 0, DCCRGX_ENOTFOUND, "no data for removed cell %llu or its parent",
+                 (unsigned long long)c);
+        auto& g = groups[(uint64_t)ps];
+        DX_CHECK(g.size() < 8, DCCRGX_EINTERNAL, "more than 8 children of cell %llu", (unsigned long long)par);
+        g.push_back((uint64_t)cs);
+    }
+    std::vector<uint64_t> parent, children;
+    for (auto& kv : groups) {
+        parent.push_back(kv.first);
+        children.insert(children.end(), kv.second.begin(), kv.second.end());
+        children.resize(8 * parent.size(), ~0ull);
+    }
+    hipStream_t st = grid->ctx->compute;
+    uint64_t *d_par = nullptr, *d_ch = nullptr;
+    DX_HIP(hipMalloc(&d_par, parent.size() * 8));
+    DX_HIP(hipMalloc(&d_ch, children.size() * 8));
+    DX_HIP(hipMemcpyAsync(d_par, parent.data(), parent.size() * 8, hipMemcpyHostToDevice, st));
+    DX_HIP(hipMemcpyAsync(d_ch, children.data(), children.size() * 8, hipMemcpyHostToDevice, st));
+    int s = DCCRGX_OK;
+    for (size_t k = 0; k < nf; k++) {
+        if (fields[k] < 0 || (size_t)fields[k] >= grid->fields.size() || grid->fields[fields[k]].variable ||
+            grid->fields[fields[k]].elem != 8) {
+            s = set_error(DCCRGX_EINVAL, "field %d is not an f64 field", fields[k]);
+            break;
+        }
+        hipLaunchKernelGGL(k_average_children, dim3(grid_for(parent.size())), dim3(256), 0, st,
+                           (double*)grid->fields[fields[k]].ptr, d_par, d_ch, (uint64_t)parent.size());
+    }
+    DX_HIP(hipGetLastError());
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_par);
+    hipFree(d_ch);
+    return s;
 }
 
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt)

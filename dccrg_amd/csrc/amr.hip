@@ -280,12 +280,15 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     };
 
     // the new leaf state and neighborhoods (fields untouched meanwhile)
+    PhaseTimer T("rebuild");
     grid->ex = nullptr;
     grid->uniform = false;
     int s = explicit_init(grid, leaves.data(), leaves.size());
+    T.lap("explicit_init");
     if (s == DCCRGX_OK) grid->ex->defer_fields = true;
     for (auto it = grid->hoods.begin(); s == DCCRGX_OK && it != grid->hoods.end(); ++it)
         s = explicit_build_hood(grid, it->second);
+    T.lap("neighborhoods");
     if (s == DCCRGX_OK) s = explicit_add_slots(grid, retired);
     if (s != DCCRGX_OK) return rollback(s);
     Explicit* E = grid->ex;
@@ -293,28 +296,26 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     E->retired = retired;
     const uint64_t ns = E->slot_ids.size();
 
-    // old slot of every new slot, from the old layout's own lookup
-    std::vector<uint64_t> sidx, didx;
-    for (uint64_t k = 0; k < ns; k++) {
-        const int64_t o = host_primary_slot(&old, E->slot_ids[k]);
-        if (o >= 0) {
-            sidx.push_back((uint64_t)o);
-            didx.push_back(k);
-        }
-    }
-    uint64_t *d_s = nullptr, *d_d = nullptr;
+    // old slot of every new slot: on the device from the old leaf hash and
+    // slot map when the old grid was explicit (its retired cells were
+    // cleared and are not leaves: they come back value-initialised), from
+    // the uniform layout's arithmetic otherwise
+    int64_t* d_from = nullptr;
     auto fail = [&](int code) {
-        hipFree(d_s);
-        hipFree(d_d);
+        hipFree(d_from);
         return rollback(code);
     };
-    if (hipMalloc(&d_s, std::max<size_t>(sidx.size(), 1) * 8) != hipSuccess ||
-        hipMalloc(&d_d, std::max<size_t>(didx.size(), 1) * 8) != hipSuccess)
+    if (hipMalloc(&d_from, std::max<uint64_t>(ns, 1) * 8) != hipSuccess)
         return fail(set_error(DCCRGX_ENOMEM, "out of device memory for the rebuild plan"));
-    if (!sidx.empty() &&
-        (hipMemcpyAsync(d_s, sidx.data(), sidx.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-         hipMemcpyAsync(d_d, didx.data(), didx.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess))
-        return fail(set_error(DCCRGX_EHIP, "uploading the rebuild plan failed"));
+    if (!old.uniform && old.ex) {
+        const int e = explicit_old_slots(grid, old.ex, d_from, st);
+        if (e != DCCRGX_OK) return fail(e);
+    } else {
+        std::vector<int64_t> from(ns);
+        for (uint64_t k = 0; k < ns; k++) from[k] = host_primary_slot(&old, E->slot_ids[k]);
+        if (ns && hipMemcpy(d_from, from.data(), ns * 8, hipMemcpyHostToDevice) != hipSuccess)
+            return fail(set_error(DCCRGX_EHIP, "uploading the rebuild plan failed"));
+    }
     for (size_t i = 0; i < grid->fields.size(); i++) {
         const Field& F = grid->fields[i];
         const size_t bytes = std::max<uint64_t>(ns, 1) * F.elem;
@@ -322,18 +323,15 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
             np[i] = nullptr;
             return fail(set_error(DCCRGX_ENOMEM, "out of device memory for a refined field (%zu bytes)", bytes));
         }
-        // new cells are value-initialised (dccrg.hpp:10375, 10590)
-        if (hipMemsetAsync(np[i], 0, bytes, st) != hipSuccess)
-            return fail(set_error(DCCRGX_EHIP, "clearing a refined field failed"));
     }
+    // every new slot written once: surviving data moved, new cells
+    // value-initialised (dccrg.hpp:10375, 10590)
     for (size_t i = 0; i < grid->fields.size(); i++) {
         const Field& F = grid->fields[i];
-        if (!sidx.empty() && launch_scatter_ext(F.ptr, d_s, d_d, sidx.size(), F.elem, np[i], st) != DCCRGX_OK)
-            return fail(DCCRGX_EHIP);
+        if (launch_move(F.ptr, d_from, ns, F.elem, np[i], st) != DCCRGX_OK) return fail(DCCRGX_EHIP);
     }
     if (hipStreamSynchronize(st) != hipSuccess) return fail(set_error(DCCRGX_EHIP, "moving field data failed"));
-    hipFree(d_s);
-    hipFree(d_d);
+    hipFree(d_from);
     // commit
     for (size_t i = 0; i < grid->fields.size(); i++) {
         hipFree(grid->fields[i].ptr);
@@ -342,6 +340,7 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     for (auto& kv : old_hoods) free_hood(kv.second);
     explicit_free(old.ex);
     old.ex = nullptr;
+    T.lap("fields moved");
     return DCCRGX_OK;
 }
 
@@ -572,6 +571,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     A.new_cells.clear();
     A.removed.clear();
     if (n_new) *n_new = 0;
+    PhaseTimer T("stop_refining");
     std::set<uint64_t> R(sets[0], sets[0] + counts[0]), NR(sets[1], sets[1] + counts[1]);
     std::set<uint64_t> U(sets[2], sets[2] + counts[2]), NU(sets[3], sets[3] + counts[3]);
     if (grid->uniform && R.empty() && U.empty()) {
@@ -606,6 +606,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
         frontier.swap(next);
     }
     for (uint64_t c : donts) R.erase(c);
+    T.lap("override_refines");
 
     // induce_refines, dccrg.hpp:9730-9907: every coarser neighbor (of / to)
     // of a refined cell is refined, transitively
@@ -623,6 +624,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
         frontier.swap(next);
     }
 
+    T.lap("induce_refines");
     // override_unrefines, dccrg.hpp:9935-10124
     std::set<uint64_t> final_un;
     for (uint64_t u : U) {
@@ -664,6 +666,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
         if (can) final_un.insert(u);
     }
 
+    T.lap("override_unrefines");
     // execute_refines, dccrg.hpp:10243-10693
     const Explicit* E = grid->ex;
     std::unordered_set<uint64_t> gone;
@@ -693,13 +696,20 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
         }
         added.push_back(p);
     }
-    std::vector<uint64_t> leaves;
-    leaves.reserve(E->leaves.size() + added.size());
-    for (uint64_t c : E->leaves)
-        if (!gone.count(c)) leaves.push_back(c);
-    leaves.insert(leaves.end(), added.begin(), added.end());
-    std::sort(leaves.begin(), leaves.end());
-    leaves.erase(std::unique(leaves.begin(), leaves.end()), leaves.end());
+    // surviving leaves (already ascending) merged with the added cells
+    std::vector<uint8_t> gone_flag(E->leaves.size(), 0);
+    for (uint64_t c : gone) {
+        const int64_t g = v.gidx(c);
+        if (g >= 0) gone_flag[g] = 1;
+    }
+    std::vector<uint64_t> kept;
+    kept.reserve(E->leaves.size());
+    for (size_t k = 0; k < E->leaves.size(); k++)
+        if (!gone_flag[k]) kept.push_back(E->leaves[k]);
+    std::sort(added.begin(), added.end());
+    added.erase(std::unique(added.begin(), added.end()), added.end());
+    std::vector<uint64_t> leaves(kept.size() + added.size());
+    leaves.erase(std::set_union(kept.begin(), kept.end(), added.begin(), added.end(), leaves.begin()), leaves.end());
     std::sort(retired.begin(), retired.end());
     std::sort(A.new_cells.begin(), A.new_cells.end());
     std::sort(A.removed.begin(), A.removed.end());
@@ -708,10 +718,12 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     A.to_unrefine.clear();
     A.not_to_unrefine.clear();
     A.not_to_refine = donts;
+    T.lap("new leaf set");
     if (!R.empty() || !final_un.empty()) {
         if (grid->ex) explicit_clear_retired(grid->ex);
         DX_TRY(rebuild(grid, leaves, retired));
     }
+    T.lap("rebuild");
     if (n_new) *n_new = A.new_cells.size();
     return DCCRGX_OK;
 }

@@ -267,20 +267,31 @@ int dccrgx_map_host_cell(const dccrgx_mapping* map, const uint64_t idx3[3], int3
     return DCCRGX_OK;
 }
 
+}  // extern "C"
+
+namespace dccrgx {
+static uint64_t host_op(const MapParams& p, int op, uint64_t c)
+{
+    uint64_t idx[3];
+    int l;
+    const bool ok = map_indices(p, c, idx, &l);
+    switch (op) {
+    case DCCRGX_OP_LENGTH_IN_INDICES: return ok ? ((uint64_t)1 << (p.max_lvl - l)) : DCCRGX_ERROR_INDEX;
+    case DCCRGX_OP_PARENT: return !ok ? 0 : (l == 0 ? c : map_cell(p, idx, l - 1));
+    case DCCRGX_OP_LEVEL_0_PARENT: return !ok ? 0 : (l == 0 ? c : map_cell(p, idx, 0));
+    default: return !ok ? 0 : (l >= p.max_lvl ? c : map_cell(p, idx, l + 1));
+    }
+}
+}  // namespace dccrgx
+
+extern "C" {
+
 int dccrgx_map_host_op(const dccrgx_mapping* map, int op, uint64_t c, uint64_t* out)
 {
     MapParams p;
     DX_TRY(make_map_params(map, &p));
     DX_CHECK(out && op >= 0 && op <= DCCRGX_OP_CHILD, DCCRGX_EINVAL, "bad argument");
-    uint64_t idx[3];
-    int l;
-    const bool ok = map_indices(p, c, idx, &l);
-    switch (op) {
-    case DCCRGX_OP_LENGTH_IN_INDICES: *out = ok ? ((uint64_t)1 << (p.max_lvl - l)) : DCCRGX_ERROR_INDEX; break;
-    case DCCRGX_OP_PARENT: *out = !ok ? 0 : (l == 0 ? c : map_cell(p, idx, l - 1)); break;
-    case DCCRGX_OP_LEVEL_0_PARENT: *out = !ok ? 0 : (l == 0 ? c : map_cell(p, idx, 0)); break;
-    default: *out = !ok ? 0 : (l >= p.max_lvl ? c : map_cell(p, idx, l + 1)); break;
-    }
+    *out = host_op(p, op, c);
     return DCCRGX_OK;
 }
 
@@ -306,8 +317,11 @@ int dccrgx_map_host_ids_to_indices(const dccrgx_mapping* map, const uint64_t* id
 
 int dccrgx_map_host_ids_op(const dccrgx_mapping* map, int op, const uint64_t* ids, size_t n, uint64_t* out)
 {
-    DX_CHECK(ids || !n, DCCRGX_EINVAL, "null argument");
-    for (size_t i = 0; i < n; i++) DX_TRY(dccrgx_map_host_op(map, op, ids[i], out + i));
+    DX_CHECK((ids && out) || !n, DCCRGX_EINVAL, "null argument");
+    DX_CHECK(op >= 0 && op <= DCCRGX_OP_CHILD, DCCRGX_EINVAL, "bad op %d", op);
+    MapParams p;
+    DX_TRY(make_map_params(map, &p));
+    for (size_t i = 0; i < n; i++) out[i] = host_op(p, op, ids[i]);
     return DCCRGX_OK;
 }
 

@@ -396,10 +396,10 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     auto* E = new Explicit();
     grid->ex = E;
     E->leaves.assign(leaves, leaves + n);
-    std::sort(E->leaves.begin(), E->leaves.end());
+    if (!std::is_sorted(E->leaves.begin(), E->leaves.end())) std::sort(E->leaves.begin(), E->leaves.end());
     E->leaves.erase(std::unique(E->leaves.begin(), E->leaves.end()), E->leaves.end());
-    for (uint64_t c : E->leaves)
-        DX_CHECK(map_level(grid->map, c) >= 0, DCCRGX_EINVAL, "invalid cell %llu", (unsigned long long)c);
+    DX_CHECK(E->leaves[0] > 0 && E->leaves.back() <= grid->map.last_cell, DCCRGX_EINVAL, "invalid cell %llu",
+             (unsigned long long)(E->leaves[0] == 0 ? 0 : E->leaves.back()));
     E->n = E->leaves.size();
     uint64_t cap = 16;
     while (cap < 2 * E->n) cap <<= 1;
@@ -413,12 +413,14 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     DX_HIP(hipGetLastError());
     // ownership: the process of the level-0 ancestor (no load balancing)
     E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
+    E->owner.resize(E->n);
     for (uint64_t i = 0; i < E->n; i++) {
         uint64_t idx[3];
         int l;
         map_indices(grid->map, E->leaves[i], idx, &l);
-        const uint64_t l0 = map_cell(grid->map, idx, 0);
-        if (part_owner(E->part, l0) == ctx->rank) {
+        const uint64_t l0 = l == 0 ? E->leaves[i] : map_cell(grid->map, idx, 0);
+        E->owner[i] = part_owner(E->part, l0);
+        if (E->owner[i] == ctx->rank) {
             E->local.push_back(E->leaves[i]);
             E->local_g.push_back((uint32_t)i);
         }
@@ -580,6 +582,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
     free_hood(h);
+    PhaseTimer T("build_hood");
     h.K = (int32_t)(h.items.size() / 3);
     h.of_c = h.items;  // explicit grids use the original axes
     h.to_c.resize(h.items.size());
@@ -594,6 +597,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     DX_HIP(hipMalloc(&h.d_nof_row, (N + 1) * 8));
     uint64_t tot = 0;
     DX_TRY(nof_device(grid, h, E->d_leaves, N, h.d_nof_row, &h.d_nof_id, &h.d_nof_off, &h.d_nof_g, &tot, st));
+    T.lap("neighbors_of");
     // neighbors_to = transpose (rows: leaves)
     uint32_t *d_cnt = nullptr, *d_cur = nullptr, *d_tmp = nullptr, *d_ucnt = nullptr;
     DX_HIP(hipMalloc(&d_cnt, N * 4));
@@ -623,6 +627,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     hipFree(d_ucnt);
     hipFree(d_trow);
 
+    T.lap("neighbors_to");
     // per-rank bookkeeping from the device lists (dccrg.hpp:9131-9234, 8729-8891)
     const uint64_t nl = E->local.size();
     std::vector<uint64_t> nof_row(N + 1);
@@ -638,14 +643,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     if (nof_row[N]) DX_HIP(hipMemcpyAsync(L.h_nof_g.data(), h.d_nof_g, nof_row[N] * 4, hipMemcpyDeviceToHost, st));
     if (nto_row[N]) DX_HIP(hipMemcpyAsync(L.h_nto_g.data(), h.d_nto_g, nto_row[N] * 4, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
-    auto owner_of = [&](uint32_t g) {
-        uint64_t idx[3];
-        int l;
-        map_indices(grid->map, E->leaves[g], idx, &l);
-        return part_owner(E->part, map_cell(grid->map, idx, 0));
-    };
-    std::vector<int> owner(N);
-    for (uint64_t g = 0; g < N; g++) owner[g] = owner_of((uint32_t)g);
+    const std::vector<int32_t>& owner = E->owner;
     const int me = ctx->rank;
     std::set<uint64_t> remote;
     std::map<int, std::set<uint64_t>> send, recv;
@@ -672,6 +670,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
         if (outer) h.outer.push_back(E->local[i]);
     }
     h.remote.assign(remote.begin(), remote.end());
+    T.lap("classification");
     // ghost slots for this neighborhood's remote neighbors
     DX_TRY(explicit_add_slots(grid, h.remote));
 
@@ -704,6 +703,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     hipFree(d_pairs);
     hipFree(d_pc);
 
+    T.lap("stencil rows");
     // per-peer plans: send from local slots, receive into ghost slots
     std::set<int> peers;
     for (auto& kv : send) peers.insert(kv.first);
@@ -770,6 +770,67 @@ int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id)
     // clear_refined_unrefined_data
     auto jt = E->extra.find(id);
     return jt != E->extra.end() ? (int64_t)jt->second : -1;
+}
+
+// rebuild(): new slot k takes old slot src[k] (-1: value-initialised), looked
+// up in the old leaf hash and slot map on the device
+__global__ void __launch_bounds__(256) k_old_slots(ExView old, const uint32_t* __restrict__ old_slot_of_g,
+                                                   const uint64_t* __restrict__ ids, uint64_t n,
+                                                   int64_t* __restrict__ src)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+        const int64_t g = ex_find(old, ids[k]);
+        const uint32_t s = g < 0 ? NO_SLOT : old_slot_of_g[g];
+        src[k] = s == NO_SLOT ? -1 : (int64_t)s;
+    }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_move(const T* __restrict__ src, const int64_t* __restrict__ from, uint64_t n,
+                                              uint32_t words, T* __restrict__ dst)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const uint64_t tot = n * words;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += stride) {
+        const uint64_t k = i / words, w = i - k * words;
+        const int64_t f = from[k];
+        dst[i] = f >= 0 ? src[(uint64_t)f * words + w] : T(0);
+    }
+}
+
+int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_src, hipStream_t st)
+{
+    const Explicit* E = grid->ex;
+    const uint64_t n = E->slot_ids.size();
+    if (!n) return DCCRGX_OK;
+    uint64_t* d_ids = nullptr;
+    DX_TRY(upload(E->slot_ids, &d_ids, st));
+    ExView v{};
+    v.mp = grid->map;
+    v.keys = old->d_keys;
+    v.vals = old->d_vals;
+    v.mask = old->mask;
+    hipLaunchKernelGGL(k_old_slots, dim3(grid_for(n)), dim3(256), 0, st, v, old->d_slot_of_g, d_ids, n, d_src);
+    const hipError_t e = hipGetLastError();
+    DX_HIP(hipStreamSynchronize(st));
+    hipFree(d_ids);
+    DX_HIP(e);
+    return DCCRGX_OK;
+}
+
+// dst[k] = src[from[k]] (or zero), elements of `elem` bytes
+int launch_move(const void* src, const int64_t* from, uint64_t n, uint32_t elem, void* dst, hipStream_t st)
+{
+    if (!n) return DCCRGX_OK;
+    if (elem % 4 == 0)
+        hipLaunchKernelGGL(k_move<uint32_t>, dim3(grid_for(n * (elem / 4))), dim3(256), 0, st, (const uint32_t*)src,
+                           from, n, elem / 4, (uint32_t*)dst);
+    else
+        hipLaunchKernelGGL(k_move<uint8_t>, dim3(grid_for(n * elem)), dim3(256), 0, st, (const uint8_t*)src, from, n,
+                           elem, (uint8_t*)dst);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
 }
 
 int explicit_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int64_t* slots, hipStream_t st)

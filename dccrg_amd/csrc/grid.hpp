@@ -129,6 +129,7 @@ struct Explicit {
     Partition part;                 // over level-0 cells
     std::vector<uint64_t> local;    // ascending local ids
     std::vector<uint32_t> local_g;  // their global indices
+    std::vector<int32_t> owner;     // process of each leaf (level-0 ancestor's, dccrg.hpp:8098-8145)
     uint32_t* d_local_g = nullptr;
     // Storage (per rank, not replicated): slots [0, nl) hold the local cells
     // in ascending id order, then ghost copies of remote neighbors (of every
@@ -278,6 +279,10 @@ void explicit_clear_retired(Explicit* E);
 // explicit grids: give `ids` (leaves or retired cells) storage slots if they
 // have none, growing every field unless a rebuild defers that
 int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids);
+// rebuild(): old slot (or -1) of every slot of the new layout, device output
+int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_src, hipStream_t st);
+// dst[k] = src[from[k]], or zero where from[k] < 0
+int launch_move(const void* src, const int64_t* from, uint64_t n, uint32_t elem, void* dst, hipStream_t st);
 int explicit_build_hood(dccrgx_grid* grid, Hood& h);
 int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, uint64_t* ids,
                        size_t cap, size_t* n);

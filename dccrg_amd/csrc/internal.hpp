@@ -4,8 +4,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <string>
@@ -46,6 +48,29 @@ int set_error(int code, const char* fmt, ...);
     do {                                                              \
         if (!(cond)) return ::dccrgx::set_error((code), __VA_ARGS__); \
     } while (0)
+
+// ---------------------------------------------------------------------------
+// host phase timing of structural calls (AMR rebuild, neighbor builds):
+// DCCRGX_TIMING=1 prints one line per phase to stderr
+// ---------------------------------------------------------------------------
+struct PhaseTimer {
+    const char* scope;
+    std::chrono::steady_clock::time_point t;
+    bool on;
+    explicit PhaseTimer(const char* s) : scope(s), t(std::chrono::steady_clock::now())
+    {
+        const char* e = std::getenv("DCCRGX_TIMING");
+        on = e && *e && *e != '0';
+    }
+    void lap(const char* what)
+    {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[dccrgx] %s %s %.3f ms\n", scope, what,
+                     std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
 
 // ---------------------------------------------------------------------------
 // 64-bit division by an invariant divisor (Granlund-Montgomery, "unsigned

@@ -337,6 +337,12 @@ int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_a
 /* one step of tests/advection/2d.cpp:321-390: density halo start, inner
  * fluxes, halo wait, outer fluxes, apply */
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt);
+/* velocities and lengths of every local cell, adapter.hpp:304-314 /
+ * initialize.hpp:50-58: Cartesian_Geometry get_length / get_center
+ * (dccrg_cartesian_geometry.hpp:284-364) and solve.hpp:336-342's
+ * vx = 0.5 - y, vy = x - 0.5, vz = 0 */
+int dccrgx_advect_set_geometry(dccrgx_grid* grid, const dccrgx_advect_fields* f, const double start[3],
+                               const double level_0_cell_length[3]);
 
 /* ------------------------------------------------------------------------ *
  * Adaptive mesh refinement (dccrg.hpp:2456-2806, 3483-3543, 5550-5567,
@@ -375,6 +381,14 @@ int dccrgx_get_new_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, siz
 int dccrgx_get_removed_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, size_t* n);
 /* Dccrg::clear_refined_unrefined_data, dccrg.hpp:5550-5567 */
 int dccrgx_clear_refined_unrefined_data(dccrgx_grid* grid);
+/* before clear_refined_unrefined_data: every cell the last stop_refining
+ * created takes its parent's (refined, retired) values of `fields`
+ * (tests/advection/adapter.hpp:229-251) */
+int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_t nf);
+/* before clear_refined_unrefined_data: the parent of removed cells gets 0,
+ * then += child / 8 over its children in ascending id order, for each f64
+ * field (adapter.hpp:253-300) */
+int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf);
 
 /* ------------------------------------------------------------------------ *
  * Poisson, tests/poisson/poisson_solve.hpp: Poisson_Solve (BiCG over face

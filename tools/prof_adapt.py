@@ -1,0 +1,49 @@
+"""Where the adaptive advection step's time goes (configs[2], 400x400x1,
+max_ref_lvl 2, adapt every step): cProfile of the host side plus the
+library's phase timers (DCCRGX_TIMING=1, stderr)."""
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import dccrg_amd as D  # noqa: E402
+from dccrg_amd import advection as A  # noqa: E402
+
+rel, thr, sens, cfl, M = 0.025, 0.25, 0.5, 0.5, 2
+ctx = D.Context(0, 0, 1)
+g = (D.Dccrg().set_initial_length((400, 400, 1)).set_maximum_refinement_level(M)
+     .set_periodic(True, True, False).set_neighborhood_length(0).initialize(ctx))
+g.add_advection_fields()
+geom = A.geometry_2d(g)
+A.initialize(g, geom)
+for _ in range(M):
+    A.adapt_grid(g, geom, *A.check_for_adaptation(g, rel / M, thr, sens))
+    A.initialize(g, geom)
+dt = g.max_time_step()
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+
+
+def loop():
+    global dt
+    for _ in range(steps):
+        g.update_copies_of_remote_neighbors(fields=["density"])
+        t0 = time.perf_counter()
+        sets = A.check_for_adaptation(g, rel / M, thr, sens)
+        t1 = time.perf_counter()
+        g.advect_step(cfl * dt)
+        ctx.synchronize()
+        t2 = time.perf_counter()
+        A.adapt_grid(g, geom, *sets)
+        t3 = time.perf_counter()
+        dt = g.max_time_step()
+        print(f"cells {g.n_local} check {1e3*(t1-t0):.1f} ms solve {1e3*(t2-t1):.1f} ms adapt {1e3*(t3-t2):.1f} ms",
+              flush=True)
+
+
+pr = cProfile.Profile()
+pr.enable()
+loop()
+pr.disable()
+pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
