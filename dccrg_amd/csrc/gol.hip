@@ -205,9 +205,13 @@ __device__ __forceinline__ uint32_t pack_bits(uint4 v)
            (v.w != 0u ? 0x1000000u : 0u);
 }
 
-template <int NW, int RW, bool NT = false>
+// PF: planes in flight (1: the next plane is loaded while the current one is
+// computed; 2: two planes ahead, twice the bytes in flight per lane).
+// NTL: non-temporal loads for the rows no other tile reads as its apron.
+template <int NW, int RW, bool NT = false, int PF = 1, bool NTL = false>
 __global__ void __launch_bounds__(64 * NW) k_gol26v(Gol4Args g)
 {
+    static_assert(PF == 1 || PF == 2, "one or two planes in flight");
     constexpr int TA = 256, TB = NW * RW;
     static_assert(NW >= 2, "apron rows are loaded by the first and last wave");
     __shared__ uint32_t P[2][TB + 2][64];
@@ -272,25 +276,37 @@ __global__ void __launch_bounds__(64 * NW) k_gol26v(Gol4Args g)
 
     uint4 F[RW + 1];       // fetched plane (own rows + extra row)
     uint32_t FE[RW + 1];   // fetched apron scalars
-    auto fetch = [&](int64_t sc) {
+    uint4 F2[RW + 1];      // PF == 2: the plane after
+    uint32_t FE2[RW + 1];
+    auto fetch_into = [&](int64_t sc, uint4 (&Fd)[RW + 1], uint32_t (&FEd)[RW + 1]) {
         const uint32_t* __restrict__ plane = g.in + (uint64_t)sc * g.S;
 #pragma unroll
         for (int k = 0; k <= RW; k++) {
             if (k == RW && xrow < 0) {
-                F[k] = make_uint4(0, 0, 0, 0);
+                Fd[k] = make_uint4(0, 0, 0, 0);
             } else {
-                const uint4 v = *reinterpret_cast<const uint4*>(plane + roff[k]);
-                F[k] = (rmask >> k) & 1u ? v : make_uint4(0, 0, 0, 0);
+                // tile rows 0 and TB-1 are the neighbouring tiles' aprons
+                const bool priv = k < RW && (RW * w + k) != 0 && (RW * w + k) != TB - 1;
+                uint4 v;
+                if (NTL && priv) {
+                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(plane + roff[k]));
+                    v = make_uint4(x.x, x.y, x.z, x.w);
+                } else {
+                    v = *reinterpret_cast<const uint4*>(plane + roff[k]);
+                }
+                Fd[k] = (rmask >> k) & 1u ? v : make_uint4(0, 0, 0, 0);
             }
         }
         if (emask) {
 #pragma unroll
-            for (int k = 0; k <= RW; k++) FE[k] = (emask >> k) & 1u ? plane[eoff[k]] : 0u;
+            for (int k = 0; k <= RW; k++) FEd[k] = (emask >> k) & 1u ? plane[eoff[k]] : 0u;
         } else {
 #pragma unroll
-            for (int k = 0; k <= RW; k++) FE[k] = 0u;
+            for (int k = 0; k <= RW; k++) FEd[k] = 0u;
         }
     };
+    auto fetch = [&](int64_t sc) { fetch_into(sc, F, FE); };
     auto stash = [&](int buf) {
 #pragma unroll
         for (int k = 0; k < RW; k++) P[buf][1 + RW * w + k][lane] = pack_bits(F[k]);
@@ -332,6 +348,7 @@ __global__ void __launch_bounds__(64 * NW) k_gol26v(Gol4Args g)
 #pragma unroll
     for (int k = 0; k < RW; k++) Vc[k] = F[k];
     fetch(c0 + 1);
+    if (PF == 2 && c0 + 2 <= c1) fetch_into(c0 + 2, F2, FE2);
     __syncthreads();
     plane_sums(1);
 #pragma unroll
@@ -346,7 +363,16 @@ __global__ void __launch_bounds__(64 * NW) k_gol26v(Gol4Args g)
         stash(buf);
 #pragma unroll
         for (int k = 0; k < RW; k++) Vn[k] = F[k];
-        if (c + 2 <= c1) fetch(c + 2);
+        if (PF == 1) {
+            if (c + 2 <= c1) fetch(c + 2);
+        } else {
+#pragma unroll
+            for (int k = 0; k <= RW; k++) {
+                F[k] = F2[k];
+                FE[k] = FE2[k];
+            }
+            if (c + 3 <= c1) fetch_into(c + 3, F2, FE2);
+        }
         __syncthreads();
         plane_sums(buf);
         buf ^= 1;
@@ -399,6 +425,159 @@ __global__ void __launch_bounds__(64 * NW) k_gol26v(Gol4Args g)
 
 // Vectorised LB == 1 kernel (2-D grids, LA % 4 == 0): a workgroup owns 256*NW
 // cells of a row and marches along C (the y rows); lane = 4 cells (dwordx4),
+// Wave-independent 26-neighbor stencil (LA % 4 == 0): every wavefront owns a
+// 256-cell x RW-row tile and marches it along C with no workgroup barrier and
+// no LDS.  Per plane a lane loads its dwordx4 of the RW own rows and of the
+// two apron rows (those come from L2: the neighbouring tiles load them as
+// their own rows), packs the alive bits 4 cells per u32, and takes its
+// neighbours' edge bytes with cross-lane shuffles; the left / right apron
+// cells come from scalar loads of lanes 0 and 63.  The next plane's loads are
+// issued right after the current plane's values are taken out of their
+// registers, so they overlap the sums and the stores.  Without barriers every
+// wave keeps its own loads in flight (k_gol26v's 8-wave workgroups stall the
+// CU's memory stream at each plane's __syncthreads).
+template <int RW>
+__global__ void __launch_bounds__(256) k_gol26w(Gol4Args g)
+{
+    constexpr int TA = 256, NR = RW + 2;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, q8 = g.nwg >> 3, r8 = g.nwg & 7;
+    const uint32_t wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const uint32_t tiles = g.tiles_a * g.tiles_b;
+    const uint64_t wave_id = (uint64_t)wgid * 4 + w;
+    const uint32_t tile_id = (uint32_t)(wave_id % tiles);
+    const int64_t chunk_id = (int64_t)(wave_id / tiles);
+    const int64_t a0 = (int64_t)(tile_id % g.tiles_a) * TA;
+    const int64_t b0 = (int64_t)(tile_id / g.tiles_a) * RW;
+    const int64_t c0 = g.s0 + chunk_id * g.chunk;
+    const int64_t c1 = min(g.s1, c0 + g.chunk);
+    if (c0 >= c1) return;  // wave-uniform: the whole wave leaves
+
+    const int64_t LA = (int64_t)g.LA, LB = (int64_t)g.LB;
+    auto wrapA = [&](int64_t a) -> int64_t {
+        if (a >= 0 && a < LA) return a;
+        return g.perA ? ug_wrap(a, LA) : -1;
+    };
+    auto wrapB = [&](int64_t b) -> int64_t {
+        if (b >= 0 && b < LB) return b;
+        return g.perB ? ug_wrap(b, LB) : -1;
+    };
+    // rows b0-1 .. b0+RW (r = 0 .. RW+1)
+    const int64_t av = wrapA(a0 + 4 * lane);
+    const int64_t ae = lane == 0 ? wrapA(a0 - 1) : (lane == 63 ? wrapA(a0 + TA) : -1);
+    uint32_t roff[NR], eoff[NR];
+    uint32_t rmask = 0, emask = 0;
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+        const int64_t b = wrapB(b0 - 1 + r);
+        const bool ok = av >= 0 && b >= 0;
+        roff[r] = ok ? (uint32_t)(av + LA * b) : 0u;
+        rmask |= ok ? (1u << r) : 0u;
+        const bool eok = ae >= 0 && b >= 0;
+        eoff[r] = eok ? (uint32_t)(ae + LA * b) : 0u;
+        emask |= eok ? (1u << r) : 0u;
+    }
+
+    uint4 F[NR];
+    uint32_t FE[NR];
+    auto fetch = [&](int64_t sc) {
+        const uint32_t* __restrict__ plane = g.in + (uint64_t)sc * g.S;
+#pragma unroll
+        for (int r = 0; r < NR; r++) {
+            const uint4 v = *reinterpret_cast<const uint4*>(plane + roff[r]);
+            F[r] = (rmask >> r) & 1u ? v : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < NR; r++) FE[r] = (emask >> r) & 1u ? plane[eoff[r]] : 0u;
+    };
+    // packed alive bits of the fetched plane and its 3x3 sums for the own
+    // rows; nbx: some own cell of the plane holds a raw value other than 0 / 1
+    // (then the rule re-reads the raw values instead of using the bits)
+    uint32_t Sx[RW], Bx[RW];
+    bool nbx = false;
+    auto plane_sums = [&]() {
+        uint32_t h[NR];
+        uint32_t odd = 0;
+#pragma unroll
+        for (int r = 0; r < NR; r++) {
+            const uint32_t m = pack_bits(F[r]);
+            const uint32_t up = __shfl_up(m, 1, 64), dn = __shfl_down(m, 1, 64);
+            const uint32_t lft = lane > 0 ? (up >> 24) : (FE[r] != 0u ? 1u : 0u);
+            const uint32_t rgt = lane < 63 ? (dn & 0xffu) : (FE[r] != 0u ? 1u : 0u);
+            h[r] = m + ((m << 8) | lft) + ((m >> 8) | (rgt << 24));
+            if (r >= 1 && r <= RW) {
+                Bx[r - 1] = m;
+                odd |= (F[r].x | F[r].y | F[r].z | F[r].w) >> 1;
+            }
+        }
+        nbx = __any(odd != 0u);
+#pragma unroll
+        for (int k = 0; k < RW; k++) Sx[k] = h[k] + h[k + 1] + h[k + 2];
+    };
+
+    uint32_t Sp[RW], Sc[RW], Bc[RW];
+    bool nbc;
+    fetch(c0 - 1);
+    plane_sums();
+#pragma unroll
+    for (int k = 0; k < RW; k++) Sp[k] = Sx[k];
+    fetch(c0);
+    plane_sums();
+#pragma unroll
+    for (int k = 0; k < RW; k++) {
+        Sc[k] = Sx[k];
+        Bc[k] = Bx[k];
+    }
+    nbc = nbx;
+    fetch(c0 + 1);
+    const uint64_t ua = (uint64_t)(a0 + 4 * lane);
+    const bool a_ok = (int64_t)ua < LA;
+    for (int64_t c = c0; c < c1; c++) {
+        // plane c+1 arrived: take it out of F, then issue plane c+2
+        plane_sums();
+        if (c + 2 <= c1) fetch(c + 2);
+        const uint32_t* __restrict__ pin = g.in + (uint64_t)c * g.S;
+        const uint64_t plin = g.S * (uint64_t)(c + g.cbase);
+        const bool full = plin >= g.lo && plin + g.S <= g.hi;
+        uint32_t* pcnt = g.cnt + (uint64_t)c * g.S;
+        uint32_t* pout = g.out + (uint64_t)c * g.S;
+#pragma unroll
+        for (int k = 0; k < RW; k++) {
+            const uint32_t cnt4 = Sp[k] + Sc[k] + Sx[k] - Bc[k];
+            const int64_t b = b0 + k;
+            if (a_ok && b < LB) {
+                const uint32_t n0 = cnt4 & 0xffu, n1 = (cnt4 >> 8) & 0xffu, n2 = (cnt4 >> 16) & 0xffu,
+                               n3 = cnt4 >> 24;
+                const uint32_t p = (uint32_t)ua + (uint32_t)LA * (uint32_t)b;
+                const uint32_t bc = Bc[k];
+                // raw centre values: the alive bits unless the plane holds other values
+                const uint4 v = nbc ? *reinterpret_cast<const uint4*>(pin + p)
+                                    : make_uint4(bc & 1u, (bc >> 8) & 1u, (bc >> 16) & 1u, bc >> 24);
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 xc = {n0, n1, n2, n3};
+                const u32x4 xv = {gol_rule(n0, v.x), gol_rule(n1, v.y), gol_rule(n2, v.z), gol_rule(n3, v.w)};
+                if (full) {
+                    __builtin_nontemporal_store(xc, reinterpret_cast<u32x4*>(pcnt + p));
+                    __builtin_nontemporal_store(xv, reinterpret_cast<u32x4*>(pout + p));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const uint64_t lin = plin + p + j;
+                        if (lin >= g.lo && lin < g.hi) {
+                            pcnt[p + j] = xc[j];
+                            pout[p + j] = xv[j];
+                        }
+                    }
+                }
+            }
+            Sp[k] = Sc[k];
+            Sc[k] = Sx[k];
+            Bc[k] = Bx[k];
+        }
+        nbc = nbx;
+    }
+}
+
 // packed-byte row sums as in k_gol26v; rows b-1 / b+1 are the row itself
 // (periodic B: mult = 3) or absent (mult = 1).
 template <int NW, bool NTS = false>
@@ -882,11 +1061,26 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
         // 8 x 4 with non-temporal stores measured fastest on MI355X
         // (tools/gol_sweep.py; profiles/r1_summary.md)
         int64_t var = getenv_int("DCCRGX_GOL_VARIANT", 841);
-        if (var != 44 && var != 42 && var != 81 && var != 162 && var != 82 && var != 84 &&
-            var != 1621)
+        // 8 4 1 [P [L]]: 8 waves x 4 rows, NT stores, P planes in flight, L non-temporal loads
+        // 9RR: wave-independent tiles of RR rows (k_gol26w)
+        if (var != 44 && var != 42 && var != 81 && var != 162 && var != 82 && var != 84 && var != 1621 &&
+            var != 8412 && var != 8411 && var != 84121 && var != 84111 && var != 4412 && var != 44121 &&
+            var != 904 && var != 906 && var != 908 && var != 912 && var != 916)
             var = 841;
-        const int64_t shape = var >= 1000 ? var / 10 : (var == 841 ? 84 : var);  // drop the NT digit
-        const int NW = (int)(shape / 10), RW = (int)(shape % 10);
+        int NW = 8, RW = 4;  // waves per workgroup (1: independent waves) x rows per wave
+        switch (var) {
+        case 44: case 4412: case 44121: NW = 4; RW = 4; break;
+        case 42: NW = 4; RW = 2; break;
+        case 81: NW = 8; RW = 1; break;
+        case 82: NW = 8; RW = 2; break;
+        case 162: case 1621: NW = 16; RW = 2; break;
+        default:
+            if (var >= 900 && var < 1000) {
+                NW = 1;
+                RW = (int)(var - 900);
+            }
+            break;
+        }
         const int TB = NW * RW;
         v.tiles_a = (uint32_t)((u.LA + 255) / 256);
         v.tiles_b = (uint32_t)((u.LB + TB - 1) / TB);
@@ -902,7 +1096,13 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
         const int64_t chunks = (nsl + chunk - 1) / chunk;
         DX_CHECK(tiles * chunks < (int64_t)UINT32_MAX, DCCRGX_EINVAL, "grid too large for one launch");
         v.nwg = (uint32_t)(tiles * chunks);
+        if (NW == 1) v.nwg = (uint32_t)((tiles * chunks + 3) / 4);  // four independent waves per workgroup
         switch (var) {
+        case 904: hipLaunchKernelGGL((k_gol26w<4>), dim3(v.nwg), dim3(256), 0, st, v); break;
+        case 906: hipLaunchKernelGGL((k_gol26w<6>), dim3(v.nwg), dim3(256), 0, st, v); break;
+        case 908: hipLaunchKernelGGL((k_gol26w<8>), dim3(v.nwg), dim3(256), 0, st, v); break;
+        case 912: hipLaunchKernelGGL((k_gol26w<12>), dim3(v.nwg), dim3(256), 0, st, v); break;
+        case 916: hipLaunchKernelGGL((k_gol26w<16>), dim3(v.nwg), dim3(256), 0, st, v); break;
         case 44: hipLaunchKernelGGL((k_gol26v<4, 4>), dim3(v.nwg), dim3(256), 0, st, v); break;
         case 42: hipLaunchKernelGGL((k_gol26v<4, 2>), dim3(v.nwg), dim3(256), 0, st, v); break;
         case 81: hipLaunchKernelGGL((k_gol26v<8, 1>), dim3(v.nwg), dim3(512), 0, st, v); break;
@@ -910,6 +1110,12 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
         case 82: hipLaunchKernelGGL((k_gol26v<8, 2>), dim3(v.nwg), dim3(512), 0, st, v); break;
         case 84: hipLaunchKernelGGL((k_gol26v<8, 4>), dim3(v.nwg), dim3(512), 0, st, v); break;
         case 1621: hipLaunchKernelGGL((k_gol26v<16, 2, true>), dim3(v.nwg), dim3(1024), 0, st, v); break;
+        case 8412: hipLaunchKernelGGL((k_gol26v<8, 4, true, 2>), dim3(v.nwg), dim3(512), 0, st, v); break;
+        case 8411: hipLaunchKernelGGL((k_gol26v<8, 4, true, 1, false>), dim3(v.nwg), dim3(512), 0, st, v); break;
+        case 84121: hipLaunchKernelGGL((k_gol26v<8, 4, true, 2, true>), dim3(v.nwg), dim3(512), 0, st, v); break;
+        case 84111: hipLaunchKernelGGL((k_gol26v<8, 4, true, 1, true>), dim3(v.nwg), dim3(512), 0, st, v); break;
+        case 4412: hipLaunchKernelGGL((k_gol26v<4, 4, true, 2>), dim3(v.nwg), dim3(256), 0, st, v); break;
+        case 44121: hipLaunchKernelGGL((k_gol26v<4, 4, true, 2, true>), dim3(v.nwg), dim3(256), 0, st, v); break;
         case 841:
         default: hipLaunchKernelGGL((k_gol26v<8, 4, true>), dim3(v.nwg), dim3(512), 0, st, v); break;
         }

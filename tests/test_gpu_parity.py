@@ -271,7 +271,8 @@ VEC_CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", ["82", "44", "42", "84", "81", "162", "841", "1621", "scalar"])
+@pytest.mark.parametrize("variant", ["82", "44", "42", "84", "81", "162", "841", "1621", "8412", "84111", "84121",
+                                     "4412", "44121", "904", "906", "908", "912", "scalar"])
 @pytest.mark.parametrize("length,periodic,P", VEC_CASES)
 def test_gol_kernel_variants_bit_exact(monkeypatch, variant, length, periodic, P):
     """Every build of the 26-neighbor stencil (tile shapes, scalar fallback)
