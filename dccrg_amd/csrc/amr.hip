@@ -22,6 +22,8 @@
 // Ownership needs no migration: without load balancing every cell stays on
 // the process of its level-0 ancestor (children on the parent's process,
 // :10368; parent on its first child's process, :10437).
+#include <array>
+#include <unordered_map>
 #include <algorithm>
 #include <cstring>
 #include <unordered_set>
@@ -625,45 +627,63 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     }
 
     T.lap("induce_refines");
-    // override_unrefines, dccrg.hpp:9935-10124
+    // override_unrefines, dccrg.hpp:9935-10124.  The reference's walk visits
+    // the closure of u's face neighbors under "face neighbor that is a
+    // neighbor of u's parent" (a non-neighbor is marked processed and never
+    // entered, a fixed property of the cell), and u is dropped if any visited
+    // cell is finer than u or of u's size and about to be refined: an
+    // existence test over that closure, independent of the visiting order.
+    // Requests are independent and only read R, NU and the leaf set, so they
+    // are split over host threads, each with its own memo of the face graph
+    // (siblings' walks cover the same cells).
     std::set<uint64_t> final_un;
-    for (uint64_t u : U) {
-        const uint64_t parent = v.parent(u);
-        uint64_t sib[8];
-        v.children(parent, sib);
-        bool can = true;
-        for (uint64_t s : sib)
-            if (s && (R.count(s) || NU.count(s))) can = false;
-        if (!can) continue;
-        const int ul = v.level(u);
-        std::set<uint64_t> processed, process;
-        uint64_t f6[6];
-        v.face(u, f6);
-        for (uint64_t x : f6)
-            if (x) process.insert(x);
-        while (!process.empty()) {
-            const uint64_t next = *process.begin();
-            processed.insert(next);
-            process.erase(process.begin());
-            v.face(next, f6);
-            for (uint64_t x : f6) {
-                if (!x || processed.count(x)) continue;
-                if (v.is_neighbor(parent, x)) process.insert(x);
-                else processed.insert(x);
-            }
-            const int rl = v.level(next);
-            if (rl < ul) continue;
-            if (rl == ul) {
-                if (R.count(next)) {
-                    can = false;
-                    break;
+    {
+        const std::vector<uint64_t> Uv(U.begin(), U.end());
+        std::vector<uint8_t> keep(Uv.size(), 0);
+        auto work = [&](size_t b, size_t e) {
+            std::unordered_map<uint64_t, std::array<uint64_t, 6>> memo;
+            auto face = [&](uint64_t c) -> const std::array<uint64_t, 6>& {
+                auto it = memo.find(c);
+                if (it != memo.end()) return it->second;
+                std::array<uint64_t, 6> f;
+                v.face(c, f.data());
+                return memo.emplace(c, f).first->second;
+            };
+            std::unordered_set<uint64_t> seen;  // processed or queued
+            std::vector<uint64_t> queue;
+            for (size_t i = b; i < e; i++) {
+                const uint64_t u = Uv[i];
+                const uint64_t parent = v.parent(u);
+                uint64_t sib[8];
+                v.children(parent, sib);
+                bool can = true;
+                for (uint64_t s : sib)
+                    if (s && (R.count(s) || NU.count(s))) can = false;
+                if (!can) continue;
+                const int ul = v.level(u);
+                seen.clear();
+                queue.clear();
+                for (uint64_t x : face(u))
+                    if (x && seen.insert(x).second) queue.push_back(x);
+                for (size_t q = 0; q < queue.size() && can; q++) {
+                    const uint64_t next = queue[q];
+                    const int rl = v.level(next);
+                    if (rl > ul || (rl == ul && R.count(next))) {
+                        can = false;
+                        break;
+                    }
+                    const std::array<uint64_t, 6> f6 = face(next);
+                    for (uint64_t x : f6) {
+                        if (!x || !seen.insert(x).second) continue;
+                        if (v.is_neighbor(parent, x)) queue.push_back(x);
+                    }
                 }
-                continue;
+                keep[i] = can ? 1 : 0;
             }
-            can = false;
-            break;
-        }
-        if (can) final_un.insert(u);
+        };
+        parallel_ranges(Uv.size(), 256, work);
+        for (size_t i = 0; i < Uv.size(); i++)
+            if (keep[i]) final_un.insert(Uv[i]);
     }
 
     T.lap("override_unrefines");

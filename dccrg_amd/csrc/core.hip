@@ -132,6 +132,54 @@ __global__ void __launch_bounds__(256) k_ids_to_indices_v(MapParams p, const uin
     }
 }
 
+// The same with U ids per lane per pass: the U loads of a lane are issued
+// together (k_ids_to_indices_v keeps one 8-B load per lane in flight, which
+// leaves HBM under-subscribed), the 3*256*U triples are staged in LDS and
+// leave as one contiguous run of 16-B non-temporal stores.
+template <int U>
+__global__ void __launch_bounds__(256) k_ids_to_indices_u(MapParams p, const uint64_t* __restrict__ ids,
+                                                          size_t n, uint64_t* __restrict__ idx3,
+                                                          int32_t* __restrict__ lvl)
+{
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    constexpr int B = 256 * U;
+    __shared__ uint64_t s[3 * B];
+    for (size_t base = (size_t)blockIdx.x * B; base < n; base += (size_t)gridDim.x * B) {
+        uint64_t c[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t i = base + k * 256 + threadIdx.x;
+            c[k] = i < n ? __builtin_nontemporal_load(ids + i) : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t i = base + k * 256 + threadIdx.x;
+            uint64_t o[3] = {0, 0, 0};
+            int l = -1;
+            if (i < n) {
+                map_indices(p, c[k], o, &l);
+                if (lvl) __builtin_nontemporal_store(l, lvl + i);
+            }
+            const int j = k * 256 + threadIdx.x;
+            s[3 * j + 0] = o[0];
+            s[3 * j + 1] = o[1];
+            s[3 * j + 2] = o[2];
+        }
+        __syncthreads();
+        const size_t cnt = 3 * (n - base < (size_t)B ? n - base : (size_t)B);
+        if (cnt == 3 * (size_t)B) {
+            u64x2* dst = (u64x2*)(idx3 + 3 * base);
+            for (int k = threadIdx.x; k < 3 * B / 2; k += 256) {
+                const u64x2 v = {s[2 * k], s[2 * k + 1]};
+                __builtin_nontemporal_store(v, dst + k);
+            }
+        } else {
+            for (size_t k = threadIdx.x; k < cnt; k += 256) idx3[3 * base + k] = s[k];
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void __launch_bounds__(256) k_indices_to_ids(MapParams p, const uint64_t* __restrict__ idx3,
                                                         const int32_t* __restrict__ lvl, size_t n,
                                                         uint64_t* __restrict__ ids)
@@ -210,7 +258,20 @@ int dccrgx_map_ids_to_indices(const dccrgx_mapping* map, const uint64_t* ids, si
     DX_TRY(make_map_params(map, &p));
     if (n == 0) return DCCRGX_OK;
     DX_CHECK(ids, DCCRGX_EINVAL, "null ids");
-    if (idx3 && ((uintptr_t)idx3 & 15) == 0)
+    const int64_t mv = getenv_int("DCCRGX_MAP_VARIANT", 2);  // ids per lane per pass (1: k_ids_to_indices_v)
+    if (idx3 && ((uintptr_t)idx3 & 15) == 0 && (mv == 2 || mv == 4 || mv == 8)) {
+        const size_t per = 256 * (size_t)mv;
+        const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>((n + per - 1) / per, 256 * 8));
+        if (mv == 2)
+            hipLaunchKernelGGL(k_ids_to_indices_u<2>, dim3(g), dim3(256), 0, (hipStream_t)stream, p, ids, n, idx3,
+                               lvl);
+        else if (mv == 4)
+            hipLaunchKernelGGL(k_ids_to_indices_u<4>, dim3(g), dim3(256), 0, (hipStream_t)stream, p, ids, n, idx3,
+                               lvl);
+        else
+            hipLaunchKernelGGL(k_ids_to_indices_u<8>, dim3(g), dim3(256), 0, (hipStream_t)stream, p, ids, n, idx3,
+                               lvl);
+    } else if (idx3 && ((uintptr_t)idx3 & 15) == 0)
         hipLaunchKernelGGL(k_ids_to_indices_v, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, ids, n,
                            idx3, lvl);
     else

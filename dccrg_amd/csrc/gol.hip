@@ -949,18 +949,6 @@ static unsigned grid_for(uint64_t n)
     return (unsigned)g;
 }
 
-static bool getenv_flag(const char* name)
-{
-    const char* v = getenv(name);
-    return v && *v && *v != '0';
-}
-
-static int64_t getenv_int(const char* name, int64_t dflt)
-{
-    const char* v = getenv(name);
-    return (v && *v) ? atoll(v) : dflt;
-}
-
 int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out, const Field& cnt,
                int64_t s0, int64_t s1, hipStream_t st)
 {

@@ -11,6 +11,8 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
+#include <algorithm>
 #include <vector>
 
 #include "dccrgx.h"
@@ -71,6 +73,53 @@ struct PhaseTimer {
         t = now;
     }
 };
+
+// variant switches for kernel sweeps (DCCRGX_GOL_VARIANT, DCCRGX_MAP_VARIANT, ...)
+inline bool getenv_flag(const char* name)
+{
+    const char* v = std::getenv(name);
+    return v && *v && *v != '0';
+}
+
+inline int64_t getenv_int(const char* name, int64_t dflt)
+{
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atoll(v) : dflt;
+}
+
+// ---------------------------------------------------------------------------
+// host-side parallel loop for structural work that is independent per item
+// (AMR request filtering): [0, n) in contiguous ranges of at least `grain`
+// items over up to DCCRGX_HOST_THREADS (else OMP_NUM_THREADS, else the
+// hardware's count) threads, capped at 16.  f(begin, end) must only read
+// shared state and write disjoint outputs.
+// ---------------------------------------------------------------------------
+template <class F>
+void parallel_ranges(size_t n, size_t grain, F&& f)
+{
+    size_t nt = 0;
+    for (const char* var : {"DCCRGX_HOST_THREADS", "OMP_NUM_THREADS"}) {
+        const char* e = std::getenv(var);
+        if (e && std::atoi(e) > 0) {
+            nt = (size_t)std::atoi(e);
+            break;
+        }
+    }
+    if (!nt) nt = std::max(1u, std::thread::hardware_concurrency());
+    nt = std::min<size_t>({nt, 16, (n + grain - 1) / std::max<size_t>(grain, 1)});
+    if (nt <= 1) {
+        f((size_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + nt - 1) / nt;
+    for (size_t t = 1; t < nt; t++) {
+        const size_t b = std::min(n, t * per), e = std::min(n, b + per);
+        if (b < e) th.emplace_back([&f, b, e] { f(b, e); });
+    }
+    f((size_t)0, std::min(n, per));
+    for (auto& t : th) t.join();
+}
 
 // ---------------------------------------------------------------------------
 // 64-bit division by an invariant divisor (Granlund-Montgomery, "unsigned

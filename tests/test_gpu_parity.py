@@ -91,6 +91,24 @@ def test_mapping_bit_exact(ctx, length, lvl):
         assert np.array_equal(got[:600], want), op
 
 
+@pytest.mark.parametrize("variant", ["1", "2", "4", "8"])
+@pytest.mark.parametrize("n", [1, 255, 1024, 5000, (1 << 21) + 7])
+def test_mapping_kernel_variants_bit_exact(ctx, monkeypatch, variant, n):
+    """Every build of the batched get_indices kernel (ids per lane per pass),
+    with partial last passes, against the oracle."""
+    monkeypatch.setenv("DCCRGX_MAP_VARIANT", variant)
+    length, lvl = (2048, 2048, 2048), 10
+    om = O.Mapping(length, lvl)
+    dm = D.Mapping(length, lvl)
+    rng = np.random.default_rng(n)
+    ids = rng.integers(0, om.last_cell + 2, size=n, dtype=np.uint64)
+    ref_idx, ref_lvl = om.ids_to_indices(ids)
+    idx, lv = dm.ids_to_indices(torch.from_numpy(ids.view(np.int64)).to(DEV))
+    torch.cuda.synchronize()
+    assert np.array_equal(lv.cpu().numpy(), ref_lvl)
+    assert np.array_equal(idx.cpu().numpy().view(np.uint64), ref_idx)
+
+
 # ------------------------------------------------------- neighbor lists ----
 NBR_CASES = [
     ((10, 10, 1), (False, False, False), 1, 0),
