@@ -58,7 +58,7 @@ def pmc_traffic(kernel: str, cells_per_launch: int):
     WRITE_SIZE in separate passes, gfx950 corrections applied), or None."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=os.path.getmtime):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):  # by round: latest wins
         try:
             s = json.load(open(f))
         except (OSError, ValueError):
@@ -389,7 +389,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "dccrgx::k_gol26v<8, 4, true>",
+            "kernel": "dccrgx::k_gol26v<8, 4, true, 1, false>",
             "kernel_ms_per_step": kern_ms / args.steps,
             "launches_per_step": launches / max(args.steps, 1),
             "bytes_per_cell": BYTES_PER_CELL,
@@ -397,7 +397,7 @@ def main():
         "init_s": t_init,
     }
     if launches == args.steps:  # one stencil launch per step (no remote halo split)
-        t = pmc_traffic("k_gol26v<8, 4, true>", n_local)
+        t = pmc_traffic("k_gol26v<8, 4, true", n_local)
         if t:
             line["roofline"]["traffic"] = t[0]
             line["roofline"]["traffic_source"] = t[1]
