@@ -171,13 +171,17 @@ class Mapping:
 
     def get_all_children(self, cell: int):
         """dccrg_mapping.hpp:392-442: x fastest, then y, z; error_cell x 8
-        for an invalid cell or one at the maximum level."""
+        for error_cell or a cell at the maximum level.  As in the reference,
+        an id beyond the last cell (level -1) is not rejected: its error_index
+        corner wraps in unsigned 64-bit arithmetic."""
         lvl = self.get_refinement_level(cell)
-        if lvl < 0 or lvl >= self.max_ref_lvl:
+        if cell == 0 or lvl >= self.max_ref_lvl:
             return [0] * 8
         i = self.get_indices(cell)
-        h = self.get_cell_length_in_indices(cell) // 2
-        return [self.get_cell_from_indices((i[0] + dx * h, i[1] + dy * h, i[2] + dz * h), lvl + 1)
+        h = 1 << (self.max_ref_lvl - lvl - 1)
+        w = (1 << 64) - 1
+        return [self.get_cell_from_indices(((i[0] + dx * h) & w, (i[1] + dy * h) & w, (i[2] + dz * h) & w),
+                                           lvl + 1)
                 for dz in (0, 1) for dy in (0, 1) for dx in (0, 1)]
 
     def get_siblings(self, cell: int):

@@ -205,13 +205,15 @@ public:
     uint64_t get_parent(uint64_t c) const { return op(DCCRGX_OP_PARENT, c); }
     uint64_t get_level_0_parent(uint64_t c) const { return op(DCCRGX_OP_LEVEL_0_PARENT, c); }
     uint64_t get_child(uint64_t c) const { return op(DCCRGX_OP_CHILD, c); }
-    // dccrg_mapping.hpp:392-442, x fastest then y then z
+    // dccrg_mapping.hpp:392-442, x fastest then y then z.  Like the reference,
+    // an id beyond the last cell (level -1) is not rejected: its error_index
+    // corner wraps in unsigned arithmetic (pinned by tests/golden/ref_mapping.npz)
     std::array<uint64_t, 8> get_all_children(uint64_t cell) const
     {
         std::array<uint64_t, 8> ch;
         ch.fill(error_cell);
         const int l = get_refinement_level(cell);
-        if (cell == error_cell || l < 0 || l >= max_lvl_) return ch;
+        if (cell == error_cell || l >= max_lvl_) return ch;
         const auto idx = get_indices(cell);
         const uint64_t off = uint64_t(1) << (max_lvl_ - l - 1);
         size_t i = 0;
