@@ -287,6 +287,52 @@ def secondary(ctx, torch, D):
     return out
 
 
+def halo_payload(ctx, D, world, barrier, reduce_max):
+    """tests/scalability/scalability.cpp:170-191 on the device: cells carry
+    data_size opaque bytes (its Cell::data, :39-57), each step is
+    start_remote_neighbor_copy_updates, wait receives, wait sends around an
+    empty "solve" (the busy-wait :79-99 has no device meaning).  A z-slab of
+    2048 x 2048 x 8 cells per rank, hood 1, periodic z: at N > 1 the two
+    boundary planes go to the ring neighbours through RCCL over xGMI; at N = 1
+    the rank's own periodic images go through RCCL to itself."""
+    own = None
+    c = ctx
+    if world == 1:
+        own = c = D.Context(ctx.device, 0, 1)
+        own.comm_init(D.Context.unique_id())
+        own.route_self_through_rccl(True)
+    n, depth, steps = 2048, 8, 10
+    rows = []
+    for ds in (1, 8, 72):
+        g = (D.Dccrg().set_initial_length((n, n, depth * world)).set_neighborhood_length(1)
+             .set_maximum_refinement_level(0).set_periodic(False, False, True).initialize(c))
+        g.add_field("data", np.dtype((np.uint8, ds)))
+        ns = g.get_number_of_update_send_cells()
+        nr = g.get_number_of_update_receive_cells()
+        for _ in range(2):
+            g.update_copies_of_remote_neighbors(fields=["data"])
+        c.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.start_remote_neighbor_copy_updates(fields=["data"])
+            g.wait_remote_neighbor_copy_update_receives()
+            g.wait_remote_neighbor_copy_update_sends()
+        c.synchronize()
+        barrier()
+        dt = reduce_max(time.perf_counter() - t0)
+        rows.append({"data_size": ds, "send_cells_per_rank": ns, "receive_cells_per_rank": nr,
+                     "bytes_sent_per_step": ns * ds * world, "ms_per_update": dt * 1e3 / steps,
+                     "GBs_per_rank": ns * ds * steps / dt / 1e9})
+        g.close()
+    if own is not None:
+        own.close()
+    return {"workload": "tests/scalability/scalability.cpp byte payloads, 2048x2048x8 z-slab per rank, hood 1, "
+                        "periodic z, start / wait receives / wait sends, empty solve"
+                        + (" (N = 1: own periodic images through RCCL)" if world == 1 else ", RCCL over xGMI"),
+            "steps": steps, "sizes": rows}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -295,6 +341,7 @@ def main():
     ap.add_argument("--n", type=int, default=2048, help="cells per axis per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the other configs' lines (N = 1)")
+    ap.add_argument("--no-halo-payload", action="store_true", help="skip the byte-payload halo line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -402,6 +449,19 @@ def main():
             line["roofline"]["traffic"] = t[0]
             line["roofline"]["traffic_source"] = t[1]
     grid.close()
+
+    def reduce_max(v: float) -> float:
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    if not args.no_halo_payload:  # collective: every rank
+        try:
+            line["halo_payload"] = halo_payload(ctx, D, world, barrier, reduce_max)
+        except Exception as e:  # the headline line still prints
+            line["halo_payload"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_secondary:
         line["secondary"] = secondary(ctx, torch, D)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

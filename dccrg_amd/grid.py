@@ -502,6 +502,27 @@ class Dccrg:
             out[int(p)] = ids.tolist()
         return out
 
+    def _update_cells(self, send: int, hood: int) -> int:
+        n = C.c_size_t()
+        st = lib().dccrgx_get_peers(self._h, hood, send, None, None, 0, C.byref(n))
+        if st == 7:  # DCCRGX_ENOTFOUND: dccrg.hpp:5454-5456
+            return (1 << 64) - 1
+        if st not in (X.DCCRGX_OK, 5):
+            check(st)
+        counts = np.zeros(n.value, dtype=np.uint64)
+        check(lib().dccrgx_get_peers(self._h, hood, send, None, counts.ctypes.data_as(X._u64p), n.value,
+                                     C.byref(n)))
+        return int(counts.sum())
+
+    def get_number_of_update_send_cells(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> int:
+        """dccrg.hpp:5428-5480: cells sent per update (a cell sent to N
+        processes counts N times); maximum uint64 for an unknown id."""
+        return self._update_cells(1, hood)
+
+    def get_number_of_update_receive_cells(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> int:
+        """dccrg.hpp:5489-5536."""
+        return self._update_cells(0, hood)
+
     def get_cells_to_send(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> Dict[int, List[int]]:
         """dccrg.hpp:7008-7020: per receiving process, ascending cell ids."""
         return self._peer_lists(1, hood)

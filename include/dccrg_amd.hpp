@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <array>
+#include <limits>
 #include <cstdint>
 #include <cstdio>
 #include <map>
@@ -616,14 +617,18 @@ public:
     {
         return hs(default_neighborhood_id).recv_tagged;
     }
+    // dccrg.hpp:5428-5536: a cell sent to N processes counts N times; an
+    // unknown neighborhood id gives the maximum uint64_t
     uint64_t get_number_of_update_send_cells(int hood = default_neighborhood_id) const
     {
+        if (!hoods_.count(hood)) return std::numeric_limits<uint64_t>::max();
         uint64_t n = 0;
         for (auto& kv : hs(hood).send) n += kv.second.size();
         return n;
     }
     uint64_t get_number_of_update_receive_cells(int hood = default_neighborhood_id) const
     {
+        if (!hoods_.count(hood)) return std::numeric_limits<uint64_t>::max();
         uint64_t n = 0;
         for (auto& kv : hs(hood).recv) n += kv.second.size();
         return n;

@@ -166,6 +166,9 @@ def test_rank_structures_match_oracle(length, periodic, hood, P):
         assert g.remote_cells().tolist() == ref["remote"]
         assert g.get_cells_to_send() == ref["send"]
         assert g.get_cells_to_receive() == ref["recv"]
+        assert g.get_number_of_update_send_cells() == sum(len(v) for v in ref["send"].values())
+        assert g.get_number_of_update_receive_cells() == sum(len(v) for v in ref["recv"].values())
+        assert g.get_number_of_update_send_cells(12345) == (1 << 64) - 1  # dccrg.hpp:5454-5456
         g.close()
 
 
