@@ -21,6 +21,7 @@ WAIT_ALL, WAIT_RECEIVES, WAIT_SENDS = 0, 1, 2
 REGION_ALL, REGION_INNER, REGION_OUTER = 0, 1, 2
 OP_LENGTH_IN_INDICES, OP_PARENT, OP_LEVEL_0_PARENT, OP_CHILD = 0, 1, 2, 3
 AMR_REFINE, AMR_DONT_REFINE, AMR_UNREFINE, AMR_DONT_UNREFINE = 0, 1, 2, 3
+GOLH_RECORD, GOLH_SPREAD_APPLY = 1, 2
 
 ERRORS = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "ERCCL", 5: "ERANGE", 6: "ESTATE",
           7: "ENOTFOUND", 8: "EINTERNAL"}
@@ -134,6 +135,8 @@ SIGNATURES = {
     "dccrgx_halo_self": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t]),
     "dccrgx_gol_compute": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "dccrgx_gol_step": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "dccrgx_gol_amr_phase": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32]),
+    "dccrgx_gol_amr_step": (C.c_int, [_vp, C.c_int32, C.c_int32]),
     "dccrgx_field_init_hash": (C.c_int, [_vp, C.c_int32, C.c_uint32]),
     "dccrgx_kernel_timer": (C.c_int, [_vp, C.c_int32, C.POINTER(C.c_double), _u64p]),
     "dccrgx_advect_fluxes": (C.c_int, [_vp, C.c_int32, C.POINTER(AdvectFields_t), C.c_double, C.c_int32]),

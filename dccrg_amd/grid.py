@@ -590,20 +590,25 @@ class Dccrg:
         return self._fields[name][0]
 
     def write_local(self, name: str, values: np.ndarray):
+        """values: one element per local cell, ascending ids; a field whose
+        element is an array (e.g. np.dtype((np.uint64, 9))) takes (n, ...)."""
         fid, dt = self._fields[name]
-        v = np.ascontiguousarray(values, dtype=dt)
-        check(lib().dccrgx_field_write_local(self._h, fid, v.ctypes.data, v.size))
+        base, shape = (dt.base, dt.shape) if dt.subdtype is not None else (dt, ())
+        v = np.ascontiguousarray(values, dtype=base).reshape((-1,) + shape)
+        check(lib().dccrgx_field_write_local(self._h, fid, v.ctypes.data, v.shape[0]))
 
     def read_local(self, name: str) -> np.ndarray:
         fid, dt = self._fields[name]
-        out = np.zeros(self.info.n_local, dtype=dt)
-        check(lib().dccrgx_field_read_local(self._h, fid, out.ctypes.data, out.size))
+        base, shape = (dt.base, dt.shape) if dt.subdtype is not None else (dt, ())
+        out = np.zeros((self.info.n_local,) + shape, dtype=base)
+        check(lib().dccrgx_field_read_local(self._h, fid, out.ctypes.data, self.info.n_local))
         return out
 
     def read_remote(self, name: str, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> np.ndarray:
         fid, dt = self._fields[name]
         n = len(self.remote_cells(hood))
-        out = np.zeros(n, dtype=dt)
+        base, shape = (dt.base, dt.shape) if dt.subdtype is not None else (dt, ())
+        out = np.zeros((n,) + shape, dtype=base)
         check(lib().dccrgx_field_read_remote(self._h, hood, fid, out.ctypes.data, n))
         return out
 
@@ -742,6 +747,15 @@ class Dccrg:
     def gol_step(self, fin: str, fout: str, fcnt: str, hood: int = DEFAULT_NEIGHBORHOOD_ID):
         check(lib().dccrgx_gol_step(self._h, hood, self.field_id(fin), self.field_id(fout),
                                     self.field_id(fcnt)))
+
+    def gol_amr_step(self, field: str, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        """tests/game_of_life/solve.hpp:40-170 get_live_neighbors on a 9 x u64
+        field (cell.hpp:47): record, halo, spread + apply."""
+        check(lib().dccrgx_gol_amr_step(self._h, hood, self.field_id(field)))
+
+    def gol_amr_phase(self, field: str, phase: int, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        """One phase of gol_amr_step (X.GOLH_RECORD / X.GOLH_SPREAD_APPLY)."""
+        check(lib().dccrgx_gol_amr_phase(self._h, hood, self.field_id(field), phase))
 
     # ---- advection, tests/advection/solve.hpp ------------------------------
     ADVECT_FIELDS = ("density", "flux", "vx", "vy", "vz", "length_x", "length_y", "length_z")

@@ -289,6 +289,20 @@ int dccrgx_gol_compute(dccrgx_grid* grid, int32_t hood_id, int32_t f_alive_in,
  * overlap pattern of scalability3d.cpp:122-166); swaps nothing */
 int dccrgx_gol_step(dccrgx_grid* grid, int32_t hood_id, int32_t f_alive_in, int32_t f_alive_out,
                     int32_t f_count);
+/* The AMR-aware game of life of tests/game_of_life/solve.hpp:40-170 (=
+ * solve_optimized.hpp:40-133, "emulating unrefined behaviour" on refined
+ * grids): f_data is the test's Cell::data, 9 x u64 per cell (72-byte
+ * field, tests/game_of_life/cell.hpp:47).  RECORD lists the distinct level-0
+ * parents of live neighbors in data[1..8]; SPREAD_APPLY merges the lists of
+ * cells sharing a level-0 parent, then B3/S23 on the number of parents and
+ * resets the lists.  The step is RECORD, update_copies_of_remote_neighbors
+ * of the field, SPREAD_APPLY (the caller updates the ghosts before, as
+ * game_of_life_test.cpp:378-380 does).  The reference's aborts: more than 8
+ * parents -> DCCRGX_ERANGE, a dead neighbor's parent already recorded ->
+ * DCCRGX_ESTATE. */
+enum { DCCRGX_GOLH_RECORD = 1, DCCRGX_GOLH_SPREAD_APPLY = 2 };
+int dccrgx_gol_amr_phase(dccrgx_grid* grid, int32_t hood_id, int32_t f_data, int32_t phase);
+int dccrgx_gol_amr_step(dccrgx_grid* grid, int32_t hood_id, int32_t f_data);
 /* synthetic initial state of a 4-byte field on local cells: 1 where
  * splitmix64(id) % 1000 < permille, else 0 (replaces the rand() loops of
  * tests/game_of_life/scalability3d.cpp:106-114 with an order-independent,

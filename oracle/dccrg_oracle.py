@@ -650,3 +650,96 @@ class PoissonSystem:
         if it < 0:
             raise RuntimeError("dox_poisson_solve failed")
         return sol, int(it), res.value
+
+
+# ---- AMR-aware game of life (tests/game_of_life/solve.hpp) -------------------
+class GolHierarchical:
+    """tests/game_of_life/solve.hpp:40-170 (= solve_optimized.hpp:40-133) on
+    every rank of a block-partitioned grid, restated literally.  A cell is
+    ``Cell::data`` = 9 x u64 (tests/game_of_life/cell.hpp:32-47): data[0] the
+    state, data[1..8] the level-0 parents of live neighbors.  One call of
+    ``get_live_neighbors`` is: (1) every local cell records the distinct
+    level-0 parents of its live neighbors_of entries (own parent skipped, in
+    list order), (2) update_copies_of_remote_neighbors, (3) in ``order`` each
+    local cell merges the lists of neighbors sharing its level-0 parent (the
+    CURRENT lists: earlier merges of this phase are seen, as the reference's
+    sequential loop sees them), (4) B3/S23 on the number of recorded parents
+    and the lists reset to error_cell.  The reference aborts when a list
+    overflows or a dead neighbor's parent is already recorded: raised here.
+    ``halo()`` is the caller's update before each call
+    (game_of_life_test.cpp:378-380)."""
+
+    def __init__(self, grid: "Grid", comm_size: int = 1):
+        self.grid = grid
+        self.P = comm_size
+        self.cells = [int(c) for c in grid.cells()]
+        m = grid.mapping
+        self.par = {c: m.get_level_0_parent(c) for c in self.cells}
+        self.owner = {c: grid.owner(c, comm_size) for c in self.cells}
+        self.nof = {c: [n for n, _ in grid.find_neighbors_of(c)] for c in self.cells}
+        self.data = {c: [0] * 9 for c in self.cells}
+        self.ghost = [dict() for _ in range(comm_size)]
+
+    def halo(self):
+        """update_copies_of_remote_neighbors on every rank."""
+        for c in self.cells:
+            r = self.owner[c]
+            for n in self.nof[c]:
+                if n != ERROR_CELL and self.owner[n] != r:
+                    self.ghost[r][n] = list(self.data[n])
+
+    def _d(self, rank: int, cell: int):
+        return self.data[cell] if self.owner[cell] == rank else self.ghost[rank][cell]
+
+    def get_live_neighbors(self, order: str = "ascending"):
+        for c in self.cells:  # phase 1 (independent per cell)
+            r, d = self.owner[c], self.data[c]
+            for i in range(1, 9):
+                d[i] = 0
+            for n in self.nof[c]:
+                if n == ERROR_CELL or self.par[n] == self.par[c]:
+                    continue
+                pn = self.par[n]
+                if self._d(r, n)[0] == 0:
+                    if pn in d[1:]:
+                        raise RuntimeError(f"neighbor {n} of cell {c} should not be alive")
+                    continue
+                for i in range(1, 9):
+                    if d[i] == pn:
+                        break
+                    if d[i] == ERROR_CELL:
+                        d[i] = pn
+                        break
+                    if i == 8:
+                        raise OverflowError("No more room in live neighbor list")
+        self.halo()
+        seq = sorted(self.cells, reverse=(order == "descending"))
+        for c in seq:  # phase 2 (sequential per rank; siblings share the rank)
+            r, d = self.owner[c], self.data[c]
+            for n in self.nof[c]:
+                if n == ERROR_CELL or self.par[n] != self.par[c]:
+                    continue
+                nd = self._d(r, n)
+                for i in range(1, 9):
+                    if nd[i] == ERROR_CELL:
+                        break
+                    for j in range(1, 9):
+                        if d[j] == ERROR_CELL:
+                            d[j] = nd[i]
+                            break
+                        if d[j] == nd[i]:
+                            break
+                        if j == 8:
+                            raise OverflowError("No room in live neighbor list")
+        for c in self.cells:  # phase 3
+            d = self.data[c]
+            live = sum(1 for i in range(1, 9) if d[i] != ERROR_CELL)
+            for i in range(1, 9):
+                d[i] = ERROR_CELL
+            if live == 3:
+                d[0] = 1
+            elif live != 2:
+                d[0] = 0
+
+    def alive(self) -> np.ndarray:
+        return np.array([self.data[c][0] for c in self.cells], dtype=np.uint64)
