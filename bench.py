@@ -284,6 +284,79 @@ def secondary(ctx, torch, D):
                                   "grid, max_ref_lvl 10", "value": nid / (ms * 1e-3), "unit": "ids/s",
                       "achieved_GBs": 36 * nid / (ms * 1e-3) / 1e9,
                       "frac": 36 * nid / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_id": 36}
+    del ids
+    out["neighbor_lists"] = neighbor_lists(ctx, D, torch)
+    return out
+
+
+def neighbor_lists(ctx, D, torch):
+    """SURVEY 8(d) 'neighbor build': batched get_neighbors_of (dccrgx_neighbors_of:
+    count pass, scan, fill pass) on the device.  Output bytes = entries x 20 B
+    (u64 id + 3 x i32 offset) + 8 B of row pointer per cell.
+    (a) uniform 1024^3 grid, hood 1, periodic z: the first 2^24 cells
+        (closed-form lists, dccrg.hpp:4375-4716 on a level-0 grid);
+    (b) mixed levels: 128^3 with 5 % of the cells refined once (2.8 M
+        leaves), hood 1: lists of every leaf by the face-graph walk kernel
+        (k_ex_nof), plus the wall time of initialize() for that grid (hash,
+        face graph, lists of every leaf, per-rank lists, stencil rows)."""
+    dev = torch.device("cuda", ctx.device)
+    X = D._capi
+    out = {}
+
+    def query(g, cells, reps):
+        q = cells.numel()
+        row = torch.zeros(q + 1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
+        X.check(D.lib().dccrgx_neighbors_of(g._h, X.DEFAULT_NEIGHBORHOOD_ID, cells.data_ptr(), q, row.data_ptr(),
+                                            None, None, 0, None))
+        total = int(row[-1].item())
+        ids = torch.empty(total, dtype=torch.int64, device=dev)
+        off = torch.empty((total, 3), dtype=torch.int32, device=dev)
+
+        def once():
+            X.check(D.lib().dccrgx_neighbors_of(g._h, X.DEFAULT_NEIGHBORHOOD_ID, cells.data_ptr(), q,
+                                                row.data_ptr(), None, None, 0, None))
+            X.check(D.lib().dccrgx_neighbors_of(g._h, X.DEFAULT_NEIGHBORHOOD_ID, cells.data_ptr(), q,
+                                                row.data_ptr(), ids.data_ptr(), off.data_ptr(), total, None))
+        once()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            once()
+        ctx.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        byt = 20 * total + 8 * (q + 1)
+        del ids, off, row
+        return {"cells": q, "entries": total, "ms": dt * 1e3, "cells_per_s": q / dt, "output_GBs": byt / dt / 1e9}
+
+    n = 1024
+    g = (D.Dccrg().set_initial_length((n, n, n)).set_neighborhood_length(1)
+         .set_maximum_refinement_level(0).set_periodic(False, False, True).initialize(ctx))
+    out["uniform"] = {"workload": "get_neighbors_of of the first 2^24 cells of a 1024^3 grid, hood 1, periodic z",
+                      **query(g, torch.arange(1, (1 << 24) + 1, dtype=torch.int64, device=dev), 5)}
+    g.close()
+
+    L0 = 128
+    n0 = L0 ** 3
+    rng = np.random.default_rng(5)
+    ref = np.sort(rng.choice(np.arange(1, n0 + 1, dtype=np.int64), size=n0 // 20, replace=False))
+    keep = np.setdiff1d(np.arange(1, n0 + 1, dtype=np.int64), ref, assume_unique=True)
+    x, y, z = (ref - 1) % L0, ((ref - 1) // L0) % L0, (ref - 1) // (L0 * L0)
+    kids = [n0 + 1 + (2 * x + dx) + (2 * y + dy) * 2 * L0 + (2 * z + dz) * 4 * L0 * L0
+            for dz in (0, 1) for dy in (0, 1) for dx in (0, 1)]
+    leaves = np.sort(np.concatenate([keep] + kids)).astype(np.uint64)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    g = (D.Dccrg().set_initial_length((L0, L0, L0)).set_neighborhood_length(1)
+         .set_maximum_refinement_level(1).set_periodic(True, True, True).initialize(ctx, leaves=leaves))
+    ctx.synchronize()
+    t_init = time.perf_counter() - t0
+    cells = torch.from_numpy(leaves.view(np.int64)).to(dev)
+    out["mixed_levels"] = {"workload": f"get_neighbors_of of every leaf of a 128^3 grid with 5 % of the cells "
+                                       f"refined once ({leaves.size} leaves), hood 1, periodic",
+                           "initialize_s": t_init, "initialize_leaves_per_s": leaves.size / t_init,
+                           **query(g, cells, 3)}
+    g.close()
     return out
 
 

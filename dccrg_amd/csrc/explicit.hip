@@ -357,13 +357,7 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
         hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(n)), dim3(256), 0, st, v, h.d_of_c, h.K, cells, n, row,
                            (uint64_t*)nullptr, (int32_t*)nullptr, (uint32_t*)nullptr, d_err);
     DX_HIP(hipGetLastError());
-    std::vector<uint64_t> hr(n + 1);
-    DX_HIP(hipMemcpyAsync(hr.data(), row, (n + 1) * 8, hipMemcpyDeviceToHost, st));
-    DX_HIP(hipStreamSynchronize(st));
-    hr[0] = 0;
-    for (size_t i = 0; i < n; i++) hr[i + 1] += hr[i];
-    DX_HIP(hipMemcpyAsync(row, hr.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-    *total = hr[n];
+    DX_TRY(device_scan_rows(row, n, st, total));
     int32_t err = 0;
     DX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));

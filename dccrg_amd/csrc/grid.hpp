@@ -296,6 +296,10 @@ void amr_destroy(dccrgx_grid* grid);
 void load_state_free(dccrgx_grid* grid);
 // switch a uniform grid to the explicit layout (amr.hip)
 int amr_ensure_explicit(dccrgx_grid* grid);
+// device prefix sums (scan.hip): x[0..m) inclusive in place; CSR rows
+// (counts in row[1..n] -> row pointers, row[0] = 0, *total = row[n] if given)
+int device_inclusive_scan(uint64_t* x, uint64_t m, hipStream_t st);
+int device_scan_rows(uint64_t* row, uint64_t n, hipStream_t st, uint64_t* total);
 int launch_gather_ext(const void* src, const uint64_t* idx, uint64_t n, uint32_t elem, void* dst,
                       hipStream_t st);
 int launch_scatter_ext(const void* src, const uint64_t* sidx, const uint64_t* didx, uint64_t n,

@@ -73,22 +73,67 @@ __global__ void __launch_bounds__(256) k_uniform_nbrs(UGeom g, const int32_t* __
     }
 }
 
+// fill pass with coalesced stores: one wave per 64 query cells.  Each lane
+// lists its cell's valid items in LDS at the cell's position in the wave's
+// output run (row[] is already scanned), then the wave writes the run entry
+// by entry, consecutive lanes on consecutive entries.  LDS: 4 B per
+// (cell, item) record + the cells' coordinates.
+__global__ void __launch_bounds__(64) k_uniform_fill(UGeom g, const int32_t* __restrict__ items, int K,
+                                                     const uint64_t* __restrict__ cells, size_t n,
+                                                     const uint64_t* __restrict__ row, uint64_t* __restrict__ ids,
+                                                     int32_t* __restrict__ off3, int32_t sx, int32_t sy, int32_t sz)
+{
+    extern __shared__ uint32_t rec[];  // 64 * K records (lane << 16 | item)
+    __shared__ int64_t abc[3][64];
+    const int lane = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t i = t0 + lane;
+    const uint64_t base = row[t0];
+    const uint64_t end = row[t0 + 64 < n ? t0 + 64 : n];
+    if (i < n) {
+        const uint64_t id = cells[i];
+        if (id >= 1 && id <= g.N) {
+            int64_t a, b, c;
+            ug_decompose(g, id - 1, a, b, c);
+            abc[0][lane] = a;
+            abc[1][lane] = b;
+            abc[2][lane] = c;
+            uint32_t w = (uint32_t)(row[i] - base);
+            for (int k = 0; k < K; k++) {
+                uint64_t nlin;
+                int64_t cu;
+                if (ug_neighbor(g, a, b, c, items + 3 * k, nlin, cu)) rec[w++] = ((uint32_t)lane << 16) | (uint32_t)k;
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t tot = end - base;
+    for (uint64_t e = lane; e < tot; e += 64) {
+        const uint32_t r = rec[e];
+        const int l = (int)(r >> 16), k = (int)(r & 0xffffu);
+        uint64_t nlin;
+        int64_t cu;
+        ug_neighbor(g, abc[0][l], abc[1][l], abc[2][l], items + 3 * k, nlin, cu);
+        ids[base + e] = nlin + 1;
+        if (off3) {
+            int32_t o[3];
+            for (int d = 0; d < 3; d++) o[g.perm[d]] = items[3 * k + d];
+            off3[3 * (base + e) + 0] = o[0] * sx;
+            off3[3 * (base + e) + 1] = o[1] * sy;
+            off3[3 * (base + e) + 2] = o[2] * sz;
+        }
+    }
+}
+
 int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n,
                           uint64_t* row, uint64_t* ids, int32_t* off3, size_t cap, hipStream_t st);
 int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n,
                           uint64_t* row, uint64_t* ids, size_t cap, hipStream_t st);
 
-// exclusive scan of row[1..n] counts in place on the host (API, not hot path)
+// row[1..n] counts -> row pointers, on the device (scan.hip)
 static int scan_rows(uint64_t* row, size_t n, hipStream_t st, uint64_t* total)
 {
-    std::vector<uint64_t> h(n + 1);
-    DX_HIP(hipMemcpyAsync(h.data(), row, (n + 1) * 8, hipMemcpyDeviceToHost, st));
-    DX_HIP(hipStreamSynchronize(st));
-    h[0] = 0;
-    for (size_t i = 0; i < n; i++) h[i + 1] += h[i];
-    DX_HIP(hipMemcpyAsync(row, h.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-    *total = h[n];
-    return DCCRGX_OK;
+    return device_scan_rows(row, n, st, total);
 }
 
 }  // namespace dccrgx
@@ -106,27 +151,36 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
     if (!grid->uniform) return explicit_neighbors_of(grid, *h, cells, n, row, ids, off3, cap, st);
     const UGeom& g = grid->g;
-    int32_t* d_err = nullptr;
-    DX_HIP(hipMalloc(&d_err, 4));
-    DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
-    DX_HIP(hipMemsetAsync(row, 0, 8, st));
+    struct ErrWord {
+        int32_t* p = nullptr;
+        ~ErrWord()
+        {
+            if (p) (void)hipFree(p);
+        }
+    } d_err;
+    DX_HIP(hipMalloc(&d_err.p, 4));
+    DX_HIP(hipMemsetAsync(d_err.p, 0, 4, st));
     const int32_t sc = 1 << grid->map.max_lvl;  // offsets in indices of the finest level
     if (n)
         hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells,
-                           n, row, (uint64_t*)nullptr, (int32_t*)nullptr, d_err, sc, sc, sc);
+                           n, row, (uint64_t*)nullptr, (int32_t*)nullptr, d_err.p, sc, sc, sc);
     DX_HIP(hipGetLastError());
     uint64_t total = 0;
     DX_TRY(scan_rows(row, n, st, &total));
     int32_t err = 0;
-    DX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipMemcpyAsync(&err, d_err.p, 4, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_err);
     DX_CHECK(!err, DCCRGX_ENOTFOUND, "cell outside the grid");
     if (!ids) return DCCRGX_OK;
     DX_CHECK(cap >= total, DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total);
-    if (n)
+    if (n && h->K <= 192) {  // LDS records: 256 B per item (48 KiB at 192)
+        hipLaunchKernelGGL(k_uniform_fill, dim3((unsigned)((n + 63) / 64)), dim3(64), 64 * 4 * h->K, st, g,
+                           h->d_of_c, h->K, cells, n, row, ids, off3, sc, sc, sc);
+    } else if (n) {
         hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells,
-                           n, row, ids, off3, d_err, sc, sc, sc);
+                           n, row, ids, off3, d_err.p, sc, sc, sc);
+        DX_HIP(hipStreamSynchronize(st));  // d_err is freed on return
+    }
     DX_HIP(hipGetLastError());
     return DCCRGX_OK;
 }

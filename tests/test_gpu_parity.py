@@ -154,6 +154,38 @@ RANK_CASES = [
 ]
 
 
+@pytest.mark.parametrize("length,periodic,hood", [
+    ((128, 128, 80), (False, False, False), 1),
+    ((96, 64, 40), (True, False, True), 2),
+    ((3000, 7, 1), (False, True, False), 1),
+    ((40, 30, 20), (True, True, False), 3),   # 342 items: the per-cell fill path
+])
+def test_neighbor_lists_many_cells(length, periodic, hood):
+    """Row pointers of every cell (device scan over many tiles) against the
+    closed-form count, the entries of a random sample against the oracle."""
+    og = O.Grid(length, 0, periodic, hood)
+    g = make_grid(length, periodic, hood, 0)
+    n = int(np.prod(length))
+    cells = np.arange(1, n + 1, dtype=np.uint64)
+    row, ids, off = g.neighbors_of(cells)
+    lin = np.arange(n)
+    pos = [lin % length[0], (lin // length[0]) % length[1], lin // (length[0] * length[1])]
+    cnt = np.ones(n, dtype=np.int64)
+    for d in range(3):
+        valid = np.zeros(n, dtype=np.int64)
+        for o in range(-hood, hood + 1):
+            valid += 1 if periodic[d] else ((pos[d] + o >= 0) & (pos[d] + o < length[d]))
+        cnt *= valid
+    cnt -= 1
+    assert row[0] == 0 and np.array_equal(np.diff(row.astype(np.int64)), cnt)
+    rng = np.random.default_rng(3)
+    for c in rng.choice(cells, size=400, replace=False):
+        i = int(c) - 1
+        got = [(int(ids[k]), tuple(int(v) for v in off[k])) for k in range(int(row[i]), int(row[i + 1]))]
+        assert got == og.find_neighbors_of(int(c)), int(c)
+    g.close()
+
+
 @pytest.mark.parametrize("length,periodic,hood,P", RANK_CASES)
 def test_rank_structures_match_oracle(length, periodic, hood, P):
     og = O.Grid(length, 0, periodic, hood)
