@@ -22,6 +22,7 @@ REGION_ALL, REGION_INNER, REGION_OUTER = 0, 1, 2
 OP_LENGTH_IN_INDICES, OP_PARENT, OP_LEVEL_0_PARENT, OP_CHILD = 0, 1, 2, 3
 AMR_REFINE, AMR_DONT_REFINE, AMR_UNREFINE, AMR_DONT_UNREFINE = 0, 1, 2, 3
 GOLH_RECORD, GOLH_SPREAD_APPLY = 1, 2
+PARTITION_BLOCK, PARTITION_SFC = 0, 1
 
 ERRORS = {1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "ERCCL", 5: "ERANGE", 6: "ESTATE",
           7: "ENOTFOUND", 8: "EINTERNAL"}
@@ -40,7 +41,7 @@ class Mapping_t(C.Structure):
 class GridParams_t(C.Structure):
     _fields_ = [("length", C.c_uint64 * 3), ("max_ref_lvl", C.c_int32),
                 ("neighborhood_length", C.c_uint32), ("periodic", C.c_uint8 * 3),
-                ("reserved", C.c_uint8 * 5)]
+                ("partition", C.c_uint8), ("reserved", C.c_uint8 * 4)]
 
 
 class GridInfo_t(C.Structure):
@@ -135,6 +136,8 @@ SIGNATURES = {
     "dccrgx_halo_self": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t]),
     "dccrgx_gol_compute": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "dccrgx_gol_step": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "dccrgx_sfc_owners": (C.c_int, [_vp, _u64p, C.c_int32, _i32p]),
+    "dccrgx_hilbert_keys_host": (C.c_int, [_u64p, _u64p]),
     "dccrgx_gol_amr_phase": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32]),
     "dccrgx_gol_amr_step": (C.c_int, [_vp, C.c_int32, C.c_int32]),
     "dccrgx_field_init_hash": (C.c_int, [_vp, C.c_int32, C.c_uint32]),

@@ -52,7 +52,7 @@ struct View {
         uint64_t idx[3];
         int l;
         map_indices(g->map, c, idx, &l);
-        return part_owner(E->part, map_cell(g->map, idx, 0));
+        return level0_owner(g, E->part, map_cell(g->map, idx, 0));
     }
     bool local(uint64_t c) const { return owner(c) == g->ctx->rank; }
     uint64_t parent(uint64_t c) const

@@ -460,6 +460,8 @@ int dccrgx_file_read_info(const char* path, uint64_t offset, void* header, size_
 int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* info, dccrgx_grid** out)
 {
     DX_CHECK(ctx && path && info && out, DCCRGX_EINVAL, "null argument");
+    DX_CHECK(info->params.partition == DCCRGX_PARTITION_BLOCK, DCCRGX_EINVAL,
+             "loaded grids are placed by the block partition (the file records no placement)");
     *out = nullptr;
     Fd fd;
     fd.fd = open(path, O_RDONLY);

@@ -405,7 +405,8 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(E->n)), dim3(256), 0, st, E->d_leaves, E->n,
                        (unsigned long long*)E->d_keys, E->d_vals, E->mask);
     DX_HIP(hipGetLastError());
-    // ownership: the process of the level-0 ancestor (no load balancing)
+    // ownership: the process of the level-0 ancestor (no load balancing),
+    // block partition or the grid's SFC table
     E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
     E->owner.resize(E->n);
     for (uint64_t i = 0; i < E->n; i++) {
@@ -413,7 +414,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
         int l;
         map_indices(grid->map, E->leaves[i], idx, &l);
         const uint64_t l0 = l == 0 ? E->leaves[i] : map_cell(grid->map, idx, 0);
-        E->owner[i] = part_owner(E->part, l0);
+        E->owner[i] = level0_owner(grid, E->part, l0);
         if (E->owner[i] == ctx->rank) {
             E->local.push_back(E->leaves[i]);
             E->local_g.push_back((uint32_t)i);

@@ -639,6 +639,18 @@ int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uin
     grid->params.max_ref_lvl = grid->map.max_lvl;
     DX_HIP(hipEventCreate(&grid->t0));
     DX_HIP(hipEventCreate(&grid->t1));
+    DX_CHECK(prm->partition == DCCRGX_PARTITION_BLOCK || prm->partition == DCCRGX_PARTITION_SFC, DCCRGX_EINVAL,
+             "unknown partition %d", (int)prm->partition);
+    std::vector<uint64_t> all_level0;
+    if (prm->partition == DCCRGX_PARTITION_SFC) {
+        DX_TRY(sfc_owners(prm->length, ctx->comm_size, ctx->compute, grid->sfc_owner));
+        if (!leaves) {  // every level-0 cell, on the explicit layout
+            all_level0.resize(grid->map.nlevel0);
+            for (uint64_t i = 0; i < all_level0.size(); i++) all_level0[i] = i + 1;
+            leaves = all_level0.data();
+            n_leaves = all_level0.size();
+        }
+    }
     if (leaves) {
         grid->uniform = false;
         DX_TRY(explicit_create(grid.get(), leaves, n_leaves));

@@ -246,6 +246,8 @@ struct dccrgx_grid {
     dccrgx::Amr* amr = nullptr;
     // grid data file being loaded (checkpoint.hip)
     dccrgx::LoadState* load = nullptr;
+    // SFC placement (params.partition): owner of each level-0 cell, id - 1
+    std::vector<int32_t> sfc_owner;
     // kernel timing (dccrgx_kernel_timer)
     hipEvent_t t0 = nullptr, t1 = nullptr;
     double timed_ms = 0;
@@ -253,6 +255,14 @@ struct dccrgx_grid {
 };
 
 namespace dccrgx {
+// process of a level-0 cell: the SFC table if the grid has one, else the
+// block partition P (dccrg.hpp:8098-8145)
+inline int level0_owner(const dccrgx_grid* g, const Partition& P, uint64_t l0)
+{
+    return g->sfc_owner.empty() ? part_owner(P, l0) : g->sfc_owner[l0 - 1];
+}
+// owner table of the SFC placement (sfc.hip)
+int sfc_owners(const uint64_t length[3], int comm_size, hipStream_t st, std::vector<int32_t>& owner);
 Hood* find_hood(dccrgx_grid* g, int32_t id);
 const Hood* find_hood(const dccrgx_grid* g, int32_t id);
 int build_hood(dccrgx_grid* g, Hood& h);

@@ -255,6 +255,18 @@ class Dccrg:
         self._lb_method = method
         return self
 
+    def set_initial_partition(self, method: str = "block"):
+        """Placement of the level-0 cells at initialize: "block" (contiguous
+        ids, dccrg.hpp:8116-8145) or "sfc" (the same per-process counts
+        along a Hilbert curve computed on the device; the reference's
+        compile-time USE_SFC branch, :8147-8220).  An SFC grid uses the
+        explicit layout."""
+        m = method.lower()
+        if m not in ("block", "sfc"):
+            raise ValueError(f"unknown partition {method!r}")
+        self._partition = X.PARTITION_SFC if m == "sfc" else X.PARTITION_BLOCK
+        return self
+
     def initialize(self, ctx: Context, leaves: Optional[Sequence[int]] = None):
         """dccrg.hpp:485-562.  leaves: existing cells of a mixed-level grid."""
         self.ctx = ctx
@@ -263,6 +275,7 @@ class Dccrg:
         p.max_ref_lvl = self._max_ref_lvl
         p.neighborhood_length = self._hood_length
         p.periodic = (C.c_uint8 * 3)(*[1 if v else 0 for v in self._periodic])
+        p.partition = getattr(self, "_partition", X.PARTITION_BLOCK)
         h = C.c_void_p()
         if leaves is None:
             check(lib().dccrgx_grid_create(ctx._h, C.byref(p), None, 0, C.byref(h)))

@@ -329,6 +329,17 @@ public:
         return *this;
     }
     Dccrg& set_load_balancing_method(const std::string&) { return *this; }
+    // placement of the level-0 cells (create_level_0_cells, dccrg.hpp:8089-8224):
+    // DCCRGX_PARTITION_BLOCK (the default build) or DCCRGX_PARTITION_SFC (what
+    // the reference selects at compile time with USE_SFC, :8147-8220)
+    Dccrg& set_initial_partition(int partition)
+    {
+        if (initialized_) throw std::invalid_argument("set_initial_partition after initialize");
+        if (partition != DCCRGX_PARTITION_BLOCK && partition != DCCRGX_PARTITION_SFC)
+            throw std::invalid_argument("unknown partition");
+        partition_ = (uint8_t)partition;
+        return *this;
+    }
     bool set_geometry(const typename Geometry::Parameters& p) { return geometry.set(p); }
     Dccrg& balance_load(bool = true) { return *this; }  // block partition kept (dccrg.hpp:1048-1062)
 
@@ -344,6 +355,7 @@ public:
         }
         p.max_ref_lvl = mapping.get_maximum_refinement_level();
         p.neighborhood_length = hood_length_;
+        p.partition = partition_;
         detail::check(dccrgx_grid_create(ctx_, &p, nullptr, 0, &grid_), "grid");
         for (uint64_t c : query_cells(default_neighborhood_id, DCCRGX_CELLS_LOCAL)) cell_data_[c];
         initialized_ = true;
@@ -921,6 +933,7 @@ private:
     dccrgx_grid* grid_ = nullptr;
     MPI_Comm comm_ = MPI_COMM_NULL;
     int rank_ = 0, size_ = 1;
+    uint8_t partition_ = DCCRGX_PARTITION_BLOCK;
     unsigned hood_length_ = 1;
     bool initialized_ = false;
 };

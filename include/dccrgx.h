@@ -131,8 +131,21 @@ typedef struct {
     int32_t max_ref_lvl;           /* set_maximum_refinement_level (<0: max possible), :8276 */
     uint32_t neighborhood_length;  /* set_neighborhood_length, :8328 */
     uint8_t periodic[3];           /* set_periodic, :8305 */
-    uint8_t reserved[5];
+    uint8_t partition;             /* DCCRGX_PARTITION_*: placement of the level-0 cells */
+    uint8_t reserved[4];
 } dccrgx_grid_params;
+
+/* Placement of the level-0 cells at initialize (create_level_0_cells,
+ * dccrg.hpp:8089-8224).  BLOCK: contiguous ids (:8116-8145, the reference's
+ * build without USE_SFC).  SFC: the same per-process counts taken along a
+ * space-filling curve (the USE_SFC branch :8147-8220; Hilbert curve computed on
+ * the device, sfc.hip; sfc++'s own curve is not in the reference tree).  An
+ * SFC grid always uses the explicit (replicated leaf list) layout. */
+enum { DCCRGX_PARTITION_BLOCK = 0, DCCRGX_PARTITION_SFC = 1 };
+/* owner of every level-0 cell (index id - 1) under the SFC placement */
+int dccrgx_sfc_owners(dccrgx_ctx* ctx, const uint64_t length[3], int32_t comm_size, int32_t* owner_host);
+/* the Hilbert key of every level-0 cell (index id - 1), host computation */
+int dccrgx_hilbert_keys_host(const uint64_t length[3], uint64_t* keys_out);
 
 typedef struct {
     uint64_t n_local;        /* cells owned by this rank */
@@ -147,7 +160,7 @@ typedef struct {
 /* leaves_host == NULL: every refinement-level-0 cell exists (implicit uniform
  * grid, arbitrarily large).  Otherwise the replicated set of existing leaf
  * cells (mixed refinement levels); each cell is owned by the rank owning its
- * level-0 parent under the block partition. */
+ * level-0 parent under params->partition (block or SFC). */
 int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* params,
                        const uint64_t* leaves_host, size_t n_leaves, dccrgx_grid** out);
 int dccrgx_grid_destroy(dccrgx_grid* grid);

@@ -49,7 +49,10 @@ ERROR_CELL = 0
 
 class AmrOracle:
     def __init__(self, length, max_ref_lvl, periodic=(False, False, False), hood_length=1, comm_size=1,
-                 leaves: Optional[Sequence[int]] = None):
+                 leaves: Optional[Sequence[int]] = None, l0_owner=None):
+        """l0_owner: owner table of the level-0 cells (SFC placement,
+        dccrg_oracle.sfc_owner_table); None = the block partition."""
+        self.l0_owner = l0_owner
         self.length = tuple(int(v) for v in length)
         self.mapping = Mapping(self.length, max_ref_lvl)
         self.M = self.mapping.max_ref_lvl
@@ -72,6 +75,7 @@ class AmrOracle:
     # ---- structure ---------------------------------------------------------
     def _rebuild(self):
         self.grid = Grid(self.length, self.M, self.periodic, self.hood_length, sorted(self.leaves))
+        self.grid.l0_owner = self.l0_owner
         self._nof: Dict[int, List[int]] = {}
         self._nto: Dict[int, List[int]] = {}
         self._bdy = None
@@ -83,7 +87,10 @@ class AmrOracle:
         return c in self.leaves
 
     def owner(self, c: int) -> int:
-        return block_owner(self.N0, self.P, self.mapping.get_level_0_parent(c))
+        l0 = self.mapping.get_level_0_parent(c)
+        if self.l0_owner is not None:
+            return int(self.l0_owner[l0 - 1])
+        return block_owner(self.N0, self.P, l0)
 
     def nof(self, c: int) -> List[int]:
         if c not in self._nof:

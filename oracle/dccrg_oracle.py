@@ -294,9 +294,14 @@ class Grid:
     def owner(self, cell: int, comm_size: int) -> int:
         """Owner of a cell without load balancing: children stay on the process
         of their refinement-level-0 ancestor (dccrg.hpp:8116-8145 + refines in
-        place, no migration under DCCRG_NO_LB)."""
+        place, no migration under DCCRG_NO_LB).  ``self.l0_owner`` (a table
+        from sfc_owner_table) replaces the block partition when set."""
+        l0 = self.mapping.get_level_0_parent(cell)
+        table = getattr(self, "l0_owner", None)
+        if table is not None:
+            return int(table[l0 - 1])
         total = self.length[0] * self.length[1] * self.length[2]
-        return block_owner(total, comm_size, self.mapping.get_level_0_parent(cell))
+        return block_owner(total, comm_size, l0)
 
     def rank_view(self, rank: int, comm_size: int, items_of=None, items_to=None):
         """Everything one rank derives at initialize() time.
@@ -743,3 +748,61 @@ class GolHierarchical:
 
     def alive(self) -> np.ndarray:
         return np.array([self.data[c][0] for c in self.cells], dtype=np.uint64)
+
+
+# ---- space-filling-curve placement (dccrg.hpp:8147-8220, USE_SFC) -----------
+def hilbert_keys(length) -> np.ndarray:
+    """Hilbert index of every level-0 cell (index id - 1): Skilling's
+    axes-to-transpose (AIP Conf. Proc. 707, 2004) with b bits per axis, the
+    smallest power of two >= the longest side, x = X[0]; the transpose is
+    read out most significant bit first, X[0] X[1] X[2] per bit.  Restated
+    independently of sfc.hip (numpy, vectorised over cells)."""
+    L = [int(v) for v in length]
+    n = L[0] * L[1] * L[2]
+    side = max(L)
+    b = 1
+    while (1 << b) < side:
+        b += 1
+    lin = np.arange(n, dtype=np.uint64)
+    X = [lin % np.uint64(L[0]), (lin // np.uint64(L[0])) % np.uint64(L[1]), lin // np.uint64(L[0] * L[1])]
+    M = 1 << (b - 1)
+    Q = M
+    while Q > 1:
+        P = np.uint64(Q - 1)
+        q = np.uint64(Q)
+        for i in range(3):
+            hit = (X[i] & q) != 0
+            t = (X[0] ^ X[i]) & P
+            X[0] = np.where(hit, X[0] ^ P, X[0] ^ t)
+            if i:
+                X[i] = np.where(hit, X[i], X[i] ^ t)
+        Q >>= 1
+    X[1] = X[1] ^ X[0]
+    X[2] = X[2] ^ X[1]
+    t = np.zeros(n, dtype=np.uint64)
+    Q = M
+    while Q > 1:
+        t = np.where((X[2] & np.uint64(Q)) != 0, t ^ np.uint64(Q - 1), t)
+        Q >>= 1
+    X = [x ^ t for x in X]
+    key = np.zeros(n, dtype=np.uint64)
+    for bit in range(b - 1, -1, -1):
+        for i in range(3):
+            key = (key << np.uint64(1)) | ((X[i] >> np.uint64(bit)) & np.uint64(1))
+    return key
+
+
+def sfc_owner_table(length, comm_size: int) -> np.ndarray:
+    """create_level_0_cells with USE_SFC (dccrg.hpp:8147-8220): the cells in
+    curve order get the block partition's per-process counts (:8098-8114)."""
+    key = hilbert_keys(length)
+    order = np.argsort(key, kind="stable")
+    n = key.size
+    cpp = 1 if n < comm_size else (n // comm_size + (1 if n % comm_size else 0))
+    fewer = cpp * comm_size - n
+    pos = np.arange(n, dtype=np.int64)
+    split = fewer * (cpp - 1)
+    owner_of_pos = np.where(pos < split, pos // max(cpp - 1, 1), fewer + (pos - split) // cpp)
+    table = np.empty(n, dtype=np.int32)
+    table[order] = owner_of_pos
+    return table
