@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(256) k_ex_advect_faces(AdvPtrs p, double dt, F
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint32_t q = pos ? pos[i] : (uint32_t)i;
-        const uint32_t c = local_g[q];
+        const uint32_t c = local_g ? local_g[q] : q;  // null: identity (explicit local slots are [0, n_local))
         uint32_t s[6];
         int8_t d[6];
 #pragma unroll
@@ -478,11 +478,11 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
     const uint64_t n = R.n;
     fc->n = n;
     const size_t m = std::max<uint64_t>(n, 1);
-    DX_HIP(hipMalloc(&fc->ell_slot, 6 * m * 4));
-    DX_HIP(hipMalloc(&fc->ell_dir, 6 * m));
-    DX_HIP(hipMalloc(&fc->o_row, (m + 1) * 8));
+    DX_HIP(dx_malloc(&fc->ell_slot, 6 * m * 4));
+    DX_HIP(dx_malloc(&fc->ell_dir, 6 * m));
+    DX_HIP(dx_malloc(&fc->o_row, (m + 1) * 8));
     uint32_t* d_cnt = nullptr;
-    DX_HIP(hipMalloc(&d_cnt, m * 4));
+    DX_HIP(dx_malloc(&d_cnt, m * 4));
     const int M = grid->map.max_lvl;
     if (n)
         hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
@@ -492,13 +492,13 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
     std::vector<uint32_t> cnt(n);
     if (n) DX_HIP(hipMemcpyAsync(cnt.data(), d_cnt, n * 4, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_cnt);
+    dx_free(d_cnt);
     std::vector<uint64_t> row(n + 1, 0);
     for (uint64_t q = 0; q < n; q++) row[q + 1] = row[q] + cnt[q];
     fc->overflow = row[n] > 0;
     DX_HIP(hipMemcpyAsync(fc->o_row, row.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-    DX_HIP(hipMalloc(&fc->o_slot, std::max<uint64_t>(row[n], 1) * 4));
-    DX_HIP(hipMalloc(&fc->o_dir, std::max<uint64_t>(row[n], 1)));
+    DX_HIP(dx_malloc(&fc->o_slot, std::max<uint64_t>(row[n], 1) * 4));
+    DX_HIP(dx_malloc(&fc->o_dir, std::max<uint64_t>(row[n], 1)));
     if (fc->overflow)
         hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
                            R.local_slot, R.level, M, n, fc->ell_slot, fc->ell_dir, (uint32_t*)nullptr, fc->o_row,
@@ -513,7 +513,7 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
 
 FaceCache::~FaceCache()
 {
-    for (void* q : {(void*)ell_slot, (void*)ell_dir, (void*)o_row, (void*)o_slot, (void*)o_dir}) hipFree(q);
+    for (void* q : {(void*)ell_slot, (void*)ell_dir, (void*)o_row, (void*)o_slot, (void*)o_dir}) dx_free(q);
 }
 
 }  // namespace dccrgx
@@ -545,7 +545,9 @@ int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect
         else {
             const FaceCache& F = *hm->faces;
             const FaceView fv{F.n, F.ell_slot, F.ell_dir, F.o_row, F.o_slot, F.o_dir, F.overflow};
-            hipLaunchKernelGGL(k_ex_advect_faces, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, fv, R.local_slot,
+            // explicit grids store local cell q in slot q (explicit.hip): no slot loads
+            hipLaunchKernelGGL(k_ex_advect_faces, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, fv,
+                               (const uint32_t*)nullptr,
                                region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos, R.n);
         }
         DX_HIP(hipGetLastError());
@@ -579,9 +581,9 @@ int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f)
     const uint32_t* slots = nullptr;
     if (grid->uniform) uniform_local_run(grid, &s0, &n);
     else {
-        ExRegion R;
-        DX_TRY(explicit_region(grid, grid->hoods.begin()->second, DCCRGX_REGION_ALL, &R));
-        slots = R.local_slot;
+        // local cell q lives in slot q on explicit grids (explicit.hip)
+        s0 = 0;
+        n = grid->ex->local.size();
     }
     hipLaunchKernelGGL(k_apply_slots, dim3(grid_for(n)), dim3(256), 0, st, (double*)p.rho, p.flux, s0, n, slots);
     DX_HIP(hipGetLastError());
@@ -605,7 +607,7 @@ int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f
         slots = R.local_slot;
     }
     unsigned long long* d = nullptr;
-    DX_HIP(hipMalloc((void**)&d, 8));
+    DX_HIP(dx_malloc((void**)&d, 8));
     const unsigned long long init = 0xffffffffffffffffull;  // above every key
     DX_HIP(hipMemcpyAsync(d, &init, 8, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_max_dt, dim3(std::min<unsigned>(grid_for(n), 1024)), dim3(256), 0, st, p, s0, n, slots, d);
@@ -613,7 +615,7 @@ int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f
     unsigned long long k = 0;
     DX_HIP(hipMemcpyAsync(&k, d, 8, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d);
+    dx_free(d);
     if (k != init) *local_min = dunkey(k);
     return DCCRGX_OK;
 }
@@ -638,10 +640,10 @@ int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_a
     int8_t* d_marks = nullptr;
     double* d_diff = nullptr;
     const uint64_t ns = grid->n_slots;
-    DX_HIP(hipMalloc(&d_max, ns * 8));
-    DX_HIP(hipMalloc(&d_flag, ns));
-    DX_HIP(hipMalloc(&d_marks, n));
-    DX_HIP(hipMalloc(&d_diff, n * 8));
+    DX_HIP(dx_malloc(&d_max, ns * 8));
+    DX_HIP(dx_malloc(&d_flag, ns));
+    DX_HIP(dx_malloc(&d_marks, n));
+    DX_HIP(dx_malloc(&d_diff, n * 8));
     DX_HIP(hipMemsetAsync(d_max, 0, ns * 8, st));  // max_diff = 0 (:62-64)
     DX_HIP(hipMemsetAsync(d_flag, 0, ns, st));
     hipLaunchKernelGGL(k_flag_slots, dim3(grid_for(n)), dim3(256), 0, st, R.local_slot, n, d_flag);
@@ -654,10 +656,10 @@ int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_a
     DX_HIP(hipMemcpyAsync(marks_out, d_marks, n, hipMemcpyDeviceToHost, st));
     if (max_diff_out) DX_HIP(hipMemcpyAsync(max_diff_out, d_diff, n * 8, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_max);
-    hipFree(d_flag);
-    hipFree(d_marks);
-    hipFree(d_diff);
+    dx_free(d_max);
+    dx_free(d_flag);
+    dx_free(d_marks);
+    dx_free(d_diff);
     return DCCRGX_OK;
 }
 
@@ -701,8 +703,8 @@ int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_
     }
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_src = nullptr, *d_dst = nullptr;
-    DX_HIP(hipMalloc(&d_src, src.size() * 8));
-    DX_HIP(hipMalloc(&d_dst, dst.size() * 8));
+    DX_HIP(dx_malloc(&d_src, src.size() * 8));
+    DX_HIP(dx_malloc(&d_dst, dst.size() * 8));
     DX_HIP(hipMemcpyAsync(d_src, src.data(), src.size() * 8, hipMemcpyHostToDevice, st));
     DX_HIP(hipMemcpyAsync(d_dst, dst.data(), dst.size() * 8, hipMemcpyHostToDevice, st));
     int s = DCCRGX_OK;
@@ -715,8 +717,8 @@ int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_
         s = launch_scatter_ext(F.ptr, d_src, d_dst, src.size(), F.elem, F.ptr, st);
     }
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_src);
-    hipFree(d_dst);
+    dx_free(d_src);
+    dx_free(d_dst);
     return s;
 }
 
@@ -748,8 +750,8 @@ int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t
     }
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_par = nullptr, *d_ch = nullptr;
-    DX_HIP(hipMalloc(&d_par, parent.size() * 8));
-    DX_HIP(hipMalloc(&d_ch, children.size() * 8));
+    DX_HIP(dx_malloc(&d_par, parent.size() * 8));
+    DX_HIP(dx_malloc(&d_ch, children.size() * 8));
     DX_HIP(hipMemcpyAsync(d_par, parent.data(), parent.size() * 8, hipMemcpyHostToDevice, st));
     DX_HIP(hipMemcpyAsync(d_ch, children.data(), children.size() * 8, hipMemcpyHostToDevice, st));
     int s = DCCRGX_OK;
@@ -764,8 +766,8 @@ int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t
     }
     DX_HIP(hipGetLastError());
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_par);
-    hipFree(d_ch);
+    dx_free(d_par);
+    dx_free(d_ch);
     return s;
 }
 

@@ -269,7 +269,7 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     }
     std::vector<void*> np(grid->fields.size(), nullptr);
     auto rollback = [&](int code) {
-        for (void* q : np) hipFree(q);
+        for (void* q : np) dx_free(q);
         for (auto& kv : grid->hoods) free_hood(kv.second);
         grid->hoods.swap(old_hoods);
         explicit_free(grid->ex);
@@ -304,10 +304,10 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     // the uniform layout's arithmetic otherwise
     int64_t* d_from = nullptr;
     auto fail = [&](int code) {
-        hipFree(d_from);
+        dx_free(d_from);
         return rollback(code);
     };
-    if (hipMalloc(&d_from, std::max<uint64_t>(ns, 1) * 8) != hipSuccess)
+    if (dx_malloc(&d_from, std::max<uint64_t>(ns, 1) * 8) != hipSuccess)
         return fail(set_error(DCCRGX_ENOMEM, "out of device memory for the rebuild plan"));
     if (!old.uniform && old.ex) {
         const int e = explicit_old_slots(grid, old.ex, d_from, st);
@@ -318,10 +318,25 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
         if (ns && hipMemcpy(d_from, from.data(), ns * 8, hipMemcpyHostToDevice) != hipSuccess)
             return fail(set_error(DCCRGX_EHIP, "uploading the rebuild plan failed"));
     }
+    // new field arrays: a spare of the last rebuild when one is large enough
+    // (an adaptive run rebuilds every step with similar sizes), else a fresh
+    // allocation with 1/8 headroom
+    std::vector<size_t> cap(grid->fields.size(), 0);
     for (size_t i = 0; i < grid->fields.size(); i++) {
         const Field& F = grid->fields[i];
         const size_t bytes = std::max<uint64_t>(ns, 1) * F.elem;
-        if (hipMalloc(&np[i], bytes) != hipSuccess) {
+        auto& sp = grid->spare_bufs;
+        auto it = std::find_if(sp.begin(), sp.end(), [&](const std::pair<void*, size_t>& b) {
+            return b.second >= bytes && b.second <= 2 * bytes;
+        });
+        if (it != sp.end()) {
+            np[i] = it->first;
+            cap[i] = it->second;
+            sp.erase(it);
+            continue;
+        }
+        cap[i] = bytes + bytes / 8;
+        if (dx_malloc(&np[i], cap[i]) != hipSuccess) {
             np[i] = nullptr;
             return fail(set_error(DCCRGX_ENOMEM, "out of device memory for a refined field (%zu bytes)", bytes));
         }
@@ -333,11 +348,15 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
         if (launch_move(F.ptr, d_from, ns, F.elem, np[i], st) != DCCRGX_OK) return fail(DCCRGX_EHIP);
     }
     if (hipStreamSynchronize(st) != hipSuccess) return fail(set_error(DCCRGX_EHIP, "moving field data failed"));
-    hipFree(d_from);
-    // commit
+    dx_free(d_from);
+    // commit; the old arrays become the spares of the next rebuild
+    for (auto& b : grid->spare_bufs) dx_free(b.first);
+    grid->spare_bufs.clear();
     for (size_t i = 0; i < grid->fields.size(); i++) {
-        hipFree(grid->fields[i].ptr);
-        grid->fields[i].ptr = np[i];
+        Field& F = grid->fields[i];
+        if (F.ptr) grid->spare_bufs.emplace_back(F.ptr, F.cap_bytes ? F.cap_bytes : old.n_slots * F.elem);
+        F.ptr = np[i];
+        F.cap_bytes = cap[i];
     }
     for (auto& kv : old_hoods) free_hood(kv.second);
     explicit_free(old.ex);
@@ -473,6 +492,12 @@ int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result
         }
         if (A.to_refine.count(s) || A.not_to_unrefine.count(s)) return DCCRGX_OK;
     }
+    // a sibling already recorded: nothing to add.  The reference tests this
+    // after the parent's neighbors (:2660-2668), but either test failing
+    // returns true without inserting, so testing it first (skipping the
+    // neighbor scan for 7 of 8 siblings) changes no result.
+    for (uint64_t s : sib)
+        if (A.to_unrefine.count(s)) return DCCRGX_OK;
     const uint64_t parent = v.parent(cell);
     const int plvl = v.level(parent);
     std::vector<uint64_t> nb;
@@ -482,8 +507,6 @@ int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result
         if (nl > plvl + 1) return DCCRGX_OK;
         if (nl == plvl + 1 && A.to_refine.count(n)) return DCCRGX_OK;
     }
-    for (uint64_t s : sib)
-        if (A.to_unrefine.count(s)) return DCCRGX_OK;
     A.to_unrefine.insert(cell);
     return DCCRGX_OK;
 }

@@ -174,17 +174,17 @@ struct Staging {
     uint64_t cap = 0;
     ~Staging()
     {
-        hipFree(d);
+        dx_free(d);
         hipHostFree(h);
     }
     int ensure(uint64_t n)
     {
         if (n <= cap) return DCCRGX_OK;
-        hipFree(d);
+        dx_free(d);
         hipHostFree(h);
         d = h = nullptr;
         cap = 0;
-        DX_HIP(hipMalloc(&d, n));
+        DX_HIP(dx_malloc(&d, n));
         DX_HIP(hipHostMalloc(&h, n));
         cap = n;
         return DCCRGX_OK;
@@ -247,13 +247,13 @@ int var_records(const dccrgx_grid* g, const int32_t* f, size_t nf, uint64_t s0, 
         }
         if (segs.empty()) continue;
         VSeg* d = nullptr;
-        DX_HIP(hipMalloc(&d, segs.size() * sizeof(VSeg)));
+        DX_HIP(dx_malloc(&d, segs.size() * sizeof(VSeg)));
         DX_HIP(hipMemcpyAsync(d, segs.data(), segs.size() * sizeof(VSeg), hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_vsegs, dim3((unsigned)std::min<uint64_t>((segs.size() + 3) / 4, 4096)), dim3(256), 0, st,
                            d, (uint64_t)segs.size(), (char*)F.ptr, dbuf, pack ? 1 : 0);
         DX_HIP(hipGetLastError());
         DX_HIP(hipStreamSynchronize(st));
-        hipFree(d);
+        dx_free(d);
     }
     return DCCRGX_OK;
 }

@@ -405,6 +405,12 @@ int dccrgx_ctx_create(int device, int rank, int comm_size, dccrgx_ctx** out)
     DX_HIP(hipGetDeviceCount(&ndev));
     DX_CHECK(device >= 0 && device < ndev, DCCRGX_EINVAL, "device %d of %d", device, ndev);
     DX_HIP(hipSetDevice(device));
+    {  // keep freed pool memory for reuse (dx_malloc / dx_free)
+        hipMemPool_t pool = nullptr;
+        DX_HIP(hipDeviceGetDefaultMemPool(&pool, device));
+        uint64_t keep = UINT64_MAX;
+        DX_HIP(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
+    }
     auto* c = new dccrgx_ctx();
     c->device = device;
     c->rank = rank;

@@ -339,7 +339,7 @@ template <class T>
 static int upload(const std::vector<T>& v, T** d, hipStream_t st)
 {
     *d = nullptr;
-    DX_HIP(hipMalloc(d, std::max<size_t>(v.size(), 1) * sizeof(T)));
+    DX_HIP(dx_malloc(d, std::max<size_t>(v.size(), 1) * sizeof(T)));
     if (!v.empty()) DX_HIP(hipMemcpyAsync(*d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
     return DCCRGX_OK;
 }
@@ -350,7 +350,7 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
 {
     const ExView v = view(grid);
     int32_t* d_err = nullptr;
-    DX_HIP(hipMalloc(&d_err, 4));
+    DX_HIP(dx_malloc(&d_err, 4));
     DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
     DX_HIP(hipMemsetAsync(row, 0, 8, st));
     if (n)
@@ -362,21 +362,21 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     DX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
     if (err) {
-        hipFree(d_err);
+        dx_free(d_err);
         return set_error(err & 1 ? DCCRGX_ENOTFOUND : DCCRGX_EINTERNAL,
                          err & 1 ? "cell does not exist" : "neighbor more than one level apart");
     }
     if (ids) {
         uint64_t t = std::max<uint64_t>(*total, 1);
-        DX_HIP(hipMalloc(ids, t * 8));
-        DX_HIP(hipMalloc(off, t * 12));
-        DX_HIP(hipMalloc(gidx, t * 4));
+        DX_HIP(dx_malloc(ids, t * 8));
+        DX_HIP(dx_malloc(off, t * 12));
+        DX_HIP(dx_malloc(gidx, t * 4));
         if (n)
             hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(n)), dim3(256), 0, st, v, h.d_of_c, h.K, cells, n, row,
                                *ids, *off, *gidx, d_err);
         DX_HIP(hipGetLastError());
     }
-    hipFree(d_err);
+    dx_free(d_err);
     return DCCRGX_OK;
 }
 
@@ -399,8 +399,8 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     while (cap < 2 * E->n) cap <<= 1;
     E->mask = cap - 1;
     DX_TRY(upload(E->leaves, &E->d_leaves, st));
-    DX_HIP(hipMalloc(&E->d_keys, cap * 8));
-    DX_HIP(hipMalloc(&E->d_vals, cap * 4));
+    DX_HIP(dx_malloc(&E->d_keys, cap * 8));
+    DX_HIP(dx_malloc(&E->d_vals, cap * 4));
     DX_HIP(hipMemsetAsync(E->d_keys, 0, cap * 8, st));
     hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(E->n)), dim3(256), 0, st, E->d_leaves, E->n,
                        (unsigned long long*)E->d_keys, E->d_vals, E->mask);
@@ -409,7 +409,13 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     // block partition or the grid's SFC table
     E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
     E->owner.resize(E->n);
-    for (uint64_t i = 0; i < E->n; i++) {
+    if (ctx->comm_size == 1) {  // one process owns every leaf
+        std::fill(E->owner.begin(), E->owner.end(), 0);
+        E->local = E->leaves;
+        E->local_g.resize(E->n);
+        for (uint64_t i = 0; i < E->n; i++) E->local_g[i] = (uint32_t)i;
+    }
+    for (uint64_t i = 0; ctx->comm_size > 1 && i < E->n; i++) {
         uint64_t idx[3];
         int l;
         map_indices(grid->map, E->leaves[i], idx, &l);
@@ -440,8 +446,8 @@ static int sync_slots(dccrgx_grid* grid)
     Explicit* E = grid->ex;
     hipStream_t st = grid->ctx->compute;
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(E->d_slot_of_g);
-    hipFree(E->d_level);
+    dx_free(E->d_slot_of_g);
+    dx_free(E->d_level);
     E->d_slot_of_g = nullptr;
     E->d_level = nullptr;
     std::vector<uint8_t> level(E->slot_ids.size());
@@ -464,7 +470,7 @@ static int grow_fields(dccrgx_grid* grid, uint64_t old_ns, uint64_t ns)
     for (size_t i = 0; i < grid->fields.size() && s == DCCRGX_OK; i++) {
         const Field& F = grid->fields[i];
         if (F.variable) continue;
-        if (hipMalloc(&np[i], std::max<uint64_t>(ns, 1) * F.elem) != hipSuccess) {
+        if (dx_malloc(&np[i], std::max<uint64_t>(ns, 1) * F.elem) != hipSuccess) {
             np[i] = nullptr;
             s = set_error(DCCRGX_ENOMEM, "out of device memory for %llu ghost slots", (unsigned long long)ns);
             break;
@@ -475,7 +481,7 @@ static int grow_fields(dccrgx_grid* grid, uint64_t old_ns, uint64_t ns)
     }
     if (s == DCCRGX_OK && hipStreamSynchronize(st) != hipSuccess) s = set_error(DCCRGX_EHIP, "growing fields failed");
     if (s != DCCRGX_OK) {
-        for (void* q : np) hipFree(q);
+        for (void* q : np) dx_free(q);
         return s;
     }
     for (size_t i = 0; i < grid->fields.size(); i++) {
@@ -485,8 +491,9 @@ static int grow_fields(dccrgx_grid* grid, uint64_t old_ns, uint64_t ns)
             F.off.resize(ns, F.pool_bytes);
             continue;
         }
-        hipFree(F.ptr);
+        dx_free(F.ptr);
         F.ptr = np[i];
+        F.cap_bytes = 0;  // exact size
     }
     return DCCRGX_OK;
 }
@@ -548,11 +555,11 @@ void explicit_free(Explicit* E)
     if (!E) return;
     for (void* q : {(void*)E->d_leaves, (void*)E->d_keys, (void*)E->d_vals, (void*)E->d_local_g,
                     (void*)E->d_level, (void*)E->d_slot_of_g, (void*)E->d_local_slot})
-        hipFree(q);
+        dx_free(q);
     for (auto& kv : E->hl) {
-        hipFree(kv.second.d_inner_pos);
-        hipFree(kv.second.d_outer_pos);
-        hipFree(kv.second.d_all_pos);
+        dx_free(kv.second.d_inner_pos);
+        dx_free(kv.second.d_outer_pos);
+        dx_free(kv.second.d_all_pos);
     }
     delete E;
 }
@@ -589,14 +596,14 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     const uint64_t N = E->n;
     h.n_rows = N;
     // neighbors_of of every leaf (the reference also builds all of them)
-    DX_HIP(hipMalloc(&h.d_nof_row, (N + 1) * 8));
+    DX_HIP(dx_malloc(&h.d_nof_row, (N + 1) * 8));
     uint64_t tot = 0;
     DX_TRY(nof_device(grid, h, E->d_leaves, N, h.d_nof_row, &h.d_nof_id, &h.d_nof_off, &h.d_nof_g, &tot, st));
     T.lap("neighbors_of");
     // neighbors_to = transpose (rows: leaves)
     uint32_t *d_cnt = nullptr, *d_cur = nullptr, *d_tmp = nullptr, *d_ucnt = nullptr;
-    DX_HIP(hipMalloc(&d_cnt, N * 4));
-    DX_HIP(hipMalloc(&d_cur, N * 4));
+    DX_HIP(dx_malloc(&d_cnt, N * 4));
+    DX_HIP(dx_malloc(&d_cur, N * 4));
     DX_HIP(hipMemsetAsync(d_cnt, 0, N * 4, st));
     DX_HIP(hipMemsetAsync(d_cur, 0, N * 4, st));
     hipLaunchKernelGGL(k_tr_count, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_cnt);
@@ -604,23 +611,23 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     DX_TRY(scan_counts_u32(d_cnt, N, trow, st));
     uint64_t* d_trow = nullptr;
     DX_TRY(upload(trow, &d_trow, st));
-    DX_HIP(hipMalloc(&d_tmp, std::max<uint64_t>(trow[N], 1) * 4));
+    DX_HIP(dx_malloc(&d_tmp, std::max<uint64_t>(trow[N], 1) * 4));
     hipLaunchKernelGGL(k_tr_scatter, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_trow,
                        d_cur, d_tmp);
-    DX_HIP(hipMalloc(&d_ucnt, N * 4));
+    DX_HIP(dx_malloc(&d_ucnt, N * 4));
     hipLaunchKernelGGL(k_sort_unique_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, N, d_tmp, d_ucnt);
     DX_HIP(hipGetLastError());
     std::vector<uint64_t> nto_row;
     DX_TRY(scan_counts_u32(d_ucnt, N, nto_row, st));
     DX_TRY(upload(nto_row, &h.d_nto_row, st));
-    DX_HIP(hipMalloc(&h.d_nto_g, std::max<uint64_t>(nto_row[N], 1) * 4));
+    DX_HIP(dx_malloc(&h.d_nto_g, std::max<uint64_t>(nto_row[N], 1) * 4));
     hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, d_tmp, h.d_nto_row, N, h.d_nto_g);
     DX_HIP(hipGetLastError());
-    hipFree(d_cnt);
-    hipFree(d_cur);
-    hipFree(d_tmp);
-    hipFree(d_ucnt);
-    hipFree(d_trow);
+    dx_free(d_cnt);
+    dx_free(d_cur);
+    dx_free(d_tmp);
+    dx_free(d_ucnt);
+    dx_free(d_trow);
 
     T.lap("neighbors_to");
     // per-rank bookkeeping from the device lists (dccrg.hpp:9131-9234, 8729-8891)
@@ -628,7 +635,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     std::vector<uint64_t> nof_row(N + 1);
     DX_HIP(hipMemcpyAsync(nof_row.data(), h.d_nof_row, (N + 1) * 8, hipMemcpyDeviceToHost, st));
     Explicit::HoodLists& L = E->hl[h.id];
-    for (uint32_t* p : {L.d_inner_pos, L.d_outer_pos, L.d_all_pos}) hipFree(p);
+    for (uint32_t* p : {L.d_inner_pos, L.d_outer_pos, L.d_all_pos}) dx_free(p);
     L = Explicit::HoodLists{};
     L.h_nto_row = nto_row;
     L.h_nto_g.resize(nto_row[N]);
@@ -642,7 +649,11 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     const int me = ctx->rank;
     std::set<uint64_t> remote;
     std::map<int, std::set<uint64_t>> send, recv;
-    for (uint64_t i = 0; i < nl; i++) {
+    if (ctx->comm_size == 1) {  // one process: every cell is inner, nothing remote
+        L.inner_pos.resize(nl);
+        for (uint64_t i = 0; i < nl; i++) L.inner_pos[i] = (uint32_t)i;
+    }
+    for (uint64_t i = 0; ctx->comm_size > 1 && i < nl; i++) {
         const uint32_t r = E->local_g[i];
         bool outer = false;
         for (uint64_t e = nof_row[r]; e < nof_row[r + 1]; e++) {
@@ -679,24 +690,24 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     Pair* d_pairs = nullptr;
     uint32_t* d_pc = nullptr;
     DX_TRY(upload(tmp_row, &d_tmp_row, st));
-    DX_HIP(hipMalloc(&d_pairs, std::max<uint64_t>(tmp_row[nl], 1) * sizeof(Pair)));
-    DX_HIP(hipMalloc(&d_pc, std::max<uint64_t>(nl, 1) * 4));
+    DX_HIP(dx_malloc(&d_pairs, std::max<uint64_t>(tmp_row[nl], 1) * sizeof(Pair)));
+    DX_HIP(dx_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4));
     if (nl)
         hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
                            h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
     std::vector<uint64_t> st_row;
     DX_TRY(scan_counts_u32(d_pc, nl, st_row, st));
     DX_TRY(upload(st_row, &h.d_st_row, st));
-    DX_HIP(hipMalloc(&h.d_st_slot, std::max<uint64_t>(st_row[nl], 1) * 4));
-    DX_HIP(hipMalloc(&h.d_st_off, std::max<uint64_t>(st_row[nl], 1) * 12));
+    DX_HIP(dx_malloc(&h.d_st_slot, std::max<uint64_t>(st_row[nl], 1) * 4));
+    DX_HIP(dx_malloc(&h.d_st_off, std::max<uint64_t>(st_row[nl], 1) * 12));
     if (nl)
         hipLaunchKernelGGL(k_stencil_slots, dim3(grid_for(nl)), dim3(256), 0, st, d_tmp_row, d_pairs, h.d_st_row, nl,
                            E->d_slot_of_g, h.d_st_slot, h.d_st_off);
     DX_HIP(hipGetLastError());
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_tmp_row);
-    hipFree(d_pairs);
-    hipFree(d_pc);
+    dx_free(d_tmp_row);
+    dx_free(d_pairs);
+    dx_free(d_pc);
 
     T.lap("stencil rows");
     // per-peer plans: send from local slots, receive into ghost slots
@@ -809,7 +820,7 @@ int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_
     hipLaunchKernelGGL(k_old_slots, dim3(grid_for(n)), dim3(256), 0, st, v, old->d_slot_of_g, d_ids, n, d_src);
     const hipError_t e = hipGetLastError();
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_ids);
+    dx_free(d_ids);
     DX_HIP(e);
     return DCCRGX_OK;
 }
@@ -853,9 +864,9 @@ int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t
         if (off3) DX_HIP(hipMemcpyAsync(off3, t_off, total * 12, hipMemcpyDeviceToDevice, st));
     }
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(t_ids);
-    hipFree(t_off);
-    hipFree(t_g);
+    dx_free(t_ids);
+    dx_free(t_off);
+    dx_free(t_g);
     return s;
 }
 

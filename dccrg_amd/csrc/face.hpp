@@ -142,7 +142,7 @@ int face_neighbors_launch(const MapParams& mp, const uint8_t periodic[3], const 
     uint64_t g = (n + 255) / 256;
     g = g == 0 ? 1 : (g > 4096 ? 4096 : g);
     int32_t* d_err = nullptr;
-    DX_HIP(hipMalloc(&d_err, 4));
+    DX_HIP(dx_malloc(&d_err, 4));
     DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
     DX_HIP(hipMemsetAsync(row, 0, 8, st));
     if (n)
@@ -155,7 +155,7 @@ int face_neighbors_launch(const MapParams& mp, const uint8_t periodic[3], const 
     DX_HIP(hipMemcpyAsync(h.data(), row, (n + 1) * 8, hipMemcpyDeviceToHost, st));
     DX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
-    if (err) hipFree(d_err);
+    if (err) dx_free(d_err);
     DX_CHECK(!err, DCCRGX_ENOTFOUND, "cell is not an existing leaf");
     h[0] = 0;
     for (size_t i = 0; i < n; i++) h[i + 1] += h[i];
@@ -168,7 +168,7 @@ int face_neighbors_launch(const MapParams& mp, const uint8_t periodic[3], const 
                            (int32_t)periodic[1], (int32_t)periodic[2], exists, cells, n, row, ids, dirs, d_err);
     DX_HIP(hipGetLastError());
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_err);
+    dx_free(d_err);
     return s;
 }
 

@@ -233,8 +233,8 @@ struct Scratch {
     uint32_t* live = nullptr;
     ~Scratch()
     {
-        if (err) (void)hipFree(err);
-        if (live) (void)hipFree(live);
+        if (err) (void)dx_free(err);
+        if (live) (void)dx_free(live);
     }
 };
 
@@ -254,7 +254,7 @@ int golh_phase(dccrgx_grid* grid, const Hood& h, const Field& F, int32_t phase)
 {
     hipStream_t st = grid->ctx->compute;
     Scratch s;
-    DX_HIP(hipMalloc(&s.err, sizeof(int)));
+    DX_HIP(dx_malloc(&s.err, sizeof(int)));
     DX_HIP(hipMemsetAsync(s.err, 0, sizeof(int), st));
     uint64_t* data = (uint64_t*)F.ptr;
     if (grid->uniform) {
@@ -276,7 +276,7 @@ int golh_phase(dccrgx_grid* grid, const Hood& h, const Field& F, int32_t phase)
         if (phase == DCCRGX_GOLH_RECORD) {
             hipLaunchKernelGGL(k_golh_record_x, dim3(blocks_for(x.n)), dim3(256), 0, st, x, data, s.err);
         } else {
-            DX_HIP(hipMalloc(&s.live, x.n * sizeof(uint32_t)));
+            DX_HIP(dx_malloc(&s.live, x.n * sizeof(uint32_t)));
             hipLaunchKernelGGL(k_golh_spread_x, dim3(blocks_for(x.n)), dim3(256), 0, st, x,
                                (const uint64_t*)data, s.live, s.err);
             hipLaunchKernelGGL(k_golh_apply_x, dim3(blocks_for(x.n)), dim3(256), 0, st, x, data,

@@ -84,7 +84,7 @@ static int compact(const std::vector<Iv>& ivs, P pred, std::vector<uint64_t>& ou
         const uint64_t nb = (iv.n + TILE - 1) / TILE;
         uint32_t* d_counts = nullptr;
         uint64_t* d_off = nullptr;
-        DX_HIP(hipMalloc(&d_counts, nb * sizeof(uint32_t)));
+        DX_HIP(dx_malloc(&d_counts, nb * sizeof(uint32_t)));
         hipLaunchKernelGGL(k_compact_count<P>, dim3((unsigned)nb), dim3(CT), 0, st, iv.first, iv.n,
                            pred, d_counts);
         DX_HIP(hipGetLastError());
@@ -99,8 +99,8 @@ static int compact(const std::vector<Iv>& ivs, P pred, std::vector<uint64_t>& ou
         }
         if (tot) {
             uint64_t* d_out = nullptr;
-            DX_HIP(hipMalloc(&d_off, nb * sizeof(uint64_t)));
-            DX_HIP(hipMalloc(&d_out, tot * sizeof(uint64_t)));
+            DX_HIP(dx_malloc(&d_off, nb * sizeof(uint64_t)));
+            DX_HIP(dx_malloc(&d_out, tot * sizeof(uint64_t)));
             DX_HIP(hipMemcpyAsync(d_off, off.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
             hipLaunchKernelGGL(k_compact_fill<P>, dim3((unsigned)nb), dim3(CT), 0, st, iv.first,
                                iv.n, pred, d_off, d_out);
@@ -110,10 +110,10 @@ static int compact(const std::vector<Iv>& ivs, P pred, std::vector<uint64_t>& ou
             DX_HIP(hipMemcpyAsync(out.data() + old, d_out, tot * sizeof(uint64_t),
                                   hipMemcpyDeviceToHost, st));
             DX_HIP(hipStreamSynchronize(st));
-            hipFree(d_out);
-            hipFree(d_off);
+            dx_free(d_out);
+            dx_free(d_off);
         }
-        hipFree(d_counts);
+        dx_free(d_counts);
     }
     return DCCRGX_OK;
 }
@@ -265,23 +265,23 @@ static int upload(const std::vector<T>& v, T** d, hipStream_t st)
 {
     *d = nullptr;
     if (v.empty()) return DCCRGX_OK;
-    DX_HIP(hipMalloc(d, v.size() * sizeof(T)));
+    DX_HIP(dx_malloc(d, v.size() * sizeof(T)));
     DX_HIP(hipMemcpyAsync(*d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
     return DCCRGX_OK;
 }
 
 void free_hood(Hood& h)
 {
-    hipFree(h.d_of_c);
-    hipFree(h.d_to_c);
-    hipFree(h.d_self_dst);
-    hipFree(h.d_self_src);
+    dx_free(h.d_of_c);
+    dx_free(h.d_to_c);
+    dx_free(h.d_self_dst);
+    dx_free(h.d_self_src);
     for (PeerPlan& p : h.peers) {
-        hipFree(p.d_send_slots);
-        hipFree(p.d_unpack_dst);
-        hipFree(p.d_unpack_src);
-        hipFree(p.d_send_buf);
-        hipFree(p.d_recv_buf);
+        dx_free(p.d_send_slots);
+        dx_free(p.d_unpack_dst);
+        dx_free(p.d_unpack_src);
+        dx_free(p.d_send_buf);
+        dx_free(p.d_recv_buf);
     }
     h.d_of_c = h.d_to_c = nullptr;
     h.d_self_dst = h.d_self_src = nullptr;
@@ -289,7 +289,7 @@ void free_hood(Hood& h)
     for (void* p : {(void*)h.d_nof_row, (void*)h.d_nof_id, (void*)h.d_nof_off, (void*)h.d_nof_g,
                     (void*)h.d_nto_row, (void*)h.d_nto_g, (void*)h.d_st_row, (void*)h.d_st_slot,
                     (void*)h.d_st_off})
-        hipFree(p);
+        dx_free(p);
     h.d_st_off = nullptr;
     h.d_nof_row = h.d_nof_id = h.d_nto_row = h.d_st_row = nullptr;
     h.d_nof_off = nullptr;
@@ -462,9 +462,9 @@ int build_hood(dccrgx_grid* grid, Hood& h)
         int8_t* d_kind = nullptr;
         int32_t* d_pidx = nullptr;
         uint64_t* d_val = nullptr;
-        DX_HIP(hipMalloc(&d_kind, n));
-        DX_HIP(hipMalloc(&d_pidx, n * 4));
-        DX_HIP(hipMalloc(&d_val, n * 8));
+        DX_HIP(dx_malloc(&d_kind, n));
+        DX_HIP(dx_malloc(&d_pidx, n * 4));
+        DX_HIP(dx_malloc(&d_val, n * 8));
         hipLaunchKernelGGL(k_pad_plan, dim3(grid_for(n)), dim3(256), 0, st, g, r[0], n, d_recv, d_poff,
                            d_prank, (int)prank.size(), d_kind, d_pidx, d_val);
         DX_HIP(hipGetLastError());
@@ -475,17 +475,17 @@ int build_hood(dccrgx_grid* grid, Hood& h)
         DX_HIP(hipMemcpyAsync(pidx.data(), d_pidx, n * 4, hipMemcpyDeviceToHost, st));
         DX_HIP(hipMemcpyAsync(val.data(), d_val, n * 8, hipMemcpyDeviceToHost, st));
         DX_HIP(hipStreamSynchronize(st));
-        hipFree(d_kind);
-        hipFree(d_pidx);
-        hipFree(d_val);
+        dx_free(d_kind);
+        dx_free(d_pidx);
+        dx_free(d_val);
         for (uint64_t i = 0; i < n; i++) {
             if (kind[i] == 1) self.push_back({r[0] + i, val[i]});
             else if (kind[i] == 2) unpack[pidx[i]].push_back({val[i], r[0] + i});
         }
     }
-    hipFree(d_recv);
-    hipFree(d_poff);
-    hipFree(d_prank);
+    dx_free(d_recv);
+    dx_free(d_poff);
+    dx_free(d_prank);
 
     for (size_t j = 0; j < h.peers.size(); j++) {
         PeerPlan& pp = h.peers[j];
@@ -705,7 +705,8 @@ int dccrgx_grid_destroy(dccrgx_grid* grid)
     hipStreamSynchronize(grid->ctx->compute);
     hipStreamSynchronize(grid->ctx->comm);
     for (auto& kv : grid->hoods) free_hood(kv.second);
-    for (Field& f : grid->fields) hipFree(f.ptr);
+    for (Field& f : grid->fields) dx_free(f.ptr);
+    for (auto& b : grid->spare_bufs) dx_free(b.first);
     if (!grid->uniform) explicit_destroy(grid);
     amr_destroy(grid);
     load_state_free(grid);

@@ -84,6 +84,7 @@ __host__ __device__ inline uint64_t ug_slot(const UGeom& g, int64_t a, int64_t b
 struct Field {
     void* ptr = nullptr;
     uint32_t elem = 0;
+    size_t cap_bytes = 0;  // allocation size when it exceeds n_slots * elem (AMR rebuild), else 0
     // variable-size cell data (tests/variable_data_size): `ptr` is a pool,
     // slot s holds count[s] elements at byte offset off[s] (host mirrors;
     // message sizes are computed from them)
@@ -246,6 +247,8 @@ struct dccrgx_grid {
     dccrgx::Amr* amr = nullptr;
     // grid data file being loaded (checkpoint.hip)
     dccrgx::LoadState* load = nullptr;
+    // device buffers kept for reuse by the next AMR rebuild (ptr, bytes)
+    std::vector<std::pair<void*, size_t>> spare_bufs;
     // SFC placement (params.partition): owner of each level-0 cell, id - 1
     std::vector<int32_t> sfc_owner;
     // kernel timing (dccrgx_kernel_timer)

@@ -130,14 +130,14 @@ static int seg_copy(const std::vector<Seg>& segs, const void* src, void* dst, hi
 {
     if (segs.empty()) return DCCRGX_OK;
     Seg* d = nullptr;
-    DX_HIP(hipMalloc(&d, segs.size() * sizeof(Seg)));
+    DX_HIP(dx_malloc(&d, segs.size() * sizeof(Seg)));
     DX_HIP(hipMemcpyAsync(d, segs.data(), segs.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
     const uint64_t blocks = std::min<uint64_t>((segs.size() + 3) / 4, 4096);
     hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)blocks), dim3(256), 0, st, d, (uint64_t)segs.size(),
                        (const char*)src, (char*)dst);
     DX_HIP(hipGetLastError());
     DX_HIP(hipStreamSynchronize(st));  // variable-size exchanges are not the bandwidth path
-    hipFree(d);
+    dx_free(d);
     return DCCRGX_OK;
 }
 
@@ -174,10 +174,10 @@ static size_t message_bytes(const dccrgx_grid* g, const PeerPlan& p, const int32
 static int ensure(void** p, size_t* have, size_t need)
 {
     if (*have >= need) return DCCRGX_OK;
-    hipFree(*p);
+    dx_free(*p);
     *p = nullptr;
     *have = 0;
-    DX_HIP(hipMalloc(p, need));
+    DX_HIP(dx_malloc(p, need));
     *have = need;
     return DCCRGX_OK;
 }
@@ -367,7 +367,7 @@ int dccrgx_field_create(dccrgx_grid* grid, uint32_t elem, int32_t* fid)
     Field F;
     F.elem = elem;
     const size_t bytes = std::max<uint64_t>(grid->n_slots, 1) * elem;
-    DX_HIP(hipMalloc(&F.ptr, bytes));
+    DX_HIP(dx_malloc(&F.ptr, bytes));
     // ghost slots of cells outside the grid stay zero forever; default-constructed
     // (value-initialised) ghosts as in allocate_copies_of_remote_neighbors, dccrg.hpp:7153-7184
     DX_HIP(hipMemsetAsync(F.ptr, 0, bytes, grid->ctx->compute));
@@ -449,17 +449,17 @@ int dccrgx_field_read_remote(const dccrgx_grid* grid, int32_t hood_id, int32_t f
     uint64_t* d_ids = nullptr;
     int64_t* d_slots = nullptr;
     void* d_out = nullptr;
-    DX_HIP(hipMalloc(&d_ids, n * 8));
-    DX_HIP(hipMalloc(&d_slots, n * 8));
-    DX_HIP(hipMalloc(&d_out, n * F.elem));
+    DX_HIP(dx_malloc(&d_ids, n * 8));
+    DX_HIP(dx_malloc(&d_slots, n * 8));
+    DX_HIP(dx_malloc(&d_out, n * F.elem));
     DX_HIP(hipMemcpyAsync(d_ids, h->remote.data(), n * 8, hipMemcpyHostToDevice, st));
     DX_TRY(dccrgx_slots_of(grid, d_ids, n, d_slots, st));
     DX_TRY(launch_gather(F.ptr, (const uint64_t*)d_slots, n, F.elem, d_out, st));
     DX_HIP(hipMemcpyAsync(host, d_out, n * F.elem, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_ids);
-    hipFree(d_slots);
-    hipFree(d_out);
+    dx_free(d_ids);
+    dx_free(d_slots);
+    dx_free(d_out);
     return DCCRGX_OK;
 }
 
@@ -659,7 +659,7 @@ int dccrgx_field_create_variable(dccrgx_grid* grid, uint32_t elem, int32_t* fid)
     F.count.assign(grid->n_slots, 0);
     F.off.assign(grid->n_slots, 0);
     F.pool_bytes = 0;
-    DX_HIP(hipMalloc(&F.ptr, 16));
+    DX_HIP(dx_malloc(&F.ptr, 16));
     grid->fields.push_back(std::move(F));
     *fid = (int32_t)grid->fields.size() - 1;
     return DCCRGX_OK;
@@ -688,7 +688,7 @@ int dccrgx_field_resize(dccrgx_grid* grid, int32_t fid, const uint64_t* ids, con
     }
     hipStream_t st = grid->ctx->compute;
     void* pool = nullptr;
-    DX_HIP(hipMalloc(&pool, std::max<uint64_t>(tot, 16)));
+    DX_HIP(dx_malloc(&pool, std::max<uint64_t>(tot, 16)));
     DX_HIP(hipMemsetAsync(pool, 0, std::max<uint64_t>(tot, 16), st));  // new elements value-initialised
     std::vector<Seg> keep;
     for (size_t k = 0; k < cnt.size(); k++) {
@@ -697,7 +697,7 @@ int dccrgx_field_resize(dccrgx_grid* grid, int32_t fid, const uint64_t* ids, con
     }
     DX_TRY(seg_copy(keep, F.ptr, pool, st));
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(F.ptr);
+    dx_free(F.ptr);
     F.ptr = pool;
     F.pool_bytes = tot;
     F.count.swap(cnt);
@@ -749,10 +749,10 @@ int dccrgx_field_write_cells(dccrgx_grid* grid, int32_t fid, const uint64_t* ids
     if (!tot) return DCCRGX_OK;
     hipStream_t st = grid->ctx->compute;
     void* d = nullptr;
-    DX_HIP(hipMalloc(&d, tot));
+    DX_HIP(dx_malloc(&d, tot));
     DX_HIP(hipMemcpyAsync(d, data, tot, hipMemcpyHostToDevice, st));
     const int s = seg_copy(segs, d, F.ptr, st);
-    hipFree(d);
+    dx_free(d);
     return s;
 }
 
@@ -771,13 +771,13 @@ int dccrgx_field_read_cells(const dccrgx_grid* grid, int32_t fid, const uint64_t
     if (!tot) return DCCRGX_OK;
     hipStream_t st = grid->ctx->compute;
     void* d = nullptr;
-    DX_HIP(hipMalloc(&d, tot));
+    DX_HIP(dx_malloc(&d, tot));
     int s = seg_copy(segs, F.ptr, d, st);
     if (s == DCCRGX_OK) {
         DX_HIP(hipMemcpyAsync(data, d, tot, hipMemcpyDeviceToHost, st));
         DX_HIP(hipStreamSynchronize(st));
     }
-    hipFree(d);
+    dx_free(d);
     return s;
 }
 

@@ -40,6 +40,27 @@ int set_error(int code, const char* fmt, ...);
                                        #expr, ncclGetErrorString(r_));                   \
     } while (0)
 
+// Device allocations of the library come from the device's default memory
+// pool, which keeps freed memory for reuse (release threshold raised in
+// dccrgx_ctx_create): an adaptive run frees and allocates grid structures
+// every step, and returning them to the driver each time cost tens of ms.
+// dx_free waits for the device first, as hipFree does.
+template <class T>
+inline hipError_t dx_malloc(T** p, size_t bytes)
+{
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(p), bytes ? bytes : 1, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    return e;
+}
+
+inline hipError_t dx_free(void* p)
+{
+    if (!p) return hipSuccess;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipFreeAsync(p, nullptr);
+    return e;
+}
+
 #define DX_TRY(expr)                       \
     do {                                   \
         int s_ = (expr);                   \

@@ -155,10 +155,10 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
         int32_t* p = nullptr;
         ~ErrWord()
         {
-            if (p) (void)hipFree(p);
+            if (p) (void)dx_free(p);
         }
     } d_err;
-    DX_HIP(hipMalloc(&d_err.p, 4));
+    DX_HIP(dx_malloc(&d_err.p, 4));
     DX_HIP(hipMemsetAsync(d_err.p, 0, 4, st));
     const int32_t sc = 1 << grid->map.max_lvl;  // offsets in indices of the finest level
     if (n)
@@ -202,10 +202,10 @@ int dccrgx_face_neighbors_of_host(const dccrgx_grid* grid, const uint64_t* cells
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_cells = nullptr, *d_row = nullptr, *d_ids = nullptr;
     int32_t* d_dirs = nullptr;
-    DX_HIP(hipMalloc(&d_cells, std::max<size_t>(n, 1) * 8));
-    DX_HIP(hipMalloc(&d_row, (n + 1) * 8));
-    DX_HIP(hipMalloc(&d_ids, std::max<size_t>(cap, 1) * 8));
-    DX_HIP(hipMalloc(&d_dirs, std::max<size_t>(cap, 1) * 4));
+    DX_HIP(dx_malloc(&d_cells, std::max<size_t>(n, 1) * 8));
+    DX_HIP(dx_malloc(&d_row, (n + 1) * 8));
+    DX_HIP(dx_malloc(&d_ids, std::max<size_t>(cap, 1) * 8));
+    DX_HIP(dx_malloc(&d_dirs, std::max<size_t>(cap, 1) * 4));
     if (n) DX_HIP(hipMemcpyAsync(d_cells, cells, n * 8, hipMemcpyHostToDevice, st));
     int s = dccrgx_face_neighbors_of(grid, d_cells, n, d_row, ids ? d_ids : nullptr, d_dirs, cap, st);
     if (s == DCCRGX_OK || s == DCCRGX_ERANGE) {
@@ -217,10 +217,10 @@ int dccrgx_face_neighbors_of_host(const dccrgx_grid* grid, const uint64_t* cells
         }
     }
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_cells);
-    hipFree(d_row);
-    hipFree(d_ids);
-    hipFree(d_dirs);
+    dx_free(d_cells);
+    dx_free(d_row);
+    dx_free(d_ids);
+    dx_free(d_dirs);
     return s;
 }
 
@@ -236,16 +236,16 @@ int dccrgx_neighbors_to(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     const UGeom& g = grid->g;
     int32_t* d_err = nullptr;
     uint64_t *d_row = nullptr, *d_ids = nullptr;
-    DX_HIP(hipMalloc(&d_err, 4));
+    DX_HIP(dx_malloc(&d_err, 4));
     DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
-    DX_HIP(hipMalloc(&d_row, (n + 1) * 8));
+    DX_HIP(dx_malloc(&d_row, (n + 1) * 8));
     DX_HIP(hipMemsetAsync(d_row, 0, 8, st));
     if (n)
         hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_to_c, h->K, cells, n,
                            d_row, (uint64_t*)nullptr, (int32_t*)nullptr, d_err, 1, 1, 1);
     uint64_t total = 0;
     DX_TRY(scan_rows(d_row, n, st, &total));
-    DX_HIP(hipMalloc(&d_ids, std::max<uint64_t>(total, 1) * 8));
+    DX_HIP(dx_malloc(&d_ids, std::max<uint64_t>(total, 1) * 8));
     if (n)
         hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_to_c, h->K, cells, n,
                            d_row, d_ids, (int32_t*)nullptr, d_err, 1, 1, 1);
@@ -256,9 +256,9 @@ int dccrgx_neighbors_to(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     if (total) DX_HIP(hipMemcpyAsync(hi.data(), d_ids, total * 8, hipMemcpyDeviceToHost, st));
     DX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_err);
-    hipFree(d_row);
-    hipFree(d_ids);
+    dx_free(d_err);
+    dx_free(d_row);
+    dx_free(d_ids);
     DX_CHECK(!err, DCCRGX_ENOTFOUND, "cell outside the grid");
     std::vector<uint64_t> orow(n + 1, 0), oids;
     oids.reserve(total);
@@ -286,8 +286,8 @@ int dccrgx_neighbors_of_host(const dccrgx_grid* grid, int32_t hood_id, const uin
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_cells = nullptr, *d_row = nullptr, *d_ids = nullptr;
     int32_t* d_off = nullptr;
-    DX_HIP(hipMalloc(&d_cells, std::max<size_t>(n, 1) * 8));
-    DX_HIP(hipMalloc(&d_row, (n + 1) * 8));
+    DX_HIP(dx_malloc(&d_cells, std::max<size_t>(n, 1) * 8));
+    DX_HIP(dx_malloc(&d_row, (n + 1) * 8));
     if (n) DX_HIP(hipMemcpyAsync(d_cells, cells, n * 8, hipMemcpyHostToDevice, st));
     int s = dccrgx_neighbors_of(grid, hood_id, d_cells, n, d_row, nullptr, nullptr, 0, st);
     if (s == DCCRGX_OK) {
@@ -298,8 +298,8 @@ int dccrgx_neighbors_of_host(const dccrgx_grid* grid, int32_t hood_id, const uin
             if (cap < total) {
                 s = set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total);
             } else {
-                DX_HIP(hipMalloc(&d_ids, std::max<uint64_t>(total, 1) * 8));
-                DX_HIP(hipMalloc(&d_off, std::max<uint64_t>(total, 1) * 12));
+                DX_HIP(dx_malloc(&d_ids, std::max<uint64_t>(total, 1) * 8));
+                DX_HIP(dx_malloc(&d_off, std::max<uint64_t>(total, 1) * 12));
                 s = dccrgx_neighbors_of(grid, hood_id, d_cells, n, d_row, d_ids, d_off, total, st);
                 if (s == DCCRGX_OK && total) {
                     DX_HIP(hipMemcpyAsync(ids, d_ids, total * 8, hipMemcpyDeviceToHost, st));
@@ -309,10 +309,10 @@ int dccrgx_neighbors_of_host(const dccrgx_grid* grid, int32_t hood_id, const uin
         }
     }
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_cells);
-    hipFree(d_row);
-    hipFree(d_ids);
-    hipFree(d_off);
+    dx_free(d_cells);
+    dx_free(d_row);
+    dx_free(d_ids);
+    dx_free(d_off);
     return s;
 }
 
@@ -322,8 +322,8 @@ int dccrgx_neighbors_to_host(const dccrgx_grid* grid, int32_t hood_id, const uin
     DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_cells = nullptr, *d_row = nullptr, *d_ids = nullptr;
-    DX_HIP(hipMalloc(&d_cells, std::max<size_t>(n, 1) * 8));
-    DX_HIP(hipMalloc(&d_row, (n + 1) * 8));
+    DX_HIP(dx_malloc(&d_cells, std::max<size_t>(n, 1) * 8));
+    DX_HIP(dx_malloc(&d_row, (n + 1) * 8));
     if (n) DX_HIP(hipMemcpyAsync(d_cells, cells, n * 8, hipMemcpyHostToDevice, st));
     int s = dccrgx_neighbors_to(grid, hood_id, d_cells, n, d_row, nullptr, 0, st);
     if (s == DCCRGX_OK) {
@@ -334,16 +334,16 @@ int dccrgx_neighbors_to_host(const dccrgx_grid* grid, int32_t hood_id, const uin
             if (cap < total) {
                 s = set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total);
             } else {
-                DX_HIP(hipMalloc(&d_ids, std::max<uint64_t>(total, 1) * 8));
+                DX_HIP(dx_malloc(&d_ids, std::max<uint64_t>(total, 1) * 8));
                 s = dccrgx_neighbors_to(grid, hood_id, d_cells, n, d_row, d_ids, total, st);
                 if (s == DCCRGX_OK && total) DX_HIP(hipMemcpyAsync(ids, d_ids, total * 8, hipMemcpyDeviceToHost, st));
             }
         }
     }
     DX_HIP(hipStreamSynchronize(st));
-    hipFree(d_cells);
-    hipFree(d_row);
-    hipFree(d_ids);
+    dx_free(d_cells);
+    dx_free(d_row);
+    dx_free(d_ids);
     return s;
 }
 

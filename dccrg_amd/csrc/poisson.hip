@@ -505,7 +505,7 @@ template <class T>
 int dalloc(T** p, size_t n)
 {
     *p = nullptr;
-    DX_HIP(hipMalloc(p, std::max<size_t>(n, 1) * sizeof(T)));
+    DX_HIP(dx_malloc(p, std::max<size_t>(n, 1) * sizeof(T)));
     return DCCRGX_OK;
 }
 
@@ -529,7 +529,7 @@ struct dccrgx_poisson {
 
     void free_cache()
     {
-        for (void* q : {(void*)d_slot, (void*)d_row, (void*)d_nb, (void*)d_code}) hipFree(q);
+        for (void* q : {(void*)d_slot, (void*)d_row, (void*)d_nb, (void*)d_code}) dx_free(q);
         d_slot = d_row = d_nb = nullptr;
         d_code = nullptr;
         n_info = 0;
@@ -667,9 +667,9 @@ int build_cache(dccrgx_poisson* P, const uint64_t* cells, size_t n, const uint64
             }
             frow[i + 1] = fnb.size();
         }
-        hipFree(d_nb6);
-        hipFree(d_dir6);
-        hipFree(d_cnt);
+        dx_free(d_nb6);
+        dx_free(d_dir6);
+        dx_free(d_cnt);
         DX_TRY(dalloc(&d_fnb, fnb.size()));
         DX_TRY(dalloc(&d_fdir, fdir.size()));
         DX_TRY(dalloc(&d_frel, fdir.size()));
@@ -713,10 +713,10 @@ int build_cache(dccrgx_poisson* P, const uint64_t* cells, size_t n, const uint64
         int32_t err = 0;
         DX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
         DX_HIP(hipStreamSynchronize(st));
-        hipFree(d_cells);
-        hipFree(d_fid);
-        hipFree(d_s);
-        hipFree(d_err);
+        dx_free(d_cells);
+        dx_free(d_fid);
+        dx_free(d_s);
+        dx_free(d_err);
         DX_CHECK(!err, DCCRGX_EINTERNAL, "face neighbor without storage slot");
     }
 
@@ -782,7 +782,7 @@ int build_cache(dccrgx_poisson* P, const uint64_t* cells, size_t n, const uint64
     }
     for (void* q : {(void*)d_cslot, (void*)d_frow, (void*)d_fnb, (void*)d_fdir, (void*)d_frel, (void*)d_cnt,
                     (void*)d_row_all, (void*)d_nb_all, (void*)d_code_all})
-        hipFree(q);
+        dx_free(q);
     if (changed) DX_TRY(dccrgx_field_write_local(g, P->fid[F_TYPE], type.data(), nl));
 
     P->n_info = info_slot.size();
@@ -829,11 +829,11 @@ int dccrgx_poisson_create(dccrgx_grid* grid, const dccrgx_poisson_params* prm, c
     else P->prm = dccrgx_poisson_params{1000, 0, 1e-15, 2.0, 10.0};  // Poisson_Solve(), :147-155
     int s = DCCRGX_OK;
     for (int k = 0; k < F_N && s == DCCRGX_OK; k++) s = dccrgx_field_create(grid, 8, &P->fid[k]);
-    if (s == DCCRGX_OK && hipMalloc(&P->d_state, sizeof(PState)) != hipSuccess) s = DCCRGX_EHIP;
-    if (s == DCCRGX_OK && hipMalloc(&P->d_part, RG * sizeof(double)) != hipSuccess) s = DCCRGX_EHIP;
+    if (s == DCCRGX_OK && dx_malloc(&P->d_state, sizeof(PState)) != hipSuccess) s = DCCRGX_EHIP;
+    if (s == DCCRGX_OK && dx_malloc(&P->d_part, RG * sizeof(double)) != hipSuccess) s = DCCRGX_EHIP;
     if (s != DCCRGX_OK) {
-        hipFree(P->d_state);
-        hipFree(P->d_part);
+        dx_free(P->d_state);
+        dx_free(P->d_part);
         delete P;
         return s;
     }
@@ -845,8 +845,8 @@ int dccrgx_poisson_destroy(dccrgx_poisson* P)
 {
     if (!P) return DCCRGX_OK;
     P->free_cache();
-    hipFree(P->d_state);
-    hipFree(P->d_part);
+    dx_free(P->d_state);
+    dx_free(P->d_part);
     delete P;
     return DCCRGX_OK;
 }

@@ -82,12 +82,12 @@ struct Bufs {
     std::vector<void*> p;
     ~Bufs()
     {
-        for (void* q : p) (void)hipFree(q);
+        for (void* q : p) (void)dx_free(q);
     }
     template <class T> int get(T** out, size_t bytes)
     {
         void* q = nullptr;
-        DX_HIP(hipMalloc(&q, bytes ? bytes : 1));
+        DX_HIP(dx_malloc(&q, bytes ? bytes : 1));
         p.push_back(q);
         *out = (T*)q;
         return DCCRGX_OK;

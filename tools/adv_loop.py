@@ -1,0 +1,33 @@
+"""configs[2]'s solver loop alone (for rocprofv3): tests/advection/2d.cpp's
+pre-refined 400x400x1 grid, then 200 advect_step calls."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import dccrg_amd as D  # noqa: E402
+from dccrg_amd import advection as A  # noqa: E402
+
+ctx = D.Context(0, 0, 1)
+rel, thr, sens, cfl, M = 0.025, 0.25, 0.5, 0.5, 2
+g = (D.Dccrg().set_initial_length((400, 400, 1)).set_maximum_refinement_level(M)
+     .set_periodic(True, True, False).set_neighborhood_length(0).initialize(ctx))
+g.add_advection_fields()
+geom = A.geometry_2d(g)
+A.initialize(g, geom)
+for _ in range(M):
+    A.adapt_grid(g, geom, *A.check_for_adaptation(g, rel / M, thr, sens))
+    A.initialize(g, geom)
+dt = g.max_time_step()
+for _ in range(5):
+    g.advect_step(cfl * dt)
+ctx.synchronize()
+steps = int(os.environ.get("ADV_STEPS", "200"))
+t0 = time.perf_counter()
+for _ in range(steps):
+    g.advect_step(cfl * dt)
+ctx.synchronize()
+el = time.perf_counter() - t0
+print(f"cells {g.n_local} steps {steps} us/step {el / steps * 1e6:.2f}", flush=True)
+g.close()
+ctx.close()

@@ -8,7 +8,10 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
 import dccrg_amd as D  # noqa: E402
+from dccrg_amd import _capi as X  # noqa: E402
 from dccrg_amd import advection as A  # noqa: E402
 
 rel, thr, sens, cfl, M = 0.025, 0.25, 0.5, 0.5, 2
@@ -35,8 +38,25 @@ def loop():
         g.advect_step(cfl * dt)
         ctx.synchronize()
         t2 = time.perf_counter()
-        A.adapt_grid(g, geom, *sets)
+        A.request_adaptation(g, *sets)
+        ta = time.perf_counter()
+        new = g.stop_refining()
+        g.get_removed_cells()
+        ctx.synchronize()
+        tb = time.perf_counter()
+        fd = np.array([g.field_id("density")], dtype=np.int32)
+        X.check(D.lib().dccrgx_amr_copy_from_parents(g._h, fd.ctypes.data_as(X._i32p), fd.size))
+        X.check(D.lib().dccrgx_amr_average_children(g._h, fd.ctypes.data_as(X._i32p), fd.size))
+        g.clear_refined_unrefined_data()
+        ctx.synchronize()
+        tc = time.perf_counter()
+        A._velocities_lengths(g, geom)
+        ctx.synchronize()
+        td = time.perf_counter()
+        g.update_copies_of_remote_neighbors(fields=list(A.ALL))
         t3 = time.perf_counter()
+        print(f"  requests {1e3*(ta-t2):.1f} stop_refining {1e3*(tb-ta):.1f} data {1e3*(tc-tb):.1f} "
+              f"velocities {1e3*(td-tc):.1f} update {1e3*(t3-td):.1f} ms (new {new.size})", flush=True)
         dt = g.max_time_step()
         print(f"cells {g.n_local} check {1e3*(t1-t0):.1f} ms solve {1e3*(t2-t1):.1f} ms adapt {1e3*(t3-t2):.1f} ms",
               flush=True)
