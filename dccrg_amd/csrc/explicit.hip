@@ -847,6 +847,89 @@ int explicit_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, in
     return DCCRGX_OK;
 }
 
+// neighbor gather (dccrgx_gather_neighbors) on explicit grids: the query
+// cells' rows of the neighborhood's device CSR (reference list order), each
+// entry's field element copied from its storage slot
+__global__ void __launch_bounds__(256) k_ex_gather_count(ExView v, const uint64_t* __restrict__ cells, size_t n,
+                                                         const uint64_t* __restrict__ nof_row,
+                                                         const uint32_t* __restrict__ slot_of_g, uint64_t n_local,
+                                                         uint32_t* __restrict__ gidx, uint64_t* __restrict__ row,
+                                                         int32_t* __restrict__ err)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t g = ex_find(v, cells[i]);
+        if (g < 0 || slot_of_g[g] >= n_local) {  // not a local cell of this rank
+            atomicOr(err, 1);
+            row[i + 1] = 0;
+            gidx[i] = 0;
+            continue;
+        }
+        gidx[i] = (uint32_t)g;
+        row[i + 1] = nof_row[g + 1] - nof_row[g];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ex_gather_fill(const uint32_t* __restrict__ gidx, size_t n,
+                                                        const uint64_t* __restrict__ nof_row,
+                                                        const uint32_t* __restrict__ nof_g,
+                                                        const uint32_t* __restrict__ slot_of_g,
+                                                        const uint64_t* __restrict__ row, const uint8_t* __restrict__ field,
+                                                        uint32_t elem, uint8_t* __restrict__ out)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t g = gidx[i];
+        uint64_t w = row[i];
+        for (uint64_t e = nof_row[g]; e < nof_row[g + 1]; e++, w++) {
+            const uint8_t* src = field + (uint64_t)slot_of_g[nof_g[e]] * elem;
+            uint8_t* dst = out + w * elem;
+            if (elem % 4 == 0)
+                for (uint32_t k = 0; k < elem; k += 4)
+                    *reinterpret_cast<uint32_t*>(dst + k) = *reinterpret_cast<const uint32_t*>(src + k);
+            else
+                for (uint32_t k = 0; k < elem; k++) dst[k] = src[k];
+        }
+    }
+}
+
+int explicit_gather_neighbors(const dccrgx_grid* grid, const Hood& h, const Field& F, const uint64_t* cells, size_t n,
+                              uint64_t* row, void* out, size_t cap_bytes, hipStream_t st)
+{
+    const Explicit* E = grid->ex;
+    DX_CHECK(h.d_nof_row, DCCRGX_EINTERNAL, "no device lists for neighborhood %d", h.id);
+    uint32_t* gidx = nullptr;
+    int32_t* d_err = nullptr;
+    DX_HIP(dx_malloc(&gidx, std::max<size_t>(n, 1) * 4));
+    DX_HIP(dx_malloc(&d_err, 4));
+    auto done = [&](int code) {
+        (void)dx_free(gidx);
+        (void)dx_free(d_err);
+        return code;
+    };
+    if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
+    if (n)
+        hipLaunchKernelGGL(k_ex_gather_count, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nof_row,
+                           E->d_slot_of_g, (uint64_t)E->local.size(), gidx, row, d_err);
+    uint64_t total = 0;
+    int s = device_scan_rows(row, n, st, &total);
+    if (s != DCCRGX_OK) return done(s);
+    int32_t err = 0;
+    if (hipMemcpy(&err, d_err, 4, hipMemcpyDeviceToHost) != hipSuccess) return done(set_error(DCCRGX_EHIP, "copy"));
+    if (err) return done(set_error(DCCRGX_ENOTFOUND, "a query cell is not a local cell of this rank"));
+    if (!out) return done(DCCRGX_OK);
+    if (cap_bytes < total * F.elem)
+        return done(set_error(DCCRGX_ERANGE, "capacity %zu < %llu bytes", cap_bytes,
+                              (unsigned long long)(total * F.elem)));
+    if (n)
+        hipLaunchKernelGGL(k_ex_gather_fill, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)gidx, n,
+                           h.d_nof_row, h.d_nof_g, E->d_slot_of_g, (const uint64_t*)row, (const uint8_t*)F.ptr, F.elem,
+                           (uint8_t*)out);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        return done(set_error(DCCRGX_EHIP, "gather kernel failed"));
+    return done(DCCRGX_OK);
+}
+
 int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n, uint64_t* row,
                           uint64_t* ids, int32_t* off3, size_t cap, hipStream_t st)
 {

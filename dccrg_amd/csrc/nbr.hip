@@ -125,6 +125,81 @@ __global__ void __launch_bounds__(64) k_uniform_fill(UGeom g, const int32_t* __r
     }
 }
 
+// neighbor gather on uniform grids: the field element of every neighbors_of
+// entry of the query cells, laid out like dccrgx_neighbors_of's ids (one wave
+// per 64 cells, LDS records, consecutive lanes on consecutive entries).
+__global__ void __launch_bounds__(64) k_uniform_gather(UGeom g, const int32_t* __restrict__ items, int K,
+                                                       const uint64_t* __restrict__ cells, size_t n,
+                                                       const uint64_t* __restrict__ row,
+                                                       const uint8_t* __restrict__ field, uint32_t elem,
+                                                       uint8_t* __restrict__ out)
+{
+    extern __shared__ uint32_t rec[];
+    __shared__ int64_t abc[3][64];
+    const int lane = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t i = t0 + lane;
+    const uint64_t base = row[t0];
+    const uint64_t end = row[t0 + 64 < n ? t0 + 64 : n];
+    if (i < n) {
+        const uint64_t id = cells[i];
+        if (id >= 1 && id <= g.N) {
+            int64_t a, b, c;
+            ug_decompose(g, id - 1, a, b, c);
+            abc[0][lane] = a;
+            abc[1][lane] = b;
+            abc[2][lane] = c;
+            uint32_t w = (uint32_t)(row[i] - base);
+            for (int k = 0; k < K; k++) {
+                uint64_t nlin;
+                int64_t cu;
+                if (ug_neighbor(g, a, b, c, items + 3 * k, nlin, cu)) rec[w++] = ((uint32_t)lane << 16) | (uint32_t)k;
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t tot = end - base;
+    for (uint64_t e = lane; e < tot; e += 64) {
+        const uint32_t r = rec[e];
+        const int l = (int)(r >> 16), k = (int)(r & 0xffffu);
+        uint64_t nlin;
+        int64_t cu;
+        ug_neighbor(g, abc[0][l], abc[1][l], abc[2][l], items + 3 * k, nlin, cu);
+        // a local neighbor (also one reached through a periodic wrap) is read
+        // from its own slot, as the reference reads the cell itself; a remote
+        // one from its ghost slot (unwrapped c)
+        const int64_t cw = ug_wrap(cu, (int64_t)g.LC);
+        const int64_t cs = ug_local(g, nlin) ? cw : cu;
+        const uint64_t slot = nlin - (uint64_t)cw * g.S + (uint64_t)(cs - g.cbase) * g.S;
+        const uint8_t* src = field + slot * elem;
+        uint8_t* dst = out + (base + e) * elem;
+        if (elem == 4) {
+            *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(src);
+        } else if (elem == 8) {
+            *reinterpret_cast<uint64_t*>(dst) = *reinterpret_cast<const uint64_t*>(src);
+        } else if (elem % 4 == 0) {
+            for (uint32_t q = 0; q < elem; q += 4)
+                *reinterpret_cast<uint32_t*>(dst + q) = *reinterpret_cast<const uint32_t*>(src + q);
+        } else {
+            for (uint32_t q = 0; q < elem; q++) dst[q] = src[q];
+        }
+    }
+}
+
+int explicit_gather_neighbors(const dccrgx_grid* grid, const Hood& h, const Field& F, const uint64_t* cells, size_t n,
+                              uint64_t* row, void* out, size_t cap_bytes, hipStream_t st);
+
+// query cells must be local (lin in [lo, hi))
+__global__ void __launch_bounds__(256) k_check_local(UGeom g, const uint64_t* __restrict__ cells, size_t n,
+                                                     int32_t* __restrict__ err)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t id = cells[i];
+        if (id < 1 || id - 1 < g.lo || id - 1 >= g.hi) atomicOr(err, 1);
+    }
+}
+
 int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n,
                           uint64_t* row, uint64_t* ids, int32_t* off3, size_t cap, hipStream_t st);
 int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n,
@@ -181,6 +256,51 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
                            n, row, ids, off3, d_err.p, sc, sc, sc);
         DX_HIP(hipStreamSynchronize(st));  // d_err is freed on return
     }
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+int dccrgx_gather_neighbors(const dccrgx_grid* grid, int32_t hood_id, int32_t field_id, const uint64_t* cells,
+                            size_t n, uint64_t* row, void* out, size_t cap_bytes, void* stream)
+{
+    DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    const Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    DX_CHECK(field_id >= 0 && (size_t)field_id < grid->fields.size(), DCCRGX_EINVAL, "bad field %d", field_id);
+    const Field& F = grid->fields[field_id];
+    DX_CHECK(!F.variable, DCCRGX_EINVAL, "variable-size field: use dccrgx_field_read_cells");
+    hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
+    if (!grid->uniform) return explicit_gather_neighbors(grid, *h, F, cells, n, row, out, cap_bytes, st);
+    const UGeom& g = grid->g;
+    struct ErrWord {
+        int32_t* p = nullptr;
+        ~ErrWord()
+        {
+            if (p) (void)dx_free(p);
+        }
+    } d_err;
+    DX_HIP(dx_malloc(&d_err.p, 4));
+    DX_HIP(hipMemsetAsync(d_err.p, 0, 4, st));
+    if (n) {
+        hipLaunchKernelGGL(k_check_local, dim3(grid_for(n)), dim3(256), 0, st, g, cells, n, d_err.p);
+        hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells, n, row,
+                           (uint64_t*)nullptr, (int32_t*)nullptr, d_err.p, 1, 1, 1);
+    }
+    DX_HIP(hipGetLastError());
+    uint64_t total = 0;
+    DX_TRY(scan_rows(row, n, st, &total));
+    int32_t err = 0;
+    DX_HIP(hipMemcpyAsync(&err, d_err.p, 4, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    DX_CHECK(!err, DCCRGX_ENOTFOUND, "a query cell is not a local cell of this rank");
+    if (!out) return DCCRGX_OK;
+    DX_CHECK(cap_bytes >= total * F.elem, DCCRGX_ERANGE, "capacity %zu < %llu bytes", cap_bytes,
+             (unsigned long long)(total * F.elem));
+    DX_CHECK(h->K <= 192, DCCRGX_EINVAL, "neighborhoods of more than 192 items are not gathered");
+    if (n)
+        hipLaunchKernelGGL(k_uniform_gather, dim3((unsigned)((n + 63) / 64)), dim3(64), 64 * 4 * h->K, st, g,
+                           h->d_of_c, h->K, cells, n, (const uint64_t*)row, (const uint8_t*)F.ptr, F.elem,
+                           (uint8_t*)out);
     DX_HIP(hipGetLastError());
     return DCCRGX_OK;
 }

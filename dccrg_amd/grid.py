@@ -436,6 +436,28 @@ class Dccrg:
         return (row.cpu().numpy().astype(np.uint64), ids[:total].cpu().numpy().view(np.uint64),
                 off[:total].cpu().numpy())
 
+    def gather_neighbors(self, name: str, cells=None, hood: int = DEFAULT_NEIGHBORHOOD_ID):
+        """Neighbor gather for user stencils (dccrgx_gather_neighbors): for
+        local cells (default: all, ascending), torch tensors (row_ptr,
+        values) with values[row[i]:row[i+1]] = the field element of each
+        get_neighbors_of(cells[i]) entry, in list order (ghosts from their
+        copies)."""
+        import torch
+        dev = torch.device("cuda", self.ctx.device)
+        fid, dt = self._fields[name]
+        c = self.local_cells() if cells is None else cells
+        ct = torch.from_numpy(_u64(c).view(np.int64)).to(dev)
+        n = ct.numel()
+        row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
+        check(lib().dccrgx_gather_neighbors(self._h, hood, fid, ct.data_ptr(), n, row.data_ptr(), None, 0, None))
+        total = int(row[-1].item())
+        out = torch.zeros(max(total, 1) * dt.itemsize, dtype=torch.uint8, device=dev)
+        check(lib().dccrgx_gather_neighbors(self._h, hood, fid, ct.data_ptr(), n, row.data_ptr(), out.data_ptr(),
+                                            out.numel(), None))
+        self.ctx.synchronize()
+        return row, out[:total * dt.itemsize]
+
     def neighbors_to(self, cells: np.ndarray, hood: int = DEFAULT_NEIGHBORHOOD_ID):
         import torch
         dev = torch.device("cuda", self.ctx.device)

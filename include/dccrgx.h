@@ -185,6 +185,14 @@ int dccrgx_get_cells(const dccrgx_grid* grid, int32_t hood_id, int32_t which, ui
 int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t* cells_dev,
                         size_t n, uint64_t* row_ptr_dev, uint64_t* ids_dev, int32_t* off3_dev,
                         size_t cap, void* stream);
+/* Neighbor gather for user stencils (the iteration cache's neighbor data,
+ * Neighbors_Item::data, dccrg.hpp:7404-7456, in get_neighbors_of order): for
+ * n LOCAL cells, row pointers as dccrgx_neighbors_of and the element of
+ * field_id of every neighbors_of entry, elem bytes each, ghosts read from
+ * their copies (update them first).  out == NULL: rows only.
+ * DCCRGX_ENOTFOUND if a cell is not local. */
+int dccrgx_gather_neighbors(const dccrgx_grid* grid, int32_t hood_id, int32_t field_id, const uint64_t* cells_dev,
+                            size_t n, uint64_t* row_ptr_dev, void* out_dev, size_t cap_bytes, void* stream);
 /* Dccrg::get_face_neighbors_of (dccrg.hpp:2828-2955) for n cells: the face
  * graph (update_neighbors_, :9463-9597) neighbor in -x,+x,-y,+y,-z,+z order
  * plus, for a smaller neighbor, its 3 siblings sharing the face; dirs_dev
