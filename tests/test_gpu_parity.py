@@ -186,6 +186,58 @@ def test_neighbor_lists_many_cells(length, periodic, hood):
     g.close()
 
 
+def block_owner_np(total, P, ids):
+    """dccrg.hpp:8098-8145 vectorised (the oracle's block_owner)."""
+    cpp = 1 if total < P else total // P + (1 if total % P else 0)
+    fewer = cpp * P - total
+    i = ids.astype(np.int64) - 1
+    split = fewer * (cpp - 1)
+    return np.where(i < split, i // max(cpp - 1, 1), fewer + (i - split) // cpp)
+
+
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("periodic", [(False, False, False), (True, False, True)])
+def test_rank_lists_100_cubed(P, periodic):
+    """every rank's per-peer send / receive lists of the
+    100^3 block partition (slabs that end mid-plane), hood 1, against a
+    vectorised restatement of dccrg.hpp:8729-8891 (uniform hood 1 is
+    symmetric, so neighbors_to = neighbors_of as sets)."""
+    L = (100, 100, 100)
+    n = int(np.prod(L))
+    ids = np.arange(1, n + 1, dtype=np.int64)
+    x, y, z = (ids - 1) % L[0], ((ids - 1) // L[0]) % L[1], (ids - 1) // (L[0] * L[1])
+    own = block_owner_np(n, P, ids)
+    pairs = []
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                if not (dx or dy or dz):
+                    continue
+                c = [x + dx, y + dy, z + dz]
+                ok = np.ones(n, dtype=bool)
+                for d in range(3):
+                    if periodic[d]:
+                        c[d] = c[d] % L[d]
+                    else:
+                        ok &= (c[d] >= 0) & (c[d] < L[d])
+                nid = c[0] + L[0] * (c[1] + L[1] * c[2]) + 1
+                pairs.append((ids[ok], nid[ok]))
+    cell = np.concatenate([p[0] for p in pairs])
+    nbr = np.concatenate([p[1] for p in pairs])
+    oc, on = own[cell - 1], own[nbr - 1]
+    for r in range(P):
+        g = make_grid(L, periodic, 1, 0, r, P)
+        m = (oc == r) & (on != r)
+        want_recv = {int(p): np.unique(nbr[m & (on == p)]).tolist() for p in np.unique(on[m])}
+        want_send = {int(p): np.unique(cell[m & (on == p)]).tolist() for p in np.unique(on[m])}
+        assert g.get_cells_to_receive() == want_recv, r
+        assert g.get_cells_to_send() == want_send, r
+        assert g.get_number_of_update_send_cells() == sum(len(v) for v in want_send.values())
+        outer = np.unique(cell[m])
+        assert np.array_equal(g.outer_cells(), outer.astype(np.uint64)), r
+        g.close()
+
+
 @pytest.mark.parametrize("length,periodic,hood,P", RANK_CASES)
 def test_rank_structures_match_oracle(length, periodic, hood, P):
     og = O.Grid(length, 0, periodic, hood)
