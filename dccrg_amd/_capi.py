@@ -136,6 +136,7 @@ SIGNATURES = {
     "dccrgx_halo_self": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t]),
     "dccrgx_gol_compute": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "dccrgx_gol_step": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "dccrgx_get_process": (C.c_int, [_vp, _u64p, C.c_size_t, _i32p]),
     "dccrgx_gather_neighbors": (C.c_int, [_vp, C.c_int32, C.c_int32, _vp, C.c_size_t, _vp, _vp, C.c_size_t,
                                           _vp]),
     "dccrgx_sfc_owners": (C.c_int, [_vp, _u64p, C.c_int32, _i32p]),

@@ -698,6 +698,22 @@ int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uin
     return DCCRGX_OK;
 }
 
+int dccrgx_get_process(const dccrgx_grid* grid, const uint64_t* cells, size_t n, int32_t* out)
+{
+    DX_CHECK(grid && (cells || !n) && (out || !n), DCCRGX_EINVAL, "null argument");
+    for (size_t i = 0; i < n; i++) {
+        const uint64_t c = cells[i];
+        if (grid->uniform) {
+            out[i] = (c >= 1 && c <= grid->g.N) ? level0_owner(grid, grid->g.part, c) : -1;
+            continue;
+        }
+        const Explicit* E = grid->ex;
+        auto it = std::lower_bound(E->leaves.begin(), E->leaves.end(), c);
+        out[i] = (it != E->leaves.end() && *it == c) ? E->owner[it - E->leaves.begin()] : -1;
+    }
+    return DCCRGX_OK;
+}
+
 int dccrgx_grid_destroy(dccrgx_grid* grid)
 {
     if (!grid) return DCCRGX_OK;

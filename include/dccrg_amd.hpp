@@ -41,6 +41,10 @@
 #include <limits>
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
+#include <iomanip>
+#include <iostream>
+#include <sstream>
 #include <map>
 #include <set>
 #include <stdexcept>
@@ -256,12 +260,123 @@ private:
 };
 
 struct No_Geometry {  // dccrg_no_geometry.hpp (nothing on the hot path)
+    static const int geometry_id = 0;
     struct Parameters {};
+    explicit No_Geometry(const Mapping* = nullptr) {}
     bool set(const Parameters&) { return true; }
+    bool read_file_data(const std::vector<char>& b) const
+    {
+        int id = -1;
+        if (b.size() < 4) return false;
+        std::memcpy(&id, b.data(), 4);
+        return id == geometry_id;
+    }
+    // file data, dccrg_no_geometry.hpp:486-549: the id
+    std::vector<char> file_data() const
+    {
+        std::vector<char> b(4);
+        std::memcpy(b.data(), &geometry_id, 4);
+        return b;
+    }
 };
 
-template <class Cell_Data, class Geometry = No_Geometry>
-class Dccrg {
+// dccrg_cartesian_geometry.hpp:51-812: level-0 cells of the same size from a
+// starting corner; lengths and centers of any cell from the mapping
+struct Cartesian_Geometry_Parameters {
+    std::array<double, 3> start{{0, 0, 0}}, level_0_cell_length{{1, 1, 1}};
+    Cartesian_Geometry_Parameters() = default;
+    Cartesian_Geometry_Parameters(const std::array<double, 3>& s, const std::array<double, 3>& l)
+        : start(s), level_0_cell_length(l)
+    {
+        for (double v : l)
+            if (!(v > 0)) throw std::invalid_argument("level-0 cell length must be > 0");
+    }
+};
+
+struct Cartesian_Geometry {
+    static const int geometry_id = 1;
+    typedef Cartesian_Geometry_Parameters Parameters;
+    explicit Cartesian_Geometry(const Mapping* m = nullptr) : mapping_(m) {}
+    bool set(const Parameters& p)
+    {
+        for (double v : p.level_0_cell_length)
+            if (!(v > 0)) return false;
+        par_ = p;
+        return true;
+    }
+    const Parameters& get() const { return par_; }
+    std::array<double, 3> get_start() const { return par_.start; }
+    std::array<double, 3> get_level_0_cell_length() const { return par_.level_0_cell_length; }
+    // :284-309 (NaN for error_cell or an invalid cell)
+    std::array<double, 3> get_length(uint64_t cell) const
+    {
+        const int l = mapping_->get_refinement_level(cell);
+        if (cell == error_cell || l < 0 || l > mapping_->get_maximum_refinement_level()) return nan3();
+        const double f = 1.0 / double(uint64_t(1) << l);
+        return {{par_.level_0_cell_length[0] * f, par_.level_0_cell_length[1] * f, par_.level_0_cell_length[2] * f}};
+    }
+    // :318-364: start + index * l0 / 2^max + length / 2, in that order
+    std::array<double, 3> get_center(uint64_t cell) const
+    {
+        const int l = mapping_->get_refinement_level(cell);
+        if (cell == error_cell || l < 0 || l > mapping_->get_maximum_refinement_level()) return nan3();
+        const auto idx = mapping_->get_indices(cell);
+        const auto len = get_length(cell);
+        const double top = double(uint64_t(1) << mapping_->get_maximum_refinement_level());
+        std::array<double, 3> c;
+        for (int d = 0; d < 3; d++) c[d] = par_.start[d] + double(idx[d]) * par_.level_0_cell_length[d] / top + len[d] / 2;
+        return c;
+    }
+    std::array<double, 3> get_min(uint64_t cell) const  // :378-400
+    {
+        const auto c = get_center(cell), len = get_length(cell);
+        return {{c[0] - len[0] / 2, c[1] - len[1] / 2, c[2] - len[2] / 2}};
+    }
+    std::array<double, 3> get_max(uint64_t cell) const  // :404-422
+    {
+        const auto c = get_center(cell), len = get_length(cell);
+        return {{c[0] + len[0] / 2, c[1] + len[1] / 2, c[2] + len[2] / 2}};
+    }
+    bool read_file_data(const std::vector<char>& b)  // :683-756
+    {
+        int id = -1;
+        if (b.size() < 52) return false;
+        std::memcpy(&id, b.data(), 4);
+        if (id != geometry_id) return false;
+        Parameters p;
+        std::memcpy(p.start.data(), b.data() + 4, 24);
+        std::memcpy(p.level_0_cell_length.data(), b.data() + 28, 24);
+        return set(p);
+    }
+    // file data, :620-680: id, start, level-0 cell length
+    std::vector<char> file_data() const
+    {
+        std::vector<char> b(4 + 48);
+        std::memcpy(b.data(), &geometry_id, 4);
+        std::memcpy(b.data() + 4, par_.start.data(), 24);
+        std::memcpy(b.data() + 28, par_.level_0_cell_length.data(), 24);
+        return b;
+    }
+
+private:
+    static std::array<double, 3> nan3()
+    {
+        const double q = std::numeric_limits<double>::quiet_NaN();
+        return {{q, q, q}};
+    }
+    const Mapping* mapping_;
+    Parameters par_;
+};
+
+template <class Cell_Data, class Geometry = No_Geometry, class Additional_Cell_Items = std::tuple<>,
+          class Additional_Neighbor_Items = std::tuple<>>
+class Dccrg;
+
+// Additional cell / neighbor items (dccrg.hpp:151-156, 7404-7518): the
+// iteration cache's items derive from them, and each item's update() is
+// called when the cache is (re)built, as update_caller does (:11548, 11650)
+template <class Cell_Data, class Geometry, class... ACI, class... ANI>
+class Dccrg<Cell_Data, Geometry, std::tuple<ACI...>, std::tuple<ANI...>> {
 public:
     typedef std::vector<std::pair<uint64_t, std::array<int, 3>>> neighbor_list_t;
 
@@ -273,12 +388,12 @@ public:
         typename std::vector<T>::const_iterator end() const { return end_; }
         typename std::vector<T>::const_iterator cend() const { return end_; }
     };
-    struct Neighbors_Item {  // dccrg.hpp:7404-7456
-        uint64_t id;
-        Cell_Data* data;
-        int x, y, z;
+    struct Neighbors_Item : ANI... {  // dccrg.hpp:7404-7456
+        uint64_t id = error_cell;
+        Cell_Data* data = nullptr;
+        int x = 0, y = 0, z = 0;
     };
-    struct Cells_Item {  // dccrg.hpp:7480-7518
+    struct Cells_Item : ACI... {  // dccrg.hpp:7480-7518
         uint64_t id = error_cell;
         Cell_Data* data = nullptr;
         Iterator_Storage<Neighbors_Item> neighbors_of, neighbors_to, all_neighbors;
@@ -286,7 +401,7 @@ public:
 
     Mapping mapping;
     Grid_Topology topology;
-    Geometry geometry;
+    Geometry geometry{&mapping};
 
     Dccrg() = default;
     Dccrg(const Dccrg&) = delete;
@@ -341,7 +456,18 @@ public:
         return *this;
     }
     bool set_geometry(const typename Geometry::Parameters& p) { return geometry.set(p); }
-    Dccrg& balance_load(bool = true) { return *this; }  // block partition kept (dccrg.hpp:1048-1062)
+    // dccrg.hpp:1046-1064: the block partition is kept (Zoltan stays out of
+    // the device path), but like finish_balance_load the iteration caches are
+    // rebuilt (update_cell_pointers, :11453), so additional cell / neighbor
+    // items are updated again (e.g. a Center item after set_geometry)
+    Dccrg& balance_load(bool = true)
+    {
+        if (!initialized_) return *this;
+        std::vector<int> ids;
+        for (auto& kv : hoods_) ids.push_back(kv.first);
+        for (int id : ids) build_hood(id);
+        return *this;
+    }
 
     // dccrg.hpp:485-562
     Dccrg& initialize(const MPI_Comm& comm, uint64_t = 1)
@@ -389,9 +515,9 @@ public:
                 bytes_before += all[2 * r + 1];
             }
         }
-        const int32_t geometry_id = 0;  // No_Geometry::geometry_id, dccrg_no_geometry.hpp:55
+        const std::vector<char> gb = geometry.file_data();  // the geometry's write(), e.g. :620-680
         const int s = dccrgx_save_grid_data_host(grid_, name.c_str(), (uint64_t)offset, hb.data(), hb.size(),
-                                                 &geometry_id, 4, total, cells_before, bytes_before, sizes.data(),
+                                                 gb.data(), gb.size(), total, cells_before, bytes_before, sizes.data(),
                                                  recs.data(), recs.size());
         int ok = s == DCCRGX_OK, all_ok = 0;
         if (!ok) std::fprintf(stderr, "save_grid_data: %s\n", dccrgx_last_error());
@@ -415,9 +541,15 @@ public:
         init_comm(comm);
         std::vector<char> hb(pack_header(header).size());
         dccrgx_file_info info{};
-        if (dccrgx_file_read_info(name.c_str(), (uint64_t)offset, hb.data(), hb.size(), &info, nullptr, 0) !=
+        std::vector<char> gb(4096);
+        if (dccrgx_file_read_info(name.c_str(), (uint64_t)offset, hb.data(), hb.size(), &info, gb.data(), gb.size()) !=
             DCCRGX_OK) {
             std::fprintf(stderr, "start_loading_grid_data: %s\n", dccrgx_last_error());
+            return false;
+        }
+        gb.resize(std::min<size_t>(gb.size(), info.geometry_bytes));
+        if (!geometry.read_file_data(gb)) {
+            std::fprintf(stderr, "start_loading_grid_data: the file's geometry is not this grid's geometry\n");
             return false;
         }
         int pos = 0;
@@ -592,6 +724,24 @@ public:
     }
     int get_refinement_level(uint64_t cell) const { return mapping.get_refinement_level(cell); }
     bool is_local(uint64_t cell) const { return cell_data_.count(cell) > 0; }
+    // dccrg.hpp:5886-5902: the owning process of an existing cell, else -1
+    int get_process(uint64_t cell) const
+    {
+        int32_t p = -1;
+        detail::check(dccrgx_get_process(grid_, &cell, 1, &p), "get_process");
+        return p;
+    }
+    // dccrg.hpp:4193-4226: the parent if it exists, else the cell if it
+    // exists, else error_cell
+    uint64_t get_parent(uint64_t cell) const
+    {
+        if (mapping.get_refinement_level(cell) == 0) return get_process(cell) >= 0 ? cell : error_cell;
+        const uint64_t parent =
+            mapping.get_cell_from_indices(mapping.get_indices(cell), mapping.get_refinement_level(cell) - 1);
+        if (get_process(parent) >= 0) return parent;
+        if (get_process(cell) >= 0) return cell;
+        return error_cell;
+    }
 
     std::vector<uint64_t> get_cells() const  // local cells, ascending
     {
@@ -853,20 +1003,28 @@ private:
                 if (ids_to.count(t)) both.insert(x);
                 else only_of.insert(x);
             }
+            Cells_Item ci{};
+            ci.id = order[i];
+            ci.data = (*this)[order[i]];
+            (ci.ACI::update(*this, ci, ACI()), ...);  // :11548
             ranges[i][0] = S.neighbors.size();
             for (const auto* group : {&only_of, &both, &only_to})
-                for (const item& x : *group)
-                    S.neighbors.push_back(Neighbors_Item{x.first, (*this)[x.first], x.second[0], x.second[1],
-                                                         x.second[2]});
+                for (const item& x : *group) {
+                    Neighbors_Item ni{};
+                    ni.id = x.first;
+                    ni.data = (*this)[x.first];
+                    ni.x = x.second[0];
+                    ni.y = x.second[1];
+                    ni.z = x.second[2];
+                    (ni.ANI::update(*this, ci, ni, hood, ANI()), ...);  // :11650-11715
+                    S.neighbors.push_back(std::move(ni));
+                }
             ranges[i][1] = ranges[i][0] + only_of.size();
             ranges[i][2] = ranges[i][1] + both.size();
             ranges[i][3] = ranges[i][2] + only_to.size();
             S.nof[order[i]] = std::move(nof);
             S.nto[order[i]] = std::move(nto);
-            Cells_Item ci;
-            ci.id = order[i];
-            ci.data = (*this)[order[i]];
-            S.cells.push_back(ci);
+            S.cells.push_back(std::move(ci));
         }
         auto b = S.neighbors.cbegin();
         for (size_t i = 0; i < n; i++) {

@@ -166,6 +166,11 @@ int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* params,
 int dccrgx_grid_destroy(dccrgx_grid* grid);
 int dccrgx_grid_get_info(const dccrgx_grid* grid, dccrgx_grid_info* out);
 
+/* Dccrg::get_process (dccrg.hpp:5886-5902) for n cells on the host: the
+ * process owning each existing cell (the replicated cell_process), -1 for a
+ * cell that does not exist */
+int dccrgx_get_process(const dccrgx_grid* grid, const uint64_t* cells, size_t n, int32_t* process_out);
+
 /* Dccrg::add_neighborhood / remove_neighborhood, dccrg.hpp:6491-6711
  * (validation as :6573-6618: returns DCCRGX_EINVAL when the reference returns false) */
 int dccrgx_add_neighborhood(dccrgx_grid* grid, int32_t hood_id, const int32_t* items3,
