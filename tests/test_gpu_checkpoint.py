@@ -248,3 +248,31 @@ def test_large_uniform_round_trip(tmp_path):
     assert np.array_equal(g.read_local("a"), a)
     g.close()
     ctx.close()
+
+
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("case", CASES)
+def test_reference_reader_parses_device_files(tmp_path, P, case):
+    """A device-written file (header u64 time step, u64 is_alive per cell, as
+    tests/restart writes) parsed by the reference's own reader
+    (tests/restart/dc2vtk.cpp built where it lies, oracle/_ref)."""
+    import ref_reader as R
+    if not R.available():
+        pytest.skip("oracle/_ref/restart_dc2vtk is built where the reference is")
+    length, M, per, hood, _ = case
+    grids = make(length, M, per, hood, P, leaves_of(case))
+    start, l0 = (0.5, -1.0, 2.0), (0.25, 0.5, 0.125)
+    order = []
+    for g in grids:
+        ids = g.local_cells()
+        order += ids.tolist()
+        g.add_field("alive", np.uint64)
+        g.write_local("alive", (ids % 3 == 0).astype(np.uint64))
+    path = str(tmp_path / "dev.dc")
+    save_all(grids, path, ["alive"], 0, struct.pack("<Q", 9), K.cartesian_geometry(start, l0))
+    pts, alive = R.read_with_reference(path)
+    assert alive.tolist() == [int(c % 3 == 0) for c in order]
+    np.testing.assert_allclose(pts, R.expected_corners(order, length, grids[0].get_maximum_refinement_level(),
+                                                       start, l0), rtol=1e-5, atol=1e-9)
+    for g in grids:
+        g.close()
