@@ -285,7 +285,44 @@ def secondary(ctx, torch, D):
                       "achieved_GBs": 36 * nid / (ms * 1e-3) / 1e9,
                       "frac": 36 * nid / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_id": 36}
     del ids
+    out["mapping_reference_speed_test"] = mapping_speed_test(D, torch, dev)
     out["neighbor_lists"] = neighbor_lists(ctx, D, torch)
+    return out
+
+
+def mapping_speed_test(D, torch, dev):
+    """tests/geometry/cartesian_grid_speed.cpp's workload: ids 1..1e8 of a
+    100x200x300 grid at its maximum refinement level (13).  The reference's
+    own program (built where it lies into oracle/_ref/geometry_speed; one
+    core, clock()) times get_length and get_center over them; the device
+    maps the same ids to indices + level (dccrgx_map_ids_to_indices, what
+    get_center spends its time on)."""
+    out = {"workload": "Mapping ids 1..1e8 of 100x200x300 at max_ref_lvl 13 (cartesian_grid_speed.cpp)"}
+    m = D.Mapping((100, 200, 300), -1)
+    n = 100_000_000
+    ids = torch.arange(1, n + 1, dtype=torch.int64, device=dev)
+    m.ids_to_indices(ids)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    e0.record()
+    for _ in range(reps):
+        m.ids_to_indices(ids)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    out["device_ids_per_s"] = n / (ms * 1e-3)
+    del ids
+    exe = os.path.join(ROOT, "oracle", "_ref", "geometry_speed")
+    if os.path.exists(exe):
+        import re
+        import subprocess
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+        t = [float(x) for x in re.findall(r"time for 1e\+08 cells: ([0-9.eE+-]+) s", r.stdout)]
+        if len(t) == 2:
+            out["reference_cpu"] = {"kind": "reference", "cores": 1,
+                                    "get_length_ids_per_s": 1e8 / t[0], "get_center_ids_per_s": 1e8 / t[1]}
+            out["device_over_reference_get_center"] = out["device_ids_per_s"] / (1e8 / t[1])
     return out
 
 
