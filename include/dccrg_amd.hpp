@@ -63,6 +63,14 @@ namespace dccrg {
 static const uint64_t error_cell = DCCRGX_ERROR_CELL;    // dccrg_mapping.hpp:38
 static const uint64_t error_index = DCCRGX_ERROR_INDEX;  // dccrg_mapping.hpp:41
 static const int default_neighborhood_id = DCCRGX_DEFAULT_NEIGHBORHOOD_ID;  // dccrg.hpp:99
+// neighbor-type criteria of get_cells (dccrg.hpp:103-114)
+static const int has_no_neighbor = 0;
+static const int has_local_neighbor_of = 1 << 0;
+static const int has_local_neighbor_to = 1 << 1;
+static const int has_remote_neighbor_of = 1 << 2;
+static const int has_remote_neighbor_to = 1 << 3;
+static const int has_local_neighbor_both = has_local_neighbor_of | has_local_neighbor_to;
+static const int has_remote_neighbor_both = has_remote_neighbor_of | has_remote_neighbor_to;
 
 template <unsigned N> struct Types;
 template <> struct Types<3> {  // dccrg_types.hpp:34-86
@@ -743,9 +751,44 @@ public:
         return error_cell;
     }
 
-    std::vector<uint64_t> get_cells() const  // local cells, ascending
+    // dccrg.hpp:661-742 / is_neighbor_type_match :2960-3081: local cells whose
+    // neighbor types (has_*_neighbor_* of the neighborhood's neighbors_of and
+    // neighbors_to) match the criteria; nothing for an unknown neighborhood.
+    // Cells come ascending (the reference: hash order unless sorted).
+    std::vector<uint64_t> get_cells(const std::vector<int>& criteria = std::vector<int>(), bool exact_match = false,
+                                    int hood = default_neighborhood_id, bool /*sorted*/ = false) const
     {
-        return query_cells(default_neighborhood_id, DCCRGX_CELLS_LOCAL);
+        if (!hoods_.count(hood)) return {};
+        std::vector<uint64_t> local = query_cells(hood, DCCRGX_CELLS_LOCAL);
+        if (criteria.empty()) return local;
+        const HoodState& S = hs(hood);
+        std::vector<uint64_t> out;
+        int merged = 0;
+        for (int c : criteria) merged |= c;
+        for (uint64_t cell : local) {
+            int types = 0;
+            for (const auto& n : S.nof.at(cell))
+                if (n.first != error_cell) types |= is_local(n.first) ? has_local_neighbor_of : has_remote_neighbor_of;
+            for (const auto& n : S.nto.at(cell))
+                if (n.first != error_cell) types |= is_local(n.first) ? has_local_neighbor_to : has_remote_neighbor_to;
+            bool match = false;
+            if (exact_match) {
+                for (int c : criteria) match |= types == c;
+            } else {
+                match = (types & merged) > 0;
+            }
+            if (match) out.push_back(cell);
+        }
+        return out;
+    }
+    // dccrg.hpp:6158-6300 (ascending; the reference: hash order unless sorted)
+    std::vector<uint64_t> get_local_cells_on_process_boundary(int hood = default_neighborhood_id, bool = false) const
+    {
+        return hoods_.count(hood) ? query_cells(hood, DCCRGX_CELLS_OUTER) : std::vector<uint64_t>();
+    }
+    std::vector<uint64_t> get_local_cells_not_on_process_boundary(int hood = default_neighborhood_id, bool = false) const
+    {
+        return hoods_.count(hood) ? query_cells(hood, DCCRGX_CELLS_INNER) : std::vector<uint64_t>();
     }
 
     const Iterator_Storage<Cells_Item>& local_cells(int hood = default_neighborhood_id) const { return hs(hood).local; }
@@ -795,10 +838,9 @@ public:
         for (auto& kv : hs(hood).recv) n += kv.second.size();
         return n;
     }
-    std::unordered_set<uint64_t> get_remote_cells_on_process_boundary(int hood = default_neighborhood_id) const
+    std::vector<uint64_t> get_remote_cells_on_process_boundary(int hood = default_neighborhood_id, bool = false) const
     {
-        const auto& r = hs(hood).remote_ids;
-        return std::unordered_set<uint64_t>(r.begin(), r.end());
+        return hoods_.count(hood) ? hs(hood).remote_ids : std::vector<uint64_t>();
     }
 
     // dccrg.hpp:6491-6711

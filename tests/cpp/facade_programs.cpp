@@ -265,6 +265,43 @@ static int amr(int argc, char** argv)
     return 0;
 }
 
+static void print_matches(const char* tag, const std::vector<uint64_t>& ids)
+{
+    printf("%s", tag);
+    for (uint64_t c : ids) printf(" %llu", (unsigned long long)c);
+    printf("\n");
+}
+
+// get_cells(criteria, exact_match, hood) and the process-boundary accessors
+// (dccrg.hpp:661, 2968, 6158-6300); a user neighborhood {+x} as hood 7
+static int cells(int argc, char** argv)
+{
+    dccrg::Dccrg<int> grid;
+    grid.set_initial_length({strtoull(argv[2], 0, 10), strtoull(argv[3], 0, 10), strtoull(argv[4], 0, 10)})
+        .set_neighborhood_length(atoi(argv[8]))
+        .set_maximum_refinement_level(0)
+        .set_periodic(atoi(argv[5]), atoi(argv[6]), atoi(argv[7]))
+        .initialize(MPI_COMM_WORLD);
+    if (!grid.add_neighborhood(7, {{1, 0, 0}})) abort();
+    const int crit[] = {dccrg::has_no_neighbor, dccrg::has_local_neighbor_of, dccrg::has_local_neighbor_to,
+                        dccrg::has_local_neighbor_both, dccrg::has_remote_neighbor_of,
+                        dccrg::has_remote_neighbor_both};
+    for (int hood : {dccrg::default_neighborhood_id, 7}) {
+        for (int c : crit)
+            for (int exact : {0, 1}) {
+                char tag[64];
+                snprintf(tag, sizeof tag, "hood %d crit %d exact %d :", hood == 7 ? 7 : 0, c, exact);
+                print_matches(tag, grid.get_cells({c}, exact, hood));
+            }
+        print_matches(hood == 7 ? "hood 7 all :" : "hood 0 all :", grid.get_cells({}, false, hood));
+        if (!grid.get_local_cells_on_process_boundary(hood).empty()) abort();
+        if (!grid.get_remote_cells_on_process_boundary(hood, true).empty()) abort();
+        if (grid.get_local_cells_not_on_process_boundary(hood) != grid.get_cells()) abort();
+    }
+    if (!grid.get_cells({dccrg::has_local_neighbor_of}, false, 99).empty()) abort();  // unknown hood
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     if (MPI_Init(&argc, &argv) != MPI_SUCCESS) abort();
@@ -278,6 +315,7 @@ int main(int argc, char** argv)
         else if (mode == "lists") rc = lists(argc, argv);
         else if (mode == "amr") rc = amr(argc, argv);
         else if (mode == "restart") rc = restart(argc, argv);
+        else if (mode == "cells") rc = cells(argc, argv);
     }
     MPI_Finalize();
     return rc;

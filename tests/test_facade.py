@@ -156,3 +156,35 @@ def test_facade_restart(tmp_path):
     assert got["length"] == (15, 15, 1) and got["geometry"] == K.no_geometry()
     assert got["order"] == list(range(1, 226))
     assert all(len(b) == 4 and struct.unpack("<I", b)[0] in (0, 1) for b in got["cells"].values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims,per,hood", [((3, 1, 1), (0, 0, 0), 1), ((4, 3, 2), (1, 0, 1), 1),
+                                           ((1, 1, 1), (0, 0, 0), 1), ((5, 4, 1), (0, 0, 0), 0)])
+def test_facade_get_cells_criteria(dims, per, hood):
+    """get_cells(criteria, exact_match, hood) picks local cells by their
+    neighbor types (is_neighbor_type_match, dccrg.hpp:2968-3075): exact =
+    type mask equal to a criterion, inexact = mask AND the OR of them > 0;
+    one process, so every neighbor is local and no cell is on a boundary."""
+    pers = tuple(bool(p) for p in per)
+    grids = {0: O.Grid(dims, 0, pers, hood)}
+    n = int(np.prod(dims))
+    got = {}
+    for line in run("cells", *dims, *per, hood).strip().splitlines():
+        head, _, ids = line.partition(":")
+        got[head.strip()] = [int(x) for x in ids.split()]
+    for h, items in ((0, None), (7, [(1, 0, 0)])):
+        g = grids[0]
+        types = {}
+        for cid in range(1, n + 1):
+            t = 0
+            if any(c for c, _ in g.find_neighbors_of(cid, items)):
+                t |= 1
+            if any(c for c in g.find_neighbors_to(cid, None if items is None else O.neighborhood_to(items))):
+                t |= 2
+            types[cid] = t
+        assert got[f"hood {h} all"] == list(range(1, n + 1))
+        for c in (0, 1, 2, 3, 4, 12):
+            for exact in (0, 1):
+                want = [cid for cid in range(1, n + 1) if (types[cid] == c if exact else types[cid] & c)]
+                assert got[f"hood {h} crit {c} exact {exact}"] == want, (h, c, exact)
