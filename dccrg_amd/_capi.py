@@ -156,6 +156,8 @@ SIGNATURES = {
     "dccrgx_amr_request_cells": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _i32p]),
     "dccrgx_advect_adapt_marks": (C.c_int, [_vp, C.c_int32, _vp, C.c_double, C.c_double, C.c_double,
                                             C.POINTER(C.c_int8), C.POINTER(C.c_double)]),
+    "dccrgx_advect_adaptation_sets": (C.c_int, [_vp, C.c_int32, _vp, C.c_double, C.c_double, C.c_double,
+                                                _u64p, _u64p, _u64p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "dccrgx_refine_completely": (C.c_int, [_vp, C.c_uint64, _i32p]),
     "dccrgx_unrefine_completely": (C.c_int, [_vp, C.c_uint64, _i32p]),
     "dccrgx_dont_unrefine": (C.c_int, [_vp, C.c_uint64, _i32p]),

@@ -86,37 +86,23 @@ def _velocities_lengths(grid, geom, cells=None, center=None, ln=None):
 
 def check_for_adaptation(grid: Dccrg, diff_increase: float, diff_threshold: float,
                          unrefine_sensitivity: float):
-    """adapter.hpp:43-176.  The differences and categories come from the
-    device; the sibling rules of :120-175 are applied per sibling group (their
-    effect does not depend on the order the reference visits cells in).
-    Returns (cells_to_refine, cells_not_to_unrefine, cells_to_unrefine)."""
+    """adapter.hpp:43-176 on the device (dccrgx_advect_adaptation_sets): the
+    differences, categories and the per-sibling-group rules of :120-175
+    (their outcome does not depend on the order the reference visits cells
+    in).  Returns (cells_to_refine, cells_not_to_unrefine, cells_to_unrefine),
+    each ascending."""
     empty = np.zeros(0, dtype=np.uint64)
     if grid.get_maximum_refinement_level() == 0:
         return empty, empty, empty
     n = grid.n_local
-    marks = np.zeros(n, dtype=np.int8)
+    out = [np.zeros(max(n, 1), dtype=np.uint64) for _ in range(3)]
+    counts = (C.c_size_t * 3)()
     f = grid._advect_fields()
-    check(lib().dccrgx_advect_adapt_marks(grid._h, X.DEFAULT_NEIGHBORHOOD_ID, C.byref(f), diff_increase,
-                                          diff_threshold, unrefine_sensitivity,
-                                          marks.ctypes.data_as(C.POINTER(C.c_int8)), None))
+    check(lib().dccrgx_advect_adaptation_sets(grid._h, X.DEFAULT_NEIGHBORHOOD_ID, C.byref(f), diff_increase,
+                                              diff_threshold, unrefine_sensitivity,
+                                              *[a.ctypes.data_as(X._u64p) for a in out], max(n, 1), counts))
     grid._refresh_info()
-    cells = grid.local_cells()
-    m = grid.mapping
-    _, lvl = m.levels_and_indices(cells)
-    group = m.parents(cells)  # level-0 cells are their own group
-    refine = cells[marks == 2]
-    # per sibling group: any refine blocks keep/unrefine marks; any keep (level > 0)
-    # blocks unrefine marks (:126-174)
-    g_ref = np.isin(group, group[marks == 2])
-    g_keep = np.isin(group, group[(marks == 1) & (lvl > 0)])
-    kmask = (marks == 1) & (lvl > 0) & ~g_ref
-    keep = cells[kmask]
-    # one dont_unrefine per group is what the reference leaves behind (:146-155)
-    if keep.size:
-        _, first = np.unique(group[kmask], return_index=True)
-        keep = keep[np.sort(first)]
-    unref = cells[(marks == 0) & (lvl > 0) & ~g_ref & ~g_keep]
-    return refine.astype(np.uint64), keep.astype(np.uint64), unref.astype(np.uint64)
+    return tuple(a[:k].copy() for a, k in zip(out, counts))
 
 
 def _request(grid: Dccrg, kind: int, ids: np.ndarray):

@@ -267,6 +267,71 @@ __global__ void __launch_bounds__(256) k_adapt_marks(const unsigned long long* _
     }
 }
 
+// the 8 siblings of every local cell (dccrg_mapping.hpp:450-471: the
+// parent's children, x fastest; a level-0 cell is its own only sibling)
+__global__ void __launch_bounds__(256) k_sibling_ids(MapParams mp, const uint64_t* __restrict__ leaves,
+                                                     const uint32_t* __restrict__ local_g, uint64_t n,
+                                                     uint64_t* __restrict__ sib, int8_t* __restrict__ lvl_out)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        const uint64_t c = leaves[local_g[q]];
+        uint64_t idx[3];
+        int l = 0;
+        map_indices(mp, c, idx, &l);
+        lvl_out[q] = (int8_t)l;
+        if (l == 0) {
+            sib[8 * q] = c;
+            for (int k = 1; k < 8; k++) sib[8 * q + k] = 0;
+            continue;
+        }
+        const uint64_t h = (uint64_t)1 << (mp.max_lvl - l);
+        uint64_t p[3];
+        for (int d = 0; d < 3; d++) p[d] = idx[d] - idx[d] % (2 * h);
+        int k = 0;
+        for (int dz = 0; dz < 2; dz++)
+            for (int dy = 0; dy < 2; dy++)
+                for (int dx = 0; dx < 2; dx++) {
+                    const uint64_t ci[3] = {p[0] + dx * h, p[1] + dy * h, p[2] + dz * h};
+                    sib[8 * q + k++] = map_cell(mp, ci, l);
+                }
+    }
+}
+
+// adapter.hpp:109-176 per sibling group.  The reference's loop inserts and
+// erases while it walks the local cells; its outcome per group is: refine
+// every cell marked 2; if any sibling is marked 2 nothing else; else keep
+// (dont_unrefine) the first sibling marked 1 -- later ones find it recorded
+// (:144-150) -- and unrefine cells marked 0 only when no sibling is marked 1
+// (a keep erases its siblings' unrefines, :155-157).  Level-0 cells are
+// never kept or unrefined (:152, :173).  Local positions are in ascending id
+// order and siblings are local (same level-0 ancestor), so "first" is the
+// smallest position.  Codes: 0 none, 1 refine, 2 dont_unrefine, 3 unrefine.
+__global__ void __launch_bounds__(256) k_adapt_codes(const int8_t* __restrict__ marks,
+                                                     const int64_t* __restrict__ sib_pos,
+                                                     const int8_t* __restrict__ lvl, uint64_t n,
+                                                     uint8_t* __restrict__ code)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        const int m = marks[q];
+        if (lvl[q] == 0) {
+            code[q] = m == 2 ? 1 : 0;
+            continue;
+        }
+        bool g_ref = false, g_keep = false, earlier_keep = false;
+        for (int k = 0; k < 8; k++) {
+            const int64_t s = sib_pos[8 * q + k];
+            if (s < 0 || (uint64_t)s >= n) continue;  // refined sibling (not a leaf)
+            const int ms = marks[s];
+            g_ref |= ms == 2;
+            g_keep |= ms == 1;
+            earlier_keep |= ms == 1 && (uint64_t)s < q;
+        }
+        code[q] = m == 2 ? 1 : (m == 1 ? ((!g_ref && !earlier_keep) ? 2 : 0) : ((!g_ref && !g_keep) ? 3 : 0));
+    }
+}
+
 __global__ void __launch_bounds__(256) k_flag_slots(const uint32_t* __restrict__ local_g, uint64_t n,
                                                     uint8_t* __restrict__ flag)
 {
@@ -620,11 +685,17 @@ int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f
     return DCCRGX_OK;
 }
 
-int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
-                              double diff_increase, double diff_threshold, double unrefine_sensitivity,
-                              int8_t* marks_out, double* max_diff_out)
+}  // extern "C"
+
+namespace dccrgx {
+namespace {
+
+// device marks (and optionally the max diffs) of every local cell; the
+// caller frees *d_marks_out (left on the compute stream, not synchronised)
+int adapt_marks_device(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double diff_increase,
+                       double diff_threshold, double unrefine_sensitivity, int8_t** d_marks_out, double* max_diff_out)
 {
-    DX_CHECK(grid && f && (marks_out || !grid->n_local), DCCRGX_EINVAL, "null argument");
+    *d_marks_out = nullptr;
     DX_TRY(amr_ensure_explicit(grid));
     const Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -653,13 +724,81 @@ int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_a
     hipLaunchKernelGGL(k_adapt_marks, dim3(grid_for(n)), dim3(256), 0, st, (const unsigned long long*)d_max,
                        R.local_slot, R.level, n, diff_increase, unrefine_sensitivity, d_marks, d_diff);
     DX_HIP(hipGetLastError());
-    DX_HIP(hipMemcpyAsync(marks_out, d_marks, n, hipMemcpyDeviceToHost, st));
     if (max_diff_out) DX_HIP(hipMemcpyAsync(max_diff_out, d_diff, n * 8, hipMemcpyDeviceToHost, st));
-    DX_HIP(hipStreamSynchronize(st));
-    dx_free(d_max);
+    dx_free(d_max);  // dx_free waits for the kernels above
     dx_free(d_flag);
-    dx_free(d_marks);
     dx_free(d_diff);
+    *d_marks_out = d_marks;
+    return DCCRGX_OK;
+}
+
+}  // namespace
+}  // namespace dccrgx
+
+extern "C" {
+
+int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
+                              double diff_increase, double diff_threshold, double unrefine_sensitivity,
+                              int8_t* marks_out, double* max_diff_out)
+{
+    DX_CHECK(grid && f && (marks_out || !grid->n_local), DCCRGX_EINVAL, "null argument");
+    int8_t* d_marks = nullptr;
+    DX_TRY(adapt_marks_device(grid, hood_id, f, diff_increase, diff_threshold, unrefine_sensitivity, &d_marks,
+                              max_diff_out));
+    if (!d_marks) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    const hipError_t e = hipMemcpyAsync(marks_out, d_marks, grid->n_local, hipMemcpyDeviceToHost, st);
+    const hipError_t e2 = hipStreamSynchronize(st);
+    dx_free(d_marks);
+    DX_HIP(e);
+    DX_HIP(e2);
+    return DCCRGX_OK;
+}
+
+int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
+                                  double diff_increase, double diff_threshold, double unrefine_sensitivity,
+                                  uint64_t* to_refine, uint64_t* not_to_unrefine, uint64_t* to_unrefine, size_t cap,
+                                  size_t counts[3])
+{
+    DX_CHECK(grid && f && counts, DCCRGX_EINVAL, "null argument");
+    counts[0] = counts[1] = counts[2] = 0;
+    if (grid->map.max_lvl == 0) return DCCRGX_OK;  // adapter.hpp:57-59
+    const uint64_t n = grid->n_local;
+    DX_CHECK(cap >= n, DCCRGX_ERANGE, "capacity %zu < %llu local cells", cap, (unsigned long long)n);
+    DX_CHECK((to_refine && not_to_unrefine && to_unrefine) || !n, DCCRGX_EINVAL, "null output");
+    int8_t* d_marks = nullptr;
+    DX_TRY(adapt_marks_device(grid, hood_id, f, diff_increase, diff_threshold, unrefine_sensitivity, &d_marks,
+                              nullptr));
+    if (!d_marks) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    const Explicit* E = grid->ex;
+    uint64_t* d_sib = nullptr;
+    int64_t* d_pos = nullptr;
+    int8_t* d_lvl = nullptr;
+    uint8_t* d_code = nullptr;
+    int s = DCCRGX_OK;
+    if (dx_malloc(&d_sib, n * 64) != hipSuccess || dx_malloc(&d_pos, n * 64) != hipSuccess ||
+        dx_malloc(&d_lvl, n) != hipSuccess || dx_malloc(&d_code, n) != hipSuccess)
+        s = set_error(DCCRGX_ENOMEM, "out of device memory for the adaptation sets");
+    std::vector<uint8_t> code(n);
+    if (s == DCCRGX_OK) {
+        hipLaunchKernelGGL(k_sibling_ids, dim3(grid_for(n)), dim3(256), 0, st, grid->map, E->d_leaves, E->d_local_g,
+                           n, d_sib, d_lvl);
+        s = explicit_slots_of(grid, d_sib, 8 * n, d_pos, st);
+    }
+    if (s == DCCRGX_OK) {
+        hipLaunchKernelGGL(k_adapt_codes, dim3(grid_for(n)), dim3(256), 0, st, (const int8_t*)d_marks,
+                           (const int64_t*)d_pos, (const int8_t*)d_lvl, n, d_code);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(code.data(), d_code, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            s = set_error(DCCRGX_EHIP, "adaptation sets failed");
+    }
+    for (void* q : {(void*)d_marks, (void*)d_sib, (void*)d_pos, (void*)d_lvl, (void*)d_code}) dx_free(q);
+    if (s != DCCRGX_OK) return s;
+    uint64_t* out[4] = {nullptr, to_refine, not_to_unrefine, to_unrefine};
+    for (uint64_t q = 0; q < n; q++)
+        if (code[q]) out[code[q]][counts[code[q] - 1]++] = E->local[q];
     return DCCRGX_OK;
 }
 

@@ -41,12 +41,8 @@ struct View {
     int M;
 
     int level(uint64_t c) const { return map_level(g->map, c); }
-    bool exists(uint64_t c) const { return std::binary_search(E->leaves.begin(), E->leaves.end(), c); }
-    int64_t gidx(uint64_t c) const
-    {
-        auto it = std::lower_bound(E->leaves.begin(), E->leaves.end(), c);
-        return (it != E->leaves.end() && *it == c) ? (int64_t)(it - E->leaves.begin()) : -1;
-    }
+    bool exists(uint64_t c) const { return E->find(c) >= 0; }
+    int64_t gidx(uint64_t c) const { return E->find(c); }
     int owner(uint64_t c) const
     {
         uint64_t idx[3];
@@ -293,6 +289,7 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     T.lap("neighborhoods");
     if (s == DCCRGX_OK) s = explicit_add_slots(grid, retired);
     if (s != DCCRGX_OK) return rollback(s);
+    T.lap("retired slots");
     Explicit* E = grid->ex;
     E->defer_fields = false;
     E->retired = retired;
@@ -318,6 +315,7 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
         if (ns && hipMemcpy(d_from, from.data(), ns * 8, hipMemcpyHostToDevice) != hipSuccess)
             return fail(set_error(DCCRGX_EHIP, "uploading the rebuild plan failed"));
     }
+    T.lap("move plan");
     // new field arrays: a spare of the last rebuild when one is large enough
     // (an adaptive run rebuilds every step with similar sizes), else a fresh
     // allocation with 1/8 headroom
@@ -577,14 +575,15 @@ int dccrgx_amr_requests(const dccrgx_grid* grid, int32_t which, uint64_t* ids, s
     *n = 0;
     if (!grid->amr) return DCCRGX_OK;
     const Amr& A = *grid->amr;
-    const std::set<uint64_t>& s = which == DCCRGX_AMR_REFINE       ? A.to_refine
+    const FlatSet& s = which == DCCRGX_AMR_REFINE       ? A.to_refine
                                   : which == DCCRGX_AMR_DONT_REFINE ? A.not_to_refine
                                   : which == DCCRGX_AMR_UNREFINE    ? A.to_unrefine
                                                                     : A.not_to_unrefine;
     *n = s.size();
     if (!ids) return DCCRGX_OK;
     DX_CHECK(cap >= s.size(), DCCRGX_ERANGE, "capacity %zu < %zu", cap, s.size());
-    std::copy(s.begin(), s.end(), ids);
+    const std::vector<uint64_t> v = s.sorted();  // ascending, as the reference's std::set
+    std::copy(v.begin(), v.end(), ids);
     return DCCRGX_OK;
 }
 
@@ -597,8 +596,8 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     A.removed.clear();
     if (n_new) *n_new = 0;
     PhaseTimer T("stop_refining");
-    std::set<uint64_t> R(sets[0], sets[0] + counts[0]), NR(sets[1], sets[1] + counts[1]);
-    std::set<uint64_t> U(sets[2], sets[2] + counts[2]), NU(sets[3], sets[3] + counts[3]);
+    FlatSet R(sets[0], sets[0] + counts[0]), NR(sets[1], sets[1] + counts[1]);
+    FlatSet U(sets[2], sets[2] + counts[2]), NU(sets[3], sets[3] + counts[3]);
     if (grid->uniform && R.empty() && U.empty()) {
         // nothing can change; on a level-0 grid the dont_refine closure is the
         // set itself, and it persists (:10188)
@@ -613,7 +612,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
 
     // override_refines, dccrg.hpp:10130-10236: dont_refine spreads to every
     // finer cell among the neighbors of a dont_refine cell, transitively
-    std::set<uint64_t> donts;
+    FlatSet donts;
     std::vector<uint64_t> frontier;
     for (uint64_t c : NR)
         if (donts.insert(c).second) frontier.push_back(c);
@@ -635,7 +634,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
 
     // induce_refines, dccrg.hpp:9730-9907: every coarser neighbor (of / to)
     // of a refined cell is refined, transitively
-    frontier.assign(R.begin(), R.end());
+    frontier = R.sorted();
     while (!frontier.empty()) {
         std::vector<uint64_t> next;
         for (uint64_t r : frontier) {
@@ -659,9 +658,9 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     // Requests are independent and only read R, NU and the leaf set, so they
     // are split over host threads, each with its own memo of the face graph
     // (siblings' walks cover the same cells).
-    std::set<uint64_t> final_un;
+    FlatSet final_un;
     {
-        const std::vector<uint64_t> Uv(U.begin(), U.end());
+        const std::vector<uint64_t> Uv = U.sorted();
         std::vector<uint8_t> keep(Uv.size(), 0);
         auto work = [&](size_t b, size_t e) {
             std::unordered_map<uint64_t, std::array<uint64_t, 6>> memo;
@@ -724,7 +723,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
             retired.push_back(r);
         }
     }
-    std::set<uint64_t> parents;
+    FlatSet parents;
     for (uint64_t u : final_un) {
         const uint64_t p = v.parent(u);
         if (!parents.insert(p).second) continue;

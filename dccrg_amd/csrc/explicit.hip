@@ -387,6 +387,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
     DX_CHECK(n > 0 && n < (1ull << 32), DCCRGX_EINVAL, "leaf count %zu", n);
+    PhaseTimer T("explicit_init");
     auto* E = new Explicit();
     grid->ex = E;
     E->leaves.assign(leaves, leaves + n);
@@ -395,6 +396,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     DX_CHECK(E->leaves[0] > 0 && E->leaves.back() <= grid->map.last_cell, DCCRGX_EINVAL, "invalid cell %llu",
              (unsigned long long)(E->leaves[0] == 0 ? 0 : E->leaves.back()));
     E->n = E->leaves.size();
+    E->build_dir();
     uint64_t cap = 16;
     while (cap < 2 * E->n) cap <<= 1;
     E->mask = cap - 1;
@@ -405,6 +407,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(E->n)), dim3(256), 0, st, E->d_leaves, E->n,
                        (unsigned long long*)E->d_keys, E->d_vals, E->mask);
     DX_HIP(hipGetLastError());
+    T.lap("leaves+hash");
     // ownership: the process of the level-0 ancestor (no load balancing),
     // block partition or the grid's SFC table
     E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
@@ -436,7 +439,9 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     std::vector<uint32_t> ident(E->local.size());
     for (uint64_t i = 0; i < ident.size(); i++) ident[i] = (uint32_t)i;
     DX_TRY(upload(ident, &E->d_local_slot, st));
+    T.lap("owners+local");
     DX_TRY(sync_slots(grid));
+    T.lap("sync_slots");
     return DCCRGX_OK;
 }
 
@@ -507,8 +512,8 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
         const uint32_t s = (uint32_t)E->slot_ids.size();
         E->slot_ids.push_back(c);
         E->extra[c] = s;
-        auto it = std::lower_bound(E->leaves.begin(), E->leaves.end(), c);
-        if (it != E->leaves.end() && *it == c) E->slot_of_g[it - E->leaves.begin()] = s;
+        const int64_t g = E->find(c);
+        if (g >= 0) E->slot_of_g[g] = s;
     }
     const uint64_t ns = E->slot_ids.size();
     DX_CHECK(ns < NO_SLOT, DCCRGX_EINVAL, "%llu storage slots on one rank", (unsigned long long)ns);
@@ -519,8 +524,8 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
             for (uint64_t k = old_ns; k < ns; k++) {
                 const uint64_t c = E->slot_ids[k];
                 E->extra.erase(c);
-                auto it = std::lower_bound(E->leaves.begin(), E->leaves.end(), c);
-                if (it != E->leaves.end() && *it == c) E->slot_of_g[it - E->leaves.begin()] = NO_SLOT;
+                const int64_t g = E->find(c);
+                if (g >= 0) E->slot_of_g[g] = NO_SLOT;
             }
             E->slot_ids.resize(old_ns);
             return s;
@@ -645,6 +650,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     if (nof_row[N]) DX_HIP(hipMemcpyAsync(L.h_nof_g.data(), h.d_nof_g, nof_row[N] * 4, hipMemcpyDeviceToHost, st));
     if (nto_row[N]) DX_HIP(hipMemcpyAsync(L.h_nto_g.data(), h.d_nto_g, nto_row[N] * 4, hipMemcpyDeviceToHost, st));
     DX_HIP(hipStreamSynchronize(st));
+    T.lap("lists to host");
     const std::vector<int32_t>& owner = E->owner;
     const int me = ctx->rank;
     std::set<uint64_t> remote;
@@ -679,6 +685,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     T.lap("classification");
     // ghost slots for this neighborhood's remote neighbors
     DX_TRY(explicit_add_slots(grid, h.remote));
+    T.lap("ghost slots");
 
     // stencil rows of local cells (iteration-cache neighbors_of: unique pairs)
     std::vector<uint64_t> tmp_row(nl + 1, 0);
@@ -710,6 +717,10 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     dx_free(d_pc);
 
     T.lap("stencil rows");
+    struct Lap {
+        PhaseTimer& t;
+        ~Lap() { t.lap("peer plans"); }
+    } lap_end{T};
     // per-peer plans: send from local slots, receive into ghost slots
     std::set<int> peers;
     for (auto& kv : send) peers.insert(kv.first);
@@ -963,10 +974,9 @@ int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t
     DX_HIP(hipStreamSynchronize(st));
     std::vector<uint64_t> orow(n + 1, 0), oids;
     for (size_t i = 0; i < n; i++) {
-        auto it = std::lower_bound(E->leaves.begin(), E->leaves.end(), hc[i]);
-        DX_CHECK(it != E->leaves.end() && *it == hc[i], DCCRGX_ENOTFOUND, "cell %llu does not exist",
-                 (unsigned long long)hc[i]);
-        const uint64_t g = (uint64_t)(it - E->leaves.begin());
+        const int64_t gi = E->find(hc[i]);
+        DX_CHECK(gi >= 0, DCCRGX_ENOTFOUND, "cell %llu does not exist", (unsigned long long)hc[i]);
+        const uint64_t g = (uint64_t)gi;
         for (uint64_t e = L.h_nto_row[g]; e < L.h_nto_row[g + 1]; e++) oids.push_back(E->leaves[L.h_nto_g[e]]);
         orow[i + 1] = oids.size();
     }

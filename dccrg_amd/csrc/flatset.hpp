@@ -1,0 +1,141 @@
+// flatset.hpp -- host-side set of cell ids for the AMR bookkeeping (no HIP).
+#pragma once
+
+#include <algorithm>
+#include <cstddef>
+#include <cstdint>
+#include <iterator>
+#include <vector>
+
+namespace dccrgx {
+
+// A set of nonzero cell ids (0 is error_cell): open addressing, linear
+// probing, backward-shift deletion.  The AMR request filters and
+// stop_refining do millions of membership tests per adaptive step, which a
+// node-based std::set spends in pointer chasing.  Iteration is in table
+// order; sorted() gives the ascending ids.
+class FlatSet {
+  public:
+    struct Inserted {
+        bool second;
+    };
+    FlatSet() = default;
+    template <class It>
+    FlatSet(It b, It e)
+    {
+        reserve((size_t)std::distance(b, e));
+        for (; b != e; ++b) insert(*b);
+    }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    void clear()
+    {
+        std::fill(t_.begin(), t_.end(), 0);
+        n_ = 0;
+    }
+    void reserve(size_t n)
+    {
+        size_t cap = 16;
+        while (cap < 2 * n + 2) cap <<= 1;
+        if (cap > t_.size()) rehash(cap);
+    }
+    size_t count(uint64_t x) const
+    {
+        if (!n_ || !x) return 0;
+        for (size_t i = slot(x);; i = (i + 1) & mask_) {
+            if (t_[i] == x) return 1;
+            if (!t_[i]) return 0;
+        }
+    }
+    Inserted insert(uint64_t x)
+    {
+        if (!x) return {false};
+        if (2 * (n_ + 1) > t_.size()) rehash(std::max<size_t>(16, 2 * t_.size()));
+        for (size_t i = slot(x);; i = (i + 1) & mask_) {
+            if (t_[i] == x) return {false};
+            if (!t_[i]) {
+                t_[i] = x;
+                n_++;
+                return {true};
+            }
+        }
+    }
+    size_t erase(uint64_t x)
+    {
+        if (!n_ || !x) return 0;
+        size_t i = slot(x);
+        for (;; i = (i + 1) & mask_) {
+            if (!t_[i]) return 0;
+            if (t_[i] == x) break;
+        }
+        // backward shift: move later entries of the probe run into the hole
+        size_t j = i;
+        for (;;) {
+            j = (j + 1) & mask_;
+            if (!t_[j]) break;
+            const size_t home = slot(t_[j]);
+            const bool stays = i <= j ? (i < home && home <= j) : (i < home || home <= j);
+            if (stays) continue;
+            t_[i] = t_[j];
+            i = j;
+        }
+        t_[i] = 0;
+        n_--;
+        return 1;
+    }
+    std::vector<uint64_t> sorted() const
+    {
+        std::vector<uint64_t> v;
+        v.reserve(n_);
+        for (uint64_t x : t_)
+            if (x) v.push_back(x);
+        std::sort(v.begin(), v.end());
+        return v;
+    }
+    class const_iterator {
+      public:
+        const_iterator(const uint64_t* p, const uint64_t* e) : p_(p), e_(e) { skip(); }
+        uint64_t operator*() const { return *p_; }
+        const_iterator& operator++()
+        {
+            ++p_;
+            skip();
+            return *this;
+        }
+        bool operator!=(const const_iterator& o) const { return p_ != o.p_; }
+
+      private:
+        void skip()
+        {
+            while (p_ != e_ && !*p_) ++p_;
+        }
+        const uint64_t* p_;
+        const uint64_t* e_;
+    };
+    const_iterator begin() const { return const_iterator(t_.data(), t_.data() + t_.size()); }
+    const_iterator end() const { return const_iterator(t_.data() + t_.size(), t_.data() + t_.size()); }
+
+  private:
+    size_t slot(uint64_t x) const
+    {
+        x ^= x >> 33;
+        x *= 0xff51afd7ed558ccdull;
+        x ^= x >> 33;
+        return (size_t)x & mask_;
+    }
+    void rehash(size_t cap)
+    {
+        std::vector<uint64_t> old;
+        old.swap(t_);
+        t_.assign(cap, 0);
+        mask_ = cap - 1;
+        n_ = 0;
+        for (uint64_t x : old)
+            if (x) insert(x);
+    }
+    std::vector<uint64_t> t_;
+    size_t mask_ = 0;
+    size_t n_ = 0;
+};
+
+}  // namespace dccrgx

@@ -708,8 +708,8 @@ int dccrgx_get_process(const dccrgx_grid* grid, const uint64_t* cells, size_t n,
             continue;
         }
         const Explicit* E = grid->ex;
-        auto it = std::lower_bound(E->leaves.begin(), E->leaves.end(), c);
-        out[i] = (it != E->leaves.end() && *it == c) ? E->owner[it - E->leaves.begin()] : -1;
+        const int64_t g = E->find(c);
+        out[i] = g >= 0 ? E->owner[g] : -1;
     }
     return DCCRGX_OK;
 }

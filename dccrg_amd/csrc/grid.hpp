@@ -2,6 +2,7 @@
 // per-peer halo plans, field pools.
 #pragma once
 
+#include "flatset.hpp"
 #include "internal.hpp"
 
 #include <set>
@@ -153,6 +154,39 @@ struct Explicit {
         uint32_t* d_all_pos = nullptr;
     };
     std::map<int32_t, HoodLists> hl;
+    // host lookups into `leaves` (the AMR request filters and stop_refining
+    // query it millions of times per adaptive step): a bucket directory over
+    // the id range -- dir[b] = first leaf whose bucket is >= b, ~0.5 leaves
+    // per bucket -- narrows each search to a bucket
+    std::vector<uint32_t> dir;
+    uint64_t dir_base = 0;
+    int dir_shift = 0;
+    void build_dir()
+    {
+        dir.clear();
+        if (leaves.empty()) return;
+        dir_base = leaves.front();
+        const uint64_t span = leaves.back() - dir_base + 1;
+        uint64_t nb = 16;
+        while (nb < 2 * leaves.size() && nb < (1ull << 30)) nb <<= 1;
+        dir_shift = 0;
+        while ((span >> dir_shift) >= nb) dir_shift++;
+        nb = (span >> dir_shift) + 1;
+        dir.assign(nb + 1, (uint32_t)leaves.size());
+        uint64_t b = 0;
+        for (size_t i = 0; i < leaves.size(); i++) {
+            const uint64_t bi = (leaves[i] - dir_base) >> dir_shift;
+            while (b <= bi) dir[b++] = (uint32_t)i;
+        }
+    }
+    int64_t find(uint64_t c) const  // global index of a leaf, -1 if none
+    {
+        if (dir.empty() || c < dir_base || c > leaves.back()) return -1;
+        const uint64_t b = (c - dir_base) >> dir_shift;
+        const auto lo = leaves.begin() + dir[b], hi = leaves.begin() + dir[b + 1];
+        const auto it = std::lower_bound(lo, hi, c);
+        return (it != hi && *it == c) ? (int64_t)(it - leaves.begin()) : -1;
+    }
     // data of cells removed by the last stop_refining (refined parents and
     // unrefined children of this rank), readable until
     // clear_refined_unrefined_data (dccrg.hpp:3519-3543, 5550-5567): ascending
@@ -165,7 +199,7 @@ struct Explicit {
 struct LoadState;
 
 struct Amr {
-    std::set<uint64_t> to_refine, not_to_refine, to_unrefine, not_to_unrefine;
+    FlatSet to_refine, not_to_refine, to_unrefine, not_to_unrefine;
     std::vector<uint64_t> new_cells, removed;
 };
 
@@ -284,6 +318,8 @@ struct ExRegion {
 };
 constexpr uint32_t NO_SLOT = 0xffffffffu;
 int explicit_region(const dccrgx_grid* grid, const Hood& h, int32_t region, ExRegion* out);
+// storage slot of each id (-1: none), on the device
+int explicit_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int64_t* slots, hipStream_t st);
 // explicit (mixed refinement level) grids, explicit.hip
 int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n);
 void explicit_destroy(dccrgx_grid* grid);

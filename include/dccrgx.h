@@ -374,6 +374,17 @@ int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f
 int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
                               double diff_increase, double diff_threshold, double unrefine_sensitivity,
                               int8_t* marks_out, double* max_diff_out);
+/* check_for_adaptation, tests/advection/adapter.hpp:43-176, complete: the
+ * marks above turned into the reference's three sets per sibling group
+ * (:109-176) on the device -- to_refine: cells marked 2; not_to_unrefine: the
+ * first (lowest id) cell marked 1 of a group without a 2, level > 0;
+ * to_unrefine: cells marked 0, level > 0, in a group without a 1 or 2.
+ * Each output holds up to `cap` >= local cell count ids, ascending; counts[3]
+ * receives the three sizes.  Nothing on a grid with maximum level 0. */
+int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
+                                  double diff_increase, double diff_threshold, double unrefine_sensitivity,
+                                  uint64_t* to_refine, uint64_t* not_to_unrefine, uint64_t* to_unrefine, size_t cap,
+                                  size_t counts[3]);
 /* one step of tests/advection/2d.cpp:321-390: density halo start, inner
  * fluxes, halo wait, outer fluxes, apply */
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt);

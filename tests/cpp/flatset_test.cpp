@@ -1,0 +1,43 @@
+// FlatSet (dccrg_amd/csrc/flatset.hpp) against std::set under random
+// inserts, erases and lookups, including ids that collide in the table.
+#include <cstdio>
+#include <random>
+#include <set>
+
+#include "flatset.hpp"
+
+int main()
+{
+    std::mt19937_64 rng(7);
+    for (int round = 0; round < 40; round++) {
+        dccrgx::FlatSet f;
+        std::set<uint64_t> s;
+        const uint64_t range = round % 2 ? 64 : 1 + (rng() % 100000);
+        for (int op = 0; op < 20000; op++) {
+            const uint64_t x = rng() % (range + 1);  // 0 (error_cell) is never stored
+            switch (rng() % 4) {
+            case 0:
+            case 1: {
+                const bool a = f.insert(x).second, b = x && s.insert(x).second;
+                if (a != b) return std::printf("insert %llu\n", (unsigned long long)x), 1;
+                break;
+            }
+            case 2:
+                if (f.erase(x) != s.erase(x)) return std::printf("erase %llu\n", (unsigned long long)x), 1;
+                break;
+            default:
+                if (f.count(x) != s.count(x)) return std::printf("count %llu\n", (unsigned long long)x), 1;
+            }
+            if (f.size() != s.size()) return std::printf("size\n"), 1;
+        }
+        const std::vector<uint64_t> v = f.sorted();
+        if (v != std::vector<uint64_t>(s.begin(), s.end())) return std::printf("sorted\n"), 1;
+        size_t n = 0;
+        for (uint64_t x : f) n += s.count(x);
+        if (n != s.size()) return std::printf("iteration\n"), 1;
+        f.clear();
+        if (!f.empty() || f.count(v.empty() ? 1 : v[0])) return std::printf("clear\n"), 1;
+    }
+    std::printf("PASS\n");
+    return 0;
+}

@@ -255,6 +255,11 @@ def test_adaptive_advection_matches_oracle(cells, M, steps):
     for s in range(steps):
         g.update_copies_of_remote_neighbors(fields=["density"])
         sets = A.check_for_adaptation(g, rel / M, thr, sens)
+        # the three sets themselves (device sibling-group pass) equal the
+        # reference loop's, cell for cell
+        want = ref.check_for_adaptation()[0]
+        for got, w in zip(sets, want):
+            assert [int(c) for c in got] == list(w), f"step {s}"
         g.advect_step(cfl * dt)
         A.adapt_grid(g, geom, *sets)
         dt = g.max_time_step()

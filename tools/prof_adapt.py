@@ -38,18 +38,29 @@ def loop():
         g.advect_step(cfl * dt)
         ctx.synchronize()
         t2 = time.perf_counter()
-        A.request_adaptation(g, *sets)
+        tr = []
+        for kind, ids in ((X.AMR_REFINE, sets[0]), (X.AMR_DONT_UNREFINE, sets[1]), (X.AMR_UNREFINE, sets[2])):
+            A._request(g, kind, ids)
+            tr.append(time.perf_counter())
+        g._refresh_info()
         ta = time.perf_counter()
+        print(f"  check {1e3*(t1-t0):.1f} requests: refine {len(sets[0])} {1e3*(tr[0]-t2):.1f} "
+              f"dont_unrefine {len(sets[1])} {1e3*(tr[1]-tr[0]):.1f} unrefine {len(sets[2])} {1e3*(tr[2]-tr[1]):.1f}"
+              f" refresh {1e3*(ta-tr[2]):.1f} ms", flush=True)
         new = g.stop_refining()
         g.get_removed_cells()
         ctx.synchronize()
         tb = time.perf_counter()
         fd = np.array([g.field_id("density")], dtype=np.int32)
         X.check(D.lib().dccrgx_amr_copy_from_parents(g._h, fd.ctypes.data_as(X._i32p), fd.size))
+        tp = time.perf_counter()
         X.check(D.lib().dccrgx_amr_average_children(g._h, fd.ctypes.data_as(X._i32p), fd.size))
+        tq = time.perf_counter()
         g.clear_refined_unrefined_data()
         ctx.synchronize()
         tc = time.perf_counter()
+        print(f"  data: copy_from_parents {1e3*(tp-tb):.1f} average_children {1e3*(tq-tp):.1f} "
+              f"clear {1e3*(tc-tq):.1f} ms", flush=True)
         A._velocities_lengths(g, geom)
         ctx.synchronize()
         td = time.perf_counter()
