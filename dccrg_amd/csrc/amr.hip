@@ -655,13 +655,44 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     // entered, a fixed property of the cell), and u is dropped if any visited
     // cell is finer than u or of u's size and about to be refined: an
     // existence test over that closure, independent of the visiting order.
-    // Requests are independent and only read R, NU and the leaf set, so they
-    // are split over host threads, each with its own memo of the face graph
-    // (siblings' walks cover the same cells).
+    // Requests are independent and only read R, NU and the leaf set.  The
+    // outcome depends on u only through its parent: the sibling test reads
+    // the parent's children, and the walk's closure is the same from every
+    // sibling -- the siblings of a requested u are leaves (unrefine_completely
+    // refuses u otherwise, :2617-2628, against the same leaf set), face
+    // adjacent inside the parent and neighbors of it, so a walk from any one
+    // reaches all of them and their faces; the face neighbors of u it starts
+    // from are neighbors of the parent.  So the walk runs once per parent,
+    // the parents split over host threads, each with its own memo of the
+    // face graph.
     FlatSet final_un;
     {
         const std::vector<uint64_t> Uv = U.sorted();
-        std::vector<uint8_t> keep(Uv.size(), 0);
+        std::vector<uint64_t> par(Uv.size());
+        for (size_t i = 0; i < Uv.size(); i++) par[i] = v.parent(Uv[i]);
+        // (parent, requested child): one per parent whose children are all
+        // leaves; a request set not filtered by unrefine_completely keeps one
+        // walk per child
+        std::vector<std::pair<uint64_t, uint64_t>> pu;
+        pu.reserve(Uv.size());
+        for (size_t i = 0; i < Uv.size(); i++) pu.emplace_back(par[i], Uv[i]);
+        std::sort(pu.begin(), pu.end());
+        auto all_leaves = [&](uint64_t p) {
+            uint64_t ch[8];
+            v.children(p, ch);
+            for (uint64_t c : ch)
+                if (c && !v.exists(c)) return false;
+            return true;
+        };
+        {
+            size_t w = 0;
+            for (size_t i = 0; i < pu.size(); i++) {
+                if (w && pu[w - 1].first == pu[i].first && all_leaves(pu[i].first)) continue;
+                pu[w++] = pu[i];
+            }
+            pu.resize(w);
+        }
+        std::vector<uint8_t> keep(pu.size(), 0);
         auto work = [&](size_t b, size_t e) {
             std::unordered_map<uint64_t, std::array<uint64_t, 6>> memo;
             auto face = [&](uint64_t c) -> const std::array<uint64_t, 6>& {
@@ -674,8 +705,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
             std::unordered_set<uint64_t> seen;  // processed or queued
             std::vector<uint64_t> queue;
             for (size_t i = b; i < e; i++) {
-                const uint64_t u = Uv[i];
-                const uint64_t parent = v.parent(u);
+                const uint64_t parent = pu[i].first, u = pu[i].second;
                 uint64_t sib[8];
                 v.children(parent, sib);
                 bool can = true;
@@ -703,9 +733,17 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
                 keep[i] = can ? 1 : 0;
             }
         };
-        parallel_ranges(Uv.size(), 256, work);
+        parallel_ranges(pu.size(), 64, work);
+        FlatSet ok_parent, split;  // split: parents walked per child
+        for (size_t i = 0; i + 1 < pu.size(); i++)
+            if (pu[i].first == pu[i + 1].first) split.insert(pu[i].first);
+        for (size_t i = 0; i < pu.size(); i++) {
+            if (!keep[i]) continue;
+            if (split.count(pu[i].first)) final_un.insert(pu[i].second);
+            else ok_parent.insert(pu[i].first);
+        }
         for (size_t i = 0; i < Uv.size(); i++)
-            if (keep[i]) final_un.insert(Uv[i]);
+            if (ok_parent.count(par[i])) final_un.insert(Uv[i]);
     }
 
     T.lap("override_unrefines");

@@ -325,14 +325,21 @@ static ExView view(const dccrgx_grid* grid)
     return v;
 }
 
-static int scan_counts_u32(const uint32_t* d_cnt, uint64_t n, std::vector<uint64_t>& row, hipStream_t st)
+__global__ void __launch_bounds__(256) k_counts_to_row(const uint32_t* __restrict__ cnt, uint64_t n,
+                                                       uint64_t* __restrict__ row)
 {
-    std::vector<uint32_t> h(n);
-    if (n) DX_HIP(hipMemcpyAsync(h.data(), d_cnt, n * 4, hipMemcpyDeviceToHost, st));
-    DX_HIP(hipStreamSynchronize(st));
-    row.assign(n + 1, 0);
-    for (uint64_t i = 0; i < n; i++) row[i + 1] = row[i] + h[i];
-    return DCCRGX_OK;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) row[i + 1] = cnt[i];
+}
+
+// CSR row offsets (n + 1, device, allocated here) of per-row counts on the
+// device; *total (host) = row[n]
+static int scan_counts_device(const uint32_t* d_cnt, uint64_t n, uint64_t** d_row, uint64_t* total, hipStream_t st)
+{
+    DX_HIP(dx_malloc(d_row, (n + 1) * 8));
+    if (n) hipLaunchKernelGGL(k_counts_to_row, dim3(grid_for(n)), dim3(256), 0, st, d_cnt, n, *d_row);
+    DX_HIP(hipGetLastError());
+    return device_scan_rows(*d_row, n, st, total);
 }
 
 template <class T>
@@ -455,8 +462,11 @@ static int sync_slots(dccrgx_grid* grid)
     dx_free(E->d_level);
     E->d_slot_of_g = nullptr;
     E->d_level = nullptr;
-    std::vector<uint8_t> level(E->slot_ids.size());
-    for (size_t s = 0; s < level.size(); s++) level[s] = (uint8_t)map_level(grid->map, E->slot_ids[s]);
+    // slots only ever append (or roll back), so only new slots' levels are computed
+    std::vector<uint8_t>& level = E->h_level;
+    if (level.size() > E->slot_ids.size()) level.resize(E->slot_ids.size());
+    for (size_t s = level.size(); s < E->slot_ids.size(); s++)
+        level.push_back((uint8_t)map_level(grid->map, E->slot_ids[s]));
     DX_TRY(upload(E->slot_of_g, &E->d_slot_of_g, st));
     DX_TRY(upload(level, &E->d_level, st));
     DX_HIP(hipStreamSynchronize(st));
@@ -612,20 +622,20 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     DX_HIP(hipMemsetAsync(d_cnt, 0, N * 4, st));
     DX_HIP(hipMemsetAsync(d_cur, 0, N * 4, st));
     hipLaunchKernelGGL(k_tr_count, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_cnt);
-    std::vector<uint64_t> trow;
-    DX_TRY(scan_counts_u32(d_cnt, N, trow, st));
     uint64_t* d_trow = nullptr;
-    DX_TRY(upload(trow, &d_trow, st));
-    DX_HIP(dx_malloc(&d_tmp, std::max<uint64_t>(trow[N], 1) * 4));
+    uint64_t ttot = 0;
+    DX_TRY(scan_counts_device(d_cnt, N, &d_trow, &ttot, st));
+    DX_HIP(dx_malloc(&d_tmp, std::max<uint64_t>(ttot, 1) * 4));
     hipLaunchKernelGGL(k_tr_scatter, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_trow,
                        d_cur, d_tmp);
     DX_HIP(dx_malloc(&d_ucnt, N * 4));
     hipLaunchKernelGGL(k_sort_unique_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, N, d_tmp, d_ucnt);
     DX_HIP(hipGetLastError());
-    std::vector<uint64_t> nto_row;
-    DX_TRY(scan_counts_u32(d_ucnt, N, nto_row, st));
-    DX_TRY(upload(nto_row, &h.d_nto_row, st));
-    DX_HIP(dx_malloc(&h.d_nto_g, std::max<uint64_t>(nto_row[N], 1) * 4));
+    uint64_t ntot = 0;
+    DX_TRY(scan_counts_device(d_ucnt, N, &h.d_nto_row, &ntot, st));
+    std::vector<uint64_t> nto_row(N + 1);
+    DX_HIP(hipMemcpyAsync(nto_row.data(), h.d_nto_row, (N + 1) * 8, hipMemcpyDeviceToHost, st));
+    DX_HIP(dx_malloc(&h.d_nto_g, std::max<uint64_t>(ntot, 1) * 4));
     hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, d_tmp, h.d_nto_row, N, h.d_nto_g);
     DX_HIP(hipGetLastError());
     dx_free(d_cnt);
@@ -702,11 +712,10 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     if (nl)
         hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
                            h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
-    std::vector<uint64_t> st_row;
-    DX_TRY(scan_counts_u32(d_pc, nl, st_row, st));
-    DX_TRY(upload(st_row, &h.d_st_row, st));
-    DX_HIP(dx_malloc(&h.d_st_slot, std::max<uint64_t>(st_row[nl], 1) * 4));
-    DX_HIP(dx_malloc(&h.d_st_off, std::max<uint64_t>(st_row[nl], 1) * 12));
+    uint64_t stot = 0;
+    DX_TRY(scan_counts_device(d_pc, nl, &h.d_st_row, &stot, st));
+    DX_HIP(dx_malloc(&h.d_st_slot, std::max<uint64_t>(stot, 1) * 4));
+    DX_HIP(dx_malloc(&h.d_st_off, std::max<uint64_t>(stot, 1) * 12));
     if (nl)
         hipLaunchKernelGGL(k_stencil_slots, dim3(grid_for(nl)), dim3(256), 0, st, d_tmp_row, d_pairs, h.d_st_row, nl,
                            E->d_slot_of_g, h.d_st_slot, h.d_st_off);

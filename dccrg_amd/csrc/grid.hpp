@@ -144,6 +144,7 @@ struct Explicit {
     uint32_t* d_slot_of_g = nullptr;
     uint32_t* d_local_slot = nullptr;               // local position -> slot (identity)
     uint8_t* d_level = nullptr;                     // refinement level of each slot
+    std::vector<uint8_t> h_level;                   // host copy
     bool defer_fields = false;                      // rebuild(): fields are moved afterwards
     struct HoodLists {
         std::vector<uint64_t> h_nof_row, h_nto_row;
