@@ -214,7 +214,7 @@ def secondary(ctx, torch, D):
                         "prerefine_s": t_pre}
     # (b) adaptive loop
     g.update_copies_of_remote_neighbors(fields=list(A.ALL))
-    steps, cells_steps = 5, 0
+    steps, cells_steps = 20, 0
     t_adapt = 0.0
     t0 = time.perf_counter()
     for _ in range(steps):

@@ -838,6 +838,26 @@ public:
         for (auto& kv : hs(hood).recv) n += kv.second.size();
         return n;
     }
+    // dccrg.hpp:7153-7184: default-constructed copies of the neighborhood's
+    // remote neighbors (already present here: build_hood allocates them)
+    Dccrg& allocate_copies_of_remote_neighbors(int hood = default_neighborhood_id)
+    {
+        if (!hoods_.count(hood)) throw std::invalid_argument("Neighborhood with given id doesn't exist.");
+        for (uint64_t c : hs(hood).remote_ids) remote_data_[c];
+        return *this;
+    }
+    // dccrg.hpp:2828-2955: face neighbors (the face graph neighbor and, for a
+    // smaller one, its siblings sharing the face) with directions +-1/2/3;
+    // empty for a cell that is not an existing leaf (the reference aborts)
+    std::vector<std::pair<uint64_t, int>> get_face_neighbors_of(uint64_t cell) const
+    {
+        std::vector<std::pair<uint64_t, int>> out;
+        uint64_t row[2] = {0, 0}, ids[24];
+        int32_t dirs[24];
+        if (dccrgx_face_neighbors_of_host(grid_, &cell, 1, row, ids, dirs, 24) != DCCRGX_OK) return out;
+        for (uint64_t e = row[0]; e < row[1]; e++) out.emplace_back(ids[e], (int)dirs[e]);
+        return out;
+    }
     std::vector<uint64_t> get_remote_cells_on_process_boundary(int hood = default_neighborhood_id, bool = false) const
     {
         return hoods_.count(hood) ? hs(hood).remote_ids : std::vector<uint64_t>();

@@ -299,6 +299,19 @@ static int cells(int argc, char** argv)
         if (grid.get_local_cells_not_on_process_boundary(hood) != grid.get_cells()) abort();
     }
     if (!grid.get_cells({dccrg::has_local_neighbor_of}, false, 99).empty()) abort();  // unknown hood
+    for (uint64_t c : grid.get_cells()) {
+        printf("face %llu :", (unsigned long long)c);
+        for (const auto& f : grid.get_face_neighbors_of(c)) printf(" %llu/%d", (unsigned long long)f.first, f.second);
+        printf("\n");
+    }
+    grid.allocate_copies_of_remote_neighbors(7);
+    bool threw = false;
+    try {
+        grid.allocate_copies_of_remote_neighbors(99);
+    } catch (const std::invalid_argument&) {
+        threw = true;
+    }
+    if (!threw) abort();
     return 0;
 }
 

@@ -169,10 +169,16 @@ def test_facade_get_cells_criteria(dims, per, hood):
     pers = tuple(bool(p) for p in per)
     grids = {0: O.Grid(dims, 0, pers, hood)}
     n = int(np.prod(dims))
-    got = {}
+    got, faces = {}, {}
     for line in run("cells", *dims, *per, hood).strip().splitlines():
         head, _, ids = line.partition(":")
-        got[head.strip()] = [int(x) for x in ids.split()]
+        if head.startswith("face "):
+            faces[int(head.split()[1])] = [(int(a), int(b)) for a, b in (t.split("/") for t in ids.split())]
+        else:
+            got[head.strip()] = [int(x) for x in ids.split()]
+    # get_face_neighbors_of (dccrg.hpp:2828-2955) of every cell
+    for cid in range(1, n + 1):
+        assert faces[cid] == [(int(i), int(d)) for i, d in grids[0].face_neighbors_of(cid)], cid
     for h, items in ((0, None), (7, [(1, 0, 0)])):
         g = grids[0]
         types = {}
