@@ -18,9 +18,11 @@
 // TYPE = cell type (:94-131).
 #include <cfloat>
 #include <cmath>
+#include <unordered_map>
 #include <vector>
 
 #include "face.hpp"
+
 #include "grid.hpp"
 
 namespace dccrgx {
@@ -471,6 +473,173 @@ __global__ void __launch_bounds__(SB) k_solo(PPtrs p, PSys s, PState* S, double 
     if (threadIdx.x == 0) *S = T;
 }
 
+// Small systems (at most SL info cells, one rank): one thread per cell for
+// the whole solve, the cell's vectors in registers and the two searched
+// directions p0 / p1 in LDS, so A.p0 and A^T.p1 gather from LDS instead of
+// global memory.  The first EK face-neighbor entries of a cell live in
+// registers with their factors (m of A.p0, the neighbor's reversed factor of
+// A^T.p1, each /4 for a finer neighbor, computed once as the per-iteration
+// code computes them); a neighbor outside the info cells never changes during
+// the solve, so its product with the factor is kept instead.  Further entries
+// are read each iteration as k_solo does.  Sums are per wave (shuffles) then
+// over the 16 waves in a fixed order; every thread runs the scalar control on
+// its own copy of the state, so no broadcast is needed.  Same arithmetic per
+// cell as k_solo; only the summation order of the dot products differs.
+// The 2-norm residual only (the reference's default p_of_norm; pow() would
+// push the kernel past its registers).
+constexpr int SL = 1024;
+constexpr int EK = 6;
+
+__device__ __forceinline__ double wg_sum(double v, double* ws)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = 0;
+#pragma unroll
+    for (int k = 0; k < SL / 64; k++) r += ws[k];
+    __syncthreads();
+    return r;
+}
+
+__global__ void __launch_bounds__(SL) k_solo_lds(PPtrs p, PSys s, const int32_t* __restrict__ ej, PState* S,
+                                                double stop_residual, double increase, uint32_t min_it,
+                                                uint32_t max_it)
+{
+#pragma clang fp contract(off)
+    __shared__ double lp0[SL], lp1[SL], ws[SL / 64];
+    const uint32_t i = threadIdx.x;
+    const bool have = i < s.n;
+    uint64_t c = 0, e0 = 0, e1 = 0;
+    bool solve = false;
+    double sf = 0, x0 = 0, x1 = 0, r0 = 0, r1 = 0, sol = 0, best = 0, adp = 0;
+    int32_t jr[EK];
+    double ma[EK], mt[EK];
+#pragma unroll
+    for (int k = 0; k < EK; k++) {
+        jr[k] = -2;  // no entry
+        ma[k] = mt[k] = 0;
+    }
+    if (have) {
+        c = s.slot[i];
+        solve = p.type[c] == SOLVE;
+        sf = p.sf[c];
+        x0 = p.p0[c];
+        x1 = p.p1[c];
+        r0 = p.r0[c];
+        r1 = p.r1[c];
+        sol = p.sol[c];
+        best = p.best[c];
+        adp = p.adp0[c];
+        e0 = s.row[i];
+        e1 = s.row[i + 1];
+#pragma unroll
+        for (int k = 0; k < EK; k++) {
+            const uint64_t e = e0 + k;
+            if (e >= e1) continue;
+            const int code = s.code[e];
+            const int dir = (code & 15) - 3;
+            const uint64_t nb = s.nb[e];
+            double m = p.f[fidx(dir)][c], m2 = p.f[fidx(-dir)][nb];
+            if ((code >> 4) - 1 > 0) {
+                m /= 4.0;
+                m2 /= 4.0;
+            }
+            jr[k] = ej[e];
+            if (jr[k] >= 0) {
+                ma[k] = m;
+                mt[k] = m2;
+            } else {  // constant neighbor: the products themselves
+                ma[k] = m * p.p0[nb];
+                mt[k] = m2 * p.p1[nb];
+            }
+        }
+        lp0[i] = x0;
+        lp1[i] = x1;
+    }
+    __shared__ PState T0;
+    if (threadIdx.x == 0) T0 = *S;
+    __syncthreads();
+    PState T = T0;  // every thread's own copy (a direct load of *S miscompiles at -O2+)
+    for (;;) {
+        // A . p0 and p1 . (A . p0)
+        double acc = 0;
+        if (have && solve) {
+            double a = sf * x0;
+#pragma unroll
+            for (int k = 0; k < EK; k++)
+                if (jr[k] != -2) a += jr[k] >= 0 ? ma[k] * lp0[jr[k]] : ma[k];
+            for (uint64_t e = e0 + EK; e < e1; e++) {
+                const int code = s.code[e];
+                double m = p.f[fidx((code & 15) - 3)][c];
+                if ((code >> 4) - 1 > 0) m /= 4.0;
+                const int32_t j = ej[e];
+                a += m * (j >= 0 ? lp0[j] : p.p0[s.nb[e]]);
+            }
+            adp = a;
+            acc = x1 * a;
+        }
+        double v = wg_sum(acc, ws);
+        control(&T, PH_ALPHA, v, 2.0, stop_residual, increase, min_it, max_it);
+        if (T.done) break;
+        // solution update and |r0|^p over every info cell
+        acc = 0;
+        if (have) {
+            if (solve) sol += T.alpha * x0;
+            acc = fabs(r0) * fabs(r0);  // pw(|r0|, 2)
+        }
+        v = wg_sum(acc, ws);
+        control(&T, PH_RES, v, 2.0, stop_residual, increase, min_it, max_it);
+        // best solution, r0 and r1, r0 . r1
+        acc = 0;
+        if (have && solve) {
+            if (T.save) best = sol;
+            if (!T.halt) {
+                const double nr0 = r0 - T.alpha * adp;
+                double a = sf * x1;
+#pragma unroll
+                for (int k = 0; k < EK; k++)
+                    if (jr[k] != -2) a += jr[k] >= 0 ? mt[k] * lp1[jr[k]] : mt[k];
+                for (uint64_t e = e0 + EK; e < e1; e++) {
+                    const int code = s.code[e];
+                    const uint64_t nb = s.nb[e];
+                    double m = p.f[fidx(-((code & 15) - 3))][nb];
+                    if ((code >> 4) - 1 > 0) m /= 4.0;
+                    const int32_t j = ej[e];
+                    a += m * (j >= 0 ? lp1[j] : p.p1[nb]);
+                }
+                r1 = r1 - T.alpha * a;
+                r0 = nr0;
+                acc = r0 * r1;
+            }
+        }
+        v = wg_sum(acc, ws);
+        control(&T, PH_BETA, v, 2.0, stop_residual, increase, min_it, max_it);
+        if (T.done) break;
+        if (have && solve) {
+            x0 = r0 + T.beta * x0;
+            x1 = r1 + T.beta * x1;
+            lp0[i] = x0;
+            lp1[i] = x1;
+        }
+        __syncthreads();  // the next A . p0 reads the neighbors' p0
+        if (T.end) {
+            T.done = 1;
+            break;
+        }
+    }
+    if (have && solve) {
+        p.sol[c] = sol;
+        p.best[c] = best;
+        p.p0[c] = x0;
+        p.p1[c] = x1;
+        p.r0[c] = r0;
+        p.r1[c] = r1;
+        p.adp0[c] = adp;
+    }
+    if (threadIdx.x == 0) *S = T;
+}
+
 __global__ void __launch_bounds__(256) k_rel(const uint64_t* __restrict__ cells, const uint64_t* __restrict__ row,
                                              const uint64_t* __restrict__ ids, uint64_t n, MapParams mp,
                                              int8_t* __restrict__ rel)
@@ -524,14 +693,15 @@ struct dccrgx_poisson {
     uint64_t n_info = 0;
     uint64_t *d_slot = nullptr, *d_row = nullptr, *d_nb = nullptr;
     int32_t* d_code = nullptr;
+    int32_t* d_ej = nullptr;  // k_solo_lds: info index of each entry's neighbor, -1 outside the info cells
     PState* d_state = nullptr;
     double* d_part = nullptr;
 
     void free_cache()
     {
-        for (void* q : {(void*)d_slot, (void*)d_row, (void*)d_nb, (void*)d_code}) dx_free(q);
+        for (void* q : {(void*)d_slot, (void*)d_row, (void*)d_nb, (void*)d_code, (void*)d_ej}) dx_free(q);
         d_slot = d_row = d_nb = nullptr;
-        d_code = nullptr;
+        d_code = d_ej = nullptr;
         n_info = 0;
         cached = false;
     }
@@ -796,6 +966,17 @@ int build_cache(dccrgx_poisson* P, const uint64_t* cells, size_t n, const uint64
         DX_HIP(hipMemcpyAsync(P->d_nb, nb.data(), nb.size() * 8, hipMemcpyHostToDevice, st));
         DX_HIP(hipMemcpyAsync(P->d_code, code.data(), code.size() * 4, hipMemcpyHostToDevice, st));
     }
+    if (P->n_info <= (uint64_t)SL) {  // k_solo_lds's neighbor indices
+        std::unordered_map<uint64_t, int32_t> info_of;
+        for (size_t k = 0; k < info_slot.size(); k++) info_of[info_slot[k]] = (int32_t)k;
+        std::vector<int32_t> ej(nb.size());
+        for (size_t e = 0; e < nb.size(); e++) {
+            auto it = info_of.find(nb[e]);
+            ej[e] = it == info_of.end() ? -1 : it->second;
+        }
+        DX_TRY(dalloc(&P->d_ej, ej.size()));
+        if (!ej.empty()) DX_HIP(hipMemcpyAsync(P->d_ej, ej.data(), ej.size() * 4, hipMemcpyHostToDevice, st));
+    }
     if (P->n_info)
         hipLaunchKernelGGL(k_scaling, dim3(blocks_for(P->n_info)), dim3(256), 0, st, P->ptrs(), P->sys());
     DX_HIP(hipGetLastError());
@@ -878,8 +1059,12 @@ int dccrgx_poisson_solve(dccrgx_poisson* P, const uint64_t* cells, size_t n, con
                       !getenv("DCCRGX_POISSON_MULTI");
     if (solo) {
         const dccrgx_poisson_params& q = P->prm;
-        hipLaunchKernelGGL(k_solo, dim3(1), dim3(SB), 0, st, p, s, P->d_state, pn, q.stop_residual,
-                           q.stop_after_residual_increase, q.min_iterations, q.max_iterations);
+        if (P->d_ej && pn == 2.0 && !getenv("DCCRGX_POISSON_SOLO_GLOBAL"))
+            hipLaunchKernelGGL(k_solo_lds, dim3(1), dim3(SL), 0, st, p, s, (const int32_t*)P->d_ej, P->d_state,
+                               q.stop_residual, q.stop_after_residual_increase, q.min_iterations, q.max_iterations);
+        else
+            hipLaunchKernelGGL(k_solo, dim3(1), dim3(SB), 0, st, p, s, P->d_state, pn, q.stop_residual,
+                               q.stop_after_residual_increase, q.min_iterations, q.max_iterations);
         DX_HIP(hipGetLastError());
         DX_HIP(hipMemcpyAsync(&hs, P->d_state, sizeof(PState), hipMemcpyDeviceToHost, st));
     }
