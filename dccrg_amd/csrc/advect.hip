@@ -555,13 +555,13 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
                            (uint32_t*)nullptr, (int8_t*)nullptr);
     DX_HIP(hipGetLastError());
     std::vector<uint32_t> cnt(n);
-    if (n) DX_HIP(hipMemcpyAsync(cnt.data(), d_cnt, n * 4, hipMemcpyDeviceToHost, st));
+    DX_TRY(dx_d2h(grid->ctx, cnt.data(), d_cnt, n * 4, st));
     DX_HIP(hipStreamSynchronize(st));
     dx_free(d_cnt);
     std::vector<uint64_t> row(n + 1, 0);
     for (uint64_t q = 0; q < n; q++) row[q + 1] = row[q] + cnt[q];
     fc->overflow = row[n] > 0;
-    DX_HIP(hipMemcpyAsync(fc->o_row, row.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    DX_TRY(dx_h2d(grid->ctx, fc->o_row, row.data(), (n + 1) * 8, st));
     DX_HIP(dx_malloc(&fc->o_slot, std::max<uint64_t>(row[n], 1) * 4));
     DX_HIP(dx_malloc(&fc->o_dir, std::max<uint64_t>(row[n], 1)));
     if (fc->overflow)
@@ -674,12 +674,11 @@ int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f
     unsigned long long* d = nullptr;
     DX_HIP(dx_malloc((void**)&d, 8));
     const unsigned long long init = 0xffffffffffffffffull;  // above every key
-    DX_HIP(hipMemcpyAsync(d, &init, 8, hipMemcpyHostToDevice, st));
+    DX_TRY(dx_h2d(grid->ctx, d, &init, 8, st));
     hipLaunchKernelGGL(k_max_dt, dim3(std::min<unsigned>(grid_for(n), 1024)), dim3(256), 0, st, p, s0, n, slots, d);
     DX_HIP(hipGetLastError());
     unsigned long long k = 0;
-    DX_HIP(hipMemcpyAsync(&k, d, 8, hipMemcpyDeviceToHost, st));
-    DX_HIP(hipStreamSynchronize(st));
+    DX_TRY(dx_d2h(grid->ctx, &k, d, 8, st));
     dx_free(d);
     if (k != init) *local_min = dunkey(k);
     return DCCRGX_OK;
@@ -724,7 +723,7 @@ int adapt_marks_device(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_f
     hipLaunchKernelGGL(k_adapt_marks, dim3(grid_for(n)), dim3(256), 0, st, (const unsigned long long*)d_max,
                        R.local_slot, R.level, n, diff_increase, unrefine_sensitivity, d_marks, d_diff);
     DX_HIP(hipGetLastError());
-    if (max_diff_out) DX_HIP(hipMemcpyAsync(max_diff_out, d_diff, n * 8, hipMemcpyDeviceToHost, st));
+    if (max_diff_out) DX_TRY(dx_d2h(grid->ctx, max_diff_out, d_diff, n * 8, st));
     dx_free(d_max);  // dx_free waits for the kernels above
     dx_free(d_flag);
     dx_free(d_diff);
@@ -747,12 +746,9 @@ int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_a
                               max_diff_out));
     if (!d_marks) return DCCRGX_OK;
     hipStream_t st = grid->ctx->compute;
-    const hipError_t e = hipMemcpyAsync(marks_out, d_marks, grid->n_local, hipMemcpyDeviceToHost, st);
-    const hipError_t e2 = hipStreamSynchronize(st);
+    const int e = dx_d2h(grid->ctx, marks_out, d_marks, grid->n_local, st);
     dx_free(d_marks);
-    DX_HIP(e);
-    DX_HIP(e2);
-    return DCCRGX_OK;
+    return e;
 }
 
 int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
@@ -789,10 +785,8 @@ int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccr
     if (s == DCCRGX_OK) {
         hipLaunchKernelGGL(k_adapt_codes, dim3(grid_for(n)), dim3(256), 0, st, (const int8_t*)d_marks,
                            (const int64_t*)d_pos, (const int8_t*)d_lvl, n, d_code);
-        if (hipGetLastError() != hipSuccess ||
-            hipMemcpyAsync(code.data(), d_code, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            s = set_error(DCCRGX_EHIP, "adaptation sets failed");
+        if (hipGetLastError() != hipSuccess) s = set_error(DCCRGX_EHIP, "adaptation sets failed");
+        if (s == DCCRGX_OK) s = dx_d2h(grid->ctx, code.data(), d_code, n, st);
     }
     for (void* q : {(void*)d_marks, (void*)d_sib, (void*)d_pos, (void*)d_lvl, (void*)d_code}) dx_free(q);
     if (s != DCCRGX_OK) return s;
@@ -828,6 +822,7 @@ int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_
 {
     DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
     if (!grid->amr || grid->amr->new_cells.empty()) return DCCRGX_OK;
+    PhaseTimer T("copy_from_parents");
     std::vector<uint64_t> src, dst;
     for (uint64_t c : grid->amr->new_cells) {
         uint64_t idx[3];
@@ -840,12 +835,15 @@ int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_
         dst.push_back((uint64_t)a);
         src.push_back((uint64_t)b);
     }
+    T.lap("host lookups");
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_src = nullptr, *d_dst = nullptr;
     DX_HIP(dx_malloc(&d_src, src.size() * 8));
     DX_HIP(dx_malloc(&d_dst, dst.size() * 8));
-    DX_HIP(hipMemcpyAsync(d_src, src.data(), src.size() * 8, hipMemcpyHostToDevice, st));
-    DX_HIP(hipMemcpyAsync(d_dst, dst.data(), dst.size() * 8, hipMemcpyHostToDevice, st));
+    T.lap("alloc");
+    DX_TRY(dx_h2d(grid->ctx, d_src, src.data(), src.size() * 8, st));
+    DX_TRY(dx_h2d(grid->ctx, d_dst, dst.data(), dst.size() * 8, st));
+    T.lap("upload");
     int s = DCCRGX_OK;
     for (size_t k = 0; k < nf && s == DCCRGX_OK; k++) {
         if (fields[k] < 0 || (size_t)fields[k] >= grid->fields.size() || grid->fields[fields[k]].variable) {
@@ -856,8 +854,10 @@ int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_
         s = launch_scatter_ext(F.ptr, d_src, d_dst, src.size(), F.elem, F.ptr, st);
     }
     DX_HIP(hipStreamSynchronize(st));
+    T.lap("scatter");
     dx_free(d_src);
     dx_free(d_dst);
+    T.lap("free");
     return s;
 }
 
@@ -868,7 +868,10 @@ int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t
     // parent slot -> its removed children's slots, children in ascending id
     // order (removed is ascending; siblings of one parent interleave with
     // other parents' children, so group explicitly)
-    std::map<uint64_t, std::vector<uint64_t>> groups;
+    // (parent slot, child slot) in removed (ascending child id) order; a
+    // stable sort by parent slot keeps each group's children ascending
+    std::vector<std::pair<uint64_t, uint64_t>> pc;
+    pc.reserve(grid->amr->removed.size());
     for (uint64_t c : grid->amr->removed) {
         uint64_t idx[3];
         int l;
@@ -877,22 +880,26 @@ int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t
         const int64_t ps = host_primary_slot(grid, par), cs = host_primary_slot(grid, c);
         DX_CHECK(ps >= 0 && cs >= 0, DCCRGX_ENOTFOUND, "no data for removed cell %llu or its parent",
                  (unsigned long long)c);
-        auto& g = groups[(uint64_t)ps];
-        DX_CHECK(g.size() < 8, DCCRGX_EINTERNAL, "more than 8 children of cell %llu", (unsigned long long)par);
-        g.push_back((uint64_t)cs);
+        pc.emplace_back((uint64_t)ps, (uint64_t)cs);
     }
+    std::stable_sort(pc.begin(), pc.end(), [](const std::pair<uint64_t, uint64_t>& a,
+                                              const std::pair<uint64_t, uint64_t>& b) { return a.first < b.first; });
     std::vector<uint64_t> parent, children;
-    for (auto& kv : groups) {
-        parent.push_back(kv.first);
-        children.insert(children.end(), kv.second.begin(), kv.second.end());
+    for (size_t i = 0; i < pc.size();) {
+        size_t j = i;
+        while (j < pc.size() && pc[j].first == pc[i].first) j++;
+        DX_CHECK(j - i <= 8, DCCRGX_EINTERNAL, "more than 8 children of slot %llu", (unsigned long long)pc[i].first);
+        parent.push_back(pc[i].first);
+        for (size_t k = i; k < j; k++) children.push_back(pc[k].second);
         children.resize(8 * parent.size(), ~0ull);
+        i = j;
     }
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_par = nullptr, *d_ch = nullptr;
     DX_HIP(dx_malloc(&d_par, parent.size() * 8));
     DX_HIP(dx_malloc(&d_ch, children.size() * 8));
-    DX_HIP(hipMemcpyAsync(d_par, parent.data(), parent.size() * 8, hipMemcpyHostToDevice, st));
-    DX_HIP(hipMemcpyAsync(d_ch, children.data(), children.size() * 8, hipMemcpyHostToDevice, st));
+    DX_TRY(dx_h2d(grid->ctx, d_par, parent.data(), parent.size() * 8, st));
+    DX_TRY(dx_h2d(grid->ctx, d_ch, children.data(), children.size() * 8, st));
     int s = DCCRGX_OK;
     for (size_t k = 0; k < nf; k++) {
         if (fields[k] < 0 || (size_t)fields[k] >= grid->fields.size() || grid->fields[fields[k]].variable ||

@@ -312,8 +312,8 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     } else {
         std::vector<int64_t> from(ns);
         for (uint64_t k = 0; k < ns; k++) from[k] = host_primary_slot(&old, E->slot_ids[k]);
-        if (ns && hipMemcpy(d_from, from.data(), ns * 8, hipMemcpyHostToDevice) != hipSuccess)
-            return fail(set_error(DCCRGX_EHIP, "uploading the rebuild plan failed"));
+        const int e = dx_h2d(ctx, d_from, from.data(), ns * 8, st);
+        if (e != DCCRGX_OK) return fail(e);
     }
     T.lap("move plan");
     // new field arrays: a spare of the last rebuild when one is large enough
@@ -749,7 +749,8 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     T.lap("override_unrefines");
     // execute_refines, dccrg.hpp:10243-10693
     const Explicit* E = grid->ex;
-    std::unordered_set<uint64_t> gone;
+    FlatSet gone;
+    gone.reserve(2 * R.size() + 8 * final_un.size());
     std::vector<uint64_t> added, retired;
     for (uint64_t r : R) {
         uint64_t ch[8];

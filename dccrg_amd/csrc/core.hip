@@ -21,6 +21,71 @@ int set_error(int code, const char* fmt, ...)
     return code;
 }
 
+void dx_slow_note(const char* what, size_t bytes, double ms)
+{
+    static const bool on = [] {
+        const char* e = std::getenv("DCCRGX_TIMING");
+        return e && *e && *e != '0';
+    }();
+    if (on) std::fprintf(stderr, "[dccrgx] slow %s %zu bytes %.3f ms\n", what, bytes, ms);
+}
+
+static int stage_reserve(Ctx* c, size_t bytes)
+{
+    if (c->stage_bytes >= bytes) return DCCRGX_OK;
+    size_t want = std::max<size_t>(bytes, 1 << 20);
+    if (c->stage) DX_HIP(hipHostFree(c->stage));
+    c->stage = nullptr;
+    c->stage_bytes = 0;
+    DX_HIP(hipHostMalloc(&c->stage, want, hipHostMallocDefault));
+    c->stage_bytes = want;
+    return DCCRGX_OK;
+}
+
+constexpr size_t STAGE_CHUNK = 64ull << 20;
+
+static bool pageable_copies()  // DCCRGX_PAGEABLE=1: direct pageable copies (comparison runs)
+{
+    static const bool on = getenv_flag("DCCRGX_PAGEABLE");
+    return on;
+}
+
+int dx_h2d(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
+{
+    if (!bytes) return DCCRGX_OK;
+    if (pageable_copies()) {
+        DX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+        DX_HIP(hipStreamSynchronize(st));
+        return DCCRGX_OK;
+    }
+    DX_TRY(stage_reserve(c, std::min(bytes, STAGE_CHUNK)));
+    for (size_t off = 0; off < bytes; off += STAGE_CHUNK) {
+        const size_t k = std::min(STAGE_CHUNK, bytes - off);
+        std::memcpy(c->stage, (const char*)src + off, k);
+        DX_HIP(hipMemcpyAsync((char*)dst + off, c->stage, k, hipMemcpyHostToDevice, st));
+        DX_HIP(hipStreamSynchronize(st));
+    }
+    return DCCRGX_OK;
+}
+
+int dx_d2h(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
+{
+    if (!bytes) return DCCRGX_OK;
+    if (pageable_copies()) {
+        DX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+        DX_HIP(hipStreamSynchronize(st));
+        return DCCRGX_OK;
+    }
+    DX_TRY(stage_reserve(c, std::min(bytes, STAGE_CHUNK)));
+    for (size_t off = 0; off < bytes; off += STAGE_CHUNK) {
+        const size_t k = std::min(STAGE_CHUNK, bytes - off);
+        DX_HIP(hipMemcpyAsync(c->stage, (const char*)src + off, k, hipMemcpyDeviceToHost, st));
+        DX_HIP(hipStreamSynchronize(st));
+        std::memcpy((char*)dst + off, c->stage, k);
+    }
+    return DCCRGX_OK;
+}
+
 // dccrg_mapping.hpp:317-330 (double arithmetic, as the reference)
 int max_possible_level(const uint64_t length[3])
 {
@@ -434,6 +499,7 @@ int dccrgx_ctx_destroy(dccrgx_ctx* c)
     hipEventDestroy(c->ev_comm);
     hipStreamDestroy(c->compute);
     hipStreamDestroy(c->comm);
+    if (c->stage) hipHostFree(c->stage);
     delete c;
     return DCCRGX_OK;
 }

@@ -342,13 +342,27 @@ static int scan_counts_device(const uint32_t* d_cnt, uint64_t n, uint64_t** d_ro
     return device_scan_rows(*d_row, n, st, total);
 }
 
+__global__ void __launch_bounds__(256) k_iota(uint32_t* __restrict__ out, uint64_t n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = (uint32_t)i;
+}
+
+// 0, 1, ..., n-1 on the device (identity maps need no upload)
+static int device_iota(uint32_t** d, uint64_t n, hipStream_t st)
+{
+    DX_HIP(dx_malloc(d, std::max<uint64_t>(n, 1) * 4));
+    if (n) hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(256), 0, st, *d, n);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
 template <class T>
-static int upload(const std::vector<T>& v, T** d, hipStream_t st)
+static int upload(Ctx* c, const std::vector<T>& v, T** d, hipStream_t st)
 {
     *d = nullptr;
     DX_HIP(dx_malloc(d, std::max<size_t>(v.size(), 1) * sizeof(T)));
-    if (!v.empty()) DX_HIP(hipMemcpyAsync(*d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
-    return DCCRGX_OK;
+    return dx_h2d(c, *d, v.data(), v.size() * sizeof(T), st);
 }
 
 // neighbors_of for a device array of cells: row (n+1, device) + optional outputs
@@ -366,7 +380,7 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     DX_HIP(hipGetLastError());
     DX_TRY(device_scan_rows(row, n, st, total));
     int32_t err = 0;
-    DX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
+    DX_TRY(dx_d2h(grid->ctx, &err, d_err, 4, st));
     DX_HIP(hipStreamSynchronize(st));
     if (err) {
         dx_free(d_err);
@@ -407,7 +421,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     uint64_t cap = 16;
     while (cap < 2 * E->n) cap <<= 1;
     E->mask = cap - 1;
-    DX_TRY(upload(E->leaves, &E->d_leaves, st));
+    DX_TRY(upload(grid->ctx, E->leaves, &E->d_leaves, st));
     DX_HIP(dx_malloc(&E->d_keys, cap * 8));
     DX_HIP(dx_malloc(&E->d_vals, cap * 4));
     DX_HIP(hipMemsetAsync(E->d_keys, 0, cap * 8, st));
@@ -436,16 +450,15 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
             E->local_g.push_back((uint32_t)i);
         }
     }
-    DX_TRY(upload(E->local_g, &E->d_local_g, st));
+    if (ctx->comm_size == 1) DX_TRY(device_iota(&E->d_local_g, E->n, st));
+    else DX_TRY(upload(grid->ctx, E->local_g, &E->d_local_g, st));
     grid->n_local = E->local.size();
     grid->first_local = E->local.empty() ? 0 : E->local[0];
     // storage: the local cells first (ghosts are added by the neighborhoods)
     E->slot_ids = E->local;
     E->slot_of_g.assign(E->n, NO_SLOT);
     for (uint64_t i = 0; i < E->local.size(); i++) E->slot_of_g[E->local_g[i]] = (uint32_t)i;
-    std::vector<uint32_t> ident(E->local.size());
-    for (uint64_t i = 0; i < ident.size(); i++) ident[i] = (uint32_t)i;
-    DX_TRY(upload(ident, &E->d_local_slot, st));
+    DX_TRY(device_iota(&E->d_local_slot, E->local.size(), st));  // local position -> slot: identity
     T.lap("owners+local");
     DX_TRY(sync_slots(grid));
     T.lap("sync_slots");
@@ -467,8 +480,8 @@ static int sync_slots(dccrgx_grid* grid)
     if (level.size() > E->slot_ids.size()) level.resize(E->slot_ids.size());
     for (size_t s = level.size(); s < E->slot_ids.size(); s++)
         level.push_back((uint8_t)map_level(grid->map, E->slot_ids[s]));
-    DX_TRY(upload(E->slot_of_g, &E->d_slot_of_g, st));
-    DX_TRY(upload(level, &E->d_level, st));
+    DX_TRY(upload(grid->ctx, E->slot_of_g, &E->d_slot_of_g, st));
+    DX_TRY(upload(grid->ctx, level, &E->d_level, st));
     DX_HIP(hipStreamSynchronize(st));
     grid->n_slots = E->slot_ids.size();
     return DCCRGX_OK;
@@ -604,8 +617,8 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     h.of_c = h.items;  // explicit grids use the original axes
     h.to_c.resize(h.items.size());
     for (size_t i = 0; i < h.items.size(); i++) h.to_c[i] = -h.items[i];
-    DX_TRY(upload(h.of_c, &h.d_of_c, st));
-    DX_TRY(upload(h.to_c, &h.d_to_c, st));
+    DX_TRY(upload(grid->ctx, h.of_c, &h.d_of_c, st));
+    DX_TRY(upload(grid->ctx, h.to_c, &h.d_to_c, st));
     h.outer.clear();
     h.remote.clear();
     const uint64_t N = E->n;
@@ -634,7 +647,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     uint64_t ntot = 0;
     DX_TRY(scan_counts_device(d_ucnt, N, &h.d_nto_row, &ntot, st));
     std::vector<uint64_t> nto_row(N + 1);
-    DX_HIP(hipMemcpyAsync(nto_row.data(), h.d_nto_row, (N + 1) * 8, hipMemcpyDeviceToHost, st));
+    DX_TRY(dx_d2h(ctx, nto_row.data(), h.d_nto_row, (N + 1) * 8, st));
     DX_HIP(dx_malloc(&h.d_nto_g, std::max<uint64_t>(ntot, 1) * 4));
     hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, d_tmp, h.d_nto_row, N, h.d_nto_g);
     DX_HIP(hipGetLastError());
@@ -648,7 +661,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     // per-rank bookkeeping from the device lists (dccrg.hpp:9131-9234, 8729-8891)
     const uint64_t nl = E->local.size();
     std::vector<uint64_t> nof_row(N + 1);
-    DX_HIP(hipMemcpyAsync(nof_row.data(), h.d_nof_row, (N + 1) * 8, hipMemcpyDeviceToHost, st));
+    DX_TRY(dx_d2h(ctx, nof_row.data(), h.d_nof_row, (N + 1) * 8, st));
     Explicit::HoodLists& L = E->hl[h.id];
     for (uint32_t* p : {L.d_inner_pos, L.d_outer_pos, L.d_all_pos}) dx_free(p);
     L = Explicit::HoodLists{};
@@ -657,8 +670,8 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     DX_HIP(hipStreamSynchronize(st));
     L.h_nof_row = nof_row;
     L.h_nof_g.resize(nof_row[N]);
-    if (nof_row[N]) DX_HIP(hipMemcpyAsync(L.h_nof_g.data(), h.d_nof_g, nof_row[N] * 4, hipMemcpyDeviceToHost, st));
-    if (nto_row[N]) DX_HIP(hipMemcpyAsync(L.h_nto_g.data(), h.d_nto_g, nto_row[N] * 4, hipMemcpyDeviceToHost, st));
+    DX_TRY(dx_d2h(ctx, L.h_nof_g.data(), h.d_nof_g, nof_row[N] * 4, st));
+    DX_TRY(dx_d2h(ctx, L.h_nto_g.data(), h.d_nto_g, nto_row[N] * 4, st));
     DX_HIP(hipStreamSynchronize(st));
     T.lap("lists to host");
     const std::vector<int32_t>& owner = E->owner;
@@ -698,16 +711,24 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     T.lap("ghost slots");
 
     // stencil rows of local cells (iteration-cache neighbors_of: unique pairs)
-    std::vector<uint64_t> tmp_row(nl + 1, 0);
-    for (uint64_t i = 0; i < nl; i++) {
-        const uint32_t r = E->local_g[i];
-        tmp_row[i + 1] = tmp_row[i] + (nof_row[r + 1] - nof_row[r]);
-    }
     uint64_t* d_tmp_row = nullptr;
     Pair* d_pairs = nullptr;
     uint32_t* d_pc = nullptr;
-    DX_TRY(upload(tmp_row, &d_tmp_row, st));
-    DX_HIP(dx_malloc(&d_pairs, std::max<uint64_t>(tmp_row[nl], 1) * sizeof(Pair)));
+    uint64_t tmp_tot = 0;
+    if (ctx->comm_size == 1) {  // every leaf is local, in leaf order: the rows are neighbors_of's
+        DX_HIP(dx_malloc(&d_tmp_row, (nl + 1) * 8));
+        DX_HIP(hipMemcpyAsync(d_tmp_row, h.d_nof_row, (nl + 1) * 8, hipMemcpyDeviceToDevice, st));
+        tmp_tot = nof_row[nl];
+    } else {
+        std::vector<uint64_t> tmp_row(nl + 1, 0);
+        for (uint64_t i = 0; i < nl; i++) {
+            const uint32_t r = E->local_g[i];
+            tmp_row[i + 1] = tmp_row[i] + (nof_row[r + 1] - nof_row[r]);
+        }
+        DX_TRY(upload(grid->ctx, tmp_row, &d_tmp_row, st));
+        tmp_tot = tmp_row[nl];
+    }
+    DX_HIP(dx_malloc(&d_pairs, std::max<uint64_t>(tmp_tot, 1) * sizeof(Pair)));
     DX_HIP(dx_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4));
     if (nl)
         hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
@@ -745,8 +766,8 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
         std::vector<uint64_t> ss, rd;
         for (uint64_t c : pp.send_ids) ss.push_back(local_pos(c));
         for (uint64_t c : pp.recv_ids) rd.push_back(E->extra.at(c));
-        if (!ss.empty()) DX_TRY(upload(ss, &pp.d_send_slots, st));
-        if (!rd.empty()) DX_TRY(upload(rd, &pp.d_unpack_dst, st));
+        if (!ss.empty()) DX_TRY(upload(grid->ctx, ss, &pp.d_send_slots, st));
+        if (!rd.empty()) DX_TRY(upload(grid->ctx, rd, &pp.d_unpack_dst, st));
         pp.n_unpack = rd.size();
         pp.h_send_slots = ss;
         pp.h_unpack_dst = rd;
@@ -754,11 +775,11 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
         for (size_t i = 0; i < rd.size(); i++) pp.h_unpack_src[i] = i;
         h.peers.push_back(std::move(pp));
     }
-    std::vector<uint32_t> all(nl);
-    for (uint64_t i = 0; i < nl; i++) all[i] = (uint32_t)i;
-    DX_TRY(upload(L.inner_pos, &L.d_inner_pos, st));
-    DX_TRY(upload(L.outer_pos, &L.d_outer_pos, st));
-    DX_TRY(upload(all, &L.d_all_pos, st));
+
+    if (ctx->comm_size == 1) DX_TRY(device_iota(&L.d_inner_pos, nl, st));  // every cell inner
+    else DX_TRY(upload(grid->ctx, L.inner_pos, &L.d_inner_pos, st));
+    DX_TRY(upload(grid->ctx, L.outer_pos, &L.d_outer_pos, st));
+    DX_TRY(device_iota(&L.d_all_pos, nl, st));
     DX_HIP(hipStreamSynchronize(st));
     return DCCRGX_OK;
 }
@@ -831,7 +852,7 @@ int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_
     const uint64_t n = E->slot_ids.size();
     if (!n) return DCCRGX_OK;
     uint64_t* d_ids = nullptr;
-    DX_TRY(upload(E->slot_ids, &d_ids, st));
+    DX_TRY(upload(grid->ctx, E->slot_ids, &d_ids, st));
     ExView v{};
     v.mp = grid->map;
     v.keys = old->d_keys;
@@ -979,7 +1000,7 @@ int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t
     const Explicit* E = grid->ex;
     const auto& L = E->hl.at(h.id);
     std::vector<uint64_t> hc(n);
-    if (n) DX_HIP(hipMemcpyAsync(hc.data(), cells, n * 8, hipMemcpyDeviceToHost, st));
+    DX_TRY(dx_d2h(grid->ctx, hc.data(), cells, n * 8, st));
     DX_HIP(hipStreamSynchronize(st));
     std::vector<uint64_t> orow(n + 1, 0), oids;
     for (size_t i = 0; i < n; i++) {
@@ -989,10 +1010,10 @@ int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t
         for (uint64_t e = L.h_nto_row[g]; e < L.h_nto_row[g + 1]; e++) oids.push_back(E->leaves[L.h_nto_g[e]]);
         orow[i + 1] = oids.size();
     }
-    DX_HIP(hipMemcpyAsync(row, orow.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    DX_TRY(dx_h2d(grid->ctx, row, orow.data(), (n + 1) * 8, st));
     if (ids) {
         DX_CHECK(cap >= oids.size(), DCCRGX_ERANGE, "capacity %zu < %zu", cap, oids.size());
-        if (!oids.empty()) DX_HIP(hipMemcpyAsync(ids, oids.data(), oids.size() * 8, hipMemcpyHostToDevice, st));
+        DX_TRY(dx_h2d(grid->ctx, ids, oids.data(), oids.size() * 8, st));
     }
     DX_HIP(hipStreamSynchronize(st));
     return DCCRGX_OK;
@@ -1045,8 +1066,8 @@ int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, boo
     const uint64_t n = grid->ex->local.size();
     if (!n) return DCCRGX_OK;
     hipStream_t st = grid->ctx->compute;
-    if (to_device) DX_HIP(hipMemcpyAsync(F.ptr, host, n * F.elem, hipMemcpyHostToDevice, st));
-    else DX_HIP(hipMemcpyAsync(host, F.ptr, n * F.elem, hipMemcpyDeviceToHost, st));
+    if (to_device) DX_TRY(dx_h2d(grid->ctx, F.ptr, host, n * F.elem, st));
+    else DX_TRY(dx_d2h(grid->ctx, host, F.ptr, n * F.elem, st));
     DX_HIP(hipStreamSynchronize(st));
     return DCCRGX_OK;
 }

@@ -413,10 +413,7 @@ int dccrgx_field_write_local(dccrgx_grid* grid, int32_t fid, const void* host, s
     if (!n) return DCCRGX_OK;
     const Field& F = grid->fields[fid];
     if (!grid->uniform) return explicit_local_copy(grid, F, const_cast<void*>(host), true);
-    DX_HIP(hipMemcpyAsync((char*)F.ptr + local_slot0(grid) * F.elem, host, n * F.elem,
-                          hipMemcpyHostToDevice, grid->ctx->compute));
-    DX_HIP(hipStreamSynchronize(grid->ctx->compute));
-    return DCCRGX_OK;
+    return dx_h2d(grid->ctx, (char*)F.ptr + local_slot0(grid) * F.elem, host, n * F.elem, grid->ctx->compute);
 }
 
 int dccrgx_field_read_local(const dccrgx_grid* grid, int32_t fid, void* host, size_t n)
@@ -428,10 +425,7 @@ int dccrgx_field_read_local(const dccrgx_grid* grid, int32_t fid, void* host, si
     if (!n) return DCCRGX_OK;
     const Field& F = grid->fields[fid];
     if (!grid->uniform) return explicit_local_copy(grid, F, host, false);
-    DX_HIP(hipMemcpyAsync(host, (char*)F.ptr + local_slot0(grid) * F.elem, n * F.elem,
-                          hipMemcpyDeviceToHost, grid->ctx->compute));
-    DX_HIP(hipStreamSynchronize(grid->ctx->compute));
-    return DCCRGX_OK;
+    return dx_d2h(grid->ctx, host, (char*)F.ptr + local_slot0(grid) * F.elem, n * F.elem, grid->ctx->compute);
 }
 
 int dccrgx_field_read_remote(const dccrgx_grid* grid, int32_t hood_id, int32_t fid, void* host,
@@ -452,11 +446,10 @@ int dccrgx_field_read_remote(const dccrgx_grid* grid, int32_t hood_id, int32_t f
     DX_HIP(dx_malloc(&d_ids, n * 8));
     DX_HIP(dx_malloc(&d_slots, n * 8));
     DX_HIP(dx_malloc(&d_out, n * F.elem));
-    DX_HIP(hipMemcpyAsync(d_ids, h->remote.data(), n * 8, hipMemcpyHostToDevice, st));
+    DX_TRY(dx_h2d(grid->ctx, d_ids, h->remote.data(), n * 8, st));
     DX_TRY(dccrgx_slots_of(grid, d_ids, n, d_slots, st));
     DX_TRY(launch_gather(F.ptr, (const uint64_t*)d_slots, n, F.elem, d_out, st));
-    DX_HIP(hipMemcpyAsync(host, d_out, n * F.elem, hipMemcpyDeviceToHost, st));
-    DX_HIP(hipStreamSynchronize(st));
+    DX_TRY(dx_d2h(grid->ctx, host, d_out, n * F.elem, st));
     dx_free(d_ids);
     dx_free(d_slots);
     dx_free(d_out);

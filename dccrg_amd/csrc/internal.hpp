@@ -45,19 +45,27 @@ int set_error(int code, const char* fmt, ...);
 // dccrgx_ctx_create): an adaptive run frees and allocates grid structures
 // every step, and returning them to the driver each time cost tens of ms.
 // dx_free waits for the device first, as hipFree does.
+void dx_slow_note(const char* what, size_t bytes, double ms);  // DCCRGX_TIMING: allocations over 1 ms
+
 template <class T>
 inline hipError_t dx_malloc(T** p, size_t bytes)
 {
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipMallocAsync(reinterpret_cast<void**>(p), bytes ? bytes : 1, nullptr);
     if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > 1.0) dx_slow_note("dx_malloc", bytes, ms);
     return e;
 }
 
 inline hipError_t dx_free(void* p)
 {
     if (!p) return hipSuccess;
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipFreeAsync(p, nullptr);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > 1.0) dx_slow_note("dx_free", 0, ms);
     return e;
 }
 
@@ -302,7 +310,18 @@ struct Ctx {
     // the multi-rank halo path (pack, grouped send/recv, unpack, inner/outer
     // overlap) runs on one GPU through the real communicator
     bool self_peer = false;
+    // pinned bounce buffer of dx_h2d / dx_d2h
+    void* stage = nullptr;
+    size_t stage_bytes = 0;
 };
+
+// Host <-> device copies of pageable host memory through the context's pinned
+// bounce buffer, in chunks of at most 64 MiB; they return after the copy has
+// completed on `st`.  A pageable hipMemcpyAsync of even a few KB stalls for
+// ~16 ms now and then on this runtime (seen in the adaptive loop); copies
+// from pinned memory do not.
+int dx_h2d(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st);
+int dx_d2h(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st);
 
 }  // namespace dccrgx
 

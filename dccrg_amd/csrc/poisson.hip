@@ -1066,7 +1066,7 @@ int dccrgx_poisson_solve(dccrgx_poisson* P, const uint64_t* cells, size_t n, con
             hipLaunchKernelGGL(k_solo, dim3(1), dim3(SB), 0, st, p, s, P->d_state, pn, q.stop_residual,
                                q.stop_after_residual_increase, q.min_iterations, q.max_iterations);
         DX_HIP(hipGetLastError());
-        DX_HIP(hipMemcpyAsync(&hs, P->d_state, sizeof(PState), hipMemcpyDeviceToHost, st));
+        DX_TRY(dx_d2h(P->grid->ctx, &hs, P->d_state, sizeof(PState), st));
     }
     uint32_t batch = 4;
     for (; !solo;) {
@@ -1081,8 +1081,7 @@ int dccrgx_poisson_solve(dccrgx_poisson* P, const uint64_t* cells, size_t n, con
             hipLaunchKernelGGL(k_p, dim3(RG), dim3(RB), 0, st, p, s, (const PState*)P->d_state);
             DX_HIP(hipGetLastError());
         }
-        DX_HIP(hipMemcpyAsync(&hs, P->d_state, sizeof(PState), hipMemcpyDeviceToHost, st));
-        DX_HIP(hipStreamSynchronize(st));
+        DX_TRY(dx_d2h(P->grid->ctx, &hs, P->d_state, sizeof(PState), st));
         if (hs.done || hs.end) break;
         batch = std::min<uint32_t>(batch * 2, 64);
     }
