@@ -534,7 +534,7 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
         if (std::binary_search(E->local.begin(), E->local.end(), c) || E->extra.count(c)) continue;
         const uint32_t s = (uint32_t)E->slot_ids.size();
         E->slot_ids.push_back(c);
-        E->extra[c] = s;
+        E->extra.set(c, s);
         const int64_t g = E->find(c);
         if (g >= 0) E->slot_of_g[g] = s;
     }
@@ -765,7 +765,11 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
         pp.recv_ids.assign(recv[p].begin(), recv[p].end());
         std::vector<uint64_t> ss, rd;
         for (uint64_t c : pp.send_ids) ss.push_back(local_pos(c));
-        for (uint64_t c : pp.recv_ids) rd.push_back(E->extra.at(c));
+        for (uint64_t c : pp.recv_ids) {
+            const uint32_t* x = E->extra.find(c);
+            DX_CHECK(x, DCCRGX_EINTERNAL, "remote cell %llu has no ghost slot", (unsigned long long)c);
+            rd.push_back(*x);
+        }
         if (!ss.empty()) DX_TRY(upload(grid->ctx, ss, &pp.d_send_slots, st));
         if (!rd.empty()) DX_TRY(upload(grid->ctx, rd, &pp.d_unpack_dst, st));
         pp.n_unpack = rd.size();
@@ -815,8 +819,8 @@ int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id)
     if (it != E->local.end() && *it == id) return (int64_t)(it - E->local.begin());
     // ghosts, and data of refined / unrefined cells kept until
     // clear_refined_unrefined_data
-    auto jt = E->extra.find(id);
-    return jt != E->extra.end() ? (int64_t)jt->second : -1;
+    const uint32_t* x = E->extra.find(id);
+    return x ? (int64_t)*x : -1;
 }
 
 // rebuild(): new slot k takes old slot src[k] (-1: value-initialised), looked

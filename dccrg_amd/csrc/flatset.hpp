@@ -138,4 +138,84 @@ class FlatSet {
     size_t n_ = 0;
 };
 
+// id -> 32-bit value (ghost / retired slots), same table scheme as FlatSet
+class FlatMap32 {
+  public:
+    size_t size() const { return keys_.size() ? n_ : 0; }
+    size_t count(uint64_t k) const { return find(k) ? 1 : 0; }
+    const uint32_t* find(uint64_t k) const
+    {
+        if (!n_ || !k) return nullptr;
+        for (size_t i = slot(k);; i = (i + 1) & mask_) {
+            if (keys_[i] == k) return &vals_[i];
+            if (!keys_[i]) return nullptr;
+        }
+    }
+    void set(uint64_t k, uint32_t v)  // insert or assign; k != 0
+    {
+        if (2 * (n_ + 1) > keys_.size()) rehash(std::max<size_t>(16, 2 * keys_.size()));
+        for (size_t i = slot(k);; i = (i + 1) & mask_) {
+            if (keys_[i] == k) {
+                vals_[i] = v;
+                return;
+            }
+            if (!keys_[i]) {
+                keys_[i] = k;
+                vals_[i] = v;
+                n_++;
+                return;
+            }
+        }
+    }
+    size_t erase(uint64_t k)
+    {
+        if (!n_ || !k) return 0;
+        size_t i = slot(k);
+        for (;; i = (i + 1) & mask_) {
+            if (!keys_[i]) return 0;
+            if (keys_[i] == k) break;
+        }
+        size_t j = i;
+        for (;;) {
+            j = (j + 1) & mask_;
+            if (!keys_[j]) break;
+            const size_t home = slot(keys_[j]);
+            const bool stays = i <= j ? (i < home && home <= j) : (i < home || home <= j);
+            if (stays) continue;
+            keys_[i] = keys_[j];
+            vals_[i] = vals_[j];
+            i = j;
+        }
+        keys_[i] = 0;
+        n_--;
+        return 1;
+    }
+
+  private:
+    size_t slot(uint64_t x) const
+    {
+        x ^= x >> 33;
+        x *= 0xff51afd7ed558ccdull;
+        x ^= x >> 33;
+        return (size_t)x & mask_;
+    }
+    void rehash(size_t cap)
+    {
+        std::vector<uint64_t> ok;
+        std::vector<uint32_t> ov;
+        ok.swap(keys_);
+        ov.swap(vals_);
+        keys_.assign(cap, 0);
+        vals_.assign(cap, 0);
+        mask_ = cap - 1;
+        n_ = 0;
+        for (size_t i = 0; i < ok.size(); i++)
+            if (ok[i]) set(ok[i], ov[i]);
+    }
+    std::vector<uint64_t> keys_;
+    std::vector<uint32_t> vals_;
+    size_t mask_ = 0;
+    size_t n_ = 0;
+};
+
 }  // namespace dccrgx

@@ -139,7 +139,7 @@ struct Explicit {
     // these slots only, as the reference stores data only for local cells and
     // remote neighbors (dccrg.hpp:7238, 7330).
     std::vector<uint64_t> slot_ids;                 // id held by each slot
-    std::unordered_map<uint64_t, uint32_t> extra;   // ghost / retired id -> slot
+    FlatMap32 extra;                                // ghost / retired id -> slot
     std::vector<uint32_t> slot_of_g;                // global leaf index -> slot (NO_SLOT)
     uint32_t* d_slot_of_g = nullptr;
     uint32_t* d_local_slot = nullptr;               // local position -> slot (identity)

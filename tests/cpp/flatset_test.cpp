@@ -1,7 +1,9 @@
-// FlatSet (dccrg_amd/csrc/flatset.hpp) against std::set under random
-// inserts, erases and lookups, including ids that collide in the table.
+// FlatSet / FlatMap32 (dccrg_amd/csrc/flatset.hpp) against std::set / std::map
+// under random inserts, erases and lookups, including ids that collide in
+// the table.
 #include <cstdio>
 #include <random>
+#include <map>
 #include <set>
 
 #include "flatset.hpp"
@@ -37,6 +39,32 @@ int main()
         if (n != s.size()) return std::printf("iteration\n"), 1;
         f.clear();
         if (!f.empty() || f.count(v.empty() ? 1 : v[0])) return std::printf("clear\n"), 1;
+    }
+    for (int round = 0; round < 40; round++) {
+        dccrgx::FlatMap32 f;
+        std::map<uint64_t, uint32_t> m;
+        const uint64_t range = round % 2 ? 64 : 1 + (rng() % 100000);
+        for (int op = 0; op < 20000; op++) {
+            const uint64_t x = 1 + rng() % range;
+            switch (rng() % 3) {
+            case 0: {
+                const uint32_t v = (uint32_t)rng();
+                f.set(x, v);
+                m[x] = v;
+                break;
+            }
+            case 1:
+                if (f.erase(x) != m.erase(x)) return std::printf("map erase %llu\n", (unsigned long long)x), 1;
+                break;
+            default: {
+                const uint32_t* p = f.find(x);
+                auto it = m.find(x);
+                if ((p == nullptr) != (it == m.end()) || (p && *p != it->second))
+                    return std::printf("map find %llu\n", (unsigned long long)x), 1;
+            }
+            }
+            if (f.size() != m.size()) return std::printf("map size\n"), 1;
+        }
     }
     std::printf("PASS\n");
     return 0;

@@ -1,5 +1,6 @@
-"""The host-side id set of the AMR bookkeeping (dccrg_amd/csrc/flatset.hpp)
-against std::set: random inserts, erases and lookups (CPU)."""
+"""The host-side id set and id -> slot map of the AMR bookkeeping
+(dccrg_amd/csrc/flatset.hpp) against std::set / std::map: random inserts,
+erases and lookups (CPU)."""
 import os
 import subprocess
 
