@@ -787,13 +787,14 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     kept.reserve(E->leaves.size());
     for (size_t k = 0; k < E->leaves.size(); k++)
         if (!gone_flag[k]) kept.push_back(E->leaves[k]);
-    std::sort(added.begin(), added.end());
+    T.lap("new leaf set: collect");
+    radix_sort_u64(added);
     added.erase(std::unique(added.begin(), added.end()), added.end());
     std::vector<uint64_t> leaves(kept.size() + added.size());
     leaves.erase(std::set_union(kept.begin(), kept.end(), added.begin(), added.end(), leaves.begin()), leaves.end());
-    std::sort(retired.begin(), retired.end());
-    std::sort(A.new_cells.begin(), A.new_cells.end());
-    std::sort(A.removed.begin(), A.removed.end());
+    radix_sort_u64(retired);
+    radix_sort_u64(A.new_cells);
+    radix_sort_u64(A.removed);
     // the dont_refine closure persists (:10188), everything else is consumed
     A.to_refine.clear();
     A.to_unrefine.clear();

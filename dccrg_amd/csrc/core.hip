@@ -33,7 +33,8 @@ void dx_slow_note(const char* what, size_t bytes, double ms)
 static int stage_reserve(Ctx* c, size_t bytes)
 {
     if (c->stage_bytes >= bytes) return DCCRGX_OK;
-    size_t want = std::max<size_t>(bytes, 1 << 20);
+    // geometric growth (pinning is slow), at least 4 MiB, at most one chunk
+    size_t want = std::min<size_t>(std::max<size_t>({bytes, 2 * c->stage_bytes, 4u << 20}), 64ull << 20);
     if (c->stage) DX_HIP(hipHostFree(c->stage));
     c->stage = nullptr;
     c->stage_bytes = 0;

@@ -815,8 +815,8 @@ int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, ui
 int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id)
 {
     const Explicit* E = grid->ex;
-    auto it = std::lower_bound(E->local.begin(), E->local.end(), id);
-    if (it != E->local.end() && *it == id) return (int64_t)(it - E->local.begin());
+    const int64_t g = E->find(id);  // a leaf: local or ghost slot, if any
+    if (g >= 0 && E->slot_of_g[g] != NO_SLOT) return (int64_t)E->slot_of_g[g];
     // ghosts, and data of refined / unrefined cells kept until
     // clear_refined_unrefined_data
     const uint32_t* x = E->extra.find(id);

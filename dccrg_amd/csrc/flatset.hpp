@@ -9,6 +9,36 @@
 
 namespace dccrgx {
 
+// Ascending sort of 64-bit ids: least-significant-digit radix sort over the
+// bytes in which the keys differ (ids of a grid span few bytes); std::sort
+// for short inputs.
+inline void radix_sort_u64(std::vector<uint64_t>& v)
+{
+    const size_t n = v.size();
+    if (n < 4096) {
+        std::sort(v.begin(), v.end());
+        return;
+    }
+    uint64_t all_or = 0, all_and = ~0ull;
+    for (uint64_t x : v) {
+        all_or |= x;
+        all_and &= x;
+    }
+    const uint64_t varying = all_or ^ all_and;
+    std::vector<uint64_t> tmp(n);
+    uint64_t* a = v.data();
+    uint64_t* b = tmp.data();
+    for (int sh = 0; sh < 64; sh += 8) {
+        if (!((varying >> sh) & 0xff)) continue;
+        size_t cnt[257] = {0};
+        for (size_t i = 0; i < n; i++) cnt[((a[i] >> sh) & 0xff) + 1]++;
+        for (int k = 0; k < 256; k++) cnt[k + 1] += cnt[k];
+        for (size_t i = 0; i < n; i++) b[cnt[(a[i] >> sh) & 0xff]++] = a[i];
+        std::swap(a, b);
+    }
+    if (a != v.data()) std::copy(a, a + n, v.data());
+}
+
 // A set of nonzero cell ids (0 is error_cell): open addressing, linear
 // probing, backward-shift deletion.  The AMR request filters and
 // stop_refining do millions of membership tests per adaptive step, which a
@@ -89,7 +119,7 @@ class FlatSet {
         v.reserve(n_);
         for (uint64_t x : t_)
             if (x) v.push_back(x);
-        std::sort(v.begin(), v.end());
+        radix_sort_u64(v);
         return v;
     }
     class const_iterator {

@@ -66,6 +66,14 @@ int main()
             if (f.size() != m.size()) return std::printf("map size\n"), 1;
         }
     }
+    for (size_t n : {0, 5, 4095, 4096, 100000, 100001}) {  // radix_sort_u64 against std::sort
+        std::vector<uint64_t> v(n);
+        for (auto& x : v) x = (n % 2 ? rng() : (rng() % 1000003) * 8 + 1);
+        std::vector<uint64_t> w = v;
+        dccrgx::radix_sort_u64(v);
+        std::sort(w.begin(), w.end());
+        if (v != w) return std::printf("radix sort %zu\n", n), 1;
+    }
     std::printf("PASS\n");
     return 0;
 }
