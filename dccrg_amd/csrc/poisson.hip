@@ -490,15 +490,19 @@ __global__ void __launch_bounds__(SB) k_solo(PPtrs p, PSys s, PState* S, double 
 constexpr int SL = 1024;
 constexpr int EK = 6;
 
-__device__ __forceinline__ double wg_sum(double v, double* ws)
+// One barrier per sum: successive calls alternate between the two halves of
+// ws, so a half is rewritten only after every thread has passed the barrier
+// of the call in between (and so has read it).
+__device__ __forceinline__ double wg_sum(double v, double* ws, int& par)
 {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    double* w = ws + par * (SL / 64);
+    par ^= 1;
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = v;
     __syncthreads();
     double r = 0;
 #pragma unroll
-    for (int k = 0; k < SL / 64; k++) r += ws[k];
-    __syncthreads();
+    for (int k = 0; k < SL / 64; k++) r += w[k];
     return r;
 }
 
@@ -507,7 +511,8 @@ __global__ void __launch_bounds__(SL) k_solo_lds(PPtrs p, PSys s, const int32_t*
                                                 uint32_t max_it)
 {
 #pragma clang fp contract(off)
-    __shared__ double lp0[SL], lp1[SL], ws[SL / 64];
+    __shared__ double lp0[SL], lp1[SL], ws[2 * SL / 64];
+    int par = 0;
     const uint32_t i = threadIdx.x;
     const bool have = i < s.n;
     uint64_t c = 0, e0 = 0, e1 = 0;
@@ -579,7 +584,7 @@ __global__ void __launch_bounds__(SL) k_solo_lds(PPtrs p, PSys s, const int32_t*
             adp = a;
             acc = x1 * a;
         }
-        double v = wg_sum(acc, ws);
+        double v = wg_sum(acc, ws, par);
         control(&T, PH_ALPHA, v, 2.0, stop_residual, increase, min_it, max_it);
         if (T.done) break;
         // solution update and |r0|^p over every info cell
@@ -588,7 +593,7 @@ __global__ void __launch_bounds__(SL) k_solo_lds(PPtrs p, PSys s, const int32_t*
             if (solve) sol += T.alpha * x0;
             acc = fabs(r0) * fabs(r0);  // pw(|r0|, 2)
         }
-        v = wg_sum(acc, ws);
+        v = wg_sum(acc, ws, par);
         control(&T, PH_RES, v, 2.0, stop_residual, increase, min_it, max_it);
         // best solution, r0 and r1, r0 . r1
         acc = 0;
@@ -613,7 +618,7 @@ __global__ void __launch_bounds__(SL) k_solo_lds(PPtrs p, PSys s, const int32_t*
                 acc = r0 * r1;
             }
         }
-        v = wg_sum(acc, ws);
+        v = wg_sum(acc, ws, par);
         control(&T, PH_BETA, v, 2.0, stop_residual, increase, min_it, max_it);
         if (T.done) break;
         if (have && solve) {
