@@ -261,7 +261,7 @@ def secondary(ctx, torch, D):
     out["poisson"] = {"workload": "configs[4] tests/poisson/poisson3d 8^3 refined twice (792 leaves), BiCG, "
                                   "1 GPU", "solve_ms": dt * 1e3 / reps, "iterations_per_s": its / dt,
                       "iterations_per_solve": its / reps,
-                      "note": "792 cells: one workgroup runs the whole solve (k_solo_lds), latency bound, not bandwidth"}
+                      "note": "792 cells: one workgroup runs the whole solve (k_solo_lds, LDS-resident), latency bound"}
     s.close()
     g.close()
 

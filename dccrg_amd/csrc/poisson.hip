@@ -481,7 +481,7 @@ __global__ void __launch_bounds__(SB) k_solo(PPtrs p, PSys s, PState* S, double 
 // A^T.p1, each /4 for a finer neighbor, computed once as the per-iteration
 // code computes them); a neighbor outside the info cells never changes during
 // the solve, so its product with the factor is kept instead.  Further entries
-// are read each iteration as k_solo does.  Sums are per wave (shuffles) then
+// (at most OVCAP over all cells) sit in LDS the same way.  Sums are per wave (shuffles) then
 // over the 16 waves in a fixed order; every thread runs the scalar control on
 // its own copy of the state, so no broadcast is needed.  Same arithmetic per
 // cell as k_solo; only the summation order of the dot products differs.
@@ -489,6 +489,7 @@ __global__ void __launch_bounds__(SB) k_solo(PPtrs p, PSys s, PState* S, double 
 // push the kernel past its registers).
 constexpr int SL = 1024;
 constexpr int EK = 6;
+constexpr int OVCAP = 1024;  // face-neighbor entries beyond EK per cell, all cells together, kept in LDS
 
 // One barrier per sum: successive calls alternate between the two halves of
 // ws, so a half is rewritten only after every thread has passed the barrier
@@ -512,6 +513,9 @@ __global__ void __launch_bounds__(SL) k_solo_lds(PPtrs p, PSys s, const int32_t*
 {
 #pragma clang fp contract(off)
     __shared__ double lp0[SL], lp1[SL], ws[2 * SL / 64];
+    __shared__ double oma[OVCAP], omt[OVCAP];
+    __shared__ int32_t oj[OVCAP];
+    __shared__ uint32_t wtot[SL / 64];
     int par = 0;
     const uint32_t i = threadIdx.x;
     const bool have = i < s.n;
@@ -562,6 +566,34 @@ __global__ void __launch_bounds__(SL) k_solo_lds(PPtrs p, PSys s, const int32_t*
         lp0[i] = x0;
         lp1[i] = x1;
     }
+    // entries beyond the first EK of every cell, packed into LDS at this
+    // thread's offset (the host launches this kernel only if they fit)
+    const uint32_t ov = e1 - e0 > (uint64_t)EK ? (uint32_t)(e1 - e0 - EK) : 0u;
+    uint32_t x = ov;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[w] = x;
+    __syncthreads();
+    uint32_t o0 = x - ov;
+    for (int k = 0; k < w; k++) o0 += wtot[k];
+    for (uint32_t k = 0; k < ov; k++) {
+        const uint64_t e = e0 + EK + k;
+        const int code = s.code[e];
+        const int dir = (code & 15) - 3;
+        const uint64_t nb = s.nb[e];
+        double m = p.f[fidx(dir)][c], m2 = p.f[fidx(-dir)][nb];
+        if ((code >> 4) - 1 > 0) {
+            m /= 4.0;
+            m2 /= 4.0;
+        }
+        const int32_t j = ej[e];
+        oj[o0 + k] = j;
+        oma[o0 + k] = j >= 0 ? m : m * p.p0[nb];
+        omt[o0 + k] = j >= 0 ? m2 : m2 * p.p1[nb];
+    }
     __shared__ PState T0;
     if (threadIdx.x == 0) T0 = *S;
     __syncthreads();
@@ -574,13 +606,7 @@ __global__ void __launch_bounds__(SL) k_solo_lds(PPtrs p, PSys s, const int32_t*
 #pragma unroll
             for (int k = 0; k < EK; k++)
                 if (jr[k] != -2) a += jr[k] >= 0 ? ma[k] * lp0[jr[k]] : ma[k];
-            for (uint64_t e = e0 + EK; e < e1; e++) {
-                const int code = s.code[e];
-                double m = p.f[fidx((code & 15) - 3)][c];
-                if ((code >> 4) - 1 > 0) m /= 4.0;
-                const int32_t j = ej[e];
-                a += m * (j >= 0 ? lp0[j] : p.p0[s.nb[e]]);
-            }
+            for (uint32_t k = o0; k < o0 + ov; k++) a += oj[k] >= 0 ? oma[k] * lp0[oj[k]] : oma[k];
             adp = a;
             acc = x1 * a;
         }
@@ -605,14 +631,7 @@ __global__ void __launch_bounds__(SL) k_solo_lds(PPtrs p, PSys s, const int32_t*
 #pragma unroll
                 for (int k = 0; k < EK; k++)
                     if (jr[k] != -2) a += jr[k] >= 0 ? mt[k] * lp1[jr[k]] : mt[k];
-                for (uint64_t e = e0 + EK; e < e1; e++) {
-                    const int code = s.code[e];
-                    const uint64_t nb = s.nb[e];
-                    double m = p.f[fidx(-((code & 15) - 3))][nb];
-                    if ((code >> 4) - 1 > 0) m /= 4.0;
-                    const int32_t j = ej[e];
-                    a += m * (j >= 0 ? lp1[j] : p.p1[nb]);
-                }
+                for (uint32_t k = o0; k < o0 + ov; k++) a += oj[k] >= 0 ? omt[k] * lp1[oj[k]] : omt[k];
                 r1 = r1 - T.alpha * a;
                 r0 = nr0;
                 acc = r0 * r1;
@@ -971,7 +990,10 @@ int build_cache(dccrgx_poisson* P, const uint64_t* cells, size_t n, const uint64
         DX_HIP(hipMemcpyAsync(P->d_nb, nb.data(), nb.size() * 8, hipMemcpyHostToDevice, st));
         DX_HIP(hipMemcpyAsync(P->d_code, code.data(), code.size() * 4, hipMemcpyHostToDevice, st));
     }
-    if (P->n_info <= (uint64_t)SL) {  // k_solo_lds's neighbor indices
+    uint64_t overflow = 0;  // entries beyond EK per cell (k_solo_lds keeps them in LDS)
+    for (size_t k = 0; k + 1 < info_row.size(); k++)
+        overflow += info_row[k + 1] - info_row[k] > (uint64_t)EK ? info_row[k + 1] - info_row[k] - EK : 0;
+    if (P->n_info <= (uint64_t)SL && overflow <= (uint64_t)OVCAP) {  // k_solo_lds's neighbor indices
         std::unordered_map<uint64_t, int32_t> info_of;
         for (size_t k = 0; k < info_slot.size(); k++) info_of[info_slot[k]] = (int32_t)k;
         std::vector<int32_t> ej(nb.size());
