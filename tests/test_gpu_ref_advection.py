@@ -72,7 +72,8 @@ def device_run(n, M, steps, adapt_n):
 
 
 @pytest.mark.skipif(not os.path.exists(BIN), reason="oracle/_ref/ref_advection is built where /root/reference is")
-@pytest.mark.parametrize("n,M,steps,adapt_n", [(20, 2, 12, 1), (40, 2, 8, 1), (32, 1, 10, 2), (24, 0, 10, 0)])
+@pytest.mark.parametrize("n,M,steps,adapt_n", [(20, 2, 12, 1), (40, 2, 8, 1), (32, 1, 10, 2), (24, 0, 10, 0),
+                                              (64, 2, 24, 1)])
 def test_device_matches_reference_solver(tmp_path, n, M, steps, adapt_n):
     ref = reference_run(n, M, steps, adapt_n, str(tmp_path / "ref.bin"))
     dev = device_run(n, M, steps, adapt_n)
