@@ -6,7 +6,8 @@ does); it runs here on the GPU box, then the device path (dccrg_amd.advection
 + the advect/AMR kernels) runs the same program.  Leaf sets must be equal after
 every step, densities within 1e-12 of the largest, time steps within 1e-12
 relative (the device gathers each cell's face fluxes in a different order
-than the reference's scatter; SURVEY 8(d) parity gate)."""
+than the reference's scatter; SURVEY 8(d) parity gate).  The last case is
+configs[2] itself: 400 x 400, maximum level 2, adapting every step."""
 import os
 import subprocess
 
@@ -73,7 +74,7 @@ def device_run(n, M, steps, adapt_n):
 
 @pytest.mark.skipif(not os.path.exists(BIN), reason="oracle/_ref/ref_advection is built where /root/reference is")
 @pytest.mark.parametrize("n,M,steps,adapt_n", [(20, 2, 12, 1), (40, 2, 8, 1), (32, 1, 10, 2), (24, 0, 10, 0),
-                                              (64, 2, 24, 1)])
+                                              (64, 2, 24, 1), (400, 2, 8, 1)])
 def test_device_matches_reference_solver(tmp_path, n, M, steps, adapt_n):
     ref = reference_run(n, M, steps, adapt_n, str(tmp_path / "ref.bin"))
     dev = device_run(n, M, steps, adapt_n)
