@@ -401,7 +401,7 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     return DCCRGX_OK;
 }
 
-static int sync_slots(dccrgx_grid* grid);
+static int sync_slots(dccrgx_grid* grid, bool slot_map_changed);
 
 int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
 {
@@ -460,30 +460,59 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     for (uint64_t i = 0; i < E->local.size(); i++) E->slot_of_g[E->local_g[i]] = (uint32_t)i;
     DX_TRY(device_iota(&E->d_local_slot, E->local.size(), st));  // local position -> slot: identity
     T.lap("owners+local");
-    DX_TRY(sync_slots(grid));
+    DX_TRY(sync_slots(grid, true));
     T.lap("sync_slots");
     return DCCRGX_OK;
 }
 
 // device copies of the slot map and per-slot levels; n_slots
-static int sync_slots(dccrgx_grid* grid)
+__global__ void __launch_bounds__(256) k_slot_levels(MapParams mp, const uint64_t* __restrict__ leaves,
+                                                     const uint32_t* __restrict__ local_g, uint64_t n,
+                                                     uint8_t* __restrict__ level)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride)
+        level[q] = (uint8_t)map_level(mp, leaves[local_g[q]]);
+}
+
+// device copies of the slot map (when it changed) and of the per-slot levels
+// (slots only ever append, or roll back: the local cells' levels come from
+// the device leaf list, appended slots' from the host); n_slots
+static int sync_slots(dccrgx_grid* grid, bool slot_map_changed)
 {
     Explicit* E = grid->ex;
     hipStream_t st = grid->ctx->compute;
     DX_HIP(hipStreamSynchronize(st));
-    dx_free(E->d_slot_of_g);
-    dx_free(E->d_level);
-    E->d_slot_of_g = nullptr;
-    E->d_level = nullptr;
-    // slots only ever append (or roll back), so only new slots' levels are computed
-    std::vector<uint8_t>& level = E->h_level;
-    if (level.size() > E->slot_ids.size()) level.resize(E->slot_ids.size());
-    for (size_t s = level.size(); s < E->slot_ids.size(); s++)
-        level.push_back((uint8_t)map_level(grid->map, E->slot_ids[s]));
-    DX_TRY(upload(grid->ctx, E->slot_of_g, &E->d_slot_of_g, st));
-    DX_TRY(upload(grid->ctx, level, &E->d_level, st));
+    const uint64_t ns = E->slot_ids.size(), nl = E->local.size();
+    if (slot_map_changed || !E->d_slot_of_g) {
+        dx_free(E->d_slot_of_g);
+        E->d_slot_of_g = nullptr;
+        DX_TRY(upload(grid->ctx, E->slot_of_g, &E->d_slot_of_g, st));
+    }
+    if (ns > E->d_level_cap || !E->d_level) {
+        const uint64_t cap = std::max<uint64_t>(ns + ns / 4, 16);
+        uint8_t* d = nullptr;
+        DX_HIP(dx_malloc(&d, cap));
+        if (E->d_level && E->d_level_n) DX_HIP(hipMemcpyAsync(d, E->d_level, E->d_level_n, hipMemcpyDeviceToDevice, st));
+        dx_free(E->d_level);  // waits for the copy
+        E->d_level = d;
+        E->d_level_cap = cap;
+    }
+    if (E->d_level_n == 0 && nl) {
+        hipLaunchKernelGGL(k_slot_levels, dim3(grid_for(nl)), dim3(256), 0, st, grid->map, E->d_leaves, E->d_local_g,
+                           nl, E->d_level);
+        DX_HIP(hipGetLastError());
+        E->d_level_n = nl;
+    }
+    E->d_level_n = std::min(E->d_level_n, ns);
+    if (ns > E->d_level_n) {
+        std::vector<uint8_t> tail(ns - E->d_level_n);
+        for (uint64_t k = E->d_level_n; k < ns; k++) tail[k - E->d_level_n] = (uint8_t)map_level(grid->map, E->slot_ids[k]);
+        DX_TRY(dx_h2d(grid->ctx, E->d_level + E->d_level_n, tail.data(), tail.size(), st));
+        E->d_level_n = ns;
+    }
     DX_HIP(hipStreamSynchronize(st));
-    grid->n_slots = E->slot_ids.size();
+    grid->n_slots = ns;
     return DCCRGX_OK;
 }
 
@@ -530,13 +559,17 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
 {
     Explicit* E = grid->ex;
     const uint64_t old_ns = E->slot_ids.size();
+    bool leaf_slot = false;  // a leaf got a (ghost) slot: the slot map changes
     for (uint64_t c : ids) {
-        if (std::binary_search(E->local.begin(), E->local.end(), c) || E->extra.count(c)) continue;
+        const int64_t g = E->find(c);
+        if ((g >= 0 && E->slot_of_g[g] != NO_SLOT) || E->extra.count(c)) continue;  // has a slot
         const uint32_t s = (uint32_t)E->slot_ids.size();
         E->slot_ids.push_back(c);
         E->extra.set(c, s);
-        const int64_t g = E->find(c);
-        if (g >= 0) E->slot_of_g[g] = s;
+        if (g >= 0) {
+            E->slot_of_g[g] = s;
+            leaf_slot = true;
+        }
     }
     const uint64_t ns = E->slot_ids.size();
     DX_CHECK(ns < NO_SLOT, DCCRGX_EINVAL, "%llu storage slots on one rank", (unsigned long long)ns);
@@ -554,7 +587,7 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
             return s;
         }
     }
-    return sync_slots(grid);
+    return sync_slots(grid, leaf_slot);
 }
 
 int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)

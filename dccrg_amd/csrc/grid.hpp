@@ -144,7 +144,7 @@ struct Explicit {
     uint32_t* d_slot_of_g = nullptr;
     uint32_t* d_local_slot = nullptr;               // local position -> slot (identity)
     uint8_t* d_level = nullptr;                     // refinement level of each slot
-    std::vector<uint8_t> h_level;                   // host copy
+    uint64_t d_level_n = 0, d_level_cap = 0;        // levels written, capacity
     bool defer_fields = false;                      // rebuild(): fields are moved afterwards
     struct HoodLists {
         std::vector<uint64_t> h_nof_row, h_nto_row;
