@@ -74,11 +74,64 @@ __global__ void __launch_bounds__(256) k_uniform_nbrs(UGeom g, const int32_t* __
 }
 
 // fill pass with coalesced stores: one wave per 64 query cells.  Each lane
-// lists its cell's valid items in LDS at the cell's position in the wave's
-// output run (row[] is already scanned), then the wave writes the run entry
-// by entry, consecutive lanes on consecutive entries.  LDS: 4 B per
-// (cell, item) record + the cells' coordinates.
+// lists its cell's valid neighbors (id and item) in LDS at the cell's
+// position in the wave's output run (row[] is already scanned), then the wave
+// writes the run entry by entry, consecutive lanes on consecutive entries;
+// the offsets of an item come from a per-item table in LDS.  LDS: 10 B per
+// (cell, item) record + 12 B per item.
 __global__ void __launch_bounds__(64) k_uniform_fill(UGeom g, const int32_t* __restrict__ items, int K,
+                                                     const uint64_t* __restrict__ cells, size_t n,
+                                                     const uint64_t* __restrict__ row, uint64_t* __restrict__ ids,
+                                                     int32_t* __restrict__ off3, int32_t sx, int32_t sy, int32_t sz)
+{
+    extern __shared__ uint64_t nid[];                       // 64 * K neighbor ids
+    uint16_t* kit = reinterpret_cast<uint16_t*>(nid + 64 * K);  // 64 * K item numbers
+    int32_t* otab = reinterpret_cast<int32_t*>(kit + 64 * K);   // K * 3 offsets (original axes, scaled)
+    const int lane = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t i = t0 + lane;
+    const uint64_t base = row[t0];
+    const uint64_t end = row[t0 + 64 < n ? t0 + 64 : n];
+    if (off3)
+        for (int k = lane; k < K; k += 64) {
+            int32_t o[3];
+            for (int d = 0; d < 3; d++) o[g.perm[d]] = items[3 * k + d];
+            otab[3 * k + 0] = o[0] * sx;
+            otab[3 * k + 1] = o[1] * sy;
+            otab[3 * k + 2] = o[2] * sz;
+        }
+    if (i < n) {
+        const uint64_t id = cells[i];
+        if (id >= 1 && id <= g.N) {
+            int64_t a, b, c;
+            ug_decompose(g, id - 1, a, b, c);
+            uint32_t w = (uint32_t)(row[i] - base);
+            for (int k = 0; k < K; k++) {
+                uint64_t nlin;
+                int64_t cu;
+                if (ug_neighbor(g, a, b, c, items + 3 * k, nlin, cu)) {
+                    nid[w] = nlin + 1;
+                    kit[w] = (uint16_t)k;
+                    w++;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t tot = end - base;
+    for (uint64_t e = lane; e < tot; e += 64) {
+        ids[base + e] = nid[e];
+        if (off3) {
+            const int k = kit[e];
+            off3[3 * (base + e) + 0] = otab[3 * k + 0];
+            off3[3 * (base + e) + 1] = otab[3 * k + 1];
+            off3[3 * (base + e) + 2] = otab[3 * k + 2];
+        }
+    }
+}
+
+// the same for large neighborhoods (4-B records, ids recomputed at the store)
+__global__ void __launch_bounds__(64) k_uniform_fill_rec(UGeom g, const int32_t* __restrict__ items, int K,
                                                      const uint64_t* __restrict__ cells, size_t n,
                                                      const uint64_t* __restrict__ row, uint64_t* __restrict__ ids,
                                                      int32_t* __restrict__ off3, int32_t sx, int32_t sy, int32_t sz)
@@ -248,8 +301,11 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     DX_CHECK(!err, DCCRGX_ENOTFOUND, "cell outside the grid");
     if (!ids) return DCCRGX_OK;
     DX_CHECK(cap >= total, DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total);
-    if (n && h->K <= 192) {  // LDS records: 256 B per item (48 KiB at 192)
-        hipLaunchKernelGGL(k_uniform_fill, dim3((unsigned)((n + 63) / 64)), dim3(64), 64 * 4 * h->K, st, g,
+    if (n && h->K <= 76) {  // LDS records: 652 B per item (48 KiB at 76)
+        hipLaunchKernelGGL(k_uniform_fill, dim3((unsigned)((n + 63) / 64)), dim3(64), 64 * 10 * h->K + 12 * h->K, st,
+                           g, h->d_of_c, h->K, cells, n, row, ids, off3, sc, sc, sc);
+    } else if (n && h->K <= 192) {  // 256 B per item (48 KiB at 192)
+        hipLaunchKernelGGL(k_uniform_fill_rec, dim3((unsigned)((n + 63) / 64)), dim3(64), 64 * 4 * h->K, st, g,
                            h->d_of_c, h->K, cells, n, row, ids, off3, sc, sc, sc);
     } else if (n) {
         hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells,
