@@ -453,6 +453,23 @@ def halo_payload(ctx, D, world, barrier, reduce_max):
             "steps": steps, "sizes": rows}
 
 
+def launch_ranks(n: int) -> int:
+    """Run this script as n ranks on this node (the driver's own command:
+    torch.distributed.run --nnodes=1 --nproc-per-node n --master-addr
+    127.0.0.1), with the same arguments; returns the launcher's exit code.
+    Output of the ranks (rank 0 prints the JSON line) goes to this process's
+    stdout."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -462,11 +479,22 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the other configs' lines (N = 1)")
     ap.add_argument("--no-halo-payload", action="store_true", help="skip the byte-payload halo line")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print each rank's RANK / LOCAL_RANK / WORLD_SIZE as JSON and stop before any GPU call")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # started without a launcher: one process per GPU, spawned here before
+        # this process touches the GPU; rank 0's JSON line is relayed
+        raise SystemExit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world, "gpus": args.gpus,
+                          "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"}),
+              flush=True)
+        return
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 

@@ -79,6 +79,17 @@ _u64p = C.POINTER(C.c_uint64)
 _i32p = C.POINTER(C.c_int32)
 _i64p = C.POINTER(C.c_int64)
 _szp = C.POINTER(C.c_size_t)
+
+# dccrgx_host_transport callbacks
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, _vp, C.c_int32, _i32p, C.POINTER(_vp), _u64p, C.c_int32, _i32p,
+                          C.POINTER(_vp), _u64p)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, _vp, C.POINTER(C.c_double), C.c_int32, C.c_int32)
+
+
+class HostTransport_t(C.Structure):
+    _fields_ = [("user", _vp), ("exchange", EXCHANGE_FN), ("allreduce_f64", ALLREDUCE_FN)]
+
+
 SIGNATURES = {
     "dccrgx_last_error": (C.c_char_p, []),
     "dccrgx_version": (C.c_int, []),
@@ -88,6 +99,7 @@ SIGNATURES = {
     "dccrgx_ctx_comm_init": (C.c_int, [_vp, C.c_char_p]),
     "dccrgx_ctx_route_self_through_rccl": (C.c_int, [_vp, C.c_int32]),
     "dccrgx_ctx_compute_stream": (C.c_int, [_vp, C.POINTER(_vp)]),
+    "dccrgx_ctx_set_host_transport": (C.c_int, [_vp, C.POINTER(HostTransport_t)]),
     "dccrgx_ctx_synchronize": (C.c_int, [_vp]),
     "dccrgx_max_possible_refinement_level": (C.c_int, [_u64p, _i32p]),
     "dccrgx_last_cell": (C.c_int, [C.POINTER(Mapping_t), _u64p]),
@@ -144,6 +156,7 @@ SIGNATURES = {
     "dccrgx_gol_amr_phase": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32]),
     "dccrgx_gol_amr_step": (C.c_int, [_vp, C.c_int32, C.c_int32]),
     "dccrgx_field_init_hash": (C.c_int, [_vp, C.c_int32, C.c_uint32]),
+    "dccrgx_field_checksum": (C.c_int, [_vp, C.c_int32, _u64p]),
     "dccrgx_kernel_timer": (C.c_int, [_vp, C.c_int32, C.POINTER(C.c_double), _u64p]),
     "dccrgx_advect_fluxes": (C.c_int, [_vp, C.c_int32, C.POINTER(AdvectFields_t), C.c_double, C.c_int32]),
     "dccrgx_advect_apply": (C.c_int, [_vp, C.POINTER(AdvectFields_t)]),

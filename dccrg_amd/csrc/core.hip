@@ -521,6 +521,20 @@ int dccrgx_ctx_route_self_through_rccl(dccrgx_ctx* c, int32_t on)
     return DCCRGX_OK;
 }
 
+int dccrgx_ctx_set_host_transport(dccrgx_ctx* c, const dccrgx_host_transport* t)
+{
+    DX_CHECK(c, DCCRGX_EINVAL, "null context");
+    if (!t) {
+        c->host_tx = dccrgx_host_transport{};
+        c->has_host_tx = false;
+        return DCCRGX_OK;
+    }
+    DX_CHECK(t->exchange && t->allreduce_f64, DCCRGX_EINVAL, "transport without exchange / allreduce_f64");
+    c->host_tx = *t;
+    c->has_host_tx = true;
+    return DCCRGX_OK;
+}
+
 int dccrgx_ctx_comm_init(dccrgx_ctx* c, const uint8_t uid[128])
 {
     DX_CHECK(c && uid, DCCRGX_EINVAL, "null argument");

@@ -1109,4 +1109,12 @@ int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, boo
     return DCCRGX_OK;
 }
 
+// id of each local slot [0, nl): the ascending local ids
+int explicit_local_ids(const dccrgx_grid* grid, uint64_t* d_ids, hipStream_t st)
+{
+    const auto& L = grid->ex->local;
+    if (L.empty()) return DCCRGX_OK;
+    return dx_h2d(grid->ctx, d_ids, L.data(), L.size() * 8, st);
+}
+
 }  // namespace dccrgx

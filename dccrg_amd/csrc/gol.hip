@@ -949,6 +949,59 @@ static unsigned grid_for(uint64_t n)
     return (unsigned)g;
 }
 
+// checksum of a 4-byte field over the local cells: (sum v, sum v * splitmix64(id))
+// mod 2^64.  Local position i holds cell ids[i] (explicit grids) or lin0 + i + 1
+// (uniform grids, slot lin0 + i + soff).  Per-block partials, then one block
+// sums them in a fixed order (no atomics, bit-reproducible).
+__global__ void __launch_bounds__(256) k_checksum(const uint32_t* __restrict__ f, uint64_t n, uint64_t lin0,
+                                                  uint64_t soff, const uint64_t* __restrict__ ids,
+                                                  uint64_t* __restrict__ partial)
+{
+    uint64_t s0 = 0, s1 = 0;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t v = ids ? f[i] : f[lin0 + i + soff];
+        const uint64_t id = ids ? ids[i] : lin0 + i + 1;
+        s0 += v;
+        s1 += v * splitmix64(id);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += __shfl_down(s0, o, 64);
+        s1 += __shfl_down(s1, o, 64);
+    }
+    __shared__ uint64_t w0[4], w1[4];
+    if (threadIdx.x % 64 == 0) {
+        w0[threadIdx.x / 64] = s0;
+        w1[threadIdx.x / 64] = s1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partial[2 * blockIdx.x] = w0[0] + w0[1] + w0[2] + w0[3];
+        partial[2 * blockIdx.x + 1] = w1[0] + w1[1] + w1[2] + w1[3];
+    }
+}
+
+__global__ void __launch_bounds__(64) k_checksum_final(const uint64_t* __restrict__ partial, uint32_t nb,
+                                                       uint64_t* __restrict__ out)
+{
+    uint64_t s0 = 0, s1 = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += 64) {
+        s0 += partial[2 * b];
+        s1 += partial[2 * b + 1];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += __shfl_down(s0, o, 64);
+        s1 += __shfl_down(s1, o, 64);
+    }
+    if (threadIdx.x == 0) {
+        out[0] = s0;
+        out[1] = s1;
+    }
+}
+
+// the local cells' ids in slot order, explicit grids (explicit.hip)
+int explicit_local_ids(const dccrgx_grid* grid, uint64_t* d_ids, hipStream_t st);
+
 int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& out, const Field& cnt,
                int64_t s0, int64_t s1, hipStream_t st)
 {
@@ -1242,6 +1295,41 @@ int dccrgx_field_init_hash(dccrgx_grid* grid, int32_t fid, uint32_t permille)
     DX_HIP(hipGetLastError());
     DX_HIP(hipStreamSynchronize(grid->ctx->compute));
     return DCCRGX_OK;
+}
+
+int dccrgx_field_checksum(const dccrgx_grid* grid, int32_t fid, uint64_t out[2])
+{
+    DX_CHECK(grid && out && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad argument");
+    const Field& F = grid->fields[fid];
+    DX_CHECK(F.elem == 4 && !F.variable, DCCRGX_EINVAL, "4-byte field expected");
+    out[0] = out[1] = 0;
+    const uint64_t n = grid->n_local;
+    if (!n) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    const unsigned nb = grid_for(n);
+    uint64_t* d = nullptr;
+    uint64_t* ids = nullptr;
+    DX_HIP(dx_malloc(&d, (2 * (size_t)nb + 2) * 8));
+    int s = DCCRGX_OK;
+    uint64_t lin0 = 0, soff = 0;
+    if (grid->uniform) {
+        lin0 = grid->g.lo;
+        soff = (uint64_t)(-grid->g.cbase * (int64_t)grid->g.S);
+    } else {
+        if (dx_malloc(&ids, n * 8) != hipSuccess) s = set_error(DCCRGX_ENOMEM, "checksum: no device memory");
+        if (s == DCCRGX_OK) s = explicit_local_ids(grid, ids, st);
+    }
+    if (s == DCCRGX_OK) {
+        hipLaunchKernelGGL(k_checksum, dim3(nb), dim3(256), 0, st, (const uint32_t*)F.ptr, n, lin0, soff,
+                           (const uint64_t*)ids, d);
+        hipLaunchKernelGGL(k_checksum_final, dim3(1), dim3(64), 0, st, (const uint64_t*)d, nb, d + 2 * nb);
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(out, d + 2 * nb, 16, hipMemcpyDeviceToHost, st) ||
+            hipStreamSynchronize(st) != hipSuccess)
+            s = set_error(DCCRGX_EHIP, "checksum kernel failed");
+    }
+    dx_free(ids);
+    dx_free(d);
+    return s;
 }
 
 int dccrgx_kernel_timer(dccrgx_grid* grid, int32_t reset, double* ms, uint64_t* launches)

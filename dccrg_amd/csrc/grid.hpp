@@ -119,6 +119,8 @@ struct PeerPlan {
     size_t send_buf_bytes = 0;
     void* d_recv_buf = nullptr;
     size_t recv_buf_bytes = 0;
+    // host copies of the messages (host-staged transport)
+    std::vector<char> h_send_msg, h_recv_msg;
 };
 
 struct Explicit {

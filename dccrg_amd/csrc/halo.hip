@@ -344,6 +344,54 @@ static int64_t primary_slot(const dccrgx_grid* grid, uint64_t id)
 
 int64_t host_primary_slot(const dccrgx_grid* grid, uint64_t id) { return primary_slot(grid, id); }
 
+// One whole update through the host-staged transport (dccrgx_ctx_set_host_transport):
+// pack every peer's message on the compute stream (after the queued work),
+// copy the messages to host memory, one exchange() call, copy back, unpack.
+// Complete on return, so the wait calls have nothing left to do.
+static int host_exchange(dccrgx_grid* g, Hood& h, const int32_t* f, size_t nf)
+{
+    Ctx* c = g->ctx;
+    hipStream_t st = c->compute;
+    std::vector<int32_t> sp, rp;
+    std::vector<const void*> sb;
+    std::vector<void*> rb;
+    std::vector<uint64_t> sn, rn;
+    for (PeerPlan& p : h.peers) {
+        if (!p.send_ids.empty()) {
+            const size_t b = message_bytes(g, p, f, nf, true);
+            p.h_send_msg.resize(std::max<size_t>(b, 1));
+            if (b) {
+                DX_TRY(ensure(&p.d_send_buf, &p.send_buf_bytes, b));
+                DX_TRY(pack_peer(g, p, f, nf, p.d_send_buf, st));
+                DX_TRY(dx_d2h(c, p.h_send_msg.data(), p.d_send_buf, b, st));
+            }
+            sp.push_back(p.peer);
+            sb.push_back(p.h_send_msg.data());
+            sn.push_back(b);
+        }
+        if (!p.recv_ids.empty()) {
+            const size_t b = message_bytes(g, p, f, nf, false);
+            p.h_recv_msg.resize(std::max<size_t>(b, 1));
+            rp.push_back(p.peer);
+            rb.push_back(p.h_recv_msg.data());
+            rn.push_back(b);
+        }
+    }
+    const int r = c->host_tx.exchange(c->host_tx.user, (int32_t)sp.size(), sp.data(), sb.data(), sn.data(),
+                                      (int32_t)rp.size(), rp.data(), rb.data(), rn.data());
+    DX_CHECK(r == 0, DCCRGX_ERCCL, "host transport: exchange returned %d", r);
+    size_t k = 0;
+    for (PeerPlan& p : h.peers) {
+        if (p.recv_ids.empty()) continue;
+        const size_t b = rn[k++];
+        if (!b) continue;
+        DX_TRY(ensure(&p.d_recv_buf, &p.recv_buf_bytes, b));
+        DX_TRY(dx_h2d(c, p.d_recv_buf, p.h_recv_msg.data(), b, st));
+        DX_TRY(unpack_peer(g, p, f, nf, p.d_recv_buf, st));
+    }
+    return DCCRGX_OK;
+}
+
 static int halo_finish(dccrgx_grid* grid, Hood& h, const int32_t* f, size_t nf)
 {
     bool var = false;
@@ -479,6 +527,7 @@ int dccrgx_halo_start(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size
     bool any = false;
     for (const PeerPlan& p : h->peers) any |= !p.send_ids.empty() || !p.recv_ids.empty();
     if (!any) return DCCRGX_OK;
+    if (!c->has_comm && c->has_host_tx) return host_exchange(grid, *h, f, nf);
     DX_CHECK(c->has_comm, DCCRGX_ESTATE,
              "rank %d has remote neighbors but no RCCL communicator (dccrgx_ctx_comm_init)", c->rank);
     // the comm stream starts after everything queued so far on the compute stream
@@ -572,6 +621,28 @@ int dccrgx_exchange_start(dccrgx_grid* grid, int32_t hood_id, const void* const*
         msgs.push_back(m);
     }
     if (!any) return DCCRGX_OK;
+    if (!c->has_comm && c->has_host_tx) {  // host-resident payloads: straight to the transport
+        std::vector<int32_t> sp, rp;
+        std::vector<const void*> sb;
+        std::vector<void*> rb;
+        std::vector<uint64_t> sn, rn;
+        for (Msg& m : msgs) {
+            if (!m.p->send_ids.empty()) {
+                sp.push_back(m.p->peer);
+                sb.push_back(m.sh);
+                sn.push_back(m.sb);
+            }
+            if (!m.p->recv_ids.empty()) {
+                rp.push_back(m.p->peer);
+                rb.push_back(m.rh);
+                rn.push_back(m.rb);
+            }
+        }
+        const int r = c->host_tx.exchange(c->host_tx.user, (int32_t)sp.size(), sp.data(), sb.data(), sn.data(),
+                                          (int32_t)rp.size(), rp.data(), rb.data(), rn.data());
+        DX_CHECK(r == 0, DCCRGX_ERCCL, "host transport: exchange returned %d", r);
+        return DCCRGX_OK;
+    }
     DX_CHECK(c->has_comm, DCCRGX_ESTATE, "rank %d has remote neighbors but no RCCL communicator", c->rank);
     for (Msg& m : msgs) {
         if (m.sb) {

@@ -310,6 +310,10 @@ struct Ctx {
     // the multi-rank halo path (pack, grouped send/recv, unpack, inner/outer
     // overlap) runs on one GPU through the real communicator
     bool self_peer = false;
+    // host-staged transport (dccrgx_ctx_set_host_transport) for ranks without
+    // a communicator
+    dccrgx_host_transport host_tx{};
+    bool has_host_tx = false;
     // pinned bounce buffer of dx_h2d / dx_d2h
     void* stage = nullptr;
     size_t stage_bytes = 0;

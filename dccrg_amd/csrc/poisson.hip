@@ -772,8 +772,15 @@ int allreduce(dccrgx_poisson* P)
 {
     Ctx* c = P->grid->ctx;
     if (!multi_rank(c)) return DCCRGX_OK;
-    DX_CHECK(c->has_comm, DCCRGX_ESTATE, "Poisson solve on %d ranks needs the RCCL communicator", c->comm_size);
     double* red = &P->d_state->red;
+    if (!c->has_comm && c->has_host_tx) {  // host-staged transport (ranks sharing a GPU)
+        double v = 0;
+        DX_TRY(dx_d2h(c, &v, red, 8, c->compute));
+        const int r = c->host_tx.allreduce_f64(c->host_tx.user, &v, 1, 0);
+        DX_CHECK(r == 0, DCCRGX_ERCCL, "host transport: allreduce returned %d", r);
+        return dx_h2d(c, red, &v, 8, c->compute);
+    }
+    DX_CHECK(c->has_comm, DCCRGX_ESTATE, "Poisson solve on %d ranks needs the RCCL communicator", c->comm_size);
     DX_RCCL(ncclAllReduce(red, red, 1, ncclFloat64, ncclSum, c->nccl, c->compute));
     return DCCRGX_OK;
 }

@@ -624,6 +624,13 @@ class Dccrg:
     def field_id(self, name: str) -> int:
         return self._fields[name][0]
 
+    def checksum(self, name: str) -> Tuple[int, int]:
+        """(sum of values, sum of value * splitmix64(id)) mod 2^64 of a 4-byte
+        field over the local cells, on the device (dccrgx_field_checksum)."""
+        out = (C.c_uint64 * 2)()
+        check(lib().dccrgx_field_checksum(self._h, self.field_id(name), out))
+        return int(out[0]), int(out[1])
+
     def write_local(self, name: str, values: np.ndarray):
         """values: one element per local cell, ascending ids; a field whose
         element is an array (e.g. np.dtype((np.uint64, 9))) takes (n, ...)."""

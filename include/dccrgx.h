@@ -74,6 +74,24 @@ int dccrgx_ctx_comm_init(dccrgx_ctx* ctx, const uint8_t uid[128]);
  * (a peer plan with peer == rank) instead of device copies, so the whole
  * multi-rank halo path runs on a single GPU.  Needs dccrgx_ctx_comm_init. */
 int dccrgx_ctx_route_self_through_rccl(dccrgx_ctx* ctx, int32_t on);
+/* Host-staged transport for ranks that cannot have an RCCL communicator --
+ * several processes sharing one GPU, which RCCL refuses ("Duplicate GPU").
+ * With no communicator and a transport set, every halo message of a peer is
+ * packed on the device (the same plans as the RCCL path), copied to host
+ * memory, and one exchange() call moves all messages of the update between
+ * the processes (blocking: it returns when every receive buffer is filled);
+ * the received bytes are copied back and unpacked.  allreduce_f64 combines
+ * the solvers' scalars across ranks (op: 0 sum, 1 min, 2 max), the
+ * MPI_Allreduce of tests/poisson/poisson_solve.hpp:349, 426, 486.  The
+ * callbacks return 0 on success.  Pass NULL to remove the transport. */
+typedef struct {
+    void* user;
+    int (*exchange)(void* user, int32_t n_send, const int32_t* send_peers, const void* const* send_bufs,
+                    const uint64_t* send_bytes, int32_t n_recv, const int32_t* recv_peers,
+                    void* const* recv_bufs, const uint64_t* recv_bytes);
+    int (*allreduce_f64)(void* user, double* values, int32_t n, int32_t op);
+} dccrgx_host_transport;
+int dccrgx_ctx_set_host_transport(dccrgx_ctx* ctx, const dccrgx_host_transport* transport);
 int dccrgx_ctx_compute_stream(dccrgx_ctx* ctx, void** hip_stream_out);
 int dccrgx_ctx_synchronize(dccrgx_ctx* ctx);
 
@@ -334,6 +352,11 @@ int dccrgx_gol_amr_step(dccrgx_grid* grid, int32_t hood_id, int32_t f_data);
  * tests/game_of_life/scalability3d.cpp:106-114 with an order-independent,
  * reproducible generator) */
 int dccrgx_field_init_hash(dccrgx_grid* grid, int32_t field_id, uint32_t permille);
+/* checksum of a 4-byte field over this rank's local cells, computed on the
+ * device: out[0] = sum of the values, out[1] = sum of value *
+ * splitmix64(cell id), both mod 2^64 (the live-cell count of the game of
+ * life, and a position-sensitive check of a whole grid without copying it) */
+int dccrgx_field_checksum(const dccrgx_grid* grid, int32_t field_id, uint64_t out[2]);
 /* time the last dccrgx_gol_compute kernels (HIP events on the compute
  * stream): total ms and launch count since the last reset */
 int dccrgx_kernel_timer(dccrgx_grid* grid, int32_t reset, double* ms_out, uint64_t* launches_out);

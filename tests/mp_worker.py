@@ -1,0 +1,378 @@
+"""One rank of the multi-process GPU tests (tests/test_gpu_multiprocess.py).
+
+Every rank is its own process with its own libdccrgx context on the one GPU
+of the box, as the reference runs one MPI process per rank.  RCCL refuses
+two ranks on one device, so the halo moves through the library's
+host-staged transport (dccrgx_ctx_set_host_transport) over a gloo process
+group: device pack with the per-peer plans, host copy, isend / irecv,
+device unpack.  Each scenario checks this rank's results against the oracle
+(which computes every rank's view) and the worker writes one JSON object
+{scenario: "ok" | traceback} to <outdir>/rank<r>.json.
+
+usage: python tests/mp_worker.py <outdir> <scenario>[,<scenario>...]
+(RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT in the environment)
+"""
+import json
+import os
+import sys
+import time
+import traceback
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import dccrg_amd as D  # noqa: E402
+from dccrg_amd.transport import TorchDistTransport  # noqa: E402
+from oracle import dccrg_oracle as O  # noqa: E402
+
+RANK = int(os.environ["RANK"])
+P = int(os.environ["WORLD_SIZE"])
+
+
+def log(msg):
+    print(f"[rank {RANK}/{P} {time.strftime('%H:%M:%S')}] {msg}", flush=True)
+
+
+def make(ctx, length, per, hood, M=0, leaves=None):
+    return (D.Dccrg().set_initial_length(length).set_maximum_refinement_level(M).set_periodic(*per)
+            .set_neighborhood_length(hood).initialize(ctx, leaves=leaves))
+
+
+def gather_all(x):
+    out = [None] * P
+    dist.all_gather_object(out, x)
+    return out
+
+
+# ---------------------------------------------------------------- scenarios --
+def sc_gol(ctx):
+    """Uniform game of life through dccrgx_gol_step (halo start, inner, wait,
+    outer) vs the oracle's run of the whole grid."""
+    cases = [((33, 20, 17), (True, True, True), 1), ((16, 16, 16), (True, True, True), 2),
+             ((65, 17, 9), (True, False, True), 1), ((20, 20, 1), (True, True, False), 1),
+             ((12, 10, 8), (False, True, False), 0)]
+    for length, per, hood in cases:
+        n = int(np.prod(length))
+        a0 = O.random_alive(np.arange(1, n + 1, dtype=np.uint64), 300)
+        steps = 6
+        ref_a, ref_n = O.gol_reference_run(length, per, hood, a0, steps)
+        g = make(ctx, length, per, hood)
+        ref = O.Grid(length, 0, per, hood).rank_view(RANK, P)
+        assert g.local_cells().tolist() == ref["local"]
+        assert g.get_cells_to_send() == ref["send"] and g.get_cells_to_receive() == ref["recv"]
+        for f in ("a", "b", "n"):
+            g.add_field(f, np.uint32)
+        loc = g.local_cells().astype(np.int64)
+        g.write_local("a", a0[loc - 1])
+        cur, nxt = "a", "b"
+        for _ in range(steps):
+            g.gol_step(cur, nxt, "n")
+            cur, nxt = nxt, cur
+        assert np.array_equal(g.read_local(cur), ref_a[loc - 1]), (length, per, hood)
+        assert np.array_equal(g.read_local("n"), ref_n[loc - 1]), (length, per, hood)
+        g.close()
+
+
+def sc_gol_explicit(ctx):
+    """Mixed-level grids: the iteration-cache game of life (game_of_life.cpp:
+    54-79 over neighbors_of) with the split start / inner / wait / outer."""
+    from test_gpu_explicit import CASES, gol_cache_reference, leaves_for
+    for case in (CASES[2], CASES[4], CASES[8]):
+        leaves = leaves_for(case)
+        length, M, per, hood = case[:4]
+        og = O.Grid(length, M, per, hood, leaves)
+        a0 = O.random_alive(np.array(leaves, dtype=np.uint64), 400)
+        steps = 4
+        ref_a, ref_n = gol_cache_reference(og, leaves, a0, steps)
+        g = make(ctx, length, per, hood, M, leaves)
+        ref = og.rank_view(RANK, P)
+        assert g.get_cells_to_send() == ref["send"] and g.get_cells_to_receive() == ref["recv"]
+        pos = {c: i for i, c in enumerate(leaves)}
+        for f in ("a", "b", "n"):
+            g.add_field(f, np.uint32)
+        idx = [pos[int(c)] for c in g.local_cells()]
+        g.write_local("a", a0[idx])
+        cur, nxt = "a", "b"
+        for _ in range(steps):
+            g.start_remote_neighbor_copy_updates(fields=[cur])
+            g.gol_compute(cur, nxt, "n", D._capi.REGION_INNER)
+            g.wait_remote_neighbor_copy_update_receives()
+            g.gol_compute(cur, nxt, "n", D._capi.REGION_OUTER)
+            g.wait_remote_neighbor_copy_update_sends()
+            cur, nxt = nxt, cur
+        assert np.array_equal(g.read_local(cur), ref_a[idx]), case
+        assert np.array_equal(g.read_local("n"), ref_n[idx]), case
+        g.close()
+
+
+def sc_halo_ids(ctx):
+    """examples/basic_cell_data.cpp:27-53 (data = id, periodic, hood 2,
+    max_ref_lvl 1, with one cell refined): every neighbor's copy is its id."""
+    GOLD = json.load(open(os.path.join(HERE, "golden", "reference_kats.json")))
+    k = GOLD["halo_kat"]
+    length, per, hood = tuple(k["length"]), tuple(bool(p) for p in k["periodic"]), k["hood_length"]
+    for leaves in (None, "refined"):
+        lv = None
+        M = 0
+        if leaves:
+            M = 1
+            m = O.Mapping(length, 1)
+            c = int(np.prod(length)) // 2
+            lv = sorted((set(range(1, int(np.prod(length)) + 1)) - {c}) | set(m.get_all_children(c)))
+        g = make(ctx, length, per, hood, M, lv)
+        g.add_field("id", np.uint64)
+        g.write_local("id", g.local_cells())
+        g.update_copies_of_remote_neighbors(fields=["id"])
+        rem = g.remote_cells()
+        assert len(rem) > 0 or P == 1
+        recv = sorted(set(c for v in g.get_cells_to_receive().values() for c in v))
+        got = np.concatenate(g.read_cells("id", recv)) if recv else np.zeros(0, np.uint64)
+        bad = [(c, int(v)) for c, v in zip(recv, got) if int(v) != c]
+        assert not bad, (leaves, len(recv), len(rem), bad[:20])
+        for c in g.local_cells()[:50]:
+            nb = [n for n, _ in g.get_neighbors_of(int(c))]
+            assert [int(v) for v in np.concatenate(g.read_cells("id", nb))] == nb, (leaves, int(c))
+        g.close()
+
+
+def sc_variable(ctx):
+    """tests/variable_data_size/variable_neighbour_data.cpp:82-130."""
+    g = make(ctx, (3, 1, 1), (False, False, False), 1)
+    g.add_variable_field("v1", np.int32)
+    g.add_variable_field("v2", np.int32)
+    local = [int(c) for c in g.local_cells()]
+    g.resize("v1", local, local)
+    g.resize("v2", local, local)
+    g.write_cells("v1", local, [np.arange(c, 2 * c) for c in local])
+    g.write_cells("v2", local, [-np.arange(c, 2 * c) for c in local])
+    remote = [int(c) for c in g.remote_cells()]
+    g.resize("v1", remote, remote)
+    g.resize("v2", remote, remote)
+    g.update_copies_of_remote_neighbors(fields=["v1", "v2"])
+    seen = {}
+    for c in local:
+        assert g.read_cells("v1", [c])[0].tolist() == list(range(c, 2 * c))
+        nbrs = [n for n, _ in g.get_neighbors_of(c)]
+        seen[c] = [v for arr in g.read_cells("v2", nbrs) for v in arr.tolist()]
+    want = {1: [-2, -3], 2: [-1, -3, -4, -5], 3: [-2, -3]}
+    assert seen == {c: want[c] for c in local}
+    # a fixed field in the same message, then variable payloads on a 3-D grid
+    length = (6, 5, 9)
+    g2 = make(ctx, length, (False, False, True), 1)
+    rng = np.random.default_rng(11)
+    n = int(np.prod(length))
+    counts = rng.integers(0, 6, n + 1)
+    payload = {c: rng.standard_normal(counts[c]) for c in range(1, n + 1)}
+    g2.add_variable_field("var", np.float64)
+    g2.add_field("tag", np.uint32)
+    local = [int(c) for c in g2.local_cells()]
+    g2.resize("var", local, counts[local])
+    g2.write_cells("var", local, [payload[c] for c in local])
+    g2.write_local("tag", np.array(local, dtype=np.uint32) * 7)
+    remote = [int(c) for c in g2.remote_cells()]
+    if remote:
+        g2.resize("var", remote, counts[remote])
+    g2.update_copies_of_remote_neighbors(fields=["var", "tag"])
+    for c, arr in zip(remote, g2.read_cells("var", remote)):
+        assert np.array_equal(arr, payload[c]), c
+    for c, t in zip(remote, g2.read_remote("tag")):
+        assert int(t) == 7 * c
+    g.close()
+    g2.close()
+
+
+def sc_amr(ctx):
+    """Random refine / unrefine sequences with the collective stop_refining
+    (requests all-gathered over the process group), vs the oracle's ranks."""
+    from oracle.dccrg_amr import AmrOracle
+    for length, M, per, hood, rounds, seed in [((4, 4, 1), 2, (True, True, False), 1, 4, 1),
+                                               ((5, 3, 3), 2, (True, False, True), 1, 3, 2),
+                                               ((3, 3, 3), 1, (True, True, True), 2, 3, 4)]:
+        rng = np.random.default_rng(seed)
+        o = AmrOracle(length, M, per, hood, P)
+        g = make(ctx, length, per, hood, M)
+        g.add_field("v", np.float64)
+        g.write_local("v", g.local_cells().astype(np.float64))
+        for rnd in range(rounds):
+            cells = o.cells()
+            picks = rng.choice(cells, min(len(cells), 8), replace=False)
+            for c in picks:
+                c = int(c)
+                r = o.owner(c)
+                k = int(rng.integers(4)) if rnd > 0 else 0
+                fn = ("refine_completely", "unrefine_completely", "dont_unrefine", "dont_refine")[k]
+                if k == 3 and rng.integers(3):
+                    continue
+                want = getattr(o, fn)(r, c)
+                if r == RANK:
+                    assert getattr(g, fn)(c) == want, (fn, c)
+            new = g.stop_refining()
+            want = o.stop_refining()
+            assert [int(c) for c in new] == want[RANK]
+            assert [int(c) for c in g.get_removed_cells()] == o.get_removed_cells(RANK)
+            g.clear_refined_unrefined_data()
+            allc = sorted(c for part in gather_all([int(c) for c in g.local_cells()]) for c in part)
+            assert allc == o.cells()
+            ref = o.grid.rank_view(RANK, P)
+            assert [int(c) for c in g.local_cells()] == ref["local"]
+            assert [int(c) for c in g.inner_cells()] == ref["inner"]
+            assert [int(c) for c in g.outer_cells()] == ref["outer"]
+            assert g.get_cells_to_send() == ref["send"] and g.get_cells_to_receive() == ref["recv"]
+            # data moves with the new plans: surviving cells keep theirs, ghosts match
+            loc = g.local_cells()
+            vals = g.read_local("v")
+            isnew = np.isin(loc, new)
+            assert np.all(vals[isnew] == 0)
+            g.write_local("v", loc.astype(np.float64))
+            g.update_copies_of_remote_neighbors(fields=["v"])
+            rem = g.remote_cells()
+            if len(rem):
+                assert np.array_equal(np.concatenate(g.read_cells("v", rem)), rem.astype(np.float64))
+        g.close()
+
+
+def sc_advection(ctx):
+    """tests/advection/2d.cpp with adapt_n = 1: per-rank leaf sets and
+    densities vs the oracle's P-rank run; dt reduced with MIN across ranks
+    (solve.hpp:317)."""
+    from dccrg_amd import advection as A
+    from oracle.dccrg_amr import AdvectionAmrOracle
+    cells, M, steps = 16, 2, 4
+    rel, thr, sens, cfl = 0.025, 0.25, 0.5, 0.5
+    ref = AdvectionAmrOracle(cells, M, P, rel, thr, sens, cfl)
+    g = (D.Dccrg().set_initial_length((cells, cells, 1)).set_maximum_refinement_level(M)
+         .set_periodic(True, True, False).set_neighborhood_length(0).initialize(ctx))
+    g.add_advection_fields()
+    geom = A.geometry_2d(g)
+    A.initialize(g, geom)
+    for _ in range(M):
+        A.adapt_grid(g, geom, *A.check_for_adaptation(g, rel / M, thr, sens))
+        A.initialize(g, geom)
+
+    def dt_min():
+        t = torch.tensor([g.max_time_step()], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return float(t[0])
+
+    def compare(tag):
+        rc, ra = ref.arrays()
+        pos = {c: i for i, c in enumerate(rc)}
+        loc = [int(c) for c in g.local_cells()]
+        assert loc == [c for c in rc if ref.o.owner(c) == RANK], tag
+        scale = np.max(np.abs(ra[0]))
+        want = ra[0][[pos[c] for c in loc]]
+        assert np.max(np.abs(g.read_local("density") - want), initial=0.0) <= 1e-12 * scale, tag
+
+    compare("prerefined")
+    dt = dt_min()
+    assert abs(dt - ref.dt) <= 1e-15 * ref.dt
+    for s in range(steps):
+        g.update_copies_of_remote_neighbors(fields=["density"])
+        sets = A.check_for_adaptation(g, rel / M, thr, sens)
+        g.start_remote_neighbor_copy_updates(fields=["density"])
+        g.calculate_fluxes(cfl * dt, True)
+        g.wait_remote_neighbor_copy_update_receives()
+        g.calculate_fluxes(cfl * dt, False)
+        g.wait_remote_neighbor_copy_update_sends()
+        g.apply_fluxes()
+        A.adapt_grid(g, geom, *sets)
+        dt = dt_min()
+        ref.step()
+        compare(f"step {s}")
+        assert abs(dt - ref.dt) <= 1e-15 * ref.dt
+    g.close()
+
+
+def sc_poisson(ctx):
+    """Poisson BiCG across ranks (tests/poisson/poisson_solve.hpp:283-522):
+    per-rank partial dot products summed through the transport's all-reduce,
+    ghosts of p0 / p1 exchanged every iteration, vs the oracle's P-rank
+    system (the same per-rank partial sums)."""
+    import test_gpu_poisson as T
+    for name in ("refined792", "stretch_z", "line_boundary", "plane_open"):
+        length, M, per, leaves, l0, solve, skip = T.CASES[name]
+        if leaves == "poisson3d":
+            _, leaves = T.poisson3d_leaves()
+        elif leaves == "random":
+            leaves = O.random_balanced_leaves(length, M, per, 0, 12, 5)
+        og = O.Grid(length, M, per, 0, leaves)
+        cells = [int(c) for c in og.cells()]
+        ln, ctr = T.geometry(length, M, cells, l0)
+        if name == "refined792":
+            rhs = -(81.0 / 16.0) * T.solution_value(ctr[:, 0], ctr[:, 1], ctr[:, 2])
+            guess = np.zeros(len(cells))
+        else:
+            rhs = np.sin(3 * ctr[:, 0]) * np.cos(ctr[:, 1]) + 0.1 * ctr[:, 2]
+            guess = ctr[:, 0] * 0.3 - ctr[:, 1] * 0.1
+        sysm = O.PoissonSystem(og, P, (ln[:, 0], ln[:, 1], ln[:, 2]), solve_cells=solve, skip_cells=skip)
+        g = make(ctx, length, per, 0, M, leaves)
+        for f in ("rhs", "solution", "length_x", "length_y", "length_z"):
+            g.add_field(f, np.float64)
+        pos = {c: i for i, c in enumerate(cells)}
+        loc = [int(c) for c in g.local_cells()]
+        idx = [pos[c] for c in loc]
+        g.write_local("rhs", rhs[idx])
+        for k, a in enumerate(("length_x", "length_y", "length_z")):
+            g.write_local(a, ln[idx, k])
+        solve_set = set(cells if solve is None else solve)
+        my_solve = [c for c in loc if c in solve_set]
+        my_skip = [c for c in loc if c in set(skip)]
+        for iters in (1, 5, 12, None):
+            kw = {} if iters is None else {"max_iterations": iters}
+            s = D.PoissonSolve(g, **kw)
+            g.write_local("solution", guess[idx])
+            it, res = s.solve(my_solve, my_skip)
+            refx, rit, rres = sysm.solve(rhs, guess, **kw)
+            got = g.read_local("solution")
+            scale = max(np.abs(refx).max(), 1.0)
+            diff = np.abs(got - refx[idx]).max(initial=0.0) / scale
+            log(f"poisson {name} iters {iters}: it {it} ref {rit} res {res:.3e} ref {rres:.3e} diff {diff:.2e}")
+            # fixed iteration counts and full solves alike: the oracle's
+            # iteration count, and its iterate within 1e-12 of max|x|
+            assert it == rit, (name, iters, it, rit)
+            assert diff <= 1e-12, (name, iters, diff)
+            s.close()
+        g.close()
+
+
+SCENARIOS = {"gol": sc_gol, "gol_explicit": sc_gol_explicit, "halo_ids": sc_halo_ids, "variable": sc_variable,
+             "amr": sc_amr, "advection": sc_advection, "poisson": sc_poisson}
+
+
+def main():
+    outdir, names = sys.argv[1], sys.argv[2].split(",")
+    dist.init_process_group("gloo", rank=RANK, world_size=P)
+    ctx = D.Context(0, RANK, P)
+    TorchDistTransport().attach(ctx)
+    results = {}
+    for name in names:
+        log(f"{name} ...")
+        try:
+            SCENARIOS[name](ctx)
+            results[name] = "ok"
+        except Exception:
+            results[name] = traceback.format_exc()
+            log(results[name])
+        log(f"{name} {'ok' if results[name] == 'ok' else 'FAILED'}")
+        # keep the ranks in step: a failed rank must not leave the others in a collective
+        ok = gather_all(results[name] == "ok")
+        if not all(ok):
+            for rest in names[names.index(name) + 1:]:
+                results[rest] = "skipped after a failure"
+            break
+    with open(os.path.join(outdir, f"rank{RANK}.json"), "w") as f:
+        json.dump(results, f)
+    ctx.synchronize()
+    ctx.close()
+    dist.destroy_process_group()
+    return 0 if all(v == "ok" for v in results.values()) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -131,12 +131,18 @@ def test_poisson_full_solve(name, path):
     ref, rit, rres = sysm.solve(rhs, guess)
     got = g.read_local("solution")
     scale = max(np.abs(ref).max(), 1.0)
-    if rres <= 1e-15:  # converged: the same discrete solution
-        assert res <= 1e-15 and abs(it - rit) <= 2
-        assert np.abs(got - ref).max() <= 1e-9 * scale
-    else:  # stopped on the residual-increase rule: same best iterate
-        assert it == rit and res == pytest.approx(rres, rel=1e-6)
-        assert np.abs(got - ref).max() <= 1e-9 * scale
+    # the north-star gate: the oracle's iteration count and stopping rule
+    # (converged below stop_residual, or stopped on the residual-increase
+    # rule with the same best iterate), and the solution within 1e-12 of
+    # max|x|.  Only the dot products' summation order differs (block tree vs
+    # the reference's sequential loop), measured at <= 3e-15 of max|x| on
+    # every case and iteration driver (tools/poisson_full_diff.py,
+    # profiles/r3a_poisson_diff.log)
+    assert it == rit
+    assert (res <= 1e-15) == (rres <= 1e-15)
+    if rres > 1e-15:
+        assert res == pytest.approx(rres, rel=1e-9)
+    assert np.abs(got - ref).max() <= TOL * scale
 
 
 def test_poisson_cache_reuse(path):
