@@ -375,8 +375,12 @@ static int check_explicit_memory(const dccrgx_grid* grid, uint64_t N)
         const double K = (double)(kv.second.items.size() / 3);
         need += (double)N * (16 + K * (8 + 12 + 4 + 4));  // rows, neighbors_of (+ transpose)
     }
+    // memory the pool keeps for reuse is free for this purpose: trim it, and
+    // count the spare field buffers of earlier rebuilds as available
+    dx_trim_pool();
     size_t free_b = 0, total_b = 0;
     DX_HIP(hipMemGetInfo(&free_b, &total_b));
+    for (const auto& b : grid->spare_bufs) free_b += b.second;
     DX_CHECK(need < 0.9 * (double)free_b, DCCRGX_ENOMEM,
              "refining a uniform grid of %llu cells needs ~%.1f GB of replicated leaf state and neighbor lists; "
              "%.1f GB free", (unsigned long long)N, need / 1e9, free_b / 1e9);
@@ -795,16 +799,23 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     radix_sort_u64(retired);
     radix_sort_u64(A.new_cells);
     radix_sort_u64(A.removed);
+    T.lap("new leaf set");
+    if (!R.empty() || !final_un.empty()) {
+        // the previous round's refined / unrefined data goes first, as in
+        // execute_refines (dccrg.hpp:10266-10267)
+        if (grid->ex) explicit_clear_retired(grid->ex);
+        const int s = rebuild(grid, leaves, retired);  // transactional: on failure the grid is unchanged
+        if (s != DCCRGX_OK) {  // requests stay pending, nothing was created or removed
+            A.new_cells.clear();
+            A.removed.clear();
+            return s;
+        }
+    }
     // the dont_refine closure persists (:10188), everything else is consumed
     A.to_refine.clear();
     A.to_unrefine.clear();
     A.not_to_unrefine.clear();
     A.not_to_refine = donts;
-    T.lap("new leaf set");
-    if (!R.empty() || !final_un.empty()) {
-        if (grid->ex) explicit_clear_retired(grid->ex);
-        DX_TRY(rebuild(grid, leaves, retired));
-    }
     T.lap("rebuild");
     if (n_new) *n_new = A.new_cells.size();
     return DCCRGX_OK;

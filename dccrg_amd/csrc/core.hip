@@ -462,6 +462,22 @@ int dccrgx_device_count(int* n)
 // ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------
+}  // extern "C"
+
+namespace dccrgx {
+void dx_trim_pool()
+{
+    int dev = 0;
+    hipMemPool_t pool = nullptr;
+    if (hipDeviceSynchronize() != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess)
+        return;
+    (void)hipMemPoolTrimTo(pool, 0);
+}
+}  // namespace dccrgx
+
+extern "C" {
+
 int dccrgx_ctx_create(int device, int rank, int comm_size, dccrgx_ctx** out)
 {
     DX_CHECK(out, DCCRGX_EINVAL, "null out");

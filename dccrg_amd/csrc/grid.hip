@@ -729,6 +729,7 @@ int dccrgx_grid_destroy(dccrgx_grid* grid)
     hipEventDestroy(grid->t0);
     hipEventDestroy(grid->t1);
     delete grid;
+    dx_trim_pool();  // a destroyed grid's memory goes back to the driver (other users of the device)
     return DCCRGX_OK;
 }
 

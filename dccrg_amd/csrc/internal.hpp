@@ -47,11 +47,20 @@ int set_error(int code, const char* fmt, ...);
 // dx_free waits for the device first, as hipFree does.
 void dx_slow_note(const char* what, size_t bytes, double ms);  // DCCRGX_TIMING: allocations over 1 ms
 
+// return the pool's unused memory to the driver (after the device is idle):
+// when a grid is destroyed, and before an allocation is retried
+void dx_trim_pool();
+
 template <class T>
 inline hipError_t dx_malloc(T** p, size_t bytes)
 {
     const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipMallocAsync(reinterpret_cast<void**>(p), bytes ? bytes : 1, nullptr);
+    if (e == hipErrorOutOfMemory) {  // memory held by the pool may still be free for the driver
+        (void)hipGetLastError();
+        dx_trim_pool();
+        e = hipMallocAsync(reinterpret_cast<void**>(p), bytes ? bytes : 1, nullptr);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (ms > 1.0) dx_slow_note("dx_malloc", bytes, ms);

@@ -239,6 +239,35 @@ __global__ void __launch_bounds__(64) k_uniform_gather(UGeom g, const int32_t* _
     }
 }
 
+// the same for neighborhoods too large for the LDS records (> 192 items):
+// one thread per query cell writes its own run
+__global__ void __launch_bounds__(256) k_uniform_gather_direct(UGeom g, const int32_t* __restrict__ items, int K,
+                                                               const uint64_t* __restrict__ cells, size_t n,
+                                                               const uint64_t* __restrict__ row,
+                                                               const uint8_t* __restrict__ field, uint32_t elem,
+                                                               uint8_t* __restrict__ out)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t id = cells[i];
+        if (id < 1 || id > g.N) continue;
+        int64_t a, b, c;
+        ug_decompose(g, id - 1, a, b, c);
+        uint64_t w = row[i];
+        for (int k = 0; k < K; k++) {
+            uint64_t nlin;
+            int64_t cu;
+            if (!ug_neighbor(g, a, b, c, items + 3 * k, nlin, cu)) continue;
+            const int64_t cw = ug_wrap(cu, (int64_t)g.LC);
+            const int64_t cs = ug_local(g, nlin) ? cw : cu;
+            const uint64_t slot = nlin - (uint64_t)cw * g.S + (uint64_t)(cs - g.cbase) * g.S;
+            const uint8_t* src = field + slot * elem;
+            uint8_t* dst = out + (w++) * elem;
+            for (uint32_t q = 0; q < elem; q++) dst[q] = src[q];
+        }
+    }
+}
+
 int explicit_gather_neighbors(const dccrgx_grid* grid, const Hood& h, const Field& F, const uint64_t* cells, size_t n,
                               uint64_t* row, void* out, size_t cap_bytes, hipStream_t st);
 
@@ -352,11 +381,13 @@ int dccrgx_gather_neighbors(const dccrgx_grid* grid, int32_t hood_id, int32_t fi
     if (!out) return DCCRGX_OK;
     DX_CHECK(cap_bytes >= total * F.elem, DCCRGX_ERANGE, "capacity %zu < %llu bytes", cap_bytes,
              (unsigned long long)(total * F.elem));
-    DX_CHECK(h->K <= 192, DCCRGX_EINVAL, "neighborhoods of more than 192 items are not gathered");
-    if (n)
+    if (n && h->K <= 192)  // LDS records: 256 B per item (48 KiB at 192)
         hipLaunchKernelGGL(k_uniform_gather, dim3((unsigned)((n + 63) / 64)), dim3(64), 64 * 4 * h->K, st, g,
                            h->d_of_c, h->K, cells, n, (const uint64_t*)row, (const uint8_t*)F.ptr, F.elem,
                            (uint8_t*)out);
+    else if (n)
+        hipLaunchKernelGGL(k_uniform_gather_direct, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells, n,
+                           (const uint64_t*)row, (const uint8_t*)F.ptr, F.elem, (uint8_t*)out);
     DX_HIP(hipGetLastError());
     return DCCRGX_OK;
 }

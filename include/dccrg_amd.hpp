@@ -112,22 +112,40 @@ struct has_gmd0<C, decltype(void(std::declval<C&>().get_mpi_datatype()))> : std:
 template <class T> struct is_std_array : std::false_type {};
 template <class T, size_t N> struct is_std_array<std::array<T, N>> : std::true_type {};
 
-// the (address, count, datatype) a cell puts on the wire, dccrg_get_cell_datatype.hpp:48-339
+// the (address, count, datatype) a cell puts on the wire, dccrg_get_cell_datatype.hpp:48-339:
+// get_mpi_datatype(id, sender, receiver, receiving, hood), get_mpi_datatype(),
+// a builtin, or a std::array of builtins -- chosen in that order (tag dispatch)
+template <class C>
+struct datatype_kind
+    : std::integral_constant<int, has_gmd5<C>::value ? 0 : has_gmd0<C>::value ? 1 : std::is_arithmetic<C>::value ? 2 : 3> {
+};
+template <class C>
+std::tuple<void*, int, MPI_Datatype> cell_datatype_(C& c, uint64_t id, int s, int r, bool rc, int h,
+                                                    std::integral_constant<int, 0>)
+{
+    return c.get_mpi_datatype(id, s, r, rc, h);
+}
+template <class C>
+std::tuple<void*, int, MPI_Datatype> cell_datatype_(C& c, uint64_t, int, int, bool, int, std::integral_constant<int, 1>)
+{
+    return c.get_mpi_datatype();
+}
+template <class C>
+std::tuple<void*, int, MPI_Datatype> cell_datatype_(C& c, uint64_t, int, int, bool, int, std::integral_constant<int, 2>)
+{
+    return std::make_tuple((void*)&c, 1, builtin_type<C>());
+}
+template <class C>
+std::tuple<void*, int, MPI_Datatype> cell_datatype_(C& c, uint64_t, int, int, bool, int, std::integral_constant<int, 3>)
+{
+    static_assert(is_std_array<C>::value, "Cell_Data needs get_mpi_datatype() or must be a builtin / std::array");
+    return std::make_tuple((void*)c.data(), (int)c.size(), builtin_type<typename C::value_type>());
+}
 template <class C>
 std::tuple<void*, int, MPI_Datatype> cell_datatype(C& c, uint64_t id, int sender, int receiver, bool receiving,
                                                    int hood)
 {
-    if constexpr (has_gmd5<C>::value) {
-        return c.get_mpi_datatype(id, sender, receiver, receiving, hood);
-    } else if constexpr (has_gmd0<C>::value) {
-        (void)id, (void)sender, (void)receiver, (void)receiving, (void)hood;
-        return c.get_mpi_datatype();
-    } else if constexpr (std::is_arithmetic<C>::value) {
-        return std::make_tuple((void*)&c, 1, builtin_type<C>());
-    } else {
-        static_assert(is_std_array<C>::value, "Cell_Data needs get_mpi_datatype() or must be a builtin / std::array");
-        return std::make_tuple((void*)c.data(), (int)c.size(), builtin_type<typename C::value_type>());
-    }
+    return cell_datatype_(c, id, sender, receiver, receiving, hood, datatype_kind<C>());
 }
 
 // dccrg_mpi_support.hpp:66-95
@@ -136,6 +154,35 @@ inline bool is_named(MPI_Datatype t)
     int ni = 0, na = 0, nd = 0, comb = 0;
     MPI_Type_get_envelope(t, &ni, &na, &nd, &comb);
     return comb == MPI_COMBINER_NAMED;
+}
+
+// Host-staged transport over MPI (dccrgx_host_transport) for ranks that
+// share a GPU -- RCCL refuses two ranks on one device.  One update's
+// messages go as the reference's transfer engine moves them: Irecv / Isend
+// per peer, then Waitall (dccrg.hpp:10726-11209); scalars by MPI_Allreduce.
+inline int mpi_exchange(void* user, int32_t ns, const int32_t* sp, const void* const* sb, const uint64_t* sn,
+                        int32_t nr, const int32_t* rp, void* const* rb, const uint64_t* rn)
+{
+    const MPI_Comm comm = *static_cast<const MPI_Comm*>(user);
+    std::vector<MPI_Request> req;
+    for (int32_t i = 0; i < nr; i++)
+        if (rn[i]) {
+            req.push_back(MPI_REQUEST_NULL);
+            if (MPI_Irecv(rb[i], (int)rn[i], MPI_BYTE, rp[i], 0, comm, &req.back()) != MPI_SUCCESS) return 1;
+        }
+    for (int32_t i = 0; i < ns; i++)
+        if (sn[i]) {
+            req.push_back(MPI_REQUEST_NULL);
+            if (MPI_Isend(const_cast<void*>(sb[i]), (int)sn[i], MPI_BYTE, sp[i], 0, comm, &req.back()) != MPI_SUCCESS)
+                return 1;
+        }
+    return MPI_Waitall((int)req.size(), req.data(), MPI_STATUSES_IGNORE) == MPI_SUCCESS ? 0 : 1;
+}
+inline int mpi_allreduce_f64(void* user, double* v, int32_t n, int32_t op)
+{
+    const MPI_Comm comm = *static_cast<const MPI_Comm*>(user);
+    const MPI_Op o = op == 0 ? MPI_SUM : op == 1 ? MPI_MIN : MPI_MAX;
+    return MPI_Allreduce(MPI_IN_PLACE, v, n, MPI_DOUBLE, o, comm) == MPI_SUCCESS ? 0 : 1;
 }
 
 }  // namespace detail
@@ -283,7 +330,8 @@ struct No_Geometry {  // dccrg_no_geometry.hpp (nothing on the hot path)
     std::vector<char> file_data() const
     {
         std::vector<char> b(4);
-        std::memcpy(b.data(), &geometry_id, 4);
+        const int id = geometry_id;
+        std::memcpy(b.data(), &id, 4);
         return b;
     }
 };
@@ -360,7 +408,8 @@ struct Cartesian_Geometry {
     std::vector<char> file_data() const
     {
         std::vector<char> b(4 + 48);
-        std::memcpy(b.data(), &geometry_id, 4);
+        const int id = geometry_id;
+        std::memcpy(b.data(), &id, 4);
         std::memcpy(b.data() + 4, par_.start.data(), 24);
         std::memcpy(b.data() + 28, par_.level_0_cell_length.data(), 24);
         return b;
@@ -612,13 +661,24 @@ private:
         MPI_Comm_size(comm_, &size_);
         MPI_Comm node;
         MPI_Comm_split_type(comm_, MPI_COMM_TYPE_SHARED, rank_, MPI_INFO_NULL, &node);
-        int node_rank = 0, ndev = 0;
+        int node_rank = 0, node_size = 1, ndev = 0;
         MPI_Comm_rank(node, &node_rank);
+        MPI_Comm_size(node, &node_size);
         MPI_Comm_free(&node);
         detail::check(dccrgx_device_count(&ndev), "device count");
         if (ndev < 1) throw std::runtime_error("no GPU");
         detail::check(dccrgx_ctx_create(node_rank % ndev, rank_, size_, &ctx_), "context");
-        if (size_ > 1) {
+        int shared = node_size > ndev ? 1 : 0, any_shared = 0;  // one transport for every rank
+        MPI_Allreduce(&shared, &any_shared, 1, MPI_INT, MPI_MAX, comm_);
+        if (size_ > 1 && any_shared) {
+            // more ranks than GPUs on this node: ranks share a device, which
+            // RCCL refuses, so halos go through the host over MPI
+            dccrgx_host_transport t;
+            t.user = &comm_;
+            t.exchange = &detail::mpi_exchange;
+            t.allreduce_f64 = &detail::mpi_allreduce_f64;
+            detail::check(dccrgx_ctx_set_host_transport(ctx_, &t), "host transport");
+        } else if (size_ > 1) {
             uint8_t uid[128] = {0};
             if (rank_ == 0) detail::check(dccrgx_get_unique_id(uid), "unique id");
             MPI_Bcast(uid, 128, MPI_BYTE, 0, comm_);
@@ -688,7 +748,14 @@ public:
         const uint64_t* ptrs[4] = {sets[0].data(), sets[1].data(), sets[2].data(), sets[3].data()};
         const size_t counts[4] = {sets[0].size(), sets[1].size(), sets[2].size(), sets[3].size()};
         size_t n_new = 0;
-        detail::check(dccrgx_stop_refining(grid_, ptrs, counts, &n_new), "stop_refining");
+        // every rank must reach the same leaf set: a rank whose rebuild failed
+        // (it keeps its old grid) takes all ranks down, as the reference aborts
+        const int st = dccrgx_stop_refining(grid_, ptrs, counts, &n_new);
+        int ok = st == DCCRGX_OK ? 1 : 0, all_ok = 0;
+        MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_MIN, comm_);
+        if (!all_ok)
+            throw std::runtime_error(std::string("stop_refining failed on ") + (ok ? "another rank" : "this rank: ") +
+                                     (ok ? "" : dccrgx_last_error()));
         std::vector<uint64_t> created = id_list(dccrgx_get_new_cells);
         // data moves as execute_refines moves it (dccrg.hpp:10266-10267,
         // 10354-10375, 10526-10590): previous refined/unrefined data dropped,
@@ -891,67 +958,120 @@ public:
         wait_remote_neighbor_copy_updates(hood);
         return hood != default_neighborhood_id;
     }
-    bool start_remote_neighbor_copy_updates(int hood = default_neighborhood_id)  // :5046-5078
+    // :5046-5078: receives, then sends.  The library moves one update of a
+    // neighborhood as one group of RCCL sends and receives (one message per
+    // peer, dccrg.hpp:10726-11209), so it is launched once both halves are
+    // started (or at the first wait); it then runs on the communication stream
+    // while the caller computes, and each wait completes its own half: ghosts
+    // are unpacked by wait_..._receives, buffers released by wait_..._sends.
+    bool start_remote_neighbor_copy_updates(int hood = default_neighborhood_id)
+    {
+        if (!start_remote_neighbor_copy_receives(hood)) return false;
+        return start_remote_neighbor_copy_sends(hood);
+    }
+    bool start_remote_neighbor_copy_receives(int hood = default_neighborhood_id)  // :5091-5188
     {
         auto h = hoods_.find(hood);
         if (h == hoods_.end()) return false;
         HoodState& S = h->second;
-        S.sbuf.clear();
+        if (S.recv_posted) throw std::runtime_error("receives of this neighborhood already started");
         S.rbuf.clear();
-        std::vector<const void*> sp;
-        std::vector<void*> rp;
-        std::vector<uint64_t> sb, rb;
+        for (auto& kv : S.recv) {
+            size_t total = 0;
+            for (uint64_t c : kv.second) total += pack_size(c, *(*this)[c], kv.first, rank_, true, hood);
+            S.rbuf.emplace_back(total);
+        }
+        S.recv_posted = true;
+        if (S.send_posted) launch(hood, S);
+        return true;
+    }
+    bool start_remote_neighbor_copy_sends(int hood = default_neighborhood_id)  // :5198-5298
+    {
+        auto h = hoods_.find(hood);
+        if (h == hoods_.end()) return false;
+        HoodState& S = h->second;
+        if (S.send_posted) throw std::runtime_error("sends of this neighborhood already started");
+        S.sbuf.clear();
         for (auto& kv : S.send) {
             std::vector<char> buf;
             for (uint64_t c : kv.second) pack(c, *(*this)[c], rank_, kv.first, false, hood, buf);
             S.sbuf.push_back(std::move(buf));
         }
-        for (auto& kv : S.recv) {
-            int total = 0;
-            for (uint64_t c : kv.second) total += pack_size(c, *(*this)[c], kv.first, rank_, true, hood);
-            S.rbuf.emplace_back((size_t)total);
-        }
-        for (auto& b : S.sbuf) {
-            sp.push_back(b.data());
-            sb.push_back(b.size());
-        }
-        for (auto& b : S.rbuf) {
-            rp.push_back(b.data());
-            rb.push_back(b.size());
-        }
-        detail::check(dccrgx_exchange_start(grid_, hood, sp.data(), sb.data(), rp.data(), rb.data()),
-                      "start_remote_neighbor_copy_updates");
-        S.pending = true;
+        S.send_posted = true;
+        if (S.recv_posted) launch(hood, S);
         return true;
     }
-    bool start_remote_neighbor_copy_receives(int hood = default_neighborhood_id)
-    {
-        return start_remote_neighbor_copy_updates(hood);
-    }
-    bool start_remote_neighbor_copy_sends(int hood = default_neighborhood_id) { return hoods_.count(hood) > 0; }
     bool wait_remote_neighbor_copy_updates(int hood = default_neighborhood_id)  // :5307-5338
+    {
+        if (!hoods_.count(hood)) return false;
+        wait_remote_neighbor_copy_update_receives(hood);
+        return wait_sends_of(hood, hoods_.at(hood));
+    }
+    bool wait_remote_neighbor_copy_update_receives(int hood = default_neighborhood_id)  // :5377-5413
     {
         auto h = hoods_.find(hood);
         if (h == hoods_.end()) return false;
         HoodState& S = h->second;
-        if (!S.pending) return true;
-        detail::check(dccrgx_exchange_wait(grid_, hood), "wait_remote_neighbor_copy_updates");
+        if (!S.recv_posted) return true;
+        complete(hood, S);
         size_t i = 0;
         for (auto& kv : S.recv) {
             int pos = 0;
             for (uint64_t c : kv.second) unpack(c, *(*this)[c], kv.first, rank_, hood, S.rbuf[i], pos);
             i++;
         }
-        S.pending = false;
+        S.rbuf.clear();
+        S.recv_posted = false;
+        end_half(S);
         return true;
     }
-    bool wait_remote_neighbor_copy_update_receives(int hood = default_neighborhood_id)
+    // :5347-5368: the sends of every started update
+    bool wait_remote_neighbor_copy_update_sends()
     {
-        return wait_remote_neighbor_copy_updates(hood);
+        bool ok = true;
+        for (auto& kv : hoods_) ok = wait_sends_of(kv.first, kv.second) && ok;
+        return ok;
     }
-    bool wait_remote_neighbor_copy_update_sends(int hood = default_neighborhood_id)
+    // :6764-6790: one message per cell instead of one per process.  The bytes
+    // each process receives are the same either way and RCCL has no tags, so
+    // the mode is recorded (and reported) but moves the same grouped messages.
+    Dccrg& set_send_single_cells(const bool given)
     {
-        return wait_remote_neighbor_copy_updates(hood);
+        send_single_cells_ = given;
+        return *this;
+    }
+    bool get_send_single_cells() const { return send_single_cells_; }
+
+    // dccrg.hpp:3100-3161: the entries of the cell's neighbors_of whose
+    // min-corner indices equal the window at (x, y, z) cell lengths
+    // (indices_from_neighborhood, :4236-4352); nothing for a cell that is not
+    // local, for (0, 0, 0) or for a window outside a non-periodic grid
+    neighbor_list_t get_neighbors_of_at_offset(const uint64_t cell, const int x, const int y, const int z) const
+    {
+        neighbor_list_t out;
+        if (!is_local(cell) || (x == 0 && y == 0 && z == 0)) return out;
+        const neighbor_list_t* nof = get_neighbors_of(cell);
+        if (!nof) return out;
+        const auto idx = mapping.get_indices(cell);
+        const uint64_t len = mapping.get_cell_length_in_indices(cell);
+        const int off[3] = {x, y, z};
+        Types<3>::indices_t ref = idx;
+        for (int d = 0; d < 3; d++) {
+            const uint64_t glen = mapping.length.get()[d] << mapping.get_maximum_refinement_level();
+            if (topology.is_periodic(d)) {  // step by step: the window may wrap several times
+                for (int i = 0; i > off[d]; i--) ref[d] = ref[d] >= len ? ref[d] - len : glen - len;
+                for (int i = 0; i < off[d]; i++) ref[d] = ref[d] < glen - len ? ref[d] + len : 0;
+            } else if (off[d] < 0) {
+                if (idx[d] < uint64_t(-off[d]) * len) return out;
+                ref[d] -= uint64_t(-off[d]) * len;
+            } else {
+                if (idx[d] + uint64_t(off[d]) * len >= glen) return out;
+                ref[d] += uint64_t(off[d]) * len;
+            }
+        }
+        for (const auto& n : *nof)
+            if (mapping.get_indices(n.first) == ref) out.push_back(n);
+        return out;
     }
 
     // device fast path
@@ -968,8 +1088,56 @@ private:
         std::unordered_map<int, std::vector<std::pair<uint64_t, int>>> send_tagged, recv_tagged;
         std::vector<uint64_t> remote_ids;
         std::vector<std::vector<char>> sbuf, rbuf;
-        bool pending = false;
+        bool recv_posted = false, send_posted = false;  // started, not yet waited
+        bool launched = false, completed = false;        // the grouped transfer
     };
+
+    // the grouped transfer of one update: both halves' buffers (a half the
+    // caller has not started yet is started here), then dccrgx_exchange_start
+    void launch(int hood, HoodState& S)
+    {
+        if (S.launched) return;
+        if (!S.recv_posted) start_remote_neighbor_copy_receives(hood);
+        if (!S.send_posted) start_remote_neighbor_copy_sends(hood);
+        if (S.launched) return;  // the line above launched it
+        std::vector<const void*> sp;
+        std::vector<void*> rp;
+        std::vector<uint64_t> sb, rb;
+        for (auto& b : S.sbuf) {
+            sp.push_back(b.data());
+            sb.push_back(b.size());
+        }
+        for (auto& b : S.rbuf) {
+            rp.push_back(b.data());
+            rb.push_back(b.size());
+        }
+        detail::check(dccrgx_exchange_start(grid_, hood, sp.data(), sb.data(), rp.data(), rb.data()),
+                      "remote neighbor copy update");
+        S.launched = true;
+        S.completed = false;
+    }
+    void complete(int hood, HoodState& S)
+    {
+        if (!S.launched) launch(hood, S);
+        if (!S.completed) {
+            detail::check(dccrgx_exchange_wait(grid_, hood), "remote neighbor copy update");
+            S.completed = true;
+        }
+    }
+    // after a half is waited: the update is over once both are
+    static void end_half(HoodState& S)
+    {
+        if (!S.recv_posted && !S.send_posted) S.launched = S.completed = false;
+    }
+    bool wait_sends_of(int hood, HoodState& S)
+    {
+        if (!S.send_posted) return true;
+        complete(hood, S);
+        S.sbuf.clear();
+        S.send_posted = false;
+        end_half(S);
+        return true;
+    }
 
     const HoodState& hs(int hood) const
     {
@@ -1068,7 +1236,10 @@ private:
             Cells_Item ci{};
             ci.id = order[i];
             ci.data = (*this)[order[i]];
-            (ci.ACI::update(*this, ci, ACI()), ...);  // :11548
+            {  // ACI::update() of every additional cell item, :11548
+                int each[] = {0, (ci.ACI::update(*this, ci, ACI()), 0)...};
+                (void)each;
+            }
             ranges[i][0] = S.neighbors.size();
             for (const auto* group : {&only_of, &both, &only_to})
                 for (const item& x : *group) {
@@ -1078,7 +1249,10 @@ private:
                     ni.x = x.second[0];
                     ni.y = x.second[1];
                     ni.z = x.second[2];
-                    (ni.ANI::update(*this, ci, ni, hood, ANI()), ...);  // :11650-11715
+                    {  // ANI::update() of every additional neighbor item, :11650-11715
+                        int each[] = {0, (ni.ANI::update(*this, ci, ni, hood, ANI()), 0)...};
+                        (void)each;
+                    }
                     S.neighbors.push_back(std::move(ni));
                 }
             ranges[i][1] = ranges[i][0] + only_of.size();
@@ -1112,39 +1286,66 @@ private:
         hoods_[hood] = std::move(S);
     }
 
+    // A cell's bytes are MPI_Pack of its get_mpi_datatype(), as the
+    // reference's struct datatypes put them on the wire.  Named (builtin)
+    // datatypes -- every caller's cells but variable_neighbour_data's derived
+    // structs -- are contiguous: their packed form is the bytes themselves,
+    // so they are copied directly with the type's size looked up once.
+    // Derived datatypes go through MPI_Type_commit / MPI_Pack / MPI_Type_free
+    // (the reference frees them after use as well, dccrg.hpp:10915-10925).
+    int named_size(MPI_Datatype t)
+    {
+        auto it = type_size_.find(t);
+        if (it != type_size_.end()) return it->second;
+        int sz = 0;
+        MPI_Type_size(t, &sz);
+        type_size_[t] = sz;
+        return sz;
+    }
     int pack_size(uint64_t id, Cell_Data& c, int sender, int receiver, bool receiving, int hood)
     {
         auto d = detail::cell_datatype(c, id, sender, receiver, receiving, hood);
         MPI_Datatype t = std::get<2>(d);
-        const bool named = detail::is_named(t);
-        if (!named) MPI_Type_commit(&t);
+        if (detail::is_named(t)) return std::get<1>(d) * named_size(t);
+        MPI_Type_commit(&t);
         int sz = 0;
         MPI_Pack_size(std::get<1>(d), t, comm_, &sz);
-        if (!named) MPI_Type_free(&t);
+        MPI_Type_free(&t);
         return sz;
     }
     void pack(uint64_t id, Cell_Data& c, int sender, int receiver, bool receiving, int hood, std::vector<char>& buf)
     {
         auto d = detail::cell_datatype(c, id, sender, receiver, receiving, hood);
         MPI_Datatype t = std::get<2>(d);
-        const bool named = detail::is_named(t);
-        if (!named) MPI_Type_commit(&t);
+        if (detail::is_named(t)) {
+            const size_t n = (size_t)std::get<1>(d) * named_size(t);
+            const size_t at = buf.size();
+            buf.resize(at + n);
+            if (n) std::memcpy(buf.data() + at, std::get<0>(d), n);
+            return;
+        }
+        MPI_Type_commit(&t);
         int sz = 0;
         MPI_Pack_size(std::get<1>(d), t, comm_, &sz);
         int pos = (int)buf.size();
         buf.resize(buf.size() + sz);
         MPI_Pack(std::get<0>(d), std::get<1>(d), t, buf.data(), (int)buf.size(), &pos, comm_);
         buf.resize(pos);
-        if (!named) MPI_Type_free(&t);
+        MPI_Type_free(&t);
     }
     void unpack(uint64_t id, Cell_Data& c, int sender, int receiver, int hood, std::vector<char>& buf, int& pos)
     {
         auto d = detail::cell_datatype(c, id, sender, receiver, true, hood);
         MPI_Datatype t = std::get<2>(d);
-        const bool named = detail::is_named(t);
-        if (!named) MPI_Type_commit(&t);
+        if (detail::is_named(t)) {
+            const size_t n = (size_t)std::get<1>(d) * named_size(t);
+            if (n) std::memcpy(std::get<0>(d), buf.data() + pos, n);
+            pos += (int)n;
+            return;
+        }
+        MPI_Type_commit(&t);
         MPI_Unpack(buf.data(), (int)buf.size(), &pos, std::get<0>(d), std::get<1>(d), t, comm_);
-        if (!named) MPI_Type_free(&t);
+        MPI_Type_free(&t);
     }
 
     std::unordered_map<uint64_t, Cell_Data> cell_data_, remote_data_, refined_data_, unrefined_data_;
@@ -1156,6 +1357,8 @@ private:
     uint8_t partition_ = DCCRGX_PARTITION_BLOCK;
     unsigned hood_length_ = 1;
     bool initialized_ = false;
+    bool send_single_cells_ = false;
+    std::map<MPI_Datatype, int> type_size_;
 };
 
 }  // namespace dccrg

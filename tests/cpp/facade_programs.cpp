@@ -13,6 +13,15 @@
 //   amr CELL...      refines CELLs (6x5x4, max level 1, hood 1, periodic y z),
 //                    checks the data movement, prints new cells and the
 //                    rebuilt iteration-cache lists; then unrefines them back
+//   overlap LX LY LZ STEPS PX PY PZ
+//                    examples/game_of_life.cpp:117-139's turn: one message per
+//                    cell (set_send_single_cells), receives and sends started
+//                    separately, inner counts, wait receives, outer counts,
+//                    inner rules, wait sends, outer rules; checks
+//                    get_neighbors_of_at_offset against neighbors_of; prints
+//                    "alive <id> <count>" lines (any number of MPI ranks)
+//   cells ...        get_cells criteria and process-boundary accessors
+// Built with the reference's own flags (-std=c++11, Makefile:8) by the tests.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -315,6 +324,70 @@ static int cells(int argc, char** argv)
     return 0;
 }
 
+static void live_neighbor_counts(const dccrg::Dccrg<game_of_life_cell>::Iterator_Storage<
+                                     dccrg::Dccrg<game_of_life_cell>::Cells_Item>& cells)
+{
+    for (const auto& cell : cells) {
+        cell.data->live_neighbor_count = 0;
+        for (const auto& neighbor : cell.neighbors_of)
+            if (neighbor.data->is_alive) cell.data->live_neighbor_count++;
+    }
+}
+
+static void apply_rules(const dccrg::Dccrg<game_of_life_cell>::Iterator_Storage<
+                        dccrg::Dccrg<game_of_life_cell>::Cells_Item>& cells)
+{
+    for (const auto& cell : cells) {
+        if (cell.data->live_neighbor_count == 3) cell.data->is_alive = 1;
+        else if (cell.data->live_neighbor_count != 2) cell.data->is_alive = 0;
+    }
+}
+
+static int overlap(int argc, char** argv)
+{
+    if (argc < 9) abort();
+    dccrg::Dccrg<game_of_life_cell> grid;
+    grid.set_initial_length({{strtoull(argv[2], 0, 10), strtoull(argv[3], 0, 10), strtoull(argv[4], 0, 10)}})
+        .set_neighborhood_length(1)
+        .set_maximum_refinement_level(0)
+        .set_periodic(atoi(argv[6]) != 0, atoi(argv[7]) != 0, atoi(argv[8]) != 0)
+        .initialize(MPI_COMM_WORLD)
+        .balance_load();
+    grid.set_send_single_cells(true);
+    if (!grid.get_send_single_cells()) abort();
+    const int turns = atoi(argv[5]);
+    const auto &local_cells = grid.local_cells(), &inner_cells = grid.inner_cells(),
+               &outer_cells = grid.outer_cells();
+    for (const auto& cell : local_cells) {
+        cell.data->live_neighbor_count = 0;
+        cell.data->is_alive = splitmix64(cell.id) % 1000 < 200;
+    }
+    // get_neighbors_of_at_offset (dccrg.hpp:3100-3161): on a level-0 grid the
+    // neighbor at each default item's offset is found there
+    for (const auto& cell : local_cells) {
+        const auto* nof = grid.get_neighbors_of(cell.id);
+        for (const auto& n : *nof) {
+            const auto at = grid.get_neighbors_of_at_offset(cell.id, n.second[0], n.second[1], n.second[2]);
+            if (std::find(at.begin(), at.end(), n) == at.end()) abort();
+        }
+        if (!grid.get_neighbors_of_at_offset(cell.id, 0, 0, 0).empty()) abort();
+    }
+    for (int turn = 0; turn < turns; turn++) {
+        grid.start_remote_neighbor_copy_receives();
+        grid.start_remote_neighbor_copy_sends();
+        live_neighbor_counts(inner_cells);
+        grid.wait_remote_neighbor_copy_update_receives();
+        live_neighbor_counts(outer_cells);
+        apply_rules(inner_cells);
+        grid.wait_remote_neighbor_copy_update_sends();
+        apply_rules(outer_cells);
+    }
+    for (const auto& cell : local_cells)
+        if (cell.data->is_alive)
+            printf("alive %llu %u\n", (unsigned long long)cell.id, cell.data->live_neighbor_count);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     if (MPI_Init(&argc, &argv) != MPI_SUCCESS) abort();
@@ -329,6 +402,7 @@ int main(int argc, char** argv)
         else if (mode == "amr") rc = amr(argc, argv);
         else if (mode == "restart") rc = restart(argc, argv);
         else if (mode == "cells") rc = cells(argc, argv);
+        else if (mode == "overlap") rc = overlap(argc, argv);
     }
     MPI_Finalize();
     return rc;

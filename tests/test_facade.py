@@ -1,6 +1,8 @@
 """The C++ drop-in facade (include/dccrg_amd.hpp): user programs written the
 way the reference's examples use dccrg::Dccrg, compiled against the facade
-and run on the GPU; results compared with the oracle."""
+with the reference's own flags (-std=c++11, Makefile:8) and run on the GPU,
+also as several MPI ranks sharing the GPU (mpiexec -n 3, as the reference's
+.tstN targets run); results compared with the oracle."""
 import os
 import subprocess
 
@@ -16,7 +18,7 @@ MPI_INC, MPI_LIB = "/opt/conda/include", "/opt/conda/lib"
 
 def compile_facade(out=BIN):
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"), "-I", MPI_INC,
+    cmd = ["g++", "-std=c++11", "-pedantic", "-Werror", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"), "-I", MPI_INC,
            os.path.join(ROOT, "tests", "cpp", "facade_programs.cpp"), "-o", out,
            os.path.join(ROOT, "dccrg_amd", "libdccrgx.so"), os.path.join(MPI_LIB, "libmpi.so"),
            f"-Wl,-rpath,{os.path.join(ROOT, 'dccrg_amd')}:{MPI_LIB}"]
@@ -29,16 +31,22 @@ def test_facade_compiles(tmp_path):
     compile_facade(str(tmp_path / "facade_programs"))
 
 
-def run(*args):
+def run(*args, ranks=1):
     srcs = [os.path.join(ROOT, "tests", "cpp", "facade_programs.cpp"), os.path.join(ROOT, "include", "dccrg_amd.hpp"),
             os.path.join(ROOT, "include", "dccrgx.h")]
     if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(f) for f in srcs):
         compile_facade()
     env = dict(os.environ)
     env["LD_LIBRARY_PATH"] = "/usr/lib/x86_64-linux-gnu:" + MPI_LIB
-    r = subprocess.run([BIN, *[str(a) for a in args]], capture_output=True, text=True, timeout=600, env=env)
+    cmd = [BIN, *[str(a) for a in args]]
+    if ranks > 1:  # the reference's .tstN targets: mpiexec -n 3 on one host
+        cmd = [MPIEXEC, "-n", str(ranks)] + cmd
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     return r.stdout
+
+
+MPIEXEC = "/opt/conda/bin/mpiexec"
 
 
 @pytest.mark.gpu
@@ -47,8 +55,12 @@ def test_facade_blinker():
 
 
 @pytest.mark.gpu
-def test_facade_halo():
-    assert "PASS halo" in run("halo")
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_facade_halo(ranks):
+    """examples/basic_cell_data.cpp: every neighbor's copy equals its id, on
+    1 rank and on 3 ranks sharing the GPU (halo over MPI through the host)."""
+    out = run("halo", ranks=ranks)
+    assert out.count("PASS halo") == ranks
 
 
 @pytest.mark.gpu
@@ -61,6 +73,31 @@ def test_facade_mapping_matches_oracle():
         assert tuple(v[2:5]) == om.get_indices(cid)
         assert v[5] == om.get_parent(cid) and v[6] == om.get_level_0_parent(cid)
         assert v[7] == om.get_cell_length_in_indices(cid)
+
+
+def _alive_counts(out):
+    got = {}
+    for line in out.strip().splitlines():
+        if line.startswith("alive "):
+            _, cid, cnt = line.split()
+            got[int(cid)] = int(cnt)
+    return got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [1, 3])
+@pytest.mark.parametrize("dims,per", [((12, 10, 9), (0, 0, 1)), ((9, 7, 1), (1, 1, 0)), ((20, 6, 5), (1, 1, 1))])
+def test_facade_overlap_loop(dims, per, ranks):
+    """examples/game_of_life.cpp:117-139 with set_send_single_cells(true):
+    start receives, start sends, inner counts, wait receives, outer counts,
+    inner rules, wait sends, outer rules; get_neighbors_of_at_offset is
+    checked inside the program."""
+    steps = 6
+    got = _alive_counts(run("overlap", *dims, steps, *per, ranks=ranks))
+    n = int(np.prod(dims))
+    a0 = O.random_alive(np.arange(1, n + 1, dtype=np.uint64), 200)
+    ra, rc = O.gol_reference_run(dims, tuple(bool(p) for p in per), 1, a0, steps)
+    assert got == {int(i) + 1: int(rc[i]) for i in np.nonzero(ra)[0]}
 
 
 @pytest.mark.gpu

@@ -59,7 +59,10 @@ CASES = [((10, 8, 6), (False, False, False), 1, 0, 1, None),
          ((1, 1, 1), (True, True, True), 1, 0, 1, None),
          ((6, 5, 4), (True, True, False), 1, 1, 1, 40),
          ((6, 5, 4), (False, True, True), 1, 1, 3, 30),
-         ((8, 8, 1), (True, True, False), 0, 1, 2, 20)]
+         ((8, 8, 1), (True, True, False), 0, 1, 2, 20),
+         # neighborhood length 3: 342 items, beyond the LDS-record kernel (192)
+         ((9, 8, 7), (True, True, True), 3, 0, 1, None),
+         ((10, 9, 8), (False, True, True), 3, 0, 2, None)]
 
 
 @pytest.mark.parametrize("length,per,hood,M,P,n_ref", CASES)
