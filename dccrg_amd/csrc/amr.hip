@@ -441,6 +441,7 @@ int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
         *result = 1;
         return DCCRGX_OK;
     }
+    DX_TRY(explicit_host_lists(grid, DCCRGX_DEFAULT_NEIGHBORHOOD_ID));
     const View v{grid, grid->ex, grid->map.max_lvl};
     Amr& A = amr_of(grid);
     // dccrg.hpp:2476-2546
@@ -612,6 +613,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
         return DCCRGX_OK;
     }
     DX_TRY(ensure_explicit(grid));
+    DX_TRY(explicit_host_lists(grid, DCCRGX_DEFAULT_NEIGHBORHOOD_ID));
     const View v{grid, grid->ex, grid->map.max_lvl};
 
     // override_refines, dccrg.hpp:10130-10236: dont_refine spreads to every

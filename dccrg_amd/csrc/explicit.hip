@@ -25,11 +25,20 @@
 
 namespace dccrgx {
 
+// lookups of existing leaves: id -> global leaf index (position in the
+// ascending leaf list).  Grids whose id space is small enough keep a rank
+// bitmap: one bit per possible id (dccrg_mapping.hpp's ids are dense per
+// level) plus, per 64-bit word, the number of leaves before it -- a lookup is
+// one word load, a popcount and one rank load, and neighbors' ids are close
+// together (same level: the same z-plane +-1), so the words stay in L2.
+// Other grids use an open-addressing hash (2x capacity, linear probing).
 struct ExView {
     MapParams mp;
     const uint64_t* keys;
     const uint32_t* vals;
     uint64_t mask;
+    const uint64_t* bits;   // rank bitmap (null: use the hash)
+    const uint32_t* rank;
     int32_t per[3];
 };
 
@@ -46,6 +55,13 @@ __host__ __device__ inline uint64_t hmix(uint64_t x)
 __device__ inline int64_t ex_find(const ExView& v, uint64_t id)
 {
     if (id == 0) return -1;
+    if (v.bits) {
+        if (id > v.mp.last_cell) return -1;
+        const uint64_t w = v.bits[id >> 6];
+        const uint32_t b = (uint32_t)(id & 63);
+        if (!((w >> b) & 1ull)) return -1;
+        return (int64_t)v.rank[id >> 6] + __popcll(w & ((1ull << b) - 1ull));
+    }
     uint64_t h = hmix(id) & v.mask;
     for (;;) {
         const uint64_t k = v.keys[h];
@@ -70,6 +86,33 @@ __global__ void __launch_bounds__(256) k_hash_insert(const uint64_t* __restrict_
             }
             h = (h + 1) & mask;
         }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_bits_set(const uint64_t* __restrict__ leaves, size_t n,
+                                                  unsigned long long* bits)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t id = leaves[i];
+        atomicOr(&bits[id >> 6], 1ull << (id & 63));
+    }
+}
+
+// rank[w] = number of leaves with id < 64 w (binary search in the ascending list)
+__global__ void __launch_bounds__(256) k_bits_rank(const uint64_t* __restrict__ leaves, uint64_t n, uint64_t nw,
+                                                   uint32_t* __restrict__ rank)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+        const uint64_t key = (uint64_t)w << 6;
+        uint64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (leaves[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        rank[w] = (uint32_t)lo;
     }
 }
 
@@ -160,6 +203,156 @@ __global__ void __launch_bounds__(256) k_ex_nof(ExView v, const int32_t* __restr
     }
 }
 
+// Fill pass of k_ex_nof with coalesced stores: one wave per 64 cells whose
+// rows (already counted and scanned) form one output run.  Each lane lists
+// its cell's entries as 8-byte records (leaf index; lane, case, item) in LDS
+// at the entry's place in the run; the wave then writes the run entry by
+// entry, consecutive lanes on consecutive entries, recomputing the id and
+// offset from the record and the cell's indices (no hash probe at store
+// time).  case 0: the window's cell, 1: its parent, 2 + d: child d (x fastest).
+// Entries beyond the LDS capacity are written by their lane directly.
+constexpr int NOF_REC_CAP = 1024;  // records per wave (8 KiB; four independent waves per workgroup)
+
+__device__ __forceinline__ bool nof_window(const MapParams& p, const int32_t* per, const uint64_t idx[3],
+                                           const int32_t* h, int64_t L, uint64_t wi[3])
+{
+    const int M = p.max_lvl;
+    for (int d = 0; d < 3; d++) {
+        const int64_t G = (int64_t)(p.length[d] << M);
+        int64_t x = (int64_t)idx[d] + (int64_t)h[d] * L;
+        if (x < 0 || x >= G) {
+            if (!per[d]) return false;
+            x %= G;
+            if (x < 0) x += G;
+        }
+        wi[d] = (uint64_t)x;
+    }
+    return true;
+}
+
+__device__ __forceinline__ void nof_entry(const MapParams& p, const uint64_t wi[3], int l, const int32_t* h, int64_t L,
+                                          int cs, uint64_t& id, int32_t o[3])
+{
+    if (cs == 0) {
+        id = map_cell(p, wi, l);
+        for (int d = 0; d < 3; d++) o[d] = (int32_t)(h[d] * L);
+    } else if (cs == 1) {
+        id = map_cell(p, wi, l - 1);
+        for (int d = 0; d < 3; d++) o[d] = (int32_t)(h[d] * L - (int64_t)(wi[d] % (uint64_t)(2 * L)));
+    } else {
+        const int c = cs - 2;
+        const int64_t hl = L / 2;
+        const int64_t dd[3] = {c & 1, (c >> 1) & 1, (c >> 2) & 1};
+        uint64_t ci[3];
+        for (int d = 0; d < 3; d++) {
+            ci[d] = wi[d] + (uint64_t)(dd[d] * hl);
+            o[d] = (int32_t)(h[d] * L + dd[d] * hl);
+        }
+        id = map_cell(p, ci, l + 1);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ex_nof_fill(ExView v, const int32_t* __restrict__ items, int K,
+                                                     const uint64_t* __restrict__ cells, size_t n,
+                                                     const uint64_t* __restrict__ row, uint64_t* __restrict__ ids,
+                                                     int32_t* __restrict__ off, uint32_t* __restrict__ gidx)
+{
+    __shared__ uint2 rec_all[4][NOF_REC_CAP];
+    __shared__ uint64_t s_idx_all[4][3][64];
+    __shared__ int32_t s_lvl_all[4][64];
+    const int wv = threadIdx.x >> 6;
+    uint2* rec = rec_all[wv];
+    uint64_t(*s_idx)[64] = s_idx_all[wv];
+    int32_t* s_lvl = s_lvl_all[wv];
+    const MapParams& p = v.mp;
+    const int M = p.max_lvl;
+    const int lane = threadIdx.x & 63;
+    const uint64_t r0 = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    const bool live = r0 < n;  // a wave past the end still meets the block barrier
+    const uint64_t last = r0 + 64 < n ? r0 + 64 : n;
+    const uint64_t base = live ? row[r0] : 0, end = live ? row[last] : 0;
+    const uint64_t i = r0 + lane;
+    if (i < n) {
+        uint64_t idx[3];
+        int l;
+        const uint64_t c = cells[i];
+        if (map_indices(p, c, idx, &l) && ex_find(v, c) >= 0) {
+            for (int d = 0; d < 3; d++) s_idx[d][lane] = idx[d];
+            s_lvl[lane] = l;
+            const int64_t L = (int64_t)1 << (M - l);
+            uint64_t w = row[i] - base;
+            auto put = [&](uint32_t g, int cs, int k, const uint64_t* wi) {
+                if (w < NOF_REC_CAP) {
+                    rec[w] = make_uint2(g, ((uint32_t)lane << 24) | ((uint32_t)cs << 16) | (uint32_t)k);
+                } else {  // beyond the staging capacity: this lane stores the entry
+                    uint64_t id;
+                    int32_t o[3];
+                    nof_entry(p, wi, l, items + 3 * k, L, cs, id, o);
+                    const uint64_t e = base + w;
+                    ids[e] = id;
+                    if (gidx) gidx[e] = g;
+                    if (off) {
+                        off[3 * e + 0] = o[0];
+                        off[3 * e + 1] = o[1];
+                        off[3 * e + 2] = o[2];
+                    }
+                }
+                w++;
+            };
+            for (int k = 0; k < K; k++) {
+                const int32_t* h = items + 3 * k;
+                uint64_t wi[3];
+                if (!nof_window(p, v.per, idx, h, L, wi)) continue;  // outside: dropped (dccrg.hpp:4670-4672)
+                int64_t g = ex_find(v, map_cell(p, wi, l));
+                if (g >= 0) {
+                    put((uint32_t)g, 0, k, wi);
+                    continue;
+                }
+                if (l > 0) {
+                    g = ex_find(v, map_cell(p, wi, l - 1));
+                    if (g >= 0) {
+                        put((uint32_t)g, 1, k, wi);
+                        continue;
+                    }
+                }
+                if (l < M) {  // the count pass has checked that all 8 children exist
+                    const uint64_t hl = (uint64_t)(L / 2);
+                    for (int cix = 0; cix < 8; cix++) {
+                        const uint64_t ci[3] = {wi[0] + (cix & 1) * hl, wi[1] + ((cix >> 1) & 1) * hl,
+                                                wi[2] + ((cix >> 2) & 1) * hl};
+                        put((uint32_t)ex_find(v, map_cell(p, ci, l + 1)), 2 + cix, k, wi);
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t tot = end - base < (uint64_t)NOF_REC_CAP ? end - base : (uint64_t)NOF_REC_CAP;
+    for (uint64_t e = lane; e < tot; e += 64) {
+        const uint2 r = rec[e];
+        const int ln = (int)(r.y >> 24), cs = (int)((r.y >> 16) & 0xffu), k = (int)(r.y & 0xffffu);
+        const uint64_t idx[3] = {s_idx[0][ln], s_idx[1][ln], s_idx[2][ln]};
+        const int l = s_lvl[ln];
+        const int64_t L = (int64_t)1 << (M - l);
+        uint64_t wi[3];
+        nof_window(p, v.per, idx, items + 3 * k, L, wi);
+        uint64_t id;
+        int32_t o[3];
+        nof_entry(p, wi, l, items + 3 * k, L, cs, id, o);
+        ids[base + e] = id;
+        if (gidx) gidx[base + e] = r.x;
+        if (off) {
+            off[3 * (base + e) + 0] = o[0];
+            off[3 * (base + e) + 1] = o[1];
+            off[3 * (base + e) + 2] = o[2];
+        }
+    }
+}
+
+// row classes of the sort-unique passes (in the count array until sorted)
+constexpr uint32_t ROW_MEDIUM = 0xfffffffeu;  // row for the LDS kernel (65..WAVE_SORT_MAX entries)
+constexpr uint32_t ROW_LONG = 0xffffffffu;    // row for the per-thread kernel (> WAVE_SORT_MAX)
+
 // transpose helpers: rows = global leaves
 __global__ void __launch_bounds__(256) k_tr_count(const uint64_t* __restrict__ row, const uint32_t* __restrict__ tgt,
                                                   uint64_t n, uint32_t* __restrict__ cnt)
@@ -182,11 +375,13 @@ __global__ void __launch_bounds__(256) k_tr_scatter(const uint64_t* __restrict__
 }
 
 // per row: insertion sort + unique in place; unique count -> ucnt
+// (rows longer than the wave kernel takes: those flagged ~0 in ucnt)
 __global__ void __launch_bounds__(256) k_sort_unique_rows(const uint64_t* __restrict__ row, uint64_t n,
                                                           uint32_t* __restrict__ v, uint32_t* __restrict__ ucnt)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
+        if (ucnt[r] != ROW_LONG) continue;
         uint32_t* a = v + row[r];
         const uint64_t m = row[r + 1] - row[r];
         for (uint64_t i = 1; i < m; i++) {
@@ -230,6 +425,7 @@ __device__ inline bool pair_eq(const Pair& a, const Pair& b)
 {
     return a.g == b.g && a.x == b.x && a.y == b.y && a.z == b.z;
 }
+__device__ __forceinline__ bool pair_less_(const Pair& a, const Pair& b) { return pair_less(a, b); }
 
 __global__ void __launch_bounds__(256) k_stencil_rows(const uint64_t* __restrict__ nof_row,
                                                       const uint32_t* __restrict__ nof_g,
@@ -240,6 +436,7 @@ __global__ void __launch_bounds__(256) k_stencil_rows(const uint64_t* __restrict
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
+        if (ucnt[i] != ROW_LONG) continue;  // done by k_stencil_rows64 / k_stencil_rows_wave
         const uint32_t r = local_g[i];
         Pair* a = tmp + tmp_row[i];
         const uint64_t m = nof_row[r + 1] - nof_row[r];
@@ -277,6 +474,15 @@ __global__ void __launch_bounds__(256) k_stencil_slots(const uint64_t* __restric
         }
 }
 
+// the same per wavefront in LDS (rows up to WAVE_SORT_MAX; longer ones flagged
+// ~0 in ucnt for k_stencil_rows); defined after the wave helpers
+__global__ void __launch_bounds__(64) k_stencil_rows_wave(const uint64_t* __restrict__ nof_row,
+                                                          const uint32_t* __restrict__ nof_g,
+                                                          const int32_t* __restrict__ nof_off,
+                                                          const uint32_t* __restrict__ local_g, uint64_t nl,
+                                                          const uint64_t* __restrict__ tmp_row, Pair* __restrict__ tmp,
+                                                          uint32_t* __restrict__ ucnt);
+
 __global__ void __launch_bounds__(256) k_ex_gol(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ cnt, const uint64_t* __restrict__ st_row,
                                                 const uint32_t* __restrict__ st_slot,
@@ -306,6 +512,311 @@ __global__ void __launch_bounds__(256) k_ex_slots(ExView v, const uint32_t* __re
     }
 }
 
+// ---------------------------------------------------------------------------
+// wave-cooperative CSR kernels.  A row of a neighbor list is short (tens of
+// entries), so one thread per row writes scattered 4-24 B pieces; instead a
+// wavefront takes 64 consecutive rows, whose output is one contiguous run,
+// and its lanes write consecutive entries of that run (each lane finds the
+// row of its entry by a binary search over the 65 row starts kept in LDS).
+// ---------------------------------------------------------------------------
+// index j in [0, 64) with s[j] <= e < s[j + 1] (s ascending, s[64] > e)
+__device__ __forceinline__ int wave_row_of(const uint64_t* s, uint64_t e)
+{
+    int lo = 0, hi = 64;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (s[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// rows of the query cells copied from the stored CSR of every leaf:
+// out entry k of query i = CSR entry nof_row[gq[i]] + k (ids, offsets)
+__global__ void __launch_bounds__(64) k_rows_gather(const uint32_t* __restrict__ gq, uint64_t n,
+                                                    const uint64_t* __restrict__ src_row,
+                                                    const uint64_t* __restrict__ row,
+                                                    const uint64_t* __restrict__ src_id,
+                                                    const int32_t* __restrict__ src_off, uint64_t* __restrict__ ids,
+                                                    int32_t* __restrict__ off3)
+{
+    __shared__ uint64_t s_dst[65], s_src[64];
+    const int lane = threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t last = r0 + 64 < n ? r0 + 64 : n;  // rows [r0, last); rows past the end are empty
+    s_dst[lane] = row[r0 + lane < last ? r0 + lane : last];
+    if (lane == 0) s_dst[64] = row[last];
+    if (r0 + lane < n) s_src[lane] = src_row[gq[r0 + lane]];
+    __syncthreads();
+    const uint64_t end = s_dst[64];
+    for (uint64_t e = s_dst[0] + lane; e < end; e += 64) {
+        const int j = wave_row_of(s_dst, e);
+        const uint64_t src = s_src[j] + (e - s_dst[j]);
+        ids[e] = src_id[src];
+        if (off3) {
+            off3[3 * e + 0] = src_off[3 * src + 0];
+            off3[3 * e + 1] = src_off[3 * src + 1];
+            off3[3 * e + 2] = src_off[3 * src + 2];
+        }
+    }
+}
+
+// query cells -> their leaf index and row length in the stored CSR
+__global__ void __launch_bounds__(256) k_ex_query_rows(ExView v, const uint64_t* __restrict__ cells, size_t n,
+                                                       const uint64_t* __restrict__ nof_row, uint32_t* __restrict__ gq,
+                                                       uint64_t* __restrict__ row, int32_t* __restrict__ err)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t g = ex_find(v, cells[i]);
+        if (g < 0) {
+            atomicOr(err, 1);
+            row[i + 1] = 0;
+            gq[i] = 0;
+            continue;
+        }
+        gq[i] = (uint32_t)g;
+        row[i + 1] = nof_row[g + 1] - nof_row[g];
+    }
+}
+
+// sort + unique of one row per wavefront, in LDS (bitonic over the next power
+// of two >= the row length, at most WAVE_SORT_MAX); the unique prefix is
+// written back in place and its length to ucnt.  Longer rows are left to the
+// per-thread kernels (flagged in ucnt as ~0).
+constexpr int WAVE_SORT_MAX = 1024;
+
+
+// bitonic sort of one element per lane across the wavefront (ascending by
+// lane), exchanges by cross-lane shuffles: no LDS
+__device__ __forceinline__ uint32_t wave_sort64_u32(uint32_t x)
+{
+    const int lane = threadIdx.x & 63;
+    for (int k = 2; k <= 64; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t y = __shfl_xor(x, j, 64);
+            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+            x = keep_min ? (y < x ? y : x) : (y < x ? x : y);
+        }
+    return x;
+}
+
+__device__ __forceinline__ bool pair_less_(const Pair& a, const Pair& b);
+__device__ __forceinline__ Pair wave_sort64_pair(Pair x)
+{
+    const int lane = threadIdx.x & 63;
+    for (int k = 2; k <= 64; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            Pair y;
+            y.g = __shfl_xor(x.g, j, 64);
+            y.x = __shfl_xor(x.x, j, 64);
+            y.y = __shfl_xor(x.y, j, 64);
+            y.z = __shfl_xor(x.z, j, 64);
+            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+            const bool ylt = pair_less_(y, x);
+            if (keep_min == ylt) x = y;
+        }
+    return x;
+}
+
+template <class T, class Less>
+__device__ void wave_bitonic(T* a, int m2, Less less)
+{
+    for (int k = 2; k <= m2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < m2; i += 64) {
+                const int p = i ^ j;
+                if (p > i) {
+                    const bool up = (i & k) == 0;
+                    const T x = a[i], y = a[p];
+                    if (up ? less(y, x) : less(x, y)) {
+                        a[i] = y;
+                        a[p] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// unique of a sorted LDS array of m entries by one wave: out[0..u) = the
+// first of every run of equal entries; returns u
+template <class T, class Eq, class Out>
+__device__ uint32_t wave_unique(const T* a, int m, Eq eq, Out out)
+{
+    uint32_t base = 0;
+    for (int c = 0; c < m; c += 64) {
+        const int i = c + (int)threadIdx.x;
+        const bool keep = i < m && (i == 0 || !eq(a[i], a[i - 1]));
+        const uint64_t mask = __ballot(keep);
+        const uint32_t before = (uint32_t)__popcll(mask & ((1ull << threadIdx.x) - 1ull));
+        if (keep) out(base + before, a[i]);
+        base += (uint32_t)__popcll(mask);
+    }
+    return base;
+}
+
+// rows of at most 64 entries: one wave per row, one entry per lane, sorted
+// in registers; longer rows are flagged for the LDS / per-thread kernels
+__global__ void __launch_bounds__(256) k_sort_unique_rows64(const uint64_t* __restrict__ row, uint64_t n,
+                                                            uint32_t* __restrict__ v, uint32_t* __restrict__ ucnt)
+{
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t r = wave; r < n; r += waves) {
+        const uint64_t b = row[r];
+        const int m = (int)(row[r + 1] - b);
+        if (m > 64) {
+            if (lane == 0) ucnt[r] = m > WAVE_SORT_MAX ? ROW_LONG : ROW_MEDIUM;
+            continue;
+        }
+        uint32_t x = lane < m ? v[b + lane] : 0xffffffffu;
+        x = wave_sort64_u32(x);
+        const uint32_t prev = __shfl_up(x, 1, 64);
+        const bool keep = lane < m && (lane == 0 || x != prev);
+        const uint64_t mask = __ballot(keep);
+        if (keep) v[b + __popcll(mask & ((1ull << lane) - 1ull))] = x;
+        if (lane == 0) ucnt[r] = (uint32_t)__popcll(mask);
+    }
+}
+
+__global__ void __launch_bounds__(64) k_sort_unique_rows_wave(const uint64_t* __restrict__ row, uint64_t n,
+                                                              uint32_t* __restrict__ v, uint32_t* __restrict__ ucnt)
+{
+    __shared__ uint32_t a[WAVE_SORT_MAX];
+    for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
+        if (ucnt[r] != ROW_MEDIUM) continue;
+        const uint64_t b = row[r];
+        const int m = (int)(row[r + 1] - b);
+        int m2 = 1;
+        while (m2 < m) m2 <<= 1;
+        for (int i = threadIdx.x; i < m2; i += 64) a[i] = i < m ? v[b + i] : 0xffffffffu;
+        __syncthreads();
+        wave_bitonic(a, m2, [](uint32_t x, uint32_t y) { return x < y; });
+        const uint32_t u = wave_unique(a, m, [](uint32_t x, uint32_t y) { return x == y; },
+                                       [&](uint32_t k, uint32_t x) { v[b + k] = x; });
+        if (threadIdx.x == 0) ucnt[r] = u;
+        __syncthreads();
+    }
+}
+
+// rows copied to their final place (drow), one wave per 64 rows
+__global__ void __launch_bounds__(64) k_copy_rows_wave(const uint64_t* __restrict__ srow, const uint32_t* __restrict__ sv,
+                                                       const uint64_t* __restrict__ drow, uint64_t n,
+                                                       uint32_t* __restrict__ dv)
+{
+    __shared__ uint64_t s_dst[65], s_src[64];
+    const int lane = threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t last = r0 + 64 < n ? r0 + 64 : n;
+    s_dst[lane] = drow[r0 + lane < last ? r0 + lane : last];
+    if (lane == 0) s_dst[64] = drow[last];
+    if (r0 + lane < n) s_src[lane] = srow[r0 + lane];
+    __syncthreads();
+    const uint64_t end = s_dst[64];
+    for (uint64_t e = s_dst[0] + lane; e < end; e += 64) {
+        const int j = wave_row_of(s_dst, e);
+        dv[e] = sv[s_src[j] + (e - s_dst[j])];
+    }
+}
+
+__global__ void __launch_bounds__(64) k_stencil_rows_wave(const uint64_t* __restrict__ nof_row,
+                                                          const uint32_t* __restrict__ nof_g,
+                                                          const int32_t* __restrict__ nof_off,
+                                                          const uint32_t* __restrict__ local_g, uint64_t nl,
+                                                          const uint64_t* __restrict__ tmp_row, Pair* __restrict__ tmp,
+                                                          uint32_t* __restrict__ ucnt)
+{
+    __shared__ Pair a[WAVE_SORT_MAX];
+    for (uint64_t i = blockIdx.x; i < nl; i += gridDim.x) {
+        if (ucnt[i] != ROW_MEDIUM) continue;
+        const uint32_t r = local_g[i];
+        const uint64_t b = nof_row[r];
+        const int m = (int)(nof_row[r + 1] - b);
+        int m2 = 1;
+        while (m2 < m) m2 <<= 1;
+        for (int k = threadIdx.x; k < m2; k += 64) {
+            if (k < m) {
+                const uint64_t e = b + k;
+                a[k] = Pair{nof_g[e], nof_off[3 * e], nof_off[3 * e + 1], nof_off[3 * e + 2]};
+            } else {
+                a[k] = Pair{0xffffffffu, 0x7fffffff, 0x7fffffff, 0x7fffffff};  // sorts last
+            }
+        }
+        __syncthreads();
+        wave_bitonic(a, m2, [](const Pair& x, const Pair& y) { return pair_less(x, y); });
+        Pair* out = tmp + tmp_row[i];
+        const uint32_t u = wave_unique(a, m, [](const Pair& x, const Pair& y) { return pair_eq(x, y); },
+                                       [&](uint32_t k, const Pair& x) { out[k] = x; });
+        if (threadIdx.x == 0) ucnt[i] = u;
+        __syncthreads();
+    }
+}
+
+// rows of at most 64 entries in registers (see k_sort_unique_rows64)
+__global__ void __launch_bounds__(256) k_stencil_rows64(const uint64_t* __restrict__ nof_row,
+                                                        const uint32_t* __restrict__ nof_g,
+                                                        const int32_t* __restrict__ nof_off,
+                                                        const uint32_t* __restrict__ local_g, uint64_t nl,
+                                                        const uint64_t* __restrict__ tmp_row, Pair* __restrict__ tmp,
+                                                        uint32_t* __restrict__ ucnt)
+{
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t i = wave; i < nl; i += waves) {
+        const uint32_t r = local_g[i];
+        const uint64_t b = nof_row[r];
+        const int m = (int)(nof_row[r + 1] - b);
+        if (m > 64) {
+            if (lane == 0) ucnt[i] = m > WAVE_SORT_MAX ? ROW_LONG : ROW_MEDIUM;
+            continue;
+        }
+        Pair x{0xffffffffu, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+        if (lane < m) {
+            const uint64_t e = b + lane;
+            x = Pair{nof_g[e], nof_off[3 * e], nof_off[3 * e + 1], nof_off[3 * e + 2]};
+        }
+        x = wave_sort64_pair(x);
+        Pair prev;
+        prev.g = __shfl_up(x.g, 1, 64);
+        prev.x = __shfl_up(x.x, 1, 64);
+        prev.y = __shfl_up(x.y, 1, 64);
+        prev.z = __shfl_up(x.z, 1, 64);
+        const bool keep = lane < m && (lane == 0 || !pair_eq(x, prev));
+        const uint64_t mask = __ballot(keep);
+        if (keep) tmp[tmp_row[i] + __popcll(mask & ((1ull << lane) - 1ull))] = x;
+        if (lane == 0) ucnt[i] = (uint32_t)__popcll(mask);
+    }
+}
+
+// stencil rows' final form: storage slot + offset of each unique entry
+__global__ void __launch_bounds__(64) k_stencil_slots_wave(const uint64_t* __restrict__ tmp_row,
+                                                           const Pair* __restrict__ tmp,
+                                                           const uint64_t* __restrict__ st_row, uint64_t nl,
+                                                           const uint32_t* __restrict__ slot_of_g,
+                                                           uint32_t* __restrict__ st_slot, int32_t* __restrict__ st_off)
+{
+    __shared__ uint64_t s_dst[65], s_src[64];
+    const int lane = threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t last = r0 + 64 < nl ? r0 + 64 : nl;
+    s_dst[lane] = st_row[r0 + lane < last ? r0 + lane : last];
+    if (lane == 0) s_dst[64] = st_row[last];
+    if (r0 + lane < nl) s_src[lane] = tmp_row[r0 + lane];
+    __syncthreads();
+    const uint64_t end = s_dst[64];
+    for (uint64_t o = s_dst[0] + lane; o < end; o += 64) {
+        const int j = wave_row_of(s_dst, o);
+        const Pair p = tmp[s_src[j] + (o - s_dst[j])];
+        st_slot[o] = slot_of_g[p.g];
+        st_off[3 * o + 0] = p.x;
+        st_off[3 * o + 1] = p.y;
+        st_off[3 * o + 2] = p.z;
+    }
+}
+
 static unsigned grid_for(uint64_t n)
 {
     uint64_t g = (n + 255) / 256;
@@ -321,6 +832,8 @@ static ExView view(const dccrgx_grid* grid)
     v.keys = grid->ex->d_keys;
     v.vals = grid->ex->d_vals;
     v.mask = grid->ex->mask;
+    v.bits = grid->ex->d_bits;
+    v.rank = grid->ex->d_rank;
     for (int d = 0; d < 3; d++) v.per[d] = grid->params.periodic[d] ? 1 : 0;
     return v;
 }
@@ -393,8 +906,8 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
         DX_HIP(dx_malloc(off, t * 12));
         DX_HIP(dx_malloc(gidx, t * 4));
         if (n)
-            hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(n)), dim3(256), 0, st, v, h.d_of_c, h.K, cells, n, row,
-                               *ids, *off, *gidx, d_err);
+            hipLaunchKernelGGL(k_ex_nof_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, h.d_of_c, h.K,
+                               cells, n, (const uint64_t*)row, *ids, *off, *gidx);
         DX_HIP(hipGetLastError());
     }
     dx_free(d_err);
@@ -420,15 +933,27 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     E->build_dir();
     uint64_t cap = 16;
     while (cap < 2 * E->n) cap <<= 1;
-    E->mask = cap - 1;
     DX_TRY(upload(grid->ctx, E->leaves, &E->d_leaves, st));
-    DX_HIP(dx_malloc(&E->d_keys, cap * 8));
-    DX_HIP(dx_malloc(&E->d_vals, cap * 4));
-    DX_HIP(hipMemsetAsync(E->d_keys, 0, cap * 8, st));
-    hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(E->n)), dim3(256), 0, st, E->d_leaves, E->n,
-                       (unsigned long long*)E->d_keys, E->d_vals, E->mask);
+    // the rank bitmap when it is small (at most 1 GiB, and at most 16x the hash)
+    const uint64_t nw = (grid->map.last_cell >> 6) + 1;
+    if (nw <= (1ull << 26) && nw * 12 <= 16 * cap * 12) {
+        E->nwords = nw;
+        DX_HIP(dx_malloc(&E->d_bits, nw * 8));
+        DX_HIP(dx_malloc(&E->d_rank, nw * 4));
+        DX_HIP(hipMemsetAsync(E->d_bits, 0, nw * 8, st));
+        hipLaunchKernelGGL(k_bits_set, dim3(grid_for(E->n)), dim3(256), 0, st, E->d_leaves, E->n,
+                           (unsigned long long*)E->d_bits);
+        hipLaunchKernelGGL(k_bits_rank, dim3(grid_for(nw)), dim3(256), 0, st, E->d_leaves, E->n, nw, E->d_rank);
+    } else {
+        E->mask = cap - 1;
+        DX_HIP(dx_malloc(&E->d_keys, cap * 8));
+        DX_HIP(dx_malloc(&E->d_vals, cap * 4));
+        DX_HIP(hipMemsetAsync(E->d_keys, 0, cap * 8, st));
+        hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(E->n)), dim3(256), 0, st, E->d_leaves, E->n,
+                           (unsigned long long*)E->d_keys, E->d_vals, E->mask);
+    }
     DX_HIP(hipGetLastError());
-    T.lap("leaves+hash");
+    T.lap("leaves+lookup");
     // ownership: the process of the level-0 ancestor (no load balancing),
     // block partition or the grid's SFC table
     E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
@@ -614,7 +1139,8 @@ int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
 void explicit_free(Explicit* E)
 {
     if (!E) return;
-    for (void* q : {(void*)E->d_leaves, (void*)E->d_keys, (void*)E->d_vals, (void*)E->d_local_g,
+    for (void* q : {(void*)E->d_leaves, (void*)E->d_keys, (void*)E->d_vals, (void*)E->d_bits, (void*)E->d_rank,
+                    (void*)E->d_local_g,
                     (void*)E->d_level, (void*)E->d_slot_of_g, (void*)E->d_local_slot})
         dx_free(q);
     for (auto& kv : E->hl) {
@@ -637,6 +1163,35 @@ void explicit_destroy(dccrgx_grid* grid)
 {
     explicit_free(grid->ex);
     grid->ex = nullptr;
+}
+
+// host copies of a neighborhood's device CSRs (neighbors_of / neighbors_to
+// as global leaf indices), made once per build when host code needs them
+int explicit_host_lists(const dccrgx_grid* grid, const Hood& h)
+{
+    Explicit* E = grid->ex;
+    Explicit::HoodLists& L = E->hl[h.id];
+    if (L.host_valid) return DCCRGX_OK;
+    Ctx* ctx = grid->ctx;
+    hipStream_t st = ctx->compute;
+    const uint64_t N = E->n;
+    L.h_nof_row.resize(N + 1);
+    L.h_nto_row.resize(N + 1);
+    DX_TRY(dx_d2h(ctx, L.h_nof_row.data(), h.d_nof_row, (N + 1) * 8, st));
+    DX_TRY(dx_d2h(ctx, L.h_nto_row.data(), h.d_nto_row, (N + 1) * 8, st));
+    L.h_nof_g.resize(L.h_nof_row[N]);
+    L.h_nto_g.resize(L.h_nto_row[N]);
+    DX_TRY(dx_d2h(ctx, L.h_nof_g.data(), h.d_nof_g, L.h_nof_g.size() * 4, st));
+    DX_TRY(dx_d2h(ctx, L.h_nto_g.data(), h.d_nto_g, L.h_nto_g.size() * 4, st));
+    L.host_valid = true;
+    return DCCRGX_OK;
+}
+
+int explicit_host_lists(const dccrgx_grid* grid, int32_t hood_id)
+{
+    const Hood* h = find_hood(grid, hood_id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    return explicit_host_lists(grid, *h);
 }
 
 int explicit_build_hood(dccrgx_grid* grid, Hood& h)
@@ -675,14 +1230,17 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     hipLaunchKernelGGL(k_tr_scatter, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_trow,
                        d_cur, d_tmp);
     DX_HIP(dx_malloc(&d_ucnt, N * 4));
+    hipLaunchKernelGGL(k_sort_unique_rows64, dim3((unsigned)std::min<uint64_t>((N + 3) / 4, 16384)), dim3(256), 0, st,
+                       d_trow, N, d_tmp, d_ucnt);
+    hipLaunchKernelGGL(k_sort_unique_rows_wave, dim3((unsigned)std::min<uint64_t>(N, 4096)), dim3(64), 0, st, d_trow,
+                       N, d_tmp, d_ucnt);
     hipLaunchKernelGGL(k_sort_unique_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, N, d_tmp, d_ucnt);
     DX_HIP(hipGetLastError());
     uint64_t ntot = 0;
     DX_TRY(scan_counts_device(d_ucnt, N, &h.d_nto_row, &ntot, st));
-    std::vector<uint64_t> nto_row(N + 1);
-    DX_TRY(dx_d2h(ctx, nto_row.data(), h.d_nto_row, (N + 1) * 8, st));
     DX_HIP(dx_malloc(&h.d_nto_g, std::max<uint64_t>(ntot, 1) * 4));
-    hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, d_tmp, h.d_nto_row, N, h.d_nto_g);
+    hipLaunchKernelGGL(k_copy_rows_wave, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, d_trow, d_tmp, h.d_nto_row,
+                       N, h.d_nto_g);
     DX_HIP(hipGetLastError());
     dx_free(d_cnt);
     dx_free(d_cur);
@@ -693,20 +1251,18 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     T.lap("neighbors_to");
     // per-rank bookkeeping from the device lists (dccrg.hpp:9131-9234, 8729-8891)
     const uint64_t nl = E->local.size();
-    std::vector<uint64_t> nof_row(N + 1);
-    DX_TRY(dx_d2h(ctx, nof_row.data(), h.d_nof_row, (N + 1) * 8, st));
     Explicit::HoodLists& L = E->hl[h.id];
     for (uint32_t* p : {L.d_inner_pos, L.d_outer_pos, L.d_all_pos}) dx_free(p);
     L = Explicit::HoodLists{};
-    L.h_nto_row = nto_row;
-    L.h_nto_g.resize(nto_row[N]);
-    DX_HIP(hipStreamSynchronize(st));
-    L.h_nof_row = nof_row;
-    L.h_nof_g.resize(nof_row[N]);
-    DX_TRY(dx_d2h(ctx, L.h_nof_g.data(), h.d_nof_g, nof_row[N] * 4, st));
-    DX_TRY(dx_d2h(ctx, L.h_nto_g.data(), h.d_nto_g, nto_row[N] * 4, st));
-    DX_HIP(hipStreamSynchronize(st));
-    T.lap("lists to host");
+    // host copies of the lists only where host code reads them: the
+    // classification of several ranks here; refinement requests and
+    // neighbors_to queries fetch them on first use (explicit_host_lists)
+    if (ctx->comm_size > 1) {
+        DX_TRY(explicit_host_lists(grid, h));
+        T.lap("lists to host");
+    }
+    const std::vector<uint64_t>& nof_row = L.h_nof_row;
+    const std::vector<uint64_t>& nto_row = L.h_nto_row;
     const std::vector<int32_t>& owner = E->owner;
     const int me = ctx->rank;
     std::set<uint64_t> remote;
@@ -751,7 +1307,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     if (ctx->comm_size == 1) {  // every leaf is local, in leaf order: the rows are neighbors_of's
         DX_HIP(dx_malloc(&d_tmp_row, (nl + 1) * 8));
         DX_HIP(hipMemcpyAsync(d_tmp_row, h.d_nof_row, (nl + 1) * 8, hipMemcpyDeviceToDevice, st));
-        tmp_tot = nof_row[nl];
+        tmp_tot = tot;
     } else {
         std::vector<uint64_t> tmp_row(nl + 1, 0);
         for (uint64_t i = 0; i < nl; i++) {
@@ -763,16 +1319,21 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     }
     DX_HIP(dx_malloc(&d_pairs, std::max<uint64_t>(tmp_tot, 1) * sizeof(Pair)));
     DX_HIP(dx_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4));
-    if (nl)
+    if (nl) {
+        hipLaunchKernelGGL(k_stencil_rows64, dim3((unsigned)std::min<uint64_t>((nl + 3) / 4, 16384)), dim3(256), 0, st,
+                           h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
+        hipLaunchKernelGGL(k_stencil_rows_wave, dim3((unsigned)std::min<uint64_t>(nl, 4096)), dim3(64), 0, st,
+                           h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
         hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
                            h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
+    }
     uint64_t stot = 0;
     DX_TRY(scan_counts_device(d_pc, nl, &h.d_st_row, &stot, st));
     DX_HIP(dx_malloc(&h.d_st_slot, std::max<uint64_t>(stot, 1) * 4));
     DX_HIP(dx_malloc(&h.d_st_off, std::max<uint64_t>(stot, 1) * 12));
     if (nl)
-        hipLaunchKernelGGL(k_stencil_slots, dim3(grid_for(nl)), dim3(256), 0, st, d_tmp_row, d_pairs, h.d_st_row, nl,
-                           E->d_slot_of_g, h.d_st_slot, h.d_st_off);
+        hipLaunchKernelGGL(k_stencil_slots_wave, dim3((unsigned)((nl + 63) / 64)), dim3(64), 0, st, d_tmp_row,
+                           d_pairs, h.d_st_row, nl, E->d_slot_of_g, h.d_st_slot, h.d_st_off);
     DX_HIP(hipGetLastError());
     DX_HIP(hipStreamSynchronize(st));
     dx_free(d_tmp_row);
@@ -895,6 +1456,8 @@ int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_
     v.keys = old->d_keys;
     v.vals = old->d_vals;
     v.mask = old->mask;
+    v.bits = old->d_bits;
+    v.rank = old->d_rank;
     hipLaunchKernelGGL(k_old_slots, dim3(grid_for(n)), dim3(256), 0, st, v, old->d_slot_of_g, d_ids, n, d_src);
     const hipError_t e = hipGetLastError();
     DX_HIP(hipStreamSynchronize(st));
@@ -1008,33 +1571,47 @@ int explicit_gather_neighbors(const dccrgx_grid* grid, const Hood& h, const Fiel
     return done(DCCRGX_OK);
 }
 
+// get_neighbors_of (dccrg.hpp:836-883) is a lookup of lists built with the
+// grid (initialize_neighbors, :8371-8420): the query cells' rows are copied
+// out of the neighborhood's device CSR of every leaf -- row lengths, a scan,
+// then one coalesced copy of the ids and offsets
 int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n, uint64_t* row,
                           uint64_t* ids, int32_t* off3, size_t cap, hipStream_t st)
 {
-    dccrgx_grid* g = const_cast<dccrgx_grid*>(grid);
+    DX_CHECK(h.d_nof_row, DCCRGX_EINTERNAL, "no device lists for neighborhood %d", h.id);
+    uint32_t* gq = nullptr;
+    int32_t* d_err = nullptr;
+    DX_HIP(hipMallocAsync((void**)&gq, std::max<size_t>(n, 1) * 4, st));
+    DX_HIP(hipMallocAsync((void**)&d_err, 4, st));
+    auto done = [&](int code) {
+        (void)hipFreeAsync(gq, st);
+        (void)hipFreeAsync(d_err, st);
+        return code;
+    };
+    if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
+    if (n)
+        hipLaunchKernelGGL(k_ex_query_rows, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nof_row, gq,
+                           row, d_err);
     uint64_t total = 0;
-    uint64_t* t_ids = nullptr;
-    int32_t* t_off = nullptr;
-    uint32_t* t_g = nullptr;
-    DX_TRY(nof_device(g, h, cells, n, row, ids ? &t_ids : nullptr, &t_off, &t_g, &total, st));
-    if (!ids) return DCCRGX_OK;
-    int s = DCCRGX_OK;
-    if (cap < total) s = set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total);
-    else if (total) {
-        DX_HIP(hipMemcpyAsync(ids, t_ids, total * 8, hipMemcpyDeviceToDevice, st));
-        if (off3) DX_HIP(hipMemcpyAsync(off3, t_off, total * 12, hipMemcpyDeviceToDevice, st));
-    }
-    DX_HIP(hipStreamSynchronize(st));
-    dx_free(t_ids);
-    dx_free(t_off);
-    dx_free(t_g);
-    return s;
+    int s = device_scan_rows(row, n, st, &total);  // synchronises (total)
+    if (s != DCCRGX_OK) return done(s);
+    int32_t err = 0;
+    if ((s = dx_d2h(grid->ctx, &err, d_err, 4, st)) != DCCRGX_OK) return done(s);
+    if (err) return done(set_error(DCCRGX_ENOTFOUND, "cell does not exist"));
+    if (!ids) return done(DCCRGX_OK);
+    if (cap < total) return done(set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total));
+    if (n)
+        hipLaunchKernelGGL(k_rows_gather, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, (const uint32_t*)gq,
+                           (uint64_t)n, h.d_nof_row, (const uint64_t*)row, h.d_nof_id, h.d_nof_off, ids, off3);
+    if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "neighbor list copy failed"));
+    return done(DCCRGX_OK);
 }
 
 int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n, uint64_t* row,
                           uint64_t* ids, size_t cap, hipStream_t st)
 {
     const Explicit* E = grid->ex;
+    DX_TRY(explicit_host_lists(grid, h));
     const auto& L = E->hl.at(h.id);
     std::vector<uint64_t> hc(n);
     DX_TRY(dx_d2h(grid->ctx, hc.data(), cells, n * 8, st));

@@ -9,6 +9,7 @@
 //   update_remote_neighbor_info dccrg.hpp:9131-9409 (inner / outer / remote)
 //   recalculate_..._lists     dccrg.hpp:8729-8891  (ascending per-peer lists)
 #include <algorithm>
+#include <array>
 #include <cstring>
 
 #include "grid.hpp"
@@ -370,6 +371,27 @@ int build_hood(dccrgx_grid* grid, Hood& h)
             all = (m == 1);
         }
         h.cube1 = all;
+    }
+    // neighbor counts in closed form (dccrgx_neighbors_of on uniform grids):
+    // the full cube of some length, or the six face items
+    {
+        std::set<std::array<int32_t, 3>> distinct;
+        int m = 0;
+        bool faces = h.K == 6;
+        for (int k = 0; k < h.K; k++) {
+            const std::array<int32_t, 3> it = {h.items[3 * k], h.items[3 * k + 1], h.items[3 * k + 2]};
+            distinct.insert(it);
+            int mk = 0, nz = 0;
+            for (int d = 0; d < 3; d++) {
+                mk = std::max(mk, std::abs(it[d]));
+                nz += it[d] != 0;
+            }
+            m = std::max(m, mk);
+            faces &= mk == 1 && nz == 1;
+        }
+        const bool unique = (int)distinct.size() == h.K && !distinct.count({0, 0, 0});
+        h.count_cube = unique && m >= 1 && h.K == (2 * m + 1) * (2 * m + 1) * (2 * m + 1) - 1 ? m : -1;
+        h.count_faces = unique && faces;
     }
     DX_TRY(upload(h.of_c, &h.d_of_c, st));
     DX_TRY(upload(h.to_c, &h.d_to_c, st));

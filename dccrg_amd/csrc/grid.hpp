@@ -130,6 +130,9 @@ struct Explicit {
     uint64_t* d_keys = nullptr;     // hash keys (0 = empty)
     uint32_t* d_vals = nullptr;     // global index
     uint64_t mask = 0;
+    uint64_t* d_bits = nullptr;     // rank bitmap over the id space (instead of the hash)
+    uint32_t* d_rank = nullptr;     // leaves before each 64-bit word
+    uint64_t nwords = 0;
     Partition part;                 // over level-0 cells
     std::vector<uint64_t> local;    // ascending local ids
     std::vector<uint32_t> local_g;  // their global indices
@@ -149,6 +152,8 @@ struct Explicit {
     uint64_t d_level_n = 0, d_level_cap = 0;        // levels written, capacity
     bool defer_fields = false;                      // rebuild(): fields are moved afterwards
     struct HoodLists {
+        // host copies (explicit_host_lists), made on first use after a build
+        bool host_valid = false;
         std::vector<uint64_t> h_nof_row, h_nto_row;
         std::vector<uint32_t> h_nof_g, h_nto_g;
         std::vector<uint32_t> inner_pos, outer_pos;  // positions in `local`
@@ -236,6 +241,8 @@ struct Hood {
     int32_t* d_to_c = nullptr;
     int32_t K = 0;
     bool cube1 = false;            // the full 26-item cube: fast stencil path
+    int32_t count_cube = -1;       // the full cube of this length (closed-form neighbor counts), else -1
+    bool count_faces = false;      // the six face items (closed-form counts)
     // classification, dccrg.hpp:9131-9409
     std::vector<uint64_t> outer;   // ascending
     std::vector<uint64_t> remote;  // ascending
@@ -336,6 +343,9 @@ int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_
 // dst[k] = src[from[k]], or zero where from[k] < 0
 int launch_move(const void* src, const int64_t* from, uint64_t n, uint32_t elem, void* dst, hipStream_t st);
 int explicit_build_hood(dccrgx_grid* grid, Hood& h);
+// host copies of a neighborhood's neighbor lists, fetched once per build
+int explicit_host_lists(const dccrgx_grid* grid, const Hood& h);
+int explicit_host_lists(const dccrgx_grid* grid, int32_t hood_id);
 int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, uint64_t* ids,
                        size_t cap, size_t* n);
 int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device);

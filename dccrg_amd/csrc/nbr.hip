@@ -73,6 +73,144 @@ __global__ void __launch_bounds__(256) k_uniform_nbrs(UGeom g, const int32_t* __
     }
 }
 
+// ---------------------------------------------------------------------------
+// Row pointers of a batch of query cells without a count array: each cell's count in
+// closed form where the neighborhood allows (the full cube of length L: the
+// product over axes of the in-grid offsets in [-L, L], minus the cell itself;
+// the six face items: the in-grid ones), else by testing every item; then
+// reduce-then-scan over tiles of 1024 cells (tile totals, their scan, and the
+// rows written with the counts recomputed -- no count array in memory).
+// ---------------------------------------------------------------------------
+constexpr int RT = 256, RE = 4, RTILE = RT * RE;  // threads, cells per thread, cells per tile
+
+__device__ __forceinline__ uint32_t uniform_count(const UGeom& g, const int32_t* items, int K, int cube, bool faces,
+                                                  int64_t a, int64_t b, int64_t c)
+{
+    const int64_t pos[3] = {a, b, c};
+    const uint64_t len[3] = {g.LA, g.LB, g.LC};
+    const int32_t per[3] = {g.perA, g.perB, g.perC};
+    if (cube >= 0) {
+        uint32_t prod = 1;
+        for (int d = 0; d < 3; d++) {
+            const int64_t L = cube;
+            const int64_t lo = per[d] ? L : (pos[d] < L ? pos[d] : L);
+            const int64_t hi = per[d] ? L : ((int64_t)len[d] - 1 - pos[d] < L ? (int64_t)len[d] - 1 - pos[d] : L);
+            prod *= (uint32_t)(lo + hi + 1);
+        }
+        return prod - 1;
+    }
+    if (faces) {
+        uint32_t n = 0;
+        for (int d = 0; d < 3; d++)
+            n += per[d] ? 2u : (uint32_t)(pos[d] > 0) + (uint32_t)(pos[d] + 1 < (int64_t)len[d]);
+        return n;
+    }
+    uint32_t n = 0;
+    for (int k = 0; k < K; k++) {
+        uint64_t nlin;
+        int64_t cu;
+        n += ug_neighbor(g, a, b, c, items + 3 * k, nlin, cu) ? 1u : 0u;
+    }
+    return n;
+}
+
+// pass 1 (tile_sum != null): the total of each tile; pass 2: row[i + 1] =
+// (the inclusive scan of the tile totals before this tile) + the prefix
+// inside the tile.  The counts are recomputed in pass 2 (a few ALU ops).
+__global__ void __launch_bounds__(RT) k_uniform_rows(UGeom g, const int32_t* __restrict__ items, int K, int cube,
+                                                     int faces, const uint64_t* __restrict__ cells, size_t n,
+                                                     int check_local, uint64_t* __restrict__ tile_sum,
+                                                     const uint64_t* __restrict__ tile_incl, uint64_t* __restrict__ row,
+                                                     int32_t* __restrict__ err)
+{
+    __shared__ uint64_t s_wave[RT / 64];
+    const uint64_t tile = blockIdx.x;
+    const uint64_t i0 = tile * RTILE + (uint64_t)threadIdx.x * RE;
+    uint64_t inc[RE];
+    uint64_t t = 0;
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < RE; k++) {
+        const uint64_t i = i0 + k;
+        uint32_t cnt = 0;
+        if (i < n) {
+            const uint64_t id = cells[i];
+            if (id < 1 || id > g.N || (check_local && (id - 1 < g.lo || id - 1 >= g.hi))) {
+                bad = true;
+            } else {
+                int64_t a, b, c;
+                ug_decompose(g, id - 1, a, b, c);
+                cnt = uniform_count(g, items, K, cube, faces != 0, a, b, c);
+            }
+        }
+        t += cnt;
+        inc[k] = t;
+    }
+    if (bad && tile_sum) atomicOr(err, 1);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t v = t;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t u = __shfl_up(v, d, 64);
+        if (lane >= d) v += u;
+    }
+    if (lane == 63) s_wave[w] = v;
+    __syncthreads();
+    uint64_t before = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < RT / 64; k++) {
+        before += k < w ? s_wave[k] : 0;
+        total += s_wave[k];
+    }
+    if (tile_sum) {
+        if (threadIdx.x == 0) tile_sum[tile] = total;
+        return;
+    }
+    const uint64_t base = (tile ? tile_incl[tile - 1] : 0) + before + v - t;
+    if (tile == 0 && threadIdx.x == 0) row[0] = 0;
+#pragma unroll
+    for (int k = 0; k < RE; k++)
+        if (i0 + k < n) row[i0 + k + 1] = base + inc[k];
+}
+
+// row pointers of `cells` into row[0..n] (device); *total on the host.
+// check_local: every query cell must be local to this rank
+static int uniform_rows(const dccrgx_grid* grid, const Hood& h, const int32_t* d_items, const uint64_t* cells,
+                        size_t n, int check_local, uint64_t* row, uint64_t* total, hipStream_t st)
+{
+    const UGeom& g = grid->g;
+    const uint64_t tiles = std::max<uint64_t>((n + RTILE - 1) / RTILE, 1);
+    DX_CHECK(tiles < (1ull << 31), DCCRGX_EINVAL, "%zu query cells", n);
+    // one scratch block: the tile sums (scanned in place), the error word, the total
+    uint64_t* scratch = nullptr;
+    const size_t words = tiles + 2;
+    DX_HIP(hipMallocAsync((void**)&scratch, words * 8, st));
+    auto done = [&](int code) {
+        (void)hipFreeAsync(scratch, st);
+        return code;
+    };
+    if (hipMemsetAsync(scratch, 0, words * 8, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
+    int32_t* err = reinterpret_cast<int32_t*>(scratch + tiles);
+    hipLaunchKernelGGL(k_uniform_rows, dim3((unsigned)tiles), dim3(RT), 0, st, g, d_items, h.K, (int)h.count_cube,
+                       h.count_faces ? 1 : 0, cells, n, check_local, scratch, (const uint64_t*)nullptr, row, err);
+    int s = device_inclusive_scan(scratch, tiles, st);
+    if (s != DCCRGX_OK) return done(s);
+    hipLaunchKernelGGL(k_uniform_rows, dim3((unsigned)tiles), dim3(RT), 0, st, g, d_items, h.K, (int)h.count_cube,
+                       h.count_faces ? 1 : 0, cells, n, check_local, (uint64_t*)nullptr, (const uint64_t*)scratch, row,
+                       err);
+    if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "row kernel launch failed"));
+    // the error word and the total in one copy
+    if (hipMemcpyAsync(scratch + tiles + 1, scratch + tiles - 1, 8, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return done(set_error(DCCRGX_EHIP, "copy"));
+    uint64_t tail[2] = {0, 0};
+    if ((s = dx_d2h(grid->ctx, tail, scratch + tiles, 16, st)) != DCCRGX_OK) return done(s);
+    *total = tail[1];
+    if (tail[0])
+        return done(set_error(DCCRGX_ENOTFOUND, check_local ? "a query cell is not a local cell of this rank"
+                                                            : "cell outside the grid"));
+    return done(DCCRGX_OK);
+}
+
 // fill pass with coalesced stores: one wave per 64 query cells.  Each lane
 // lists its cell's valid neighbors (id and item) in LDS at the cell's
 // position in the wave's output run (row[] is already scanned), then the wave
@@ -308,26 +446,9 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
     if (!grid->uniform) return explicit_neighbors_of(grid, *h, cells, n, row, ids, off3, cap, st);
     const UGeom& g = grid->g;
-    struct ErrWord {
-        int32_t* p = nullptr;
-        ~ErrWord()
-        {
-            if (p) (void)dx_free(p);
-        }
-    } d_err;
-    DX_HIP(dx_malloc(&d_err.p, 4));
-    DX_HIP(hipMemsetAsync(d_err.p, 0, 4, st));
     const int32_t sc = 1 << grid->map.max_lvl;  // offsets in indices of the finest level
-    if (n)
-        hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells,
-                           n, row, (uint64_t*)nullptr, (int32_t*)nullptr, d_err.p, sc, sc, sc);
-    DX_HIP(hipGetLastError());
     uint64_t total = 0;
-    DX_TRY(scan_rows(row, n, st, &total));
-    int32_t err = 0;
-    DX_HIP(hipMemcpyAsync(&err, d_err.p, 4, hipMemcpyDeviceToHost, st));
-    DX_HIP(hipStreamSynchronize(st));
-    DX_CHECK(!err, DCCRGX_ENOTFOUND, "cell outside the grid");
+    DX_TRY(uniform_rows(grid, *h, h->d_of_c, cells, n, 0, row, &total, st));
     if (!ids) return DCCRGX_OK;
     DX_CHECK(cap >= total, DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total);
     if (n && h->K <= 76) {  // LDS records: 652 B per item (48 KiB at 76)
@@ -336,10 +457,12 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     } else if (n && h->K <= 192) {  // 256 B per item (48 KiB at 192)
         hipLaunchKernelGGL(k_uniform_fill_rec, dim3((unsigned)((n + 63) / 64)), dim3(64), 64 * 4 * h->K, st, g,
                            h->d_of_c, h->K, cells, n, row, ids, off3, sc, sc, sc);
-    } else if (n) {
+    } else if (n) {  // per-thread rows (the cells were checked by uniform_rows)
+        int32_t* d_err = nullptr;
+        DX_HIP(hipMallocAsync((void**)&d_err, 4, st));
         hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells,
-                           n, row, ids, off3, d_err.p, sc, sc, sc);
-        DX_HIP(hipStreamSynchronize(st));  // d_err is freed on return
+                           n, row, ids, off3, d_err, sc, sc, sc);
+        DX_HIP(hipFreeAsync(d_err, st));
     }
     DX_HIP(hipGetLastError());
     return DCCRGX_OK;
@@ -357,27 +480,8 @@ int dccrgx_gather_neighbors(const dccrgx_grid* grid, int32_t hood_id, int32_t fi
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
     if (!grid->uniform) return explicit_gather_neighbors(grid, *h, F, cells, n, row, out, cap_bytes, st);
     const UGeom& g = grid->g;
-    struct ErrWord {
-        int32_t* p = nullptr;
-        ~ErrWord()
-        {
-            if (p) (void)dx_free(p);
-        }
-    } d_err;
-    DX_HIP(dx_malloc(&d_err.p, 4));
-    DX_HIP(hipMemsetAsync(d_err.p, 0, 4, st));
-    if (n) {
-        hipLaunchKernelGGL(k_check_local, dim3(grid_for(n)), dim3(256), 0, st, g, cells, n, d_err.p);
-        hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells, n, row,
-                           (uint64_t*)nullptr, (int32_t*)nullptr, d_err.p, 1, 1, 1);
-    }
-    DX_HIP(hipGetLastError());
     uint64_t total = 0;
-    DX_TRY(scan_rows(row, n, st, &total));
-    int32_t err = 0;
-    DX_HIP(hipMemcpyAsync(&err, d_err.p, 4, hipMemcpyDeviceToHost, st));
-    DX_HIP(hipStreamSynchronize(st));
-    DX_CHECK(!err, DCCRGX_ENOTFOUND, "a query cell is not a local cell of this rank");
+    DX_TRY(uniform_rows(grid, *h, h->d_of_c, cells, n, 1, row, &total, st));
     if (!out) return DCCRGX_OK;
     DX_CHECK(cap_bytes >= total * F.elem, DCCRGX_ERANGE, "capacity %zu < %llu bytes", cap_bytes,
              (unsigned long long)(total * F.elem));
