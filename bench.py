@@ -49,7 +49,38 @@ def cpu_baseline(seconds: float = 10.0):
             "kind": "port",
             "sample": f"{L[0]}x{L[1]}x{L[2]} uniform grid, hood 1, periodic z, {steps} steps "
                       f"({dt:.1f} s) of oracle/dccrg_oracle.c dox_gol_count+apply over "
-                      f"face-graph-walk neighbor lists"}
+                      f"face-graph-walk neighbor lists",
+            "host": host_cpu(),
+            # the reference program itself cannot be built here (dccrg.hpp needs
+            # Boost.TTI and Zoltan, absent from this image),
+            # so its own MPI-CPU figures are the ones the survey measured (BASELINE.md
+            # section 2), quoted as measured there -- not on this box
+            "reference_measured": {
+                "kind": "reference", "source": "BASELINE.md section 2 / SURVEY.md section 6",
+                "program": "tests/game_of_life/scalability3d.cpp, unmodified, 100^3, 26 neighbors, 100 steps, "
+                           "its own timer around the step loop incl. halo",
+                "host": "survey container: Intel Xeon, 8 cores (1 thread/core), g++ 11.4 -O3, MPICH 3.3.2",
+                "unit": "cell-updates/s", "by_ranks": {"1": 7.90e6, "2": 1.55e7, "4": 2.69e7, "8": 4.30e7}}}
+
+
+def host_cpu():
+    """CPU model and the cores this process may use (lscpu's model name, the
+    affinity mask; on the GPU box the machine's count is larger than the
+    share a one-GPU job gets)."""
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"model": model, "logical_cpus": os.cpu_count(), "usable_cpus": usable,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def pmc_traffic(kernel: str, cells_per_launch: int):
@@ -491,9 +522,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
-        print(json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world, "gpus": args.gpus,
-                          "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"}),
-              flush=True)
+        line = json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world, "gpus": args.gpus,
+                           "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"})
+        os.write(1, (line + "\n").encode())  # one write: ranks share the launcher's stdout pipe
         return
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")

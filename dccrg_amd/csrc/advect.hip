@@ -578,7 +578,8 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
 
 FaceCache::~FaceCache()
 {
-    for (void* q : {(void*)ell_slot, (void*)ell_dir, (void*)o_row, (void*)o_slot, (void*)o_dir}) dx_free(q);
+    FreeBatch fb;
+    for (void* q : {(void*)ell_slot, (void*)ell_dir, (void*)o_row, (void*)o_slot, (void*)o_dir}) fb.add(q);
 }
 
 }  // namespace dccrgx

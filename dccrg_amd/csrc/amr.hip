@@ -97,22 +97,44 @@ struct View {
         if (exists(map_cell(g->map, idx, l + 1))) return true;
         return !exists(c);
     }
-    // neighbors_of / neighbors_to of an existing leaf (default neighborhood)
+    // neighbors_of / neighbors_to of an existing leaf (default neighborhood):
+    // from the host copy of the lists when one was made, else from the row
+    // cache (rows are prefetched in batches by prefetch(); a miss fetches one)
     template <class F>
-    void for_nof(uint64_t c, F f) const
+    void for_row(uint64_t c, bool to, F f) const
     {
+        const Hood& h = g->hoods.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
         const auto& L = E->hl.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
         const int64_t r = gidx(c);
         if (r < 0) return;
-        for (uint64_t e = L.h_nof_row[r]; e < L.h_nof_row[r + 1]; e++) f(E->leaves[L.h_nof_g[e]]);
+        if (L.host_valid) {
+            const auto& row = to ? L.h_nto_row : L.h_nof_row;
+            const auto& val = to ? L.h_nto_g : L.h_nof_g;
+            for (uint64_t e = row[r]; e < row[r + 1]; e++) f(E->leaves[val[e]]);
+            return;
+        }
+        auto it = L.row_at.find((uint32_t)r);
+        if (it == L.row_at.end()) {
+            if (explicit_fetch_rows(g, h, {(uint32_t)r}) != DCCRGX_OK) return;
+            it = L.row_at.find((uint32_t)r);
+        }
+        const uint64_t off = it->second[to ? 2 : 0], len = it->second[to ? 3 : 1];
+        for (uint64_t e = off; e < off + len; e++) f(E->leaves[L.row_vals[e]]);
     }
     template <class F>
-    void for_nto(uint64_t c, F f) const
+    void for_nof(uint64_t c, F f) const { for_row(c, false, f); }
+    template <class F>
+    void for_nto(uint64_t c, F f) const { for_row(c, true, f); }
+    // one device gather for the rows of many cells (existing leaves only)
+    int prefetch(const uint64_t* cells, size_t n) const
     {
-        const auto& L = E->hl.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
-        const int64_t r = gidx(c);
-        if (r < 0) return;
-        for (uint64_t e = L.h_nto_row[r]; e < L.h_nto_row[r + 1]; e++) f(E->leaves[L.h_nto_g[e]]);
+        std::vector<uint32_t> gs;
+        gs.reserve(n);
+        for (size_t i = 0; i < n; i++) {
+            const int64_t r = gidx(cells[i]);
+            if (r >= 0) gs.push_back((uint32_t)r);
+        }
+        return explicit_fetch_rows(g, g->hoods.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID), gs);
     }
     // the face graph neighbors_ of a leaf (update_neighbors_, :9463-9597)
     void face(uint64_t c, uint64_t out[6]) const
@@ -357,7 +379,7 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
         F.cap_bytes = cap[i];
     }
     for (auto& kv : old_hoods) free_hood(kv.second);
-    explicit_free(old.ex);
+    explicit_recycle(grid, old.ex);
     old.ex = nullptr;
     T.lap("fields moved");
     return DCCRGX_OK;
@@ -441,7 +463,6 @@ int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
         *result = 1;
         return DCCRGX_OK;
     }
-    DX_TRY(explicit_host_lists(grid, DCCRGX_DEFAULT_NEIGHBORHOOD_ID));
     const View v{grid, grid->ex, grid->map.max_lvl};
     Amr& A = amr_of(grid);
     // dccrg.hpp:2476-2546
@@ -561,6 +582,8 @@ int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 int dccrgx_amr_request_cells(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results)
 {
     DX_CHECK(grid && (ids || !n) && kind >= 0 && kind < 4, DCCRGX_EINVAL, "bad argument");
+    if (kind == DCCRGX_AMR_REFINE && !grid->uniform && n > 1)  // the rows refine_completely reads, in one gather
+        DX_TRY((View{grid, grid->ex, grid->map.max_lvl}.prefetch(ids, n)));
     for (size_t i = 0; i < n; i++) {
         int32_t r = 0;
         switch (kind) {
@@ -613,7 +636,6 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
         return DCCRGX_OK;
     }
     DX_TRY(ensure_explicit(grid));
-    DX_TRY(explicit_host_lists(grid, DCCRGX_DEFAULT_NEIGHBORHOOD_ID));
     const View v{grid, grid->ex, grid->map.max_lvl};
 
     // override_refines, dccrg.hpp:10130-10236: dont_refine spreads to every
@@ -624,6 +646,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
         if (donts.insert(c).second) frontier.push_back(c);
     while (!frontier.empty()) {
         std::vector<uint64_t> next;
+        DX_TRY(v.prefetch(frontier.data(), frontier.size()));
         for (uint64_t c : frontier) {
             if (!v.exists(c)) continue;
             const int cl = v.level(c);
@@ -643,6 +666,7 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     frontier = R.sorted();
     while (!frontier.empty()) {
         std::vector<uint64_t> next;
+        DX_TRY(v.prefetch(frontier.data(), frontier.size()));
         for (uint64_t r : frontier) {
             const int rl = v.level(r);
             auto induce = [&](uint64_t n) {

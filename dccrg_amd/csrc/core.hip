@@ -5,6 +5,8 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstring>
+#include <condition_variable>
+#include <mutex>
 
 #include "internal.hpp"
 
@@ -465,6 +467,90 @@ int dccrgx_device_count(int* n)
 }  // extern "C"
 
 namespace dccrgx {
+size_t host_threads()
+{
+    static const size_t nt = [] {
+        size_t v = 0;
+        for (const char* var : {"DCCRGX_HOST_THREADS", "OMP_NUM_THREADS"}) {
+            const char* e = std::getenv(var);
+            if (e && std::atoi(e) > 0) {
+                v = (size_t)std::atoi(e);
+                break;
+            }
+        }
+        if (!v) v = std::max(1u, std::thread::hardware_concurrency());
+        return std::min<size_t>(v, 16);
+    }();
+    return nt;
+}
+
+namespace {
+// persistent workers for pool_run: each waits for a new generation, runs
+// its share, and counts itself done
+struct Pool {
+    std::mutex m;
+    std::condition_variable go, fin;
+    std::vector<std::thread> th;
+    const std::function<void(size_t)>* job = nullptr;
+    size_t gen = 0, active = 0, pending = 0;
+    bool stop = false;
+    void ensure(size_t workers)
+    {
+        while (th.size() < workers) {
+            const size_t id = th.size() + 1;
+            th.emplace_back([this, id] {
+                size_t seen = 0;
+                std::unique_lock<std::mutex> lk(m);
+                for (;;) {
+                    go.wait(lk, [&] { return stop || gen != seen; });
+                    if (stop) return;
+                    seen = gen;
+                    if (id >= active) continue;
+                    const std::function<void(size_t)>* j = job;
+                    lk.unlock();
+                    (*j)(id);
+                    lk.lock();
+                    if (--pending == 0) fin.notify_one();
+                }
+            });
+        }
+    }
+    ~Pool()
+    {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        go.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
+Pool& pool()
+{
+    static Pool p;
+    return p;
+}
+std::mutex g_pool_use;  // one parallel loop at a time
+}  // namespace
+
+void pool_run(size_t nt, const std::function<void(size_t)>& job)
+{
+    std::lock_guard<std::mutex> use(g_pool_use);
+    Pool& p = pool();
+    {
+        std::lock_guard<std::mutex> lk(p.m);
+        p.ensure(nt - 1);
+        p.job = &job;
+        p.active = nt;
+        p.pending = nt - 1;
+        p.gen++;
+    }
+    p.go.notify_all();
+    job(0);
+    std::unique_lock<std::mutex> lk(p.m);
+    p.fin.wait(lk, [&] { return p.pending == 0; });
+}
+
 void dx_trim_pool()
 {
     int dev = 0;

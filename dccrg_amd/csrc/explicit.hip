@@ -849,7 +849,7 @@ __global__ void __launch_bounds__(256) k_counts_to_row(const uint32_t* __restric
 // device; *total (host) = row[n]
 static int scan_counts_device(const uint32_t* d_cnt, uint64_t n, uint64_t** d_row, uint64_t* total, hipStream_t st)
 {
-    DX_HIP(dx_malloc(d_row, (n + 1) * 8));
+    DX_HIP(ds_malloc(d_row, (n + 1) * 8, st));
     if (n) hipLaunchKernelGGL(k_counts_to_row, dim3(grid_for(n)), dim3(256), 0, st, d_cnt, n, *d_row);
     DX_HIP(hipGetLastError());
     return device_scan_rows(*d_row, n, st, total);
@@ -864,7 +864,7 @@ __global__ void __launch_bounds__(256) k_iota(uint32_t* __restrict__ out, uint64
 // 0, 1, ..., n-1 on the device (identity maps need no upload)
 static int device_iota(uint32_t** d, uint64_t n, hipStream_t st)
 {
-    DX_HIP(dx_malloc(d, std::max<uint64_t>(n, 1) * 4));
+    DX_HIP(ds_malloc(d, std::max<uint64_t>(n, 1) * 4, st));
     if (n) hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(256), 0, st, *d, n);
     DX_HIP(hipGetLastError());
     return DCCRGX_OK;
@@ -874,7 +874,7 @@ template <class T>
 static int upload(Ctx* c, const std::vector<T>& v, T** d, hipStream_t st)
 {
     *d = nullptr;
-    DX_HIP(dx_malloc(d, std::max<size_t>(v.size(), 1) * sizeof(T)));
+    DX_HIP(ds_malloc(d, std::max<size_t>(v.size(), 1) * sizeof(T), st));
     return dx_h2d(c, *d, v.data(), v.size() * sizeof(T), st);
 }
 
@@ -884,7 +884,7 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
 {
     const ExView v = view(grid);
     int32_t* d_err = nullptr;
-    DX_HIP(dx_malloc(&d_err, 4));
+    DX_HIP(ds_malloc(&d_err, 4, st));
     DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
     DX_HIP(hipMemsetAsync(row, 0, 8, st));
     if (n)
@@ -896,21 +896,21 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     DX_TRY(dx_d2h(grid->ctx, &err, d_err, 4, st));
     DX_HIP(hipStreamSynchronize(st));
     if (err) {
-        dx_free(d_err);
+        ds_free(d_err, st);
         return set_error(err & 1 ? DCCRGX_ENOTFOUND : DCCRGX_EINTERNAL,
                          err & 1 ? "cell does not exist" : "neighbor more than one level apart");
     }
     if (ids) {
         uint64_t t = std::max<uint64_t>(*total, 1);
-        DX_HIP(dx_malloc(ids, t * 8));
-        DX_HIP(dx_malloc(off, t * 12));
-        DX_HIP(dx_malloc(gidx, t * 4));
+        DX_HIP(ds_malloc(ids, t * 8, st));
+        DX_HIP(ds_malloc(off, t * 12, st));
+        DX_HIP(ds_malloc(gidx, t * 4, st));
         if (n)
             hipLaunchKernelGGL(k_ex_nof_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, h.d_of_c, h.K,
                                cells, n, (const uint64_t*)row, *ids, *off, *gidx);
         DX_HIP(hipGetLastError());
     }
-    dx_free(d_err);
+    ds_free(d_err, st);
     return DCCRGX_OK;
 }
 
@@ -923,6 +923,21 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     DX_CHECK(n > 0 && n < (1ull << 32), DCCRGX_EINVAL, "leaf count %zu", n);
     PhaseTimer T("explicit_init");
     auto* E = new Explicit();
+    if (grid->spare_host) {  // the previous state's host arrays: their capacity is reused
+        Explicit* S = grid->spare_host;
+        E->leaves.swap(S->leaves);
+        E->local.swap(S->local);
+        E->local_g.swap(S->local_g);
+        E->owner.swap(S->owner);
+        E->slot_ids.swap(S->slot_ids);
+        E->slot_of_g.swap(S->slot_of_g);
+        E->dir.swap(S->dir);
+        E->local.clear();
+        E->local_g.clear();
+        E->slot_ids.clear();
+        delete S;
+        grid->spare_host = nullptr;
+    }
     grid->ex = E;
     E->leaves.assign(leaves, leaves + n);
     if (!std::is_sorted(E->leaves.begin(), E->leaves.end())) std::sort(E->leaves.begin(), E->leaves.end());
@@ -938,16 +953,16 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     const uint64_t nw = (grid->map.last_cell >> 6) + 1;
     if (nw <= (1ull << 26) && nw * 12 <= 16 * cap * 12) {
         E->nwords = nw;
-        DX_HIP(dx_malloc(&E->d_bits, nw * 8));
-        DX_HIP(dx_malloc(&E->d_rank, nw * 4));
+        DX_HIP(ds_malloc(&E->d_bits, nw * 8, st));
+        DX_HIP(ds_malloc(&E->d_rank, nw * 4, st));
         DX_HIP(hipMemsetAsync(E->d_bits, 0, nw * 8, st));
         hipLaunchKernelGGL(k_bits_set, dim3(grid_for(E->n)), dim3(256), 0, st, E->d_leaves, E->n,
                            (unsigned long long*)E->d_bits);
         hipLaunchKernelGGL(k_bits_rank, dim3(grid_for(nw)), dim3(256), 0, st, E->d_leaves, E->n, nw, E->d_rank);
     } else {
         E->mask = cap - 1;
-        DX_HIP(dx_malloc(&E->d_keys, cap * 8));
-        DX_HIP(dx_malloc(&E->d_vals, cap * 4));
+        DX_HIP(ds_malloc(&E->d_keys, cap * 8, st));
+        DX_HIP(ds_malloc(&E->d_vals, cap * 4, st));
         DX_HIP(hipMemsetAsync(E->d_keys, 0, cap * 8, st));
         hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(E->n)), dim3(256), 0, st, E->d_leaves, E->n,
                            (unsigned long long*)E->d_keys, E->d_vals, E->mask);
@@ -1136,18 +1151,32 @@ int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     return explicit_build_hood(grid, grid->hoods[h.id]);
 }
 
+void explicit_recycle(dccrgx_grid* grid, Explicit* E)
+{
+    if (!E) return;
+    auto* S = new Explicit();
+    S->leaves.swap(E->leaves);
+    S->local.swap(E->local);
+    S->local_g.swap(E->local_g);
+    S->owner.swap(E->owner);
+    S->slot_ids.swap(E->slot_ids);
+    S->slot_of_g.swap(E->slot_of_g);
+    S->dir.swap(E->dir);
+    explicit_free(E);
+    delete grid->spare_host;
+    grid->spare_host = S;
+}
+
 void explicit_free(Explicit* E)
 {
     if (!E) return;
+    FreeBatch fb;
     for (void* q : {(void*)E->d_leaves, (void*)E->d_keys, (void*)E->d_vals, (void*)E->d_bits, (void*)E->d_rank,
-                    (void*)E->d_local_g,
-                    (void*)E->d_level, (void*)E->d_slot_of_g, (void*)E->d_local_slot})
-        dx_free(q);
-    for (auto& kv : E->hl) {
-        dx_free(kv.second.d_inner_pos);
-        dx_free(kv.second.d_outer_pos);
-        dx_free(kv.second.d_all_pos);
-    }
+                    (void*)E->d_local_g, (void*)E->d_level, (void*)E->d_slot_of_g, (void*)E->d_local_slot})
+        fb.add(q);
+    for (auto& kv : E->hl)
+        for (void* q : {(void*)kv.second.d_inner_pos, (void*)kv.second.d_outer_pos, (void*)kv.second.d_all_pos})
+            fb.add(q);
     delete E;
 }
 
@@ -1163,6 +1192,8 @@ void explicit_destroy(dccrgx_grid* grid)
 {
     explicit_free(grid->ex);
     grid->ex = nullptr;
+    delete grid->spare_host;
+    grid->spare_host = nullptr;
 }
 
 // host copies of a neighborhood's device CSRs (neighbors_of / neighbors_to
@@ -1185,6 +1216,81 @@ int explicit_host_lists(const dccrgx_grid* grid, const Hood& h)
     DX_TRY(dx_d2h(ctx, L.h_nto_g.data(), h.d_nto_g, L.h_nto_g.size() * 4, st));
     L.host_valid = true;
     return DCCRGX_OK;
+}
+
+// the rows of leaves gs[]: row[i + 1] = neighbors_of + neighbors_to length,
+// alen[i] = neighbors_of length; then the rows concatenated (of, then to)
+__global__ void __launch_bounds__(256) k_rows_len(const uint32_t* __restrict__ gs, uint64_t n,
+                                                  const uint64_t* __restrict__ arow, const uint64_t* __restrict__ brow,
+                                                  uint64_t* __restrict__ row, uint64_t* __restrict__ alen)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t g = gs[i];
+        alen[i] = arow[g + 1] - arow[g];
+        row[i + 1] = alen[i] + (brow[g + 1] - brow[g]);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_rows_cat(const uint32_t* __restrict__ gs, uint64_t n,
+                                                  const uint64_t* __restrict__ arow, const uint32_t* __restrict__ aval,
+                                                  const uint64_t* __restrict__ brow, const uint32_t* __restrict__ bval,
+                                                  const uint64_t* __restrict__ row, uint32_t* __restrict__ out)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t g = gs[i];
+        uint64_t w = row[i];
+        for (uint64_t e = arow[g]; e < arow[g + 1]; e++) out[w++] = aval[e];
+        for (uint64_t e = brow[g]; e < brow[g + 1]; e++) out[w++] = bval[e];
+    }
+}
+
+int explicit_fetch_rows(const dccrgx_grid* grid, const Hood& h, const std::vector<uint32_t>& leaves)
+{
+    Explicit* E = grid->ex;
+    Explicit::HoodLists& L = E->hl[h.id];
+    if (L.host_valid) return DCCRGX_OK;  // the whole lists are on the host already
+    std::vector<uint32_t> want;
+    for (uint32_t g : leaves)
+        if (g < E->n && !L.row_at.count(g)) want.push_back(g);
+    std::sort(want.begin(), want.end());
+    want.erase(std::unique(want.begin(), want.end()), want.end());
+    if (want.empty()) return DCCRGX_OK;
+    Ctx* ctx = grid->ctx;
+    hipStream_t st = ctx->compute;
+    const uint64_t n = want.size();
+    uint32_t* d_g = nullptr;
+    uint64_t* d_row = nullptr;  // n + 1 row pointers, then n neighbors_of lengths
+    uint32_t* d_out = nullptr;
+    DX_HIP(hipMallocAsync((void**)&d_g, n * 4, st));
+    DX_HIP(hipMallocAsync((void**)&d_row, (2 * n + 1) * 8, st));
+    auto done = [&](int code) {
+        (void)hipFreeAsync(d_g, st);
+        (void)hipFreeAsync(d_row, st);
+        if (d_out) (void)hipFreeAsync(d_out, st);
+        return code;
+    };
+    int s = dx_h2d(ctx, d_g, want.data(), n * 4, st);
+    if (s != DCCRGX_OK) return done(s);
+    hipLaunchKernelGGL(k_rows_len, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)d_g, n, h.d_nof_row,
+                       h.d_nto_row, d_row, d_row + n + 1);
+    uint64_t total = 0;
+    if ((s = device_scan_rows(d_row, n, st, &total)) != DCCRGX_OK) return done(s);
+    if (hipMallocAsync((void**)&d_out, std::max<uint64_t>(total, 1) * 4, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "row cache"));
+    hipLaunchKernelGGL(k_rows_cat, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)d_g, n, h.d_nof_row,
+                       h.d_nof_g, h.d_nto_row, h.d_nto_g, (const uint64_t*)d_row, d_out);
+    std::vector<uint64_t> row(2 * n + 1);
+    if ((s = dx_d2h(ctx, row.data(), d_row, (2 * n + 1) * 8, st)) != DCCRGX_OK) return done(s);
+    const uint64_t base = L.row_vals.size();
+    L.row_vals.resize(base + total);
+    if ((s = dx_d2h(ctx, L.row_vals.data() + base, d_out, total * 4, st)) != DCCRGX_OK) return done(s);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t a = row[n + 1 + i];
+        L.row_at[want[i]] = {base + row[i], a, base + row[i] + a, row[i + 1] - row[i] - a};
+    }
+    return done(DCCRGX_OK);
 }
 
 int explicit_host_lists(const dccrgx_grid* grid, int32_t hood_id)
@@ -1212,24 +1318,24 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     const uint64_t N = E->n;
     h.n_rows = N;
     // neighbors_of of every leaf (the reference also builds all of them)
-    DX_HIP(dx_malloc(&h.d_nof_row, (N + 1) * 8));
+    DX_HIP(ds_malloc(&h.d_nof_row, (N + 1) * 8, st));
     uint64_t tot = 0;
     DX_TRY(nof_device(grid, h, E->d_leaves, N, h.d_nof_row, &h.d_nof_id, &h.d_nof_off, &h.d_nof_g, &tot, st));
     T.lap("neighbors_of");
     // neighbors_to = transpose (rows: leaves)
     uint32_t *d_cnt = nullptr, *d_cur = nullptr, *d_tmp = nullptr, *d_ucnt = nullptr;
-    DX_HIP(dx_malloc(&d_cnt, N * 4));
-    DX_HIP(dx_malloc(&d_cur, N * 4));
+    DX_HIP(ds_malloc(&d_cnt, N * 4, st));
+    DX_HIP(ds_malloc(&d_cur, N * 4, st));
     DX_HIP(hipMemsetAsync(d_cnt, 0, N * 4, st));
     DX_HIP(hipMemsetAsync(d_cur, 0, N * 4, st));
     hipLaunchKernelGGL(k_tr_count, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_cnt);
     uint64_t* d_trow = nullptr;
     uint64_t ttot = 0;
     DX_TRY(scan_counts_device(d_cnt, N, &d_trow, &ttot, st));
-    DX_HIP(dx_malloc(&d_tmp, std::max<uint64_t>(ttot, 1) * 4));
+    DX_HIP(ds_malloc(&d_tmp, std::max<uint64_t>(ttot, 1) * 4, st));
     hipLaunchKernelGGL(k_tr_scatter, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_trow,
                        d_cur, d_tmp);
-    DX_HIP(dx_malloc(&d_ucnt, N * 4));
+    DX_HIP(ds_malloc(&d_ucnt, N * 4, st));
     hipLaunchKernelGGL(k_sort_unique_rows64, dim3((unsigned)std::min<uint64_t>((N + 3) / 4, 16384)), dim3(256), 0, st,
                        d_trow, N, d_tmp, d_ucnt);
     hipLaunchKernelGGL(k_sort_unique_rows_wave, dim3((unsigned)std::min<uint64_t>(N, 4096)), dim3(64), 0, st, d_trow,
@@ -1238,15 +1344,15 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     DX_HIP(hipGetLastError());
     uint64_t ntot = 0;
     DX_TRY(scan_counts_device(d_ucnt, N, &h.d_nto_row, &ntot, st));
-    DX_HIP(dx_malloc(&h.d_nto_g, std::max<uint64_t>(ntot, 1) * 4));
+    DX_HIP(ds_malloc(&h.d_nto_g, std::max<uint64_t>(ntot, 1) * 4, st));
     hipLaunchKernelGGL(k_copy_rows_wave, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, d_trow, d_tmp, h.d_nto_row,
                        N, h.d_nto_g);
     DX_HIP(hipGetLastError());
-    dx_free(d_cnt);
-    dx_free(d_cur);
-    dx_free(d_tmp);
-    dx_free(d_ucnt);
-    dx_free(d_trow);
+    ds_free(d_cnt, st);
+    ds_free(d_cur, st);
+    ds_free(d_tmp, st);
+    ds_free(d_ucnt, st);
+    ds_free(d_trow, st);
 
     T.lap("neighbors_to");
     // per-rank bookkeeping from the device lists (dccrg.hpp:9131-9234, 8729-8891)
@@ -1305,7 +1411,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     uint32_t* d_pc = nullptr;
     uint64_t tmp_tot = 0;
     if (ctx->comm_size == 1) {  // every leaf is local, in leaf order: the rows are neighbors_of's
-        DX_HIP(dx_malloc(&d_tmp_row, (nl + 1) * 8));
+        DX_HIP(ds_malloc(&d_tmp_row, (nl + 1) * 8, st));
         DX_HIP(hipMemcpyAsync(d_tmp_row, h.d_nof_row, (nl + 1) * 8, hipMemcpyDeviceToDevice, st));
         tmp_tot = tot;
     } else {
@@ -1317,8 +1423,8 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
         DX_TRY(upload(grid->ctx, tmp_row, &d_tmp_row, st));
         tmp_tot = tmp_row[nl];
     }
-    DX_HIP(dx_malloc(&d_pairs, std::max<uint64_t>(tmp_tot, 1) * sizeof(Pair)));
-    DX_HIP(dx_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4));
+    DX_HIP(ds_malloc(&d_pairs, std::max<uint64_t>(tmp_tot, 1) * sizeof(Pair), st));
+    DX_HIP(ds_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4, st));
     if (nl) {
         hipLaunchKernelGGL(k_stencil_rows64, dim3((unsigned)std::min<uint64_t>((nl + 3) / 4, 16384)), dim3(256), 0, st,
                            h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
@@ -1329,16 +1435,16 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     }
     uint64_t stot = 0;
     DX_TRY(scan_counts_device(d_pc, nl, &h.d_st_row, &stot, st));
-    DX_HIP(dx_malloc(&h.d_st_slot, std::max<uint64_t>(stot, 1) * 4));
-    DX_HIP(dx_malloc(&h.d_st_off, std::max<uint64_t>(stot, 1) * 12));
+    DX_HIP(ds_malloc(&h.d_st_slot, std::max<uint64_t>(stot, 1) * 4, st));
+    DX_HIP(ds_malloc(&h.d_st_off, std::max<uint64_t>(stot, 1) * 12, st));
     if (nl)
         hipLaunchKernelGGL(k_stencil_slots_wave, dim3((unsigned)((nl + 63) / 64)), dim3(64), 0, st, d_tmp_row,
                            d_pairs, h.d_st_row, nl, E->d_slot_of_g, h.d_st_slot, h.d_st_off);
     DX_HIP(hipGetLastError());
     DX_HIP(hipStreamSynchronize(st));
-    dx_free(d_tmp_row);
-    dx_free(d_pairs);
-    dx_free(d_pc);
+    ds_free(d_tmp_row, st);
+    ds_free(d_pairs, st);
+    ds_free(d_pc, st);
 
     T.lap("stencil rows");
     struct Lap {

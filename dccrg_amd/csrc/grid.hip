@@ -273,24 +273,19 @@ static int upload(const std::vector<T>& v, T** d, hipStream_t st)
 
 void free_hood(Hood& h)
 {
-    dx_free(h.d_of_c);
-    dx_free(h.d_to_c);
-    dx_free(h.d_self_dst);
-    dx_free(h.d_self_src);
-    for (PeerPlan& p : h.peers) {
-        dx_free(p.d_send_slots);
-        dx_free(p.d_unpack_dst);
-        dx_free(p.d_unpack_src);
-        dx_free(p.d_send_buf);
-        dx_free(p.d_recv_buf);
-    }
+    FreeBatch fb;
+    for (void* p : {(void*)h.d_of_c, (void*)h.d_to_c, (void*)h.d_self_dst, (void*)h.d_self_src}) fb.add(p);
+    for (PeerPlan& p : h.peers)
+        for (void* q : {(void*)p.d_send_slots, (void*)p.d_unpack_dst, (void*)p.d_unpack_src, p.d_send_buf,
+                        p.d_recv_buf})
+            fb.add(q);
     h.d_of_c = h.d_to_c = nullptr;
     h.d_self_dst = h.d_self_src = nullptr;
     h.peers.clear();
     for (void* p : {(void*)h.d_nof_row, (void*)h.d_nof_id, (void*)h.d_nof_off, (void*)h.d_nof_g,
                     (void*)h.d_nto_row, (void*)h.d_nto_g, (void*)h.d_st_row, (void*)h.d_st_slot,
                     (void*)h.d_st_off})
-        dx_free(p);
+        fb.add(p);
     h.d_st_off = nullptr;
     h.d_nof_row = h.d_nof_id = h.d_nto_row = h.d_st_row = nullptr;
     h.d_nof_off = nullptr;
@@ -746,6 +741,7 @@ int dccrgx_grid_destroy(dccrgx_grid* grid)
     for (Field& f : grid->fields) dx_free(f.ptr);
     for (auto& b : grid->spare_bufs) dx_free(b.first);
     if (!grid->uniform) explicit_destroy(grid);
+    delete grid->spare_host;
     amr_destroy(grid);
     load_state_free(grid);
     hipEventDestroy(grid->t0);

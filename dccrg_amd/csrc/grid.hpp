@@ -5,6 +5,7 @@
 #include "flatset.hpp"
 #include "internal.hpp"
 
+#include <array>
 #include <set>
 #include <unordered_map>
 
@@ -156,6 +157,10 @@ struct Explicit {
         bool host_valid = false;
         std::vector<uint64_t> h_nof_row, h_nto_row;
         std::vector<uint32_t> h_nof_g, h_nto_g;
+        // single rows fetched for the refinement decisions (explicit_fetch_rows):
+        // leaf -> (neighbors_of offset, length, neighbors_to offset, length) in vals
+        std::unordered_map<uint32_t, std::array<uint64_t, 4>> row_at;
+        std::vector<uint32_t> row_vals;
         std::vector<uint32_t> inner_pos, outer_pos;  // positions in `local`
         uint32_t* d_inner_pos = nullptr;
         uint32_t* d_outer_pos = nullptr;
@@ -293,6 +298,10 @@ struct dccrgx_grid {
     dccrgx::LoadState* load = nullptr;
     // device buffers kept for reuse by the next AMR rebuild (ptr, bytes)
     std::vector<std::pair<void*, size_t>> spare_bufs;
+    // host arrays of the previous explicit state, reused by the next rebuild
+    // (their capacity: an adaptive run rebuilds every step at similar sizes,
+    // and fresh multi-MB vectors cost page faults)
+    dccrgx::Explicit* spare_host = nullptr;
     // SFC placement (params.partition): owner of each level-0 cell, id - 1
     std::vector<int32_t> sfc_owner;
     // kernel timing (dccrgx_kernel_timer)
@@ -334,6 +343,8 @@ int explicit_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, in
 int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n);
 void explicit_destroy(dccrgx_grid* grid);
 void explicit_free(Explicit* E);
+// free E's device memory and keep its host arrays for the next explicit_init
+void explicit_recycle(dccrgx_grid* grid, Explicit* E);
 void explicit_clear_retired(Explicit* E);
 // explicit grids: give `ids` (leaves or retired cells) storage slots if they
 // have none, growing every field unless a rebuild defers that
@@ -346,6 +357,9 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h);
 // host copies of a neighborhood's neighbor lists, fetched once per build
 int explicit_host_lists(const dccrgx_grid* grid, const Hood& h);
 int explicit_host_lists(const dccrgx_grid* grid, int32_t hood_id);
+// the neighbors_of / neighbors_to rows of the given leaves (global indices)
+// copied to the host row cache of the neighborhood, one gather for all
+int explicit_fetch_rows(const dccrgx_grid* grid, const Hood& h, const std::vector<uint32_t>& leaves);
 int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, uint64_t* ids,
                        size_t cap, size_t* n);
 int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device);

@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -78,6 +79,40 @@ inline hipError_t dx_free(void* p)
     return e;
 }
 
+// Frees of many buffers after one wait for the device (structures are
+// released together: a neighborhood, an explicit grid's state)
+struct FreeBatch {
+    std::vector<void*> v;
+    void add(void* p)
+    {
+        if (p) v.push_back(p);
+    }
+    ~FreeBatch()
+    {
+        if (v.empty() || hipDeviceSynchronize() != hipSuccess) return;
+        for (void* p : v) (void)hipFreeAsync(p, nullptr);
+    }
+};
+
+// Stream-ordered allocation for structures built on one stream (neighbor
+// lists, scratch of a build): no synchronisation -- the memory is valid for
+// work queued on `st` after the call, and a ds_free on `st` returns it once
+// the work queued before it is done.  Such memory may later be released
+// with dx_free.
+template <class T>
+inline hipError_t ds_malloc(T** p, size_t bytes, hipStream_t st)
+{
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(p), bytes ? bytes : 1, st);
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        dx_trim_pool();
+        e = hipMallocAsync(reinterpret_cast<void**>(p), bytes ? bytes : 1, st);
+    }
+    return e;
+}
+
+inline hipError_t ds_free(void* p, hipStream_t st) { return p ? hipFreeAsync(p, st) : hipSuccess; }
+
 #define DX_TRY(expr)                       \
     do {                                   \
         int s_ = (expr);                   \
@@ -130,33 +165,27 @@ inline int64_t getenv_int(const char* name, int64_t dflt)
 // (AMR request filtering): [0, n) in contiguous ranges of at least `grain`
 // items over up to DCCRGX_HOST_THREADS (else OMP_NUM_THREADS, else the
 // hardware's count) threads, capped at 16.  f(begin, end) must only read
-// shared state and write disjoint outputs.
+// shared state and write disjoint outputs.  The worker threads persist
+// between calls (an adaptive run calls this every step; starting 16 threads
+// costs more than the work).
 // ---------------------------------------------------------------------------
+size_t host_threads();
+// run job(t) for t in [0, nt) on the pool (t = 0 on the calling thread)
+void pool_run(size_t nt, const std::function<void(size_t)>& job);
+
 template <class F>
 void parallel_ranges(size_t n, size_t grain, F&& f)
 {
-    size_t nt = 0;
-    for (const char* var : {"DCCRGX_HOST_THREADS", "OMP_NUM_THREADS"}) {
-        const char* e = std::getenv(var);
-        if (e && std::atoi(e) > 0) {
-            nt = (size_t)std::atoi(e);
-            break;
-        }
-    }
-    if (!nt) nt = std::max(1u, std::thread::hardware_concurrency());
-    nt = std::min<size_t>({nt, 16, (n + grain - 1) / std::max<size_t>(grain, 1)});
+    const size_t nt = std::min<size_t>(host_threads(), (n + grain - 1) / std::max<size_t>(grain, 1));
     if (nt <= 1) {
         f((size_t)0, n);
         return;
     }
-    std::vector<std::thread> th;
     const size_t per = (n + nt - 1) / nt;
-    for (size_t t = 1; t < nt; t++) {
+    pool_run(nt, [&](size_t t) {
         const size_t b = std::min(n, t * per), e = std::min(n, b + per);
-        if (b < e) th.emplace_back([&f, b, e] { f(b, e); });
-    }
-    f((size_t)0, std::min(n, per));
-    for (auto& t : th) t.join();
+        if (b < e) f(b, e);
+    });
 }
 
 // ---------------------------------------------------------------------------
