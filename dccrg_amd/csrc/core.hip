@@ -164,46 +164,12 @@ __global__ void __launch_bounds__(256) k_ids_to_indices(MapParams p, const uint6
     }
 }
 
-// Same results, block-contiguous: a block maps 256 consecutive ids, stages
-// the (x, y, z) triples in LDS and writes them back as one contiguous run of
-// 16-byte non-temporal stores (the triples are 24 B apart, so per-lane
-// stores of k_ids_to_indices only fill a third of each wave's store span).
-__global__ void __launch_bounds__(256) k_ids_to_indices_v(MapParams p, const uint64_t* __restrict__ ids,
-                                                          size_t n, uint64_t* __restrict__ idx3,
-                                                          int32_t* __restrict__ lvl)
-{
-    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-    __shared__ uint64_t s[3 * 256];
-    for (size_t base = (size_t)blockIdx.x * 256; base < n; base += (size_t)gridDim.x * 256) {
-        const size_t i = base + threadIdx.x;
-        uint64_t o[3] = {0, 0, 0};
-        int l = -1;
-        if (i < n) {
-            map_indices(p, __builtin_nontemporal_load(ids + i), o, &l);
-            if (lvl) __builtin_nontemporal_store(l, lvl + i);
-        }
-        s[3 * threadIdx.x + 0] = o[0];
-        s[3 * threadIdx.x + 1] = o[1];
-        s[3 * threadIdx.x + 2] = o[2];
-        __syncthreads();
-        const size_t cnt = 3 * (n - base < 256 ? n - base : 256);
-        if (cnt == 3 * 256) {
-            u64x2* dst = (u64x2*)(idx3 + 3 * base);
-            for (int k = threadIdx.x; k < 3 * 128; k += 256) {
-                const u64x2 v = {s[2 * k], s[2 * k + 1]};
-                __builtin_nontemporal_store(v, dst + k);
-            }
-        } else {
-            for (size_t k = threadIdx.x; k < cnt; k += 256) idx3[3 * base + k] = s[k];
-        }
-        __syncthreads();
-    }
-}
-
-// The same with U ids per lane per pass: the U loads of a lane are issued
-// together (k_ids_to_indices_v keeps one 8-B load per lane in flight, which
-// leaves HBM under-subscribed), the 3*256*U triples are staged in LDS and
-// leave as one contiguous run of 16-B non-temporal stores.
+// Same results, block-contiguous, U ids per lane per pass: the U loads of a
+// lane are issued together, the 3*256*U (x, y, z) triples are staged in LDS
+// and leave as one contiguous run of 16-byte non-temporal stores (the triples
+// are 24 B apart, so per-lane stores of k_ids_to_indices only fill a third of
+// each wave's store span).  U = 2 won the sweep over U = 1, 4, 8
+// (profiles/r2_map_variant_sweep.log); k_ids_to_indices takes unaligned outputs.
 template <int U>
 __global__ void __launch_bounds__(256) k_ids_to_indices_u(MapParams p, const uint64_t* __restrict__ ids,
                                                           size_t n, uint64_t* __restrict__ idx3,
@@ -326,23 +292,12 @@ int dccrgx_map_ids_to_indices(const dccrgx_mapping* map, const uint64_t* ids, si
     DX_TRY(make_map_params(map, &p));
     if (n == 0) return DCCRGX_OK;
     DX_CHECK(ids, DCCRGX_EINVAL, "null ids");
-    const int64_t mv = getenv_int("DCCRGX_MAP_VARIANT", 2);  // ids per lane per pass (1: k_ids_to_indices_v)
-    if (idx3 && ((uintptr_t)idx3 & 15) == 0 && (mv == 2 || mv == 4 || mv == 8)) {
-        const size_t per = 256 * (size_t)mv;
+    if (idx3 && ((uintptr_t)idx3 & 15) == 0) {
+        constexpr size_t per = 256 * 2;
         const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>((n + per - 1) / per, 256 * 8));
-        if (mv == 2)
-            hipLaunchKernelGGL(k_ids_to_indices_u<2>, dim3(g), dim3(256), 0, (hipStream_t)stream, p, ids, n, idx3,
-                               lvl);
-        else if (mv == 4)
-            hipLaunchKernelGGL(k_ids_to_indices_u<4>, dim3(g), dim3(256), 0, (hipStream_t)stream, p, ids, n, idx3,
-                               lvl);
-        else
-            hipLaunchKernelGGL(k_ids_to_indices_u<8>, dim3(g), dim3(256), 0, (hipStream_t)stream, p, ids, n, idx3,
-                               lvl);
-    } else if (idx3 && ((uintptr_t)idx3 & 15) == 0)
-        hipLaunchKernelGGL(k_ids_to_indices_v, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, ids, n,
-                           idx3, lvl);
-    else
+        hipLaunchKernelGGL(k_ids_to_indices_u<2>, dim3(g), dim3(256), 0, (hipStream_t)stream, p, ids, n, idx3,
+                           lvl);
+    } else
         hipLaunchKernelGGL(k_ids_to_indices, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, ids, n,
                            idx3, lvl);
     DX_HIP(hipGetLastError());

@@ -147,7 +147,7 @@ struct PhaseTimer {
     }
 };
 
-// variant switches for kernel sweeps (DCCRGX_GOL_VARIANT, DCCRGX_MAP_VARIANT, ...)
+// test hooks and tuning knobs read from the environment (DCCRGX_GOL_CHUNK, ...)
 inline bool getenv_flag(const char* name)
 {
     const char* v = std::getenv(name);
