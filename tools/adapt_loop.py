@@ -1,0 +1,40 @@
+"""configs[2]'s adaptive loop alone (for rocprofv3 and phase timing): the
+pre-refined 400x400x1 grid of tests/advection/2d.cpp, then ADAPT_STEPS steps
+of bench.py's loop (b): ghost update, check_for_adaptation, solve, adapt_grid,
+max_time_step.  Prints ms per step."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import dccrg_amd as D  # noqa: E402
+from dccrg_amd import advection as A  # noqa: E402
+
+ctx = D.Context(0, 0, 1)
+rel, thr, sens, cfl, M = 0.025, 0.25, 0.5, 0.5, 2
+g = (D.Dccrg().set_initial_length((400, 400, 1)).set_maximum_refinement_level(M)
+     .set_periodic(True, True, False).set_neighborhood_length(0).initialize(ctx))
+g.add_advection_fields()
+geom = A.geometry_2d(g)
+A.initialize(g, geom)
+for _ in range(M):
+    A.adapt_grid(g, geom, *A.check_for_adaptation(g, rel / M, thr, sens))
+    A.initialize(g, geom)
+dt = g.max_time_step()
+g.update_copies_of_remote_neighbors(fields=list(A.ALL))
+steps = int(os.environ.get("ADAPT_STEPS", "20"))
+per = []
+for _ in range(steps):
+    t0 = time.perf_counter()
+    g.update_copies_of_remote_neighbors(fields=["density"])
+    sets = A.check_for_adaptation(g, rel / M, thr, sens)
+    g.advect_step(cfl * dt)
+    A.adapt_grid(g, geom, *sets)
+    dt = g.max_time_step()
+    per.append((time.perf_counter() - t0) * 1e3)
+ctx.synchronize()
+print("ms/step " + " ".join(f"{x:.2f}" for x in per), flush=True)
+print(f"leaves {g.n_local} mean of last {max(steps - 4, 1)}: "
+      f"{sum(per[4:]) / max(len(per[4:]), 1):.2f} ms", flush=True)
+g.close()
+ctx.close()
