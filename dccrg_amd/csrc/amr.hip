@@ -244,6 +244,16 @@ Amr& amr_of(dccrgx_grid* grid)
     return *grid->amr;
 }
 
+// the host sets, up to date, for a single request call that changes them
+int host_sets(dccrgx_grid* grid, Amr** out)
+{
+    Amr& A = amr_of(grid);
+    DX_TRY(amr_host_sync(grid));
+    A.dev_current = false;
+    *out = &A;
+    return DCCRGX_OK;
+}
+
 __global__ void __launch_bounds__(256) k_level0_ids(uint64_t* __restrict__ out, uint64_t n)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -256,13 +266,20 @@ __global__ void __launch_bounds__(256) k_level0_ids(uint64_t* __restrict__ out, 
 // and keep their old data.  Transactional: the new state and every new field
 // array are built first; on any failure they are freed and the old grid is
 // left exactly as it was.
-int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired)
+int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired,
+            uint64_t* d_leaves = nullptr)
 {
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
-    for (const Field& F : grid->fields)
-        DX_CHECK(!F.variable, DCCRGX_EINVAL, "refinement of grids with variable-size fields is not supported");
-    for (auto& kv : grid->hoods) DX_CHECK(!kv.second.pending, DCCRGX_ESTATE, "a halo update is in progress");
+    bool variable = false, pending = false;
+    for (const Field& F : grid->fields) variable |= F.variable;
+    for (auto& kv : grid->hoods) pending |= kv.second.pending;
+    if (variable || pending) {
+        ds_free(d_leaves, st);
+        return set_error(variable ? DCCRGX_EINVAL : DCCRGX_ESTATE, "%s",
+                         variable ? "refinement of grids with variable-size fields is not supported"
+                                  : "a halo update is in progress");
+    }
     DX_HIP(hipStreamSynchronize(st));
     DX_HIP(hipStreamSynchronize(ctx->comm));
 
@@ -303,7 +320,7 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     PhaseTimer T("rebuild");
     grid->ex = nullptr;
     grid->uniform = false;
-    int s = explicit_init(grid, leaves.data(), leaves.size());
+    int s = explicit_init(grid, leaves.data(), leaves.size(), d_leaves);  // adopts d_leaves
     T.lap("explicit_init");
     if (s == DCCRGX_OK) grid->ex->defer_fields = true;
     for (auto it = grid->hoods.begin(); s == DCCRGX_OK && it != grid->hoods.end(); ++it)
@@ -381,6 +398,7 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     for (auto& kv : old_hoods) free_hood(kv.second);
     explicit_recycle(grid, old.ex);
     old.ex = nullptr;
+    if (grid->amr) grid->amr->dev_current = false;  // request flags were over the old leaves
     T.lap("fields moved");
     return DCCRGX_OK;
 }
@@ -397,11 +415,12 @@ static int check_explicit_memory(const dccrgx_grid* grid, uint64_t N)
         const double K = (double)(kv.second.items.size() / 3);
         need += (double)N * (16 + K * (8 + 12 + 4 + 4));  // rows, neighbors_of (+ transpose)
     }
-    // memory the pool keeps for reuse is free for this purpose: trim it, and
-    // count the spare field buffers of earlier rebuilds as available
-    dx_trim_pool();
+    // memory the pool keeps for reuse and the spare field buffers of earlier
+    // rebuilds are free for this purpose
+    DX_HIP(hipDeviceSynchronize());
     size_t free_b = 0, total_b = 0;
     DX_HIP(hipMemGetInfo(&free_b, &total_b));
+    free_b += dx_pool_idle_bytes();
     for (const auto& b : grid->spare_bufs) free_b += b.second;
     DX_CHECK(need < 0.9 * (double)free_b, DCCRGX_ENOMEM,
              "refining a uniform grid of %llu cells needs ~%.1f GB of replicated leaf state and neighbor lists; "
@@ -457,14 +476,18 @@ int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
         if (map_level(grid->map, cell) != 0 || cell > grid->g.N ||
             part_owner(grid->g.part, cell) != grid->ctx->rank)
             return DCCRGX_OK;
-        Amr& A = amr_of(grid);
+        Amr* Ap = nullptr;
+        DX_TRY(host_sets(grid, &Ap));
+        Amr& A = *Ap;
         if (A.not_to_refine.count(cell)) return DCCRGX_OK;
         A.to_refine.insert(cell);
         *result = 1;
         return DCCRGX_OK;
     }
     const View v{grid, grid->ex, grid->map.max_lvl};
-    Amr& A = amr_of(grid);
+    Amr* Ap = nullptr;
+    DX_TRY(host_sets(grid, &Ap));
+    Amr& A = *Ap;
     // dccrg.hpp:2476-2546
     if (!v.exists(cell) || !v.local(cell)) return DCCRGX_OK;
     const int lvl = v.level(cell);
@@ -502,7 +525,9 @@ int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result
         return DCCRGX_OK;
     }
     const View v{grid, grid->ex, grid->map.max_lvl};
-    Amr& A = amr_of(grid);
+    Amr* Ap = nullptr;
+    DX_TRY(host_sets(grid, &Ap));
+    Amr& A = *Ap;
     // dccrg.hpp:2596-2675
     if (!v.exists(cell) || !v.local(cell)) return DCCRGX_OK;
     *result = 1;
@@ -545,7 +570,9 @@ int dccrgx_dont_unrefine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
         return DCCRGX_OK;
     }
     const View v{grid, grid->ex, grid->map.max_lvl};
-    Amr& A = amr_of(grid);
+    Amr* Ap = nullptr;
+    DX_TRY(host_sets(grid, &Ap));
+    Amr& A = *Ap;
     // dccrg.hpp:2715-2759
     if (!v.exists(cell)) return DCCRGX_OK;
     *result = 1;
@@ -573,7 +600,9 @@ int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
     // dccrg.hpp:2782-2805
     *result = 1;
     if (lvl == grid->map.max_lvl) return DCCRGX_OK;
-    Amr& A = amr_of(grid);
+    Amr* Ap = nullptr;
+    DX_TRY(host_sets(grid, &Ap));
+    Amr& A = *Ap;
     A.to_refine.erase(cell);
     A.not_to_refine.insert(cell);
     return DCCRGX_OK;
@@ -582,8 +611,10 @@ int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 int dccrgx_amr_request_cells(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results)
 {
     DX_CHECK(grid && (ids || !n) && kind >= 0 && kind < 4, DCCRGX_EINVAL, "bad argument");
-    if (kind == DCCRGX_AMR_REFINE && !grid->uniform && n > 1)  // the rows refine_completely reads, in one gather
-        DX_TRY((View{grid, grid->ex, grid->map.max_lvl}.prefetch(ids, n)));
+    if (!grid->uniform) {  // the batch on the device (amr_dev.hip), results as the calls in this order
+        amr_of(grid);
+        return amr_dev_requests(grid, kind, ids, n, results);
+    }
     for (size_t i = 0; i < n; i++) {
         int32_t r = 0;
         switch (kind) {
@@ -602,6 +633,7 @@ int dccrgx_amr_requests(const dccrgx_grid* grid, int32_t which, uint64_t* ids, s
     DX_CHECK(grid && n && which >= 0 && which < 4, DCCRGX_EINVAL, "bad argument");
     *n = 0;
     if (!grid->amr) return DCCRGX_OK;
+    DX_TRY(amr_host_sync(const_cast<dccrgx_grid*>(grid)));
     const Amr& A = *grid->amr;
     const FlatSet& s = which == DCCRGX_AMR_REFINE       ? A.to_refine
                                   : which == DCCRGX_AMR_DONT_REFINE ? A.not_to_refine
@@ -617,231 +649,72 @@ int dccrgx_amr_requests(const dccrgx_grid* grid, int32_t which, uint64_t* ids, s
 
 int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const size_t* counts, size_t* n_new)
 {
-    DX_CHECK(grid && sets && counts, DCCRGX_EINVAL, "null argument");
-    for (int k = 0; k < 4; k++) DX_CHECK(sets[k] || !counts[k], DCCRGX_EINVAL, "null request set %d", k);
+    DX_CHECK(grid && (!sets || counts), DCCRGX_EINVAL, "null argument");
+    if (sets)
+        for (int k = 0; k < 4; k++) DX_CHECK(sets[k] || !counts[k], DCCRGX_EINVAL, "null request set %d", k);
     Amr& A = amr_of(grid);
     A.new_cells.clear();
     A.removed.clear();
     if (n_new) *n_new = 0;
     PhaseTimer T("stop_refining");
-    FlatSet R(sets[0], sets[0] + counts[0]), NR(sets[1], sets[1] + counts[1]);
-    FlatSet U(sets[2], sets[2] + counts[2]), NU(sets[3], sets[3] + counts[3]);
-    if (grid->uniform && R.empty() && U.empty()) {
-        // nothing can change; on a level-0 grid the dont_refine closure is the
-        // set itself, and it persists (:10188)
-        A.to_refine.clear();
-        A.to_unrefine.clear();
-        A.not_to_unrefine.clear();
-        A.not_to_refine = NR;
-        return DCCRGX_OK;
+    if (sets) {  // the union of every rank's requests (dccrg.hpp:10130-10236 gathers them)
+        A.to_refine = FlatSet(sets[0], sets[0] + counts[0]);
+        A.not_to_refine = FlatSet(sets[1], sets[1] + counts[1]);
+        A.to_unrefine = FlatSet(sets[2], sets[2] + counts[2]);
+        A.not_to_unrefine = FlatSet(sets[3], sets[3] + counts[3]);
+        A.host_current = true;
+        A.dev_current = false;
     }
-    DX_TRY(ensure_explicit(grid));
-    const View v{grid, grid->ex, grid->map.max_lvl};
-
-    // override_refines, dccrg.hpp:10130-10236: dont_refine spreads to every
-    // finer cell among the neighbors of a dont_refine cell, transitively
-    FlatSet donts;
-    std::vector<uint64_t> frontier;
-    for (uint64_t c : NR)
-        if (donts.insert(c).second) frontier.push_back(c);
-    while (!frontier.empty()) {
-        std::vector<uint64_t> next;
-        DX_TRY(v.prefetch(frontier.data(), frontier.size()));
-        for (uint64_t c : frontier) {
-            if (!v.exists(c)) continue;
-            const int cl = v.level(c);
-            auto spread = [&](uint64_t n) {
-                if (v.level(n) > cl && donts.insert(n).second) next.push_back(n);
-            };
-            v.for_nof(c, spread);
-            v.for_nto(c, spread);
+    if (grid->uniform) {  // requests of a uniform grid live on the host (amr_dev.hip: explicit grids)
+        if (A.to_refine.empty() && A.to_unrefine.empty()) {
+            // nothing can change; on a level-0 grid the dont_refine closure is
+            // the set itself, and it persists (:10188)
+            A.to_refine.clear();
+            A.not_to_unrefine.clear();
+            return DCCRGX_OK;
         }
-        frontier.swap(next);
+        DX_TRY(ensure_explicit(grid));
     }
-    for (uint64_t c : donts) R.erase(c);
-    T.lap("override_refines");
-
-    // induce_refines, dccrg.hpp:9730-9907: every coarser neighbor (of / to)
-    // of a refined cell is refined, transitively
-    frontier = R.sorted();
-    while (!frontier.empty()) {
-        std::vector<uint64_t> next;
-        DX_TRY(v.prefetch(frontier.data(), frontier.size()));
-        for (uint64_t r : frontier) {
-            const int rl = v.level(r);
-            auto induce = [&](uint64_t n) {
-                if (v.level(n) < rl && R.insert(n).second) next.push_back(n);
-            };
-            v.for_nof(r, induce);
-            v.for_nto(r, induce);
-        }
-        frontier.swap(next);
-    }
-
-    T.lap("induce_refines");
-    // override_unrefines, dccrg.hpp:9935-10124.  The reference's walk visits
-    // the closure of u's face neighbors under "face neighbor that is a
-    // neighbor of u's parent" (a non-neighbor is marked processed and never
-    // entered, a fixed property of the cell), and u is dropped if any visited
-    // cell is finer than u or of u's size and about to be refined: an
-    // existence test over that closure, independent of the visiting order.
-    // Requests are independent and only read R, NU and the leaf set.  The
-    // outcome depends on u only through its parent: the sibling test reads
-    // the parent's children, and the walk's closure is the same from every
-    // sibling -- the siblings of a requested u are leaves (unrefine_completely
-    // refuses u otherwise, :2617-2628, against the same leaf set), face
-    // adjacent inside the parent and neighbors of it, so a walk from any one
-    // reaches all of them and their faces; the face neighbors of u it starts
-    // from are neighbors of the parent.  So the walk runs once per parent,
-    // the parents split over host threads, each with its own memo of the
-    // face graph.
-    FlatSet final_un;
-    {
-        const std::vector<uint64_t> Uv = U.sorted();
-        std::vector<uint64_t> par(Uv.size());
-        for (size_t i = 0; i < Uv.size(); i++) par[i] = v.parent(Uv[i]);
-        // (parent, requested child): one per parent whose children are all
-        // leaves; a request set not filtered by unrefine_completely keeps one
-        // walk per child
-        std::vector<std::pair<uint64_t, uint64_t>> pu;
-        pu.reserve(Uv.size());
-        for (size_t i = 0; i < Uv.size(); i++) pu.emplace_back(par[i], Uv[i]);
-        std::sort(pu.begin(), pu.end());
-        auto all_leaves = [&](uint64_t p) {
-            uint64_t ch[8];
-            v.children(p, ch);
-            for (uint64_t c : ch)
-                if (c && !v.exists(c)) return false;
-            return true;
-        };
-        {
-            size_t w = 0;
-            for (size_t i = 0; i < pu.size(); i++) {
-                if (w && pu[w - 1].first == pu[i].first && all_leaves(pu[i].first)) continue;
-                pu[w++] = pu[i];
-            }
-            pu.resize(w);
-        }
-        std::vector<uint8_t> keep(pu.size(), 0);
-        auto work = [&](size_t b, size_t e) {
-            std::unordered_map<uint64_t, std::array<uint64_t, 6>> memo;
-            auto face = [&](uint64_t c) -> const std::array<uint64_t, 6>& {
-                auto it = memo.find(c);
-                if (it != memo.end()) return it->second;
-                std::array<uint64_t, 6> f;
-                v.face(c, f.data());
-                return memo.emplace(c, f).first->second;
-            };
-            std::unordered_set<uint64_t> seen;  // processed or queued
-            std::vector<uint64_t> queue;
-            for (size_t i = b; i < e; i++) {
-                const uint64_t parent = pu[i].first, u = pu[i].second;
-                uint64_t sib[8];
-                v.children(parent, sib);
-                bool can = true;
-                for (uint64_t s : sib)
-                    if (s && (R.count(s) || NU.count(s))) can = false;
-                if (!can) continue;
-                const int ul = v.level(u);
-                seen.clear();
-                queue.clear();
-                for (uint64_t x : face(u))
-                    if (x && seen.insert(x).second) queue.push_back(x);
-                for (size_t q = 0; q < queue.size() && can; q++) {
-                    const uint64_t next = queue[q];
-                    const int rl = v.level(next);
-                    if (rl > ul || (rl == ul && R.count(next))) {
-                        can = false;
-                        break;
-                    }
-                    const std::array<uint64_t, 6> f6 = face(next);
-                    for (uint64_t x : f6) {
-                        if (!x || !seen.insert(x).second) continue;
-                        if (v.is_neighbor(parent, x)) queue.push_back(x);
-                    }
-                }
-                keep[i] = can ? 1 : 0;
-            }
-        };
-        parallel_ranges(pu.size(), 64, work);
-        FlatSet ok_parent, split;  // split: parents walked per child
-        for (size_t i = 0; i + 1 < pu.size(); i++)
-            if (pu[i].first == pu[i + 1].first) split.insert(pu[i].first);
-        for (size_t i = 0; i < pu.size(); i++) {
-            if (!keep[i]) continue;
-            if (split.count(pu[i].first)) final_un.insert(pu[i].second);
-            else ok_parent.insert(pu[i].first);
-        }
-        for (size_t i = 0; i < Uv.size(); i++)
-            if (ok_parent.count(par[i])) final_un.insert(Uv[i]);
-    }
-
-    T.lap("override_unrefines");
-    // execute_refines, dccrg.hpp:10243-10693
-    const Explicit* E = grid->ex;
-    FlatSet gone;
-    gone.reserve(2 * R.size() + 8 * final_un.size());
-    std::vector<uint64_t> added, retired;
-    for (uint64_t r : R) {
-        uint64_t ch[8];
-        v.children(r, ch);
-        gone.insert(r);
-        added.insert(added.end(), ch, ch + 8);
-        if (v.local(r)) {
-            A.new_cells.insert(A.new_cells.end(), ch, ch + 8);
-            retired.push_back(r);
-        }
-    }
-    FlatSet parents;
-    for (uint64_t u : final_un) {
-        const uint64_t p = v.parent(u);
-        if (!parents.insert(p).second) continue;
-        uint64_t ch[8];
-        v.children(p, ch);
-        for (uint64_t c : ch) {
-            gone.insert(c);
-            if (v.local(c)) {  // the parent is local too (same level-0 ancestor)
-                A.removed.push_back(c);
-                retired.push_back(c);
-            }
-        }
-        added.push_back(p);
-    }
-    // surviving leaves (already ascending) merged with the added cells
-    std::vector<uint8_t> gone_flag(E->leaves.size(), 0);
-    for (uint64_t c : gone) {
-        const int64_t g = v.gidx(c);
-        if (g >= 0) gone_flag[g] = 1;
-    }
-    std::vector<uint64_t> kept;
-    kept.reserve(E->leaves.size());
-    for (size_t k = 0; k < E->leaves.size(); k++)
-        if (!gone_flag[k]) kept.push_back(E->leaves[k]);
-    T.lap("new leaf set: collect");
-    radix_sort_u64(added);
-    added.erase(std::unique(added.begin(), added.end()), added.end());
-    std::vector<uint64_t> leaves(kept.size() + added.size());
-    leaves.erase(std::set_union(kept.begin(), kept.end(), added.begin(), added.end(), leaves.begin()), leaves.end());
-    radix_sort_u64(retired);
-    radix_sort_u64(A.new_cells);
-    radix_sort_u64(A.removed);
-    T.lap("new leaf set");
-    if (!R.empty() || !final_un.empty()) {
+    // override_refines (:10130-10236), induce_refines (:9730-9907),
+    // override_unrefines (:9935-10124) and the new leaf set of
+    // execute_refines (:10243-10693), on the device
+    uint64_t* d_leaves = nullptr;
+    uint64_t n_leaves = 0;
+    std::vector<uint64_t> leaves, retired, nr;
+    bool changed = false;
+    // the request flags before the decisions: restored if the rebuild fails,
+    // so the requests stay pending
+    DX_TRY(amr_dev_sync(grid));
+    hipStream_t st = grid->ctx->compute;
+    uint32_t* d_saved = nullptr;
+    DX_HIP(ds_malloc(&d_saved, std::max<uint64_t>(A.flags_n, 1) * 4, st));
+    DX_HIP(hipMemcpyAsync(d_saved, A.d_flags, A.flags_n * 4, hipMemcpyDeviceToDevice, st));
+    auto restore = [&](int code) {
+        (void)hipMemcpyAsync(A.d_flags, d_saved, A.flags_n * 4, hipMemcpyDeviceToDevice, st);
+        ds_free(d_saved, st);
+        A.dev_current = true;
+        A.new_cells.clear();
+        A.removed.clear();
+        return code;
+    };
+    int s = amr_dev_decide(grid, &d_leaves, &n_leaves, leaves, retired, nr, &changed);
+    if (s != DCCRGX_OK) return restore(s);
+    T.lap("decisions");
+    if (changed) {
         // the previous round's refined / unrefined data goes first, as in
         // execute_refines (dccrg.hpp:10266-10267)
-        if (grid->ex) explicit_clear_retired(grid->ex);
-        const int s = rebuild(grid, leaves, retired);  // transactional: on failure the grid is unchanged
-        if (s != DCCRGX_OK) {  // requests stay pending, nothing was created or removed
-            A.new_cells.clear();
-            A.removed.clear();
-            return s;
-        }
+        explicit_clear_retired(grid->ex);
+        s = rebuild(grid, leaves, retired, d_leaves);  // transactional: on failure the grid is unchanged
+        if (s != DCCRGX_OK) return restore(s);
     }
-    // the dont_refine closure persists (:10188), everything else is consumed
+    ds_free(d_saved, st);
+    // the dont_refine closure persists (:10178), everything else is consumed
     A.to_refine.clear();
     A.to_unrefine.clear();
     A.not_to_unrefine.clear();
-    A.not_to_refine = donts;
+    A.not_to_refine = FlatSet(nr.data(), nr.data() + nr.size());
+    A.host_current = true;
+    A.dev_current = false;
     T.lap("rebuild");
     if (n_new) *n_new = A.new_cells.size();
     return DCCRGX_OK;

@@ -1,0 +1,1022 @@
+// amr_dev.hip -- the refinement requests and the decisions of stop_refining on
+// the device, for grids with the explicit (mixed-level) layout.
+//
+// The reference keeps four per-rank id sets (cells_to_refine,
+// cells_not_to_refine, cells_to_unrefine, cells_not_to_unrefine,
+// dccrg.hpp:7355-7360) and walks neighbor lists on the host for every request
+// (:2456-2806) and every decision pass (:9730-10240).  Here the sets of an
+// explicit grid are bit flags over the replicated leaf list (one u32 per
+// leaf), and each phase is a batch of independent per-cell kernels over the
+// device neighbor CSRs:
+//   - requests (refine_completely, dont_unrefine, unrefine_completely,
+//     dont_refine) of a whole id array at once.  Their outcome within a batch
+//     does not depend on the order of the calls except through "a sibling is
+//     already recorded" (dont_unrefine, unrefine_completely): the first
+//     request of each sibling group in call order wins (atomicMin of the call
+//     index), as the sequential calls would have it;
+//   - override_refines / induce_refines as frontier expansions, at most
+//     max_refinement_level rounds each (a dont_refine spreads only to finer
+//     cells, an induced refine only to coarser ones), with no host round trip;
+//   - override_unrefines as one wave per sibling group walking the face graph
+//     in LDS (the walk's outcome is an existence test over a closure, so a
+//     level-synchronous walk gives the sequential walk's answer, amr.hip);
+//   - execute_refines' new leaf list: surviving leaves compacted in order,
+//     new cells radix-sorted, one merge.
+// The host keeps the same four sets for single request calls (amr.hip); each
+// side is brought up to date from the other only when it is next used.
+#include <hipcub/hipcub.hpp>
+
+#include "exview.hpp"
+#include "face.hpp"
+#include "grid.hpp"
+
+namespace dccrgx {
+
+enum : uint32_t {
+    RF_REFINE = 1u,
+    RF_UNREFINE = 2u,
+    RF_NOT_UNREFINE = 4u,
+    RF_NOT_REFINE = 8u,
+    RF_GONE = 16u,   // execute: the leaf disappears
+    RF_KEEP = 32u,   // override_unrefines: the walk of this group / cell passed
+    RF_FINAL = 64u,  // override_unrefines: the unrefinement happens
+};
+constexpr uint32_t RF_SETS = RF_REFINE | RF_UNREFINE | RF_NOT_UNREFINE | RF_NOT_REFINE;
+constexpr uint32_t NONE32 = 0xffffffffu;
+
+// one explicit grid, its default neighborhood and the request flags
+struct AView {
+    ExView v;
+    const uint64_t* leaves;
+    uint64_t n;
+    const uint64_t* nof_row;
+    const uint32_t* nof_g;
+    const uint64_t* nto_row;
+    const uint32_t* nto_g;
+    const int32_t* items;  // default neighborhood items (original axes)
+    int32_t K;
+    uint32_t hood_len;
+    Partition part;
+    const int32_t* sfc;  // SFC owner table of the level-0 cells, or null (block partition)
+    int32_t rank;
+    uint32_t* flags;
+};
+
+struct AExists {
+    ExView v;
+    __device__ bool operator()(uint64_t c) const { return ex_find(v, c) >= 0; }
+};
+
+__device__ inline int a_level(const AView& a, uint64_t c) { return map_level(a.v.mp, c); }
+
+// Mapping::get_parent (dccrg_mapping.hpp:298-330): a level-0 cell is its own
+__device__ inline uint64_t a_parent(const AView& a, uint64_t c)
+{
+    uint64_t idx[3];
+    int l;
+    if (!map_indices(a.v.mp, c, idx, &l)) return 0;
+    return l == 0 ? c : map_cell(a.v.mp, idx, l - 1);
+}
+
+// Mapping::get_all_children (:392-442), x fastest; zeros at the maximum level
+__device__ inline void a_children(const AView& a, uint64_t c, uint64_t out[8])
+{
+    uint64_t idx[3];
+    int l;
+    for (int i = 0; i < 8; i++) out[i] = 0;
+    if (!map_indices(a.v.mp, c, idx, &l) || l >= a.v.mp.max_lvl) return;
+    const uint64_t h = (uint64_t)1 << (a.v.mp.max_lvl - l - 1);
+    for (int i = 0; i < 8; i++) {
+        const uint64_t ci[3] = {idx[0] + (i & 1) * h, idx[1] + ((i >> 1) & 1) * h, idx[2] + ((i >> 2) & 1) * h};
+        out[i] = map_cell(a.v.mp, ci, l + 1);
+    }
+}
+
+// Mapping::get_siblings (:450-471)
+__device__ inline void a_siblings(const AView& a, uint64_t c, uint64_t out[8])
+{
+    if (a_level(a, c) == 0) {
+        out[0] = c;
+        for (int i = 1; i < 8; i++) out[i] = 0;
+        return;
+    }
+    a_children(a, a_parent(a, c), out);
+}
+
+// process of a cell: its level-0 ancestor's (dccrg.hpp:10368, :10437)
+__device__ inline int a_owner(const AView& a, uint64_t c)
+{
+    uint64_t idx[3];
+    int l;
+    map_indices(a.v.mp, c, idx, &l);
+    const uint64_t l0 = map_cell(a.v.mp, idx, 0);
+    return a.sfc ? a.sfc[l0 - 1] : part_owner(a.part, l0);
+}
+
+// c != get_child(c), dccrg.hpp:9694-9718
+__device__ inline bool a_has_children(const AView& a, uint64_t c)
+{
+    const int l = a_level(a, c);
+    const bool ex = ex_find(a.v, c) >= 0;
+    if (l == a.v.mp.max_lvl) return !ex;
+    uint64_t idx[3];
+    int ll;
+    map_indices(a.v.mp, c, idx, &ll);
+    if (ex_find(a.v, map_cell(a.v.mp, idx, l + 1)) >= 0) return true;
+    return !ex;
+}
+
+// is_neighbor, dccrg.hpp:9603-9683
+__device__ inline bool a_is_neighbor(const AView& a, uint64_t c1, uint64_t c2)
+{
+    const MapParams& mp = a.v.mp;
+    const int M = mp.max_lvl;
+    uint64_t i1[3], i2[3];
+    int l1, l2;
+    map_indices(mp, c1, i1, &l1);
+    map_indices(mp, c2, i2, &l2);
+    const uint64_t len1 = (uint64_t)1 << (M - l1), len2 = (uint64_t)1 << (M - l2);
+    uint64_t maxd = 0;
+    int overlap = 0;
+    for (int d = 0; d < 3; d++) {
+        const uint64_t G = mp.length[d] << M;
+        uint64_t dist;
+        if (i1[d] <= i2[d]) {
+            dist = i2[d] <= i1[d] + len1 ? 0 : i2[d] - (i1[d] + len1);
+            if (a.v.per[d]) dist = min(dist, i1[d] + (G - (i2[d] + len2)));
+        } else {
+            dist = i1[d] <= i2[d] + len2 ? 0 : i1[d] - (i2[d] + len2);
+            if (a.v.per[d]) dist = min(dist, i2[d] + (G - (i1[d] + len1)));
+        }
+        maxd = max(maxd, dist);
+        overlap += (i1[d] + len1 > i2[d] && i1[d] < i2[d] + len2) ? 1 : 0;  // dccrg.hpp:11364-11405
+    }
+    if (a.hood_len == 0) return maxd < len1 && overlap >= 2;
+    return maxd < (uint64_t)a.hood_len * len1;
+}
+
+// cells_to_unrefine.erase(every sibling of c)
+__device__ inline void a_erase_sibling_unrefines(const AView& a, uint64_t c)
+{
+    uint64_t s[8];
+    a_siblings(a, c, s);
+    for (int k = 0; k < 8; k++) {
+        if (!s[k]) continue;
+        const int64_t g = ex_find(a.v, s[k]);
+        if (g >= 0 && (a.flags[g] & RF_UNREFINE)) atomicAnd(&a.flags[g], ~RF_UNREFINE);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// requests
+// ---------------------------------------------------------------------------
+
+// refine_completely, dccrg.hpp:2476-2546.  Requests at the maximum level are
+// dont_unrefine calls (:2486-2488): they are queued for the dont_unrefine
+// kernels with their call index.
+__global__ void __launch_bounds__(256) k_req_refine(AView a, const uint64_t* __restrict__ ids, uint64_t n,
+                                                    int32_t* __restrict__ res, uint64_t* __restrict__ du_ids,
+                                                    uint32_t* __restrict__ du_ord, uint32_t* __restrict__ du_n)
+{
+    const int M = a.v.mp.max_lvl;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t c = ids[i];
+        int32_t r = 0;
+        const int64_t g = ex_find(a.v, c);
+        if (g >= 0 && a_owner(a, c) == a.rank) {
+            const int lvl = a_level(a, c);
+            if (lvl == M) {
+                const uint32_t p = atomicAdd(du_n, 1u);
+                du_ids[p] = c;
+                du_ord[p] = (uint32_t)i;
+                r = 1;  // dont_unrefine of an existing cell
+            } else if (!(a.flags[g] & RF_NOT_REFINE)) {
+                bool blocked = false;
+                for (uint64_t e = a.nof_row[g]; e < a.nof_row[g + 1] && !blocked; e++) {
+                    const uint32_t t = a.nof_g[e];
+                    blocked = a_level(a, a.leaves[t]) < lvl && (a.flags[t] & RF_NOT_REFINE);
+                }
+                if (!blocked) {
+                    r = 1;
+                    atomicOr(&a.flags[g], RF_REFINE);
+                    a_erase_sibling_unrefines(a, c);
+                    for (int pass = 0; pass < 2; pass++) {
+                        const uint64_t* row = pass ? a.nto_row : a.nof_row;
+                        const uint32_t* val = pass ? a.nto_g : a.nof_g;
+                        for (uint64_t e = row[g]; e < row[g + 1]; e++) {
+                            const uint64_t nb = a.leaves[val[e]];
+                            if (a_level(a, nb) <= lvl) a_erase_sibling_unrefines(a, nb);
+                        }
+                    }
+                }
+            }
+        }
+        if (res) res[i] = r;
+    }
+}
+
+// dont_unrefine, dccrg.hpp:2715-2759, phase 1 (reads the flags only): the
+// sibling group's key (its smallest existing leaf index) unless a sibling is
+// already in cells_not_to_unrefine; the first call of each group wins
+__global__ void __launch_bounds__(256) k_req_du_a(AView a, const uint64_t* __restrict__ ids,
+                                                  const uint32_t* __restrict__ ord, const uint32_t* __restrict__ n_dev,
+                                                  uint64_t n_host, int32_t* __restrict__ res, uint32_t* __restrict__ grp,
+                                                  uint32_t* __restrict__ key)
+{
+    const uint64_t n = n_dev ? *n_dev : n_host;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t c = ids[i];
+        const uint32_t o = ord ? ord[i] : (uint32_t)i;
+        key[i] = NONE32;
+        const int64_t g = ex_find(a.v, c);
+        if (res) res[o] = g >= 0 ? 1 : 0;
+        if (g < 0 || a_level(a, c) == 0) continue;
+        uint64_t s[8];
+        a_siblings(a, c, s);
+        uint32_t kmin = NONE32;
+        bool recorded = false;
+        for (int k = 0; k < 8; k++) {
+            const int64_t gs = s[k] ? ex_find(a.v, s[k]) : -1;
+            if (gs < 0) continue;
+            kmin = min(kmin, (uint32_t)gs);
+            recorded |= (a.flags[gs] & RF_NOT_UNREFINE) != 0;
+        }
+        if (recorded) continue;
+        key[i] = kmin;
+        atomicMin(&grp[kmin], o);
+    }
+}
+
+// phase 2: the winner erases its siblings from cells_to_unrefine and is recorded
+__global__ void __launch_bounds__(256) k_req_du_b(AView a, const uint64_t* __restrict__ ids,
+                                                  const uint32_t* __restrict__ ord, const uint32_t* __restrict__ n_dev,
+                                                  uint64_t n_host, const uint32_t* __restrict__ grp,
+                                                  const uint32_t* __restrict__ key)
+{
+    const uint64_t n = n_dev ? *n_dev : n_host;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t k = key[i];
+        if (k == NONE32 || grp[k] != (ord ? ord[i] : (uint32_t)i)) continue;
+        const uint64_t c = ids[i];
+        a_erase_sibling_unrefines(a, c);
+        atomicOr(&a.flags[ex_find(a.v, c)], RF_NOT_UNREFINE);
+    }
+}
+
+// the leaves overlapping the neighborhood windows of a parent that does not
+// exist (its children are leaves): does any of them block unrefining it?
+// (amr.hip View::parent_window_leaves and unrefine_completely's tests, :2638-2670.)
+// A window W at the parent's level is covered by W itself, by W's parent, by
+// a coarser ancestor (no leaf inside W) or by W's children; a child that is
+// not a leaf is refined, so its leaves are finer than plvl + 1.
+__device__ inline bool a_window_blocks(const AView& a, uint64_t parent)
+{
+    const MapParams& mp = a.v.mp;
+    const int M = mp.max_lvl;
+    uint64_t pi[3];
+    int pl;
+    map_indices(mp, parent, pi, &pl);
+    const int64_t L = (int64_t)1 << (M - pl);
+    for (int k = 0; k < a.K; k++) {
+        uint64_t wi[3];
+        bool ok = true;
+        for (int d = 0; d < 3; d++) {
+            const int64_t G = (int64_t)(mp.length[d] << M);
+            int64_t x = (int64_t)pi[d] + (int64_t)a.items[3 * k + d] * L;
+            if (x < 0 || x >= G) {
+                if (!a.v.per[d]) {
+                    ok = false;
+                    break;
+                }
+                x %= G;
+                if (x < 0) x += G;
+            }
+            wi[d] = (uint64_t)x;
+        }
+        if (!ok) continue;
+        const uint64_t W = map_cell(mp, wi, pl);
+        const int64_t gw = ex_find(a.v, W);
+        if (gw >= 0) continue;  // a leaf of the parent's level: never blocks
+        if (pl > 0 && ex_find(a.v, map_cell(mp, wi, pl - 1)) >= 0) continue;  // coarser
+        bool covered = false;  // by a coarser ancestor: no leaf inside W
+        for (int l = pl - 2; l >= 0 && !covered; l--) covered = ex_find(a.v, map_cell(mp, wi, l)) >= 0;
+        if (covered || pl >= M) continue;
+        uint64_t ch[8];
+        a_children(a, W, ch);
+        for (int j = 0; j < 8; j++) {
+            const int64_t gc = ex_find(a.v, ch[j]);
+            if (gc < 0) return true;                            // refined: leaves at plvl + 2 or finer
+            if (a.flags[gc] & RF_REFINE) return true;           // plvl + 1 and about to be refined
+        }
+    }
+    return false;
+}
+
+// unrefine_completely, dccrg.hpp:2596-2675, phase 1 (reads the flags only)
+__global__ void __launch_bounds__(256) k_req_unref_a(AView a, const uint64_t* __restrict__ ids, uint64_t n,
+                                                     int32_t* __restrict__ res, uint32_t* __restrict__ grp,
+                                                     uint32_t* __restrict__ key)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t c = ids[i];
+        key[i] = NONE32;
+        int32_t r = 0;
+        const int64_t g = ex_find(a.v, c);
+        if (g >= 0 && a_owner(a, c) == a.rank) {
+            r = 1;
+            if (a_level(a, c) > 0) {
+                uint64_t s[8];
+                a_siblings(a, c, s);
+                bool stop = false;
+                for (int k = 0; k < 8 && !stop; k++) {  // in the reference's order (:2617-2633)
+                    if (!s[k]) continue;
+                    if (a_has_children(a, s[k])) {
+                        r = 0;
+                        stop = true;
+                        break;
+                    }
+                    const uint32_t f = a.flags[ex_find(a.v, s[k])];
+                    stop = (f & (RF_REFINE | RF_NOT_UNREFINE)) != 0;
+                }
+                for (int k = 0; k < 8 && !stop; k++)  // a sibling already recorded (amr.hip)
+                    stop = s[k] && (a.flags[ex_find(a.v, s[k])] & RF_UNREFINE);
+                if (!stop && !a_window_blocks(a, a_parent(a, c))) {
+                    const uint32_t k0 = (uint32_t)ex_find(a.v, s[0]);
+                    key[i] = k0;
+                    atomicMin(&grp[k0], (uint32_t)i);
+                }
+            }
+        }
+        if (res) res[i] = r;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_req_unref_b(AView a, const uint64_t* __restrict__ ids, uint64_t n,
+                                                     const uint32_t* __restrict__ grp, const uint32_t* __restrict__ key)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t k = key[i];
+        if (k != NONE32 && grp[k] == (uint32_t)i) atomicOr(&a.flags[ex_find(a.v, ids[i])], RF_UNREFINE);
+    }
+}
+
+// dont_refine, dccrg.hpp:2782-2805
+__global__ void __launch_bounds__(256) k_req_dont_refine(AView a, const uint64_t* __restrict__ ids, uint64_t n,
+                                                         int32_t* __restrict__ res)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t c = ids[i];
+        const int64_t g = ex_find(a.v, c);
+        if (res) res[i] = g >= 0 ? 1 : 0;
+        if (g < 0 || a_level(a, c) == a.v.mp.max_lvl) continue;
+        atomicAnd(&a.flags[g], ~RF_REFINE);
+        atomicOr(&a.flags[g], RF_NOT_REFINE);
+    }
+}
+
+// host sets -> flags: ids[i] gets bits[i]; dont_refine ids that are not
+// leaves are kept aside (the set persists, :10178)
+__global__ void __launch_bounds__(256) k_flags_scatter(AView a, const uint64_t* __restrict__ ids,
+                                                       const uint32_t* __restrict__ bits, uint64_t n,
+                                                       uint64_t* __restrict__ other, uint32_t* __restrict__ other_n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t g = ex_find(a.v, ids[i]);
+        if (g >= 0) atomicOr(&a.flags[g], bits[i]);
+        else if (bits[i] & RF_NOT_REFINE) other[atomicAdd(other_n, 1u)] = ids[i];
+    }
+}
+
+// flags -> (id, bits) of every leaf in any set
+__global__ void __launch_bounds__(256) k_flags_gather(AView a, uint64_t* __restrict__ ids, uint32_t* __restrict__ bits,
+                                                      uint32_t* __restrict__ cnt)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
+        const uint32_t f = a.flags[g] & RF_SETS;
+        if (!f) continue;
+        const uint32_t p = atomicAdd(cnt, 1u);
+        ids[p] = a.leaves[g];
+        bits[p] = f;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// stop_refining
+// ---------------------------------------------------------------------------
+
+// frontier: leaves with `bit`; refines of dont_refine leaves are dropped
+// first (override_refines' last step, :10181-10183)
+__global__ void __launch_bounds__(256) k_collect(AView a, uint32_t bit, uint32_t* __restrict__ out,
+                                                 uint32_t* __restrict__ cnt)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
+        uint32_t f = a.flags[g];
+        if (bit == RF_REFINE && (f & RF_NOT_REFINE) && (f & RF_REFINE)) a.flags[g] = f &= ~RF_REFINE;
+        if (f & bit) out[atomicAdd(cnt, 1u)] = (uint32_t)g;
+    }
+}
+
+// one round of override_refines (finer = 1: every finer neighbor of a
+// dont_refine leaf joins, :10130-10177) or induce_refines (finer = 0: every
+// coarser neighbor of a refined leaf, :9730-9907); neighbors of / to
+__global__ void __launch_bounds__(256) k_spread(AView a, uint32_t bit, int finer, const uint32_t* __restrict__ front,
+                                                const uint32_t* __restrict__ front_n, uint32_t* __restrict__ next,
+                                                uint32_t* __restrict__ next_n)
+{
+    const uint32_t n = *front_n;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t g = front[i];
+        const int l = a_level(a, a.leaves[g]);
+        for (int pass = 0; pass < 2; pass++) {
+            const uint64_t* row = pass ? a.nto_row : a.nof_row;
+            const uint32_t* val = pass ? a.nto_g : a.nof_g;
+            for (uint64_t e = row[g]; e < row[g + 1]; e++) {
+                const uint32_t t = val[e];
+                const int lt = a_level(a, a.leaves[t]);
+                if (finer ? lt <= l : lt >= l) continue;
+                if (a.flags[t] & bit) continue;
+                if (!(atomicOr(&a.flags[t], bit) & bit)) next[atomicAdd(next_n, 1u)] = t;
+            }
+        }
+    }
+}
+
+// override_unrefines, dccrg.hpp:9935-10124 (amr.hip explains the
+// restatement): sibling groups whose children are all leaves walk once, from
+// their smallest requested leaf; other requests walk alone.  key[g] = the
+// group's first child's leaf index, or NONE32 for a lone request.
+__global__ void __launch_bounds__(256) k_ou_group(AView a, const uint32_t* __restrict__ us, const uint32_t* __restrict__ nu,
+                                                  uint32_t* __restrict__ grp, uint32_t* __restrict__ key)
+{
+    const uint32_t n = *nu;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t g = us[i];
+        uint64_t ch[8];
+        a_children(a, a_parent(a, a.leaves[g]), ch);
+        uint32_t k0 = NONE32;
+        bool all = true;
+        for (int k = 0; k < 8 && all; k++) {
+            const int64_t gc = ch[k] ? ex_find(a.v, ch[k]) : -1;
+            all = gc >= 0;
+            if (k == 0) k0 = (uint32_t)gc;
+        }
+        key[i] = all ? k0 : NONE32;
+        if (all) atomicMin(&grp[k0], g);
+    }
+}
+
+// LDS-or-global workspace of one walk
+struct Walk {
+    uint64_t* queue;  // Q entries
+    uint64_t* seen;   // S entries (open addressing, 0 = empty), S a power of two
+    uint32_t Q, S;
+};
+
+// insert x into the seen set; true if it was not there.  *over on a full table.
+__device__ inline bool walk_insert(const Walk& w, uint64_t x, int* over)
+{
+    uint32_t h = (uint32_t)hmix(x) & (w.S - 1);
+    for (uint32_t probe = 0; probe < w.S; probe++) {
+        const unsigned long long prev =
+            atomicCAS(reinterpret_cast<unsigned long long*>(&w.seen[h]), 0ull, (unsigned long long)x);
+        if (prev == 0ull) return true;
+        if (prev == (unsigned long long)x) return false;
+        h = (h + 1) & (w.S - 1);
+    }
+    *over = 1;
+    return false;
+}
+
+// one wave (workgroup of 64) per walk; `lds_bytes` > 0: the workspace is in
+// LDS, else `scratch` holds one workspace per workgroup
+__global__ void __launch_bounds__(64) k_ou_walk(AView a, const uint32_t* __restrict__ us, const uint32_t* __restrict__ nu,
+                                                const uint32_t* __restrict__ grp, const uint32_t* __restrict__ key,
+                                                uint32_t Q, uint32_t S, int use_lds, uint64_t* __restrict__ scratch,
+                                                int32_t* __restrict__ err)
+{
+    extern __shared__ uint64_t lds[];
+    __shared__ uint32_t head, tail, fail;
+    __shared__ int over;
+    const int lane = threadIdx.x;
+    Walk w;
+    w.Q = Q;
+    w.S = S;
+    w.queue = use_lds ? lds : scratch + (size_t)blockIdx.x * (Q + S);
+    w.seen = w.queue + Q;
+    const uint32_t n = *nu;
+    AExists exists{a.v};
+    int32_t per[3] = {a.v.per[0], a.v.per[1], a.v.per[2]};
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t g = us[i];
+        const uint32_t k = key[i];
+        if (k != NONE32 && grp[k] != g) continue;  // not the group's walker (uniform across the wave)
+        const uint64_t u = a.leaves[g];
+        const uint64_t parent = a_parent(a, u);
+        const int ul = a_level(a, u);
+        for (uint32_t s = lane; s < S; s += 64) w.seen[s] = 0;
+        if (lane == 0) {
+            head = 0;
+            tail = 0;
+            over = 0;
+            uint64_t sib[8];
+            a_children(a, parent, sib);
+            fail = 0;
+            for (int j = 0; j < 8; j++) {  // a sibling to be refined or kept (:9960-9975)
+                const int64_t gs = sib[j] ? ex_find(a.v, sib[j]) : -1;
+                if (gs >= 0 && (a.flags[gs] & (RF_REFINE | RF_NOT_UNREFINE))) fail = 1;
+            }
+        }
+        __syncthreads();
+        if (lane == 0 && !fail) {
+            uint64_t f6[6];
+            face_graph(a.v.mp, per, u, f6, exists);
+            int ov = 0;
+            for (int j = 0; j < 6; j++)
+                if (f6[j] && walk_insert(w, f6[j], &ov)) w.queue[tail++] = f6[j];
+            over |= ov;
+        }
+        __syncthreads();
+        while (!fail && !over && head < tail) {
+            const uint32_t h0 = head, t0 = tail;
+            const uint32_t batch = min(t0 - h0, 64u);
+            if ((uint32_t)lane < batch) {
+                const uint64_t x = w.queue[h0 + lane];
+                const int rl = a_level(a, x);
+                const int64_t gx = ex_find(a.v, x);
+                if (rl > ul || (rl == ul && gx >= 0 && (a.flags[gx] & RF_REFINE))) {
+                    atomicOr(&fail, 1u);
+                } else {
+                    uint64_t f6[6];
+                    face_graph(a.v.mp, per, x, f6, exists);
+                    int ov = 0;
+                    for (int j = 0; j < 6; j++) {
+                        if (!f6[j] || !walk_insert(w, f6[j], &ov)) continue;
+                        if (!a_is_neighbor(a, parent, f6[j])) continue;
+                        const uint32_t p = atomicAdd(&tail, 1u);
+                        if (p < Q) w.queue[p] = f6[j];
+                        else ov = 1;
+                    }
+                    if (ov) atomicOr(&over, 1);
+                }
+            }
+            __syncthreads();
+            if (lane == 0) head = h0 + batch;
+            __syncthreads();
+        }
+        if (lane == 0) {
+            if (over) atomicOr(err, 1);
+            else if (!fail) atomicOr(&a.flags[k != NONE32 ? k : g], RF_KEEP);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ou_final(AView a, const uint32_t* __restrict__ us, const uint32_t* __restrict__ nu,
+                                                  const uint32_t* __restrict__ key)
+{
+    const uint32_t n = *nu;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t g = us[i], k = key[i];
+        if (a.flags[k != NONE32 ? k : g] & RF_KEEP) atomicOr(&a.flags[g], RF_FINAL);
+    }
+}
+
+// execute_refines, dccrg.hpp:10243-10693: children of refined leaves and
+// parents of unrefined groups are added; refined leaves and every child of an
+// unrefined parent go.  Local ones are reported (new / removed / retired).
+// A group with all children leaves is handled by its walker only; lone
+// requests may repeat a parent (sorted and made unique afterwards).
+struct ExecOut {
+    uint64_t* added;
+    uint64_t* newc;
+    uint64_t* removed;
+    uint64_t* retired;
+    uint32_t* cnt;  // added, new, removed, retired
+};
+
+__global__ void __launch_bounds__(256) k_exec(AView a, const uint32_t* __restrict__ grp, ExecOut o)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
+        const uint32_t f = a.flags[g];
+        const uint64_t c = a.leaves[g];
+        if (f & RF_REFINE) {
+            atomicOr(&a.flags[g], RF_GONE);
+            uint64_t ch[8];
+            a_children(a, c, ch);
+            const uint32_t p = atomicAdd(&o.cnt[0], 8u);
+            for (int k = 0; k < 8; k++) o.added[p + k] = ch[k];
+            if (a_owner(a, c) == a.rank) {
+                const uint32_t q = atomicAdd(&o.cnt[1], 8u);
+                for (int k = 0; k < 8; k++) o.newc[q + k] = ch[k];
+                o.retired[atomicAdd(&o.cnt[3], 1u)] = c;
+            }
+        }
+        if (!(f & RF_FINAL)) continue;
+        const uint64_t par = a_parent(a, c);
+        uint64_t ch[8];
+        a_children(a, par, ch);
+        const int64_t g0 = ch[0] ? ex_find(a.v, ch[0]) : -1;
+        bool all = true;
+        for (int k = 0; k < 8 && all; k++) all = ch[k] && ex_find(a.v, ch[k]) >= 0;
+        if (all && grp[(uint32_t)g0] != (uint32_t)g) continue;  // the group's walker does it
+        o.added[atomicAdd(&o.cnt[0], 1u)] = par;
+        const bool local = a_owner(a, par) == a.rank;  // the children's process too
+        for (int k = 0; k < 8; k++) {
+            if (!ch[k]) continue;
+            const int64_t gc = ex_find(a.v, ch[k]);
+            if (gc >= 0) atomicOr(&a.flags[gc], RF_GONE);
+            if (local) {
+                o.removed[atomicAdd(&o.cnt[2], 1u)] = ch[k];
+                o.retired[atomicAdd(&o.cnt[3], 1u)] = ch[k];
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_kept_flags(AView a, uint8_t* __restrict__ keep)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride)
+        keep[g] = (a.flags[g] & RF_GONE) ? 0 : 1;
+}
+
+// dont_refine ids that persist (:10178): leaves with the flag
+__global__ void __launch_bounds__(256) k_nr_ids(AView a, uint64_t* __restrict__ out, uint32_t* __restrict__ cnt)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride)
+        if (a.flags[g] & RF_NOT_REFINE) out[atomicAdd(cnt, 1u)] = a.leaves[g];
+}
+
+__device__ inline uint64_t lower_bound_u64(const uint64_t* v, uint64_t n, uint64_t x)
+{
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (v[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// merge of two ascending, disjoint lists (counts on the device)
+__global__ void __launch_bounds__(256) k_merge(const uint64_t* __restrict__ a, const uint64_t* __restrict__ na_p,
+                                               const uint64_t* __restrict__ b, const uint64_t* __restrict__ nb_p,
+                                               uint64_t* __restrict__ out)
+{
+    const uint64_t na = *na_p, nb = *nb_p;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb; i += stride) {
+        if (i < na) out[i + lower_bound_u64(b, nb, a[i])] = a[i];
+        else out[(i - na) + lower_bound_u64(a, na, b[i - na])] = b[i - na];
+    }
+}
+
+static unsigned blocks(uint64_t n, unsigned cap = 4096)
+{
+    uint64_t g = (n + 255) / 256;
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(g, cap));
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+
+// stream-ordered scratch of one call, freed in one go
+struct Scratch {
+    hipStream_t st;
+    std::vector<void*> v;
+    explicit Scratch(hipStream_t s) : st(s) {}
+    template <class T>
+    int get(T** p, size_t count)
+    {
+        *p = nullptr;
+        DX_HIP(ds_malloc(p, std::max<size_t>(count, 1) * sizeof(T), st));
+        v.push_back(*p);
+        return DCCRGX_OK;
+    }
+    ~Scratch()
+    {
+        for (void* p : v) ds_free(p, st);
+    }
+};
+
+static AView aview(const dccrgx_grid* grid, uint32_t* flags)
+{
+    const Explicit* E = grid->ex;
+    const Hood& h = grid->hoods.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
+    AView a{};
+    a.v = explicit_view(grid);
+    a.leaves = E->d_leaves;
+    a.n = E->n;
+    a.nof_row = h.d_nof_row;
+    a.nof_g = h.d_nof_g;
+    a.nto_row = h.d_nto_row;
+    a.nto_g = h.d_nto_g;
+    a.items = h.d_of_c;
+    a.K = h.K;
+    a.hood_len = grid->params.neighborhood_length;
+    a.part = E->part;
+    a.sfc = grid->d_sfc_owner;
+    a.rank = grid->ctx->rank;
+    a.flags = flags;
+    return a;
+}
+
+// the flags over the current leaves from the host sets (when the host has
+// the newer state)
+int amr_dev_sync(dccrgx_grid* grid)
+{
+    Amr& A = *grid->amr;
+    Explicit* E = grid->ex;
+    hipStream_t st = grid->ctx->compute;
+    if (!grid->sfc_owner.empty() && !grid->d_sfc_owner) {
+        DX_HIP(dx_malloc(&grid->d_sfc_owner, grid->sfc_owner.size() * 4));
+        DX_TRY(dx_h2d(grid->ctx, grid->d_sfc_owner, grid->sfc_owner.data(), grid->sfc_owner.size() * 4, st));
+    }
+    if (A.dev_current && A.flags_n == E->n && A.d_flags) return DCCRGX_OK;
+    if (A.flags_cap < E->n) {
+        ds_free(A.d_flags, st);
+        A.flags_cap = E->n + E->n / 8 + 64;
+        DX_HIP(ds_malloc(&A.d_flags, A.flags_cap * 4, st));
+    }
+    A.flags_n = E->n;
+    DX_HIP(hipMemsetAsync(A.d_flags, 0, E->n * 4, st));
+    std::vector<uint64_t> ids;
+    std::vector<uint32_t> bits;
+    const std::pair<const FlatSet*, uint32_t> sets[4] = {
+        {&A.to_refine, RF_REFINE}, {&A.not_to_refine, RF_NOT_REFINE}, {&A.to_unrefine, RF_UNREFINE},
+        {&A.not_to_unrefine, RF_NOT_UNREFINE}};
+    for (const auto& s : sets)
+        for (uint64_t c : *s.first) {
+            ids.push_back(c);
+            bits.push_back(s.second);
+        }
+    A.nr_other.clear();
+    if (!ids.empty()) {
+        Scratch S(st);
+        uint64_t *d_ids, *d_other;
+        uint32_t *d_bits, *d_cnt;
+        DX_TRY(S.get(&d_ids, ids.size()));
+        DX_TRY(S.get(&d_bits, bits.size()));
+        DX_TRY(S.get(&d_other, ids.size()));
+        DX_TRY(S.get(&d_cnt, 1));
+        DX_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
+        DX_TRY(dx_h2d(grid->ctx, d_ids, ids.data(), ids.size() * 8, st));
+        DX_TRY(dx_h2d(grid->ctx, d_bits, bits.data(), bits.size() * 4, st));
+        hipLaunchKernelGGL(k_flags_scatter, dim3(blocks(ids.size())), dim3(256), 0, st, aview(grid, A.d_flags), d_ids,
+                           d_bits, (uint64_t)ids.size(), d_other, d_cnt);
+        DX_HIP(hipGetLastError());
+        uint32_t no = 0;
+        DX_TRY(dx_d2h(grid->ctx, &no, d_cnt, 4, st));
+        A.nr_other.resize(no);
+        if (no) DX_TRY(dx_d2h(grid->ctx, A.nr_other.data(), d_other, no * 8ull, st));
+    }
+    A.dev_current = true;
+    return DCCRGX_OK;
+}
+
+// the host sets from the flags (when the device has the newer state)
+int amr_host_sync(dccrgx_grid* grid)
+{
+    Amr& A = *grid->amr;
+    if (A.host_current) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    Scratch S(st);
+    uint64_t* d_ids;
+    uint32_t *d_bits, *d_cnt;
+    DX_TRY(S.get(&d_ids, A.flags_n));
+    DX_TRY(S.get(&d_bits, A.flags_n));
+    DX_TRY(S.get(&d_cnt, 1));
+    DX_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
+    hipLaunchKernelGGL(k_flags_gather, dim3(blocks(A.flags_n)), dim3(256), 0, st, aview(grid, A.d_flags), d_ids,
+                       d_bits, d_cnt);
+    DX_HIP(hipGetLastError());
+    uint32_t n = 0;
+    DX_TRY(dx_d2h(grid->ctx, &n, d_cnt, 4, st));
+    std::vector<uint64_t> ids(n);
+    std::vector<uint32_t> bits(n);
+    if (n) {
+        DX_TRY(dx_d2h(grid->ctx, ids.data(), d_ids, n * 8ull, st));
+        DX_TRY(dx_d2h(grid->ctx, bits.data(), d_bits, n * 4ull, st));
+    }
+    A.to_refine.clear();
+    A.not_to_refine.clear();
+    A.to_unrefine.clear();
+    A.not_to_unrefine.clear();
+    for (uint32_t i = 0; i < n; i++) {
+        if (bits[i] & RF_REFINE) A.to_refine.insert(ids[i]);
+        if (bits[i] & RF_NOT_REFINE) A.not_to_refine.insert(ids[i]);
+        if (bits[i] & RF_UNREFINE) A.to_unrefine.insert(ids[i]);
+        if (bits[i] & RF_NOT_UNREFINE) A.not_to_unrefine.insert(ids[i]);
+    }
+    for (uint64_t c : A.nr_other) A.not_to_refine.insert(c);
+    A.host_current = true;
+    return DCCRGX_OK;
+}
+
+// a batch of request calls of one kind in call order (explicit grids)
+int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results)
+{
+    Amr& A = *grid->amr;
+    DX_TRY(amr_dev_sync(grid));
+    if (!n) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    const AView a = aview(grid, A.d_flags);
+    Scratch S(st);
+    uint64_t *d_ids, *d_du;
+    int32_t* d_res = nullptr;
+    uint32_t *d_grp, *d_key, *d_ord, *d_dun;
+    DX_TRY(S.get(&d_ids, n));
+    if (results) DX_TRY(S.get(&d_res, n));
+    DX_TRY(S.get(&d_grp, a.n));
+    DX_TRY(S.get(&d_key, n));
+    DX_HIP(hipMemsetAsync(d_grp, 0xff, a.n * 4, st));
+    DX_TRY(dx_h2d(grid->ctx, d_ids, ids, n * 8, st));
+    const unsigned b = blocks(n);
+    switch (kind) {
+    case DCCRGX_AMR_REFINE:
+        DX_TRY(S.get(&d_du, n));
+        DX_TRY(S.get(&d_ord, n));
+        DX_TRY(S.get(&d_dun, 1));
+        DX_HIP(hipMemsetAsync(d_dun, 0, 4, st));
+        hipLaunchKernelGGL(k_req_refine, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n, d_res, d_du,
+                           d_ord, d_dun);
+        hipLaunchKernelGGL(k_req_du_a, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_du, (const uint32_t*)d_ord,
+                           (const uint32_t*)d_dun, (uint64_t)0, (int32_t*)nullptr, d_grp, d_key);
+        hipLaunchKernelGGL(k_req_du_b, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_du, (const uint32_t*)d_ord,
+                           (const uint32_t*)d_dun, (uint64_t)0, (const uint32_t*)d_grp, (const uint32_t*)d_key);
+        break;
+    case DCCRGX_AMR_DONT_UNREFINE:
+        hipLaunchKernelGGL(k_req_du_a, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (const uint32_t*)nullptr,
+                           (const uint32_t*)nullptr, (uint64_t)n, d_res, d_grp, d_key);
+        hipLaunchKernelGGL(k_req_du_b, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (const uint32_t*)nullptr,
+                           (const uint32_t*)nullptr, (uint64_t)n, (const uint32_t*)d_grp, (const uint32_t*)d_key);
+        break;
+    case DCCRGX_AMR_UNREFINE:
+        hipLaunchKernelGGL(k_req_unref_a, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n, d_res,
+                           d_grp, d_key);
+        hipLaunchKernelGGL(k_req_unref_b, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n,
+                           (const uint32_t*)d_grp, (const uint32_t*)d_key);
+        break;
+    default:
+        hipLaunchKernelGGL(k_req_dont_refine, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n, d_res);
+        break;
+    }
+    DX_HIP(hipGetLastError());
+    if (results) DX_TRY(dx_d2h(grid->ctx, results, d_res, n * 4, st));
+    A.host_current = false;
+    return DCCRGX_OK;
+}
+
+// override_refines, induce_refines and override_unrefines on the flags, then
+// the new leaf list (device, ascending, and its host copy), this rank's new /
+// removed cells (A.new_cells / A.removed) and retired cells (ascending), and
+// the dont_refine ids that persist (`nr`).  The grid is not changed; the
+// flags hold the decisions afterwards (the caller restores them if the
+// rebuild fails).
+int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, std::vector<uint64_t>& leaves_host,
+                   std::vector<uint64_t>& retired, std::vector<uint64_t>& nr, bool* changed)
+{
+    Amr& A = *grid->amr;
+    DX_TRY(amr_dev_sync(grid));
+    Ctx* ctx = grid->ctx;
+    hipStream_t st = ctx->compute;
+    const AView a = aview(grid, A.d_flags);
+    const uint64_t N = a.n;
+    const int M = grid->map.max_lvl;
+    Scratch S(st);
+    PhaseTimer T("amr_dev_decide");
+    // counters: [0..M+1] frontier sizes of a spread, then the same again
+    uint32_t *d_cnt, *d_fa, *d_fb, *d_grp, *d_key;
+    const int NC = 2 * (M + 2) + 8;
+    DX_TRY(S.get(&d_cnt, NC));
+    DX_TRY(S.get(&d_fa, N));
+    DX_TRY(S.get(&d_fb, N));
+    DX_TRY(S.get(&d_grp, N));
+    DX_TRY(S.get(&d_key, N));
+    DX_HIP(hipMemsetAsync(d_cnt, 0, NC * 4, st));
+    DX_HIP(hipMemsetAsync(d_grp, 0xff, N * 4, st));
+    const unsigned bN = blocks(N);
+    // override_refines then induce_refines: at most M rounds each
+    for (int phase = 0; phase < 2; phase++) {
+        const uint32_t bit = phase == 0 ? RF_NOT_REFINE : RF_REFINE;
+        uint32_t* c = d_cnt + phase * (M + 2);
+        hipLaunchKernelGGL(k_collect, dim3(bN), dim3(256), 0, st, a, bit, d_fa, c);
+        uint32_t *f = d_fa, *nx = d_fb;
+        for (int r = 0; r < M; r++) {
+            hipLaunchKernelGGL(k_spread, dim3(bN), dim3(256), 0, st, a, bit, phase == 0 ? 1 : 0, (const uint32_t*)f,
+                               (const uint32_t*)(c + r), nx, c + r + 1);
+            std::swap(f, nx);
+        }
+    }
+    // refines of dont_refine cells were dropped by the second k_collect
+    // override_unrefines
+    uint32_t* cu = d_cnt + 2 * (M + 2);
+    hipLaunchKernelGGL(k_collect, dim3(bN), dim3(256), 0, st, a, RF_UNREFINE, d_fa, cu);
+    hipLaunchKernelGGL(k_ou_group, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_fa, (const uint32_t*)cu, d_grp,
+                       d_key);
+    const uint32_t hl = grid->params.neighborhood_length;
+    const uint64_t P = 8ull * (2 * hl + 3) * (2 * hl + 3) * (2 * hl + 3);
+    const uint32_t Q = (uint32_t)(6 * P + 8);
+    uint32_t Sz = 16;
+    while (Sz < 2 * Q) Sz <<= 1;
+    const size_t ws = (size_t)(Q + Sz) * 8;
+    const bool lds = ws <= 48 * 1024;
+    const unsigned waves = lds ? 4096 : 1024;
+    uint64_t* d_scr = nullptr;
+    if (!lds) DX_TRY(S.get(&d_scr, (size_t)waves * (Q + Sz)));
+    int32_t* d_err;
+    DX_TRY(S.get(&d_err, 1));
+    DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
+    hipLaunchKernelGGL(k_ou_walk, dim3(waves), dim3(64), lds ? ws : 0, st, a, (const uint32_t*)d_fa, (const uint32_t*)cu,
+                       (const uint32_t*)d_grp, (const uint32_t*)d_key, Q, Sz, lds ? 1 : 0, d_scr, d_err);
+    hipLaunchKernelGGL(k_ou_final, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_fa, (const uint32_t*)cu,
+                       (const uint32_t*)d_key);
+    // execute_refines
+    ExecOut o;
+    DX_TRY(S.get(&o.added, 8 * N + 8));
+    DX_TRY(S.get(&o.newc, 8 * N + 8));
+    DX_TRY(S.get(&o.removed, 8 * N + 8));
+    DX_TRY(S.get(&o.retired, 9 * N + 8));
+    o.cnt = d_cnt + 2 * (M + 2) + 1;  // 4 counters
+    hipLaunchKernelGGL(k_exec, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_grp, o);
+    uint64_t* d_nr;
+    DX_TRY(S.get(&d_nr, N));
+    uint32_t* nr_cnt = o.cnt + 4;
+    hipLaunchKernelGGL(k_nr_ids, dim3(bN), dim3(256), 0, st, a, d_nr, nr_cnt);
+    DX_HIP(hipGetLastError());
+    uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
+    int32_t err = 0;
+    DX_TRY(dx_d2h(ctx, &err, d_err, 4, st));
+    DX_TRY(dx_d2h(ctx, cnt, o.cnt, 5 * 4, st));
+    T.lap("decisions");
+    DX_CHECK(!err, DCCRGX_EINTERNAL, "override_unrefines walk exceeded its workspace");
+    // the persisting dont_refine set: flagged leaves and the ids that are not leaves
+    nr.resize(cnt[4]);
+    if (cnt[4]) DX_TRY(dx_d2h(ctx, nr.data(), d_nr, cnt[4] * 8ull, st));
+    nr.insert(nr.end(), A.nr_other.begin(), A.nr_other.end());
+    auto host_sorted = [&](const uint64_t* d, uint32_t k, std::vector<uint64_t>& out) -> int {
+        out.resize(k);
+        if (k) DX_TRY(dx_d2h(ctx, out.data(), d, k * 8ull, st));
+        radix_sort_u64(out);
+        out.erase(std::unique(out.begin(), out.end()), out.end());
+        return DCCRGX_OK;
+    };
+    DX_TRY(host_sorted(o.newc, cnt[1], A.new_cells));
+    DX_TRY(host_sorted(o.removed, cnt[2], A.removed));
+    DX_TRY(host_sorted(o.retired, cnt[3], retired));
+    *changed = cnt[0] > 0;
+    if (!*changed) return DCCRGX_OK;
+    // the new leaf list: surviving leaves in order, merged with the sorted new ones
+    uint8_t* d_keep;
+    uint64_t *d_kept, *d_sorted, *d_cnt64;
+    DX_TRY(S.get(&d_keep, N));
+    DX_TRY(S.get(&d_kept, N));
+    DX_TRY(S.get(&d_sorted, cnt[0]));
+    DX_TRY(S.get(&d_cnt64, 2));
+    hipLaunchKernelGGL(k_kept_flags, dim3(bN), dim3(256), 0, st, a, d_keep);
+    size_t tb = 0, tb2 = 0, tb3 = 0;
+    DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
+    DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb2, o.added, d_sorted, (int)cnt[0], 0, 64, st));
+    DX_HIP(hipcub::DeviceSelect::Unique(nullptr, tb3, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
+    uint8_t* d_tmp;
+    DX_TRY(S.get(&d_tmp, std::max({tb, tb2, tb3})));
+    tb = tb2 = tb3 = std::max({tb, tb2, tb3});
+    DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, tb, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
+    DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, tb2, o.added, d_sorted, (int)cnt[0], 0, 64, st));
+    DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, tb3, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
+    uint64_t nk[2] = {0, 0};
+    DX_TRY(dx_d2h(ctx, nk, d_cnt64, 16, st));
+    const uint64_t n_new = nk[0] + nk[1];
+    uint64_t* d_new = nullptr;
+    DX_HIP(ds_malloc(&d_new, std::max<uint64_t>(n_new, 1) * 8, st));
+    hipLaunchKernelGGL(k_merge, dim3(blocks(n_new)), dim3(256), 0, st, (const uint64_t*)d_kept,
+                       (const uint64_t*)d_cnt64, (const uint64_t*)o.added, (const uint64_t*)(d_cnt64 + 1), d_new);
+    DX_HIP(hipGetLastError());
+    leaves_host.resize(n_new);
+    const int e = dx_d2h(ctx, leaves_host.data(), d_new, n_new * 8, st);
+    if (e != DCCRGX_OK) {
+        ds_free(d_new, st);
+        return e;
+    }
+    T.lap("new leaf list");
+    *d_leaves_out = d_new;
+    *n_out = n_new;
+    return DCCRGX_OK;
+}
+
+}  // namespace dccrgx

@@ -460,8 +460,8 @@ int dccrgx_file_read_info(const char* path, uint64_t offset, void* header, size_
 int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* info, dccrgx_grid** out)
 {
     DX_CHECK(ctx && path && info && out, DCCRGX_EINVAL, "null argument");
-    DX_CHECK(info->params.partition == DCCRGX_PARTITION_BLOCK, DCCRGX_EINVAL,
-             "loaded grids are placed by the block partition (the file records no placement)");
+    DX_CHECK(info->params.partition == DCCRGX_PARTITION_BLOCK || info->params.partition == DCCRGX_PARTITION_SFC,
+             DCCRGX_EINVAL, "unknown placement %d", (int)info->params.partition);
     *out = nullptr;
     Fd fd;
     fd.fd = open(path, O_RDONLY);
@@ -472,6 +472,12 @@ int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* 
     MapParams mp;
     DX_TRY(make_map_params(&m, &mp));
     const Partition part = make_partition(mp.nlevel0, ctx->comm_size);
+    // the file records no placement: the loading grid's own (block, or the
+    // SFC table of info->params) decides which rank reads which cells, as the
+    // reference's load places cells by the new grid's partition
+    std::vector<int32_t> sfc;
+    if (info->params.partition == DCCRGX_PARTITION_SFC)
+        DX_TRY(sfc_owners(info->params.length, ctx->comm_size, ctx->compute, sfc));
     // every cell in the list (:2033-2057); this rank loads the cells whose
     // level-0 ancestor is local (cell_overlaps_local, :2059-2071).  Pass 1
     // streams the list: are all cells level 0, and are this rank's cells
@@ -492,7 +498,8 @@ int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* 
     auto owner_of = [&](uint64_t c, int* lvl) {
         uint64_t idx[3];
         if (c == 0 || !map_indices(mp, c, idx, lvl)) return -1;
-        return part_owner(part, *lvl == 0 ? c : map_cell(mp, idx, 0));
+        const uint64_t l0 = *lvl == 0 ? c : map_cell(mp, idx, 0);
+        return sfc.empty() ? part_owner(part, l0) : (int)sfc[l0 - 1];
     };
     bool all_level0 = true, simple = true;
     uint64_t n_mine = 0, first = 0, d0 = 0, stride = 0;
@@ -515,7 +522,8 @@ int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* 
         n_mine++;
         return DCCRGX_OK;
     }));
-    const bool uniform = all_level0 && total == mp.nlevel0;
+    // SFC grids always use the explicit layout (their local cells are not a slab)
+    const bool uniform = all_level0 && total == mp.nlevel0 && sfc.empty();
     std::vector<uint64_t> leaves;
     if (!uniform) {
         leaves.reserve(total);

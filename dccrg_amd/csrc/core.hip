@@ -7,6 +7,7 @@
 #include <cstring>
 #include <condition_variable>
 #include <mutex>
+#include <unordered_map>
 
 #include "internal.hpp"
 
@@ -506,14 +507,127 @@ void pool_run(size_t nt, const std::function<void(size_t)>& job)
     p.fin.wait(lk, [&] { return p.pending == 0; });
 }
 
-void dx_trim_pool()
+// ---------------------------------------------------------------------------
+// caching allocator (internal.hpp)
+// ---------------------------------------------------------------------------
+namespace {
+constexpr size_t CACHE_MAX_BLOCK = 256ull << 20;  // larger blocks go straight back to the pool
+constexpr size_t CACHE_MAX_TOTAL = 8ull << 30;    // idle bytes kept at most
+
+size_t size_class(size_t b)
+{
+    if (b <= 256) return 256;
+    size_t c = 256;
+    while (c < b) {
+        const size_t mid = c + c / 2;  // classes 2^k and 1.5 * 2^k: at most 1/3 unused
+        if (mid >= b && mid > c) return mid;
+        c <<= 1;
+    }
+    return c;
+}
+
+struct Cache {
+    std::mutex m;
+    std::unordered_map<void*, size_t> live;  // cached-class blocks in use -> class
+    std::map<size_t, std::vector<void*>> idle;  // reusable by any stream
+    std::map<hipStream_t, std::map<size_t, std::vector<void*>>> by_stream;  // reusable by that stream
+    size_t idle_bytes = 0, stream_bytes = 0;
+};
+
+Cache& cache()
+{
+    static Cache* c = new Cache();  // never destroyed: frees may come during process exit
+    return *c;
+}
+
+void* take(std::map<size_t, std::vector<void*>>& m, size_t cls)
+{
+    auto it = m.find(cls);
+    if (it == m.end() || it->second.empty()) return nullptr;
+    void* p = it->second.back();
+    it->second.pop_back();
+    return p;
+}
+}  // namespace
+
+hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_stream)
+{
+    Cache& C = cache();
+    const size_t cls = bytes <= CACHE_MAX_BLOCK ? size_class(bytes) : 0;
+    if (cls) {
+        std::lock_guard<std::mutex> lk(C.m);
+        void* q = nullptr;
+        if (!any_stream) {
+            auto it = C.by_stream.find(st);
+            if (it != C.by_stream.end() && (q = take(it->second, cls))) C.stream_bytes -= cls;
+        }
+        if (!q && (q = take(C.idle, cls))) C.idle_bytes -= cls;
+        if (q) {
+            C.live[q] = cls;
+            *p = q;
+            return hipSuccess;
+        }
+    }
+    hipError_t e = hipMallocAsync(p, cls ? cls : bytes, st);
+    if (e == hipSuccess && any_stream) e = hipStreamSynchronize(st);
+    if (e == hipSuccess && cls) {
+        std::lock_guard<std::mutex> lk(C.m);
+        C.live[*p] = cls;
+    }
+    return e;
+}
+
+void dx_cache_free(void* p, hipStream_t st, bool device_idle)
+{
+    if (!p) return;
+    Cache& C = cache();
+    std::unique_lock<std::mutex> lk(C.m);
+    auto it = C.live.find(p);
+    if (it == C.live.end()) {  // an uncached (large) block
+        lk.unlock();
+        (void)hipFreeAsync(p, st);
+        return;
+    }
+    const size_t cls = it->second;
+    C.live.erase(it);
+    if (device_idle) {
+        // the device is idle: every stream's cached blocks are free for any stream
+        for (auto& kv : C.by_stream)
+            for (auto& b : kv.second)
+                for (void* q : b.second) C.idle[b.first].push_back(q);
+        C.idle_bytes += C.stream_bytes;
+        C.stream_bytes = 0;
+        C.by_stream.clear();
+        if (C.idle_bytes + cls > CACHE_MAX_TOTAL) {
+            lk.unlock();
+            (void)hipFreeAsync(p, nullptr);
+            return;
+        }
+        C.idle[cls].push_back(p);
+        C.idle_bytes += cls;
+        return;
+    }
+    C.by_stream[st][cls].push_back(p);
+    C.stream_bytes += cls;
+}
+
+size_t dx_cache_idle_bytes()
+{
+    Cache& C = cache();
+    std::lock_guard<std::mutex> lk(C.m);
+    return C.idle_bytes + C.stream_bytes;
+}
+
+size_t dx_pool_idle_bytes()
 {
     int dev = 0;
     hipMemPool_t pool = nullptr;
-    if (hipDeviceSynchronize() != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess)
-        return;
-    (void)hipMemPoolTrimTo(pool, 0);
+    uint64_t reserved = 0, used = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess ||
+        hipMemPoolGetAttribute(pool, hipMemPoolAttrReservedMemCurrent, &reserved) != hipSuccess ||
+        hipMemPoolGetAttribute(pool, hipMemPoolAttrUsedMemCurrent, &used) != hipSuccess)
+        return 0;
+    return (reserved > used ? (size_t)(reserved - used) : 0) + dx_cache_idle_bytes();
 }
 }  // namespace dccrgx
 

@@ -20,56 +20,11 @@
 #include <cstring>
 #include <set>
 
+#include "exview.hpp"
 #include "face.hpp"
 #include "grid.hpp"
 
 namespace dccrgx {
-
-// lookups of existing leaves: id -> global leaf index (position in the
-// ascending leaf list).  Grids whose id space is small enough keep a rank
-// bitmap: one bit per possible id (dccrg_mapping.hpp's ids are dense per
-// level) plus, per 64-bit word, the number of leaves before it -- a lookup is
-// one word load, a popcount and one rank load, and neighbors' ids are close
-// together (same level: the same z-plane +-1), so the words stay in L2.
-// Other grids use an open-addressing hash (2x capacity, linear probing).
-struct ExView {
-    MapParams mp;
-    const uint64_t* keys;
-    const uint32_t* vals;
-    uint64_t mask;
-    const uint64_t* bits;   // rank bitmap (null: use the hash)
-    const uint32_t* rank;
-    int32_t per[3];
-};
-
-__host__ __device__ inline uint64_t hmix(uint64_t x)
-{
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdull;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ull;
-    x ^= x >> 33;
-    return x;
-}
-
-__device__ inline int64_t ex_find(const ExView& v, uint64_t id)
-{
-    if (id == 0) return -1;
-    if (v.bits) {
-        if (id > v.mp.last_cell) return -1;
-        const uint64_t w = v.bits[id >> 6];
-        const uint32_t b = (uint32_t)(id & 63);
-        if (!((w >> b) & 1ull)) return -1;
-        return (int64_t)v.rank[id >> 6] + __popcll(w & ((1ull << b) - 1ull));
-    }
-    uint64_t h = hmix(id) & v.mask;
-    for (;;) {
-        const uint64_t k = v.keys[h];
-        if (k == id) return (int64_t)v.vals[h];
-        if (k == 0) return -1;
-        h = (h + 1) & v.mask;
-    }
-}
 
 __global__ void __launch_bounds__(256) k_hash_insert(const uint64_t* __restrict__ ids, size_t n,
                                                      unsigned long long* keys, uint32_t* vals, uint64_t mask)
@@ -825,6 +780,16 @@ static unsigned grid_for(uint64_t n)
     return (unsigned)g;
 }
 
+__global__ void k_check_lookup(ExView v, const uint64_t* __restrict__ leaves, uint64_t n, int32_t* err)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        if (ex_find(v, leaves[i]) != (int64_t)i) {
+            atomicAdd(err, 1);
+            atomicCAS(err + 1, 0, (int32_t)i + 1);
+        }
+}
+
 static ExView view(const dccrgx_grid* grid)
 {
     ExView v{};
@@ -837,6 +802,8 @@ static ExView view(const dccrgx_grid* grid)
     for (int d = 0; d < 3; d++) v.per[d] = grid->params.periodic[d] ? 1 : 0;
     return v;
 }
+
+ExView explicit_view(const dccrgx_grid* grid) { return view(grid); }
 
 __global__ void __launch_bounds__(256) k_counts_to_row(const uint32_t* __restrict__ cnt, uint64_t n,
                                                        uint64_t* __restrict__ row)
@@ -916,13 +883,17 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
 
 static int sync_slots(dccrgx_grid* grid, bool slot_map_changed);
 
-int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
+int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t* d_leaves)
 {
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
-    DX_CHECK(n > 0 && n < (1ull << 32), DCCRGX_EINVAL, "leaf count %zu", n);
-    PhaseTimer T("explicit_init");
     auto* E = new Explicit();
+    E->d_leaves = d_leaves;  // adopted (ascending, unique, = leaves): freed with E from here on
+    if (n == 0 || n >= (1ull << 32)) {
+        explicit_free(E);
+        return set_error(DCCRGX_EINVAL, "leaf count %zu", n);
+    }
+    PhaseTimer T("explicit_init");
     if (grid->spare_host) {  // the previous state's host arrays: their capacity is reused
         Explicit* S = grid->spare_host;
         E->leaves.swap(S->leaves);
@@ -940,15 +911,17 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     }
     grid->ex = E;
     E->leaves.assign(leaves, leaves + n);
-    if (!std::is_sorted(E->leaves.begin(), E->leaves.end())) std::sort(E->leaves.begin(), E->leaves.end());
-    E->leaves.erase(std::unique(E->leaves.begin(), E->leaves.end()), E->leaves.end());
+    if (!d_leaves) {
+        if (!std::is_sorted(E->leaves.begin(), E->leaves.end())) std::sort(E->leaves.begin(), E->leaves.end());
+        E->leaves.erase(std::unique(E->leaves.begin(), E->leaves.end()), E->leaves.end());
+    }
     DX_CHECK(E->leaves[0] > 0 && E->leaves.back() <= grid->map.last_cell, DCCRGX_EINVAL, "invalid cell %llu",
              (unsigned long long)(E->leaves[0] == 0 ? 0 : E->leaves.back()));
     E->n = E->leaves.size();
     E->build_dir();
     uint64_t cap = 16;
     while (cap < 2 * E->n) cap <<= 1;
-    DX_TRY(upload(grid->ctx, E->leaves, &E->d_leaves, st));
+    if (!E->d_leaves) DX_TRY(upload(grid->ctx, E->leaves, &E->d_leaves, st));
     // the rank bitmap when it is small (at most 1 GiB, and at most 16x the hash)
     const uint64_t nw = (grid->map.last_cell >> 6) + 1;
     if (nw <= (1ull << 26) && nw * 12 <= 16 * cap * 12) {
@@ -969,6 +942,21 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     }
     DX_HIP(hipGetLastError());
     T.lap("leaves+lookup");
+    if (getenv_flag("DCCRGX_CHECK_INIT")) {  // diagnosis: device leaves and lookups against the host list
+        std::vector<uint64_t> back(E->n);
+        DX_TRY(dx_d2h(ctx, back.data(), E->d_leaves, E->n * 8, st));
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < E->n; i++) bad += back[i] != E->leaves[i];
+        int32_t* d_e = nullptr;
+        DX_HIP(dx_malloc(&d_e, 8));
+        DX_HIP(hipMemsetAsync(d_e, 0, 8, st));
+        hipLaunchKernelGGL(k_check_lookup, dim3(grid_for(E->n)), dim3(256), 0, st, view(grid), E->d_leaves, E->n, d_e);
+        int32_t e[2] = {0, 0};
+        DX_TRY(dx_d2h(ctx, e, d_e, 8, st));
+        dx_free(d_e);
+        std::fprintf(stderr, "[dccrgx] check_init n %llu leaves differing %llu lookups failing %d first %d bitmap %d\n",
+                     (unsigned long long)E->n, (unsigned long long)bad, e[0], e[1] - 1, E->d_bits != nullptr);
+    }
     // ownership: the process of the level-0 ancestor (no load balancing),
     // block partition or the grid's SFC table
     E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
@@ -1263,12 +1251,12 @@ int explicit_fetch_rows(const dccrgx_grid* grid, const Hood& h, const std::vecto
     uint32_t* d_g = nullptr;
     uint64_t* d_row = nullptr;  // n + 1 row pointers, then n neighbors_of lengths
     uint32_t* d_out = nullptr;
-    DX_HIP(hipMallocAsync((void**)&d_g, n * 4, st));
-    DX_HIP(hipMallocAsync((void**)&d_row, (2 * n + 1) * 8, st));
+    DX_HIP(ds_malloc(&d_g, n * 4, st));
+    DX_HIP(ds_malloc(&d_row, (2 * n + 1) * 8, st));
     auto done = [&](int code) {
-        (void)hipFreeAsync(d_g, st);
-        (void)hipFreeAsync(d_row, st);
-        if (d_out) (void)hipFreeAsync(d_out, st);
+        (void)ds_free(d_g, st);
+        (void)ds_free(d_row, st);
+        if (d_out) (void)ds_free(d_out, st);
         return code;
     };
     int s = dx_h2d(ctx, d_g, want.data(), n * 4, st);
@@ -1277,7 +1265,7 @@ int explicit_fetch_rows(const dccrgx_grid* grid, const Hood& h, const std::vecto
                        h.d_nto_row, d_row, d_row + n + 1);
     uint64_t total = 0;
     if ((s = device_scan_rows(d_row, n, st, &total)) != DCCRGX_OK) return done(s);
-    if (hipMallocAsync((void**)&d_out, std::max<uint64_t>(total, 1) * 4, st) != hipSuccess)
+    if (ds_malloc(&d_out, std::max<uint64_t>(total, 1) * 4, st) != hipSuccess)
         return done(set_error(DCCRGX_ENOMEM, "row cache"));
     hipLaunchKernelGGL(k_rows_cat, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)d_g, n, h.d_nof_row,
                        h.d_nof_g, h.d_nto_row, h.d_nto_g, (const uint64_t*)d_row, d_out);
@@ -1687,11 +1675,11 @@ int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t
     DX_CHECK(h.d_nof_row, DCCRGX_EINTERNAL, "no device lists for neighborhood %d", h.id);
     uint32_t* gq = nullptr;
     int32_t* d_err = nullptr;
-    DX_HIP(hipMallocAsync((void**)&gq, std::max<size_t>(n, 1) * 4, st));
-    DX_HIP(hipMallocAsync((void**)&d_err, 4, st));
+    DX_HIP(ds_malloc(&gq, std::max<size_t>(n, 1) * 4, st));
+    DX_HIP(ds_malloc(&d_err, 4, st));
     auto done = [&](int code) {
-        (void)hipFreeAsync(gq, st);
-        (void)hipFreeAsync(d_err, st);
+        (void)ds_free(gq, st);
+        (void)ds_free(d_err, st);
         return code;
     };
     if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));

@@ -740,14 +740,14 @@ int dccrgx_grid_destroy(dccrgx_grid* grid)
     for (auto& kv : grid->hoods) free_hood(kv.second);
     for (Field& f : grid->fields) dx_free(f.ptr);
     for (auto& b : grid->spare_bufs) dx_free(b.first);
+    dx_free(grid->d_sfc_owner);
     if (!grid->uniform) explicit_destroy(grid);
     delete grid->spare_host;
     amr_destroy(grid);
     load_state_free(grid);
     hipEventDestroy(grid->t0);
     hipEventDestroy(grid->t1);
-    delete grid;
-    dx_trim_pool();  // a destroyed grid's memory goes back to the driver (other users of the device)
+    delete grid;  // its memory stays in the device pool for the next grid (dx_pool_idle_bytes)
     return DCCRGX_OK;
 }
 

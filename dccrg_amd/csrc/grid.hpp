@@ -212,9 +212,24 @@ struct Explicit {
 struct LoadState;
 
 struct Amr {
+    // host view of the four sets (single request calls, amr_requests)
     FlatSet to_refine, not_to_refine, to_unrefine, not_to_unrefine;
     std::vector<uint64_t> new_cells, removed;
+    // device view (explicit grids, amr_dev.hip): RF_* flags over the current
+    // leaves, and the dont_refine ids that are not leaves.  Each view is
+    // refreshed from the other when it is next used.
+    uint32_t* d_flags = nullptr;
+    uint64_t flags_n = 0, flags_cap = 0;
+    std::vector<uint64_t> nr_other;
+    bool host_current = true, dev_current = false;
+    ~Amr() { (void)dx_free(d_flags); }
 };
+// amr_dev.hip
+int amr_dev_sync(dccrgx_grid* grid);
+int amr_host_sync(dccrgx_grid* grid);
+int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results);
+int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, std::vector<uint64_t>& leaves_host,
+                   std::vector<uint64_t>& retired, std::vector<uint64_t>& nr, bool* changed);
 
 
 struct CopySeg {
@@ -304,6 +319,7 @@ struct dccrgx_grid {
     dccrgx::Explicit* spare_host = nullptr;
     // SFC placement (params.partition): owner of each level-0 cell, id - 1
     std::vector<int32_t> sfc_owner;
+    int32_t* d_sfc_owner = nullptr;  // its device copy (AMR decisions), made on first use
     // kernel timing (dccrgx_kernel_timer)
     hipEvent_t t0 = nullptr, t1 = nullptr;
     double timed_ms = 0;
@@ -363,8 +379,9 @@ int explicit_fetch_rows(const dccrgx_grid* grid, const Hood& h, const std::vecto
 int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, uint64_t* ids,
                        size_t cap, size_t* n);
 int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device);
-// explicit grid state over an ascending leaf list (no neighborhoods built)
-int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n);
+// explicit grid state over an ascending leaf list (no neighborhoods built);
+// d_leaves: the same list on the device, adopted by the grid (amr_dev.hip)
+int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t* d_leaves = nullptr);
 int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id);
 // the slot read and written for a cell on this rank (-1: none), halo.hip
 int64_t host_primary_slot(const dccrgx_grid* grid, uint64_t id);

@@ -48,21 +48,31 @@ int set_error(int code, const char* fmt, ...);
 // dx_free waits for the device first, as hipFree does.
 void dx_slow_note(const char* what, size_t bytes, double ms);  // DCCRGX_TIMING: allocations over 1 ms
 
-// return the pool's unused memory to the driver (after the device is idle):
-// when a grid is destroyed, and before an allocation is retried
-void dx_trim_pool();
+// memory the pool holds for reuse (reserved minus in use): free for the
+// library's purposes.  The pool is never trimmed: on /opt/rocm's 7.2 runtime
+// (a process that loads the library before torch, whose bundled runtime has
+// the same soname), after hipMemPoolTrimTo a pinned-host copy into a fresh
+// stream-ordered allocation could land nowhere (a grid's leaf upload read
+// back wrong, tools/rt_bisect.py), so freed memory stays in the pool.
+size_t dx_pool_idle_bytes();
+
+// Library allocations go through a caching layer over the pool (core.hip):
+// blocks up to 256 MiB are kept in size classes when freed and handed out
+// again without a runtime call.  hipFreeAsync costs ~35 us on torch's bundled
+// HIP runtime (4 us on /opt/rocm's) and an adaptive step freed ~60 scratch
+// buffers -- 2 ms of the step (tools/api_census.py).  A block freed with
+// ds_free on a stream is reused only by that stream (stream order keeps it
+// safe); blocks freed with dx_free / FreeBatch (after a device-wide wait)
+// are reused by any.
+hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_stream);
+void dx_cache_free(void* p, hipStream_t st, bool device_idle);
+size_t dx_cache_idle_bytes();
 
 template <class T>
 inline hipError_t dx_malloc(T** p, size_t bytes)
 {
     const auto t0 = std::chrono::steady_clock::now();
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(p), bytes ? bytes : 1, nullptr);
-    if (e == hipErrorOutOfMemory) {  // memory held by the pool may still be free for the driver
-        (void)hipGetLastError();
-        dx_trim_pool();
-        e = hipMallocAsync(reinterpret_cast<void**>(p), bytes ? bytes : 1, nullptr);
-    }
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    hipError_t e = dx_cache_alloc(reinterpret_cast<void**>(p), bytes ? bytes : 1, nullptr, true);
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (ms > 1.0) dx_slow_note("dx_malloc", bytes, ms);
     return e;
@@ -73,7 +83,7 @@ inline hipError_t dx_free(void* p)
     if (!p) return hipSuccess;
     const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipFreeAsync(p, nullptr);
+    if (e == hipSuccess) dx_cache_free(p, nullptr, true);
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (ms > 1.0) dx_slow_note("dx_free", 0, ms);
     return e;
@@ -90,7 +100,7 @@ struct FreeBatch {
     ~FreeBatch()
     {
         if (v.empty() || hipDeviceSynchronize() != hipSuccess) return;
-        for (void* p : v) (void)hipFreeAsync(p, nullptr);
+        for (void* p : v) dx_cache_free(p, nullptr, true);
     }
 };
 
@@ -102,16 +112,14 @@ struct FreeBatch {
 template <class T>
 inline hipError_t ds_malloc(T** p, size_t bytes, hipStream_t st)
 {
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(p), bytes ? bytes : 1, st);
-    if (e == hipErrorOutOfMemory) {
-        (void)hipGetLastError();
-        dx_trim_pool();
-        e = hipMallocAsync(reinterpret_cast<void**>(p), bytes ? bytes : 1, st);
-    }
-    return e;
+    return dx_cache_alloc(reinterpret_cast<void**>(p), bytes ? bytes : 1, st, false);
 }
 
-inline hipError_t ds_free(void* p, hipStream_t st) { return p ? hipFreeAsync(p, st) : hipSuccess; }
+inline hipError_t ds_free(void* p, hipStream_t st)
+{
+    if (p) dx_cache_free(p, st, false);
+    return hipSuccess;
+}
 
 #define DX_TRY(expr)                       \
     do {                                   \

@@ -184,9 +184,9 @@ static int uniform_rows(const dccrgx_grid* grid, const Hood& h, const int32_t* d
     // one scratch block: the tile sums (scanned in place), the error word, the total
     uint64_t* scratch = nullptr;
     const size_t words = tiles + 2;
-    DX_HIP(hipMallocAsync((void**)&scratch, words * 8, st));
+    DX_HIP(ds_malloc(&scratch, words * 8, st));
     auto done = [&](int code) {
-        (void)hipFreeAsync(scratch, st);
+        (void)ds_free(scratch, st);
         return code;
     };
     if (hipMemsetAsync(scratch, 0, words * 8, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
@@ -459,10 +459,10 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
                            h->d_of_c, h->K, cells, n, row, ids, off3, sc, sc, sc);
     } else if (n) {  // per-thread rows (the cells were checked by uniform_rows)
         int32_t* d_err = nullptr;
-        DX_HIP(hipMallocAsync((void**)&d_err, 4, st));
+        DX_HIP(ds_malloc(&d_err, 4, st));
         hipLaunchKernelGGL(k_uniform_nbrs, dim3(grid_for(n)), dim3(256), 0, st, g, h->d_of_c, h->K, cells,
                            n, row, ids, off3, d_err, sc, sc, sc);
-        DX_HIP(hipFreeAsync(d_err, st));
+        DX_HIP(ds_free(d_err, st));
     }
     DX_HIP(hipGetLastError());
     return DCCRGX_OK;

@@ -98,14 +98,14 @@ int device_inclusive_scan(uint64_t* x, uint64_t m, hipStream_t st)
     const uint64_t nt = (m + STILE - 1) / STILE;
     DX_CHECK(nt < (1ull << 31), DCCRGX_EINVAL, "scan of %llu elements", (unsigned long long)m);
     uint64_t* sums = nullptr;
-    DX_HIP(hipMallocAsync((void**)&sums, nt * 8, st));
+    DX_HIP(ds_malloc(&sums, nt * 8, st));
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)nt), dim3(ST), 0, st, x, m, sums);
     if (nt > 1) {
         hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(ST), 0, st, sums, nt);
         hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nt), dim3(ST), 0, st, x, m, (const uint64_t*)sums);
     }
     DX_HIP(hipGetLastError());
-    DX_HIP(hipFreeAsync(sums, st));
+    DX_HIP(ds_free(sums, st));
     return DCCRGX_OK;
 }
 

@@ -324,6 +324,16 @@ class Dccrg:
     def dont_refine(self, cell: int) -> bool:
         return self._request(lib().dccrgx_dont_refine, cell)
 
+    def request_cells(self, kind: int, ids) -> np.ndarray:
+        """The request call `kind` (AMR_REFINE, AMR_DONT_REFINE, AMR_UNREFINE,
+        AMR_DONT_UNREFINE) for every id, in order, as one batch (on the device
+        for explicit grids); the calls' bool results."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        res = np.zeros(max(ids.size, 1), dtype=np.int32)
+        check(lib().dccrgx_amr_request_cells(self._h, kind, ids.ctypes.data_as(X._u64p), ids.size,
+                                             res.ctypes.data_as(X._i32p)))
+        return res[:ids.size].astype(bool)
+
     def amr_requests(self):
         """This rank's four pending request sets (refine, dont_refine,
         unrefine, dont_unrefine), for the all-gather of stop_refining."""
@@ -340,16 +350,19 @@ class Dccrg:
         """Collective (dccrg.hpp:3483-3507).  all_requests: the union over all
         ranks of amr_requests(); gathered with torch.distributed when the
         grid has several ranks and it is not given."""
+        if all_requests is None and self.ctx.comm_size == 1:
+            # one rank: its own requests are the union (they stay on the device)
+            n_new = C.c_size_t()
+            check(lib().dccrgx_stop_refining(self._h, None, None, C.byref(n_new)))
+            self._refresh_info()
+            return self.get_new_cells()
         if all_requests is None:
+            import torch.distributed as dist
             mine = self.amr_requests()
-            if self.ctx.comm_size == 1:
-                all_requests = mine
-            else:
-                import torch.distributed as dist
-                got = [None] * self.ctx.comm_size
-                dist.all_gather_object(got, [a.tolist() for a in mine])
-                all_requests = [np.unique(np.concatenate([np.asarray(g[k], dtype=np.uint64) for g in got]))
-                                for k in range(4)]
+            got = [None] * self.ctx.comm_size
+            dist.all_gather_object(got, [a.tolist() for a in mine])
+            all_requests = [np.unique(np.concatenate([np.asarray(g[k], dtype=np.uint64) for g in got]))
+                            for k in range(4)]
         sets = [_u64(a) for a in all_requests]
         ptrs = (X._u64p * 4)(*[a.ctypes.data_as(X._u64p) for a in sets])
         counts = (C.c_size_t * 4)(*[a.size for a in sets])
@@ -706,14 +719,20 @@ class Dccrg:
         return info, hdr.raw[:header_bytes], geo.raw
 
     @classmethod
-    def start_loading_grid_data(cls, ctx: "Context", name: str, offset: int = 0, header_bytes: int = 0):
+    def start_loading_grid_data(cls, ctx: "Context", name: str, offset: int = 0, header_bytes: int = 0,
+                                partition: str = "block"):
         """Dccrg::start_loading_grid_data (dccrg.hpp:1815-2105): a grid of the
-        file's cells on `ctx`.  Returns (grid, header bytes, geometry blob);
-        add fields, then continue_loading_grid_data(fields), then
-        finish_loading_grid_data()."""
+        file's cells on `ctx`, placed by `partition` ("block" or "sfc", as
+        set_initial_partition; the file records no placement).  Returns
+        (grid, header bytes, geometry blob); add fields, then
+        continue_loading_grid_data(fields), then finish_loading_grid_data()."""
         info, hdr, geo = cls.read_file_info(name, offset, header_bytes)
         g = cls()
         p = info.params
+        if partition.lower() not in ("block", "sfc"):
+            raise ValueError(f"unknown partition {partition!r}")
+        p.partition = X.PARTITION_SFC if partition.lower() == "sfc" else X.PARTITION_BLOCK
+        g._partition = p.partition
         g._length = tuple(int(v) for v in p.length)
         g._max_ref_lvl = int(p.max_ref_lvl)
         g._periodic = tuple(bool(v) for v in p.periodic)

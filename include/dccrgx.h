@@ -440,12 +440,17 @@ int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result
 int dccrgx_dont_unrefine(dccrgx_grid* grid, uint64_t cell, int32_t* result);
 /* Dccrg::dont_refine, dccrg.hpp:2768-2806 */
 int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result);
-/* the request call of `kind` (DCCRGX_AMR_*) for each id in order; results optional */
+/* the request call of `kind` (DCCRGX_AMR_*) for each id in order; results
+ * optional.  On explicit (mixed-level) grids the whole batch runs on the
+ * device (amr_dev.hip) with the results of the calls made in this order. */
 int dccrgx_amr_request_cells(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results);
 /* this rank's pending request set `which` (DCCRGX_AMR_*), ascending; ids == NULL: count only */
 int dccrgx_amr_requests(const dccrgx_grid* grid, int32_t which, uint64_t* ids, size_t cap, size_t* n);
 /* Dccrg::stop_refining, dccrg.hpp:3483-3507: sets[k] / counts[k] = union over
- * all ranks of request set k; n_new = cells created on this rank */
+ * all ranks of request set k; sets == NULL: this rank's own requests (one
+ * rank: they are the union; they then never leave the device).  The
+ * decisions and the new leaf set are computed on the device; n_new = cells
+ * created on this rank */
 int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const size_t* counts,
                          size_t* n_new);
 /* the cells the last stop_refining created on this rank (ascending; the

@@ -133,6 +133,90 @@ def test_random_request_sequences(case):
         g.close()
 
 
+BATCH_CASES = [  # length, M, periodic, hood, P, rounds, seed
+    ((6, 5, 1), 2, (True, True, False), 0, 1, 5, 10),
+    ((4, 4, 3), 2, (False, True, True), 1, 2, 4, 11),
+    ((5, 4, 2), 2, (True, False, False), 1, 3, 3, 12),
+    ((4, 3, 3), 3, (True, True, True), 0, 1, 4, 13),
+    ((3, 3, 2), 2, (False, False, False), 2, 2, 3, 14),
+]
+KINDS = (("refine_completely", 0), ("dont_unrefine", 3), ("unrefine_completely", 2), ("dont_refine", 1))
+
+
+@pytest.mark.parametrize("case", BATCH_CASES)
+def test_batched_requests_match_sequential_calls(case):
+    """dccrgx_amr_request_cells on explicit grids runs each batch on the
+    device (amr_dev.hip); its results and the four sets afterwards equal the
+    reference's calls made one by one in the same order (the oracle), with
+    whole sibling groups, repeated ids, cells of other ranks and ids that are
+    not leaves in the batches; stop_refining then decides on the device."""
+    length, M, per, hood, P, rounds, seed = case
+    rng = np.random.default_rng(seed)
+    leaves = [int(c) for c in O.random_balanced_leaves(length, M, per, hood, 12, seed)]
+    o = AmrOracle(length, M, per, hood, P, leaves=leaves)
+    grids = make_ranks(length, M, per, hood, P, leaves=np.array(leaves, dtype=np.uint64))
+    m = O.Mapping(length, M)
+    for rnd in range(rounds):
+        cells = o.cells()
+        for r in range(P):
+            for name, kind in KINDS:
+                if kind == 1 and rng.integers(2):
+                    continue  # dont_refine in some rounds only
+                pick = [int(c) for c in rng.choice(cells, min(len(cells), 10), replace=False)]
+                extra = []
+                for c in pick[:4]:  # whole sibling groups and their repeats
+                    extra += [int(s) for s in m.get_siblings(c) if s] + [c]
+                ids = pick + extra
+                ids += [int(m.get_all_children(c)[0]) for c in pick[:2] if o.level(c) < M]  # not leaves
+                ids = [i for i in ids if i] + [0]
+                rng.shuffle(ids)
+                got = grids[r].request_cells(kind, np.array(ids, dtype=np.uint64))
+                want = [getattr(o, name)(r, c) for c in ids]
+                assert [bool(x) for x in got] == want, (rnd, r, name)
+            sets = grids[r].amr_requests()
+            for k, ref in enumerate((o.to_refine, o.not_to_refine, o.to_unrefine, o.not_to_unrefine)):
+                assert [int(c) for c in sets[k]] == sorted(ref[r]), (rnd, r, k)
+        got = stop_all(grids)
+        want = o.stop_refining()
+        for r in range(P):
+            assert [int(c) for c in got[r]] == want[r]
+            assert [int(c) for c in grids[r].get_removed_cells()] == o.get_removed_cells(r)
+            grids[r].clear_refined_unrefined_data()
+        check_structure(grids, o)
+        assert o.max_level_difference() <= 1
+    for g in grids:
+        g.close()
+
+
+@pytest.mark.parametrize("P", [1, 2])
+def test_own_requests_stop_refining(P):
+    """stop_refining from each rank's own device state (sets == NULL, one
+    rank) equals the union path and the oracle; with two ranks the union is
+    gathered from the device sets (amr_requests)."""
+    length, M, per, hood = (6, 6, 1), 2, (True, True, False), 0
+    rng = np.random.default_rng(7)
+    leaves = [int(c) for c in O.random_balanced_leaves(length, M, per, hood, 12, 3)]
+    o = AmrOracle(length, M, per, hood, P, leaves=leaves)
+    grids = make_ranks(length, M, per, hood, P, leaves=np.array(leaves, dtype=np.uint64))
+    for rnd in range(4):
+        cells = o.cells()
+        for r in range(P):
+            mine = [c for c in cells if o.owner(c) == r]
+            for name, kind in KINDS[:3]:
+                ids = [int(c) for c in rng.choice(mine, min(len(mine), 12), replace=False)]
+                grids[r].request_cells(kind, np.array(ids, dtype=np.uint64))
+                for c in ids:
+                    getattr(o, name)(r, c)
+        got = [grids[0].stop_refining()] if P == 1 else stop_all(grids)
+        want = o.stop_refining()
+        for r in range(P):
+            assert [int(c) for c in got[r]] == want[r]
+            grids[r].clear_refined_unrefined_data()
+        check_structure(grids, o)
+    for g in grids:
+        g.close()
+
+
 def test_cell_data_moves_with_refinement():
     """Surviving cells keep their data, new cells start at zero, refined
     parents and removed children stay readable until

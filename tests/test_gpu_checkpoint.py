@@ -113,6 +113,46 @@ def test_load_any_rank_count(tmp_path, case, writers, readers):
     assert sorted(seen) == sorted(int(x) for g in grids for x in g.local_cells())
 
 
+@pytest.mark.parametrize("writers,readers", [(2, 3), (3, 1)])
+@pytest.mark.parametrize("case", CASES[:2] + CASES[3:])
+def test_sfc_grid_round_trip(tmp_path, case, writers, readers):
+    """A file saved by an SFC-placed grid loads into an SFC-placed grid on
+    another rank count: each reader holds exactly the cells the SFC
+    placement gives it (same table as a fresh SFC grid, sfc.hip), with their
+    data."""
+    length, M, per, hood, _ = case
+    leaves = leaves_of(case)
+    grids = []
+    for r in range(writers):
+        c = D.Context(0, r, writers)
+        g = (D.Dccrg().set_initial_length(length).set_maximum_refinement_level(M).set_periodic(*per)
+             .set_neighborhood_length(hood).set_initial_partition("sfc").initialize(c, leaves=leaves))
+        g._keep = c
+        fill(g)
+        grids.append(g)
+    path = str(tmp_path / "g.dc")
+    save_all(grids, path, ["a", "b", "c"])
+    seen = []
+    for r in range(readers):
+        c = D.Context(0, r, readers)
+        g, _, _ = D.Dccrg.start_loading_grid_data(c, path, partition="sfc")
+        fresh = (D.Dccrg().set_initial_length(length).set_maximum_refinement_level(M).set_periodic(*per)
+                 .set_neighborhood_length(hood).set_initial_partition("sfc").initialize(c, leaves=leaves))
+        ids = g.local_cells()
+        assert np.array_equal(ids, fresh.local_cells())
+        fresh.close()
+        for f, t in (("a", np.uint32), ("b", np.float64), ("c", np.uint8)):
+            g.add_field(f, t)
+        g.continue_loading_grid_data(["a", "b", "c"])
+        g.finish_loading_grid_data()
+        assert np.array_equal(g.read_local("a"), (ids % 1000).astype(np.uint32))
+        assert np.array_equal(g.read_local("b"), ids.astype(np.float64) / 7)
+        seen += [int(x) for x in ids]
+        g.close()
+        c.close()
+    assert sorted(seen) == sorted(int(x) for g in grids for x in g.local_cells())
+
+
 @pytest.mark.parametrize("case", CASES[:3])
 def test_load_shuffled_oracle_file(tmp_path, case):
     """A file whose cells are listed in a random order, split over 4 writer

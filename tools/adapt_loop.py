@@ -7,6 +7,10 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if not os.environ.get("ADAPT_NO_TORCH"):
+    # as bench.py and the tests: torch first, so its bundled HIP runtime
+    # serves the process (ADAPT_NO_TORCH=1: /opt/rocm's, the library's own)
+    import torch  # noqa: F401
 import dccrg_amd as D  # noqa: E402
 from dccrg_amd import advection as A  # noqa: E402
 

@@ -2,7 +2,7 @@
 # Round-end style GPU pass: every -m gpu test, smoke, the bench line, and the
 # rocprofv3 kernel-trace + separate FETCH_SIZE / WRITE_SIZE passes of the
 # headline bench that tools/summarize_prof.py turns into profiles/<tag>_summary.json.
-# usage (through gpurun): bash tools/gpu_full.sh <tag> [skip-tests]
+# usage (through gpurun): bash tools/gpu_full.sh <tag> [skip-tests|tests] [noprof]
 set -o pipefail
 tag=${1:?tag}
 out=gpurun_out/$tag
@@ -17,6 +17,7 @@ if [ "$2" != "skip-tests" ]; then
 fi
 timeout -k 10 600 python -u bench.py > $out/bench.log 2>&1 || { tail -n 20 $out/bench.log; exit 1; }
 tail -n 1 $out/bench.log
+[ "$3" = "noprof" ] && { echo done; exit 0; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof/trace -o run -- \
   python3 bench.py --steps 5 --warmup 1 --no-secondary --no-halo-payload --no-cpu-baseline \
   > $out/prof_trace.log 2>&1 || { tail -n 20 $out/prof_trace.log; exit 1; }
