@@ -266,8 +266,8 @@ __global__ void __launch_bounds__(256) k_level0_ids(uint64_t* __restrict__ out, 
 // and keep their old data.  Transactional: the new state and every new field
 // array are built first; on any failure they are freed and the old grid is
 // left exactly as it was.
-int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired,
-            uint64_t* d_leaves = nullptr)
+int rebuild(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired,
+            uint64_t* d_leaves = nullptr)  // leaves: moved into the grid
 {
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
@@ -320,7 +320,7 @@ int rebuild(dccrgx_grid* grid, const std::vector<uint64_t>& leaves, const std::v
     PhaseTimer T("rebuild");
     grid->ex = nullptr;
     grid->uniform = false;
-    int s = explicit_init(grid, leaves.data(), leaves.size(), d_leaves);  // adopts d_leaves
+    int s = explicit_init(grid, leaves.data(), leaves.size(), d_leaves, &leaves);  // adopts d_leaves
     T.lap("explicit_init");
     if (s == DCCRGX_OK) grid->ex->defer_fields = true;
     for (auto it = grid->hoods.begin(); s == DCCRGX_OK && it != grid->hoods.end(); ++it)

@@ -991,13 +991,15 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     hipLaunchKernelGGL(k_kept_flags, dim3(bN), dim3(256), 0, st, a, d_keep);
     size_t tb = 0, tb2 = 0, tb3 = 0;
     DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
-    DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb2, o.added, d_sorted, (int)cnt[0], 0, 64, st));
+    int bits = 1;  // ids are at most last_cell: sort only its bits
+    while (bits < 64 && (grid->map.last_cell >> bits)) bits++;
+    DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb2, o.added, d_sorted, (int)cnt[0], 0, bits, st));
     DX_HIP(hipcub::DeviceSelect::Unique(nullptr, tb3, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
     uint8_t* d_tmp;
     DX_TRY(S.get(&d_tmp, std::max({tb, tb2, tb3})));
     tb = tb2 = tb3 = std::max({tb, tb2, tb3});
     DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, tb, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
-    DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, tb2, o.added, d_sorted, (int)cnt[0], 0, 64, st));
+    DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, tb2, o.added, d_sorted, (int)cnt[0], 0, bits, st));
     DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, tb3, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
     uint64_t nk[2] = {0, 0};
     DX_TRY(dx_d2h(ctx, nk, d_cnt64, 16, st));

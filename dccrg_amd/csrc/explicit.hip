@@ -391,7 +391,7 @@ __global__ void __launch_bounds__(256) k_stencil_rows(const uint64_t* __restrict
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
-        if (ucnt[i] != ROW_LONG) continue;  // done by k_stencil_rows64 / k_stencil_rows_wave
+        if (ucnt[i] != ROW_LONG) continue;  // done by k_stencil_rows_seg / k_stencil_rows_wave
         const uint32_t r = local_g[i];
         Pair* a = tmp + tmp_row[i];
         const uint64_t m = nof_row[r + 1] - nof_row[r];
@@ -544,34 +544,11 @@ constexpr int WAVE_SORT_MAX = 1024;
 
 // bitonic sort of one element per lane across the wavefront (ascending by
 // lane), exchanges by cross-lane shuffles: no LDS
-__device__ __forceinline__ uint32_t wave_sort64_u32(uint32_t x)
+__device__ __forceinline__ uint32_t shfl_xor_any(uint32_t x, int j) { return __shfl_xor(x, j, 64); }
+__device__ __forceinline__ Pair shfl_xor_any(const Pair& x, int j)
 {
-    const int lane = threadIdx.x & 63;
-    for (int k = 2; k <= 64; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint32_t y = __shfl_xor(x, j, 64);
-            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-            x = keep_min ? (y < x ? y : x) : (y < x ? x : y);
-        }
-    return x;
-}
-
-__device__ __forceinline__ bool pair_less_(const Pair& a, const Pair& b);
-__device__ __forceinline__ Pair wave_sort64_pair(Pair x)
-{
-    const int lane = threadIdx.x & 63;
-    for (int k = 2; k <= 64; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            Pair y;
-            y.g = __shfl_xor(x.g, j, 64);
-            y.x = __shfl_xor(x.x, j, 64);
-            y.y = __shfl_xor(x.y, j, 64);
-            y.z = __shfl_xor(x.z, j, 64);
-            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-            const bool ylt = pair_less_(y, x);
-            if (keep_min == ylt) x = y;
-        }
-    return x;
+    return Pair{(uint32_t)__shfl_xor(x.g, j, 64), __shfl_xor(x.x, j, 64), __shfl_xor(x.y, j, 64),
+                __shfl_xor(x.z, j, 64)};
 }
 
 template <class T, class Less>
@@ -611,28 +588,57 @@ __device__ uint32_t wave_unique(const T* a, int m, Eq eq, Out out)
     return base;
 }
 
-// rows of at most 64 entries: one wave per row, one entry per lane, sorted
-// in registers; longer rows are flagged for the LDS / per-thread kernels
-__global__ void __launch_bounds__(256) k_sort_unique_rows64(const uint64_t* __restrict__ row, uint64_t n,
-                                                            uint32_t* __restrict__ v, uint32_t* __restrict__ ucnt)
+// bitonic sort across segments of W lanes (W | 64), ascending in every segment
+template <int W, class T, class Less>
+__device__ __forceinline__ T seg_sort(T x, Less less)
 {
+    const int lane = threadIdx.x & 63;
+    for (int k = 2; k <= W; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const T y = shfl_xor_any(x, j);
+            const bool up = k == W || (lane & k) == 0;
+            const bool keep_min = ((lane & j) == 0) == up;
+            if (keep_min == less(y, x)) x = y;
+        }
+    return x;
+}
+
+constexpr uint32_t ROW_PEND = 0xfffffffdu;  // row of 17..64 entries, for the 64-lane pass
+
+// rows sorted and made unique in registers, W lanes per row (64 / W rows per
+// wave): the short rows of face neighborhoods fill a wave 4 at a time.  A
+// row longer than W is flagged -- for the 64-lane pass (PEND_ONLY: the
+// flagged rows only), then for the LDS / per-thread kernels.
+template <int W, bool PEND_ONLY>
+__global__ void __launch_bounds__(256) k_sort_unique_rows_seg(const uint64_t* __restrict__ row, uint64_t n,
+                                                              uint32_t* __restrict__ v, uint32_t* __restrict__ ucnt)
+{
+    constexpr int R = 64 / W;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    for (uint64_t r = wave; r < n; r += waves) {
-        const uint64_t b = row[r];
-        const int m = (int)(row[r + 1] - b);
-        if (m > 64) {
-            if (lane == 0) ucnt[r] = m > WAVE_SORT_MAX ? ROW_LONG : ROW_MEDIUM;
-            continue;
+    const int lane = threadIdx.x & 63, sl = lane & (W - 1), seg = lane / W;
+    const uint64_t segmask = (W == 64 ? ~0ull : ((1ull << W) - 1ull)) << (seg * W);
+    for (uint64_t r0 = wave * R; r0 < n; r0 += waves * R) {
+        const uint64_t r = r0 + seg;
+        bool active = r < n && (!PEND_ONLY || ucnt[r] == ROW_PEND);
+        uint64_t b = 0;
+        int m = 0;
+        if (active) {
+            b = row[r];
+            m = (int)(row[r + 1] - b);
+            if (m > W) {
+                if (sl == 0) ucnt[r] = W < 64 ? ROW_PEND : (m > WAVE_SORT_MAX ? ROW_LONG : ROW_MEDIUM);
+                active = false;
+            }
         }
-        uint32_t x = lane < m ? v[b + lane] : 0xffffffffu;
-        x = wave_sort64_u32(x);
-        const uint32_t prev = __shfl_up(x, 1, 64);
-        const bool keep = lane < m && (lane == 0 || x != prev);
+        if (!__ballot(active)) continue;  // the whole wave idle (most rows in the 64-lane pass)
+        uint32_t x = active && sl < m ? v[b + sl] : 0xffffffffu;
+        x = seg_sort<W>(x, [](uint32_t a, uint32_t c) { return a < c; });
+        const uint32_t prev = __shfl_up(x, 1, W);
+        const bool keep = active && sl < m && (sl == 0 || x != prev);
         const uint64_t mask = __ballot(keep);
-        if (keep) v[b + __popcll(mask & ((1ull << lane) - 1ull))] = x;
-        if (lane == 0) ucnt[r] = (uint32_t)__popcll(mask);
+        if (keep) v[b + __popcll(mask & segmask & ((1ull << lane) - 1ull))] = x;
+        if (active && sl == 0) ucnt[r] = (uint32_t)__popcll(mask & segmask);
     }
 }
 
@@ -709,40 +715,50 @@ __global__ void __launch_bounds__(64) k_stencil_rows_wave(const uint64_t* __rest
     }
 }
 
-// rows of at most 64 entries in registers (see k_sort_unique_rows64)
-__global__ void __launch_bounds__(256) k_stencil_rows64(const uint64_t* __restrict__ nof_row,
-                                                        const uint32_t* __restrict__ nof_g,
-                                                        const int32_t* __restrict__ nof_off,
-                                                        const uint32_t* __restrict__ local_g, uint64_t nl,
-                                                        const uint64_t* __restrict__ tmp_row, Pair* __restrict__ tmp,
-                                                        uint32_t* __restrict__ ucnt)
+// the same for the stencil rows' (leaf, offset) pairs (see k_sort_unique_rows_seg)
+template <int W, bool PEND_ONLY>
+__global__ void __launch_bounds__(256) k_stencil_rows_seg(const uint64_t* __restrict__ nof_row,
+                                                          const uint32_t* __restrict__ nof_g,
+                                                          const int32_t* __restrict__ nof_off,
+                                                          const uint32_t* __restrict__ local_g, uint64_t nl,
+                                                          const uint64_t* __restrict__ tmp_row, Pair* __restrict__ tmp,
+                                                          uint32_t* __restrict__ ucnt)
 {
+    constexpr int R = 64 / W;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    for (uint64_t i = wave; i < nl; i += waves) {
-        const uint32_t r = local_g[i];
-        const uint64_t b = nof_row[r];
-        const int m = (int)(nof_row[r + 1] - b);
-        if (m > 64) {
-            if (lane == 0) ucnt[i] = m > WAVE_SORT_MAX ? ROW_LONG : ROW_MEDIUM;
-            continue;
+    const int lane = threadIdx.x & 63, sl = lane & (W - 1), seg = lane / W;
+    const uint64_t segmask = (W == 64 ? ~0ull : ((1ull << W) - 1ull)) << (seg * W);
+    for (uint64_t i0 = wave * R; i0 < nl; i0 += waves * R) {
+        const uint64_t i = i0 + seg;
+        bool active = i < nl && (!PEND_ONLY || ucnt[i] == ROW_PEND);
+        uint64_t b = 0;
+        int m = 0;
+        if (active) {
+            const uint32_t r = local_g[i];
+            b = nof_row[r];
+            m = (int)(nof_row[r + 1] - b);
+            if (m > W) {
+                if (sl == 0) ucnt[i] = W < 64 ? ROW_PEND : (m > WAVE_SORT_MAX ? ROW_LONG : ROW_MEDIUM);
+                active = false;
+            }
         }
+        if (!__ballot(active)) continue;  // the whole wave idle (most rows in the 64-lane pass)
         Pair x{0xffffffffu, 0x7fffffff, 0x7fffffff, 0x7fffffff};
-        if (lane < m) {
-            const uint64_t e = b + lane;
+        if (active && sl < m) {
+            const uint64_t e = b + sl;
             x = Pair{nof_g[e], nof_off[3 * e], nof_off[3 * e + 1], nof_off[3 * e + 2]};
         }
-        x = wave_sort64_pair(x);
+        x = seg_sort<W>(x, [](const Pair& a, const Pair& c) { return pair_less_(a, c); });
         Pair prev;
-        prev.g = __shfl_up(x.g, 1, 64);
-        prev.x = __shfl_up(x.x, 1, 64);
-        prev.y = __shfl_up(x.y, 1, 64);
-        prev.z = __shfl_up(x.z, 1, 64);
-        const bool keep = lane < m && (lane == 0 || !pair_eq(x, prev));
+        prev.g = __shfl_up(x.g, 1, W);
+        prev.x = __shfl_up(x.x, 1, W);
+        prev.y = __shfl_up(x.y, 1, W);
+        prev.z = __shfl_up(x.z, 1, W);
+        const bool keep = active && sl < m && (sl == 0 || !pair_eq(x, prev));
         const uint64_t mask = __ballot(keep);
-        if (keep) tmp[tmp_row[i] + __popcll(mask & ((1ull << lane) - 1ull))] = x;
-        if (lane == 0) ucnt[i] = (uint32_t)__popcll(mask);
+        if (keep) tmp[tmp_row[i] + __popcll(mask & segmask & ((1ull << lane) - 1ull))] = x;
+        if (active && sl == 0) ucnt[i] = (uint32_t)__popcll(mask & segmask);
     }
 }
 
@@ -850,18 +866,20 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
                       uint64_t** ids, int32_t** off, uint32_t** gidx, uint64_t* total, hipStream_t st)
 {
     const ExView v = view(grid);
-    int32_t* d_err = nullptr;
-    DX_HIP(ds_malloc(&d_err, 4, st));
-    DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
+    int32_t* d_err = nullptr;  // error word, then (at +8) the total
+    DX_HIP(ds_malloc(&d_err, 16, st));
+    DX_HIP(hipMemsetAsync(d_err, 0, 16, st));
     DX_HIP(hipMemsetAsync(row, 0, 8, st));
     if (n)
         hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(n)), dim3(256), 0, st, v, h.d_of_c, h.K, cells, n, row,
                            (uint64_t*)nullptr, (int32_t*)nullptr, (uint32_t*)nullptr, d_err);
     DX_HIP(hipGetLastError());
-    DX_TRY(device_scan_rows(row, n, st, total));
-    int32_t err = 0;
-    DX_TRY(dx_d2h(grid->ctx, &err, d_err, 4, st));
-    DX_HIP(hipStreamSynchronize(st));
+    DX_TRY(device_scan_rows(row, n, st, nullptr));
+    uint64_t back[2] = {0, 0};  // total, error word: one read-back
+    DX_HIP(hipMemcpyAsync(d_err + 2, row + n, 8, hipMemcpyDeviceToDevice, st));
+    DX_TRY(dx_d2h(grid->ctx, back, d_err, 16, st));
+    *total = back[1];
+    const int32_t err = (int32_t)(back[0] & 0xffffffffu);
     if (err) {
         ds_free(d_err, st);
         return set_error(err & 1 ? DCCRGX_ENOTFOUND : DCCRGX_EINTERNAL,
@@ -883,7 +901,8 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
 
 static int sync_slots(dccrgx_grid* grid, bool slot_map_changed);
 
-int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t* d_leaves)
+int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t* d_leaves,
+                  std::vector<uint64_t>* take)
 {
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
@@ -910,7 +929,8 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
         grid->spare_host = nullptr;
     }
     grid->ex = E;
-    E->leaves.assign(leaves, leaves + n);
+    if (take && take->data() == leaves && take->size() == n) E->leaves.swap(*take);  // the caller's list, moved
+    else E->leaves.assign(leaves, leaves + n);
     if (!d_leaves) {
         if (!std::is_sorted(E->leaves.begin(), E->leaves.end())) std::sort(E->leaves.begin(), E->leaves.end());
         E->leaves.erase(std::unique(E->leaves.begin(), E->leaves.end()), E->leaves.end());
@@ -918,7 +938,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
     DX_CHECK(E->leaves[0] > 0 && E->leaves.back() <= grid->map.last_cell, DCCRGX_EINVAL, "invalid cell %llu",
              (unsigned long long)(E->leaves[0] == 0 ? 0 : E->leaves.back()));
     E->n = E->leaves.size();
-    E->build_dir();
+    E->dir_valid = false;  // built on the first host lookup
     uint64_t cap = 16;
     while (cap < 2 * E->n) cap <<= 1;
     if (!E->d_leaves) DX_TRY(upload(grid->ctx, E->leaves, &E->d_leaves, st));
@@ -1318,21 +1338,22 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     DX_HIP(hipMemsetAsync(d_cur, 0, N * 4, st));
     hipLaunchKernelGGL(k_tr_count, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_cnt);
     uint64_t* d_trow = nullptr;
-    uint64_t ttot = 0;
-    DX_TRY(scan_counts_device(d_cnt, N, &d_trow, &ttot, st));
+    const uint64_t ttot = tot;  // the transpose has as many entries as neighbors_of: no read-back
+    DX_TRY(scan_counts_device(d_cnt, N, &d_trow, nullptr, st));
     DX_HIP(ds_malloc(&d_tmp, std::max<uint64_t>(ttot, 1) * 4, st));
     hipLaunchKernelGGL(k_tr_scatter, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_trow,
                        d_cur, d_tmp);
     DX_HIP(ds_malloc(&d_ucnt, N * 4, st));
-    hipLaunchKernelGGL(k_sort_unique_rows64, dim3((unsigned)std::min<uint64_t>((N + 3) / 4, 16384)), dim3(256), 0, st,
-                       d_trow, N, d_tmp, d_ucnt);
+    hipLaunchKernelGGL((k_sort_unique_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((N + 15) / 16, 16384)),
+                       dim3(256), 0, st, d_trow, N, d_tmp, d_ucnt);
+    hipLaunchKernelGGL((k_sort_unique_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((N + 3) / 4, 4096)),
+                       dim3(256), 0, st, d_trow, N, d_tmp, d_ucnt);
     hipLaunchKernelGGL(k_sort_unique_rows_wave, dim3((unsigned)std::min<uint64_t>(N, 4096)), dim3(64), 0, st, d_trow,
                        N, d_tmp, d_ucnt);
     hipLaunchKernelGGL(k_sort_unique_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, N, d_tmp, d_ucnt);
     DX_HIP(hipGetLastError());
-    uint64_t ntot = 0;
-    DX_TRY(scan_counts_device(d_ucnt, N, &h.d_nto_row, &ntot, st));
-    DX_HIP(ds_malloc(&h.d_nto_g, std::max<uint64_t>(ntot, 1) * 4, st));
+    DX_TRY(scan_counts_device(d_ucnt, N, &h.d_nto_row, nullptr, st));
+    DX_HIP(ds_malloc(&h.d_nto_g, std::max<uint64_t>(ttot, 1) * 4, st));  // unique entries: at most ttot
     hipLaunchKernelGGL(k_copy_rows_wave, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, d_trow, d_tmp, h.d_nto_row,
                        N, h.d_nto_g);
     DX_HIP(hipGetLastError());
@@ -1414,22 +1435,25 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     DX_HIP(ds_malloc(&d_pairs, std::max<uint64_t>(tmp_tot, 1) * sizeof(Pair), st));
     DX_HIP(ds_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4, st));
     if (nl) {
-        hipLaunchKernelGGL(k_stencil_rows64, dim3((unsigned)std::min<uint64_t>((nl + 3) / 4, 16384)), dim3(256), 0, st,
-                           h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
+        hipLaunchKernelGGL((k_stencil_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((nl + 15) / 16, 16384)),
+                           dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs,
+                           d_pc);
+        hipLaunchKernelGGL((k_stencil_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((nl + 3) / 4, 4096)),
+                           dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs,
+                           d_pc);
         hipLaunchKernelGGL(k_stencil_rows_wave, dim3((unsigned)std::min<uint64_t>(nl, 4096)), dim3(64), 0, st,
                            h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
         hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
                            h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
     }
-    uint64_t stot = 0;
-    DX_TRY(scan_counts_device(d_pc, nl, &h.d_st_row, &stot, st));
+    const uint64_t stot = tmp_tot;  // unique pairs: at most the rows' entries (no read-back)
+    DX_TRY(scan_counts_device(d_pc, nl, &h.d_st_row, nullptr, st));
     DX_HIP(ds_malloc(&h.d_st_slot, std::max<uint64_t>(stot, 1) * 4, st));
     DX_HIP(ds_malloc(&h.d_st_off, std::max<uint64_t>(stot, 1) * 12, st));
     if (nl)
         hipLaunchKernelGGL(k_stencil_slots_wave, dim3((unsigned)((nl + 63) / 64)), dim3(64), 0, st, d_tmp_row,
                            d_pairs, h.d_st_row, nl, E->d_slot_of_g, h.d_st_slot, h.d_st_off);
     DX_HIP(hipGetLastError());
-    DX_HIP(hipStreamSynchronize(st));
     ds_free(d_tmp_row, st);
     ds_free(d_pairs, st);
     ds_free(d_pc, st);

@@ -171,11 +171,15 @@ struct Explicit {
     // query it millions of times per adaptive step): a bucket directory over
     // the id range -- dir[b] = first leaf whose bucket is >= b, ~0.5 leaves
     // per bucket -- narrows each search to a bucket
-    std::vector<uint32_t> dir;
-    uint64_t dir_base = 0;
-    int dir_shift = 0;
-    void build_dir()
+    // (built on the first lookup after the leaf list changes: an adaptive
+    // step on one rank often needs none)
+    mutable std::vector<uint32_t> dir;
+    mutable uint64_t dir_base = 0;
+    mutable int dir_shift = 0;
+    mutable bool dir_valid = false;
+    void build_dir() const
     {
+        dir_valid = true;
         dir.clear();
         if (leaves.empty()) return;
         dir_base = leaves.front();
@@ -194,6 +198,7 @@ struct Explicit {
     }
     int64_t find(uint64_t c) const  // global index of a leaf, -1 if none
     {
+        if (!dir_valid) build_dir();
         if (dir.empty() || c < dir_base || c > leaves.back()) return -1;
         const uint64_t b = (c - dir_base) >> dir_shift;
         const auto lo = leaves.begin() + dir[b], hi = leaves.begin() + dir[b + 1];
@@ -381,7 +386,8 @@ int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, ui
 int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device);
 // explicit grid state over an ascending leaf list (no neighborhoods built);
 // d_leaves: the same list on the device, adopted by the grid (amr_dev.hip)
-int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t* d_leaves = nullptr);
+int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t* d_leaves = nullptr,
+                  std::vector<uint64_t>* take = nullptr);  // take: the vector holding `leaves`, moved from
 int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id);
 // the slot read and written for a cell on this rank (-1: none), halo.hip
 int64_t host_primary_slot(const dccrgx_grid* grid, uint64_t id);

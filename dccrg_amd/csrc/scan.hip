@@ -113,9 +113,12 @@ int device_scan_rows(uint64_t* row, uint64_t n, hipStream_t st, uint64_t* total)
 {
     DX_HIP(hipMemsetAsync(row, 0, 8, st));
     DX_TRY(device_inclusive_scan(row + 1, n, st));
-    if (total) {
-        DX_HIP(hipMemcpyAsync(total, row + n, 8, hipMemcpyDeviceToHost, st));
+    if (total) {  // through a pinned word: a pageable read-back costs a staging copy
+        static thread_local uint64_t* word = nullptr;
+        if (!word) DX_HIP(hipHostMalloc((void**)&word, 64, hipHostMallocDefault));
+        DX_HIP(hipMemcpyAsync(word, row + n, 8, hipMemcpyDeviceToHost, st));
         DX_HIP(hipStreamSynchronize(st));
+        *total = *word;
     }
     return DCCRGX_OK;
 }

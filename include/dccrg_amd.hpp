@@ -156,6 +156,85 @@ inline bool is_named(MPI_Datatype t)
     return comb == MPI_COMBINER_NAMED;
 }
 
+// A derived datatype as byte blocks (displacement from the cell's address,
+// length) in type-map order.  On a homogeneous run MPI_Pack's bytes are these
+// blocks concatenated, so a cell is packed by memcpy instead of
+// MPI_Type_commit + MPI_Pack + MPI_Type_free per cell and exchange (the
+// reference commits every cell's type per exchange, dccrg.hpp:10850-10925).
+// Combiners outside the usual constructors (subarray, darray, Fortran types)
+// return false and are packed through MPI.
+struct Blocks {
+    std::vector<std::pair<MPI_Aint, MPI_Aint>> b;
+    MPI_Aint bytes = 0;
+    void add(MPI_Aint d, MPI_Aint n)
+    {
+        if (n <= 0) return;
+        bytes += n;
+        if (!b.empty() && b.back().first + b.back().second == d) b.back().second += n;
+        else b.emplace_back(d, n);
+    }
+};
+
+inline bool flatten(MPI_Datatype t, MPI_Aint count, MPI_Aint disp, Blocks& out, int depth = 0)
+{
+    if (depth > 32) return false;
+    int ni = 0, na = 0, nd = 0, comb = 0;
+    MPI_Type_get_envelope(t, &ni, &na, &nd, &comb);
+    MPI_Aint lb = 0, ext = 0;
+    MPI_Type_get_extent(t, &lb, &ext);
+    if (comb == MPI_COMBINER_NAMED) {
+        int sz = 0;
+        MPI_Type_size(t, &sz);
+        if ((MPI_Aint)sz == ext) out.add(disp, count * sz);  // contiguous repetitions
+        else
+            for (MPI_Aint c = 0; c < count; c++) out.add(disp + c * ext, sz);  // e.g. MPI_DOUBLE_INT's gap
+        return true;
+    }
+    std::vector<int> ints(ni);
+    std::vector<MPI_Aint> adds(na);
+    std::vector<MPI_Datatype> types(nd);
+    MPI_Type_get_contents(t, ni, na, nd, ints.data(), adds.data(), types.data());
+    MPI_Aint lb0 = 0, ext0 = 0;
+    if (nd) MPI_Type_get_extent(types[0], &lb0, &ext0);
+    bool ok = true;
+    for (MPI_Aint c = 0; c < count && ok; c++) {
+        const MPI_Aint at = disp + c * ext;
+        switch (comb) {
+        case MPI_COMBINER_DUP:
+        case MPI_COMBINER_RESIZED: ok = flatten(types[0], 1, at, out, depth + 1); break;
+        case MPI_COMBINER_CONTIGUOUS: ok = flatten(types[0], ints[0], at, out, depth + 1); break;
+        case MPI_COMBINER_VECTOR:
+            for (int i = 0; i < ints[0] && ok; i++)
+                ok = flatten(types[0], ints[1], at + (MPI_Aint)i * ints[2] * ext0, out, depth + 1);
+            break;
+        case MPI_COMBINER_HVECTOR:
+            for (int i = 0; i < ints[0] && ok; i++) ok = flatten(types[0], ints[1], at + i * adds[0], out, depth + 1);
+            break;
+        case MPI_COMBINER_INDEXED:
+            for (int i = 0; i < ints[0] && ok; i++)
+                ok = flatten(types[0], ints[1 + i], at + (MPI_Aint)ints[1 + ints[0] + i] * ext0, out, depth + 1);
+            break;
+        case MPI_COMBINER_HINDEXED:
+            for (int i = 0; i < ints[0] && ok; i++) ok = flatten(types[0], ints[1 + i], at + adds[i], out, depth + 1);
+            break;
+        case MPI_COMBINER_INDEXED_BLOCK:
+            for (int i = 0; i < ints[0] && ok; i++)
+                ok = flatten(types[0], ints[1], at + (MPI_Aint)ints[2 + i] * ext0, out, depth + 1);
+            break;
+        case MPI_COMBINER_HINDEXED_BLOCK:
+            for (int i = 0; i < ints[0] && ok; i++) ok = flatten(types[0], ints[1], at + adds[i], out, depth + 1);
+            break;
+        case MPI_COMBINER_STRUCT:
+            for (int i = 0; i < ints[0] && ok; i++) ok = flatten(types[i], ints[1 + i], at + adds[i], out, depth + 1);
+            break;
+        default: ok = false;
+        }
+    }
+    for (MPI_Datatype& ty : types)
+        if (!is_named(ty)) MPI_Type_free(&ty);
+    return ok;
+}
+
 // Host-staged transport over MPI (dccrgx_host_transport) for ranks that
 // share a GPU -- RCCL refuses two ranks on one device.  One update's
 // messages go as the reference's transfer engine moves them: Irecv / Isend
@@ -1291,8 +1370,10 @@ private:
     // datatypes -- every caller's cells but variable_neighbour_data's derived
     // structs -- are contiguous: their packed form is the bytes themselves,
     // so they are copied directly with the type's size looked up once.
-    // Derived datatypes go through MPI_Type_commit / MPI_Pack / MPI_Type_free
-    // (the reference frees them after use as well, dccrg.hpp:10915-10925).
+    // Derived datatypes are flattened into byte blocks (detail::flatten) and
+    // copied; only unusual constructors go through MPI_Type_commit / MPI_Pack.
+    // The caller's derived type is freed after use, as the reference frees
+    // it (dccrg.hpp:10915-10925).
     int named_size(MPI_Datatype t)
     {
         auto it = type_size_.find(t);
@@ -1307,9 +1388,14 @@ private:
         auto d = detail::cell_datatype(c, id, sender, receiver, receiving, hood);
         MPI_Datatype t = std::get<2>(d);
         if (detail::is_named(t)) return std::get<1>(d) * named_size(t);
-        MPI_Type_commit(&t);
+        detail::Blocks fb;
         int sz = 0;
-        MPI_Pack_size(std::get<1>(d), t, comm_, &sz);
+        if (detail::flatten(t, std::get<1>(d), 0, fb)) {
+            sz = (int)fb.bytes;
+        } else {
+            MPI_Type_commit(&t);
+            MPI_Pack_size(std::get<1>(d), t, comm_, &sz);
+        }
         MPI_Type_free(&t);
         return sz;
     }
@@ -1322,6 +1408,18 @@ private:
             const size_t at = buf.size();
             buf.resize(at + n);
             if (n) std::memcpy(buf.data() + at, std::get<0>(d), n);
+            return;
+        }
+        detail::Blocks fb;
+        if (detail::flatten(t, std::get<1>(d), 0, fb)) {
+            size_t at = buf.size();
+            buf.resize(at + (size_t)fb.bytes);
+            const uintptr_t src = reinterpret_cast<uintptr_t>(std::get<0>(d));  // MPI_BOTTOM + absolute displacements too
+            for (const auto& blk : fb.b) {
+                std::memcpy(buf.data() + at, reinterpret_cast<const void*>(src + blk.first), (size_t)blk.second);
+                at += (size_t)blk.second;
+            }
+            MPI_Type_free(&t);
             return;
         }
         MPI_Type_commit(&t);
@@ -1341,6 +1439,16 @@ private:
             const size_t n = (size_t)std::get<1>(d) * named_size(t);
             if (n) std::memcpy(std::get<0>(d), buf.data() + pos, n);
             pos += (int)n;
+            return;
+        }
+        detail::Blocks fb;
+        if (detail::flatten(t, std::get<1>(d), 0, fb)) {
+            const uintptr_t dst = reinterpret_cast<uintptr_t>(std::get<0>(d));
+            for (const auto& blk : fb.b) {
+                std::memcpy(reinterpret_cast<void*>(dst + blk.first), buf.data() + pos, (size_t)blk.second);
+                pos += (int)blk.second;
+            }
+            MPI_Type_free(&t);
             return;
         }
         MPI_Type_commit(&t);

@@ -31,6 +31,24 @@ def test_facade_compiles(tmp_path):
     compile_facade(str(tmp_path / "facade_programs"))
 
 
+@pytest.mark.skipif(not os.path.exists(os.path.join(MPI_INC, "mpi.h")), reason="MPI headers absent")
+def test_derived_datatype_flattening(tmp_path):
+    """detail::flatten (the facade packs derived cell datatypes by memcpy of
+    their byte blocks) equals MPI_Pack / MPI_Unpack for every constructor:
+    vector, hvector, indexed, hindexed, indexed_block, struct with padding,
+    resized, dup, nesting, absolute addresses, pair types with gaps."""
+    out = str(tmp_path / "flatten_check")
+    subprocess.check_call(["g++", "-std=c++11", "-pedantic", "-Werror", "-O2", "-Wall", "-I",
+                           os.path.join(ROOT, "include"), "-I", MPI_INC,
+                           os.path.join(ROOT, "tests", "cpp", "flatten_check.cpp"), "-o", out,
+                           os.path.join(ROOT, "dccrg_amd", "libdccrgx.so"), os.path.join(MPI_LIB, "libmpi.so"),
+                           f"-Wl,-rpath,{os.path.join(ROOT, 'dccrg_amd')}:{MPI_LIB}"])
+    env = dict(os.environ, LD_LIBRARY_PATH="/usr/lib/x86_64-linux-gnu:" + MPI_LIB)
+    r = subprocess.run([out], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "MISMATCH" not in r.stdout, r.stdout + r.stderr
+    assert r.stdout.count(" ok ") == 13, r.stdout
+
+
 def run(*args, ranks=1):
     srcs = [os.path.join(ROOT, "tests", "cpp", "facade_programs.cpp"), os.path.join(ROOT, "include", "dccrg_amd.hpp"),
             os.path.join(ROOT, "include", "dccrgx.h")]
