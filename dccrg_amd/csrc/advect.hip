@@ -471,21 +471,6 @@ __global__ void __launch_bounds__(256) k_advect_geometry(MapParams mp, GeoParams
 
 // parents of removed cells: 0, then += child / 8 for each child in
 // ascending id order (adapter.hpp:265-300)
-__global__ void __launch_bounds__(256) k_average_children(double* __restrict__ f, const uint64_t* __restrict__ parent,
-                                                          const uint64_t* __restrict__ children, uint64_t n)
-{
-#pragma clang fp contract(off)
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        double acc = 0;
-        for (int k = 0; k < 8; k++) {
-            const uint64_t c = children[8 * i + k];
-            if (c != ~0ull) acc += f[c] / 8;
-        }
-        f[parent[i]] = acc;
-    }
-}
-
 int adv_ptrs(const dccrgx_grid* grid, const dccrgx_advect_fields* f, AdvPtrs* p)
 {
     DX_CHECK(f, DCCRGX_EINVAL, "null field set");
@@ -777,7 +762,6 @@ int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccr
     if (dx_malloc(&d_sib, n * 64) != hipSuccess || dx_malloc(&d_pos, n * 64) != hipSuccess ||
         dx_malloc(&d_lvl, n) != hipSuccess || dx_malloc(&d_code, n) != hipSuccess)
         s = set_error(DCCRGX_ENOMEM, "out of device memory for the adaptation sets");
-    std::vector<uint8_t> code(n);
     if (s == DCCRGX_OK) {
         hipLaunchKernelGGL(k_sibling_ids, dim3(grid_for(n)), dim3(256), 0, st, grid->map, E->d_leaves, E->d_local_g,
                            n, d_sib, d_lvl);
@@ -787,14 +771,11 @@ int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccr
         hipLaunchKernelGGL(k_adapt_codes, dim3(grid_for(n)), dim3(256), 0, st, (const int8_t*)d_marks,
                            (const int64_t*)d_pos, (const int8_t*)d_lvl, n, d_code);
         if (hipGetLastError() != hipSuccess) s = set_error(DCCRGX_EHIP, "adaptation sets failed");
-        if (s == DCCRGX_OK) s = dx_d2h(grid->ctx, code.data(), d_code, n, st);
+        uint64_t* out[3] = {to_refine, not_to_unrefine, to_unrefine};
+        if (s == DCCRGX_OK) s = amr_dev_codes_to_lists(grid, d_code, n, out, counts);
     }
     for (void* q : {(void*)d_marks, (void*)d_sib, (void*)d_pos, (void*)d_lvl, (void*)d_code}) dx_free(q);
-    if (s != DCCRGX_OK) return s;
-    uint64_t* out[4] = {nullptr, to_refine, not_to_unrefine, to_unrefine};
-    for (uint64_t q = 0; q < n; q++)
-        if (code[q]) out[code[q]][counts[code[q] - 1]++] = E->local[q];
-    return DCCRGX_OK;
+    return s;
 }
 
 int dccrgx_advect_set_geometry(dccrgx_grid* grid, const dccrgx_advect_fields* f, const double start[3],
@@ -823,99 +804,14 @@ int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_
 {
     DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
     if (!grid->amr || grid->amr->new_cells.empty()) return DCCRGX_OK;
-    PhaseTimer T("copy_from_parents");
-    std::vector<uint64_t> src, dst;
-    for (uint64_t c : grid->amr->new_cells) {
-        uint64_t idx[3];
-        int l;
-        map_indices(grid->map, c, idx, &l);
-        const uint64_t par = l > 0 ? map_cell(grid->map, idx, l - 1) : c;
-        const int64_t a = host_primary_slot(grid, c), b = host_primary_slot(grid, par);
-        DX_CHECK(a >= 0 && b >= 0, DCCRGX_ENOTFOUND, "no data for new cell %llu or its parent",
-                 (unsigned long long)c);
-        dst.push_back((uint64_t)a);
-        src.push_back((uint64_t)b);
-    }
-    T.lap("host lookups");
-    hipStream_t st = grid->ctx->compute;
-    uint64_t *d_src = nullptr, *d_dst = nullptr;
-    DX_HIP(dx_malloc(&d_src, src.size() * 8));
-    DX_HIP(dx_malloc(&d_dst, dst.size() * 8));
-    T.lap("alloc");
-    DX_TRY(dx_h2d(grid->ctx, d_src, src.data(), src.size() * 8, st));
-    DX_TRY(dx_h2d(grid->ctx, d_dst, dst.data(), dst.size() * 8, st));
-    T.lap("upload");
-    int s = DCCRGX_OK;
-    for (size_t k = 0; k < nf && s == DCCRGX_OK; k++) {
-        if (fields[k] < 0 || (size_t)fields[k] >= grid->fields.size() || grid->fields[fields[k]].variable) {
-            s = set_error(DCCRGX_EINVAL, "bad field %d", fields[k]);
-            break;
-        }
-        const Field& F = grid->fields[fields[k]];
-        s = launch_scatter_ext(F.ptr, d_src, d_dst, src.size(), F.elem, F.ptr, st);
-    }
-    DX_HIP(hipStreamSynchronize(st));
-    T.lap("scatter");
-    dx_free(d_src);
-    dx_free(d_dst);
-    T.lap("free");
-    return s;
+    return amr_dev_copy_from_parents(grid, fields, nf);
 }
 
 int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 {
     DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
     if (!grid->amr || grid->amr->removed.empty()) return DCCRGX_OK;
-    // parent slot -> its removed children's slots, children in ascending id
-    // order (removed is ascending; siblings of one parent interleave with
-    // other parents' children, so group explicitly)
-    // (parent slot, child slot) in removed (ascending child id) order; a
-    // stable sort by parent slot keeps each group's children ascending
-    std::vector<std::pair<uint64_t, uint64_t>> pc;
-    pc.reserve(grid->amr->removed.size());
-    for (uint64_t c : grid->amr->removed) {
-        uint64_t idx[3];
-        int l;
-        map_indices(grid->map, c, idx, &l);
-        const uint64_t par = map_cell(grid->map, idx, l - 1);
-        const int64_t ps = host_primary_slot(grid, par), cs = host_primary_slot(grid, c);
-        DX_CHECK(ps >= 0 && cs >= 0, DCCRGX_ENOTFOUND, "no data for removed cell %llu or its parent",
-                 (unsigned long long)c);
-        pc.emplace_back((uint64_t)ps, (uint64_t)cs);
-    }
-    std::stable_sort(pc.begin(), pc.end(), [](const std::pair<uint64_t, uint64_t>& a,
-                                              const std::pair<uint64_t, uint64_t>& b) { return a.first < b.first; });
-    std::vector<uint64_t> parent, children;
-    for (size_t i = 0; i < pc.size();) {
-        size_t j = i;
-        while (j < pc.size() && pc[j].first == pc[i].first) j++;
-        DX_CHECK(j - i <= 8, DCCRGX_EINTERNAL, "more than 8 children of slot %llu", (unsigned long long)pc[i].first);
-        parent.push_back(pc[i].first);
-        for (size_t k = i; k < j; k++) children.push_back(pc[k].second);
-        children.resize(8 * parent.size(), ~0ull);
-        i = j;
-    }
-    hipStream_t st = grid->ctx->compute;
-    uint64_t *d_par = nullptr, *d_ch = nullptr;
-    DX_HIP(dx_malloc(&d_par, parent.size() * 8));
-    DX_HIP(dx_malloc(&d_ch, children.size() * 8));
-    DX_TRY(dx_h2d(grid->ctx, d_par, parent.data(), parent.size() * 8, st));
-    DX_TRY(dx_h2d(grid->ctx, d_ch, children.data(), children.size() * 8, st));
-    int s = DCCRGX_OK;
-    for (size_t k = 0; k < nf; k++) {
-        if (fields[k] < 0 || (size_t)fields[k] >= grid->fields.size() || grid->fields[fields[k]].variable ||
-            grid->fields[fields[k]].elem != 8) {
-            s = set_error(DCCRGX_EINVAL, "field %d is not an f64 field", fields[k]);
-            break;
-        }
-        hipLaunchKernelGGL(k_average_children, dim3(grid_for(parent.size())), dim3(256), 0, st,
-                           (double*)grid->fields[fields[k]].ptr, d_par, d_ch, (uint64_t)parent.size());
-    }
-    DX_HIP(hipGetLastError());
-    DX_HIP(hipStreamSynchronize(st));
-    dx_free(d_par);
-    dx_free(d_ch);
-    return s;
+    return amr_dev_average_children(grid, fields, nf);
 }
 
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt)

@@ -332,6 +332,7 @@ int rebuild(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<
     Explicit* E = grid->ex;
     E->defer_fields = false;
     E->retired = retired;
+    if ((s = amr_dev_retired_table(grid)) != DCCRGX_OK) return rollback(s);
     const uint64_t ns = E->slot_ids.size();
 
     // old slot of every new slot: on the device from the old leaf hash and

@@ -176,7 +176,7 @@ __device__ inline void a_erase_sibling_unrefines(const AView& a, uint64_t c)
 // kernels with their call index.
 __global__ void __launch_bounds__(256) k_req_refine(AView a, const uint64_t* __restrict__ ids, uint64_t n,
                                                     int32_t* __restrict__ res, uint64_t* __restrict__ du_ids,
-                                                    uint32_t* __restrict__ du_ord, uint32_t* __restrict__ du_n)
+                                                    uint32_t* __restrict__ du_ord, uint32_t* __restrict__ du_n, int erase)
 {
     const int M = a.v.mp.max_lvl;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -200,6 +200,7 @@ __global__ void __launch_bounds__(256) k_req_refine(AView a, const uint64_t* __r
                 if (!blocked) {
                     r = 1;
                     atomicOr(&a.flags[g], RF_REFINE);
+                    if (!erase) goto done;  // no cells_to_unrefine to erase (the adapter refines first)
                     a_erase_sibling_unrefines(a, c);
                     for (int pass = 0; pass < 2; pass++) {
                         const uint64_t* row = pass ? a.nto_row : a.nof_row;
@@ -212,6 +213,7 @@ __global__ void __launch_bounds__(256) k_req_refine(AView a, const uint64_t* __r
                 }
             }
         }
+    done:
         if (res) res[i] = r;
     }
 }
@@ -253,7 +255,7 @@ __global__ void __launch_bounds__(256) k_req_du_a(AView a, const uint64_t* __res
 __global__ void __launch_bounds__(256) k_req_du_b(AView a, const uint64_t* __restrict__ ids,
                                                   const uint32_t* __restrict__ ord, const uint32_t* __restrict__ n_dev,
                                                   uint64_t n_host, const uint32_t* __restrict__ grp,
-                                                  const uint32_t* __restrict__ key)
+                                                  const uint32_t* __restrict__ key, int erase)
 {
     const uint64_t n = n_dev ? *n_dev : n_host;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -261,7 +263,7 @@ __global__ void __launch_bounds__(256) k_req_du_b(AView a, const uint64_t* __res
         const uint32_t k = key[i];
         if (k == NONE32 || grp[k] != (ord ? ord[i] : (uint32_t)i)) continue;
         const uint64_t c = ids[i];
-        a_erase_sibling_unrefines(a, c);
+        if (erase) a_erase_sibling_unrefines(a, c);
         atomicOr(&a.flags[ex_find(a.v, c)], RF_NOT_UNREFINE);
     }
 }
@@ -786,6 +788,7 @@ int amr_dev_sync(dccrgx_grid* grid)
         if (no) DX_TRY(dx_d2h(grid->ctx, A.nr_other.data(), d_other, no * 8ull, st));
     }
     A.dev_current = true;
+    A.dev_unrefines = !A.to_unrefine.empty();
     return DCCRGX_OK;
 }
 
@@ -847,6 +850,8 @@ int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_
     DX_HIP(hipMemsetAsync(d_grp, 0xff, a.n * 4, st));
     DX_TRY(dx_h2d(grid->ctx, d_ids, ids, n * 8, st));
     const unsigned b = blocks(n);
+    if (kind == DCCRGX_AMR_UNREFINE) A.dev_unrefines = true;
+    const int erase = A.dev_unrefines ? 1 : 0;
     switch (kind) {
     case DCCRGX_AMR_REFINE:
         DX_TRY(S.get(&d_du, n));
@@ -854,17 +859,17 @@ int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_
         DX_TRY(S.get(&d_dun, 1));
         DX_HIP(hipMemsetAsync(d_dun, 0, 4, st));
         hipLaunchKernelGGL(k_req_refine, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n, d_res, d_du,
-                           d_ord, d_dun);
+                           d_ord, d_dun, erase);
         hipLaunchKernelGGL(k_req_du_a, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_du, (const uint32_t*)d_ord,
                            (const uint32_t*)d_dun, (uint64_t)0, (int32_t*)nullptr, d_grp, d_key);
         hipLaunchKernelGGL(k_req_du_b, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_du, (const uint32_t*)d_ord,
-                           (const uint32_t*)d_dun, (uint64_t)0, (const uint32_t*)d_grp, (const uint32_t*)d_key);
+                           (const uint32_t*)d_dun, (uint64_t)0, (const uint32_t*)d_grp, (const uint32_t*)d_key, erase);
         break;
     case DCCRGX_AMR_DONT_UNREFINE:
         hipLaunchKernelGGL(k_req_du_a, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (const uint32_t*)nullptr,
                            (const uint32_t*)nullptr, (uint64_t)n, d_res, d_grp, d_key);
         hipLaunchKernelGGL(k_req_du_b, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (const uint32_t*)nullptr,
-                           (const uint32_t*)nullptr, (uint64_t)n, (const uint32_t*)d_grp, (const uint32_t*)d_key);
+                           (const uint32_t*)nullptr, (uint64_t)n, (const uint32_t*)d_grp, (const uint32_t*)d_key, erase);
         break;
     case DCCRGX_AMR_UNREFINE:
         hipLaunchKernelGGL(k_req_unref_a, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n, d_res,
@@ -1018,6 +1023,239 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     T.lap("new leaf list");
     *d_leaves_out = d_new;
     *n_out = n_new;
+    return DCCRGX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// data of new / removed cells, adaptation sets
+// ---------------------------------------------------------------------------
+
+// storage slot of a leaf, or of a cell retired by the last rebuild (its
+// table: ids ascending, then their slots), -1 if none
+struct SlotView {
+    ExView v;
+    const uint32_t* slot_of_g;
+    const uint64_t* ret;
+    uint64_t n_ret;
+};
+
+__device__ inline int64_t slot_lookup(const SlotView& s, uint64_t id)
+{
+    const int64_t g = ex_find(s.v, id);
+    if (g >= 0) {
+        const uint32_t x = s.slot_of_g[g];
+        return x == NO_SLOT ? -1 : (int64_t)x;
+    }
+    const uint64_t k = lower_bound_u64(s.ret, s.n_ret, id);
+    return k < s.n_ret && s.ret[k] == id ? (int64_t)s.ret[s.n_ret + k] : -1;
+}
+
+static SlotView slot_view(const dccrgx_grid* grid)
+{
+    const Explicit* E = grid->ex;
+    return SlotView{explicit_view(grid), E->d_slot_of_g, E->d_ret, E->n_ret};
+}
+
+int amr_dev_retired_table(dccrgx_grid* grid)
+{
+    Explicit* E = grid->ex;
+    const uint64_t n = E->retired.size();
+    E->n_ret = 0;
+    if (!n) return DCCRGX_OK;
+    std::vector<uint64_t> t(2 * n);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t* x = E->extra.find(E->retired[i]);
+        DX_CHECK(x, DCCRGX_EINTERNAL, "retired cell %llu has no slot", (unsigned long long)E->retired[i]);
+        t[i] = E->retired[i];
+        t[n + i] = *x;
+    }
+    hipStream_t st = grid->ctx->compute;
+    ds_free(E->d_ret, st);
+    E->d_ret = nullptr;
+    DX_HIP(ds_malloc(&E->d_ret, 16 * n, st));
+    DX_TRY(dx_h2d(grid->ctx, E->d_ret, t.data(), 16 * n, st));
+    E->n_ret = n;
+    return DCCRGX_OK;
+}
+
+struct FieldSet {
+    uint8_t* p[8];
+    uint32_t elem[8];
+    int n;
+};
+
+// adapter.hpp:229-251: a new cell takes its parent's data
+__global__ void __launch_bounds__(256) k_copy_from_parents(SlotView sv, MapParams mp, const uint64_t* __restrict__ cells,
+                                                           uint64_t n, FieldSet fs, int32_t* __restrict__ err)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t c = cells[i];
+        uint64_t idx[3];
+        int l;
+        map_indices(mp, c, idx, &l);
+        const uint64_t par = l > 0 ? map_cell(mp, idx, l - 1) : c;
+        const int64_t dst = slot_lookup(sv, c), src = slot_lookup(sv, par);
+        if (dst < 0 || src < 0) {
+            atomicOr(err, 1);
+            continue;
+        }
+        for (int k = 0; k < fs.n; k++) {
+            const uint32_t e = fs.elem[k];
+            const uint8_t* a = fs.p[k] + (uint64_t)src * e;
+            uint8_t* b = fs.p[k] + (uint64_t)dst * e;
+            if (e == 8) *reinterpret_cast<uint64_t*>(b) = *reinterpret_cast<const uint64_t*>(a);
+            else if (e == 4) *reinterpret_cast<uint32_t*>(b) = *reinterpret_cast<const uint32_t*>(a);
+            else
+                for (uint32_t q = 0; q < e; q++) b[q] = a[q];
+        }
+    }
+}
+
+// adapter.hpp:253-300: the parent of removed cells is 0, then += child / 8
+// over its removed children in ascending order (the first removed child of
+// each parent does the sum; `removed` ascending)
+__global__ void __launch_bounds__(256) k_average_children(SlotView sv, MapParams mp, const uint64_t* __restrict__ removed,
+                                                          uint64_t n, FieldSet fs, int32_t* __restrict__ err)
+{
+#pragma clang fp contract(off)
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t c = removed[i];
+        uint64_t idx[3];
+        int l;
+        map_indices(mp, c, idx, &l);
+        const uint64_t par = map_cell(mp, idx, l - 1);
+        uint64_t pi[3];
+        int pl;
+        map_indices(mp, par, pi, &pl);
+        const uint64_t h = (uint64_t)1 << (mp.max_lvl - l);
+        uint64_t ch[8];
+        for (int k = 0; k < 8; k++) {  // x fastest: ascending ids
+            const uint64_t ci[3] = {pi[0] + (k & 1) * h, pi[1] + ((k >> 1) & 1) * h, pi[2] + ((k >> 2) & 1) * h};
+            ch[k] = map_cell(mp, ci, l);
+        }
+        bool first = true;
+        for (int k = 0; k < 8 && ch[k] < c; k++) {
+            const uint64_t j = lower_bound_u64(removed, n, ch[k]);
+            first &= !(j < n && removed[j] == ch[k]);
+        }
+        if (!first) continue;
+        const int64_t ps = slot_lookup(sv, par);
+        if (ps < 0) {
+            atomicOr(err, 1);
+            continue;
+        }
+        int64_t cs[8];
+        for (int k = 0; k < 8; k++) {
+            const uint64_t j = lower_bound_u64(removed, n, ch[k]);
+            cs[k] = j < n && removed[j] == ch[k] ? slot_lookup(sv, ch[k]) : -2;
+            if (cs[k] == -1) atomicOr(err, 1);
+        }
+        for (int f = 0; f < fs.n; f++) {
+            double* d = reinterpret_cast<double*>(fs.p[f]);
+            double acc = 0;
+            for (int k = 0; k < 8; k++)
+                if (cs[k] >= 0) acc += d[cs[k]] / 8;
+            d[ps] = acc;
+        }
+    }
+}
+
+static int field_sets(const dccrgx_grid* grid, const int32_t* fields, size_t nf, bool f64, std::vector<FieldSet>& out)
+{
+    out.clear();
+    for (size_t k = 0; k < nf; k++) {
+        DX_CHECK(fields[k] >= 0 && (size_t)fields[k] < grid->fields.size() && !grid->fields[fields[k]].variable,
+                 DCCRGX_EINVAL, "bad field %d", fields[k]);
+        const Field& F = grid->fields[fields[k]];
+        DX_CHECK(!f64 || F.elem == 8, DCCRGX_EINVAL, "field %d is not an f64 field", fields[k]);
+        if (out.empty() || out.back().n == 8) out.push_back(FieldSet{});
+        FieldSet& fs = out.back();
+        fs.p[fs.n] = static_cast<uint8_t*>(F.ptr);
+        fs.elem[fs.n++] = F.elem;
+    }
+    return DCCRGX_OK;
+}
+
+static int run_rule(dccrgx_grid* grid, const std::vector<uint64_t>& cells, const int32_t* fields, size_t nf, bool avg)
+{
+    DX_CHECK(!grid->uniform, DCCRGX_ESTATE, "no refinement happened");
+    std::vector<FieldSet> sets;
+    DX_TRY(field_sets(grid, fields, nf, avg, sets));
+    hipStream_t st = grid->ctx->compute;
+    Scratch S(st);
+    uint64_t* d_cells;
+    int32_t* d_err;
+    DX_TRY(S.get(&d_cells, cells.size()));
+    DX_TRY(S.get(&d_err, 1));
+    DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
+    DX_TRY(dx_h2d(grid->ctx, d_cells, cells.data(), cells.size() * 8, st));
+    const SlotView sv = slot_view(grid);
+    for (const FieldSet& fs : sets) {
+        if (avg)
+            hipLaunchKernelGGL(k_average_children, dim3(blocks(cells.size())), dim3(256), 0, st, sv, grid->map,
+                               (const uint64_t*)d_cells, (uint64_t)cells.size(), fs, d_err);
+        else
+            hipLaunchKernelGGL(k_copy_from_parents, dim3(blocks(cells.size())), dim3(256), 0, st, sv, grid->map,
+                               (const uint64_t*)d_cells, (uint64_t)cells.size(), fs, d_err);
+    }
+    DX_HIP(hipGetLastError());
+    int32_t err = 0;
+    DX_TRY(dx_d2h(grid->ctx, &err, d_err, 4, st));
+    DX_CHECK(!err, DCCRGX_ENOTFOUND, "no data for a %s cell or its %s", avg ? "removed" : "new",
+             avg ? "parent" : "parent");
+    return DCCRGX_OK;
+}
+
+int amr_dev_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_t nf)
+{
+    return run_rule(grid, grid->amr->new_cells, fields, nf, false);
+}
+
+int amr_dev_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf)
+{
+    return run_rule(grid, grid->amr->removed, fields, nf, true);
+}
+
+__global__ void __launch_bounds__(256) k_code_ids(const uint64_t* __restrict__ leaves, const uint32_t* __restrict__ local_g,
+                                                  const uint8_t* __restrict__ code, uint64_t n, uint64_t* __restrict__ ids,
+                                                  uint8_t* __restrict__ flags)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        ids[q] = leaves[local_g[q]];
+        const uint8_t c = code[q];
+        for (int k = 0; k < 3; k++) flags[k * n + q] = c == k + 1;
+    }
+}
+
+int amr_dev_codes_to_lists(dccrgx_grid* grid, const uint8_t* d_code, uint64_t n, uint64_t* out[3], size_t counts[3])
+{
+    hipStream_t st = grid->ctx->compute;
+    const Explicit* E = grid->ex;
+    Scratch S(st);
+    uint64_t *d_ids, *d_out;
+    uint8_t* d_flags;
+    int* d_cnt;
+    DX_TRY(S.get(&d_ids, n));
+    DX_TRY(S.get(&d_out, 3 * n));
+    DX_TRY(S.get(&d_flags, 3 * n));
+    DX_TRY(S.get(&d_cnt, 4));
+    hipLaunchKernelGGL(k_code_ids, dim3(blocks(n)), dim3(256), 0, st, (const uint64_t*)E->d_leaves,
+                       (const uint32_t*)E->d_local_g, d_code, n, d_ids, d_flags);
+    size_t tb = 0;
+    DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, d_ids, d_flags, d_out, d_cnt, (int)n, st));
+    uint8_t* d_tmp;
+    DX_TRY(S.get(&d_tmp, tb));
+    for (int k = 0; k < 3; k++)  // order preserving: ascending like the local cells
+        DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, tb, d_ids, d_flags + k * n, d_out + k * n, d_cnt + k, (int)n, st));
+    int cnt[3] = {0, 0, 0};
+    DX_TRY(dx_d2h(grid->ctx, cnt, d_cnt, 12, st));
+    for (int k = 0; k < 3; k++) {
+        counts[k] = (size_t)cnt[k];
+        if (cnt[k]) DX_TRY(dx_d2h(grid->ctx, out[k], d_out + k * n, (size_t)cnt[k] * 8, st));
+    }
     return DCCRGX_OK;
 }
 

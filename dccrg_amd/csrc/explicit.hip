@@ -1180,7 +1180,8 @@ void explicit_free(Explicit* E)
     if (!E) return;
     FreeBatch fb;
     for (void* q : {(void*)E->d_leaves, (void*)E->d_keys, (void*)E->d_vals, (void*)E->d_bits, (void*)E->d_rank,
-                    (void*)E->d_local_g, (void*)E->d_level, (void*)E->d_slot_of_g, (void*)E->d_local_slot})
+                    (void*)E->d_local_g, (void*)E->d_level, (void*)E->d_slot_of_g, (void*)E->d_local_slot,
+                    (void*)E->d_ret})
         fb.add(q);
     for (auto& kv : E->hl)
         for (void* q : {(void*)kv.second.d_inner_pos, (void*)kv.second.d_outer_pos, (void*)kv.second.d_all_pos})
@@ -1194,6 +1195,7 @@ void explicit_clear_retired(Explicit* E)
 {
     for (uint64_t c : E->retired) E->extra.erase(c);
     E->retired.clear();
+    E->n_ret = 0;  // the table stays allocated until E is freed
 }
 
 void explicit_destroy(dccrgx_grid* grid)

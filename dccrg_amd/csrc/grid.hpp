@@ -210,6 +210,10 @@ struct Explicit {
     // clear_refined_unrefined_data (dccrg.hpp:3519-3543, 5550-5567): ascending
     // ids, stored in slots after the ghosts
     std::vector<uint64_t> retired;
+    // their device copy for slot lookups (amr_dev.hip): ids ascending, then
+    // the slot of each (n_ret of each), made by the rebuild that retired them
+    uint64_t* d_ret = nullptr;
+    uint64_t n_ret = 0;
 };
 
 // pending refinement requests of this rank and the results of the last
@@ -227,6 +231,7 @@ struct Amr {
     uint64_t flags_n = 0, flags_cap = 0;
     std::vector<uint64_t> nr_other;
     bool host_current = true, dev_current = false;
+    bool dev_unrefines = true;  // the flags may hold cells_to_unrefine (else erasing them is skipped)
     ~Amr() { (void)dx_free(d_flags); }
 };
 // amr_dev.hip
@@ -235,6 +240,14 @@ int amr_host_sync(dccrgx_grid* grid);
 int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results);
 int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, std::vector<uint64_t>& leaves_host,
                    std::vector<uint64_t>& retired, std::vector<uint64_t>& nr, bool* changed);
+// the retired cells' device lookup table (after their slots were assigned)
+int amr_dev_retired_table(dccrgx_grid* grid);
+// new cells take their parent's value / parents of removed cells the average
+// of their children, on the device (tests/advection/adapter.hpp:229-300)
+int amr_dev_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_t nf);
+int amr_dev_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf);
+// ordered compaction of local cells by code (1..3) into three host lists
+int amr_dev_codes_to_lists(dccrgx_grid* grid, const uint8_t* d_code, uint64_t n, uint64_t* out[3], size_t counts[3]);
 
 
 struct CopySeg {
