@@ -538,10 +538,14 @@ def main():
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = D.Context(device, rank, world)
-    if world > 1:
+    shared_gpu = world > ndev  # more ranks than GPUs (a rehearsal on one GPU): RCCL refuses that
+    if world > 1 and not shared_gpu:
         uid = [D.Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(uid[0])
+    elif world > 1:  # halos through the library's host-staged transport over gloo
+        from dccrg_amd.transport import TorchDistTransport
+        TorchDistTransport().attach(ctx)
 
     early = {}
     if rank == 0 and world == 1 and not args.no_secondary:
@@ -607,7 +611,8 @@ def main():
         "config": {
             "workload": "tests/game_of_life/scalability3d 3-D game of life, uniform "
                         f"{length[0]}x{length[1]}x{length[2]} grid, neighborhood length 1 (26 "
-                        "neighbors), periodic z, block (z-slab) partition, halo over RCCL",
+                        "neighbors), periodic z, block (z-slab) partition, halo over "
+                        + ("the host-staged transport (ranks share a GPU)" if shared_gpu else "RCCL"),
             "cells_per_gpu": n_local,
             "grid": list(length),
             "parallelism": f"z-slab x{world}",
