@@ -438,7 +438,7 @@ def neighbor_lists(ctx, D, torch):
     return out
 
 
-def halo_payload(ctx, D, world, barrier, reduce_max):
+def halo_payload(ctx, D, world, barrier, reduce_max, shared_gpu=False):
     """tests/scalability/scalability.cpp:170-191 on the device: cells carry
     data_size opaque bytes (its Cell::data, :39-57), each step is
     start_remote_neighbor_copy_updates, wait receives, wait sends around an
@@ -480,7 +480,8 @@ def halo_payload(ctx, D, world, barrier, reduce_max):
         own.close()
     return {"workload": "tests/scalability/scalability.cpp byte payloads, 2048x2048x8 z-slab per rank, hood 1, "
                         "periodic z, start / wait receives / wait sends, empty solve"
-                        + (" (N = 1: own periodic images through RCCL)" if world == 1 else ", RCCL over xGMI"),
+                        + (" (N = 1: own periodic images through RCCL)" if world == 1 else
+                           ", host-staged transport (ranks share a GPU)" if shared_gpu else ", RCCL over xGMI"),
             "steps": steps, "sizes": rows}
 
 
@@ -496,8 +497,10 @@ def launch_ranks(n: int) -> int:
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    # torch.distributed.run's parser takes "--n" for an abbreviation of its own options
+    args = ["--cells-per-axis" + a[3:] if a == "--n" or a.startswith("--n=") else a for a in sys.argv[1:]]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + args
     return subprocess.call(cmd)
 
 
@@ -506,7 +509,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=2048, help="cells per axis per GPU")
+    ap.add_argument("--n", "--cells-per-axis", dest="n", type=int, default=2048, help="cells per axis per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the other configs' lines (N = 1)")
     ap.add_argument("--no-halo-payload", action="store_true", help="skip the byte-payload halo line")
@@ -522,7 +525,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
-        line = json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world, "gpus": args.gpus,
+        line = json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world, "gpus": args.gpus, "n": args.n,
                            "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"})
         os.write(1, (line + "\n").encode())  # one write: ranks share the launcher's stdout pipe
         return
@@ -647,7 +650,7 @@ def main():
 
     if not args.no_halo_payload:  # collective: every rank
         try:
-            line["halo_payload"] = halo_payload(ctx, D, world, barrier, reduce_max)
+            line["halo_payload"] = halo_payload(ctx, D, world, barrier, reduce_max, shared_gpu)
         except Exception as e:  # the headline line still prints
             line["halo_payload"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_secondary:
