@@ -95,7 +95,7 @@ def check_for_adaptation(grid: Dccrg, diff_increase: float, diff_threshold: floa
     if grid.get_maximum_refinement_level() == 0:
         return empty, empty, empty
     n = grid.n_local
-    out = [np.zeros(max(n, 1), dtype=np.uint64) for _ in range(3)]
+    out = [np.empty(max(n, 1), dtype=np.uint64) for _ in range(3)]
     counts = (C.c_size_t * 3)()
     f = grid._advect_fields()
     check(lib().dccrgx_advect_adaptation_sets(grid._h, X.DEFAULT_NEIGHBORHOOD_ID, C.byref(f), diff_increase,

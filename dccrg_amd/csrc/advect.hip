@@ -518,6 +518,12 @@ void uniform_local_run(const dccrgx_grid* grid, uint64_t* s0, uint64_t* n)
     *n = u.hi - u.lo;
 }
 
+__global__ void __launch_bounds__(256) k_cnt_to_row(const uint32_t* __restrict__ cnt, uint64_t n, uint64_t* __restrict__ row)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) row[i + 1] = cnt[i];
+}
+
 // build the face lists of a neighborhood's local cells (explicit grids)
 int build_faces(const dccrgx_grid* grid, Hood& h)
 {
@@ -539,16 +545,14 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
                            R.local_slot, R.level, M, n, fc->ell_slot, fc->ell_dir, d_cnt, (const uint64_t*)nullptr,
                            (uint32_t*)nullptr, (int8_t*)nullptr);
     DX_HIP(hipGetLastError());
-    std::vector<uint32_t> cnt(n);
-    DX_TRY(dx_d2h(grid->ctx, cnt.data(), d_cnt, n * 4, st));
-    DX_HIP(hipStreamSynchronize(st));
-    dx_free(d_cnt);
-    std::vector<uint64_t> row(n + 1, 0);
-    for (uint64_t q = 0; q < n; q++) row[q + 1] = row[q] + cnt[q];
-    fc->overflow = row[n] > 0;
-    DX_TRY(dx_h2d(grid->ctx, fc->o_row, row.data(), (n + 1) * 8, st));
-    DX_HIP(dx_malloc(&fc->o_slot, std::max<uint64_t>(row[n], 1) * 4));
-    DX_HIP(dx_malloc(&fc->o_dir, std::max<uint64_t>(row[n], 1)));
+    // overflow rows by a device scan (one 8-byte read-back for the total)
+    if (n) hipLaunchKernelGGL(k_cnt_to_row, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)d_cnt, n, fc->o_row);
+    uint64_t total = 0;
+    DX_TRY(device_scan_rows(fc->o_row, n, st, &total));
+    ds_free(d_cnt, st);
+    fc->overflow = total > 0;
+    DX_HIP(dx_malloc(&fc->o_slot, std::max<uint64_t>(total, 1) * 4));
+    DX_HIP(dx_malloc(&fc->o_dir, std::max<uint64_t>(total, 1)));
     if (fc->overflow)
         hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
                            R.local_slot, R.level, M, n, fc->ell_slot, fc->ell_dir, (uint32_t*)nullptr, fc->o_row,

@@ -966,24 +966,26 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     DX_HIP(hipGetLastError());
     uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
     int32_t err = 0;
-    DX_TRY(dx_d2h(ctx, &err, d_err, 4, st));
-    DX_TRY(dx_d2h(ctx, cnt, o.cnt, 5 * 4, st));
+    const D2H first[2] = {{&err, d_err, 4}, {cnt, o.cnt, 5 * 4}};
+    DX_TRY(dx_d2h_many(ctx, first, 2, st));
     T.lap("decisions");
     DX_CHECK(!err, DCCRGX_EINTERNAL, "override_unrefines walk exceeded its workspace");
-    // the persisting dont_refine set: flagged leaves and the ids that are not leaves
+    // the persisting dont_refine set (flagged leaves, and the ids that are not
+    // leaves) and this rank's new / removed / retired cells, in one read-back
     nr.resize(cnt[4]);
-    if (cnt[4]) DX_TRY(dx_d2h(ctx, nr.data(), d_nr, cnt[4] * 8ull, st));
+    A.new_cells.resize(cnt[1]);
+    A.removed.resize(cnt[2]);
+    retired.resize(cnt[3]);
+    const D2H lists[4] = {{nr.data(), d_nr, cnt[4] * 8ull},
+                          {A.new_cells.data(), o.newc, cnt[1] * 8ull},
+                          {A.removed.data(), o.removed, cnt[2] * 8ull},
+                          {retired.data(), o.retired, cnt[3] * 8ull}};
+    DX_TRY(dx_d2h_many(ctx, lists, 4, st));
     nr.insert(nr.end(), A.nr_other.begin(), A.nr_other.end());
-    auto host_sorted = [&](const uint64_t* d, uint32_t k, std::vector<uint64_t>& out) -> int {
-        out.resize(k);
-        if (k) DX_TRY(dx_d2h(ctx, out.data(), d, k * 8ull, st));
-        radix_sort_u64(out);
-        out.erase(std::unique(out.begin(), out.end()), out.end());
-        return DCCRGX_OK;
-    };
-    DX_TRY(host_sorted(o.newc, cnt[1], A.new_cells));
-    DX_TRY(host_sorted(o.removed, cnt[2], A.removed));
-    DX_TRY(host_sorted(o.retired, cnt[3], retired));
+    for (std::vector<uint64_t>* v : {&A.new_cells, &A.removed, &retired}) {
+        radix_sort_u64(*v);
+        v->erase(std::unique(v->begin(), v->end()), v->end());
+    }
     *changed = cnt[0] > 0;
     if (!*changed) return DCCRGX_OK;
     // the new leaf list: surviving leaves in order, merged with the sorted new ones

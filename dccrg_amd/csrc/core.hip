@@ -72,6 +72,30 @@ int dx_h2d(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
     return DCCRGX_OK;
 }
 
+int dx_d2h_many(Ctx* c, const D2H* v, size_t n, hipStream_t st)
+{
+    size_t total = 0;
+    for (size_t i = 0; i < n; i++) total += (v[i].bytes + 15) & ~(size_t)15;
+    if (!total) return DCCRGX_OK;
+    if (total > STAGE_CHUNK) {  // large: one at a time
+        for (size_t i = 0; i < n; i++) DX_TRY(dx_d2h(c, v[i].dst, v[i].src, v[i].bytes, st));
+        return DCCRGX_OK;
+    }
+    DX_TRY(stage_reserve(c, total));
+    size_t at = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (v[i].bytes) DX_HIP(hipMemcpyAsync((char*)c->stage + at, v[i].src, v[i].bytes, hipMemcpyDeviceToHost, st));
+        at += (v[i].bytes + 15) & ~(size_t)15;
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    at = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (v[i].bytes) std::memcpy(v[i].dst, (const char*)c->stage + at, v[i].bytes);
+        at += (v[i].bytes + 15) & ~(size_t)15;
+    }
+    return DCCRGX_OK;
+}
+
 int dx_d2h(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
 {
     if (!bytes) return DCCRGX_OK;

@@ -372,6 +372,13 @@ struct Ctx {
 // from pinned memory do not.
 int dx_h2d(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st);
 int dx_d2h(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st);
+// several device -> host copies behind one synchronisation
+struct D2H {
+    void* dst;
+    const void* src;
+    size_t bytes;
+};
+int dx_d2h_many(Ctx* c, const D2H* v, size_t n, hipStream_t st);
 
 }  // namespace dccrgx
 
