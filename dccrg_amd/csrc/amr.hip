@@ -267,7 +267,8 @@ __global__ void __launch_bounds__(256) k_level0_ids(uint64_t* __restrict__ out, 
 // array are built first; on any failure they are freed and the old grid is
 // left exactly as it was.
 int rebuild(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired,
-            uint64_t* d_leaves = nullptr)  // leaves: moved into the grid
+            uint64_t* d_leaves = nullptr,  // leaves: moved into the grid
+            const uint32_t* gone_flags = nullptr)  // per old leaf, AMR_FLAG_GONE: lists rebuilt around the change
 {
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
@@ -323,8 +324,10 @@ int rebuild(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<
     int s = explicit_init(grid, leaves.data(), leaves.size(), d_leaves, &leaves);  // adopts d_leaves
     T.lap("explicit_init");
     if (s == DCCRGX_OK) grid->ex->defer_fields = true;
-    for (auto it = grid->hoods.begin(); s == DCCRGX_OK && it != grid->hoods.end(); ++it)
-        s = explicit_build_hood(grid, it->second);
+    for (auto it = grid->hoods.begin(); s == DCCRGX_OK && it != grid->hoods.end(); ++it) {
+        const NofHint hint{old.ex, &old_hoods.at(it->first), gone_flags, AMR_FLAG_GONE};
+        s = explicit_build_hood(grid, it->second, gone_flags && !old.uniform && old.ex ? &hint : nullptr);
+    }
     T.lap("neighborhoods");
     if (s == DCCRGX_OK) s = explicit_add_slots(grid, retired);
     if (s != DCCRGX_OK) return rollback(s);
@@ -705,7 +708,8 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
         // the previous round's refined / unrefined data goes first, as in
         // execute_refines (dccrg.hpp:10266-10267)
         explicit_clear_retired(grid->ex);
-        s = rebuild(grid, leaves, retired, d_leaves);  // transactional: on failure the grid is unchanged
+        // transactional: on failure the grid is unchanged; the flags mark the old leaves that go
+        s = rebuild(grid, leaves, retired, d_leaves, A.flags_n == grid->ex->n ? A.d_flags : nullptr);
         if (s != DCCRGX_OK) return restore(s);
     }
     ds_free(d_saved, st);

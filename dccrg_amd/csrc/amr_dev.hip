@@ -42,6 +42,7 @@ enum : uint32_t {
     RF_FINAL = 64u,  // override_unrefines: the unrefinement happens
 };
 constexpr uint32_t RF_SETS = RF_REFINE | RF_UNREFINE | RF_NOT_UNREFINE | RF_NOT_REFINE;
+static_assert(RF_GONE == AMR_FLAG_GONE, "the rebuild reads the gone flag (grid.hpp)");
 constexpr uint32_t NONE32 = 0xffffffffu;
 
 // one explicit grid, its default neighborhood and the request flags

@@ -6,6 +6,7 @@
 #include <cstdarg>
 #include <cstring>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <unordered_map>
 
@@ -535,8 +536,10 @@ void pool_run(size_t nt, const std::function<void(size_t)>& job)
 // caching allocator (internal.hpp)
 // ---------------------------------------------------------------------------
 namespace {
-constexpr size_t CACHE_MAX_BLOCK = 256ull << 20;  // larger blocks go straight back to the pool
-constexpr size_t CACHE_MAX_TOTAL = 8ull << 30;    // idle bytes kept at most
+constexpr size_t CACHE_MAX_BLOCK = 256ull << 20;   // larger blocks go straight back to the pool
+constexpr size_t CACHE_MAX_TOTAL = 8ull << 30;     // idle bytes kept at most per device
+constexpr size_t STREAM_LIST_MAX = 256ull << 20;   // a stream's own list is made common beyond this
+constexpr int MAX_DEV = 64;
 
 size_t size_class(size_t b)
 {
@@ -550,12 +553,30 @@ size_t size_class(size_t b)
     return c;
 }
 
+using Lists = std::map<size_t, std::vector<void*>>;
+
+// blocks freed while work may still use them: reusable by any stream once
+// the events recorded on every stream of the device at the free have passed
+struct Pending {
+    std::vector<std::pair<void*, size_t>> blocks;
+    std::vector<hipEvent_t> ev;
+    std::vector<hipStream_t> on;  // the stream each event was recorded on
+};
+
+struct DevCache {
+    std::unordered_map<void*, size_t> live;  // cached-class blocks in use -> class
+    Lists idle;                              // reusable by any stream
+    std::map<hipStream_t, Lists> by_stream;  // reusable by that stream (stream order)
+    std::map<hipStream_t, size_t> stream_bytes;
+    std::deque<Pending> pending;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<hipStream_t> streams;  // the library's streams on this device (contexts)
+    size_t idle_bytes = 0, held_bytes = 0;  // idle; by_stream + pending
+};
+
 struct Cache {
     std::mutex m;
-    std::unordered_map<void*, size_t> live;  // cached-class blocks in use -> class
-    std::map<size_t, std::vector<void*>> idle;  // reusable by any stream
-    std::map<hipStream_t, std::map<size_t, std::vector<void*>>> by_stream;  // reusable by that stream
-    size_t idle_bytes = 0, stream_bytes = 0;
+    DevCache dev[MAX_DEV];
 };
 
 Cache& cache()
@@ -564,13 +585,84 @@ Cache& cache()
     return *c;
 }
 
-void* take(std::map<size_t, std::vector<void*>>& m, size_t cls)
+int current_device()
+{
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= MAX_DEV) d = 0;
+    return d;
+}
+
+void* take(Lists& m, size_t cls)
 {
     auto it = m.find(cls);
     if (it == m.end() || it->second.empty()) return nullptr;
     void* p = it->second.back();
     it->second.pop_back();
     return p;
+}
+
+// pending groups whose events have all passed become idle (oldest first)
+void drain(DevCache& D)
+{
+    // hipEventQuery's "not ready" would stay behind as the thread's last
+    // error: clear it, unless an earlier error is waiting to be read
+    const bool clear = hipPeekAtLastError() == hipSuccess;
+    struct Clear {
+        bool on;
+        ~Clear()
+        {
+            if (on) (void)hipGetLastError();
+        }
+    } clear_on_exit{clear};
+    while (!D.pending.empty()) {
+        Pending& g = D.pending.front();
+        for (hipEvent_t e : g.ev)
+            if (hipEventQuery(e) != hipSuccess) return;
+        for (hipEvent_t e : g.ev) D.ev_pool.push_back(e);  // complete: reusable
+        for (auto& b : g.blocks) {
+            D.idle[b.second].push_back(b.first);
+            D.idle_bytes += b.second;
+            D.held_bytes -= b.second;
+        }
+        D.pending.pop_front();
+    }
+}
+
+// a pending group of `blocks`: one event on every library stream of the
+// device (the library queues work on its contexts' streams only; dx_malloc's
+// null-stream allocations are synchronised at once)
+void defer(DevCache& D, std::vector<std::pair<void*, size_t>>&& blocks)
+{
+    Pending g;
+    g.blocks = std::move(blocks);
+    if (D.streams.empty()) {  // no context: nothing can be in flight on the library's behalf
+        for (auto& b : g.blocks) {
+            D.idle[b.second].push_back(b.first);
+            D.idle_bytes += b.second;
+        }
+        return;
+    }
+    for (hipStream_t s : D.streams) {
+        hipEvent_t e = nullptr;
+        if (!D.ev_pool.empty()) {
+            e = D.ev_pool.back();
+            D.ev_pool.pop_back();
+        } else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            e = nullptr;
+        }
+        if (!e || hipEventRecord(e, s) != hipSuccess) {  // cannot fence: wait for the device instead
+            if (e) D.ev_pool.push_back(e);
+            (void)hipDeviceSynchronize();
+            for (hipEvent_t x : g.ev) D.ev_pool.push_back(x);
+            g.ev.clear();
+            g.on.clear();
+            break;
+        }
+        g.ev.push_back(e);
+        g.on.push_back(s);
+    }
+    for (auto& b : g.blocks) D.held_bytes += b.second;
+    D.pending.push_back(std::move(g));
 }
 }  // namespace
 
@@ -580,14 +672,21 @@ hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_strea
     const size_t cls = bytes <= CACHE_MAX_BLOCK ? size_class(bytes) : 0;
     if (cls) {
         std::lock_guard<std::mutex> lk(C.m);
+        DevCache& D = C.dev[current_device()];
         void* q = nullptr;
         if (!any_stream) {
-            auto it = C.by_stream.find(st);
-            if (it != C.by_stream.end() && (q = take(it->second, cls))) C.stream_bytes -= cls;
+            auto it = D.by_stream.find(st);
+            if (it != D.by_stream.end() && (q = take(it->second, cls))) {
+                D.stream_bytes[st] -= cls;
+                D.held_bytes -= cls;
+            }
         }
-        if (!q && (q = take(C.idle, cls))) C.idle_bytes -= cls;
+        if (!q) {
+            drain(D);
+            if ((q = take(D.idle, cls))) D.idle_bytes -= cls;
+        }
         if (q) {
-            C.live[q] = cls;
+            D.live[q] = cls;
             *p = q;
             return hipSuccess;
         }
@@ -596,50 +695,128 @@ hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_strea
     if (e == hipSuccess && any_stream) e = hipStreamSynchronize(st);
     if (e == hipSuccess && cls) {
         std::lock_guard<std::mutex> lk(C.m);
-        C.live[*p] = cls;
+        C.dev[current_device()].live[*p] = cls;
     }
     return e;
 }
 
-void dx_cache_free(void* p, hipStream_t st, bool device_idle)
+void dx_cache_free(void* p, hipStream_t st, bool any_stream)
 {
     if (!p) return;
+    dx_cache_free_many(&p, 1, st, any_stream);
+}
+
+void dx_cache_free_many(void* const* ps, size_t n, hipStream_t st, bool any_stream)
+{
     Cache& C = cache();
     std::unique_lock<std::mutex> lk(C.m);
-    auto it = C.live.find(p);
-    if (it == C.live.end()) {  // an uncached (large) block
-        lk.unlock();
-        (void)hipFreeAsync(p, st);
-        return;
-    }
-    const size_t cls = it->second;
-    C.live.erase(it);
-    if (device_idle) {
-        // the device is idle: every stream's cached blocks are free for any stream
-        for (auto& kv : C.by_stream)
-            for (auto& b : kv.second)
-                for (void* q : b.second) C.idle[b.first].push_back(q);
-        C.idle_bytes += C.stream_bytes;
-        C.stream_bytes = 0;
-        C.by_stream.clear();
-        if (C.idle_bytes + cls > CACHE_MAX_TOTAL) {
-            lk.unlock();
-            (void)hipFreeAsync(p, nullptr);
-            return;
+    DevCache& D = C.dev[current_device()];
+    std::vector<std::pair<void*, size_t>> blocks;
+    std::vector<void*> large;
+    for (size_t i = 0; i < n; i++) {
+        if (!ps[i]) continue;
+        auto it = D.live.find(ps[i]);
+        if (it == D.live.end()) {  // an uncached (large) block: back to the pool
+            large.push_back(ps[i]);
+            continue;
         }
-        C.idle[cls].push_back(p);
-        C.idle_bytes += cls;
-        return;
+        blocks.emplace_back(ps[i], it->second);
+        D.live.erase(it);
     }
-    C.by_stream[st][cls].push_back(p);
-    C.stream_bytes += cls;
+    if (!any_stream) {  // ds_free: reused by `st` in stream order
+        size_t& sb = D.stream_bytes[st];
+        for (auto& b : blocks) {
+            D.by_stream[st][b.second].push_back(b.first);
+            sb += b.second;
+            D.held_bytes += b.second;
+        }
+        if (sb > STREAM_LIST_MAX) {  // make them common once `st` has passed this point
+            std::vector<std::pair<void*, size_t>> all;
+            for (auto& kv : D.by_stream[st])
+                for (void* q : kv.second) all.emplace_back(q, kv.first);
+            D.by_stream.erase(st);
+            D.held_bytes -= sb;
+            sb = 0;
+            defer(D, std::move(all));
+        }
+    } else if (!blocks.empty()) {
+        // diagnosis: 1 wait for the device, 2 wait for the library's streams, 3 reuse at once (unsafe)
+        static const int64_t sync_free = getenv_int("DCCRGX_SYNC_FREE", 0);
+        if (sync_free) {
+            lk.unlock();
+            if (sync_free == 1) (void)hipDeviceSynchronize();
+            if (sync_free == 2)
+                for (hipStream_t s2 : D.streams) (void)hipStreamSynchronize(s2);
+            lk.lock();
+            for (auto& b : blocks) {
+                D.idle[b.second].push_back(b.first);
+                D.idle_bytes += b.second;
+            }
+        } else if (D.idle_bytes + D.held_bytes > CACHE_MAX_TOTAL) {  // too much kept: wait and return them
+            lk.unlock();
+            (void)hipDeviceSynchronize();
+            for (auto& b : blocks) (void)hipFreeAsync(b.first, nullptr);
+            lk.lock();
+        } else {
+            defer(D, std::move(blocks));
+        }
+    }
+    lk.unlock();
+    if (!large.empty()) {
+        if (any_stream) (void)hipDeviceSynchronize();
+        for (void* q : large) (void)hipFreeAsync(q, any_stream ? nullptr : st);
+    }
+}
+
+void dx_cache_streams(hipStream_t a, hipStream_t b, bool add)
+{
+    Cache& C = cache();
+    std::lock_guard<std::mutex> lk(C.m);
+    DevCache& D = C.dev[current_device()];
+    if (!add) {
+        // the streams are synchronised and about to be destroyed: events
+        // recorded on them are complete, and are destroyed now (querying an
+        // event whose stream is gone corrupted the runtime's memory); so are
+        // the pooled events, which may have been recorded there last
+        for (Pending& g : D.pending)
+            for (size_t k = 0; k < g.ev.size();)
+                if (g.on[k] == a || g.on[k] == b) {
+                    (void)hipEventDestroy(g.ev[k]);
+                    g.ev.erase(g.ev.begin() + k);
+                    g.on.erase(g.on.begin() + k);
+                } else {
+                    k++;
+                }
+        for (hipEvent_t e : D.ev_pool) (void)hipEventDestroy(e);
+        D.ev_pool.clear();
+        drain(D);
+    }
+    for (hipStream_t s : {a, b}) {
+        if (add) {
+            D.streams.push_back(s);
+            continue;
+        }
+        // a destroyed stream (synchronised first): its blocks are common now
+        D.streams.erase(std::remove(D.streams.begin(), D.streams.end(), s), D.streams.end());
+        auto it = D.by_stream.find(s);
+        if (it == D.by_stream.end()) continue;
+        for (auto& kv : it->second)
+            for (void* q : kv.second) {
+                D.idle[kv.first].push_back(q);
+                D.idle_bytes += kv.first;
+                D.held_bytes -= kv.first;
+            }
+        D.by_stream.erase(it);
+        D.stream_bytes.erase(s);
+    }
 }
 
 size_t dx_cache_idle_bytes()
 {
     Cache& C = cache();
     std::lock_guard<std::mutex> lk(C.m);
-    return C.idle_bytes + C.stream_bytes;
+    DevCache& D = C.dev[current_device()];
+    return D.idle_bytes + D.held_bytes;
 }
 
 size_t dx_pool_idle_bytes()
@@ -680,6 +857,7 @@ int dccrgx_ctx_create(int device, int rank, int comm_size, dccrgx_ctx** out)
     DX_HIP(hipStreamCreateWithFlags(&c->comm, hipStreamNonBlocking));
     DX_HIP(hipEventCreateWithFlags(&c->ev_compute, hipEventDisableTiming));
     DX_HIP(hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
+    dx_cache_streams(c->compute, c->comm, true);  // frees are fenced on these streams
     *out = c;
     return DCCRGX_OK;
 }
@@ -690,6 +868,7 @@ int dccrgx_ctx_destroy(dccrgx_ctx* c)
     hipSetDevice(c->device);
     hipStreamSynchronize(c->compute);
     hipStreamSynchronize(c->comm);
+    dx_cache_streams(c->compute, c->comm, false);
     if (c->has_comm) ncclCommDestroy(c->nccl);
     hipEventDestroy(c->ev_compute);
     hipEventDestroy(c->ev_comm);

@@ -617,7 +617,7 @@ __global__ void __launch_bounds__(256) k_sort_unique_rows_seg(const uint64_t* __
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const int lane = threadIdx.x & 63, sl = lane & (W - 1), seg = lane / W;
-    const uint64_t segmask = (W == 64 ? ~0ull : ((1ull << W) - 1ull)) << (seg * W);
+    const uint64_t segmask = (W >= 64 ? ~0ull : ((1ull << (W & 63)) - 1ull)) << (seg * W);
     for (uint64_t r0 = wave * R; r0 < n; r0 += waves * R) {
         const uint64_t r = r0 + seg;
         bool active = r < n && (!PEND_ONLY || ucnt[r] == ROW_PEND);
@@ -728,7 +728,7 @@ __global__ void __launch_bounds__(256) k_stencil_rows_seg(const uint64_t* __rest
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const int lane = threadIdx.x & 63, sl = lane & (W - 1), seg = lane / W;
-    const uint64_t segmask = (W == 64 ? ~0ull : ((1ull << W) - 1ull)) << (seg * W);
+    const uint64_t segmask = (W >= 64 ? ~0ull : ((1ull << (W & 63)) - 1ull)) << (seg * W);
     for (uint64_t i0 = wave * R; i0 < nl; i0 += waves * R) {
         const uint64_t i = i0 + seg;
         bool active = i < nl && (!PEND_ONLY || ucnt[i] == ROW_PEND);
@@ -1310,7 +1310,211 @@ int explicit_host_lists(const dccrgx_grid* grid, int32_t hood_id)
     return explicit_host_lists(grid, *h);
 }
 
-int explicit_build_hood(dccrgx_grid* grid, Hood& h)
+// Incremental neighbors_of after a refinement round (rebuild
+// around the changed cells).  A kept leaf whose old row references no gone
+// leaf has the same row as before -- its windows are still covered by the
+// same leaves, since new leaves only cover regions that gone leaves covered
+// -- so its ids and offsets are copied and only the leaf indices remapped;
+// rows of new leaves and of kept leaves next to a change are recomputed.
+__global__ void __launch_bounds__(256) k_inc_new2old(ExView oldv, const uint64_t* __restrict__ leaves, uint64_t n,
+                                                     uint32_t* __restrict__ new2old, uint32_t* __restrict__ old2new)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+        const int64_t o = ex_find(oldv, leaves[j]);
+        new2old[j] = o < 0 ? NO_SLOT : (uint32_t)o;
+        if (o >= 0) old2new[o] = (uint32_t)j;
+    }
+}
+
+// old leaves whose row references a gone leaf (or that are gone)
+__global__ void __launch_bounds__(256) k_inc_touched(const uint64_t* __restrict__ row, const uint32_t* __restrict__ g,
+                                                     uint64_t n, const uint32_t* __restrict__ flags, uint32_t gone,
+                                                     uint8_t* __restrict__ touched)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += stride) {
+        bool t = (flags[o] & gone) != 0;
+        for (uint64_t e = row[o]; e < row[o + 1] && !t; e++) t = (flags[g[e]] & gone) != 0;
+        touched[o] = t ? 1 : 0;
+    }
+}
+
+// counts of copied rows; the other leaves listed for recomputation
+__global__ void __launch_bounds__(256) k_inc_count(const uint32_t* __restrict__ new2old,
+                                                   const uint8_t* __restrict__ touched, const uint64_t* __restrict__ orow,
+                                                   const uint64_t* __restrict__ leaves, uint64_t n,
+                                                   uint64_t* __restrict__ row, uint32_t* __restrict__ aff,
+                                                   uint64_t* __restrict__ aff_ids, uint32_t* __restrict__ naff)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+        const uint32_t o = new2old[j];
+        if (o != NO_SLOT && !touched[o]) {
+            row[j + 1] = orow[o + 1] - orow[o];
+            continue;
+        }
+        const uint32_t k = atomicAdd(naff, 1u);
+        aff[k] = (uint32_t)j;
+        aff_ids[k] = leaves[j];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_inc_aff_rows(const uint32_t* __restrict__ aff, uint64_t naff,
+                                                      const uint64_t* __restrict__ cnt_row, uint64_t* __restrict__ row,
+                                                      uint64_t* __restrict__ start, int fill)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < naff; k += stride) {
+        if (!fill) row[aff[k] + 1] = cnt_row[k + 1];  // the count pass' counts into the full row array
+        else start[k] = row[aff[k]];                  // the recomputed rows' places
+    }
+}
+
+// copied rows: one wave per 64 new leaves, consecutive lanes on consecutive entries
+__global__ void __launch_bounds__(64) k_inc_copy(const uint32_t* __restrict__ new2old, const uint8_t* __restrict__ touched,
+                                                 uint64_t n, const uint64_t* __restrict__ orow,
+                                                 const uint64_t* __restrict__ oid, const int32_t* __restrict__ ooff,
+                                                 const uint32_t* __restrict__ og, const uint32_t* __restrict__ old2new,
+                                                 const uint64_t* __restrict__ row, uint64_t* __restrict__ ids,
+                                                 int32_t* __restrict__ off, uint32_t* __restrict__ g)
+{
+    __shared__ uint64_t s_dst[65], s_src[64];
+    const int lane = threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t j = r0 + lane;
+    // rows of recomputed leaves take no entries here (empty source runs)
+    uint64_t len = 0, src = 0;
+    if (j < n) {
+        const uint32_t o = new2old[j];
+        if (o != NO_SLOT && !touched[o]) {
+            src = orow[o];
+            len = orow[o + 1] - src;
+        }
+    }
+    s_src[lane] = src;
+    // a run per lane: the copied rows are not contiguous in the output when
+    // recomputed rows sit between them, so each entry finds its lane
+    __shared__ uint64_t s_len[64], s_out[64];
+    s_len[lane] = len;
+    s_out[lane] = j < n ? row[j] : 0;
+    __syncthreads();
+    if (lane == 0) {
+        uint64_t acc = 0;
+        for (int k = 0; k < 64; k++) {
+            s_dst[k] = acc;
+            acc += s_len[k];
+        }
+        s_dst[64] = acc;
+    }
+    __syncthreads();
+    const uint64_t tot = s_dst[64];
+    for (uint64_t e = lane; e < tot; e += 64) {
+        int lo = 0, hi = 64;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_dst[mid] <= e) lo = mid;
+            else hi = mid;
+        }
+        const uint64_t k = e - s_dst[lo];
+        const uint64_t se = s_src[lo] + k, de = s_out[lo] + k;
+        ids[de] = oid[se];
+        g[de] = old2new[og[se]];
+        off[3 * de + 0] = ooff[3 * se + 0];
+        off[3 * de + 1] = ooff[3 * se + 1];
+        off[3 * de + 2] = ooff[3 * se + 2];
+    }
+}
+
+static bool incremental_rebuild(uint64_t n)
+{
+    const int64_t force = getenv_int("DCCRGX_INCREMENTAL", -1);  // 1 / 0: always / never (tests)
+    if (force >= 0) return force != 0;
+    return n >= (1ull << 20);  // below, one full pass costs less than the extra launches
+}
+
+// neighbors_of of every leaf from the previous lists (see above)
+static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_t* total, hipStream_t st)
+{
+    Explicit* E = grid->ex;
+    Ctx* ctx = grid->ctx;
+    const uint64_t N = E->n, oN = H.old_ex->n;
+    const Hood& oh = *H.old_h;
+    const ExView v = view(grid);
+    ExView ov = v;
+    ov.keys = H.old_ex->d_keys;
+    ov.vals = H.old_ex->d_vals;
+    ov.mask = H.old_ex->mask;
+    ov.bits = H.old_ex->d_bits;
+    ov.rank = H.old_ex->d_rank;
+    uint32_t *d_n2o = nullptr, *d_o2n = nullptr, *d_aff = nullptr, *d_naff = nullptr;
+    uint8_t* d_touched = nullptr;
+    uint64_t *d_aff_ids = nullptr, *d_crow = nullptr, *d_start = nullptr;
+    int32_t* d_err = nullptr;
+    auto done = [&](int code) {
+        for (void* q : {(void*)d_n2o, (void*)d_o2n, (void*)d_aff, (void*)d_naff, (void*)d_touched, (void*)d_aff_ids,
+                        (void*)d_crow, (void*)d_start, (void*)d_err})
+            ds_free(q, st);
+        return code;
+    };
+    if (ds_malloc(&d_n2o, N * 4, st) != hipSuccess || ds_malloc(&d_o2n, oN * 4, st) != hipSuccess ||
+        ds_malloc(&d_aff, N * 4, st) != hipSuccess || ds_malloc(&d_naff, 16, st) != hipSuccess ||
+        ds_malloc(&d_touched, oN, st) != hipSuccess || ds_malloc(&d_aff_ids, N * 8, st) != hipSuccess ||
+        ds_malloc(&d_err, 16, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "incremental neighbor lists"));
+    hipMemsetAsync(d_o2n, 0xff, oN * 4, st);
+    hipMemsetAsync(d_naff, 0, 16, st);
+    hipMemsetAsync(d_err, 0, 16, st);
+    hipLaunchKernelGGL(k_inc_new2old, dim3(grid_for(N)), dim3(256), 0, st, ov, (const uint64_t*)E->d_leaves, N, d_n2o,
+                       d_o2n);
+    hipLaunchKernelGGL(k_inc_touched, dim3(grid_for(oN)), dim3(256), 0, st, (const uint64_t*)oh.d_nof_row,
+                       (const uint32_t*)oh.d_nof_g, oN, H.old_flags, H.gone_bit, d_touched);
+    hipMemsetAsync(h.d_nof_row, 0, 8, st);
+    hipLaunchKernelGGL(k_inc_count, dim3(grid_for(N)), dim3(256), 0, st, (const uint32_t*)d_n2o,
+                       (const uint8_t*)d_touched, (const uint64_t*)oh.d_nof_row, (const uint64_t*)E->d_leaves, N,
+                       h.d_nof_row, d_aff, d_aff_ids, d_naff);
+    if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "incremental neighbor lists"));
+    uint32_t naff = 0;
+    int s = dx_d2h(ctx, &naff, d_naff, 4, st);
+    if (s != DCCRGX_OK) return done(s);
+    if (ds_malloc(&d_crow, (uint64_t)(naff + 1) * 8, st) != hipSuccess ||
+        ds_malloc(&d_start, std::max<uint64_t>(naff, 1) * 8, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "incremental neighbor lists"));
+    if (naff) {  // counts of the recomputed rows
+        hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(naff)), dim3(256), 0, st, v, h.d_of_c, h.K,
+                           (const uint64_t*)d_aff_ids, (size_t)naff, d_crow, (uint64_t*)nullptr, (int32_t*)nullptr,
+                           (uint32_t*)nullptr, d_err);
+        hipLaunchKernelGGL(k_inc_aff_rows, dim3(grid_for(naff)), dim3(256), 0, st, (const uint32_t*)d_aff,
+                           (uint64_t)naff, (const uint64_t*)d_crow, h.d_nof_row, d_start, 0);
+    }
+    if ((s = device_scan_rows(h.d_nof_row, N, st, nullptr)) != DCCRGX_OK) return done(s);
+    uint64_t back[2] = {0, 0};  // error word, total
+    hipMemcpyAsync(d_err + 2, h.d_nof_row + N, 8, hipMemcpyDeviceToDevice, st);
+    if ((s = dx_d2h(ctx, back, d_err, 16, st)) != DCCRGX_OK) return done(s);
+    if (back[0] & 0xffffffffu)
+        return done(set_error(back[0] & 1 ? DCCRGX_ENOTFOUND : DCCRGX_EINTERNAL,
+                              back[0] & 1 ? "cell does not exist" : "neighbor more than one level apart"));
+    *total = back[1];
+    const uint64_t t = std::max<uint64_t>(*total, 1);
+    if (ds_malloc(&h.d_nof_id, t * 8, st) != hipSuccess || ds_malloc(&h.d_nof_off, t * 12, st) != hipSuccess ||
+        ds_malloc(&h.d_nof_g, t * 4, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "neighbor lists of %llu entries", (unsigned long long)*total));
+    hipLaunchKernelGGL(k_inc_copy, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, (const uint32_t*)d_n2o,
+                       (const uint8_t*)d_touched, N, (const uint64_t*)oh.d_nof_row, (const uint64_t*)oh.d_nof_id,
+                       (const int32_t*)oh.d_nof_off, (const uint32_t*)oh.d_nof_g, (const uint32_t*)d_o2n,
+                       (const uint64_t*)h.d_nof_row, h.d_nof_id, h.d_nof_off, h.d_nof_g);
+    if (naff) {  // the recomputed rows, each thread at its row's place
+        hipLaunchKernelGGL(k_inc_aff_rows, dim3(grid_for(naff)), dim3(256), 0, st, (const uint32_t*)d_aff,
+                           (uint64_t)naff, (const uint64_t*)d_crow, h.d_nof_row, d_start, 1);
+        hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(naff)), dim3(256), 0, st, v, h.d_of_c, h.K,
+                           (const uint64_t*)d_aff_ids, (size_t)naff, d_start, h.d_nof_id, h.d_nof_off, h.d_nof_g,
+                           d_err);
+    }
+    if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "incremental neighbor lists"));
+    return done(DCCRGX_OK);
+}
+
+int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint)
 {
     Explicit* E = grid->ex;
     Ctx* ctx = grid->ctx;
@@ -1330,7 +1534,11 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h)
     // neighbors_of of every leaf (the reference also builds all of them)
     DX_HIP(ds_malloc(&h.d_nof_row, (N + 1) * 8, st));
     uint64_t tot = 0;
-    DX_TRY(nof_device(grid, h, E->d_leaves, N, h.d_nof_row, &h.d_nof_id, &h.d_nof_off, &h.d_nof_g, &tot, st));
+    if (hint && hint->old_h && hint->old_h->d_nof_row && hint->old_h->items == h.items && hint->old_ex &&
+        incremental_rebuild(hint->old_ex->n))
+        DX_TRY(nof_incremental(grid, h, *hint, &tot, st));
+    else
+        DX_TRY(nof_device(grid, h, E->d_leaves, N, h.d_nof_row, &h.d_nof_id, &h.d_nof_off, &h.d_nof_g, &tot, st));
     T.lap("neighbors_of");
     // neighbors_to = transpose (rows: leaves)
     uint32_t *d_cnt = nullptr, *d_cur = nullptr, *d_tmp = nullptr, *d_ucnt = nullptr;

@@ -387,7 +387,17 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids);
 int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_src, hipStream_t st);
 // dst[k] = src[from[k]], or zero where from[k] < 0
 int launch_move(const void* src, const int64_t* from, uint64_t n, uint32_t elem, void* dst, hipStream_t st);
-int explicit_build_hood(dccrgx_grid* grid, Hood& h);
+// the previous leaf set's lists of the same neighborhood and which of its
+// leaves are gone (flags & gone_bit): rows of kept leaves that reference no
+// gone leaf are copied from `old_h` instead of recomputed (amr.hip rebuild)
+constexpr uint32_t AMR_FLAG_GONE = 16u;  // amr_dev.hip RF_GONE: the leaf disappears in the rebuild
+struct NofHint {
+    const Explicit* old_ex;
+    const Hood* old_h;
+    const uint32_t* old_flags;
+    uint32_t gone_bit;
+};
+int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint = nullptr);
 // host copies of a neighborhood's neighbor lists, fetched once per build
 int explicit_host_lists(const dccrgx_grid* grid, const Hood& h);
 int explicit_host_lists(const dccrgx_grid* grid, int32_t hood_id);

@@ -62,10 +62,17 @@ size_t dx_pool_idle_bytes();
 // HIP runtime (4 us on /opt/rocm's) and an adaptive step freed ~60 scratch
 // buffers -- 2 ms of the step (tools/api_census.py).  A block freed with
 // ds_free on a stream is reused only by that stream (stream order keeps it
-// safe); blocks freed with dx_free / FreeBatch (after a device-wide wait)
-// are reused by any.
+// safe); blocks freed with dx_free / FreeBatch are reused by any stream once
+// events recorded on every library stream at the free have passed -- no
+// host wait, so a free between a halo's start and wait does not block on
+// the exchange.
 hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_stream);
-void dx_cache_free(void* p, hipStream_t st, bool device_idle);
+// any_stream: the block becomes reusable by any stream once every library
+// stream of the device has passed the free (events, no host wait)
+void dx_cache_free(void* p, hipStream_t st, bool any_stream);
+void dx_cache_free_many(void* const* ps, size_t n, hipStream_t st, bool any_stream);
+// a context's streams join (add) or leave the set the frees are fenced on
+void dx_cache_streams(hipStream_t a, hipStream_t b, bool add);
 size_t dx_cache_idle_bytes();
 
 template <class T>
@@ -80,17 +87,12 @@ inline hipError_t dx_malloc(T** p, size_t bytes)
 
 inline hipError_t dx_free(void* p)
 {
-    if (!p) return hipSuccess;
-    const auto t0 = std::chrono::steady_clock::now();
-    hipError_t e = hipDeviceSynchronize();
-    if (e == hipSuccess) dx_cache_free(p, nullptr, true);
-    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    if (ms > 1.0) dx_slow_note("dx_free", 0, ms);
-    return e;
+    if (p) dx_cache_free(p, nullptr, true);
+    return hipSuccess;
 }
 
-// Frees of many buffers after one wait for the device (structures are
-// released together: a neighborhood, an explicit grid's state)
+// Frees of many buffers behind one set of events (structures are released
+// together: a neighborhood, an explicit grid's state)
 struct FreeBatch {
     std::vector<void*> v;
     void add(void* p)
@@ -99,8 +101,7 @@ struct FreeBatch {
     }
     ~FreeBatch()
     {
-        if (v.empty() || hipDeviceSynchronize() != hipSuccess) return;
-        for (void* p : v) dx_cache_free(p, nullptr, true);
+        if (!v.empty()) dx_cache_free_many(v.data(), v.size(), nullptr, true);
     }
 };
 

@@ -102,8 +102,17 @@ SEQ_CASES = [  # length, M, periodic, hood, P, rounds, seed
 ]
 
 
+@pytest.fixture(params=["full", "incremental"])
+def rebuild_mode(request, monkeypatch):
+    """The rebuild's neighbors_of: recomputed for every leaf, or copied for
+    rows that reference no removed leaf (explicit.hip nof_incremental; the
+    library picks it above 2^20 leaves, DCCRGX_INCREMENTAL forces it)."""
+    monkeypatch.setenv("DCCRGX_INCREMENTAL", "1" if request.param == "incremental" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("case", SEQ_CASES)
-def test_random_request_sequences(case):
+def test_random_request_sequences(case, rebuild_mode):
     length, M, per, hood, P, rounds, seed = case
     rng = np.random.default_rng(seed)
     o = AmrOracle(length, M, per, hood, P)
@@ -144,7 +153,7 @@ KINDS = (("refine_completely", 0), ("dont_unrefine", 3), ("unrefine_completely",
 
 
 @pytest.mark.parametrize("case", BATCH_CASES)
-def test_batched_requests_match_sequential_calls(case):
+def test_batched_requests_match_sequential_calls(case, rebuild_mode):
     """dccrgx_amr_request_cells on explicit grids runs each batch on the
     device (amr_dev.hip); its results and the four sets afterwards equal the
     reference's calls made one by one in the same order (the oracle), with
