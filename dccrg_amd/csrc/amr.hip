@@ -329,7 +329,7 @@ int rebuild(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<
         s = explicit_build_hood(grid, it->second, gone_flags && !old.uniform && old.ex ? &hint : nullptr);
     }
     T.lap("neighborhoods");
-    if (s == DCCRGX_OK) s = explicit_add_slots(grid, retired);
+    if (s == DCCRGX_OK) s = explicit_add_slots(grid, retired, true);  // retired cells are not leaves
     if (s != DCCRGX_OK) return rollback(s);
     T.lap("retired slots");
     Explicit* E = grid->ex;

@@ -981,11 +981,18 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
     // block partition or the grid's SFC table
     E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
     E->owner.resize(E->n);
-    if (ctx->comm_size == 1) {  // one process owns every leaf
-        std::fill(E->owner.begin(), E->owner.end(), 0);
-        E->local = E->leaves;
+    if (ctx->comm_size == 1) {  // one process owns every leaf: identity maps, filled by the host threads
+        E->local.resize(E->n);
         E->local_g.resize(E->n);
-        for (uint64_t i = 0; i < E->n; i++) E->local_g[i] = (uint32_t)i;
+        E->slot_ids.resize(E->n);
+        E->slot_of_g.resize(E->n);
+        parallel_ranges(E->n, 1u << 16, [E](size_t b, size_t e) {
+            std::fill(E->owner.begin() + b, E->owner.begin() + e, 0);
+            std::copy(E->leaves.begin() + b, E->leaves.begin() + e, E->local.begin() + b);
+            std::copy(E->leaves.begin() + b, E->leaves.begin() + e, E->slot_ids.begin() + b);
+            for (size_t i = b; i < e; i++) E->local_g[i] = E->slot_of_g[i] = (uint32_t)i;
+        });
+        E->slot_identity = true;
     }
     for (uint64_t i = 0; ctx->comm_size > 1 && i < E->n; i++) {
         uint64_t idx[3];
@@ -1003,9 +1010,11 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
     grid->n_local = E->local.size();
     grid->first_local = E->local.empty() ? 0 : E->local[0];
     // storage: the local cells first (ghosts are added by the neighborhoods)
-    E->slot_ids = E->local;
-    E->slot_of_g.assign(E->n, NO_SLOT);
-    for (uint64_t i = 0; i < E->local.size(); i++) E->slot_of_g[E->local_g[i]] = (uint32_t)i;
+    if (ctx->comm_size > 1) {
+        E->slot_ids = E->local;
+        E->slot_of_g.assign(E->n, NO_SLOT);
+        for (uint64_t i = 0; i < E->local.size(); i++) E->slot_of_g[E->local_g[i]] = (uint32_t)i;
+    }
     DX_TRY(device_iota(&E->d_local_slot, E->local.size(), st));  // local position -> slot: identity
     T.lap("owners+local");
     DX_TRY(sync_slots(grid, true));
@@ -1035,7 +1044,8 @@ static int sync_slots(dccrgx_grid* grid, bool slot_map_changed)
     if (slot_map_changed || !E->d_slot_of_g) {
         dx_free(E->d_slot_of_g);
         E->d_slot_of_g = nullptr;
-        DX_TRY(upload(grid->ctx, E->slot_of_g, &E->d_slot_of_g, st));
+        if (E->slot_identity) DX_TRY(device_iota(&E->d_slot_of_g, E->n, st));  // one rank: leaf g in slot g
+        else DX_TRY(upload(grid->ctx, E->slot_of_g, &E->d_slot_of_g, st));
     }
     if (ns > E->d_level_cap || !E->d_level) {
         const uint64_t cap = std::max<uint64_t>(ns + ns / 4, 16);
@@ -1103,13 +1113,13 @@ static int grow_fields(dccrgx_grid* grid, uint64_t old_ns, uint64_t ns)
     return DCCRGX_OK;
 }
 
-int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
+int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids, bool not_leaves)
 {
     Explicit* E = grid->ex;
     const uint64_t old_ns = E->slot_ids.size();
     bool leaf_slot = false;  // a leaf got a (ghost) slot: the slot map changes
     for (uint64_t c : ids) {
-        const int64_t g = E->find(c);
+        const int64_t g = not_leaves ? -1 : E->find(c);  // retired cells are no leaves: no host lookup
         if ((g >= 0 && E->slot_of_g[g] != NO_SLOT) || E->extra.count(c)) continue;  // has a slot
         const uint32_t s = (uint32_t)E->slot_ids.size();
         E->slot_ids.push_back(c);
@@ -1117,6 +1127,7 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
         if (g >= 0) {
             E->slot_of_g[g] = s;
             leaf_slot = true;
+            E->slot_identity = false;
         }
     }
     const uint64_t ns = E->slot_ids.size();
@@ -1594,7 +1605,9 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     std::map<int, std::set<uint64_t>> send, recv;
     if (ctx->comm_size == 1) {  // one process: every cell is inner, nothing remote
         L.inner_pos.resize(nl);
-        for (uint64_t i = 0; i < nl; i++) L.inner_pos[i] = (uint32_t)i;
+        parallel_ranges(nl, 1u << 16, [&L](size_t b, size_t e) {
+            for (size_t i = b; i < e; i++) L.inner_pos[i] = (uint32_t)i;
+        });
     }
     for (uint64_t i = 0; ctx->comm_size > 1 && i < nl; i++) {
         const uint32_t r = E->local_g[i];

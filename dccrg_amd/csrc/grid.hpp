@@ -147,6 +147,7 @@ struct Explicit {
     std::vector<uint64_t> slot_ids;                 // id held by each slot
     FlatMap32 extra;                                // ghost / retired id -> slot
     std::vector<uint32_t> slot_of_g;                // global leaf index -> slot (NO_SLOT)
+    bool slot_identity = false;                     // slot_of_g[g] == g (one rank, no ghost leaves)
     uint32_t* d_slot_of_g = nullptr;
     uint32_t* d_local_slot = nullptr;               // local position -> slot (identity)
     uint8_t* d_level = nullptr;                     // refinement level of each slot
@@ -382,7 +383,7 @@ void explicit_recycle(dccrgx_grid* grid, Explicit* E);
 void explicit_clear_retired(Explicit* E);
 // explicit grids: give `ids` (leaves or retired cells) storage slots if they
 // have none, growing every field unless a rebuild defers that
-int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids);
+int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids, bool not_leaves = false);
 // rebuild(): old slot (or -1) of every slot of the new layout, device output
 int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_src, hipStream_t st);
 // dst[k] = src[from[k]], or zero where from[k] < 0

@@ -16,6 +16,7 @@ from dccrg_amd import advection as A  # noqa: E402
 
 ctx = D.Context(0, 0, 1)
 rel, thr, sens, cfl, M = 0.025, 0.25, 0.5, 0.5, 2
+rel = float(os.environ.get("ADAPT_REL", rel))  # larger grids: smaller differences between neighbors
 NX = int(os.environ.get("ADAPT_N", "400"))  # cells per side (configs[2]: 400)
 g = (D.Dccrg().set_initial_length((NX, NX, 1)).set_maximum_refinement_level(M)
      .set_periodic(True, True, False).set_neighborhood_length(0).initialize(ctx))
