@@ -369,8 +369,10 @@ def mapping_speed_test(D, torch, dev):
 
 def neighbor_lists(ctx, D, torch):
     """SURVEY 8(d) 'neighbor build': batched get_neighbors_of (dccrgx_neighbors_of:
-    count pass, scan, fill pass) on the device.  Output bytes = entries x 20 B
-    (u64 id + 3 x i32 offset) + 8 B of row pointer per cell.
+    row counts, scan, fill pass) on the device, one call per query with the
+    capacity known (`ms`); `ms_with_sizing_call` adds the sizing call of the
+    two-call protocol.  Output bytes = entries x 20 B (u64 id + 3 x i32
+    offset) + 8 B of row pointer per cell.
     (a) uniform 1024^3 grid, hood 1, periodic z: the first 2^24 cells
         (closed-form lists, dccrg.hpp:4375-4716 on a level-0 grid);
     (b) mixed levels: 128^3 with 5 % of the cells refined once (2.8 M
@@ -391,21 +393,28 @@ def neighbor_lists(ctx, D, torch):
         ids = torch.empty(total, dtype=torch.int64, device=dev)
         off = torch.empty((total, 3), dtype=torch.int32, device=dev)
 
-        def once():
-            X.check(D.lib().dccrgx_neighbors_of(g._h, X.DEFAULT_NEIGHBORHOOD_ID, cells.data_ptr(), q,
-                                                row.data_ptr(), None, None, 0, None))
+        def fill():  # one call: rows and lists (the capacity is known)
             X.check(D.lib().dccrgx_neighbors_of(g._h, X.DEFAULT_NEIGHBORHOOD_ID, cells.data_ptr(), q,
                                                 row.data_ptr(), ids.data_ptr(), off.data_ptr(), total, None))
-        once()
-        ctx.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            once()
-        ctx.synchronize()
-        dt = (time.perf_counter() - t0) / reps
+
+        def sized():  # the two-call protocol: size, then fill
+            X.check(D.lib().dccrgx_neighbors_of(g._h, X.DEFAULT_NEIGHBORHOOD_ID, cells.data_ptr(), q,
+                                                row.data_ptr(), None, None, 0, None))
+            fill()
+
+        def timed(fn):
+            fn()
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            ctx.synchronize()
+            return (time.perf_counter() - t0) / reps
+        dt, dt2 = timed(fill), timed(sized)
         byt = 20 * total + 8 * (q + 1)
         del ids, off, row
-        return {"cells": q, "entries": total, "ms": dt * 1e3, "cells_per_s": q / dt, "output_GBs": byt / dt / 1e9}
+        return {"cells": q, "entries": total, "ms": dt * 1e3, "cells_per_s": q / dt, "output_GBs": byt / dt / 1e9,
+                "ms_with_sizing_call": dt2 * 1e3}
 
     n = 1024
     g = (D.Dccrg().set_initial_length((n, n, n)).set_neighborhood_length(1)
