@@ -437,9 +437,15 @@ int main(int argc, char** argv)
     uint32_t *in, *out, *cnt, *ref_out, *ref_cnt;
     unsigned long long* d_bad;
     CK(hipMalloc(&d_bad, 8));
-    CK(hipMalloc(&in, N * 4));
-    CK(hipMalloc(&out, N * 4));
-    CK(hipMalloc(&cnt, N * 4));
+    // STAGGER=<bytes> (multiple of 16): out and cnt start that many (twice as
+    // many) bytes later than their allocations, to test address aliasing
+    const size_t stg = getenv("STAGGER") ? (size_t)atoll(getenv("STAGGER")) & ~(size_t)15 : 0;
+    CK(hipMalloc(&in, N * 4 + 2 * stg));
+    CK(hipMalloc(&out, N * 4 + 2 * stg));
+    CK(hipMalloc(&cnt, N * 4 + 2 * stg));
+    out += stg / 4;
+    cnt += 2 * stg / 4;
+    if (stg) printf("stagger %zu B\n", stg);
     CK(hipMalloc(&ref_out, N * 4));
     CK(hipMalloc(&ref_cnt, N * 4));
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, in, (size_t)N);
@@ -518,8 +524,8 @@ int main(int argc, char** argv)
         printf("%-20s %s %9.4f ms %8.1f GB/s\n", v.name, same ? "ok  " : "DIFF", ms, bytes / (ms * 1e6));
     }
     CK(hipFree(in));
-    CK(hipFree(out));
-    CK(hipFree(cnt));
+    CK(hipFree(out - stg / 4));
+    CK(hipFree(cnt - 2 * stg / 4));
     CK(hipFree(ref_out));
     CK(hipFree(ref_cnt));
     CK(hipFree(d_bad));
