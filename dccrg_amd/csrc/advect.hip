@@ -71,31 +71,6 @@ __device__ inline int face_dir(int64_t cl, int64_t nl, const int32_t* off)
     return overlaps == 2 ? direction : 0;
 }
 
-// explicit (mixed-level) grids: gather over the iteration-cache stencil rows
-__global__ void __launch_bounds__(256) k_ex_advect(AdvPtrs p, double dt, const uint64_t* __restrict__ st_row,
-                                                   const uint32_t* __restrict__ st_slot,
-                                                   const int32_t* __restrict__ st_off,
-                                                   const uint32_t* __restrict__ local_g,
-                                                   const uint8_t* __restrict__ level, int M,
-                                                   const uint32_t* __restrict__ pos, uint64_t n)
-{
-#pragma clang fp contract(off)
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t q = pos[i];
-        const uint32_t c = local_g[q];
-        const int64_t cl = 1ll << (M - level[c]);
-        const double vol = p.l[0][c] * p.l[1][c] * p.l[2][c];
-        double acc = p.flux[c];
-        for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) {
-            const uint32_t nb = st_slot[e];
-            const int dir = face_dir(cl, 1ll << (M - level[nb]), st_off + 3 * e);
-            if (dir) acc += face_term(p, c, nb, dir, dt, vol);
-        }
-        p.flux[c] = acc;
-    }
-}
-
 // face lists of local cells from the stencil rows: pass 1 (o_row == null)
 // writes the first 6 faces column-major and counts the rest into o_cnt;
 // pass 2 writes the rest at o_row
@@ -594,17 +569,12 @@ int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect
         if (!R.n) return DCCRGX_OK;
         Hood* hm = find_hood(grid, hood_id);
         if (!hm->faces) DX_TRY(build_faces(grid, *hm));
-        if (getenv("DCCRGX_ADVECT_ROWS"))  // the plain stencil-row gather (comparison path)
-            hipLaunchKernelGGL(k_ex_advect, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, h->d_st_row,
-                               h->d_st_slot, h->d_st_off, R.local_slot, R.level, grid->map.max_lvl, R.pos, R.n);
-        else {
-            const FaceCache& F = *hm->faces;
-            const FaceView fv{F.n, F.ell_slot, F.ell_dir, F.o_row, F.o_slot, F.o_dir, F.overflow};
-            // explicit grids store local cell q in slot q (explicit.hip): no slot loads
-            hipLaunchKernelGGL(k_ex_advect_faces, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, fv,
-                               (const uint32_t*)nullptr,
-                               region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos, R.n);
-        }
+        const FaceCache& F = *hm->faces;
+        const FaceView fv{F.n, F.ell_slot, F.ell_dir, F.o_row, F.o_slot, F.o_dir, F.overflow};
+        // explicit grids store local cell q in slot q (explicit.hip): no slot loads
+        hipLaunchKernelGGL(k_ex_advect_faces, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, fv,
+                           (const uint32_t*)nullptr, region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos,
+                           R.n);
         DX_HIP(hipGetLastError());
         return DCCRGX_OK;
     }

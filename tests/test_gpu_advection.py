@@ -56,19 +56,9 @@ def exchange(grids, fields, uniform):
         loopback(grids, list(fields))
 
 
-@pytest.fixture(params=["faces", "rows"])
-def adv_path(request, monkeypatch):
-    """Mixed-level grids: the face-list kernel and the plain stencil-row gather."""
-    if request.param == "rows":
-        monkeypatch.setenv("DCCRGX_ADVECT_ROWS", "1")
-    else:
-        monkeypatch.delenv("DCCRGX_ADVECT_ROWS", raising=False)
-    return request.param
-
-
 @pytest.mark.parametrize("P", [1, 3])
 @pytest.mark.parametrize("case", CASES)
-def test_advection_parity(case, P, adv_path):
+def test_advection_parity(case, P):
     uniform = case[4] is None
     lists, grids = build(case, P)
     state = O.advection_initial_state(O.Mapping(case[0], case[1]), lists.cells)
