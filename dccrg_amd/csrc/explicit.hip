@@ -1104,6 +1104,7 @@ static int grow_fields(dccrgx_grid* grid, uint64_t old_ns, uint64_t ns)
         if (F.variable) {  // new slots hold zero elements
             F.count.resize(ns, 0);
             F.off.resize(ns, F.pool_bytes);
+            F.epoch = next_var_epoch();
             continue;
         }
         dx_free(F.ptr);

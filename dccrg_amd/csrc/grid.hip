@@ -275,10 +275,14 @@ void free_hood(Hood& h)
 {
     FreeBatch fb;
     for (void* p : {(void*)h.d_of_c, (void*)h.d_to_c, (void*)h.d_self_dst, (void*)h.d_self_src}) fb.add(p);
-    for (PeerPlan& p : h.peers)
+    for (PeerPlan& p : h.peers) {
         for (void* q : {(void*)p.d_send_slots, (void*)p.d_unpack_dst, (void*)p.d_unpack_src, p.d_send_buf,
                         p.d_recv_buf})
             fb.add(q);
+        free_var_plans(p.var_send, fb);
+        free_var_plans(p.var_recv, fb);
+    }
+    free_var_plans(h.var_self, fb);
     h.d_of_c = h.d_to_c = nullptr;
     h.d_self_dst = h.d_self_src = nullptr;
     h.peers.clear();
@@ -578,6 +582,10 @@ int build_hood(dccrgx_grid* grid, Hood& h)
         self.clear();
     }
     h.h_self = self;
+    {
+        FreeBatch fb;
+        free_var_plans(h.var_self, fb);  // built for the previous copies
+    }
     // self copies: contiguous runs become memcpys when there are few of them
     std::vector<CopySeg> segs;
     for (auto& e : self) {

@@ -6,6 +6,7 @@
 #include "internal.hpp"
 
 #include <array>
+#include <map>
 #include <set>
 #include <unordered_map>
 
@@ -83,6 +84,31 @@ __host__ __device__ inline uint64_t ug_slot(const UGeom& g, int64_t a, int64_t b
     return (uint64_t)a + g.LA * ((uint64_t)b + g.LB * (uint64_t)(cu - g.cbase));
 }
 
+// a byte copy between two device buffers (offsets relative to each)
+struct ByteSeg {
+    uint64_t src, dst, len;
+};
+
+// a variable-size field's byte segments for one copy -- a message's pack or
+// unpack, or the periodic self copies -- built from the host count / offset
+// mirrors once per count epoch and kept on the device
+struct VarPlan {
+    uint64_t epoch = 0;  // Field::epoch it was built for (0: none)
+    ByteSeg* d = nullptr;
+    uint64_t n = 0;      // segments
+    uint64_t bytes = 0;  // message bytes of the field (pack: sent, unpack: received)
+};
+using VarPlans = std::map<int32_t, VarPlan>;  // by field id
+
+// a fresh epoch for a variable field whose counts or offsets changed (never reused)
+uint64_t next_var_epoch();
+
+inline void free_var_plans(VarPlans& m, FreeBatch& fb)
+{
+    for (auto& kv : m) fb.add(kv.second.d);
+    m.clear();
+}
+
 struct Field {
     void* ptr = nullptr;
     uint32_t elem = 0;
@@ -94,6 +120,7 @@ struct Field {
     std::vector<uint32_t> count;
     std::vector<uint64_t> off;
     size_t pool_bytes = 0;
+    uint64_t epoch = 0;  // version of count / off (next_var_epoch), keys the cached VarPlans
 };
 
 struct PeerPlan {
@@ -122,6 +149,8 @@ struct PeerPlan {
     size_t recv_buf_bytes = 0;
     // host copies of the messages (host-staged transport)
     std::vector<char> h_send_msg, h_recv_msg;
+    // variable-size fields: pack / unpack segments per field
+    VarPlans var_send, var_recv;
 };
 
 struct Explicit {
@@ -292,6 +321,7 @@ struct Hood {
     uint64_t* d_self_dst = nullptr;
     uint64_t* d_self_src = nullptr;
     std::vector<std::pair<uint64_t, uint64_t>> h_self;  // all (dst, src) self copies
+    VarPlans var_self;                                   // their segments per variable-size field
     // slice ranges for the overlap split (storage slice indices, inclusive-exclusive)
     int64_t inner_s0 = 0, inner_s1 = 0;  // fully local and only local reads
     bool pending = false;                // halo started, not waited

@@ -8,6 +8,7 @@
 // slab layout the message is sent from / received into the field itself
 // (no pack, no unpack); otherwise a gather / scatter kernel stages it.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 
 #include "grid.hpp"
@@ -103,41 +104,82 @@ static int check_fields(const dccrgx_grid* g, const int32_t* f, size_t nf, size_
 }
 
 // ---- variable-size fields: byte segments ------------------------------------
-struct Seg {
-    uint64_t src, dst, len;  // byte offsets and length
-};
+using Seg = ByteSeg;
 
-// one wavefront per segment; 4-byte words when the segment allows it
+static std::atomic<uint64_t> g_var_epoch{0};
+uint64_t next_var_epoch() { return ++g_var_epoch; }
+
+// 16 lanes per segment (four segments per wavefront: cells of a few elements
+// are the common case); each group copies in the widest unit its segment's
+// addresses and length allow
 __global__ void __launch_bounds__(256) k_seg_copy(const Seg* __restrict__ segs, uint64_t n,
                                                   const char* __restrict__ src, char* __restrict__ dst)
 {
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
-    const uint64_t lane = threadIdx.x % 64;
-    const uint64_t waves = (uint64_t)gridDim.x * blockDim.x / 64;
-    for (uint64_t k = wave; k < n; k += waves) {
-        const Seg s = segs[k];
-        if (((s.src | s.dst | s.len) & 3) == 0) {
-            const uint32_t* a = (const uint32_t*)(src + s.src);
-            uint32_t* b = (uint32_t*)(dst + s.dst);
-            for (uint64_t i = lane; i < s.len / 4; i += 64) b[i] = a[i];
+    constexpr uint32_t G = 16;
+    const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const uint32_t lane = threadIdx.x % G;
+    const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
+    for (uint64_t k = grp; k < n; k += groups) {
+        const Seg sg = segs[k];
+        const char* a = src + sg.src;
+        char* b = dst + sg.dst;
+        const uint64_t al = (uint64_t)(uintptr_t)a | (uint64_t)(uintptr_t)b | sg.len;
+        if ((al & 15) == 0) {
+            for (uint64_t i = lane; i < sg.len / 16; i += G) ((uint4*)b)[i] = ((const uint4*)a)[i];
+        } else if ((al & 7) == 0) {
+            for (uint64_t i = lane; i < sg.len / 8; i += G) ((uint2*)b)[i] = ((const uint2*)a)[i];
+        } else if ((al & 3) == 0) {
+            for (uint64_t i = lane; i < sg.len / 4; i += G) ((uint32_t*)b)[i] = ((const uint32_t*)a)[i];
         } else {
-            for (uint64_t i = lane; i < s.len; i += 64) dst[s.dst + i] = src[s.src + i];
+            for (uint64_t i = lane; i < sg.len; i += G) b[i] = a[i];
         }
     }
 }
 
+static int launch_segs(const Seg* d, uint64_t n, const void* src, void* dst, hipStream_t st)
+{
+    if (!n) return DCCRGX_OK;
+    const uint64_t blocks = std::min<uint64_t>((n + 15) / 16, 4096);
+    hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)blocks), dim3(256), 0, st, d, n, (const char*)src, (char*)dst);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+// one-off copies from host-built segments (cell-addressed access, resize)
 static int seg_copy(const std::vector<Seg>& segs, const void* src, void* dst, hipStream_t st)
 {
     if (segs.empty()) return DCCRGX_OK;
     Seg* d = nullptr;
     DX_HIP(dx_malloc(&d, segs.size() * sizeof(Seg)));
     DX_HIP(hipMemcpyAsync(d, segs.data(), segs.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
-    const uint64_t blocks = std::min<uint64_t>((segs.size() + 3) / 4, 4096);
-    hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)blocks), dim3(256), 0, st, d, (uint64_t)segs.size(),
-                       (const char*)src, (char*)dst);
-    DX_HIP(hipGetLastError());
-    DX_HIP(hipStreamSynchronize(st));  // variable-size exchanges are not the bandwidth path
+    DX_TRY(launch_segs(d, segs.size(), src, dst, st));
+    DX_HIP(hipStreamSynchronize(st));
     dx_free(d);
+    return DCCRGX_OK;
+}
+
+// the cached plan of field fid in `plans`, (re)built by `build` when the
+// field's counts changed since
+template <class Build>
+static int var_plan(dccrgx_grid* g, VarPlans& plans, int32_t fid, Build build, const VarPlan** out)
+{
+    const Field& F = g->fields[fid];
+    VarPlan& P = plans[fid];
+    if (P.epoch != F.epoch || !F.epoch) {
+        std::vector<Seg> segs;
+        uint64_t bytes = 0;
+        build(F, segs, bytes);
+        dx_free(P.d);  // deferred past the work queued on the library's streams
+        P = VarPlan{};
+        if (!segs.empty()) {
+            DX_HIP(dx_malloc(&P.d, segs.size() * sizeof(Seg)));
+            DX_TRY(dx_h2d(g->ctx, P.d, segs.data(), segs.size() * sizeof(Seg), g->ctx->compute));
+        }
+        P.n = segs.size();
+        P.bytes = bytes;
+        P.epoch = F.epoch;
+    }
+    *out = &P;
     return DCCRGX_OK;
 }
 
@@ -150,25 +192,63 @@ static std::vector<int64_t> first_dst(const PeerPlan& p)
     return first;
 }
 
-// bytes field F contributes to the message to (send) or from (recv) peer p
-static size_t field_bytes(const Field& F, const PeerPlan& p, bool send)
+// pack plan: cells ascending, each its count[] elements, packed back to back
+static int send_plan(dccrgx_grid* g, PeerPlan& p, int32_t fid, const VarPlan** out)
 {
-    if (!F.variable) return (send ? p.send_ids.size() : p.recv_ids.size()) * F.elem;
-    size_t b = 0;
-    if (send) {
-        for (uint64_t s : p.h_send_slots) b += (size_t)F.count[s] * F.elem;
-    } else {
-        for (int64_t s : first_dst(p))
-            if (s >= 0) b += (size_t)F.count[s] * F.elem;
-    }
-    return b;
+    return var_plan(g, p.var_send, fid, [&](const Field& F, std::vector<Seg>& segs, uint64_t& bytes) {
+        uint64_t o = 0;
+        for (uint64_t s : p.h_send_slots) {
+            const uint64_t len = (uint64_t)F.count[s] * F.elem;
+            if (len) segs.push_back({F.off[s], o, len});
+            o += len;
+        }
+        bytes = o;
+    }, out);
 }
 
-static size_t message_bytes(const dccrgx_grid* g, const PeerPlan& p, const int32_t* f, size_t nf, bool send)
+// unpack plan: message cell j has the count of its ghost slots (pre-sized by
+// the caller); every ghost slot filled from it gets a copy
+static int recv_plan(dccrgx_grid* g, PeerPlan& p, int32_t fid, const VarPlan** out)
+{
+    return var_plan(g, p.var_recv, fid, [&](const Field& F, std::vector<Seg>& segs, uint64_t& bytes) {
+        const uint64_t n = p.recv_ids.size();
+        const std::vector<int64_t> first = first_dst(p);
+        std::vector<uint64_t> pre(n + 1, 0);
+        for (uint64_t j = 0; j < n; j++)
+            pre[j + 1] = pre[j] + (first[j] >= 0 ? (uint64_t)F.count[first[j]] * F.elem : 0);
+        for (size_t k = 0; k < p.h_unpack_dst.size(); k++) {
+            const uint64_t d = p.h_unpack_dst[k], j = p.h_unpack_src[k];
+            const uint64_t len = std::min<uint64_t>((uint64_t)F.count[d] * F.elem, pre[j + 1] - pre[j]);
+            if (len) segs.push_back({pre[j], F.off[d], len});
+        }
+        bytes = pre[n];
+    }, out);
+}
+
+// bytes field fid contributes to the message to (send) or from (recv) peer p
+static int field_bytes(dccrgx_grid* g, int32_t fid, PeerPlan& p, bool send, size_t* bytes)
+{
+    const Field& F = g->fields[fid];
+    if (!F.variable) {
+        *bytes = (send ? p.send_ids.size() : p.recv_ids.size()) * F.elem;
+        return DCCRGX_OK;
+    }
+    const VarPlan* P = nullptr;
+    DX_TRY(send ? send_plan(g, p, fid, &P) : recv_plan(g, p, fid, &P));
+    *bytes = P->bytes;
+    return DCCRGX_OK;
+}
+
+static int message_bytes(dccrgx_grid* g, PeerPlan& p, const int32_t* f, size_t nf, bool send, size_t* bytes)
 {
     size_t b = 0;
-    for (size_t i = 0; i < nf; i++) b += field_bytes(g->fields[f[i]], p, send);
-    return b;
+    for (size_t i = 0; i < nf; i++) {
+        size_t x = 0;
+        DX_TRY(field_bytes(g, f[i], p, send, &x));
+        b += x;
+    }
+    *bytes = b;
+    return DCCRGX_OK;
 }
 
 static int ensure(void** p, size_t* have, size_t need)
@@ -183,16 +263,19 @@ static int ensure(void** p, size_t* have, size_t need)
 }
 
 // periodic self copies into pad slots (stream st)
-static int self_copy(dccrgx_grid* g, const Hood& h, const int32_t* f, size_t nf, hipStream_t st)
+static int self_copy(dccrgx_grid* g, Hood& h, const int32_t* f, size_t nf, hipStream_t st)
 {
     for (size_t i = 0; i < nf; i++) {
         const Field& F = g->fields[f[i]];
         if (F.variable) {
-            std::vector<Seg> segs;
-            for (auto& e : h.h_self)
-                if (F.count[e.second])
-                    segs.push_back({F.off[e.second], F.off[e.first], (uint64_t)F.count[e.second] * F.elem});
-            DX_TRY(seg_copy(segs, F.ptr, F.ptr, st));
+            const VarPlan* P = nullptr;
+            DX_TRY(var_plan(g, h.var_self, f[i], [&](const Field& G, std::vector<Seg>& segs, uint64_t& bytes) {
+                for (auto& e : h.h_self)
+                    if (G.count[e.second])
+                        segs.push_back({G.off[e.second], G.off[e.first], (uint64_t)G.count[e.second] * G.elem});
+                bytes = 0;
+            }, &P));
+            DX_TRY(launch_segs(P->d, P->n, F.ptr, F.ptr, st));
             continue;
         }
         for (const CopySeg& s : h.self_segs)
@@ -213,15 +296,10 @@ static int pack_peer(dccrgx_grid* g, PeerPlan& p, const int32_t* f, size_t nf, v
         const Field& F = g->fields[f[i]];
         char* d = (char*)dst + off;
         if (F.variable) {  // cells ascending, each its count[] elements
-            std::vector<Seg> segs;
-            uint64_t o = 0;
-            for (uint64_t s : p.h_send_slots) {
-                const uint64_t len = (uint64_t)F.count[s] * F.elem;
-                if (len) segs.push_back({F.off[s], off + o, len});
-                o += len;
-            }
-            DX_TRY(seg_copy(segs, F.ptr, dst, st));
-            off += o;
+            const VarPlan* P = nullptr;
+            DX_TRY(send_plan(g, p, f[i], &P));
+            DX_TRY(launch_segs(P->d, P->n, F.ptr, d, st));
+            off += P->bytes;
             continue;
         }
         if (p.send_direct)
@@ -242,19 +320,11 @@ static int unpack_peer(dccrgx_grid* g, PeerPlan& p, const int32_t* f, size_t nf,
     for (size_t i = 0; i < nf; i++) {
         const Field& F = g->fields[f[i]];
         const char* s = (const char*)src + off;
-        if (F.variable) {  // message cell j has the count of its ghost slots (pre-sized by the caller)
-            const std::vector<int64_t> first = first_dst(p);
-            std::vector<uint64_t> pre(n + 1, 0);
-            for (uint64_t j = 0; j < n; j++)
-                pre[j + 1] = pre[j] + (first[j] >= 0 ? (uint64_t)F.count[first[j]] * F.elem : 0);
-            std::vector<Seg> segs;
-            for (size_t k = 0; k < p.h_unpack_dst.size(); k++) {
-                const uint64_t d = p.h_unpack_dst[k], j = p.h_unpack_src[k];
-                const uint64_t len = std::min<uint64_t>((uint64_t)F.count[d] * F.elem, pre[j + 1] - pre[j]);
-                if (len) segs.push_back({off + pre[j], F.off[d], len});
-            }
-            DX_TRY(seg_copy(segs, src, F.ptr, st));
-            off += pre[n];
+        if (F.variable) {
+            const VarPlan* P = nullptr;
+            DX_TRY(recv_plan(g, p, f[i], &P));
+            DX_TRY(launch_segs(P->d, P->n, s, F.ptr, st));
+            off += P->bytes;
             continue;
         }
         if (p.recv_direct)
@@ -358,7 +428,8 @@ static int host_exchange(dccrgx_grid* g, Hood& h, const int32_t* f, size_t nf)
     std::vector<uint64_t> sn, rn;
     for (PeerPlan& p : h.peers) {
         if (!p.send_ids.empty()) {
-            const size_t b = message_bytes(g, p, f, nf, true);
+            size_t b = 0;
+            DX_TRY(message_bytes(g, p, f, nf, true, &b));
             p.h_send_msg.resize(std::max<size_t>(b, 1));
             if (b) {
                 DX_TRY(ensure(&p.d_send_buf, &p.send_buf_bytes, b));
@@ -370,7 +441,8 @@ static int host_exchange(dccrgx_grid* g, Hood& h, const int32_t* f, size_t nf)
             sn.push_back(b);
         }
         if (!p.recv_ids.empty()) {
-            const size_t b = message_bytes(g, p, f, nf, false);
+            size_t b = 0;
+            DX_TRY(message_bytes(g, p, f, nf, false, &b));
             p.h_recv_msg.resize(std::max<size_t>(b, 1));
             rp.push_back(p.peer);
             rb.push_back(p.h_recv_msg.data());
@@ -537,11 +609,16 @@ int dccrgx_halo_start(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size
     for (size_t i = 0; i < nf; i++) var |= grid->fields[f[i]].variable;
     for (PeerPlan& p : h->peers) {
         if ((var || !p.send_direct) && !p.send_ids.empty()) {
-            DX_TRY(ensure(&p.d_send_buf, &p.send_buf_bytes, std::max<size_t>(message_bytes(grid, p, f, nf, true), 1)));
+            size_t b = 0;
+            DX_TRY(message_bytes(grid, p, f, nf, true, &b));
+            DX_TRY(ensure(&p.d_send_buf, &p.send_buf_bytes, std::max<size_t>(b, 1)));
             DX_TRY(pack_peer(grid, p, f, nf, p.d_send_buf, c->comm));
         }
-        if ((var || !p.recv_direct) && !p.recv_ids.empty())
-            DX_TRY(ensure(&p.d_recv_buf, &p.recv_buf_bytes, std::max<size_t>(message_bytes(grid, p, f, nf, false), 1)));
+        if ((var || !p.recv_direct) && !p.recv_ids.empty()) {
+            size_t b = 0;
+            DX_TRY(message_bytes(grid, p, f, nf, false, &b));
+            DX_TRY(ensure(&p.d_recv_buf, &p.recv_buf_bytes, std::max<size_t>(b, 1)));
+        }
     }
     // grouped point-to-point: one message per field per peer (xGMI links are
     // point-to-point; z-slab peers are the ring neighbours)
@@ -550,7 +627,9 @@ int dccrgx_halo_start(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size
         size_t soff = 0, roff = 0;
         for (size_t i = 0; i < nf; i++) {
             const Field& F = grid->fields[f[i]];
-            const size_t sb = field_bytes(F, p, true), rb = field_bytes(F, p, false);
+            size_t sb = 0, rb = 0;
+            DX_TRY(field_bytes(grid, f[i], p, true, &sb));
+            DX_TRY(field_bytes(grid, f[i], p, false, &rb));
             if (sb) {
                 const void* src = p.send_direct && !var ? (const char*)F.ptr + p.send_slot0 * F.elem
                                                         : (const char*)p.d_send_buf + soff;
@@ -686,7 +765,7 @@ int dccrgx_halo_pack_to(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, si
     *bytes = 0;
     for (PeerPlan& p : h->peers) {
         if (p.peer != peer) continue;
-        *bytes = message_bytes(grid, p, f, nf, true);
+        DX_TRY(message_bytes(grid, p, f, nf, true, bytes));
         DX_CHECK(cap >= *bytes, DCCRGX_ERANGE, "capacity %zu < %zu", cap, *bytes);
         DX_TRY(pack_peer(grid, p, f, nf, dst, grid->ctx->compute));
     }
@@ -703,7 +782,8 @@ int dccrgx_halo_unpack_from(dccrgx_grid* grid, int32_t hood_id, const int32_t* f
     DX_TRY(check_fields(grid, f, nf, &bpc));
     for (PeerPlan& p : h->peers) {
         if (p.peer != peer) continue;
-        const size_t want = message_bytes(grid, p, f, nf, false);
+        size_t want = 0;
+        DX_TRY(message_bytes(grid, p, f, nf, false, &want));
         DX_CHECK(bytes == want, DCCRGX_EINVAL, "message is %zu bytes, expected %zu", bytes, want);
         DX_TRY(unpack_peer(grid, p, f, nf, src, grid->ctx->compute));
         return DCCRGX_OK;
@@ -723,6 +803,7 @@ int dccrgx_field_create_variable(dccrgx_grid* grid, uint32_t elem, int32_t* fid)
     F.count.assign(grid->n_slots, 0);
     F.off.assign(grid->n_slots, 0);
     F.pool_bytes = 0;
+    F.epoch = next_var_epoch();
     DX_HIP(dx_malloc(&F.ptr, 16));
     grid->fields.push_back(std::move(F));
     *fid = (int32_t)grid->fields.size() - 1;
@@ -766,6 +847,7 @@ int dccrgx_field_resize(dccrgx_grid* grid, int32_t fid, const uint64_t* ids, con
     F.pool_bytes = tot;
     F.count.swap(cnt);
     F.off.swap(off);
+    F.epoch = next_var_epoch();
     return DCCRGX_OK;
 }
 

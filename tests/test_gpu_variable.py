@@ -151,3 +151,39 @@ def test_fixed_field_cell_access():
         assert np.array_equal(vals, np.array(remote, dtype=np.float64) / 3)
         local = [int(c) for c in g.local_cells()]
         assert np.array_equal(np.concatenate(g.read_cells("x", local)), g.read_local("x"))
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_variable_counts_change_between_exchanges(P):
+    """The pack / unpack / self-copy segments are cached per count epoch
+    (halo.hip VarPlan): after every resize (new counts, new values) the next
+    exchange must use the new layout.  Fields of 1-, 4- and 8-byte elements
+    share each message, so segments start at every alignment."""
+    length, per = (5, 4, 6), (True, False, True)
+    grids = grids_for(length, per, 1, P)
+    n = int(np.prod(length))
+    kinds = {"b": np.uint8, "i": np.int32, "d": np.float64}
+    for g in grids:
+        for name, dt in kinds.items():
+            g.add_variable_field(name, dt)
+    for rnd in range(3):
+        rng = np.random.default_rng(10 * P + rnd)
+        counts = {name: rng.integers(0, 7, n + 1) for name in kinds}
+        vals = {name: {c: (rng.integers(0, 100, counts[name][c]) + c).astype(dt) for c in range(1, n + 1)}
+                for name, dt in kinds.items()}
+        for g in grids:
+            local = [int(c) for c in g.local_cells()]
+            remote = [int(c) for c in g.remote_cells()]
+            for name in kinds:
+                g.resize(name, local, counts[name][local])
+                g.write_cells(name, local, [vals[name][c] for c in local])
+                if remote:
+                    g.resize(name, remote, counts[name][remote])
+        exchange(grids, list(kinds), True)
+        for g in grids:
+            recv = set(c for v in g.get_cells_to_receive().values() for c in v)
+            remote = [int(c) for c in g.remote_cells()]
+            for name in kinds:
+                for c, arr in zip(remote, g.read_cells(name, remote)):
+                    if c in recv or P == 1:
+                        assert np.array_equal(arr, vals[name][c]), (rnd, name, c)
