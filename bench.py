@@ -485,9 +485,50 @@ def halo_payload(ctx, D, world, barrier, reduce_max, shared_gpu=False):
                      "bytes_sent_per_step": ns * ds * world, "ms_per_update": dt * 1e3 / steps,
                      "GBs_per_rank": ns * ds * steps / dt / 1e9})
         g.close()
+    # variable-size cells (tests/variable_data_size): cell id holds
+    # splitmix64(id) % 17 doubles (mean 8, 64 B); receivers size their ghosts
+    # with the same rule, as the reference's receivers must know the sizes
+    g = (D.Dccrg().set_initial_length((n, n, depth * world)).set_neighborhood_length(1)
+         .set_maximum_refinement_level(0).set_periodic(False, False, True).initialize(c))
+    g.add_variable_field("var", np.float64)
+    rank, lz = c.rank, depth * world
+
+    def plane(z):
+        return (z % lz) * n * n + 1 + np.arange(n * n, dtype=np.uint64)
+
+    def counts(ids):
+        x = ids + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return ((x ^ (x >> np.uint64(31))) % np.uint64(17)).astype(np.uint32)
+
+    with np.errstate(over="ignore"):
+        send = np.concatenate([plane(rank * depth), plane((rank + 1) * depth - 1)])
+        ghost = np.concatenate([plane(rank * depth - 1), plane((rank + 1) * depth)])
+        g.resize("var", send, counts(send))
+        g.resize("var", ghost, counts(ghost))
+        sent = int(counts(send).astype(np.int64).sum()) * 8
+    for _ in range(2):  # the first update builds the cached segment plans
+        g.update_copies_of_remote_neighbors(fields=["var"])
+    c.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.start_remote_neighbor_copy_updates(fields=["var"])
+        g.wait_remote_neighbor_copy_update_receives()
+        g.wait_remote_neighbor_copy_update_sends()
+    c.synchronize()
+    barrier()
+    dt = reduce_max(time.perf_counter() - t0)
+    rows.append({"data_size": "variable: splitmix64(id) % 17 f64 per cell (mean 64 B)",
+                 "send_cells_per_rank": int(send.size), "receive_cells_per_rank": int(ghost.size),
+                 "bytes_sent_per_step": sent * world, "ms_per_update": dt * 1e3 / steps,
+                 "GBs_per_rank": sent * steps / dt / 1e9})
+    g.close()
     if own is not None:
         own.close()
-    return {"workload": "tests/scalability/scalability.cpp byte payloads, 2048x2048x8 z-slab per rank, hood 1, "
+    return {"workload": "tests/scalability/scalability.cpp byte payloads (and variable-size cells as in "
+                        "tests/variable_data_size), 2048x2048x8 z-slab per rank, hood 1, "
                         "periodic z, start / wait receives / wait sends, empty solve"
                         + (" (N = 1: own periodic images through RCCL)" if world == 1 else
                            ", host-staged transport (ranks share a GPU)" if shared_gpu else ", RCCL over xGMI"),
