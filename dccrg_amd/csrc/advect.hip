@@ -634,7 +634,7 @@ int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f
     unsigned long long* d = nullptr;
     DX_HIP(dx_malloc((void**)&d, 8));
     const unsigned long long init = 0xffffffffffffffffull;  // above every key
-    DX_TRY(dx_h2d(grid->ctx, d, &init, 8, st));
+    DX_TRY(dx_h2d_async(grid->ctx, d, &init, 8, st));
     hipLaunchKernelGGL(k_max_dt, dim3(std::min<unsigned>(grid_for(n), 1024)), dim3(256), 0, st, p, s0, n, slots, d);
     DX_HIP(hipGetLastError());
     unsigned long long k = 0;

@@ -685,6 +685,9 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
     uint64_t* d_leaves = nullptr;
     uint64_t n_leaves = 0;
     std::vector<uint64_t> leaves, retired, nr;
+    // the leaf list of two rebuilds ago lends its storage: a fresh 8 B-per-leaf
+    // vector page-faults on first touch every step
+    if (grid->spare_host) leaves.swap(grid->spare_host->leaves);
     bool changed = false;
     // the request flags before the decisions: restored if the rebuild fails,
     // so the requests stay pending

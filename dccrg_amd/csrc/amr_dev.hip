@@ -778,8 +778,8 @@ int amr_dev_sync(dccrgx_grid* grid)
         DX_TRY(S.get(&d_other, ids.size()));
         DX_TRY(S.get(&d_cnt, 1));
         DX_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
-        DX_TRY(dx_h2d(grid->ctx, d_ids, ids.data(), ids.size() * 8, st));
-        DX_TRY(dx_h2d(grid->ctx, d_bits, bits.data(), bits.size() * 4, st));
+        DX_TRY(dx_h2d_async(grid->ctx, d_ids, ids.data(), ids.size() * 8, st));
+        DX_TRY(dx_h2d_async(grid->ctx, d_bits, bits.data(), bits.size() * 4, st));
         hipLaunchKernelGGL(k_flags_scatter, dim3(blocks(ids.size())), dim3(256), 0, st, aview(grid, A.d_flags), d_ids,
                            d_bits, (uint64_t)ids.size(), d_other, d_cnt);
         DX_HIP(hipGetLastError());
@@ -849,7 +849,7 @@ int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_
     DX_TRY(S.get(&d_grp, a.n));
     DX_TRY(S.get(&d_key, n));
     DX_HIP(hipMemsetAsync(d_grp, 0xff, a.n * 4, st));
-    DX_TRY(dx_h2d(grid->ctx, d_ids, ids, n * 8, st));
+    DX_TRY(dx_h2d_async(grid->ctx, d_ids, ids, n * 8, st));
     const unsigned b = blocks(n);
     if (kind == DCCRGX_AMR_UNREFINE) A.dev_unrefines = true;
     const int erase = A.dev_unrefines ? 1 : 0;
@@ -983,9 +983,16 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
                           {retired.data(), o.retired, cnt[3] * 8ull}};
     DX_TRY(dx_d2h_many(ctx, lists, 4, st));
     nr.insert(nr.end(), A.nr_other.begin(), A.nr_other.end());
-    for (std::vector<uint64_t>* v : {&A.new_cells, &A.removed, &retired}) {
-        radix_sort_u64(*v);
-        v->erase(std::unique(v->begin(), v->end()), v->end());
+    {  // the three lists sorted side by side on the host threads
+        std::vector<uint64_t>* lv[3] = {&A.new_cells, &A.removed, &retired};
+        const size_t nt = std::min<size_t>(3, host_threads());
+        pool_run(nt, [&](size_t t) {
+            for (size_t k = t; k < 3; k += nt) {
+                std::vector<uint64_t>& v = *lv[k];
+                radix_sort_u64(v);
+                v.erase(std::unique(v.begin(), v.end()), v.end());
+            }
+        });
     }
     *changed = cnt[0] > 0;
     if (!*changed) return DCCRGX_OK;
@@ -1076,7 +1083,7 @@ int amr_dev_retired_table(dccrgx_grid* grid)
     ds_free(E->d_ret, st);
     E->d_ret = nullptr;
     DX_HIP(ds_malloc(&E->d_ret, 16 * n, st));
-    DX_TRY(dx_h2d(grid->ctx, E->d_ret, t.data(), 16 * n, st));
+    DX_TRY(dx_h2d_async(grid->ctx, E->d_ret, t.data(), 16 * n, st));
     E->n_ret = n;
     return DCCRGX_OK;
 }
@@ -1193,7 +1200,7 @@ static int run_rule(dccrgx_grid* grid, const std::vector<uint64_t>& cells, const
     DX_TRY(S.get(&d_cells, cells.size()));
     DX_TRY(S.get(&d_err, 1));
     DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
-    DX_TRY(dx_h2d(grid->ctx, d_cells, cells.data(), cells.size() * 8, st));
+    DX_TRY(dx_h2d_async(grid->ctx, d_cells, cells.data(), cells.size() * 8, st));
     const SlotView sv = slot_view(grid);
     for (const FieldSet& fs : sets) {
         if (avg)

@@ -73,6 +73,25 @@ int dx_h2d(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
     return DCCRGX_OK;
 }
 
+int dx_h2d_async(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
+{
+    if (!bytes) return DCCRGX_OK;
+    if (bytes > Ctx::UP_SLOT_BYTES || st != c->compute || pageable_copies()) return dx_h2d(c, dst, src, bytes, st);
+    if (!c->up) {
+        DX_HIP(hipHostMalloc((void**)&c->up, Ctx::UP_SLOTS * Ctx::UP_SLOT_BYTES, hipHostMallocDefault));
+        for (int k = 0; k < Ctx::UP_SLOTS; k++) DX_HIP(hipEventCreateWithFlags(&c->up_ev[k], hipEventDisableTiming));
+    }
+    const int k = c->up_next;
+    c->up_next = (k + 1) % Ctx::UP_SLOTS;
+    if (c->up_used[k]) DX_HIP(hipEventSynchronize(c->up_ev[k]));  // its previous copy has been read
+    char* slot = c->up + (size_t)k * Ctx::UP_SLOT_BYTES;
+    std::memcpy(slot, src, bytes);
+    DX_HIP(hipMemcpyAsync(dst, slot, bytes, hipMemcpyHostToDevice, st));
+    DX_HIP(hipEventRecord(c->up_ev[k], st));
+    c->up_used[k] = true;
+    return DCCRGX_OK;
+}
+
 int dx_d2h_many(Ctx* c, const D2H* v, size_t n, hipStream_t st)
 {
     size_t total = 0;
@@ -872,9 +891,12 @@ int dccrgx_ctx_destroy(dccrgx_ctx* c)
     if (c->has_comm) ncclCommDestroy(c->nccl);
     hipEventDestroy(c->ev_compute);
     hipEventDestroy(c->ev_comm);
+    for (hipEvent_t e : c->up_ev)  // recorded on the compute stream, which is idle now
+        if (e) hipEventDestroy(e);
     hipStreamDestroy(c->compute);
     hipStreamDestroy(c->comm);
     if (c->stage) hipHostFree(c->stage);
+    if (c->up) hipHostFree(c->up);
     delete c;
     return DCCRGX_OK;
 }

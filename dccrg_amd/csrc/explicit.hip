@@ -858,7 +858,7 @@ static int upload(Ctx* c, const std::vector<T>& v, T** d, hipStream_t st)
 {
     *d = nullptr;
     DX_HIP(ds_malloc(d, std::max<size_t>(v.size(), 1) * sizeof(T), st));
-    return dx_h2d(c, *d, v.data(), v.size() * sizeof(T), st);
+    return dx_h2d_async(c, *d, v.data(), v.size() * sizeof(T), st);
 }
 
 // neighbors_of for a device array of cells: row (n+1, device) + optional outputs
@@ -1066,7 +1066,7 @@ static int sync_slots(dccrgx_grid* grid, bool slot_map_changed)
     if (ns > E->d_level_n) {
         std::vector<uint8_t> tail(ns - E->d_level_n);
         for (uint64_t k = E->d_level_n; k < ns; k++) tail[k - E->d_level_n] = (uint8_t)map_level(grid->map, E->slot_ids[k]);
-        DX_TRY(dx_h2d(grid->ctx, E->d_level + E->d_level_n, tail.data(), tail.size(), st));
+        DX_TRY(dx_h2d_async(grid->ctx, E->d_level + E->d_level_n, tail.data(), tail.size(), st));
         E->d_level_n = ns;
     }
     DX_HIP(hipStreamSynchronize(st));
@@ -1293,7 +1293,7 @@ int explicit_fetch_rows(const dccrgx_grid* grid, const Hood& h, const std::vecto
         if (d_out) (void)ds_free(d_out, st);
         return code;
     };
-    int s = dx_h2d(ctx, d_g, want.data(), n * 4, st);
+    int s = dx_h2d_async(ctx, d_g, want.data(), n * 4, st);
     if (s != DCCRGX_OK) return done(s);
     hipLaunchKernelGGL(k_rows_len, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)d_g, n, h.d_nof_row,
                        h.d_nto_row, d_row, d_row + n + 1);

@@ -364,6 +364,14 @@ struct Ctx {
     // pinned bounce buffer of dx_h2d / dx_d2h
     void* stage = nullptr;
     size_t stage_bytes = 0;
+    // pinned upload slots of dx_h2d_async: slot k is reused once the event
+    // recorded after its copy has passed
+    static constexpr int UP_SLOTS = 16;
+    static constexpr size_t UP_SLOT_BYTES = 256u << 10;
+    char* up = nullptr;
+    hipEvent_t up_ev[UP_SLOTS] = {};
+    bool up_used[UP_SLOTS] = {};
+    int up_next = 0;
 };
 
 // Host <-> device copies of pageable host memory through the context's pinned
@@ -373,6 +381,12 @@ struct Ctx {
 // from pinned memory do not.
 int dx_h2d(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st);
 int dx_d2h(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st);
+// A small upload (at most Ctx::UP_SLOT_BYTES) on the context's compute stream
+// that returns at once: `src` is copied into a pinned slot, the device copy is
+// ordered on the stream like a kernel.  Work on other streams must be ordered
+// after it by the caller (the structural calls end in a synchronisation).
+// Larger copies and other streams take dx_h2d.
+int dx_h2d_async(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st);
 // several device -> host copies behind one synchronisation
 struct D2H {
     void* dst;
