@@ -326,9 +326,45 @@ def secondary(ctx, torch, D):
                       "achieved_GBs": 36 * nid / (ms * 1e-3) / 1e9,
                       "frac": 36 * nid / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_id": 36}
     del ids
+    out["advection_large"] = advection_large(ctx, D)
     out["mapping_reference_speed_test"] = mapping_speed_test(D, torch, dev)
     out["neighbor_lists"] = neighbor_lists(ctx, D, torch)
     return out
+
+
+def advection_large(ctx, D):
+    """configs[2]'s solver (tests/advection/2d.cpp, max_ref_lvl 2, hood 0,
+    fp64) on a 16x larger box, 1600 x 1600 pre-refined by the same rules at a
+    threshold scaled to the finer density differences (0.006): ~3.5 M leaves,
+    where the face-flux kernel is bandwidth- rather than launch-bound.  The
+    time is the solver steps only."""
+    from dccrg_amd import advection as A
+    rel, thr, sens, cfl, M = 0.006, 0.25, 0.5, 0.5, 2
+    g = (D.Dccrg().set_initial_length((1600, 1600, 1)).set_maximum_refinement_level(M)
+         .set_periodic(True, True, False).set_neighborhood_length(0).initialize(ctx))
+    g.add_advection_fields()
+    geom = A.geometry_2d(g)
+    A.initialize(g, geom)
+    for _ in range(M):
+        A.adapt_grid(g, geom, *A.check_for_adaptation(g, rel / M, thr, sens))
+        A.initialize(g, geom)
+    nl = g.n_local
+    dt_adv = g.max_time_step()
+    for _ in range(2):
+        g.advect_step(cfl * dt_adv)
+    ctx.synchronize()
+    steps = 50
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.advect_step(cfl * dt_adv)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    g.close()
+    return {"workload": f"tests/advection/2d.cpp solver on 1600x1600x1 pre-refined to {nl} leaf cells "
+                        "(max_ref_lvl 2, hood 0, fp64, threshold 0.006)",
+            "value": nl * steps / dt, "unit": "cell-steps/s", "steps": steps, "us_per_step": dt * 1e6 / steps,
+            "achieved_GBs": 72 * nl * steps / dt / 1e9, "frac": 72 * nl * steps / dt / 1e9 / HBM_PEAK_GBS,
+            "bytes_per_cell_step": 72}
 
 
 def mapping_speed_test(D, torch, dev):

@@ -12,7 +12,7 @@ import sys
 
 
 def short(name):
-    return name.split("(")[0].replace("dccrgx::", "").replace("(anonymous namespace)::", "")
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("dccrgx::", "")
 
 
 def main(d, out, keys):
