@@ -913,6 +913,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
         return set_error(DCCRGX_EINVAL, "leaf count %zu", n);
     }
     PhaseTimer T("explicit_init");
+    uint64_t ident = 0;  // leading identity entries of the reused one-rank maps
     if (grid->spare_host) {  // the previous state's host arrays: their capacity is reused
         Explicit* S = grid->spare_host;
         E->leaves.swap(S->leaves);
@@ -922,9 +923,13 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
         E->slot_ids.swap(S->slot_ids);
         E->slot_of_g.swap(S->slot_of_g);
         E->dir.swap(S->dir);
-        E->local.clear();
-        E->local_g.clear();
-        E->slot_ids.clear();
+        if (ctx->comm_size > 1) {  // rebuilt by push_back; one rank overwrites them in place
+            E->local.clear();
+            E->local_g.clear();
+            E->slot_ids.clear();
+        } else {
+            ident = S->ident_n;
+        }
         delete S;
         grid->spare_host = nullptr;
     }
@@ -982,17 +987,23 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
     E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
     E->owner.resize(E->n);
     if (ctx->comm_size == 1) {  // one process owns every leaf: identity maps, filled by the host threads
+        // (reused maps already hold the identity up to `ident`: only the tail is written)
+        ident = std::min<uint64_t>({ident, E->owner.size(), E->local_g.size(), E->slot_of_g.size()});
+        E->owner.resize(E->n);
         E->local.resize(E->n);
         E->local_g.resize(E->n);
         E->slot_ids.resize(E->n);
         E->slot_of_g.resize(E->n);
-        parallel_ranges(E->n, 1u << 16, [E](size_t b, size_t e) {
-            std::fill(E->owner.begin() + b, E->owner.begin() + e, 0);
+        parallel_ranges(E->n, 1u << 16, [E, ident](size_t b, size_t e) {
             std::copy(E->leaves.begin() + b, E->leaves.begin() + e, E->local.begin() + b);
             std::copy(E->leaves.begin() + b, E->leaves.begin() + e, E->slot_ids.begin() + b);
-            for (size_t i = b; i < e; i++) E->local_g[i] = E->slot_of_g[i] = (uint32_t)i;
+            for (size_t i = std::max<size_t>(b, ident); i < e; i++) {
+                E->owner[i] = 0;
+                E->local_g[i] = E->slot_of_g[i] = (uint32_t)i;
+            }
         });
         E->slot_identity = true;
+        E->ident_n = E->n;
     }
     for (uint64_t i = 0; ctx->comm_size > 1 && i < E->n; i++) {
         uint64_t idx[3];
@@ -1129,6 +1140,7 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids, bool
             E->slot_of_g[g] = s;
             leaf_slot = true;
             E->slot_identity = false;
+            E->ident_n = 0;
         }
     }
     const uint64_t ns = E->slot_ids.size();
@@ -1141,7 +1153,10 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids, bool
                 const uint64_t c = E->slot_ids[k];
                 E->extra.erase(c);
                 const int64_t g = E->find(c);
-                if (g >= 0) E->slot_of_g[g] = NO_SLOT;
+                if (g >= 0) {
+                    E->slot_of_g[g] = NO_SLOT;
+                    E->ident_n = 0;
+                }
             }
             E->slot_ids.resize(old_ns);
             return s;
@@ -1182,6 +1197,7 @@ void explicit_recycle(dccrgx_grid* grid, Explicit* E)
     S->slot_ids.swap(E->slot_ids);
     S->slot_of_g.swap(E->slot_of_g);
     S->dir.swap(E->dir);
+    S->ident_n = E->ident_n;
     explicit_free(E);
     delete grid->spare_host;
     grid->spare_host = S;

@@ -177,6 +177,8 @@ struct Explicit {
     FlatMap32 extra;                                // ghost / retired id -> slot
     std::vector<uint32_t> slot_of_g;                // global leaf index -> slot (NO_SLOT)
     bool slot_identity = false;                     // slot_of_g[g] == g (one rank, no ghost leaves)
+    uint64_t ident_n = 0;                           // one rank: owner[i] == 0, local_g[i] == slot_of_g[i] == i
+                                                    // hold for i < ident_n (kept by explicit_recycle)
     uint32_t* d_slot_of_g = nullptr;
     uint32_t* d_local_slot = nullptr;               // local position -> slot (identity)
     uint8_t* d_level = nullptr;                     // refinement level of each slot
