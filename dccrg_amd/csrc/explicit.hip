@@ -1076,7 +1076,10 @@ static int sync_slots(dccrgx_grid* grid, bool slot_map_changed)
     E->d_level_n = std::min(E->d_level_n, ns);
     if (ns > E->d_level_n) {
         std::vector<uint8_t> tail(ns - E->d_level_n);
-        for (uint64_t k = E->d_level_n; k < ns; k++) tail[k - E->d_level_n] = (uint8_t)map_level(grid->map, E->slot_ids[k]);
+        const uint64_t k0 = E->d_level_n;
+        parallel_ranges(ns - k0, 1u << 15, [&](size_t b, size_t e) {
+            for (size_t k = b; k < e; k++) tail[k] = (uint8_t)map_level(grid->map, E->slot_ids[k0 + k]);
+        });
         DX_TRY(dx_h2d_async(grid->ctx, E->d_level + E->d_level_n, tail.data(), tail.size(), st));
         E->d_level_n = ns;
     }
@@ -1130,6 +1133,8 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids, bool
     Explicit* E = grid->ex;
     const uint64_t old_ns = E->slot_ids.size();
     bool leaf_slot = false;  // a leaf got a (ghost) slot: the slot map changes
+    E->extra.reserve(E->extra.size() + ids.size());
+    E->slot_ids.reserve(old_ns + ids.size());
     for (uint64_t c : ids) {
         const int64_t g = not_leaves ? -1 : E->find(c);  // retired cells are no leaves: no host lookup
         if ((g >= 0 && E->slot_of_g[g] != NO_SLOT) || E->extra.count(c)) continue;  // has a slot
@@ -1620,12 +1625,7 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     const int me = ctx->rank;
     std::set<uint64_t> remote;
     std::map<int, std::set<uint64_t>> send, recv;
-    if (ctx->comm_size == 1) {  // one process: every cell is inner, nothing remote
-        L.inner_pos.resize(nl);
-        parallel_ranges(nl, 1u << 16, [&L](size_t b, size_t e) {
-            for (size_t i = b; i < e; i++) L.inner_pos[i] = (uint32_t)i;
-        });
-    }
+    L.inner_all = ctx->comm_size == 1;  // one process: every cell is inner, nothing remote
     for (uint64_t i = 0; ctx->comm_size > 1 && i < nl; i++) {
         const uint32_t r = E->local_g[i];
         bool outer = false;
@@ -1752,6 +1752,7 @@ int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, ui
     case DCCRGX_CELLS_REMOTE: v = &h.remote; break;
     case DCCRGX_CELLS_INNER: {
         const auto& L = E->hl.at(h.id);
+        if (L.inner_all) inner = E->local;
         for (uint32_t p : L.inner_pos) inner.push_back(E->local[p]);
         v = &inner;
         break;
@@ -2013,7 +2014,7 @@ int explicit_region(const dccrgx_grid* grid, const Hood& h, int32_t region, ExRe
     const auto& L = it->second;
     out->pos = region == DCCRGX_REGION_INNER ? L.d_inner_pos
                : region == DCCRGX_REGION_OUTER ? L.d_outer_pos : L.d_all_pos;
-    out->n = region == DCCRGX_REGION_INNER ? L.inner_pos.size()
+    out->n = region == DCCRGX_REGION_INNER ? (L.inner_all ? E->local.size() : L.inner_pos.size())
              : region == DCCRGX_REGION_OUTER ? L.outer_pos.size() : E->local.size();
     out->local_slot = E->d_local_slot;
     out->level = E->d_level;

@@ -172,6 +172,12 @@ class FlatSet {
 class FlatMap32 {
   public:
     size_t size() const { return keys_.size() ? n_ : 0; }
+    void reserve(size_t n)  // room for n keys without a rehash
+    {
+        size_t cap = 16;
+        while (cap < 2 * n + 2) cap <<= 1;
+        if (cap > keys_.size()) rehash(cap);
+    }
     size_t count(uint64_t k) const { return find(k) ? 1 : 0; }
     const uint32_t* find(uint64_t k) const
     {

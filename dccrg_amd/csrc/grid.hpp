@@ -194,6 +194,7 @@ struct Explicit {
         std::unordered_map<uint32_t, std::array<uint64_t, 4>> row_at;
         std::vector<uint32_t> row_vals;
         std::vector<uint32_t> inner_pos, outer_pos;  // positions in `local`
+        bool inner_all = false;                      // one rank: every local cell inner (inner_pos not stored)
         uint32_t* d_inner_pos = nullptr;
         uint32_t* d_outer_pos = nullptr;
         uint32_t* d_all_pos = nullptr;
