@@ -501,11 +501,16 @@ __device__ inline bool walk_insert(const Walk& w, uint64_t x, int* over)
     return false;
 }
 
-// one wave (workgroup of 64) per walk; `lds_bytes` > 0: the workspace is in
-// LDS, else `scratch` holds one workspace per workgroup
+// one wave (workgroup of 64) per walk; `use_lds`: the workspace is in LDS,
+// else `scratch` holds one workspace per workgroup.  The walks are the
+// entries of `us` (or the entries idx[0 .. *n_idx) of it).  With `retry`
+// non-null a walk whose workspace overflows is appended there (its `us`
+// index) for a pass with a larger workspace, instead of failing.
 __global__ void __launch_bounds__(64) k_ou_walk(AView a, const uint32_t* __restrict__ us, const uint32_t* __restrict__ nu,
+                                                const uint32_t* __restrict__ idx, const uint32_t* __restrict__ n_idx,
                                                 const uint32_t* __restrict__ grp, const uint32_t* __restrict__ key,
                                                 uint32_t Q, uint32_t S, int use_lds, uint64_t* __restrict__ scratch,
+                                                uint32_t* __restrict__ retry, uint32_t* __restrict__ n_retry,
                                                 int32_t* __restrict__ err)
 {
     extern __shared__ uint64_t lds[];
@@ -517,10 +522,11 @@ __global__ void __launch_bounds__(64) k_ou_walk(AView a, const uint32_t* __restr
     w.S = S;
     w.queue = use_lds ? lds : scratch + (size_t)blockIdx.x * (Q + S);
     w.seen = w.queue + Q;
-    const uint32_t n = *nu;
+    const uint32_t n = idx ? *n_idx : *nu;
     AExists exists{a.v};
     int32_t per[3] = {a.v.per[0], a.v.per[1], a.v.per[2]};
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    for (uint32_t j0 = blockIdx.x; j0 < n; j0 += gridDim.x) {
+        const uint32_t i = idx ? idx[j0] : j0;
         const uint32_t g = us[i];
         const uint32_t k = key[i];
         if (k != NONE32 && grp[k] != g) continue;  // not the group's walker (uniform across the wave)
@@ -532,13 +538,14 @@ __global__ void __launch_bounds__(64) k_ou_walk(AView a, const uint32_t* __restr
             head = 0;
             tail = 0;
             over = 0;
+            fail = 0;
+        }
+        __syncthreads();
+        if (lane < 8) {  // a sibling to be refined or kept (:9960-9975), one lookup per lane
             uint64_t sib[8];
             a_children(a, parent, sib);
-            fail = 0;
-            for (int j = 0; j < 8; j++) {  // a sibling to be refined or kept (:9960-9975)
-                const int64_t gs = sib[j] ? ex_find(a.v, sib[j]) : -1;
-                if (gs >= 0 && (a.flags[gs] & (RF_REFINE | RF_NOT_UNREFINE))) fail = 1;
-            }
+            const int64_t gs = sib[lane] ? ex_find(a.v, sib[lane]) : -1;
+            if (gs >= 0 && (a.flags[gs] & (RF_REFINE | RF_NOT_UNREFINE))) atomicOr(&fail, 1u);
         }
         __syncthreads();
         if (lane == 0 && !fail) {
@@ -578,7 +585,8 @@ __global__ void __launch_bounds__(64) k_ou_walk(AView a, const uint32_t* __restr
             __syncthreads();
         }
         if (lane == 0) {
-            if (over) atomicOr(err, 1);
+            if (over && retry) retry[atomicAdd(n_retry, 1u)] = i;
+            else if (over) atomicOr(err, 1);
             else if (!fail) atomicOr(&a.flags[k != NONE32 ? k : g], RF_KEEP);
         }
         __syncthreads();
@@ -935,6 +943,9 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     hipLaunchKernelGGL(k_collect, dim3(bN), dim3(256), 0, st, a, RF_UNREFINE, d_fa, cu);
     hipLaunchKernelGGL(k_ou_group, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_fa, (const uint32_t*)cu, d_grp,
                        d_key);
+    // the walks: first with a small LDS workspace (a walk visits tens of
+    // cells; many waves per CU), the few that overflow it again with one
+    // sized for the largest possible closure
     const uint32_t hl = grid->params.neighborhood_length;
     const uint64_t P = 8ull * (2 * hl + 3) * (2 * hl + 3) * (2 * hl + 3);
     const uint32_t Q = (uint32_t)(6 * P + 8);
@@ -947,9 +958,30 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     if (!lds) DX_TRY(S.get(&d_scr, (size_t)waves * (Q + Sz)));
     int32_t* d_err;
     DX_TRY(S.get(&d_err, 1));
+    uint32_t *d_retry, *d_nretry;
+    DX_TRY(S.get(&d_retry, N));
+    DX_TRY(S.get(&d_nretry, 1));
     DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
-    hipLaunchKernelGGL(k_ou_walk, dim3(waves), dim3(64), lds ? ws : 0, st, a, (const uint32_t*)d_fa, (const uint32_t*)cu,
-                       (const uint32_t*)d_grp, (const uint32_t*)d_key, Q, Sz, lds ? 1 : 0, d_scr, d_err);
+    DX_HIP(hipMemsetAsync(d_nretry, 0, 4, st));
+    // DCCRGX_OU_SMALL (tests): the first pass's queue length, to send walks to the second pass
+    const uint32_t Q1 = (uint32_t)std::max<int64_t>(2, getenv_int("DCCRGX_OU_SMALL", 256));
+    uint32_t S1 = 16;
+    while (S1 < 2 * Q1) S1 <<= 1;  // 256 -> 512: 6 KiB per wave
+    if (Q1 < Q && (size_t)(Q1 + S1) * 8 <= 48 * 1024) {
+        hipLaunchKernelGGL(k_ou_walk, dim3(8192), dim3(64), (Q1 + S1) * 8, st, a, (const uint32_t*)d_fa,
+                           (const uint32_t*)cu, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                           (const uint32_t*)d_grp, (const uint32_t*)d_key, Q1, S1, 1, (uint64_t*)nullptr, d_retry,
+                           d_nretry, d_err);
+        hipLaunchKernelGGL(k_ou_walk, dim3(waves), dim3(64), lds ? ws : 0, st, a, (const uint32_t*)d_fa,
+                           (const uint32_t*)cu, (const uint32_t*)d_retry, (const uint32_t*)d_nretry,
+                           (const uint32_t*)d_grp, (const uint32_t*)d_key, Q, Sz, lds ? 1 : 0, d_scr,
+                           (uint32_t*)nullptr, (uint32_t*)nullptr, d_err);
+    } else {
+        hipLaunchKernelGGL(k_ou_walk, dim3(waves), dim3(64), lds ? ws : 0, st, a, (const uint32_t*)d_fa,
+                           (const uint32_t*)cu, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                           (const uint32_t*)d_grp, (const uint32_t*)d_key, Q, Sz, lds ? 1 : 0, d_scr,
+                           (uint32_t*)nullptr, (uint32_t*)nullptr, d_err);
+    }
     hipLaunchKernelGGL(k_ou_final, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_fa, (const uint32_t*)cu,
                        (const uint32_t*)d_key);
     // execute_refines

@@ -102,12 +102,18 @@ SEQ_CASES = [  # length, M, periodic, hood, P, rounds, seed
 ]
 
 
-@pytest.fixture(params=["full", "incremental"])
+@pytest.fixture(params=["full", "incremental", "small_walks"])
 def rebuild_mode(request, monkeypatch):
     """The rebuild's neighbors_of: recomputed for every leaf, or copied for
     rows that reference no removed leaf (explicit.hip nof_incremental; the
-    library picks it above 2^20 leaves, DCCRGX_INCREMENTAL forces it)."""
+    library picks it above 2^20 leaves, DCCRGX_INCREMENTAL forces it).
+    small_walks: override_unrefines' first pass gets a 4-entry queue, so the
+    walks overflow into the second, full-size pass (amr_dev.hip k_ou_walk)."""
     monkeypatch.setenv("DCCRGX_INCREMENTAL", "1" if request.param == "incremental" else "0")
+    if request.param == "small_walks":
+        monkeypatch.setenv("DCCRGX_OU_SMALL", "4")
+    else:
+        monkeypatch.delenv("DCCRGX_OU_SMALL", raising=False)
     return request.param
 
 
