@@ -1466,8 +1466,24 @@ static bool incremental_rebuild(uint64_t n)
     return n >= (1ull << 20);  // below, one full pass costs less than the extra launches
 }
 
-// neighbors_of of every leaf from the previous lists (see above)
-static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_t* total, hipStream_t st)
+// the maps of an incremental neighbors_of, kept for the stencil rows
+struct IncMaps {
+    uint32_t* n2o = nullptr;     // new leaf -> old leaf (NO_SLOT: new)
+    uint32_t* o2n = nullptr;     // old leaf -> new leaf (NO_SLOT: gone)
+    uint8_t* touched = nullptr;  // old leaf: its row was recomputed
+    uint32_t* aff = nullptr;     // new leaves whose rows were recomputed
+    uint64_t naff = 0;
+    hipStream_t st = nullptr;
+    ~IncMaps()
+    {
+        for (void* q : {(void*)n2o, (void*)o2n, (void*)touched, (void*)aff}) ds_free(q, st);
+    }
+};
+
+// neighbors_of of every leaf from the previous lists (see above); `keep`
+// takes over the maps
+static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_t* total, hipStream_t st,
+                           IncMaps* keep)
 {
     Explicit* E = grid->ex;
     Ctx* ctx = grid->ctx;
@@ -1544,7 +1560,97 @@ static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_
                            d_err);
     }
     if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "incremental neighbor lists"));
+    if (keep) {
+        keep->st = st;
+        keep->n2o = d_n2o;
+        keep->o2n = d_o2n;
+        keep->touched = d_touched;
+        keep->aff = d_aff;
+        keep->naff = naff;
+        d_n2o = d_o2n = d_aff = nullptr;
+        d_touched = nullptr;
+    }
     return done(DCCRGX_OK);
+}
+
+// incremental stencil rows (one rank, slot == leaf index before and after):
+// the row of a leaf whose neighbors_of was copied is its old row with the
+// slots remapped (the pairs sort by leaf index, which the remap keeps in
+// order); the others were sorted anew into a compact CSR (arow / apairs)
+__global__ void __launch_bounds__(256) k_st_inc_counts(const uint32_t* __restrict__ n2o,
+                                                       const uint8_t* __restrict__ touched,
+                                                       const uint64_t* __restrict__ ost_row,
+                                                       const uint32_t* __restrict__ aidx,
+                                                       const uint32_t* __restrict__ apc, uint64_t n,
+                                                       uint32_t* __restrict__ cnt)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+        const uint32_t k = aidx[j];
+        if (k != NO_SLOT) {
+            cnt[j] = apc[k];
+        } else {
+            const uint32_t o = n2o[j];
+            cnt[j] = (uint32_t)(ost_row[o + 1] - ost_row[o]);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_st_aff_rows(const uint32_t* __restrict__ aff, uint64_t naff,
+                                                     const uint64_t* __restrict__ nof_row, uint64_t* __restrict__ arow,
+                                                     uint32_t* __restrict__ aidx)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < naff; k += stride) {
+        const uint32_t j = aff[k];
+        arow[k + 1] = nof_row[j + 1] - nof_row[j];
+        aidx[j] = (uint32_t)k;
+    }
+}
+
+// one wave per 64 rows, consecutive lanes on consecutive entries (k_inc_copy)
+__global__ void __launch_bounds__(64) k_st_inc_fill(const uint32_t* __restrict__ n2o, const uint32_t* __restrict__ o2n,
+                                                    const uint32_t* __restrict__ aidx, uint64_t n,
+                                                    const uint64_t* __restrict__ ost_row,
+                                                    const uint32_t* __restrict__ ost_slot,
+                                                    const int32_t* __restrict__ ost_off,
+                                                    const uint64_t* __restrict__ arow, const Pair* __restrict__ apairs,
+                                                    const uint64_t* __restrict__ st_row, uint32_t* __restrict__ st_slot,
+                                                    int32_t* __restrict__ st_off)
+{
+    __shared__ uint64_t s_dst[65], s_src[64];
+    __shared__ uint32_t s_aff[64];
+    const int lane = threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t last = r0 + 64 < n ? r0 + 64 : n;
+    s_dst[lane] = st_row[r0 + lane < last ? r0 + lane : last];
+    if (lane == 0) s_dst[64] = st_row[last];
+    uint32_t k = NO_SLOT;
+    uint64_t src = 0;
+    if (r0 + lane < n) {
+        k = aidx[r0 + lane];
+        src = k != NO_SLOT ? arow[k] : ost_row[n2o[r0 + lane]];
+    }
+    s_aff[lane] = k;
+    s_src[lane] = src;
+    __syncthreads();
+    const uint64_t end = s_dst[64];
+    for (uint64_t o = s_dst[0] + lane; o < end; o += 64) {
+        const int j = wave_row_of(s_dst, o);
+        const uint64_t e = s_src[j] + (o - s_dst[j]);
+        if (s_aff[j] != NO_SLOT) {
+            const Pair p = apairs[e];
+            st_slot[o] = p.g;  // slot == leaf index
+            st_off[3 * o + 0] = p.x;
+            st_off[3 * o + 1] = p.y;
+            st_off[3 * o + 2] = p.z;
+        } else {
+            st_slot[o] = o2n[ost_slot[e]];
+            st_off[3 * o + 0] = ost_off[3 * e + 0];
+            st_off[3 * o + 1] = ost_off[3 * e + 1];
+            st_off[3 * o + 2] = ost_off[3 * e + 2];
+        }
+    }
 }
 
 int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint)
@@ -1567,9 +1673,14 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     // neighbors_of of every leaf (the reference also builds all of them)
     DX_HIP(ds_malloc(&h.d_nof_row, (N + 1) * 8, st));
     uint64_t tot = 0;
-    if (hint && hint->old_h && hint->old_h->d_nof_row && hint->old_h->items == h.items && hint->old_ex &&
-        incremental_rebuild(hint->old_ex->n))
-        DX_TRY(nof_incremental(grid, h, *hint, &tot, st));
+    IncMaps inc;
+    const bool inc_nof = hint && hint->old_h && hint->old_h->d_nof_row && hint->old_h->items == h.items &&
+                         hint->old_ex && incremental_rebuild(hint->old_ex->n);
+    // the stencil rows follow incrementally where slots are leaf indices before and after
+    const bool inc_st = inc_nof && ctx->comm_size == 1 && E->slot_identity && hint->old_ex->slot_identity &&
+                        hint->old_h->d_st_row && hint->old_ex->local.size() == hint->old_ex->n;
+    if (inc_nof)
+        DX_TRY(nof_incremental(grid, h, *hint, &tot, st, inc_st ? &inc : nullptr));
     else
         DX_TRY(nof_device(grid, h, E->d_leaves, N, h.d_nof_row, &h.d_nof_id, &h.d_nof_off, &h.d_nof_g, &tot, st));
     T.lap("neighbors_of");
@@ -1655,48 +1766,103 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     T.lap("ghost slots");
 
     // stencil rows of local cells (iteration-cache neighbors_of: unique pairs)
-    uint64_t* d_tmp_row = nullptr;
-    Pair* d_pairs = nullptr;
-    uint32_t* d_pc = nullptr;
-    uint64_t tmp_tot = 0;
-    if (ctx->comm_size == 1) {  // every leaf is local, in leaf order: the rows are neighbors_of's
-        DX_HIP(ds_malloc(&d_tmp_row, (nl + 1) * 8, st));
-        DX_HIP(hipMemcpyAsync(d_tmp_row, h.d_nof_row, (nl + 1) * 8, hipMemcpyDeviceToDevice, st));
-        tmp_tot = tot;
-    } else {
-        std::vector<uint64_t> tmp_row(nl + 1, 0);
-        for (uint64_t i = 0; i < nl; i++) {
-            const uint32_t r = E->local_g[i];
-            tmp_row[i + 1] = tmp_row[i] + (nof_row[r + 1] - nof_row[r]);
+    if (inc.n2o) {  // one rank after an incremental neighbors_of: old rows remapped, the rest sorted
+        const Hood& oh = *hint->old_h;
+        const uint64_t na = inc.naff;
+        uint64_t* d_arow = nullptr;
+        uint32_t *d_aidx = nullptr, *d_apc = nullptr, *d_cnt2 = nullptr;
+        Pair* d_apairs = nullptr;
+        auto st_done = [&](int code) {
+            for (void* q : {(void*)d_arow, (void*)d_aidx, (void*)d_apc, (void*)d_cnt2, (void*)d_apairs}) ds_free(q, st);
+            return code;
+        };
+        if (ds_malloc(&d_arow, (na + 1) * 8, st) != hipSuccess || ds_malloc(&d_aidx, N * 4, st) != hipSuccess ||
+            ds_malloc(&d_apc, std::max<uint64_t>(na, 1) * 4, st) != hipSuccess ||
+            ds_malloc(&d_cnt2, std::max<uint64_t>(N, 1) * 4, st) != hipSuccess)
+            return st_done(set_error(DCCRGX_ENOMEM, "incremental stencil rows"));
+        hipMemsetAsync(d_aidx, 0xff, N * 4, st);
+        hipMemsetAsync(d_arow, 0, 8, st);
+        if (na)
+            hipLaunchKernelGGL(k_st_aff_rows, dim3(grid_for(na)), dim3(256), 0, st, (const uint32_t*)inc.aff, na,
+                               (const uint64_t*)h.d_nof_row, d_arow, d_aidx);
+        uint64_t atot = 0;
+        int e = device_scan_rows(d_arow, na, st, &atot);
+        if (e != DCCRGX_OK) return st_done(e);
+        if (ds_malloc(&d_apairs, std::max<uint64_t>(atot, 1) * sizeof(Pair), st) != hipSuccess)
+            return st_done(set_error(DCCRGX_ENOMEM, "incremental stencil rows"));
+        if (na) {
+            hipLaunchKernelGGL((k_stencil_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((na + 15) / 16, 16384)),
+                               dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, (const uint32_t*)inc.aff, na,
+                               (const uint64_t*)d_arow, d_apairs, d_apc);
+            hipLaunchKernelGGL((k_stencil_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((na + 3) / 4, 4096)),
+                               dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, (const uint32_t*)inc.aff, na,
+                               (const uint64_t*)d_arow, d_apairs, d_apc);
+            hipLaunchKernelGGL(k_stencil_rows_wave, dim3((unsigned)std::min<uint64_t>(na, 4096)), dim3(64), 0, st,
+                               h.d_nof_row, h.d_nof_g, h.d_nof_off, (const uint32_t*)inc.aff, na,
+                               (const uint64_t*)d_arow, d_apairs, d_apc);
+            hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(na)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
+                               h.d_nof_off, (const uint32_t*)inc.aff, na, (const uint64_t*)d_arow, d_apairs, d_apc);
         }
-        DX_TRY(upload(grid->ctx, tmp_row, &d_tmp_row, st));
-        tmp_tot = tmp_row[nl];
+        hipLaunchKernelGGL(k_st_inc_counts, dim3(grid_for(N)), dim3(256), 0, st, (const uint32_t*)inc.n2o,
+                           (const uint8_t*)inc.touched, (const uint64_t*)oh.d_st_row, (const uint32_t*)d_aidx,
+                           (const uint32_t*)d_apc, N, d_cnt2);
+        if ((e = scan_counts_device(d_cnt2, N, &h.d_st_row, nullptr, st)) != DCCRGX_OK) return st_done(e);
+        const uint64_t stot = tot;  // unique pairs: at most the rows' entries
+        if (ds_malloc(&h.d_st_slot, std::max<uint64_t>(stot, 1) * 4, st) != hipSuccess ||
+            ds_malloc(&h.d_st_off, std::max<uint64_t>(stot, 1) * 12, st) != hipSuccess)
+            return st_done(set_error(DCCRGX_ENOMEM, "stencil rows"));
+        if (N)
+            hipLaunchKernelGGL(k_st_inc_fill, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st,
+                               (const uint32_t*)inc.n2o, (const uint32_t*)inc.o2n, (const uint32_t*)d_aidx, N,
+                               (const uint64_t*)oh.d_st_row, (const uint32_t*)oh.d_st_slot, (const int32_t*)oh.d_st_off,
+                               (const uint64_t*)d_arow, (const Pair*)d_apairs, (const uint64_t*)h.d_st_row, h.d_st_slot,
+                               h.d_st_off);
+        if (hipGetLastError() != hipSuccess) return st_done(set_error(DCCRGX_EHIP, "incremental stencil rows"));
+        st_done(DCCRGX_OK);
+    } else {
+        uint64_t* d_tmp_row = nullptr;
+        Pair* d_pairs = nullptr;
+        uint32_t* d_pc = nullptr;
+        uint64_t tmp_tot = 0;
+        if (ctx->comm_size == 1) {  // every leaf is local, in leaf order: the rows are neighbors_of's
+            DX_HIP(ds_malloc(&d_tmp_row, (nl + 1) * 8, st));
+            DX_HIP(hipMemcpyAsync(d_tmp_row, h.d_nof_row, (nl + 1) * 8, hipMemcpyDeviceToDevice, st));
+            tmp_tot = tot;
+        } else {
+            std::vector<uint64_t> tmp_row(nl + 1, 0);
+            for (uint64_t i = 0; i < nl; i++) {
+                const uint32_t r = E->local_g[i];
+                tmp_row[i + 1] = tmp_row[i] + (nof_row[r + 1] - nof_row[r]);
+            }
+            DX_TRY(upload(grid->ctx, tmp_row, &d_tmp_row, st));
+            tmp_tot = tmp_row[nl];
+        }
+        DX_HIP(ds_malloc(&d_pairs, std::max<uint64_t>(tmp_tot, 1) * sizeof(Pair), st));
+        DX_HIP(ds_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4, st));
+        if (nl) {
+            hipLaunchKernelGGL((k_stencil_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((nl + 15) / 16, 16384)),
+                               dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs,
+                               d_pc);
+            hipLaunchKernelGGL((k_stencil_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((nl + 3) / 4, 4096)),
+                               dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs,
+                               d_pc);
+            hipLaunchKernelGGL(k_stencil_rows_wave, dim3((unsigned)std::min<uint64_t>(nl, 4096)), dim3(64), 0, st,
+                               h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
+            hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
+                               h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
+        }
+        const uint64_t stot = tmp_tot;  // unique pairs: at most the rows' entries (no read-back)
+        DX_TRY(scan_counts_device(d_pc, nl, &h.d_st_row, nullptr, st));
+        DX_HIP(ds_malloc(&h.d_st_slot, std::max<uint64_t>(stot, 1) * 4, st));
+        DX_HIP(ds_malloc(&h.d_st_off, std::max<uint64_t>(stot, 1) * 12, st));
+        if (nl)
+            hipLaunchKernelGGL(k_stencil_slots_wave, dim3((unsigned)((nl + 63) / 64)), dim3(64), 0, st, d_tmp_row,
+                               d_pairs, h.d_st_row, nl, E->d_slot_of_g, h.d_st_slot, h.d_st_off);
+        DX_HIP(hipGetLastError());
+        ds_free(d_tmp_row, st);
+        ds_free(d_pairs, st);
+        ds_free(d_pc, st);
     }
-    DX_HIP(ds_malloc(&d_pairs, std::max<uint64_t>(tmp_tot, 1) * sizeof(Pair), st));
-    DX_HIP(ds_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4, st));
-    if (nl) {
-        hipLaunchKernelGGL((k_stencil_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((nl + 15) / 16, 16384)),
-                           dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs,
-                           d_pc);
-        hipLaunchKernelGGL((k_stencil_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((nl + 3) / 4, 4096)),
-                           dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs,
-                           d_pc);
-        hipLaunchKernelGGL(k_stencil_rows_wave, dim3((unsigned)std::min<uint64_t>(nl, 4096)), dim3(64), 0, st,
-                           h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
-        hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
-                           h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
-    }
-    const uint64_t stot = tmp_tot;  // unique pairs: at most the rows' entries (no read-back)
-    DX_TRY(scan_counts_device(d_pc, nl, &h.d_st_row, nullptr, st));
-    DX_HIP(ds_malloc(&h.d_st_slot, std::max<uint64_t>(stot, 1) * 4, st));
-    DX_HIP(ds_malloc(&h.d_st_off, std::max<uint64_t>(stot, 1) * 12, st));
-    if (nl)
-        hipLaunchKernelGGL(k_stencil_slots_wave, dim3((unsigned)((nl + 63) / 64)), dim3(64), 0, st, d_tmp_row,
-                           d_pairs, h.d_st_row, nl, E->d_slot_of_g, h.d_st_slot, h.d_st_off);
-    DX_HIP(hipGetLastError());
-    ds_free(d_tmp_row, st);
-    ds_free(d_pairs, st);
-    ds_free(d_pc, st);
 
     T.lap("stencil rows");
     struct Lap {

@@ -85,3 +85,20 @@ def test_device_matches_reference_solver(tmp_path, n, M, steps, adapt_n):
         scale = max(np.abs(rho0).max(), 1e-300)
         assert np.abs(rho0 - rho1).max() <= 1e-12 * scale, f"density after step {s0}"
         assert abs(dt0 - dt1) <= 1e-12 * abs(dt0), f"dt after step {s0}"
+
+
+@pytest.mark.skipif(not os.path.exists(BIN), reason="oracle/_ref/ref_advection is built where /root/reference is")
+@pytest.mark.parametrize("n,M,steps,adapt_n", [(20, 2, 12, 1), (64, 2, 24, 1), (400, 2, 8, 1)])
+def test_incremental_rebuild_matches_reference_solver(tmp_path, monkeypatch, n, M, steps, adapt_n):
+    """The same runs with the incremental rebuild forced (the library picks it
+    above 2^20 leaves): neighbors_of rows and, on one rank, the stencil rows
+    the face lists come from are copied for untouched leaves and remapped
+    (explicit.hip nof_incremental, k_st_inc_fill)."""
+    monkeypatch.setenv("DCCRGX_INCREMENTAL", "1")
+    ref = reference_run(n, M, steps, adapt_n, str(tmp_path / "ref.bin"))
+    dev = device_run(n, M, steps, adapt_n)
+    assert len(ref) == len(dev) == steps + 1
+    for (s0, dt0, ids0, rho0), (s1, dt1, ids1, rho1) in zip(ref, dev):
+        assert np.array_equal(ids0, ids1), f"leaf sets differ after step {s0}"
+        scale = max(np.abs(rho0).max(), 1e-300)
+        assert np.abs(rho0 - rho1).max() <= 1e-12 * scale, f"density after step {s0}"
