@@ -1027,6 +1027,7 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
         });
     }
     *changed = cnt[0] > 0;
+    T.lap("lists");
     if (!*changed) return DCCRGX_OK;
     // the new leaf list: surviving leaves in order, merged with the sorted new ones
     uint8_t* d_keep;
@@ -1050,6 +1051,7 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, tb3, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
     uint64_t nk[2] = {0, 0};
     DX_TRY(dx_d2h(ctx, nk, d_cnt64, 16, st));
+    T.lap("kept + sorted new");
     const uint64_t n_new = nk[0] + nk[1];
     uint64_t* d_new = nullptr;
     DX_HIP(ds_malloc(&d_new, std::max<uint64_t>(n_new, 1) * 8, st));

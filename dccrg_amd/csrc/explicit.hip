@@ -1975,7 +1975,18 @@ int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_
     const uint64_t n = E->slot_ids.size();
     if (!n) return DCCRGX_OK;
     uint64_t* d_ids = nullptr;
-    DX_TRY(upload(grid->ctx, E->slot_ids, &d_ids, st));
+    // one rank: the slot ids are the device leaf list, then the retired cells
+    // in the order of the device retired table -- no upload of the host copy
+    const uint64_t nr = n > E->n ? n - E->n : 0;
+    if (E->slot_identity && E->d_leaves && nr == E->n_ret && (!nr || E->d_ret) && E->retired.size() == nr &&
+        std::equal(E->slot_ids.begin() + E->n, E->slot_ids.end(), E->retired.begin())) {
+        DX_HIP(ds_malloc(&d_ids, n * 8, st));
+        DX_HIP(hipMemcpyAsync(d_ids, E->d_leaves, E->n * 8, hipMemcpyDeviceToDevice, st));
+        if (nr) DX_HIP(hipMemcpyAsync(d_ids + E->n, E->d_ret, nr * 8, hipMemcpyDeviceToDevice, st));
+    } else {
+        DX_HIP(ds_malloc(&d_ids, n * 8, st));
+        DX_TRY(dx_h2d(grid->ctx, d_ids, E->slot_ids.data(), n * 8, st));
+    }
     ExView v{};
     v.mp = grid->map;
     v.keys = old->d_keys;
@@ -1985,8 +1996,7 @@ int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_
     v.rank = old->d_rank;
     hipLaunchKernelGGL(k_old_slots, dim3(grid_for(n)), dim3(256), 0, st, v, old->d_slot_of_g, d_ids, n, d_src);
     const hipError_t e = hipGetLastError();
-    DX_HIP(hipStreamSynchronize(st));
-    dx_free(d_ids);
+    ds_free(d_ids, st);  // after the kernel, in stream order
     DX_HIP(e);
     return DCCRGX_OK;
 }
