@@ -326,7 +326,7 @@ int rebuild(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<
     if (s == DCCRGX_OK) grid->ex->defer_fields = true;
     for (auto it = grid->hoods.begin(); s == DCCRGX_OK && it != grid->hoods.end(); ++it) {
         const NofHint hint{old.ex, &old_hoods.at(it->first), gone_flags, AMR_FLAG_GONE};
-        s = explicit_build_hood(grid, it->second, gone_flags && !old.uniform && old.ex ? &hint : nullptr);
+        s = explicit_build_hood_async(grid, it->second, gone_flags && !old.uniform && old.ex ? &hint : nullptr);
     }
     T.lap("neighborhoods");
     if (s == DCCRGX_OK) s = explicit_add_slots(grid, retired, true);  // retired cells are not leaves

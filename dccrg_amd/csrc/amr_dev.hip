@@ -1015,7 +1015,9 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
                           {retired.data(), o.retired, cnt[3] * 8ull}};
     DX_TRY(dx_d2h_many(ctx, lists, 4, st));
     nr.insert(nr.end(), A.nr_other.begin(), A.nr_other.end());
-    {  // the three lists sorted side by side on the host threads
+    // the three lists sorted side by side on the host threads (after the
+    // device work of the new leaf list is queued, which they overlap)
+    auto sort_lists = [&] {
         std::vector<uint64_t>* lv[3] = {&A.new_cells, &A.removed, &retired};
         const size_t nt = std::min<size_t>(3, host_threads());
         pool_run(nt, [&](size_t t) {
@@ -1025,10 +1027,13 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
                 v.erase(std::unique(v.begin(), v.end()), v.end());
             }
         });
-    }
+    };
     *changed = cnt[0] > 0;
     T.lap("lists");
-    if (!*changed) return DCCRGX_OK;
+    if (!*changed) {
+        sort_lists();
+        return DCCRGX_OK;
+    }
     // the new leaf list: surviving leaves in order, merged with the sorted new ones
     uint8_t* d_keep;
     uint64_t *d_kept, *d_sorted, *d_cnt64;
@@ -1049,6 +1054,7 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, tb, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
     DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, tb2, o.added, d_sorted, (int)cnt[0], 0, bits, st));
     DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, tb3, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
+    sort_lists();
     uint64_t nk[2] = {0, 0};
     DX_TRY(dx_d2h(ctx, nk, d_cnt64, 16, st));
     T.lap("kept + sorted new");

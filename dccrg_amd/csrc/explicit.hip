@@ -1050,7 +1050,6 @@ static int sync_slots(dccrgx_grid* grid, bool slot_map_changed)
 {
     Explicit* E = grid->ex;
     hipStream_t st = grid->ctx->compute;
-    DX_HIP(hipStreamSynchronize(st));
     const uint64_t ns = E->slot_ids.size(), nl = E->local.size();
     if (slot_map_changed || !E->d_slot_of_g) {
         dx_free(E->d_slot_of_g);
@@ -1653,7 +1652,7 @@ __global__ void __launch_bounds__(64) k_st_inc_fill(const uint32_t* __restrict__
     }
 }
 
-int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint)
+int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
 {
     Explicit* E = grid->ex;
     Ctx* ctx = grid->ctx;
@@ -1902,7 +1901,13 @@ int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     else DX_TRY(upload(grid->ctx, L.inner_pos, &L.d_inner_pos, st));
     DX_TRY(upload(grid->ctx, L.outer_pos, &L.d_outer_pos, st));
     DX_TRY(device_iota(&L.d_all_pos, nl, st));
-    DX_HIP(hipStreamSynchronize(st));
+    return DCCRGX_OK;
+}
+
+int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint)
+{
+    DX_TRY(explicit_build_hood_async(grid, h, hint));
+    DX_HIP(hipStreamSynchronize(grid->ctx->compute));
     return DCCRGX_OK;
 }
 

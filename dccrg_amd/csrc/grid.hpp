@@ -432,6 +432,8 @@ struct NofHint {
     uint32_t gone_bit;
 };
 int explicit_build_hood(dccrgx_grid* grid, Hood& h, const NofHint* hint = nullptr);
+// the same without the final synchronisation (the caller synchronises: rebuild)
+int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint = nullptr);
 // host copies of a neighborhood's neighbor lists, fetched once per build
 int explicit_host_lists(const dccrgx_grid* grid, const Hood& h);
 int explicit_host_lists(const dccrgx_grid* grid, int32_t hood_id);
