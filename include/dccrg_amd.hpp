@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cmath>
 #include <limits>
 #include <cstdint>
 #include <cstdio>
@@ -396,7 +397,7 @@ private:
 struct No_Geometry {  // dccrg_no_geometry.hpp (nothing on the hot path)
     static const int geometry_id = 0;
     struct Parameters {};
-    explicit No_Geometry(const Mapping* = nullptr) {}
+    explicit No_Geometry(const Mapping* = nullptr, const Grid_Topology* = nullptr) {}
     bool set(const Parameters&) { return true; }
     bool read_file_data(const std::vector<char>& b) const
     {
@@ -431,7 +432,10 @@ struct Cartesian_Geometry_Parameters {
 struct Cartesian_Geometry {
     static const int geometry_id = 1;
     typedef Cartesian_Geometry_Parameters Parameters;
-    explicit Cartesian_Geometry(const Mapping* m = nullptr) : mapping_(m) {}
+    explicit Cartesian_Geometry(const Mapping* m = nullptr, const Grid_Topology* t = nullptr)
+        : mapping_(m), topology_(t)
+    {
+    }
     bool set(const Parameters& p)
     {
         for (double v : p.level_0_cell_length)
@@ -442,6 +446,49 @@ struct Cartesian_Geometry {
     const Parameters& get() const { return par_; }
     std::array<double, 3> get_start() const { return par_.start; }
     std::array<double, 3> get_level_0_cell_length() const { return par_.level_0_cell_length; }
+    // :244-268: the corner with the largest coordinates
+    std::array<double, 3> get_end() const
+    {
+        const auto& len = mapping_->length.get();
+        std::array<double, 3> e;
+        for (int d = 0; d < 3; d++) e[d] = par_.start[d] + double(len[d]) * par_.level_0_cell_length[d];
+        return e;
+    }
+    // :522-566: the coordinate itself inside the grid, its periodic image
+    // inside a periodic dimension, NaN outside a non-periodic one
+    std::array<double, 3> get_real_coordinate(const std::array<double, 3>& c) const
+    {
+        const std::array<double, 3> start = par_.start, end = get_end();
+        std::array<double, 3> r = nan3();
+        for (int d = 0; d < 3; d++) {
+            if (c[d] >= start[d] && c[d] <= end[d]) {
+                r[d] = c[d];
+            } else if (topology_ && topology_->is_periodic(d)) {
+                const double L = end[d] - start[d];
+                if (c[d] < start[d]) r[d] = c[d] + L * std::ceil((start[d] - c[d]) / L);
+                else r[d] = c[d] - L * std::ceil((c[d] - end[d]) / L);
+            }
+        }
+        return r;
+    }
+    // :576-608: indices (maximum-level units) of a coordinate, error_index
+    // outside a non-periodic dimension
+    Types<3>::indices_t get_indices(const std::array<double, 3>& given) const
+    {
+        Types<3>::indices_t r{{error_index, error_index, error_index}};
+        const std::array<double, 3> start = par_.start, end = get_end(), c = get_real_coordinate(given);
+        const double top = double(uint64_t(1) << mapping_->get_maximum_refinement_level());
+        for (int d = 0; d < 3; d++)
+            if (c[d] >= start[d] && c[d] <= end[d])
+                r[d] = uint64_t(std::floor((c[d] - start[d]) / (par_.level_0_cell_length[d] / top)));
+        return r;
+    }
+    // :496-507: the cell of a refinement level at a coordinate
+    uint64_t get_cell(int level, const std::array<double, 3>& c) const
+    {
+        if (level < 0 || level > mapping_->get_maximum_refinement_level()) return error_cell;
+        return mapping_->get_cell_from_indices(get_indices(c), level);
+    }
     // :284-309 (NaN for error_cell or an invalid cell)
     std::array<double, 3> get_length(uint64_t cell) const
     {
@@ -501,6 +548,7 @@ private:
         return {{q, q, q}};
     }
     const Mapping* mapping_;
+    const Grid_Topology* topology_ = nullptr;
     Parameters par_;
 };
 
@@ -537,7 +585,7 @@ public:
 
     Mapping mapping;
     Grid_Topology topology;
-    Geometry geometry{&mapping};
+    Geometry geometry{&mapping, &topology};
 
     Dccrg() = default;
     Dccrg(const Dccrg&) = delete;
@@ -804,6 +852,48 @@ public:
     bool unrefine_completely(uint64_t cell) { return request(dccrgx_unrefine_completely, cell); }
     bool dont_refine(uint64_t cell) { return request(dccrgx_dont_refine, cell); }
     bool dont_unrefine(uint64_t cell) { return request(dccrgx_dont_unrefine, cell); }
+    // dccrg.hpp:3401-3467: the same for the smallest existing cell at a coordinate
+    bool refine_completely_at(const std::array<double, 3>& c)
+    {
+        const uint64_t cell = get_existing_cell(c);
+        return cell != error_cell && refine_completely(cell);
+    }
+    bool unrefine_completely_at(const std::array<double, 3>& c)
+    {
+        const uint64_t cell = get_existing_cell(c);
+        return cell != error_cell && unrefine_completely(cell);
+    }
+    bool dont_unrefine_at(const std::array<double, 3>& c)
+    {
+        const uint64_t cell = get_existing_cell(c);
+        return cell != error_cell && dont_unrefine(cell);
+    }
+    // dccrg.hpp:11414-11447: the smallest existing cell at the indices between
+    // two refinement levels inclusive, else error_cell
+    uint64_t get_existing_cell(const Types<3>::indices_t& idx, int min_level, int max_level) const
+    {
+        const int M = mapping.get_maximum_refinement_level();
+        for (int d = 0; d < 3; d++)
+            if (idx[d] >= mapping.length.get()[d] * (uint64_t(1) << M)) return error_cell;
+        if (min_level > max_level) return error_cell;
+        for (int l = max_level; l >= min_level; l--) {
+            const uint64_t cell = mapping.get_cell_from_indices(idx, l);
+            if (cell != error_cell && get_process(cell) >= 0) return cell;
+        }
+        return error_cell;
+    }
+    // dccrg.hpp:6424-6444: ... at a coordinate (the geometry's indices)
+    uint64_t get_existing_cell(const std::array<double, 3>& c) const
+    {
+        const Types<3>::indices_t idx = geometry.get_indices(c);
+        if (idx[0] == error_index || idx[1] == error_index || idx[2] == error_index) return error_cell;
+        return get_existing_cell(idx, 0, mapping.get_maximum_refinement_level());
+    }
+    // dccrg.hpp:6752-6755: the largest refinement level difference between neighbors
+    int get_max_ref_lvl_diff() const { return 1; }
+    // dccrg.hpp:6717-6728
+    bool get_initialized() const { return initialized_; }
+    bool get_mapping_initialized() const { return true; }
 
     // collective; returns the cells created on this rank
     std::vector<uint64_t> stop_refining(bool sorted = false)
@@ -1002,6 +1092,20 @@ public:
         int32_t dirs[24];
         if (dccrgx_face_neighbors_of_host(grid_, &cell, 1, row, ids, dirs, 24) != DCCRGX_OK) return out;
         for (uint64_t e = row[0]; e < row[1]; e++) out.emplace_back(ids[e], (int)dirs[e]);
+        return out;
+    }
+    // dccrg.hpp:3225-3287: the remote cells that consider a local cell their
+    // neighbor (nothing for a cell that is not local or an unknown neighborhood)
+    std::vector<uint64_t> get_remote_neighbors_to(uint64_t cell, int hood = default_neighborhood_id,
+                                                  bool sorted = false) const
+    {
+        std::vector<uint64_t> out;
+        if (!is_local(cell)) return out;
+        const neighbor_list_t* to = get_neighbors_to(cell, hood);
+        if (!to) return out;
+        for (const auto& x : *to)
+            if (x.first != error_cell && get_process(x.first) != rank_) out.push_back(x.first);
+        if (sorted) std::sort(out.begin(), out.end());
         return out;
     }
     std::vector<uint64_t> get_remote_cells_on_process_boundary(int hood = default_neighborhood_id, bool = false) const

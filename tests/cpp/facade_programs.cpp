@@ -324,6 +324,67 @@ static int cells(int argc, char** argv)
     return 0;
 }
 
+// the coordinate lookups: get_existing_cell, refine_completely_at,
+// dont_unrefine_at (dccrg.hpp:3401-3467, 6424-6444, 11414-11447) over the
+// Cartesian geometry's get_indices / get_real_coordinate / get_cell
+// (dccrg_cartesian_geometry.hpp:496-608), and get_remote_neighbors_to
+// (dccrg.hpp:3225-3287) against the neighbor lists; aborts on a mismatch
+static int coords()
+{
+    int rank = 0;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    dccrg::Dccrg<int, dccrg::Cartesian_Geometry> grid;
+    grid.set_initial_length({4, 4, 2})
+        .set_neighborhood_length(1)
+        .set_maximum_refinement_level(2)
+        .set_periodic(true, false, false)
+        .initialize(MPI_COMM_WORLD);
+    // x from -1 (4 cells of 0.5), y from 0 (4 of 1), z from 0 (2 of 2)
+    if (!grid.set_geometry(dccrg::Cartesian_Geometry::Parameters({{-1, 0, 0}}, {{0.5, 1, 2}}))) abort();
+    auto want = [](bool ok, const char* what) {
+        if (!ok) {
+            std::fprintf(stderr, "FAIL %s\n", what);
+            abort();
+        }
+    };
+    const uint64_t err = dccrg::error_cell;
+    want(grid.get_existing_cell({{-0.9, 0.1, 0.1}}) == 1, "first cell");
+    want(grid.get_existing_cell({{0.9, 3.9, 3.9}}) == 32, "last cell");
+    want(grid.get_existing_cell({{1.1, 0.1, 0.1}}) == 1, "periodic x wraps");
+    want(grid.get_existing_cell({{-2.9, 0.1, 0.1}}) == 1, "periodic x wraps from below");
+    want(grid.get_existing_cell({{0.0, -0.1, 0.1}}) == err, "outside non-periodic y");
+    want(grid.get_existing_cell({{0.0, 4.0, 0.1}}) == err, "on the end face of y: index past the grid");
+    want(grid.geometry.get_end()[0] == 1.0 && grid.geometry.get_end()[2] == 4.0, "get_end");
+    const bool mine = grid.is_local(1);
+    want(grid.refine_completely_at({{-0.9, 0.1, 0.1}}) == mine, "refine_completely_at on the owner");
+    want(!grid.refine_completely_at({{0.0, 9.0, 0.0}}), "refine_completely_at outside");
+    grid.stop_refining();
+    const uint64_t child = grid.mapping.get_cell_from_indices({{0, 0, 0}}, 1);
+    want(grid.get_existing_cell({{-0.9, 0.1, 0.1}}) == child, "smallest cell after refinement");
+    want(grid.get_existing_cell({{0, 0, 0}}, 0, 0) == err, "level 0 only: the parent is gone");
+    want(grid.get_existing_cell({{0, 0, 0}}, 0, 2) == child, "levels 0-2");
+    want(grid.get_existing_cell({{0, 0, 0}}, 2, 1) == err, "min level > max level");
+    want(grid.geometry.get_cell(1, {{-0.9, 0.1, 0.1}}) == child, "geometry get_cell");
+    want(grid.geometry.get_cell(3, {{-0.9, 0.1, 0.1}}) == err, "geometry get_cell beyond the maximum level");
+    const bool dont = grid.dont_unrefine_at({{-0.9, 0.1, 0.1}});
+    if (grid.is_local(child)) want(dont, "dont_unrefine_at on the owner");
+    want(!grid.dont_unrefine_at({{0.0, 9.0, 0.0}}), "dont_unrefine_at outside");
+    size_t n_remote = 0;
+    for (uint64_t c : grid.get_cells()) {
+        std::vector<uint64_t> brute;
+        for (const auto& x : *grid.get_neighbors_to(c))
+            if (grid.get_process(x.first) != rank) brute.push_back(x.first);
+        std::sort(brute.begin(), brute.end());
+        want(grid.get_remote_neighbors_to(c, dccrg::default_neighborhood_id, true) == brute, "remote neighbors to");
+        n_remote += brute.size();
+    }
+    for (uint64_t c = 1; c <= 32; c++)
+        if (!grid.is_local(c)) want(grid.get_remote_neighbors_to(c).empty(), "not local: nothing");
+    want(grid.get_max_ref_lvl_diff() == 1 && grid.get_initialized() && grid.get_mapping_initialized(), "getters");
+    std::printf("coords ok rank %d remote_to %zu\n", rank, n_remote);
+    return 0;
+}
+
 static void live_neighbor_counts(const dccrg::Dccrg<game_of_life_cell>::Iterator_Storage<
                                      dccrg::Dccrg<game_of_life_cell>::Cells_Item>& cells)
 {
@@ -403,6 +464,7 @@ int main(int argc, char** argv)
         else if (mode == "restart") rc = restart(argc, argv);
         else if (mode == "cells") rc = cells(argc, argv);
         else if (mode == "overlap") rc = overlap(argc, argv);
+        else if (mode == "coords") rc = coords();
     }
     MPI_Finalize();
     return rc;

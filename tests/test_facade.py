@@ -249,3 +249,13 @@ def test_facade_get_cells_criteria(dims, per, hood):
             for exact in (0, 1):
                 want = [cid for cid in range(1, n + 1) if (types[cid] == c if exact else types[cid] & c)]
                 assert got[f"hood {h} crit {c} exact {exact}"] == want, (h, c, exact)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_facade_coordinate_lookups(ranks):
+    """get_existing_cell / refine_completely_at / dont_unrefine_at over the
+    Cartesian geometry (periodic wrap, end face, non-periodic miss, after a
+    refinement) and get_remote_neighbors_to against the neighbor lists."""
+    out = run("coords", ranks=ranks)
+    assert out.count("coords ok") == ranks, out
