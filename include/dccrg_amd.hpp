@@ -1122,6 +1122,10 @@ public:
         if (s == DCCRGX_EINVAL) return false;
         detail::check(s, "add_neighborhood");
         build_hood(id);
+        user_hood_of_[id] = items;
+        auto& to = user_hood_to_[id];
+        to.clear();
+        for (const auto& it : items) to.push_back({{-it[0], -it[1], -it[2]}});
         return true;
     }
     Dccrg& remove_neighborhood(int id)
@@ -1129,7 +1133,64 @@ public:
         if (id == default_neighborhood_id) return *this;
         detail::check(dccrgx_remove_neighborhood(grid_, id), "remove_neighborhood");
         hoods_.erase(id);
+        user_hood_of_.erase(id);
+        user_hood_to_.erase(id);
         return *this;
+    }
+    // dccrg.hpp:6860-6880: the items of the user neighborhoods and their opposites
+    const std::unordered_map<int, std::vector<Types<3>::neighborhood_item_t>>& get_user_hood_of() const
+    {
+        return user_hood_of_;
+    }
+    const std::unordered_map<int, std::vector<Types<3>::neighborhood_item_t>>& get_user_hood_to() const
+    {
+        return user_hood_to_;
+    }
+    // dccrg.hpp:6886-6914: the default neighborhood's lists of every cell here
+    const std::unordered_map<uint64_t, neighbor_list_t>& get_all_neighbors_of() const
+    {
+        return hs(default_neighborhood_id).nof;
+    }
+    const std::unordered_map<uint64_t, neighbor_list_t>& get_all_neighbors_to() const
+    {
+        return hs(default_neighborhood_id).nto;
+    }
+    // dccrg.hpp:6978-7044: per user neighborhood, the cells with a remote
+    // neighbor, the remote cells with a local neighbor, and the tagged
+    // send / receive lists per process
+    const std::unordered_map<int, std::unordered_set<uint64_t>>& get_user_local_cells_on_process_boundary() const
+    {
+        user_local_bdy_.clear();
+        for (const auto& kv : hoods_)
+            if (kv.first != default_neighborhood_id) {
+                const std::vector<uint64_t> v = query_cells(kv.first, DCCRGX_CELLS_OUTER);
+                user_local_bdy_[kv.first].insert(v.begin(), v.end());
+            }
+        return user_local_bdy_;
+    }
+    const std::unordered_map<int, std::unordered_set<uint64_t>>& get_user_remote_cells_on_process_boundary() const
+    {
+        user_remote_bdy_.clear();
+        for (const auto& kv : hoods_)
+            if (kv.first != default_neighborhood_id)
+                user_remote_bdy_[kv.first].insert(kv.second.remote_ids.begin(), kv.second.remote_ids.end());
+        return user_remote_bdy_;
+    }
+    const std::unordered_map<int, std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>>&
+    get_user_neigh_cells_to_send() const
+    {
+        user_send_.clear();
+        for (const auto& kv : hoods_)
+            if (kv.first != default_neighborhood_id) user_send_[kv.first] = kv.second.send_tagged;
+        return user_send_;
+    }
+    const std::unordered_map<int, std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>>&
+    get_user_neigh_cells_to_receive() const
+    {
+        user_recv_.clear();
+        for (const auto& kv : hoods_)
+            if (kv.first != default_neighborhood_id) user_recv_[kv.first] = kv.second.recv_tagged;
+        return user_recv_;
     }
 
     // ---- halo ---------------------------------------------------------------
@@ -1571,6 +1632,11 @@ private:
     bool initialized_ = false;
     bool send_single_cells_ = false;
     std::map<MPI_Datatype, int> type_size_;
+    std::unordered_map<int, std::vector<Types<3>::neighborhood_item_t>> user_hood_of_, user_hood_to_;
+    // the user-neighborhood views, refreshed by their accessors
+    mutable std::unordered_map<int, std::unordered_set<uint64_t>> user_local_bdy_, user_remote_bdy_;
+    mutable std::unordered_map<int, std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>> user_send_,
+        user_recv_;
 };
 
 }  // namespace dccrg

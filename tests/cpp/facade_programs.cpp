@@ -308,6 +308,18 @@ static int cells(int argc, char** argv)
         if (grid.get_local_cells_not_on_process_boundary(hood) != grid.get_cells()) abort();
     }
     if (!grid.get_cells({dccrg::has_local_neighbor_of}, false, 99).empty()) abort();  // unknown hood
+    // the user-neighborhood views (dccrg.hpp:6860-6914, 6978-7044)
+    if (grid.get_user_hood_of().at(7) != std::vector<std::array<int, 3>>{{{1, 0, 0}}}) abort();
+    if (grid.get_user_hood_to().at(7) != std::vector<std::array<int, 3>>{{{-1, 0, 0}}}) abort();
+    if (grid.get_user_hood_of().count(dccrg::default_neighborhood_id)) abort();
+    if (!grid.get_user_local_cells_on_process_boundary().at(7).empty()) abort();  // one process
+    if (!grid.get_user_remote_cells_on_process_boundary().at(7).empty()) abort();
+    if (!grid.get_user_neigh_cells_to_send().at(7).empty() || !grid.get_user_neigh_cells_to_receive().at(7).empty())
+        abort();
+    for (uint64_t c : grid.get_cells()) {
+        if (grid.get_all_neighbors_of().at(c) != *grid.get_neighbors_of(c)) abort();
+        if (grid.get_all_neighbors_to().at(c) != *grid.get_neighbors_to(c)) abort();
+    }
     for (uint64_t c : grid.get_cells()) {
         printf("face %llu :", (unsigned long long)c);
         for (const auto& f : grid.get_face_neighbors_of(c)) printf(" %llu/%d", (unsigned long long)f.first, f.second);
