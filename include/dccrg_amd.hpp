@@ -44,6 +44,7 @@
 #include <cstdio>
 #include <cstring>
 #include <iomanip>
+#include <iterator>
 #include <iostream>
 #include <sstream>
 #include <map>
@@ -646,7 +647,7 @@ public:
     // items are updated again (e.g. a Center item after set_geometry)
     Dccrg& balance_load(bool = true)
     {
-        if (!initialized_) return *this;
+        if (!initialized_) return *this;  // weights stay: DCCRG_NO_LB skips initialize_balance_load's clear (:3839)
         std::vector<int> ids;
         for (auto& kv : hoods_) ids.push_back(kv.first);
         for (int id : ids) build_hood(id);
@@ -852,6 +853,29 @@ public:
     bool unrefine_completely(uint64_t cell) { return request(dccrgx_unrefine_completely, cell); }
     bool dont_refine(uint64_t cell) { return request(dccrgx_dont_refine, cell); }
     bool dont_unrefine(uint64_t cell) { return request(dccrgx_dont_unrefine, cell); }
+    // dccrg.hpp:5905-6130 as built with DCCRG_NO_LB (load balancing is not on
+    // this path: the partition stays the block one): pins do nothing
+    bool pin(uint64_t) { return false; }
+    bool pin(uint64_t, int) { return false; }
+    bool unpin(uint64_t) { return false; }
+    bool unpin_local_cells() { return false; }
+    Dccrg& unpin_all_cells() { return *this; }
+    // dccrg.hpp:6318-6379, 6450-6462: weights of local leaves (1 when unset),
+    // inherited by the children of a refined cell (:10392-10398), dropped with
+    // unrefined cells (:10509)
+    bool set_cell_weight(uint64_t cell, double weight)
+    {
+        if (!is_local(cell)) return false;
+        cell_weights_[cell] = weight;
+        return true;
+    }
+    double get_cell_weight(uint64_t cell) const
+    {
+        if (!is_local(cell)) return std::numeric_limits<double>::quiet_NaN();
+        auto it = cell_weights_.find(cell);
+        return it == cell_weights_.end() ? 1.0 : it->second;
+    }
+    const std::unordered_map<uint64_t, double>& get_cell_weights() const { return cell_weights_; }
     // dccrg.hpp:3401-3467: the same for the smallest existing cell at a coordinate
     bool refine_completely_at(const std::array<double, 3>& c)
     {
@@ -945,6 +969,14 @@ public:
             it = cell_data_.erase(it);
         }
         for (uint64_t c : local) cell_data_[c];
+        for (uint64_t c : created) {  // children of a refined local cell inherit its weight
+            const uint64_t parent = mapping.get_cell_from_indices(mapping.get_indices(c),
+                                                                  mapping.get_refinement_level(c) - 1);
+            auto w = cell_weights_.find(parent);
+            if (w != cell_weights_.end() && refined_data_.count(parent)) cell_weights_[c] = w->second;
+        }
+        for (auto it = cell_weights_.begin(); it != cell_weights_.end();)  // weights of cells that are gone
+            it = now.count(it->first) ? std::next(it) : cell_weights_.erase(it);
         remote_data_.clear();
         std::vector<int> ids;
         for (auto& kv : hoods_) ids.push_back(kv.first);
@@ -1633,6 +1665,7 @@ private:
     bool send_single_cells_ = false;
     std::map<MPI_Datatype, int> type_size_;
     std::unordered_map<int, std::vector<Types<3>::neighborhood_item_t>> user_hood_of_, user_hood_to_;
+    std::unordered_map<uint64_t, double> cell_weights_;
     // the user-neighborhood views, refreshed by their accessors
     mutable std::unordered_map<int, std::unordered_set<uint64_t>> user_local_bdy_, user_remote_bdy_;
     mutable std::unordered_map<int, std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>> user_send_,

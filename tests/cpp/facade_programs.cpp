@@ -22,6 +22,7 @@
 //                    "alive <id> <count>" lines (any number of MPI ranks)
 //   cells ...        get_cells criteria and process-boundary accessors
 // Built with the reference's own flags (-std=c++11, Makefile:8) by the tests.
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -393,6 +394,21 @@ static int coords()
     for (uint64_t c = 1; c <= 32; c++)
         if (!grid.is_local(c)) want(grid.get_remote_neighbors_to(c).empty(), "not local: nothing");
     want(grid.get_max_ref_lvl_diff() == 1 && grid.get_initialized() && grid.get_mapping_initialized(), "getters");
+    // load balancing as built with DCCRG_NO_LB; cell weights (dccrg.hpp:5905-6130, 6318-6379)
+    want(!grid.pin(child) && !grid.pin(child, 0) && !grid.unpin(child) && !grid.unpin_local_cells(), "no-LB pins");
+    grid.unpin_all_cells();
+    for (uint64_t c : grid.get_cells()) want(grid.get_cell_weight(c) == 1.0, "unset weight");
+    want(std::isnan(grid.get_cell_weight(0)), "weight of a non-cell");
+    if (grid.is_local(child)) {
+        want(grid.set_cell_weight(child, 2.5) && grid.get_cell_weight(child) == 2.5, "set weight");
+        want(grid.refine_completely(child), "refine the weighted cell");
+    }
+    grid.stop_refining();
+    const uint64_t grandchild = grid.mapping.get_cell_from_indices({{0, 0, 0}}, 2);
+    if (grid.is_local(grandchild)) {
+        want(grid.get_cell_weight(grandchild) == 2.5, "children inherit the weight");
+        want(grid.get_cell_weights().count(child) == 0, "the refined cell's weight is gone");
+    }
     std::printf("coords ok rank %d remote_to %zu\n", rank, n_remote);
     return 0;
 }
