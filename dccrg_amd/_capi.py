@@ -125,6 +125,7 @@ SIGNATURES = {
     "dccrgx_remove_neighborhood": (C.c_int, [_vp, C.c_int32]),
     "dccrgx_get_neighborhood": (C.c_int, [_vp, C.c_int32, _i32p, C.c_size_t, _szp]),
     "dccrgx_get_cells": (C.c_int, [_vp, C.c_int32, C.c_int32, _u64p, C.c_size_t, _szp]),
+    "dccrgx_get_all_cells": (C.c_int, [_vp, _u64p, C.c_size_t, _szp]),
     "dccrgx_neighbors_of": (C.c_int, [_vp, C.c_int32, _vp, C.c_size_t, _vp, _vp, _vp, C.c_size_t, _vp]),
     "dccrgx_neighbors_to": (C.c_int, [_vp, C.c_int32, _vp, C.c_size_t, _vp, _vp, C.c_size_t, _vp]),
     "dccrgx_get_peers": (C.c_int, [_vp, C.c_int32, C.c_int32, _i32p, _u64p, C.c_size_t, _szp]),

@@ -842,6 +842,24 @@ int dccrgx_get_neighborhood(const dccrgx_grid* grid, int32_t id, int32_t* items,
     return DCCRGX_OK;
 }
 
+int dccrgx_get_all_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, size_t* n)
+{
+    DX_CHECK(grid && n, DCCRGX_EINVAL, "null argument");
+    if (!grid->uniform) {
+        const std::vector<uint64_t>& L = grid->ex->leaves;
+        *n = L.size();
+        DX_CHECK(cap >= *n && (ids || !*n), DCCRGX_ERANGE, "capacity");
+        std::copy(L.begin(), L.end(), ids);
+        return DCCRGX_OK;
+    }
+    *n = grid->g.N;
+    DX_CHECK(cap >= *n && (ids || !*n), DCCRGX_ERANGE, "capacity");
+    parallel_ranges(*n, 1u << 16, [ids](size_t b, size_t e) {
+        for (size_t i = b; i < e; i++) ids[i] = i + 1;
+    });
+    return DCCRGX_OK;
+}
+
 int dccrgx_get_cells(const dccrgx_grid* grid, int32_t id, int32_t which, uint64_t* ids, size_t cap,
                      size_t* n)
 {

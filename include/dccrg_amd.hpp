@@ -1126,6 +1126,61 @@ public:
         for (uint64_t e = row[0]; e < row[1]; e++) out.emplace_back(ids[e], (int)dirs[e]);
         return out;
     }
+    // dccrg.hpp:3175-3222: the remote neighbors of a local cell (nothing for a
+    // cell that is not local or an unknown neighborhood)
+    std::vector<uint64_t> get_remote_neighbors_of(uint64_t cell, int hood = default_neighborhood_id,
+                                                  bool sorted = false) const
+    {
+        std::vector<uint64_t> out;
+        if (!is_local(cell)) return out;
+        const neighbor_list_t* of = get_neighbors_of(cell, hood);
+        if (!of) return out;
+        for (const auto& x : *of)
+            if (x.first != error_cell && get_process(x.first) != rank_) out.push_back(x.first);
+        if (sorted) std::sort(out.begin(), out.end());
+        return out;
+    }
+    // dccrg.hpp:3557-3590: every leaf of the grid (the replicated leaf set)
+    std::vector<uint64_t> get_all_cells(bool sorted = false) const
+    {
+        size_t n = 0;
+        detail::check(dccrgx_get_all_cells(grid_, nullptr, 0, &n) == DCCRGX_ERANGE || n == 0 ? DCCRGX_OK : DCCRGX_EINVAL,
+                      "get_all_cells");
+        std::vector<uint64_t> v(n);
+        if (n) detail::check(dccrgx_get_all_cells(grid_, v.data(), n, &n), "get_all_cells");
+        (void)sorted;  // ascending already
+        return v;
+    }
+    // dccrg.hpp:6840-6858: the default neighborhood's items and their opposites
+    std::vector<Types<3>::neighborhood_item_t> get_neighborhood_of() const
+    {
+        size_t n = 0;
+        detail::check(dccrgx_get_neighborhood(grid_, default_neighborhood_id, nullptr, 0, &n) == DCCRGX_ERANGE || n == 0
+                          ? DCCRGX_OK
+                          : DCCRGX_EINVAL,
+                      "get_neighborhood_of");
+        std::vector<int32_t> flat(3 * n);
+        if (n) detail::check(dccrgx_get_neighborhood(grid_, default_neighborhood_id, flat.data(), n, &n), "items");
+        std::vector<Types<3>::neighborhood_item_t> out(n);
+        for (size_t i = 0; i < n; i++) out[i] = {{flat[3 * i], flat[3 * i + 1], flat[3 * i + 2]}};
+        return out;
+    }
+    std::vector<Types<3>::neighborhood_item_t> get_neighborhood_to() const
+    {
+        std::vector<Types<3>::neighborhood_item_t> out = get_neighborhood_of();
+        for (auto& it : out) it = {{-it[0], -it[1], -it[2]}};
+        return out;
+    }
+    // dccrg.hpp:6733-6745, 7787-7800: MPI_TAG_UB of the communicator (32767 if unset)
+    unsigned int get_max_tag() const
+    {
+        void* attr = nullptr;
+        int flag = 0;
+        MPI_Comm_get_attr(comm_, MPI_TAG_UB, &attr, &flag);
+        return flag && attr ? (unsigned int)*static_cast<int*>(attr) : 32767u;
+    }
+    // dccrg.hpp:6836-6842: the local cells' data
+    const std::unordered_map<uint64_t, Cell_Data>& get_cell_data() const { return cell_data_; }
     // dccrg.hpp:3225-3287: the remote cells that consider a local cell their
     // neighbor (nothing for a cell that is not local or an unknown neighborhood)
     std::vector<uint64_t> get_remote_neighbors_to(uint64_t cell, int hood = default_neighborhood_id,

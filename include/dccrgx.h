@@ -202,6 +202,11 @@ int dccrgx_get_neighborhood(const dccrgx_grid* grid, int32_t hood_id, int32_t* i
  * output.  DCCRGX_ERANGE with *n = needed size if cap is too small. */
 int dccrgx_get_cells(const dccrgx_grid* grid, int32_t hood_id, int32_t which, uint64_t* ids_host,
                      size_t cap, size_t* n);
+
+/* Dccrg::get_all_cells (dccrg.hpp:3557-3590): every existing leaf cell of the
+ * grid (the replicated leaf set; uniform grids: 1..N), ascending, host output.
+ * DCCRGX_ERANGE with *n = needed size if cap is too small. */
+int dccrgx_get_all_cells(const dccrgx_grid* grid, uint64_t* ids_host, size_t cap, size_t* n);
 /* Dccrg::get_neighbors_of (dccrg.hpp:836-883 / find_neighbors_of :4375-4716)
  * for n cells in one batch, computed on the device: CSR in reference list
  * order.  row_ptr_dev has n+1 entries; call with ids_dev == NULL to size. */

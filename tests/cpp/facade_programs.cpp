@@ -382,8 +382,24 @@ static int coords()
     const bool dont = grid.dont_unrefine_at({{-0.9, 0.1, 0.1}});
     if (grid.is_local(child)) want(dont, "dont_unrefine_at on the owner");
     want(!grid.dont_unrefine_at({{0.0, 9.0, 0.0}}), "dont_unrefine_at outside");
+    const std::vector<uint64_t> all = grid.get_all_cells();
+    want(all.size() == 31 + 8 && std::is_sorted(all.begin(), all.end()), "get_all_cells: 31 level-0 cells + 8");
+    want(std::binary_search(all.begin(), all.end(), child) && !std::binary_search(all.begin(), all.end(), 1),
+         "get_all_cells: the children, not the parent");
+    const auto items = grid.get_neighborhood_of();
+    want(items.size() == 26 && items.front() == (std::array<int, 3>{{-1, -1, -1}}) &&
+             items.back() == (std::array<int, 3>{{1, 1, 1}}) &&
+             grid.get_neighborhood_to().front() == (std::array<int, 3>{{1, 1, 1}}),
+         "neighborhood items in z, y, x order");
+    want(grid.get_max_tag() >= 32767u, "max tag");
+    want(grid.get_cell_data().size() == grid.get_cells().size(), "cell data of the local cells");
     size_t n_remote = 0;
     for (uint64_t c : grid.get_cells()) {
+        std::vector<uint64_t> of;
+        for (const auto& x : *grid.get_neighbors_of(c))
+            if (grid.get_process(x.first) != rank) of.push_back(x.first);
+        std::sort(of.begin(), of.end());
+        want(grid.get_remote_neighbors_of(c, dccrg::default_neighborhood_id, true) == of, "remote neighbors of");
         std::vector<uint64_t> brute;
         for (const auto& x : *grid.get_neighbors_to(c))
             if (grid.get_process(x.first) != rank) brute.push_back(x.first);
