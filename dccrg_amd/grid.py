@@ -429,6 +429,17 @@ class Dccrg:
     def remote_cells(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> np.ndarray:
         return self._cells(X.CELLS_REMOTE, hood)
 
+    def get_all_cells(self) -> np.ndarray:
+        """Every leaf of the grid, ascending (Dccrg::get_all_cells, dccrg.hpp:3557-3590)."""
+        n = C.c_size_t()
+        s = lib().dccrgx_get_all_cells(self._h, None, 0, C.byref(n))
+        if s not in (X.DCCRGX_OK, 5):  # 5: ERANGE, the sizing call
+            check(s)
+        out = np.zeros(n.value, dtype=np.uint64)
+        if n.value:
+            check(lib().dccrgx_get_all_cells(self._h, out.ctypes.data_as(X._u64p), out.size, C.byref(n)))
+        return out
+
     def neighbors_of(self, cells: np.ndarray, hood: int = DEFAULT_NEIGHBORHOOD_ID):
         """Batched get_neighbors_of: (row_ptr, ids, offsets[x,y,z]) as numpy."""
         import torch

@@ -67,6 +67,18 @@ def test_explicit_neighbor_lists(case):
     row, ids = g.neighbors_to(cells)
     for i, c in enumerate(leaves):
         assert [int(v) for v in ids[int(row[i]):int(row[i + 1])]] == og.find_neighbors_to(c), c
+    # get_all_cells: the replicated leaf set, ascending
+    assert g.get_all_cells().tolist() == sorted(int(c) for c in leaves)
+
+
+def test_all_cells_uniform():
+    """get_all_cells of a uniform grid: every level-0 cell (dccrg.hpp:3557-3590)."""
+    c = D.Context(0, 1, 3)
+    g = (D.Dccrg().set_initial_length((5, 4, 3)).set_maximum_refinement_level(2).set_neighborhood_length(1)
+         .initialize(c))
+    assert g.get_all_cells().tolist() == list(range(1, 61))
+    g.close()
+    c.close()
 
 
 @pytest.mark.parametrize("P", [2, 3, 5])
