@@ -627,7 +627,15 @@ def main():
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = D.Context(device, rank, world)
-    shared_gpu = world > ndev  # more ranks than GPUs (a rehearsal on one GPU): RCCL refuses that
+    # ranks on the same physical GPU (a rehearsal on one GPU): RCCL refuses
+    # that.  Decided from the devices' PCI ids, so a launcher that makes one
+    # GPU visible per process still gets RCCL between distinct GPUs.
+    shared_gpu = False
+    if world > 1:
+        pr = torch.cuda.get_device_properties(device)
+        ids = [None] * world
+        dist.all_gather_object(ids, (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id))
+        shared_gpu = len(set(ids)) < world
     if world > 1 and not shared_gpu:
         uid = [D.Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
