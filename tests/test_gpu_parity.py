@@ -547,3 +547,41 @@ def test_user_neighborhood_gol_matches_oracle():
         for g in grids:
             loc = g.local_cells().astype(np.int64)
             assert np.array_equal(g.read_local("n"), cnt[loc - 1])
+
+
+# ------------------------------------------------------------ empty batches ----
+@pytest.mark.parametrize("refined", [False, True])
+def test_empty_batches(refined):
+    """Every batched entry point accepts n = 0 (null id arrays): OK, the row
+    pointer array's single entry is 0, and nothing else is written."""
+    import ctypes as C
+    L = D.lib()
+    leaves = None
+    length = (4, 3, 2)
+    if refined:
+        m = O.Mapping(length, 1)
+        leaves = sorted(set(range(1, 25)) - {5}) + m.get_all_children(5)
+    c = D.Context(0, 0, 1)
+    g = (D.Dccrg().set_initial_length(length).set_neighborhood_length(1).set_maximum_refinement_level(1)
+         .set_periodic(True, False, False).initialize(c, leaves=leaves))
+    g.add_field("x", np.uint32)
+    row = torch.full((1,), 7, dtype=torch.int64, device=DEV)
+    torch.cuda.synchronize()
+    from dccrg_amd._capi import check as ok
+    H = D.DEFAULT_NEIGHBORHOOD_ID
+    ok(L.dccrgx_neighbors_of(g._h, H, None, 0, row.data_ptr(), None, None, 0, None))
+    ok(L.dccrgx_neighbors_of(g._h, H, None, 0, row.data_ptr(), row.data_ptr(), row.data_ptr(), 0, None))
+    ok(L.dccrgx_neighbors_to(g._h, H, None, 0, row.data_ptr(), None, 0, None))
+    ok(L.dccrgx_gather_neighbors(g._h, H, g.field_id("x"), None, 0, row.data_ptr(), None, 0, None))
+    ok(L.dccrgx_face_neighbors_of(g._h, None, 0, row.data_ptr(), None, None, 0, None))
+    ok(L.dccrgx_slots_of(g._h, None, 0, None, None))
+    ok(L.dccrgx_get_process(g._h, None, 0, None))
+    mp = D.Mapping(length, 1)
+    ok(L.dccrgx_map_ids_to_indices(C.byref(mp._m), None, 0, None, None, None))
+    ok(L.dccrgx_map_indices_to_ids(C.byref(mp._m), None, None, 0, None, None))
+    ok(L.dccrgx_map_ids_op(C.byref(mp._m), 0, None, 0, None, None))
+    c.synchronize()
+    assert int(row[0]) == 0
+    assert g.get_all_cells().size == (24 if not refined else 31)
+    g.close()
+    c.close()
