@@ -508,11 +508,8 @@ __global__ void __launch_bounds__(64) k_rows_gather(const uint32_t* __restrict__
         const int j = wave_row_of(s_dst, e);
         const uint64_t src = s_src[j] + (e - s_dst[j]);
         ids[e] = src_id[src];
-        if (off3) {
-            off3[3 * e + 0] = src_off[3 * src + 0];
-            off3[3 * e + 1] = src_off[3 * src + 1];
-            off3[3 * e + 2] = src_off[3 * src + 2];
-        }
+        if (off3)  // one 12-byte load and store per entry (dwordx3)
+            reinterpret_cast<int3*>(off3)[e] = reinterpret_cast<const int3*>(src_off)[src];
     }
 }
 
