@@ -479,6 +479,29 @@ def neighbor_lists(ctx, D, torch):
                                        f"refined once ({leaves.size} leaves), hood 1, periodic",
                            "initialize_s": t_init, "initialize_leaves_per_s": leaves.size / t_init,
                            **query(g, cells, 3)}
+    # get_neighbors_to of every leaf (dccrgx_neighbors_to: rows of the stored
+    # transpose, ids looked up from leaf indices); 8 B per entry + 8 B per row
+    q = cells.numel()
+    row = torch.zeros(q + 1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    X.check(D.lib().dccrgx_neighbors_to(g._h, X.DEFAULT_NEIGHBORHOOD_ID, cells.data_ptr(), q, row.data_ptr(), None,
+                                        0, None))
+    total = int(row[-1].item())
+    ids = torch.empty(total, dtype=torch.int64, device=dev)
+
+    def to_query():
+        X.check(D.lib().dccrgx_neighbors_to(g._h, X.DEFAULT_NEIGHBORHOOD_ID, cells.data_ptr(), q, row.data_ptr(),
+                                            ids.data_ptr(), total, None))
+    to_query()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        to_query()
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / 3
+    out["mixed_levels_to"] = {"workload": "get_neighbors_to of every leaf of the same grid", "cells": q,
+                              "entries": total, "ms": dt * 1e3, "output_GBs": (8 * total + 8 * (q + 1)) / dt / 1e9}
+    del ids, row
     g.close()
     return out
 

@@ -513,6 +513,29 @@ __global__ void __launch_bounds__(64) k_rows_gather(const uint32_t* __restrict__
     }
 }
 
+// the same for neighbors_to rows, whose entries are leaf indices: out entry
+// k of query i = leaves[src_g[src_row[gq[i]] + k]]
+__global__ void __launch_bounds__(64) k_rows_gather_g(const uint32_t* __restrict__ gq, uint64_t n,
+                                                      const uint64_t* __restrict__ src_row,
+                                                      const uint64_t* __restrict__ row,
+                                                      const uint32_t* __restrict__ src_g,
+                                                      const uint64_t* __restrict__ leaves, uint64_t* __restrict__ ids)
+{
+    __shared__ uint64_t s_dst[65], s_src[64];
+    const int lane = threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t last = r0 + 64 < n ? r0 + 64 : n;
+    s_dst[lane] = row[r0 + lane < last ? r0 + lane : last];
+    if (lane == 0) s_dst[64] = row[last];
+    if (r0 + lane < n) s_src[lane] = src_row[gq[r0 + lane]];
+    __syncthreads();
+    const uint64_t end = s_dst[64];
+    for (uint64_t e = s_dst[0] + lane; e < end; e += 64) {
+        const int j = wave_row_of(s_dst, e);
+        ids[e] = leaves[src_g[s_src[j] + (e - s_dst[j])]];
+    }
+}
+
 // query cells -> their leaf index and row length in the stored CSR
 __global__ void __launch_bounds__(256) k_ex_query_rows(ExView v, const uint64_t* __restrict__ cells, size_t n,
                                                        const uint64_t* __restrict__ nof_row, uint32_t* __restrict__ gq,
@@ -2147,27 +2170,36 @@ int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t
 int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, size_t n, uint64_t* row,
                           uint64_t* ids, size_t cap, hipStream_t st)
 {
-    const Explicit* E = grid->ex;
-    DX_TRY(explicit_host_lists(grid, h));
-    const auto& L = E->hl.at(h.id);
-    std::vector<uint64_t> hc(n);
-    DX_TRY(dx_d2h(grid->ctx, hc.data(), cells, n * 8, st));
-    DX_HIP(hipStreamSynchronize(st));
-    std::vector<uint64_t> orow(n + 1, 0), oids;
-    for (size_t i = 0; i < n; i++) {
-        const int64_t gi = E->find(hc[i]);
-        DX_CHECK(gi >= 0, DCCRGX_ENOTFOUND, "cell %llu does not exist", (unsigned long long)hc[i]);
-        const uint64_t g = (uint64_t)gi;
-        for (uint64_t e = L.h_nto_row[g]; e < L.h_nto_row[g + 1]; e++) oids.push_back(E->leaves[L.h_nto_g[e]]);
-        orow[i + 1] = oids.size();
-    }
-    DX_TRY(dx_h2d(grid->ctx, row, orow.data(), (n + 1) * 8, st));
-    if (ids) {
-        DX_CHECK(cap >= oids.size(), DCCRGX_ERANGE, "capacity %zu < %zu", cap, oids.size());
-        DX_TRY(dx_h2d(grid->ctx, ids, oids.data(), oids.size() * 8, st));
-    }
-    DX_HIP(hipStreamSynchronize(st));
-    return DCCRGX_OK;
+    // rows of the neighborhood's device neighbors_to CSR (ascending leaf
+    // indices = ascending ids), looked up and copied as neighbors_of's are
+    DX_CHECK(h.d_nto_row, DCCRGX_EINTERNAL, "no device lists for neighborhood %d", h.id);
+    uint32_t* gq = nullptr;
+    int32_t* d_err = nullptr;
+    DX_HIP(ds_malloc(&gq, std::max<size_t>(n, 1) * 4, st));
+    DX_HIP(ds_malloc(&d_err, 4, st));
+    auto done = [&](int code) {
+        (void)ds_free(gq, st);
+        (void)ds_free(d_err, st);
+        return code;
+    };
+    if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
+    if (n)
+        hipLaunchKernelGGL(k_ex_query_rows, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nto_row, gq,
+                           row, d_err);
+    uint64_t total = 0;
+    int s = device_scan_rows(row, n, st, &total);  // synchronises (total)
+    if (s != DCCRGX_OK) return done(s);
+    int32_t err = 0;
+    if ((s = dx_d2h(grid->ctx, &err, d_err, 4, st)) != DCCRGX_OK) return done(s);
+    if (err) return done(set_error(DCCRGX_ENOTFOUND, "cell does not exist"));
+    if (!ids) return done(DCCRGX_OK);
+    if (cap < total) return done(set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total));
+    if (n)
+        hipLaunchKernelGGL(k_rows_gather_g, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, (const uint32_t*)gq,
+                           (uint64_t)n, h.d_nto_row, (const uint64_t*)row, h.d_nto_g,
+                           (const uint64_t*)grid->ex->d_leaves, ids);
+    if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "neighbor list copy failed"));
+    return done(DCCRGX_OK);
 }
 
 namespace {
