@@ -400,6 +400,7 @@ struct No_Geometry {  // dccrg_no_geometry.hpp (nothing on the hot path)
     struct Parameters {};
     explicit No_Geometry(const Mapping* = nullptr, const Grid_Topology* = nullptr) {}
     bool set(const Parameters&) { return true; }
+    Parameters get() const { return Parameters(); }
     bool read_file_data(const std::vector<char>& b) const
     {
         int id = -1;
@@ -590,6 +591,46 @@ public:
 
     Dccrg() = default;
     Dccrg(const Dccrg&) = delete;
+    // dccrg.hpp:327-446: a grid of another cell data type over the same cells,
+    // owners, neighborhoods (user ones included), cell weights and
+    // communicator, already initialized; the local cells' data is
+    // default-constructed and the copies of remote neighbors allocated.  Cell
+    // owners follow the level-0 ancestors here (no load balancing moves a
+    // cell), so the same leaves under the same partition give the same owners.
+    template <class O_Cell, class O_Geometry, class O_ACI, class O_ANI>
+    explicit Dccrg(const Dccrg<O_Cell, O_Geometry, O_ACI, O_ANI>& other)
+    {
+        if (!other.get_initialized()) throw std::invalid_argument("copy of a grid that is not initialized");
+        mapping.set_length(other.mapping.length.get());
+        mapping.set_maximum_refinement_level(other.mapping.get_maximum_refinement_level());
+        for (int d = 0; d < 3; d++) topology.set_periodicity(d, other.topology.is_periodic(d));
+        if (!copy_geometry(other.geometry)) throw std::invalid_argument("geometry of the other grid not accepted");
+        hood_length_ = other.get_neighborhood_length();
+        send_single_cells_ = other.get_send_single_cells();
+        partition_ = (uint8_t)other.get_initial_partition();
+        init_comm(other.get_communicator());
+        dccrgx_grid_params p{};
+        for (int d = 0; d < 3; d++) {
+            p.length[d] = mapping.length.get()[d];
+            p.periodic[d] = topology.is_periodic(d) ? 1 : 0;
+        }
+        p.max_ref_lvl = mapping.get_maximum_refinement_level();
+        p.neighborhood_length = hood_length_;
+        p.partition = partition_;
+        // every level-0 cell and nothing else: keep the uniform layout
+        const std::vector<uint64_t> leaves = other.get_all_cells();
+        const uint64_t n0 = p.length[0] * p.length[1] * p.length[2];
+        const bool level0 = leaves.size() == n0 && (n0 == 0 || leaves.back() == n0);
+        detail::check(dccrgx_grid_create(ctx_, &p, level0 ? nullptr : leaves.data(), level0 ? 0 : leaves.size(),
+                                         &grid_),
+                      "grid");
+        for (uint64_t c : query_cells(default_neighborhood_id, DCCRGX_CELLS_LOCAL)) cell_data_[c];
+        cell_weights_ = other.get_cell_weights();
+        initialized_ = true;
+        build_hood(default_neighborhood_id);
+        for (const auto& kv : other.get_user_hood_of())
+            if (!add_neighborhood(kv.first, kv.second)) throw std::invalid_argument("neighborhood of the other grid");
+    }
     ~Dccrg()
     {
         if (grid_) dccrgx_grid_destroy(grid_);
@@ -641,6 +682,7 @@ public:
         return *this;
     }
     bool set_geometry(const typename Geometry::Parameters& p) { return geometry.set(p); }
+    int get_initial_partition() const { return partition_; }
     // dccrg.hpp:1046-1064: the block partition is kept (Zoltan stays out of
     // the device path), but like finish_balance_load the iteration caches are
     // rebuilt (update_cell_pointers, :11453), so additional cell / neighbor
@@ -782,6 +824,10 @@ public:
     }
 
 private:
+    // the converting constructor's geometry: the parameters of the same
+    // geometry type, the default of this one otherwise
+    bool copy_geometry(const Geometry& g) { return geometry.set(g.get()); }
+    template <class G> bool copy_geometry(const G&) { return true; }
     void init_comm(const MPI_Comm& comm)
     {
         MPI_Comm_dup(comm, &comm_);

@@ -21,6 +21,8 @@
 //                    get_neighbors_of_at_offset against neighbors_of; prints
 //                    "alive <id> <count>" lines (any number of MPI ranks)
 //   cells ...        get_cells criteria and process-boundary accessors
+//   coords           geometry lookups, refinement at a coordinate, no-LB calls
+//   copy             the converting copy constructor (tests/constructors/copy.cpp)
 // Built with the reference's own flags (-std=c++11, Makefile:8) by the tests.
 #include <cmath>
 #include <cstdio>
@@ -429,6 +431,99 @@ static int coords()
     return 0;
 }
 
+// tests/constructors/copy.cpp's cell types: the copy holds another type
+struct copy_cell_1 {
+    int data = -1;
+    std::tuple<void*, int, MPI_Datatype> get_mpi_datatype() { return std::make_tuple((void*)&data, 1, MPI_INT); }
+};
+struct copy_cell_2 {
+    double data = -2;
+    std::tuple<void*, int, MPI_Datatype> get_mpi_datatype() { return std::make_tuple((void*)&data, 1, MPI_DOUBLE); }
+};
+
+template <class G> static void check_remote_copies(const G& grid, double factor, const char* what)
+{
+    for (uint64_t c : grid.get_remote_cells_on_process_boundary()) {
+        const auto* d = grid[c];
+        if (d == nullptr || double(d->data) != factor * grid.get_process(c)) {
+            std::fprintf(stderr, "FAIL %s: cell %llu\n", what, (unsigned long long)c);
+            abort();
+        }
+    }
+}
+
+// tests/constructors/copy.cpp, on a refined grid with a user neighborhood
+// and a cell weight: the copy (another cell type, then another geometry)
+// has the same cells, owners, lists and iterators, default-constructed
+// data, and remote neighbor updates that work independently of the original
+static int copy()
+{
+    int rank = 0;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    auto want = [](bool ok, const char* what) {
+        if (!ok) {
+            std::fprintf(stderr, "FAIL %s\n", what);
+            abort();
+        }
+    };
+    dccrg::Dccrg<copy_cell_1, dccrg::Cartesian_Geometry> grid1;
+    grid1.set_initial_length({10, 10, 10})
+        .set_neighborhood_length(1)
+        .set_maximum_refinement_level(1)
+        .set_periodic(true, false, false)
+        .initialize(MPI_COMM_WORLD);
+    want(grid1.set_geometry(dccrg::Cartesian_Geometry::Parameters({{-1, 0, 0}}, {{0.5, 1, 2}})), "geometry");
+    if (grid1.is_local(456)) grid1.refine_completely(456);
+    grid1.stop_refining();
+    const std::vector<dccrg::Types<3>::neighborhood_item_t> items{{{0, 0, -1}}, {{0, 0, 1}}, {{1, 0, 0}}};
+    want(grid1.add_neighborhood(7, items), "user neighborhood");
+    const uint64_t child = grid1.get_all_cells().back();
+    if (grid1.is_local(child)) want(grid1.set_cell_weight(child, 3.0), "weight");
+    for (const auto& cell : grid1.local_cells()) cell.data->data = rank;
+    grid1.update_copies_of_remote_neighbors();
+    check_remote_copies(grid1, 1, "grid1 update");
+
+    dccrg::Dccrg<copy_cell_2, dccrg::Cartesian_Geometry> grid2(grid1);
+    want(grid2.get_initialized(), "initialized");
+    want(grid2.get_all_cells() == grid1.get_all_cells() && grid2.get_cells() == grid1.get_cells(), "same cells");
+    for (uint64_t c : grid1.get_all_cells()) want(grid2.get_process(c) == grid1.get_process(c), "same owners");
+    want(grid2.geometry.get_start() == grid1.geometry.get_start() &&
+             grid2.geometry.get_level_0_cell_length() == grid1.geometry.get_level_0_cell_length(),
+         "geometry copied");
+    want(grid2.get_neighborhood_length() == 1 && grid2.topology.is_periodic(0) && !grid2.topology.is_periodic(1) &&
+             grid2.mapping.get_maximum_refinement_level() == 1,
+         "parameters copied");
+    want(grid2.get_user_hood_of() == grid1.get_user_hood_of() && grid2.get_cell_weights() == grid1.get_cell_weights(),
+         "user neighborhoods and weights copied");
+    for (uint64_t c : grid1.get_cells()) {
+        want(*grid2.get_neighbors_of(c) == *grid1.get_neighbors_of(c), "neighbors_of");
+        want(*grid2.get_neighbors_to(c) == *grid1.get_neighbors_to(c), "neighbors_to");
+        want(*grid2.get_neighbors_of(c, 7) == *grid1.get_neighbors_of(c, 7), "user neighbors_of");
+    }
+    for (const auto& cell : grid2.local_cells()) want(cell.data->data == -2, "default-constructed data");
+    want(size_t(std::distance(grid2.local_cells().begin(), grid2.local_cells().end())) == grid2.get_cells().size(),
+         "local iterator");
+    want(size_t(std::distance(grid2.inner_cells().begin(), grid2.inner_cells().end())) ==
+             grid2.get_local_cells_not_on_process_boundary().size(),
+         "inner iterator");
+    want(size_t(std::distance(grid2.outer_cells().begin(), grid2.outer_cells().end())) ==
+             grid2.get_local_cells_on_process_boundary().size(),
+         "outer iterator");
+    want(grid2.get_remote_cells_on_process_boundary() == grid1.get_remote_cells_on_process_boundary(),
+         "remote cells on the process boundary");
+    for (const auto& cell : grid2.local_cells()) cell.data->data = 2 * rank;
+    grid2.update_copies_of_remote_neighbors();
+    check_remote_copies(grid2, 2, "grid2 update");
+    check_remote_copies(grid1, 1, "grid1 untouched");
+    want(grid2.update_copies_of_remote_neighbors(7), "user neighborhood update");
+
+    dccrg::Dccrg<copy_cell_1> grid3(grid2);  // and into another geometry
+    want(grid3.get_all_cells() == grid1.get_all_cells() && grid3.get_cells() == grid1.get_cells(), "third grid");
+    for (const auto& cell : grid3.local_cells()) want(cell.data->data == -1, "third grid data");
+    std::printf("copy ok rank %d cells %zu\n", rank, grid2.get_cells().size());
+    return 0;
+}
+
 static void live_neighbor_counts(const dccrg::Dccrg<game_of_life_cell>::Iterator_Storage<
                                      dccrg::Dccrg<game_of_life_cell>::Cells_Item>& cells)
 {
@@ -509,6 +604,7 @@ int main(int argc, char** argv)
         else if (mode == "cells") rc = cells(argc, argv);
         else if (mode == "overlap") rc = overlap(argc, argv);
         else if (mode == "coords") rc = coords();
+        else if (mode == "copy") rc = copy();
     }
     MPI_Finalize();
     return rc;

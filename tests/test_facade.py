@@ -259,3 +259,14 @@ def test_facade_coordinate_lookups(ranks):
     refinement) and get_remote_neighbors_to against the neighbor lists."""
     out = run("coords", ranks=ranks)
     assert out.count("coords ok") == ranks, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_facade_converting_copy(ranks):
+    """tests/constructors/copy.cpp: a grid copied into another cell type (and
+    then another geometry) has the original's cells, owners, neighbor lists,
+    user neighborhoods and weights, default data, and its own working remote
+    neighbor updates."""
+    out = run("copy", ranks=ranks)
+    assert out.count("copy ok") == ranks, out
