@@ -23,6 +23,7 @@
 //   cells ...        get_cells criteria and process-boundary accessors
 //   coords           geometry lookups, refinement at a coordinate, no-LB calls
 //   copy             the converting copy constructor (tests/constructors/copy.cpp)
+//   varneigh [LX LY] variable-size cell data in halos (variable_neighbour_data.cpp)
 // Built with the reference's own flags (-std=c++11, Makefile:8) by the tests.
 #include <cmath>
 #include <cstdio>
@@ -524,6 +525,79 @@ static int copy()
     return 0;
 }
 
+// tests/variable_data_size/variable_neighbour_data.cpp's cell: two vectors,
+// the first alone or both through a struct type of their addresses
+static bool send_variables2 = false;
+struct var_cell {
+    std::vector<int> variables1, variables2;
+    std::tuple<void*, int, MPI_Datatype> get_mpi_datatype()
+    {
+        if (!send_variables2) return std::make_tuple((void*)variables1.data(), int(variables1.size()), MPI_INT);
+        int counts[2] = {int(variables1.size()), int(variables2.size())};
+        MPI_Aint displacements[2] = {0, (uint8_t*)variables2.data() - (uint8_t*)variables1.data()};
+        MPI_Datatype types[2] = {MPI_INT, MPI_INT}, t = MPI_DATATYPE_NULL;
+        if (MPI_Type_create_struct(2, counts, displacements, types, &t) != MPI_SUCCESS)
+            return std::make_tuple((void*)variables1.data(), 0, MPI_BYTE);
+        return std::make_tuple((void*)variables1.data(), 1, t);
+    }
+};
+
+// variable_neighbour_data.cpp:82-130 (its load-balancing half is out of
+// scope): cell c holds c values c+i and -(c+i); receivers size the remote
+// copies first; then the sizes change (2c) and only the first vector goes
+static int varneigh(int argc, char** argv)
+{
+    int rank = 0;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    const uint64_t lx = argc > 2 ? strtoull(argv[2], 0, 10) : 3, ly = argc > 3 ? strtoull(argv[3], 0, 10) : 1;
+    dccrg::Dccrg<var_cell> grid;
+    grid.set_initial_length({lx, ly, 1}).set_neighborhood_length(1).set_maximum_refinement_level(0).initialize(
+        MPI_COMM_WORLD);
+    grid.allocate_copies_of_remote_neighbors();
+    for (const auto& cell : grid.local_cells())
+        for (uint64_t i = 0; i < cell.id; i++) {
+            cell.data->variables1.push_back(int(cell.id + i));
+            cell.data->variables2.push_back(-int(cell.id + i));
+        }
+    for (uint64_t c : grid.get_remote_cells_on_process_boundary()) {
+        auto* d = grid[c];
+        if (d == nullptr) abort();
+        d->variables1.resize(c);
+        d->variables2.resize(c);
+    }
+    send_variables2 = true;
+    grid.update_copies_of_remote_neighbors();
+    size_t checked = 0;
+    for (const auto& cell : grid.local_cells())
+        for (const auto& n : cell.neighbors_of) {
+            if (n.data->variables1.size() != n.id || n.data->variables2.size() != n.id) abort();
+            for (uint64_t i = 0; i < n.id; i++)
+                if (n.data->variables1[i] != int(n.id + i) || n.data->variables2[i] != -int(n.id + i)) {
+                    std::fprintf(stderr, "FAIL cell %llu neighbor %llu value %llu\n", (unsigned long long)cell.id,
+                                 (unsigned long long)n.id, (unsigned long long)i);
+                    abort();
+                }
+            checked++;
+        }
+    // new sizes; the first vector alone
+    for (const auto& cell : grid.local_cells()) {
+        cell.data->variables1.assign(2 * cell.id, 0);
+        for (uint64_t i = 0; i < 2 * cell.id; i++) cell.data->variables1[i] = int(3 * cell.id + i);
+    }
+    for (uint64_t c : grid.get_remote_cells_on_process_boundary()) grid[c]->variables1.resize(2 * c);
+    send_variables2 = false;
+    grid.update_copies_of_remote_neighbors();
+    for (const auto& cell : grid.local_cells())
+        for (const auto& n : cell.neighbors_of) {
+            if (n.data->variables1.size() != 2 * n.id) abort();
+            for (uint64_t i = 0; i < 2 * n.id; i++)
+                if (n.data->variables1[i] != int(3 * n.id + i)) abort();
+            if (!grid.is_local(n.id) && n.data->variables2[0] != -int(n.id)) abort();  // untouched
+        }
+    std::printf("varneigh ok rank %d neighbors %zu\n", rank, checked);
+    return 0;
+}
+
 static void live_neighbor_counts(const dccrg::Dccrg<game_of_life_cell>::Iterator_Storage<
                                      dccrg::Dccrg<game_of_life_cell>::Cells_Item>& cells)
 {
@@ -605,6 +679,7 @@ int main(int argc, char** argv)
         else if (mode == "overlap") rc = overlap(argc, argv);
         else if (mode == "coords") rc = coords();
         else if (mode == "copy") rc = copy();
+        else if (mode == "varneigh") rc = varneigh(argc, argv);
     }
     MPI_Finalize();
     return rc;

@@ -270,3 +270,15 @@ def test_facade_converting_copy(ranks):
     neighbor updates."""
     out = run("copy", ranks=ranks)
     assert out.count("copy ok") == ranks, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,shape", [(1, (3, 1)), (3, (3, 1)), (3, (7, 5))])
+def test_facade_variable_neighbour_data(ranks, shape):
+    """tests/variable_data_size/variable_neighbour_data.cpp:82-130 through the
+    facade: per-cell vectors whose datatype is a struct of two addresses,
+    remote copies sized by the receiver, then new sizes and one vector."""
+    out = run("varneigh", *shape, ranks=ranks)
+    assert out.count("varneigh ok") == ranks, out
+    if ranks == 3 and shape == (3, 1):  # one cell per rank: every neighbor is remote
+        assert sum(int(l.split()[-1]) for l in out.splitlines() if "varneigh ok" in l) == 4
