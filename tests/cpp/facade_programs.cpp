@@ -24,11 +24,13 @@
 //   coords           geometry lookups, refinement at a coordinate, no-LB calls
 //   copy             the converting copy constructor (tests/constructors/copy.cpp)
 //   varneigh [LX LY] variable-size cell data in halos (variable_neighbour_data.cpp)
+//   interlaced       user_neighborhood/game_of_life.cpp (4 games, hood of +-2)
 // Built with the reference's own flags (-std=c++11, Makefile:8) by the tests.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <set>
 #include <string>
 
 #include "dccrg_amd.hpp"
@@ -598,6 +600,83 @@ static int varneigh(int argc, char** argv)
     return 0;
 }
 
+// tests/user_neighborhood/game_of_life.cpp's known answer: the live cells of
+// its four interlaced games (toad, blinker, beehive, beacon, block and a
+// glider moving (2, -2) every 4 steps) on the 18 x 18 grid at a step that is
+// a multiple of 4
+static std::set<uint64_t> interlaced_live(int64_t gs, int step)
+{
+    std::set<uint64_t> r;
+    const int64_t toad = 12 * gs + 6, blinker = 14 * gs + 1, hive = 10 * gs + 7, beacon = 15 * gs + 6,
+                  block = 5 * gs + 2;
+    for (int64_t v : {toad, toad + 2, toad + 4, toad + 2 + 2 * gs, toad + 4 + 2 * gs, toad + 6 + 2 * gs, blinker,
+                      blinker + 2, blinker + 4, hive + 2, hive + 4, hive - 2 * gs, hive - 2 * gs + 6,
+                      hive - 4 * gs + 2, hive - 4 * gs + 4, beacon, beacon + 2, beacon - 2 * gs, beacon + 6 - 4 * gs,
+                      beacon + 4 - 6 * gs, beacon + 6 - 6 * gs, block, block + 2, block - 2 * gs, block + 2 - 2 * gs})
+        r.insert(uint64_t(v));
+    const int64_t k = step / 4;
+    const int64_t glider[5][2] = {{3, 15}, {5, 13}, {1, 11}, {3, 11}, {5, 11}};
+    for (const auto& g : glider) {
+        const int64_t x = (g[0] + 2 * k) % gs, y = ((g[1] - 2 * k) % gs + gs) % gs;
+        r.insert(uint64_t(y * gs + x));
+    }
+    return r;
+}
+
+// tests/user_neighborhood/game_of_life.cpp: a periodic 18 x 18 game over the
+// user neighborhood {-2, 0, 2}^2 \ {0} (hood length 2), iterated with
+// local_cells(hood) and updated with update_copies_of_remote_neighbors(hood);
+// the live cells every 4 steps are the known answer above
+static int interlaced()
+{
+    int rank = 0;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    const uint64_t gs = 18;
+    dccrg::Dccrg<std::array<int, 2>> grid;
+    grid.set_initial_length({gs, gs, 1})
+        .set_neighborhood_length(2)
+        .set_maximum_refinement_level(0)
+        .set_periodic(true, true, true)
+        .set_load_balancing_method("RANDOM")
+        .initialize(MPI_COMM_WORLD);
+    const std::vector<dccrg::Types<3>::neighborhood_item_t> hood{{{-2, -2, 0}}, {{-2, 0, 0}}, {{-2, 2, 0}},
+                                                                 {{0, -2, 0}},  {{0, 2, 0}},  {{2, -2, 0}},
+                                                                 {{2, 0, 0}},   {{2, 2, 0}}};
+    const int hood_id = 1;
+    if (!grid.add_neighborhood(hood_id, hood)) abort();
+    for (uint64_t c : interlaced_live(gs, 0)) {
+        auto* d = grid[c];
+        if (d != nullptr) (*d)[0] = 1;
+    }
+    size_t checked = 0;
+    for (int step = 0; step < 36; step++) {
+        grid.balance_load();
+        grid.update_copies_of_remote_neighbors(hood_id);
+        if (step % 4 == 0) {
+            const auto live = interlaced_live(gs, step);
+            for (const auto& cell : grid.local_cells(hood_id)) {
+                if (((*cell.data)[0] != 0) != (live.count(cell.id) > 0)) {
+                    std::fprintf(stderr, "FAIL cell %llu step %d alive %d\n", (unsigned long long)cell.id, step,
+                                 (*cell.data)[0]);
+                    abort();
+                }
+                checked++;
+            }
+        }
+        for (const auto& cell : grid.local_cells(hood_id)) {
+            (*cell.data)[1] = 0;
+            for (const auto& n : cell.neighbors_of)
+                if ((*n.data)[0] == 1) (*cell.data)[1]++;
+        }
+        for (const auto& cell : grid.local_cells(hood_id)) {
+            if ((*cell.data)[1] == 3) (*cell.data)[0] = 1;
+            else if ((*cell.data)[1] != 2) (*cell.data)[0] = 0;
+        }
+    }
+    std::printf("interlaced ok rank %d checked %zu\n", rank, checked);
+    return 0;
+}
+
 static void live_neighbor_counts(const dccrg::Dccrg<game_of_life_cell>::Iterator_Storage<
                                      dccrg::Dccrg<game_of_life_cell>::Cells_Item>& cells)
 {
@@ -680,6 +759,7 @@ int main(int argc, char** argv)
         else if (mode == "coords") rc = coords();
         else if (mode == "copy") rc = copy();
         else if (mode == "varneigh") rc = varneigh(argc, argv);
+        else if (mode == "interlaced") rc = interlaced();
     }
     MPI_Finalize();
     return rc;

@@ -282,3 +282,45 @@ def test_facade_variable_neighbour_data(ranks, shape):
     assert out.count("varneigh ok") == ranks, out
     if ranks == 3 and shape == (3, 1):  # one cell per rank: every neighbor is remote
         assert sum(int(l.split()[-1]) for l in out.splitlines() if "varneigh ok" in l) == 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_facade_user_neighborhood_game_of_life(ranks):
+    """tests/user_neighborhood/game_of_life.cpp: four interlaced games over
+    the user neighborhood {-2, 0, 2}^2 minus the origin (hood length 2,
+    periodic 18 x 18), updated and iterated per neighborhood; the live cells
+    every 4 steps are the test's known answer (glider included)."""
+    out = run("interlaced", ranks=ranks)
+    lines = [l for l in out.splitlines() if "interlaced ok" in l]
+    assert len(lines) == ranks, out
+    assert sum(int(l.split()[-1]) for l in lines) == 9 * 18 * 18  # steps 0, 4, ..., 32
+
+
+def interlaced_live(gs, step):
+    """The live cells of user_neighborhood/game_of_life.cpp's known answer at
+    a step divisible by 4 (as tests/cpp/facade_programs.cpp states it)."""
+    t, b, h, c, k = 12 * gs + 6, 14 * gs + 1, 10 * gs + 7, 15 * gs + 6, 5 * gs + 2
+    r = {t, t + 2, t + 4, t + 2 + 2 * gs, t + 4 + 2 * gs, t + 6 + 2 * gs, b, b + 2, b + 4,
+         h + 2, h + 4, h - 2 * gs, h - 2 * gs + 6, h - 4 * gs + 2, h - 4 * gs + 4,
+         c, c + 2, c - 2 * gs, c + 6 - 4 * gs, c + 4 - 6 * gs, c + 6 - 6 * gs, k, k + 2, k - 2 * gs, k + 2 - 2 * gs}
+    q = step // 4
+    for x, y in [(3, 15), (5, 13), (1, 11), (3, 11), (5, 11)]:
+        r.add(((y - 2 * q) % gs) * gs + (x + 2 * q) % gs)
+    return r
+
+
+def test_interlaced_known_answer():
+    """The known answer the GPU facade test checks against, pinned by an
+    independent numpy run of the same game (periodic rolls over the +-2
+    neighborhood)."""
+    gs = 18
+    a = np.zeros((gs, gs), dtype=np.int64)  # [y, x]; id = y * gs + x + 1
+    for cid in interlaced_live(gs, 0):
+        a[(cid - 1) // gs, (cid - 1) % gs] = 1
+    for step in range(36):
+        if step % 4 == 0:
+            ys, xs = np.nonzero(a)
+            assert {int(y * gs + x + 1) for y, x in zip(ys, xs)} == interlaced_live(gs, step), step
+        n = sum(np.roll(np.roll(a, dy, 0), dx, 1) for dy in (-2, 0, 2) for dx in (-2, 0, 2) if dy or dx)
+        a = np.where(n == 3, 1, np.where(n == 2, a, 0))
