@@ -395,12 +395,96 @@ private:
     int max_lvl_ = 0;
 };
 
-struct No_Geometry {  // dccrg_no_geometry.hpp (nothing on the hot path)
+// dccrg_no_geometry.hpp: level-0 cells of unit length from the origin; its
+// parameters are a dummy integer (:104-131)
+struct No_Geometry {
     static const int geometry_id = 0;
-    struct Parameters {};
-    explicit No_Geometry(const Mapping* = nullptr, const Grid_Topology* = nullptr) {}
+    typedef int Parameters;
+    explicit No_Geometry(const Mapping* m = nullptr, const Grid_Topology* t = nullptr) : mapping_(m), topology_(t) {}
     bool set(const Parameters&) { return true; }
-    Parameters get() const { return Parameters(); }
+    bool set(const No_Geometry&) { return true; }
+    const Parameters& get() const { return par_; }
+    std::array<double, 3> get_start() const { return {{0, 0, 0}}; }
+    std::array<double, 3> get_end() const  // :155-168: the level-0 lengths
+    {
+        const auto& l = mapping_->length.get();
+        return {{double(l[0]), double(l[1]), double(l[2])}};
+    }
+    std::array<double, 3> get_level_0_cell_length() const { return {{1, 1, 1}}; }
+    // :183-206 (NaN for error_cell or an invalid cell)
+    std::array<double, 3> get_length(uint64_t cell) const
+    {
+        const int l = mapping_->get_refinement_level(cell);
+        if (cell == error_cell || l < 0 || l > mapping_->get_maximum_refinement_level()) return nan3();
+        const double len = 1.0 / double(uint64_t(1) << l);
+        return {{len, len, len}};
+    }
+    // :217-255: index / 2^max + length / 2
+    std::array<double, 3> get_center(uint64_t cell) const
+    {
+        const int l = mapping_->get_refinement_level(cell);
+        if (cell == error_cell || l < 0 || l > mapping_->get_maximum_refinement_level()) return nan3();
+        const auto idx = mapping_->get_indices(cell);
+        const auto len = get_length(cell);
+        const double top = double(uint64_t(1) << mapping_->get_maximum_refinement_level());
+        std::array<double, 3> c;
+        for (int d = 0; d < 3; d++) c[d] = double(idx[d]) / top + len[d] / 2;
+        return c;
+    }
+    std::array<double, 3> get_min(uint64_t cell) const  // :266-281
+    {
+        const auto c = get_center(cell), len = get_length(cell);
+        return {{c[0] - len[0] / 2, c[1] - len[1] / 2, c[2] - len[2] / 2}};
+    }
+    std::array<double, 3> get_max(uint64_t cell) const  // :292-307
+    {
+        const auto c = get_center(cell), len = get_length(cell);
+        return {{c[0] + len[0] / 2, c[1] + len[1] / 2, c[2] + len[2] / 2}};
+    }
+    // :313-360: the center of a cell of a level at maximum-level indices (an
+    // index may equal the grid's end, as there)
+    std::array<double, 3> get_center(int level, const Types<3>::indices_t& index) const
+    {
+        const int top_lvl = mapping_->get_maximum_refinement_level();
+        if (level < 0 || level > top_lvl) return nan3();
+        const uint64_t scale = uint64_t(1) << top_lvl;
+        const auto& l = mapping_->length.get();
+        for (int d = 0; d < 3; d++)
+            if (index[d] > l[d] * scale) return nan3();
+        const double half = 1.0 / double(uint64_t(1) << level) / 2;
+        std::array<double, 3> c;
+        for (int d = 0; d < 3; d++) c[d] = double(index[d]) / double(scale) + half;
+        return c;
+    }
+    // :397-431: inside, its periodic image, or NaN
+    std::array<double, 3> get_real_coordinate(const std::array<double, 3>& c) const
+    {
+        const std::array<double, 3> end = get_end();
+        std::array<double, 3> r = nan3();
+        for (int d = 0; d < 3; d++) {
+            if (c[d] >= 0.0 && c[d] <= end[d]) {
+                r[d] = c[d];
+            } else if (topology_ && topology_->is_periodic(d)) {
+                if (c[d] < 0.0) r[d] = c[d] + end[d] * std::ceil(-c[d] / end[d]);
+                else r[d] = c[d] - end[d] * std::ceil((c[d] - end[d]) / end[d]);
+            }
+        }
+        return r;
+    }
+    // :434-454: the floor of the (real) coordinate itself, error_index outside
+    Types<3>::indices_t get_indices(const std::array<double, 3>& given) const
+    {
+        Types<3>::indices_t r{{error_index, error_index, error_index}};
+        const std::array<double, 3> end = get_end(), c = get_real_coordinate(given);
+        for (int d = 0; d < 3; d++)
+            if (c[d] >= 0.0 && c[d] <= end[d]) r[d] = uint64_t(std::floor(c[d]));
+        return r;
+    }
+    uint64_t get_cell(int level, const std::array<double, 3>& c) const  // :371-386
+    {
+        if (level < 0 || level > mapping_->get_maximum_refinement_level()) return error_cell;
+        return mapping_->get_cell_from_indices(get_indices(c), level);
+    }
     bool read_file_data(const std::vector<char>& b) const
     {
         int id = -1;
@@ -416,6 +500,16 @@ struct No_Geometry {  // dccrg_no_geometry.hpp (nothing on the hot path)
         std::memcpy(b.data(), &id, 4);
         return b;
     }
+
+private:
+    static std::array<double, 3> nan3()
+    {
+        const double q = std::numeric_limits<double>::quiet_NaN();
+        return {{q, q, q}};
+    }
+    const Mapping* mapping_;
+    const Grid_Topology* topology_;
+    Parameters par_ = 0;
 };
 
 // dccrg_cartesian_geometry.hpp:51-812: level-0 cells of the same size from a
@@ -588,6 +682,34 @@ public:
     Mapping mapping;
     Grid_Topology topology;
     Geometry geometry{&mapping, &topology};
+
+    // dccrg.hpp:7547 (const std::vector<Cells_Item>& cells): every cell of the
+    // default neighborhood's iteration cache, local then copies of remote
+    // ones; a read-only view here, since the cache is rebuilt in place
+    class Cells_View {
+    public:
+        typedef typename std::vector<Cells_Item>::const_iterator const_iterator;
+        explicit Cells_View(const Dccrg* g) : g_(g) {}
+        const std::vector<Cells_Item>& get() const
+        {
+            static const std::vector<Cells_Item> none;
+            const auto it = g_->hoods_.find(default_neighborhood_id);
+            return it == g_->hoods_.end() ? none : it->second.cells;
+        }
+        operator const std::vector<Cells_Item>&() const { return get(); }
+        const_iterator begin() const { return get().begin(); }
+        const_iterator end() const { return get().end(); }
+        const_iterator cbegin() const { return get().begin(); }
+        const_iterator cend() const { return get().end(); }
+        size_t size() const { return get().size(); }
+        bool empty() const { return get().empty(); }
+        const Cells_Item& operator[](size_t i) const { return get()[i]; }
+        const Cells_Item& at(size_t i) const { return get().at(i); }
+
+    private:
+        const Dccrg* g_;
+    };
+    const Cells_View cells{this};
 
     Dccrg() = default;
     Dccrg(const Dccrg&) = delete;

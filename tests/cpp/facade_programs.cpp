@@ -25,6 +25,7 @@
 //   copy             the converting copy constructor (tests/constructors/copy.cpp)
 //   varneigh [LX LY] variable-size cell data in halos (variable_neighbour_data.cpp)
 //   interlaced       user_neighborhood/game_of_life.cpp (4 games, hood of +-2)
+//   items            additional_cell_data/*.cpp (items, grid.cells, No_Geometry)
 // Built with the reference's own flags (-std=c++11, Makefile:8) by the tests.
 #include <cmath>
 #include <cstdio>
@@ -677,6 +678,165 @@ static int interlaced()
     return 0;
 }
 
+// tests/additional_cell_data/{test1,test2,neighbor_data1,neighbor_data2}.cpp:
+// a cell with no data, additional cell / neighbor items with defaults or
+// filled in by update() (ids, No_Geometry centers), seen through grid.cells,
+// local_cells() and neighbors_of, again after balance_load
+struct empty_cell {
+    std::tuple<void*, int, MPI_Datatype> get_mpi_datatype() { return std::make_tuple((void*)this, 0, MPI_BYTE); }
+};
+struct aci_defaults_1 {
+    int additional_cell_data1 = 1;
+    double additional_cell_data2 = 3.125;
+    template <class Grid, class Cell> void update(const Grid&, const Cell&, const aci_defaults_1&) {}
+};
+struct aci_defaults_2 {
+    std::tuple<int, float> additional_cell_data3{2, 3.0625f};
+    unsigned int additional_cell_data4 = 4;
+    template <class Grid, class Cell> void update(const Grid&, const Cell&, const aci_defaults_2&) {}
+};
+struct aci_id {
+    uint64_t additional_cell_data1 = dccrg::error_cell;
+    template <class Grid, class Cell> void update(const Grid&, const Cell& cell, const aci_id&)
+    {
+        additional_cell_data1 = cell.id;
+    }
+};
+struct aci_center {
+    double d1 = 0, d2 = 0, d3 = 0;
+    uint64_t additional_cell_data4 = dccrg::error_cell;
+    template <class Grid, class Cell> void update(const Grid& grid, const Cell& cell, const aci_center&)
+    {
+        additional_cell_data4 = cell.id;
+        const auto c = grid.geometry.get_center(cell.id);
+        d1 = c[0];
+        d2 = c[1];
+        d3 = c[2];
+    }
+};
+struct ani_defaults {
+    int additional_neighbor_data1 = 1;
+    double additional_neighbor_data2 = 3.125;
+    template <class Grid, class C, class N> void update(const Grid&, const C&, const N&, const int&, const ani_defaults&)
+    {
+    }
+};
+struct ani_ids {
+    uint64_t additional_neighbor_data1 = dccrg::error_cell, additional_neighbor_data2 = dccrg::error_cell;
+    template <class Grid, class C, class N>
+    void update(const Grid&, const C& cell, const N& neighbor, const int&, const ani_ids&)
+    {
+        additional_neighbor_data1 = neighbor.id;
+        additional_neighbor_data2 = cell.id;
+    }
+};
+
+template <class G> static void setup_items_grid(G& grid)
+{
+    grid.set_initial_length({2, 2, 2})
+        .set_neighborhood_length(3)
+        .set_maximum_refinement_level(-1)
+        .set_load_balancing_method("RANDOM")
+        .initialize(MPI_COMM_WORLD);
+}
+
+static int items()
+{
+    int rank = 0, size = 1;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &size);
+    auto want = [](bool ok, const char* what) {
+        if (!ok) {
+            std::fprintf(stderr, "FAIL %s\n", what);
+            abort();
+        }
+    };
+    {  // test1.cpp
+        dccrg::Dccrg<empty_cell, dccrg::No_Geometry, std::tuple<aci_defaults_1, aci_defaults_2>> grid;
+        setup_items_grid(grid);
+        want(grid.cells.size() == size_t(std::distance(grid.all_cells().begin(), grid.all_cells().end())) &&
+                 grid.cells.size() >= grid.get_cells().size(),
+             "cells: local and remote copies");
+        for (const auto& cell : grid.cells)
+            want(cell.additional_cell_data1 == 1 && cell.additional_cell_data2 == 3.125 &&
+                     std::get<0>(cell.additional_cell_data3) == 2 &&
+                     std::get<1>(cell.additional_cell_data3) == 3.0625f && cell.additional_cell_data4 == 4,
+                 "default cell items");
+        // No_Geometry (dccrg_no_geometry.hpp): unit level-0 cells from the origin
+        const int top = grid.mapping.get_maximum_refinement_level();
+        want(top == grid.mapping.get_maximum_possible_refinement_level(), "maximum level -1: the largest possible");
+        const auto& g = grid.geometry;
+        want(g.get_end() == (std::array<double, 3>{{2, 2, 2}}) && g.get_start() == (std::array<double, 3>{{0, 0, 0}}),
+             "no geometry corners");
+        want(g.get_center(8) == (std::array<double, 3>{{1.5, 1.5, 1.5}}) &&
+                 g.get_length(8) == (std::array<double, 3>{{1, 1, 1}}) &&
+                 g.get_min(2) == (std::array<double, 3>{{1, 0, 0}}),
+             "no geometry level-0 cells");
+        const uint64_t child = grid.mapping.get_cell_from_indices({{0, 0, 0}}, 1);
+        want(g.get_center(child) == (std::array<double, 3>{{0.25, 0.25, 0.25}}) &&
+                 g.get_max(child) == (std::array<double, 3>{{0.5, 0.5, 0.5}}),
+             "no geometry level-1 cell");
+        want(std::isnan(g.get_center(dccrg::error_cell)[0]) && std::isnan(g.get_length(0)[1]), "no geometry errors");
+        want(std::isnan(g.get_real_coordinate({{-0.5, 1, 1}})[0]) && g.get_real_coordinate({{-0.5, 1, 1}})[1] == 1,
+             "no geometry outside a non-periodic dimension");
+        want(g.get_indices({{1.5, 0.25, 2.0}}) == (dccrg::Types<3>::indices_t{{1, 0, 2}}) &&
+                 g.get_indices({{2.5, 0, 0}})[0] == dccrg::error_index,
+             "no geometry indices (the floor of the coordinate)");
+        want(g.get_cell(0, {{0.5, 0.5, 0.5}}) == 1 && g.get_cell(top + 1, {{0.5, 0.5, 0.5}}) == dccrg::error_cell,
+             "no geometry get_cell");
+        const auto cc = g.get_center(0, {{uint64_t(1) << top, 0, 0}});
+        want(cc[0] == 1.5 && cc[1] == 0.5 && std::isnan(g.get_center(0, {{uint64_t(3) << top, 0, 0}})[0]),
+             "no geometry center at indices");
+    }
+    {  // test2.cpp
+        dccrg::Dccrg<empty_cell, dccrg::No_Geometry, std::tuple<aci_id, aci_center>> grid;
+        setup_items_grid(grid);
+        auto check = [&](const char* what) {
+            for (const auto& cell : grid.cells) {
+                const auto c = grid.geometry.get_center(cell.id);
+                want(cell.additional_cell_data1 == cell.id && cell.additional_cell_data4 == cell.id &&
+                         cell.d1 == c[0] && cell.d2 == c[1] && cell.d3 == c[2],
+                     what);
+            }
+        };
+        check("updated cell items");
+        for (auto& cell : grid.cells) {
+            const_cast<uint64_t&>(cell.additional_cell_data1) = dccrg::error_cell;
+            const_cast<uint64_t&>(cell.additional_cell_data4) = dccrg::error_cell;
+            const_cast<double&>(cell.d1) -= 3;
+        }
+        grid.balance_load();
+        check("cell items updated again by balance_load");
+    }
+    {  // neighbor_data1.cpp
+        dccrg::Dccrg<empty_cell, dccrg::No_Geometry, std::tuple<>, std::tuple<ani_defaults>> grid;
+        setup_items_grid(grid);
+        size_t n = 0;
+        for (const auto& cell : grid.local_cells())
+            for (const auto& neighbor : cell.neighbors_of) {
+                want(neighbor.additional_neighbor_data1 == 1 && neighbor.additional_neighbor_data2 == 3.125,
+                     "default neighbor items");
+                n++;
+            }
+        want(n == 7 * grid.get_cells().size(), "every other cell is a neighbor (hood 3 on 2x2x2)");
+    }
+    {  // neighbor_data2.cpp
+        dccrg::Dccrg<empty_cell, dccrg::No_Geometry, std::tuple<>, std::tuple<ani_ids>> grid;
+        setup_items_grid(grid);
+        for (int round = 0; round < 2; round++) {
+            for (const auto& cell : grid.local_cells())
+                for (const auto& neighbor : cell.neighbors_of)
+                    want(neighbor.additional_neighbor_data1 == neighbor.id &&
+                             neighbor.additional_neighbor_data2 == cell.id,
+                         "updated neighbor items");
+            grid.balance_load();
+        }
+        grid.update_copies_of_remote_neighbors();  // zero-byte cells
+    }
+    std::printf("items ok rank %d of %d\n", rank, size);
+    return 0;
+}
+
 static void live_neighbor_counts(const dccrg::Dccrg<game_of_life_cell>::Iterator_Storage<
                                      dccrg::Dccrg<game_of_life_cell>::Cells_Item>& cells)
 {
@@ -760,6 +920,7 @@ int main(int argc, char** argv)
         else if (mode == "copy") rc = copy();
         else if (mode == "varneigh") rc = varneigh(argc, argv);
         else if (mode == "interlaced") rc = interlaced();
+        else if (mode == "items") rc = items();
     }
     MPI_Finalize();
     return rc;

@@ -324,3 +324,15 @@ def test_interlaced_known_answer():
             assert {int(y * gs + x + 1) for y, x in zip(ys, xs)} == interlaced_live(gs, step), step
         n = sum(np.roll(np.roll(a, dy, 0), dx, 1) for dy in (-2, 0, 2) for dx in (-2, 0, 2) if dy or dx)
         a = np.where(n == 3, 1, np.where(n == 2, a, 0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_facade_additional_items_and_no_geometry(ranks):
+    """tests/additional_cell_data/{test1,test2,neighbor_data1,neighbor_data2}.cpp:
+    additional cell / neighbor items with defaults or filled in by update()
+    (ids, No_Geometry centers), through grid.cells, local_cells() and
+    neighbors_of, again after balance_load; zero-byte cells; No_Geometry's
+    arithmetic (dccrg_no_geometry.hpp)."""
+    out = run("items", ranks=ranks)
+    assert out.count("items ok") == ranks, out
