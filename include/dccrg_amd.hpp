@@ -1698,7 +1698,7 @@ private:
         const auto inner = query_cells(hood, DCCRGX_CELLS_INNER);
         const auto outer = query_cells(hood, DCCRGX_CELLS_OUTER);
         S.remote_ids = query_cells(hood, DCCRGX_CELLS_REMOTE);
-        for (uint64_t c : S.remote_ids) remote_data_.emplace(c, Cell_Data{});  // :7153-7184
+        for (uint64_t c : S.remote_ids) remote_data_[c];  // :7153-7184, constructed in place
         std::vector<uint64_t> order;
         order.insert(order.end(), inner.begin(), inner.end());
         order.insert(order.end(), outer.begin(), outer.end());

@@ -26,6 +26,7 @@
 //   varneigh [LX LY] variable-size cell data in halos (variable_neighbour_data.cpp)
 //   interlaced       user_neighborhood/game_of_life.cpp (4 games, hood of +-2)
 //   items            additional_cell_data/*.cpp (items, grid.cells, No_Geometry)
+//   nocopy           constructors/simple.cpp (cell data never copied or moved)
 // Built with the reference's own flags (-std=c++11, Makefile:8) by the tests.
 #include <cmath>
 #include <cstdio>
@@ -837,6 +838,43 @@ static int items()
     return 0;
 }
 
+// tests/constructors/simple.cpp: cell data is constructed in place, never
+// copied, moved or assigned (each of those throws here), through
+// initialization, remote copies, halo updates and rebuilt caches
+struct no_copy_cell {
+    double data = 0;
+    no_copy_cell() = default;
+    no_copy_cell(const no_copy_cell&) { throw std::runtime_error("cell copied"); }
+    no_copy_cell(no_copy_cell&&) { throw std::runtime_error("cell moved"); }
+    no_copy_cell& operator=(const no_copy_cell&) { throw std::runtime_error("cell assigned"); }
+    no_copy_cell& operator=(no_copy_cell&&) { throw std::runtime_error("cell move-assigned"); }
+    std::tuple<void*, int, MPI_Datatype> get_mpi_datatype() { return std::make_tuple((void*)&data, 1, MPI_DOUBLE); }
+};
+
+static int nocopy()
+{
+    int rank = 0;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    {
+        dccrg::Dccrg<no_copy_cell> grid;
+        grid.set_initial_length({1, 1, 1}).set_neighborhood_length(1).set_maximum_refinement_level(0).initialize(
+            MPI_COMM_WORLD);
+        for (const auto& cell : grid.local_cells()) cell.data->data = 1;
+    }
+    dccrg::Dccrg<no_copy_cell> grid;
+    grid.set_initial_length({6, 4, 1}).set_neighborhood_length(1).set_maximum_refinement_level(1).initialize(
+        MPI_COMM_WORLD);
+    for (const auto& cell : grid.local_cells()) cell.data->data = double(cell.id);
+    grid.update_copies_of_remote_neighbors();
+    grid.balance_load();
+    for (const auto& cell : grid.local_cells())
+        for (const auto& n : cell.neighbors_of)
+            if (n.data->data != double(n.id)) abort();
+    grid.update_copies_of_remote_neighbors();  // refinement moves data aside (the reference copies it)
+    std::printf("nocopy ok rank %d cells %zu\n", rank, grid.get_cells().size());
+    return 0;
+}
+
 static void live_neighbor_counts(const dccrg::Dccrg<game_of_life_cell>::Iterator_Storage<
                                      dccrg::Dccrg<game_of_life_cell>::Cells_Item>& cells)
 {
@@ -921,6 +959,7 @@ int main(int argc, char** argv)
         else if (mode == "varneigh") rc = varneigh(argc, argv);
         else if (mode == "interlaced") rc = interlaced();
         else if (mode == "items") rc = items();
+        else if (mode == "nocopy") rc = nocopy();
     }
     MPI_Finalize();
     return rc;

@@ -336,3 +336,13 @@ def test_facade_additional_items_and_no_geometry(ranks):
     arithmetic (dccrg_no_geometry.hpp)."""
     out = run("items", ranks=ranks)
     assert out.count("items ok") == ranks, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_facade_cell_data_never_copied(ranks):
+    """tests/constructors/simple.cpp: a cell type whose copy / move
+    constructors and assignments throw survives initialization, remote copies,
+    halo updates and balance_load."""
+    out = run("nocopy", ranks=ranks)
+    assert out.count("nocopy ok") == ranks, out
