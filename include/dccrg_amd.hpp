@@ -1367,6 +1367,33 @@ public:
     {
         return hoods_.count(hood) ? hs(hood).remote_ids : std::vector<uint64_t>();
     }
+    // dccrg.hpp:6953-6975: the owner of every cell of the grid (built when
+    // called, from the replicated leaf set: as large as the grid) and the
+    // default neighborhood's boundary cells as sets
+    const std::unordered_map<uint64_t, uint64_t>& get_cell_process() const
+    {
+        const std::vector<uint64_t> all = get_all_cells();
+        std::vector<int32_t> owner(all.size());
+        if (!all.empty()) detail::check(dccrgx_get_process(grid_, all.data(), all.size(), owner.data()), "get_process");
+        cell_process_.clear();
+        cell_process_.reserve(all.size());
+        for (size_t i = 0; i < all.size(); i++) cell_process_[all[i]] = uint64_t(owner[i]);
+        return cell_process_;
+    }
+    const std::unordered_set<uint64_t>& get_local_cells_on_process_boundary_internal() const
+    {
+        const std::vector<uint64_t> v = get_local_cells_on_process_boundary();
+        local_bdy_ = std::unordered_set<uint64_t>(v.begin(), v.end());
+        return local_bdy_;
+    }
+    const std::unordered_set<uint64_t>& get_remote_cells_on_process_boundary_internal() const
+    {
+        const std::vector<uint64_t> v = get_remote_cells_on_process_boundary();
+        remote_bdy_ = std::unordered_set<uint64_t>(v.begin(), v.end());
+        return remote_bdy_;
+    }
+    bool get_no_load_balancing() const { return true; }  // :7101-7107, as built with DCCRG_NO_LB
+    bool get_balancing_load() const { return false; }    // :7132-7135
 
     // dccrg.hpp:6491-6711
     bool add_neighborhood(int id, const std::vector<Types<3>::neighborhood_item_t>& items)
@@ -1891,6 +1918,8 @@ private:
     std::unordered_map<uint64_t, double> cell_weights_;
     // the user-neighborhood views, refreshed by their accessors
     mutable std::unordered_map<int, std::unordered_set<uint64_t>> user_local_bdy_, user_remote_bdy_;
+    mutable std::unordered_map<uint64_t, uint64_t> cell_process_;
+    mutable std::unordered_set<uint64_t> local_bdy_, remote_bdy_;
     mutable std::unordered_map<int, std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>> user_send_,
         user_recv_;
 };

@@ -446,11 +446,19 @@ struct copy_cell_2 {
     std::tuple<void*, int, MPI_Datatype> get_mpi_datatype() { return std::make_tuple((void*)&data, 1, MPI_DOUBLE); }
 };
 
+// as copy.cpp checks them: the remote boundary set and the cell -> owner map
 template <class G> static void check_remote_copies(const G& grid, double factor, const char* what)
 {
-    for (uint64_t c : grid.get_remote_cells_on_process_boundary()) {
+    const std::unordered_set<uint64_t>& remote = grid.get_remote_cells_on_process_boundary_internal();
+    const std::unordered_map<uint64_t, uint64_t>& cell_process = grid.get_cell_process();
+    if (remote.size() != grid.get_remote_cells_on_process_boundary().size() ||
+        cell_process.size() != grid.get_all_cells().size() ||
+        grid.get_local_cells_on_process_boundary_internal().size() != grid.get_local_cells_on_process_boundary().size())
+        abort();
+    for (uint64_t c : remote) {
         const auto* d = grid[c];
-        if (d == nullptr || double(d->data) != factor * grid.get_process(c)) {
+        if (d == nullptr || double(d->data) != factor * double(cell_process.at(c)) ||
+            int(cell_process.at(c)) != grid.get_process(c)) {
             std::fprintf(stderr, "FAIL %s: cell %llu\n", what, (unsigned long long)c);
             abort();
         }
