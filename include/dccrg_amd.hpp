@@ -45,6 +45,7 @@
 #include <cstring>
 #include <iomanip>
 #include <iterator>
+#include <fstream>
 #include <iostream>
 #include <sstream>
 #include <map>
@@ -1392,6 +1393,44 @@ public:
         remote_bdy_ = std::unordered_set<uint64_t>(v.begin(), v.end());
         return remote_bdy_;
     }
+    // the three-phase balance_load (:3745-4150) as built with DCCRG_NO_LB: no
+    // cell moves, so nothing is added or removed; finishing rebuilds the
+    // iteration caches like balance_load
+    Dccrg& initialize_balance_load(bool = true) { return *this; }
+    Dccrg& continue_balance_load() { return *this; }
+    Dccrg& finish_balance_load() { return balance_load(); }
+    const std::unordered_set<uint64_t>& get_cells_added_by_balance_load() const { return no_cells_; }
+    const std::unordered_set<uint64_t>& get_cells_removed_by_balance_load() const { return no_cells_; }
+    // :3320-3390: an ASCII legacy-VTK unstructured grid of this rank's leaf
+    // cells in ascending id order, 8 corner points per cell (x fastest), each
+    // cell a voxel (type 11)
+    bool write_vtk_file(const std::string& file_name) const
+    {
+        std::ofstream out(file_name);
+        if (!out.is_open()) {
+            std::cerr << "Couldn't open file " << file_name << std::endl;
+            return false;
+        }
+        std::vector<uint64_t> leaves = get_cells();
+        std::sort(leaves.begin(), leaves.end());
+        const size_t n = leaves.size();
+        out << "# vtk DataFile Version 2.0\nCartesian cell refinable grid\nASCII\nDATASET UNSTRUCTURED_GRID\n";
+        out << "POINTS " << n * 8 << " float\n";
+        for (uint64_t c : leaves) {
+            const std::array<double, 3> lo = geometry.get_min(c), hi = geometry.get_max(c);
+            for (int k = 0; k < 8; k++)
+                out << (k & 1 ? hi : lo)[0] << " " << (k & 2 ? hi : lo)[1] << " " << (k & 4 ? hi : lo)[2] << "\n";
+        }
+        out << "CELLS " << n << " " << n * 9 << "\n";
+        for (size_t j = 0; j < n; j++) {
+            out << "8 ";
+            for (size_t i = 0; i < 8; i++) out << j * 8 + i << " ";
+            out << "\n";
+        }
+        out << "CELL_TYPES " << n << "\n";
+        for (size_t i = 0; i < n; i++) out << "11\n";
+        return out.good();
+    }
     bool get_no_load_balancing() const { return true; }  // :7101-7107, as built with DCCRG_NO_LB
     bool get_balancing_load() const { return false; }    // :7132-7135
 
@@ -1920,6 +1959,7 @@ private:
     mutable std::unordered_map<int, std::unordered_set<uint64_t>> user_local_bdy_, user_remote_bdy_;
     mutable std::unordered_map<uint64_t, uint64_t> cell_process_;
     mutable std::unordered_set<uint64_t> local_bdy_, remote_bdy_;
+    const std::unordered_set<uint64_t> no_cells_{};
     mutable std::unordered_map<int, std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>> user_send_,
         user_recv_;
 };

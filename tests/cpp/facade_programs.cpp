@@ -27,6 +27,7 @@
 //   interlaced       user_neighborhood/game_of_life.cpp (4 games, hood of +-2)
 //   items            additional_cell_data/*.cpp (items, grid.cells, No_Geometry)
 //   nocopy           constructors/simple.cpp (cell data never copied or moved)
+//   vtk PREFIX       write_vtk_file of each rank's leaves (PREFIX_<rank>.vtk)
 // Built with the reference's own flags (-std=c++11, Makefile:8) by the tests.
 #include <cmath>
 #include <cstdio>
@@ -883,6 +884,32 @@ static int nocopy()
     return 0;
 }
 
+// dccrg.hpp:3320-3390's write_vtk_file after refinement and the no-LB
+// three-phase balance_load; prints each local leaf's corners for the check
+static int vtk(int argc, char** argv)
+{
+    int rank = 0;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    dccrg::Dccrg<int, dccrg::Cartesian_Geometry> grid;
+    grid.set_initial_length({3, 2, 1}).set_neighborhood_length(1).set_maximum_refinement_level(1).initialize(
+        MPI_COMM_WORLD);
+    if (!grid.set_geometry(dccrg::Cartesian_Geometry::Parameters({{-1, 0, 0}}, {{0.5, 1, 2}}))) abort();
+    if (grid.is_local(2)) grid.refine_completely(2);
+    grid.stop_refining();
+    grid.initialize_balance_load(true);
+    if (!grid.get_cells_added_by_balance_load().empty() || !grid.get_cells_removed_by_balance_load().empty()) abort();
+    grid.continue_balance_load();
+    grid.finish_balance_load();
+    const std::string name = std::string(argc > 2 ? argv[2] : "grid") + "_" + std::to_string(rank) + ".vtk";
+    if (!grid.write_vtk_file(name)) abort();
+    for (uint64_t c : grid.get_cells()) {
+        const auto lo = grid.geometry.get_min(c), hi = grid.geometry.get_max(c);
+        std::printf("leaf %d %llu %.17g %.17g %.17g %.17g %.17g %.17g\n", rank, (unsigned long long)c, lo[0], lo[1],
+                    lo[2], hi[0], hi[1], hi[2]);
+    }
+    return 0;
+}
+
 static void live_neighbor_counts(const dccrg::Dccrg<game_of_life_cell>::Iterator_Storage<
                                      dccrg::Dccrg<game_of_life_cell>::Cells_Item>& cells)
 {
@@ -968,6 +995,7 @@ int main(int argc, char** argv)
         else if (mode == "interlaced") rc = interlaced();
         else if (mode == "items") rc = items();
         else if (mode == "nocopy") rc = nocopy();
+        else if (mode == "vtk") rc = vtk(argc, argv);
     }
     MPI_Finalize();
     return rc;

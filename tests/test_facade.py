@@ -346,3 +346,32 @@ def test_facade_cell_data_never_copied(ranks):
     halo updates and balance_load."""
     out = run("nocopy", ranks=ranks)
     assert out.count("nocopy ok") == ranks, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_facade_write_vtk_file(ranks, tmp_path):
+    """dccrg.hpp:3320-3390: each rank's file lists its leaves in ascending
+    id order, 8 corners per cell (x fastest, C++ default float formatting),
+    9 ints per CELLS line and voxel types; written after a refinement and the
+    no-LB initialize / continue / finish_balance_load sequence."""
+    out = run("vtk", str(tmp_path / "grid"), ranks=ranks)
+    leaves = {}
+    for line in out.splitlines():
+        if line.startswith("leaf "):
+            f = line.split()
+            leaves.setdefault(int(f[1]), []).append((int(f[2]), [float(v) for v in f[3:]]))
+    assert sum(len(v) for v in leaves.values()) == 6 - 1 + 8
+    for r in range(ranks):
+        cells = sorted(leaves.get(r, []))
+        n = len(cells)
+        want = ["# vtk DataFile Version 2.0", "Cartesian cell refinable grid", "ASCII", "DATASET UNSTRUCTURED_GRID",
+                f"POINTS {n * 8} float"]
+        for _, (x0, y0, z0, x1, y1, z1) in cells:
+            for k in range(8):
+                want.append(" ".join("%g" % v for v in (x1 if k & 1 else x0, y1 if k & 2 else y0, z1 if k & 4 else z0)))
+        want.append(f"CELLS {n} {n * 9}")
+        want += ["8 " + "".join(f"{j * 8 + i} " for i in range(8)) for j in range(n)]
+        want.append(f"CELL_TYPES {n}")
+        want += ["11"] * n
+        assert (tmp_path / f"grid_{r}.vtk").read_text().split("\n")[:-1] == want, r
