@@ -83,13 +83,22 @@ def host_cpu():
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
+def profile_key(path: str):
+    """Natural order of profile names by round: r3z < r3z5 < r4a (digits
+    compare as numbers, a name sorts before its extensions)."""
+    import re
+    base = os.path.basename(path).split("_", 1)[0]
+    return [int(t) if t.isdigit() else t for t in re.findall(r"\d+|\D+", base)]
+
+
 def pmc_traffic(kernel: str, cells_per_launch: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of the
     same kernel and launch size (tools/summarize_prof.py; FETCH_SIZE and
     WRITE_SIZE in separate passes, gfx950 corrections applied), or None."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):  # by round: latest wins
+    # latest round wins (natural order of the round key, not lexical)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=profile_key):
         try:
             s = json.load(open(f))
         except (OSError, ValueError):
@@ -97,6 +106,187 @@ def pmc_traffic(kernel: str, cells_per_launch: int):
         if kernel in s.get("kernel", "") and s.get("cells_per_launch") == cells_per_launch:
             best = (s["traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
     return best
+
+
+# ---- self-check of the timed run (every N) ----------------------------------
+CHECK_P = 24      # patch edge
+CHECK_K = 8       # steps after seeding the patches
+CHECK_PAD = CHECK_K + 1
+
+
+def splitmix64(x):
+    with np.errstate(over="ignore"):
+        z = np.asarray(x, dtype=np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def gol_box(alive, steps):
+    """The checker: 3-D game of life (26 neighbors, born on 3, survives on 2
+    or 3: tests/game_of_life/scalability3d.cpp:136-165) on a [z, y, x] box
+    whose outside is dead, in plain numpy.  Returns (alive, live neighbor
+    count of the last step) as u32, the two fields the device step writes.
+    tests/test_bench_check.py holds it to the oracle."""
+    a = np.asarray(alive, dtype=np.uint8)
+    cnt = np.zeros(a.shape, dtype=np.uint8)
+    Z, Y, X = a.shape
+    for _ in range(steps):
+        p = np.pad(a, 1)
+        cnt = np.zeros(a.shape, dtype=np.uint8)
+        for dz in range(3):
+            for dy in range(3):
+                for dx in range(3):
+                    if dz == dy == dx == 1:
+                        continue
+                    cnt += p[dz:dz + Z, dy:dy + Y, dx:dx + X]
+        a = ((cnt == 3) | ((a == 1) & (cnt == 2))).astype(np.uint8)
+    return a.astype(np.uint32), cnt.astype(np.uint32)
+
+
+def check_windows(n: int, world: int):
+    """Patch windows of the N-rank grid n x n x (n * world), periodic z:
+    every rank's lower slab seam (for rank 0 the ring wrap from the last
+    plane), at the x/y edges and inside, each slab's middle at a stencil tile
+    seam, and -- when the grid holds more than 2^32 cells -- the planes where
+    the linear index crosses 2^32.  Returns [(corner (x, y, z), window)],
+    windows pairwise disjoint (z modulo n * world); a window is the patch
+    padded by K + 1 cells, x and y clipped to the non-periodic box."""
+    P, PAD, LZ = CHECK_P, CHECK_PAD, n * world
+    cand = []
+    edges = [(0, 0), (n - P, n - P), (0, n - P), (n - P, 0)]
+    for r in range(world):
+        z = r * n - P // 2
+        cand.append((*edges[r % 4], z))
+        cand.append(((n // 2 - P // 2 + 37 * r) % (n - P), (n // 3 + 53 * r) % (n - P), z))
+    for r in range(world):
+        xa = 256 - P // 2 if n >= 512 else n // 4
+        cand.append((xa, (1024 - P // 2) % (n - P) if n > 1024 else n // 2, r * n + n // 2 - P // 2))
+    if LZ * n * n > 1 << 32:
+        z32 = (1 << 32) // (n * n)
+        cand.append((0, 0, z32 - P // 2))
+        cand.append((n - P, n - P, z32 - P // 2))
+
+    def window(c):
+        x0, y0, z0 = c
+        return [(max(0, x0 - PAD), min(n, x0 + P + PAD)), (max(0, y0 - PAD), min(n, y0 + P + PAD)),
+                (z0 - PAD, z0 + P + PAD)]
+
+    def disjoint(w1, w2):
+        for ax in range(3):
+            (a0, a1), (b0, b1) = w1[ax], w2[ax]
+            if ax < 2 and (a1 <= b0 or b1 <= a0):
+                return True
+            if ax == 2 and all(a1 <= b0 + s or b1 + s <= a0 for s in (-LZ, 0, LZ)):
+                return True
+        return False
+    out = []
+    for c in cand:
+        w = window(c)
+        if w[2][1] - w[2][0] <= LZ and all(disjoint(w, v) for _, v in out):
+            out.append((c, w))
+    return out
+
+
+def window_ids(w, n: int, lz: int):
+    """Cell ids of a window in [z, y, x] order (z modulo lz)."""
+    (x0, x1), (y0, y1), (z0, z1) = w
+    x = np.arange(x0, x1, dtype=np.uint64)
+    y = np.arange(y0, y1, dtype=np.uint64)
+    z = np.mod(np.arange(z0, z1, dtype=np.int64), lz).astype(np.uint64)
+    Zg, Yg, Xg = np.meshgrid(z, y, x, indexing="ij")
+    nn = np.uint64(n)
+    return (Xg + nn * (Yg + nn * Zg) + np.uint64(1)).ravel()
+
+
+def check_run(grid, ctx, n: int, world: int, rank: int, fields, allgather):
+    """After the timed loop (outside the timing): reseed the same grid with
+    empty state plus random 24^3 patches at the places of check_windows,
+    step CHECK_K times through the same gol_step (halo included), and compare
+    every rank's part of every window bit for bit with gol_box, plus a
+    full-grid checksum (sum and splitmix64(id)-weighted sum of alive and of
+    live neighbor counts, summed over ranks) against the windows' sums, so
+    no cell outside the windows changed either.  `allgather(obj)` returns
+    every rank's obj."""
+    import dccrg_amd as D
+    cur, nxt, cnt = fields
+    lz = n * world
+    n_local = grid.n_local
+    lo = rank * n_local  # block partition: cells_per_process = n^3 exactly
+    D.lib().dccrgx_field_init_hash(grid._h, grid.field_id(cur), 0)  # all dead
+    rng = np.random.default_rng(1 << 20)
+    wins = check_windows(n, world)
+    expect = []
+    for (x0, y0, z0), w in wins:
+        dims = tuple(hi - lo_ for lo_, hi in w)
+        box = np.zeros(dims[::-1], dtype=np.uint8)
+        ox, oy, oz = x0 - w[0][0], y0 - w[1][0], z0 - w[2][0]
+        box[oz:oz + CHECK_P, oy:oy + CHECK_P, ox:ox + CHECK_P] = rng.random((CHECK_P,) * 3) < 0.2
+        ids = window_ids(w, n, lz)
+        mine = (ids - np.uint64(1) >= np.uint64(lo)) & (ids - np.uint64(1) < np.uint64(lo + n_local))
+        sel = (box.ravel() != 0) & mine
+        if sel.any():
+            grid.write_cells(cur, ids[sel], np.ones(int(sel.sum()), dtype=np.uint32))
+        ra, rn = gol_box(box, CHECK_K)
+        expect.append((ids, mine, ra.ravel(), rn.ravel()))
+    for _ in range(CHECK_K):
+        grid.gol_step(cur, nxt, cnt)
+        cur, nxt = nxt, cur
+    ctx.synchronize()
+    bad = []
+    sums = [0, 0, 0, 0]
+    M64 = (1 << 64) - 1
+    for k, (ids, mine, ra, rn) in enumerate(expect):
+        with np.errstate(over="ignore"):
+            mix = splitmix64(ids)
+            sums[0] += int(ra.astype(np.uint64).sum())
+            sums[1] = (sums[1] + int((ra.astype(np.uint64) * mix).sum(dtype=np.uint64))) & M64
+            sums[2] += int(rn.astype(np.uint64).sum())
+            sums[3] = (sums[3] + int((rn.astype(np.uint64) * mix).sum(dtype=np.uint64))) & M64
+        if not mine.any():
+            continue
+        got_a = np.concatenate(grid.read_cells(cur, ids[mine]))
+        got_n = np.concatenate(grid.read_cells(cnt, ids[mine]))
+        if not (np.array_equal(got_a, ra[mine]) and np.array_equal(got_n, rn[mine])):
+            bad.append({"rank": rank, "patch": list(wins[k][0]),
+                        "alive_diff": int((got_a != ra[mine]).sum()), "count_diff": int((got_n != rn[mine]).sum())})
+    ca, cn = grid.checksum(cur), grid.checksum(cnt)
+    parts = allgather({"bad": bad, "alive": ca, "count": cn, "cells": int(sum(int(m.sum()) for _, m, _, _ in expect))})
+    got = [sum(p["alive"][0] for p in parts), sum(p["alive"][1] for p in parts) & M64,
+           sum(p["count"][0] for p in parts), sum(p["count"][1] for p in parts) & M64]
+    mism = [b for p in parts for b in p["bad"]]
+    cells = sum(p["cells"] for p in parts)
+    ok = not mism and got == sums and cells == sum(ids.size for ids, _, _, _ in expect)
+    return {"patches": len(wins), "window_cells": cells, "steps": CHECK_K,
+            "corners": [list(c) for c, _ in wins],
+            "checker": "bench.gol_box (numpy B3/S23 over 26 neighbors; tests/test_bench_check.py pins it "
+                       "to the oracle)",
+            "windows_bit_exact": not mism, "checksum_equal": got == sums, "bit_exact": ok,
+            "mismatches": mism[:8]}
+
+
+class Watchdog:
+    """Ends the process (exit 3) with a message naming the rank and the phase
+    if the phase does not finish in time: a stalled ncclCommInitRank or first
+    exchange fails fast instead of holding the job."""
+
+    def __init__(self, rank: int, what: str, seconds: float):
+        self.rank, self.what, self.seconds = rank, what, seconds
+
+    def _fire(self):
+        os.write(2, f"bench.py: rank {self.rank} stalled in {self.what} for {self.seconds:.0f} s\n".encode())
+        os._exit(3)
+
+    def __enter__(self):
+        import threading
+        self.t = threading.Timer(self.seconds, self._fire)
+        self.t.daemon = True
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.t.cancel()
+        return False
 
 
 def poisson3d_leaves():
@@ -622,6 +812,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the other configs' lines (N = 1)")
     ap.add_argument("--no-halo-payload", action="store_true", help="skip the byte-payload halo line")
+    ap.add_argument("--no-check", action="store_true", help="skip the self-check after the timed loop (profiling)")
+    ap.add_argument("--stall-timeout", type=float, default=180.0,
+                    help="seconds before a rank stuck in RCCL init or the first exchange ends the run (exit 3)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print each rank's RANK / LOCAL_RANK / WORLD_SIZE as JSON and stop before any GPU call")
     args = ap.parse_args()
@@ -662,7 +855,8 @@ def main():
     if world > 1 and not shared_gpu:
         uid = [D.Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(uid[0])
+        with Watchdog(rank, "ncclCommInitRank", args.stall_timeout):
+            ctx.comm_init(uid[0])
     elif world > 1:  # halos through the library's host-staged transport over gloo
         from dccrg_amd.transport import TorchDistTransport
         TorchDistTransport().attach(ctx)
@@ -689,8 +883,13 @@ def main():
             dist.barrier()
 
     cur, nxt = "alive_a", "alive_b"
-    for _ in range(args.warmup):
-        grid.gol_step(cur, nxt, "count")
+    for i in range(args.warmup):
+        if i == 0:
+            with Watchdog(rank, "the first halo exchange (warm-up step 1)", args.stall_timeout):
+                grid.gol_step(cur, nxt, "count")
+                barrier()
+        else:
+            grid.gol_step(cur, nxt, "count")
         cur, nxt = nxt, cur
     barrier()
     grid.kernel_timer(reset=1)
@@ -756,6 +955,17 @@ def main():
         if t:
             line["roofline"]["traffic"] = t[0]
             line["roofline"]["traffic_source"] = t[1]
+
+    def allgather(obj):
+        if world == 1:
+            return [obj]
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
+    # outside the timing: the same grid, reseeded, checked against the checker
+    if not args.no_check:
+        with Watchdog(rank, "the self-check", args.stall_timeout + 300):
+            line["check"] = check_run(grid, ctx, n, world, rank, ("alive_a", "alive_b", "count"), allgather)
     grid.close()
 
     def reduce_max(v: float) -> float:
@@ -779,6 +989,9 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    if "check" in line and not line["check"]["bit_exact"]:
+        os.write(2, f"bench.py: rank {rank}: self-check failed: {json.dumps(line['check']['mismatches'])}\n".encode())
+        raise SystemExit(4)
 
 
 if __name__ == "__main__":

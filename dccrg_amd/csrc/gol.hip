@@ -309,6 +309,16 @@ int dccrgx_gol_step(dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t fou
     DX_TRY(dccrgx_halo_start(grid, hood_id, &fin, 1));
     DX_TRY(dccrgx_gol_compute(grid, hood_id, fin, fout, fcnt, DCCRGX_REGION_INNER));
     DX_TRY(dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL));
+    // DCCRGX_TEST_CORRUPT_GHOST=1 (tests only): after every exchange, mark the
+    // ghost cell just below the rank's first local cell alive, as a lost or
+    // misplaced halo message would; bench.py's self-check must then fail
+    static const bool corrupt = getenv_flag("DCCRGX_TEST_CORRUPT_GHOST");
+    if (corrupt && grid->uniform && grid->n_local) {
+        const uint64_t slot0 = grid->g.lo + (uint64_t)(-grid->g.cbase * (int64_t)grid->g.S);
+        if (slot0 > 0)
+            DX_HIP(hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)grid->fields[fin].ptr + slot0 - 1), 1, 1,
+                                     grid->ctx->compute));
+    }
     DX_TRY(dccrgx_gol_compute(grid, hood_id, fin, fout, fcnt, DCCRGX_REGION_OUTER));
     return DCCRGX_OK;
 }

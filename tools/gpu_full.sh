@@ -19,13 +19,13 @@ timeout -k 10 600 python -u bench.py > $out/bench.log 2>&1 || { tail -n 20 $out/
 tail -n 1 $out/bench.log
 [ "$3" = "noprof" ] && { echo done; exit 0; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof/trace -o run -- \
-  python3 bench.py --steps 5 --warmup 1 --no-secondary --no-halo-payload --no-cpu-baseline \
+  python3 bench.py --steps 5 --warmup 1 --no-secondary --no-halo-payload --no-cpu-baseline --no-check \
   > $out/prof_trace.log 2>&1 || { tail -n 20 $out/prof_trace.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $out/prof/fetch -o run -- \
-  python3 bench.py --steps 3 --warmup 1 --no-secondary --no-halo-payload --no-cpu-baseline \
+  python3 bench.py --steps 3 --warmup 1 --no-secondary --no-halo-payload --no-cpu-baseline --no-check \
   > $out/prof_fetch.log 2>&1 || { tail -n 20 $out/prof_fetch.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $out/prof/write -o run -- \
-  python3 bench.py --steps 3 --warmup 1 --no-secondary --no-halo-payload --no-cpu-baseline \
+  python3 bench.py --steps 3 --warmup 1 --no-secondary --no-halo-payload --no-cpu-baseline --no-check \
   > $out/prof_write.log 2>&1 || { tail -n 20 $out/prof_write.log; exit 1; }
 find $out/prof -name '*.csv' | head -n 20
 echo done
