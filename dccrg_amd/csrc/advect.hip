@@ -71,40 +71,46 @@ __device__ inline int face_dir(int64_t cl, int64_t nl, const int32_t* off)
     return overlaps == 2 ? direction : 0;
 }
 
-// face lists of local cells from the stencil rows: pass 1 (o_row == null)
-// writes the first 6 faces column-major and counts the rest into o_cnt;
-// pass 2 writes the rest at o_row
+// face lists of local cells from the stencil rows.  Column k of the first
+// six holds the cell's face neighbor in direction k = -x, +x, -y, +y, -z, +z
+// (the first one met in stencil order; 0xffffffff: none), so the kernels
+// know each column's axis and sign at compile time; further neighbors in a
+// direction (finer cells: 2 per face in 2-D, 4 in 3-D) go to the overflow
+// rows with their direction.  Pass 1 (o_row == null) writes the columns and
+// counts the overflow into o_cnt; pass 2 writes the overflow at o_row.
 __global__ void __launch_bounds__(256) k_face_build(const uint64_t* __restrict__ st_row,
                                                     const uint32_t* __restrict__ st_slot,
                                                     const int32_t* __restrict__ st_off,
                                                     const uint32_t* __restrict__ local_g,
                                                     const uint8_t* __restrict__ level, int M, uint64_t n,
-                                                    uint32_t* __restrict__ ell_slot, int8_t* __restrict__ ell_dir,
-                                                    uint32_t* __restrict__ o_cnt, const uint64_t* __restrict__ o_row,
-                                                    uint32_t* __restrict__ o_slot, int8_t* __restrict__ o_dir)
+                                                    uint32_t* __restrict__ ell_slot, uint32_t* __restrict__ o_cnt,
+                                                    const uint64_t* __restrict__ o_row, uint32_t* __restrict__ o_slot,
+                                                    int8_t* __restrict__ o_dir)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
         const int64_t cl = 1ll << (M - level[local_g[q]]);
-        uint32_t k = 0;
+        uint32_t used = 0, k = 0;
         for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) {
             const uint32_t nb = st_slot[e];
             const int dir = face_dir(cl, 1ll << (M - level[nb]), st_off + 3 * e);
             if (!dir) continue;
-            if (k < 6) {
-                if (!o_row) {
-                    ell_slot[k * n + q] = nb;
-                    ell_dir[k * n + q] = (int8_t)dir;
-                }
-            } else if (o_row) {
-                o_slot[o_row[q] + k - 6] = nb;
-                o_dir[o_row[q] + k - 6] = (int8_t)dir;
+            const int col = 2 * ((dir > 0 ? dir : -dir) - 1) + (dir > 0 ? 1 : 0);
+            if (!(used >> col & 1u)) {
+                used |= 1u << col;
+                if (!o_row) ell_slot[col * n + q] = nb;
+                continue;
+            }
+            if (o_row) {
+                o_slot[o_row[q] + k] = nb;
+                o_dir[o_row[q] + k] = (int8_t)dir;
             }
             k++;
         }
         if (!o_row) {
-            for (uint32_t j = k; j < 6; j++) ell_slot[j * n + q] = 0xffffffffu;
-            o_cnt[q] = k > 6 ? k - 6 : 0;
+            for (int col = 0; col < 6; col++)
+                if (!(used >> col & 1u)) ell_slot[col * n + q] = 0xffffffffu;
+            o_cnt[q] = k;
         }
     }
 }
@@ -114,7 +120,6 @@ __global__ void __launch_bounds__(256) k_face_build(const uint64_t* __restrict__
 struct FaceView {  // trivially copyable kernel argument
     uint64_t n;
     const uint32_t* ell_slot;
-    const int8_t* ell_dir;
     const uint64_t* o_row;
     const uint32_t* o_slot;
     const int8_t* o_dir;
@@ -145,11 +150,23 @@ __device__ inline double face_term_v(int dir, double dt, double vol_c, const dou
 // independent loads, and every neighbour value of all 6 faces is gathered
 // unconditionally (an absent face reads the cell itself and is masked out)
 // so the ~30 gathers of a cell are in flight together instead of one face's
-// loads waiting behind the previous face's branch.  The overflow (faces
-// next to finer cells beyond the first 6) is rare.
-__global__ void __launch_bounds__(256) k_ex_advect_faces(AdvPtrs p, double dt, FaceView fc,
+// loads waiting behind the previous face's branch.  Column k's direction is
+// k itself (k_face_build), so the axis of the velocity gathered and the
+// face expression are resolved at compile time.  The overflow (faces next
+// to finer cells beyond the first per direction) is rare.
+//
+// rho_out == null: calculate_fluxes (flux[c] += the cell's face terms).
+// rho_out != null: one fused solver step (calculate_fluxes then
+// apply_fluxes, solve.hpp:283-293): rho_out[c] = rho[c] + (flux[c] + terms),
+// the same additions in the same order as the two passes, and flux[c] left
+// 0; rho_out is the other buffer of a double-buffered density, so no flux
+// array is written and read back.  Slots [t0, t1) (ghosts, retired cells)
+// are carried over to rho_out unchanged.
+template <int WPE>
+__global__ void __launch_bounds__(256, WPE) k_ex_advect_faces(AdvPtrs p, double dt, FaceView fc,
                                                          const uint32_t* __restrict__ local_g,
-                                                         const uint32_t* __restrict__ pos, uint64_t n)
+                                                         const uint32_t* __restrict__ pos, uint64_t n,
+                                                         double* __restrict__ rho_out, uint64_t t0, uint64_t t1)
 {
 #pragma clang fp contract(off)
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -157,12 +174,8 @@ __global__ void __launch_bounds__(256) k_ex_advect_faces(AdvPtrs p, double dt, F
         const uint32_t q = pos ? pos[i] : (uint32_t)i;
         const uint32_t c = local_g ? local_g[q] : q;  // null: identity (explicit local slots are [0, n_local))
         uint32_t s[6];
-        int8_t d[6];
 #pragma unroll
-        for (int k = 0; k < 6; k++) {
-            s[k] = fc.ell_slot[k * fc.n + q];
-            d[k] = fc.ell_dir[k * fc.n + q];
-        }
+        for (int k = 0; k < 6; k++) s[k] = fc.ell_slot[k * fc.n + q];
         const double lc3[3] = {p.l[0][c], p.l[1][c], p.l[2][c]};
         const double vc3[3] = {p.v[0][c], p.v[1][c], p.v[2][c]};
         const double rho_c = p.rho[c];
@@ -171,23 +184,29 @@ __global__ void __launch_bounds__(256) k_ex_advect_faces(AdvPtrs p, double dt, F
 #pragma unroll
         for (int k = 0; k < 6; k++) {
             const uint32_t nb = s[k] != 0xffffffffu ? s[k] : c;
-            const int ax = d[k] > 0 ? d[k] - 1 : (d[k] < 0 ? -d[k] - 1 : 0);
-            const double* vp = ax == 0 ? p.v[0] : (ax == 1 ? p.v[1] : p.v[2]);
             ln0[k] = p.l[0][nb];
             ln1[k] = p.l[1][nb];
             ln2[k] = p.l[2][nb];
-            vn[k] = vp[nb];
+            vn[k] = p.v[k >> 1][nb];
             rn[k] = p.rho[nb];
         }
         const double vol = lc3[0] * lc3[1] * lc3[2];
 #pragma unroll
         for (int k = 0; k < 6; k++)
             if (s[k] != 0xffffffffu)
-                acc += face_term_v(d[k], dt, vol, lc3, vc3, rho_c, ln0[k], ln1[k], ln2[k], vn[k], rn[k]);
+                acc += face_term_v((k & 1) ? (k >> 1) + 1 : -((k >> 1) + 1), dt, vol, lc3, vc3, rho_c, ln0[k], ln1[k],
+                                   ln2[k], vn[k], rn[k]);
         if (fc.overflow)
             for (uint64_t e = fc.o_row[q]; e < fc.o_row[q + 1]; e++) acc += face_term(p, c, fc.o_slot[e], fc.o_dir[e], dt, vol);
-        p.flux[c] = acc;
+        if (!rho_out) {
+            p.flux[c] = acc;
+        } else {
+            rho_out[c] = rho_c + acc;
+            if (p.flux[c] != 0.0) p.flux[c] = 0.0;
+        }
     }
+    if (rho_out)
+        for (uint64_t s = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < t1; s += stride) rho_out[s] = p.rho[s];
 }
 
 // check_for_adaptation, tests/advection/adapter.hpp:66-103: max relative
@@ -316,8 +335,12 @@ __global__ void __launch_bounds__(256) k_flag_slots(const uint32_t* __restrict__
 
 // uniform grids: the face neighbors present in the neighborhood (mask bit
 // 2k / 2k+1 = canonical axis k, -1 / +1), addressed in the slab layout
+// rho_out: as k_ex_advect_faces (fused step into the other density buffer;
+// storage slots outside [soff + lin0, soff + lin0 + n) listed as [t0, t1) and
+// [t2, t3) are carried over)
 __global__ void __launch_bounds__(256) k_u_advect(UGeom g, AdvPtrs p, double dt, uint32_t mask, uint64_t lin0,
-                                                  uint64_t n)
+                                                  uint64_t n, double* __restrict__ rho_out, uint64_t t0, uint64_t t1,
+                                                  uint64_t t2, uint64_t t3)
 {
 #pragma clang fp contract(off)
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -347,7 +370,16 @@ __global__ void __launch_bounds__(256) k_u_advect(UGeom g, AdvPtrs p, double dt,
                 const int dir = (sg ? 1 : -1) * (g.perm[k] + 1);
                 acc += face_term(p, s, ug_slot(g, a2, b2, c2), dir, dt, vol);
             }
-        p.flux[s] = acc;
+        if (!rho_out) {
+            p.flux[s] = acc;
+        } else {
+            rho_out[s] = p.rho[s] + acc;
+            if (p.flux[s] != 0.0) p.flux[s] = 0.0;
+        }
+    }
+    if (rho_out) {
+        for (uint64_t s = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < t1; s += stride) rho_out[s] = p.rho[s];
+        for (uint64_t s = t2 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < t3; s += stride) rho_out[s] = p.rho[s];
     }
 }
 
@@ -510,14 +542,13 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
     fc->n = n;
     const size_t m = std::max<uint64_t>(n, 1);
     DX_HIP(dx_malloc(&fc->ell_slot, 6 * m * 4));
-    DX_HIP(dx_malloc(&fc->ell_dir, 6 * m));
     DX_HIP(dx_malloc(&fc->o_row, (m + 1) * 8));
     uint32_t* d_cnt = nullptr;
     DX_HIP(dx_malloc(&d_cnt, m * 4));
     const int M = grid->map.max_lvl;
     if (n)
         hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
-                           R.local_slot, R.level, M, n, fc->ell_slot, fc->ell_dir, d_cnt, (const uint64_t*)nullptr,
+                           R.local_slot, R.level, M, n, fc->ell_slot, d_cnt, (const uint64_t*)nullptr,
                            (uint32_t*)nullptr, (int8_t*)nullptr);
     DX_HIP(hipGetLastError());
     // overflow rows by a device scan (one 8-byte read-back for the total)
@@ -530,11 +561,85 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
     DX_HIP(dx_malloc(&fc->o_dir, std::max<uint64_t>(total, 1)));
     if (fc->overflow)
         hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
-                           R.local_slot, R.level, M, n, fc->ell_slot, fc->ell_dir, (uint32_t*)nullptr, fc->o_row,
+                           R.local_slot, R.level, M, n, fc->ell_slot, (uint32_t*)nullptr, fc->o_row,
                            fc->o_slot, fc->o_dir);
     DX_HIP(hipGetLastError());
     DX_HIP(hipStreamSynchronize(st));
     h.faces = fc;
+    return DCCRGX_OK;
+}
+
+// the face-flux kernels over a region; rho_out != null: fused step into
+// rho_out, and with `tail` the slots no launch of the step writes are
+// carried over (the last launch of a step)
+int advect_launch(dccrgx_grid* grid, Hood& h, const AdvPtrs& p, double dt, int32_t region, double* rho_out,
+                  bool tail)
+{
+    hipStream_t st = grid->ctx->compute;
+    if (!grid->uniform) {
+        ExRegion R;
+        DX_TRY(explicit_region(grid, h, region, &R));
+        const uint64_t t0 = grid->n_local, t1 = tail && rho_out ? grid->n_slots : t0;
+        const uint64_t work = std::max<uint64_t>(R.n, t1 - t0);
+        if (!work) return DCCRGX_OK;
+        if (!h.faces) DX_TRY(build_faces(grid, h));
+        const FaceCache& F = *h.faces;
+        const FaceView fv{F.n, F.ell_slot, F.o_row, F.o_slot, F.o_dir, F.overflow};
+        // explicit grids store local cell q in slot q (explicit.hip): no slot loads
+        static const int64_t wpe = getenv_int("DCCRGX_ADV_WPE", 4);  // sweep: waves per SIMD the kernel is built for
+        auto k = wpe >= 8 ? k_ex_advect_faces<8> : wpe >= 6 ? k_ex_advect_faces<6> : wpe >= 5 ? k_ex_advect_faces<5>
+                                                                                             : k_ex_advect_faces<1>;
+        hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv, (const uint32_t*)nullptr,
+                           region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos, R.n, rho_out, t0, t1);
+        DX_HIP(hipGetLastError());
+        return DCCRGX_OK;
+    }
+    const UGeom& u = grid->g;
+    const uint32_t mask = face_mask(h);
+    uint64_t s0 = 0, nloc = 0;
+    uniform_local_run(grid, &s0, &nloc);
+    int64_t r[2][2];
+    region_slices(grid, h, region, r);
+    const int64_t S = (int64_t)u.S;
+    int last = -1;
+    for (int i = 0; i < 2; i++)
+        if (r[i][1] > r[i][0]) last = i;
+    for (int i = 0; i < 2; i++) {
+        uint64_t l0 = 0, l1 = 0;
+        if (r[i][1] > r[i][0]) {
+            l0 = std::max<int64_t>((r[i][0] + u.cbase) * S, (int64_t)u.lo);
+            l1 = std::min<int64_t>((r[i][1] + u.cbase) * S, (int64_t)u.hi);
+            if (l1 < l0) l1 = l0;
+        }
+        const bool t = tail && rho_out && i == (last < 0 ? 0 : last);
+        const uint64_t a0 = 0, a1 = t ? s0 : 0, b0 = s0 + nloc, b1 = t ? grid->n_slots : b0;
+        const uint64_t work = std::max<uint64_t>(std::max<uint64_t>(l1 - l0, a1 - a0), b1 - b0);
+        if (!work || (!mask && !rho_out)) continue;
+        // no face items: the step copies density unchanged (flux + 0 terms)
+        hipLaunchKernelGGL(k_u_advect, dim3(grid_for(work)), dim3(256), 0, st, u, p, dt, mask, l0, l1 - l0, rho_out,
+                           a0, a1, b0, b1);
+        DX_HIP(hipGetLastError());
+    }
+    return DCCRGX_OK;
+}
+
+// the other density buffer of a fused step: a spare of the grid that holds
+// n_slots doubles, or a new one
+int density_spare(dccrgx_grid* grid, double** out, size_t* bytes)
+{
+    const size_t need = std::max<uint64_t>(grid->n_slots, 1) * 8;
+    auto& sp = grid->spare_bufs;
+    size_t best = sp.size();
+    for (size_t i = 0; i < sp.size(); i++)
+        if (sp[i].second >= need && (best == sp.size() || sp[i].second < sp[best].second)) best = i;
+    if (best < sp.size() && sp[best].second <= 2 * need) {
+        *out = (double*)sp[best].first;
+        *bytes = sp[best].second;
+        sp.erase(sp.begin() + best);
+        return DCCRGX_OK;
+    }
+    DX_HIP(dx_malloc(out, need));
+    *bytes = need;
     return DCCRGX_OK;
 }
 
@@ -543,7 +648,7 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
 FaceCache::~FaceCache()
 {
     FreeBatch fb;
-    for (void* q : {(void*)ell_slot, (void*)ell_dir, (void*)o_row, (void*)o_slot, (void*)o_dir}) fb.add(q);
+    for (void* q : {(void*)ell_slot, (void*)o_row, (void*)o_slot, (void*)o_dir}) fb.add(q);
 }
 
 }  // namespace dccrgx
@@ -556,43 +661,13 @@ int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect
                          int32_t region)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
-    const Hood* h = find_hood(grid, hood_id);
+    Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     DX_CHECK(region >= DCCRGX_REGION_ALL && region <= DCCRGX_REGION_OUTER, DCCRGX_EINVAL, "bad region");
     AdvPtrs p;
     DX_TRY(adv_ptrs(grid, f, &p));
     if (!grid->n_local) return DCCRGX_OK;
-    hipStream_t st = grid->ctx->compute;
-    if (!grid->uniform) {
-        ExRegion R;
-        DX_TRY(explicit_region(grid, *h, region, &R));
-        if (!R.n) return DCCRGX_OK;
-        Hood* hm = find_hood(grid, hood_id);
-        if (!hm->faces) DX_TRY(build_faces(grid, *hm));
-        const FaceCache& F = *hm->faces;
-        const FaceView fv{F.n, F.ell_slot, F.ell_dir, F.o_row, F.o_slot, F.o_dir, F.overflow};
-        // explicit grids store local cell q in slot q (explicit.hip): no slot loads
-        hipLaunchKernelGGL(k_ex_advect_faces, dim3(grid_for(R.n)), dim3(256), 0, st, p, dt, fv,
-                           (const uint32_t*)nullptr, region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos,
-                           R.n);
-        DX_HIP(hipGetLastError());
-        return DCCRGX_OK;
-    }
-    const UGeom& u = grid->g;
-    const uint32_t mask = face_mask(*h);
-    if (!mask) return DCCRGX_OK;
-    int64_t r[2][2];
-    region_slices(grid, *h, region, r);
-    const int64_t S = (int64_t)u.S;
-    for (auto& x : r) {
-        if (x[1] <= x[0]) continue;
-        const uint64_t l0 = std::max<int64_t>((x[0] + u.cbase) * S, (int64_t)u.lo);
-        const uint64_t l1 = std::min<int64_t>((x[1] + u.cbase) * S, (int64_t)u.hi);
-        if (l1 <= l0) continue;
-        hipLaunchKernelGGL(k_u_advect, dim3(grid_for(l1 - l0)), dim3(256), 0, st, u, p, dt, mask, l0, l1 - l0);
-        DX_HIP(hipGetLastError());
-    }
-    return DCCRGX_OK;
+    return advect_launch(grid, *h, p, dt, region, nullptr, false);
 }
 
 int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f)
@@ -791,22 +866,45 @@ int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt)
 {
     DX_CHECK(grid && f, DCCRGX_EINVAL, "null argument");
-    // 2d.cpp:321-390: start density halo, inner fluxes, wait, outer fluxes, apply
+    // 2d.cpp:321-390: start density halo, inner fluxes, wait, outer fluxes,
+    // apply -- fused: the flux kernels write the new density into the other
+    // buffer of a double-buffered density (k_ex_advect_faces), one launch
+    // per region, and the buffers swap (the density field's device pointer
+    // changes, dccrgx.h)
     const int32_t fd = f->density;
-    const Hood* h = find_hood(grid, hood_id);
+    Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    AdvPtrs p;
+    DX_TRY(adv_ptrs(grid, f, &p));
     bool remote = false;
     for (const PeerPlan& pp : h->peers) remote |= !pp.send_ids.empty() || !pp.recv_ids.empty();
     DX_TRY(dccrgx_halo_start(grid, hood_id, &fd, 1));
-    if (!remote) {  // nothing to overlap: one launch over every local cell
-        DX_TRY(dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL));
-        DX_TRY(dccrgx_advect_fluxes(grid, hood_id, f, dt, DCCRGX_REGION_ALL));
-        return dccrgx_advect_apply(grid, f);
+    if (!grid->n_local) return dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL);
+    double* out = nullptr;
+    size_t out_bytes = 0;
+    int s = density_spare(grid, &out, &out_bytes);
+    if (s != DCCRGX_OK) {
+        dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL);
+        return s;
     }
-    DX_TRY(dccrgx_advect_fluxes(grid, hood_id, f, dt, DCCRGX_REGION_INNER));
-    DX_TRY(dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL));
-    DX_TRY(dccrgx_advect_fluxes(grid, hood_id, f, dt, DCCRGX_REGION_OUTER));
-    return dccrgx_advect_apply(grid, f);
+    if (!remote) {  // nothing to overlap: one launch over every local cell
+        s = dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL);
+        if (s == DCCRGX_OK) s = advect_launch(grid, *h, p, dt, DCCRGX_REGION_ALL, out, true);
+    } else {
+        s = advect_launch(grid, *h, p, dt, DCCRGX_REGION_INNER, out, false);
+        const int w = dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL);
+        if (s == DCCRGX_OK) s = w;
+        if (s == DCCRGX_OK) s = advect_launch(grid, *h, p, dt, DCCRGX_REGION_OUTER, out, true);
+    }
+    Field& F = grid->fields[fd];
+    if (s != DCCRGX_OK) {
+        grid->spare_bufs.emplace_back(out, out_bytes);
+        return s;
+    }
+    grid->spare_bufs.emplace_back(F.ptr, F.cap_bytes ? F.cap_bytes : std::max<uint64_t>(grid->n_slots, 1) * 8);
+    F.ptr = out;
+    F.cap_bytes = out_bytes == std::max<uint64_t>(grid->n_slots, 1) * 8 ? 0 : out_bytes;
+    return DCCRGX_OK;
 }
 
 }  // extern "C"

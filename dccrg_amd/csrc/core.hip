@@ -6,6 +6,7 @@
 #include <cstdarg>
 #include <cstring>
 #include <condition_variable>
+#include <exception>
 #include <deque>
 #include <mutex>
 #include <unordered_map>
@@ -505,6 +506,7 @@ struct Pool {
     std::condition_variable go, fin;
     std::vector<std::thread> th;
     const std::function<void(size_t)>* job = nullptr;
+    std::exception_ptr err;  // the first exception a worker's share threw
     size_t gen = 0, active = 0, pending = 0;
     bool stop = false;
     void ensure(size_t workers)
@@ -521,8 +523,14 @@ struct Pool {
                     if (id >= active) continue;
                     const std::function<void(size_t)>* j = job;
                     lk.unlock();
-                    (*j)(id);
+                    std::exception_ptr ex;
+                    try {
+                        (*j)(id);
+                    } catch (...) {
+                        ex = std::current_exception();
+                    }
                     lk.lock();
+                    if (ex && !err) err = ex;
                     if (--pending == 0) fin.notify_one();
                 }
             });
@@ -556,12 +564,25 @@ void pool_run(size_t nt, const std::function<void(size_t)>& job)
         p.job = &job;
         p.active = nt;
         p.pending = nt - 1;
+        p.err = nullptr;
         p.gen++;
     }
     p.go.notify_all();
-    job(0);
+    // every share ends before this returns, also when one throws (the workers
+    // hold a pointer to `job`); then the first exception is rethrown
+    std::exception_ptr ex;
+    try {
+        job(0);
+    } catch (...) {
+        ex = std::current_exception();
+    }
     std::unique_lock<std::mutex> lk(p.m);
     p.fin.wait(lk, [&] { return p.pending == 0; });
+    if (!ex) ex = p.err;
+    p.err = nullptr;
+    p.job = nullptr;
+    lk.unlock();
+    if (ex) std::rethrow_exception(ex);
 }
 
 // ---------------------------------------------------------------------------
@@ -889,6 +910,7 @@ int dccrgx_ctx_create(int device, int rank, int comm_size, dccrgx_ctx** out)
     DX_HIP(hipStreamCreateWithFlags(&c->comm, hipStreamNonBlocking));
     DX_HIP(hipEventCreateWithFlags(&c->ev_compute, hipEventDisableTiming));
     DX_HIP(hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
+    DX_HIP(hipEventCreateWithFlags(&c->ev_caller, hipEventDisableTiming));
     dx_cache_streams(c->compute, c->comm, true);  // frees are fenced on these streams
     *out = c;
     return DCCRGX_OK;
@@ -904,6 +926,7 @@ int dccrgx_ctx_destroy(dccrgx_ctx* c)
     if (c->has_comm) ncclCommDestroy(c->nccl);
     hipEventDestroy(c->ev_compute);
     hipEventDestroy(c->ev_comm);
+    hipEventDestroy(c->ev_caller);
     for (hipEvent_t e : c->up_ev)  // recorded on the compute stream, which is idle now
         if (e) hipEventDestroy(e);
     hipStreamDestroy(c->compute);

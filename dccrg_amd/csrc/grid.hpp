@@ -294,8 +294,7 @@ struct CopySeg {
 // coalesced; faces beyond 6 (next to finer cells) go to a CSR overflow.
 struct FaceCache {
     uint64_t n = 0;
-    uint32_t* ell_slot = nullptr;
-    int8_t* ell_dir = nullptr;
+    uint32_t* ell_slot = nullptr;  // 6 columns: the face neighbor in direction -x, +x, -y, +y, -z, +z
     uint64_t* o_row = nullptr;
     uint32_t* o_slot = nullptr;
     int8_t* o_dir = nullptr;

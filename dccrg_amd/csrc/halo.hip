@@ -510,6 +510,7 @@ int dccrgx_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int6
     DX_CHECK(grid && (n == 0 || (ids && slots)), DCCRGX_EINVAL, "bad argument");
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
     if (n == 0) return DCCRGX_OK;
+    const CallerStream fence(grid->ctx, st);
     if (!grid->uniform) return explicit_slots_of(grid, ids, n, slots, st);
     if (grid->n_local == 0) return set_error(DCCRGX_ESTATE, "rank has no cells");
     hipLaunchKernelGGL(k_slots_of, dim3(grid_for(n)), dim3(256), 0, st, grid->g, ids, n, slots);

@@ -350,6 +350,7 @@ struct Ctx {
     int device = 0, rank = 0, comm_size = 1;
     hipStream_t compute = nullptr, comm = nullptr;
     hipEvent_t ev_compute = nullptr, ev_comm = nullptr;
+    hipEvent_t ev_caller = nullptr;  // CallerStream
     ncclComm_t nccl = nullptr;
     bool has_comm = false;
     // test mode (dccrgx_ctx_route_self_through_rccl): a rank's own periodic
@@ -372,6 +373,25 @@ struct Ctx {
     hipEvent_t up_ev[UP_SLOTS] = {};
     bool up_used[UP_SLOTS] = {};
     int up_next = 0;
+};
+
+// Entry points that take a caller's stream queue kernels there which read
+// grid-owned buffers (hash, neighbor CSRs, fields).  Freed blocks are fenced
+// by events on the library's own streams only (dx_free), so on leaving such
+// an entry point the compute stream is made to wait for what the library
+// queued on the caller's stream: a later free, rebuild or destroy then covers
+// those kernels too.  Only the library's own launches are covered; caller
+// kernels reading grid memory (dccrgx_field_device_ptr) must be synchronised
+// by the caller before structural calls (dccrgx.h).
+struct CallerStream {
+    Ctx* c;
+    hipStream_t st;
+    CallerStream(Ctx* c_, hipStream_t s) : c(c_), st(s) {}
+    ~CallerStream()
+    {
+        if (!c || !st || st == c->compute || st == c->comm) return;
+        if (hipEventRecord(c->ev_caller, st) == hipSuccess) (void)hipStreamWaitEvent(c->compute, c->ev_caller, 0);
+    }
 };
 
 // Host <-> device copies of pageable host memory through the context's pinned

@@ -444,6 +444,7 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     const Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
+    const CallerStream fence(grid->ctx, st);
     if (!grid->uniform) return explicit_neighbors_of(grid, *h, cells, n, row, ids, off3, cap, st);
     const UGeom& g = grid->g;
     const int32_t sc = 1 << grid->map.max_lvl;  // offsets in indices of the finest level
@@ -478,6 +479,7 @@ int dccrgx_gather_neighbors(const dccrgx_grid* grid, int32_t hood_id, int32_t fi
     const Field& F = grid->fields[field_id];
     DX_CHECK(!F.variable, DCCRGX_EINVAL, "variable-size field: use dccrgx_field_read_cells");
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
+    const CallerStream fence(grid->ctx, st);
     if (!grid->uniform) return explicit_gather_neighbors(grid, *h, F, cells, n, row, out, cap_bytes, st);
     const UGeom& g = grid->g;
     uint64_t total = 0;
@@ -501,6 +503,7 @@ int dccrgx_face_neighbors_of(const dccrgx_grid* grid, const uint64_t* cells, siz
 {
     DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
+    const CallerStream fence(grid->ctx, st);
     if (!grid->uniform) return explicit_face_neighbors(grid, cells, n, row, ids, dirs, cap, st);
     return face_neighbors_launch(grid->map, grid->params.periodic, UniformExists{grid->map}, cells, n, row, ids,
                                  dirs, cap, st);
@@ -542,6 +545,7 @@ int dccrgx_neighbors_to(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     const Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
+    const CallerStream fence(grid->ctx, st);
     if (!grid->uniform) return explicit_neighbors_to(grid, *h, cells, n, row, ids, cap, st);
     // candidates with hood_to on the device, unique + sort per cell on the host
     const UGeom& g = grid->g;

@@ -246,16 +246,23 @@ inline int mpi_exchange(void* user, int32_t ns, const int32_t* sp, const void* c
                         int32_t nr, const int32_t* rp, void* const* rb, const uint64_t* rn)
 {
     const MPI_Comm comm = *static_cast<const MPI_Comm*>(user);
+    // int counts: a message of 2 GiB or more goes as 1 GiB pieces in order
+    // (same source, tag and communicator: MPI keeps them in order)
+    const uint64_t piece = uint64_t(1) << 30;
     std::vector<MPI_Request> req;
     for (int32_t i = 0; i < nr; i++)
-        if (rn[i]) {
+        for (uint64_t o = 0; o < rn[i]; o += piece) {
             req.push_back(MPI_REQUEST_NULL);
-            if (MPI_Irecv(rb[i], (int)rn[i], MPI_BYTE, rp[i], 0, comm, &req.back()) != MPI_SUCCESS) return 1;
+            const int cnt = (int)std::min<uint64_t>(piece, rn[i] - o);
+            if (MPI_Irecv(static_cast<char*>(rb[i]) + o, cnt, MPI_BYTE, rp[i], 0, comm, &req.back()) != MPI_SUCCESS)
+                return 1;
         }
     for (int32_t i = 0; i < ns; i++)
-        if (sn[i]) {
+        for (uint64_t o = 0; o < sn[i]; o += piece) {
             req.push_back(MPI_REQUEST_NULL);
-            if (MPI_Isend(const_cast<void*>(sb[i]), (int)sn[i], MPI_BYTE, sp[i], 0, comm, &req.back()) != MPI_SUCCESS)
+            const int cnt = (int)std::min<uint64_t>(piece, sn[i] - o);
+            if (MPI_Isend(const_cast<char*>(static_cast<const char*>(sb[i])) + o, cnt, MPI_BYTE, sp[i], 0, comm,
+                          &req.back()) != MPI_SUCCESS)
                 return 1;
         }
     return MPI_Waitall((int)req.size(), req.data(), MPI_STATUSES_IGNORE) == MPI_SUCCESS ? 0 : 1;
@@ -804,15 +811,26 @@ public:
         partition_ = (uint8_t)partition;
         return *this;
     }
-    bool set_geometry(const typename Geometry::Parameters& p) { return geometry.set(p); }
-    int get_initial_partition() const { return partition_; }
-    // dccrg.hpp:1046-1064: the block partition is kept (Zoltan stays out of
-    // the device path), but like finish_balance_load the iteration caches are
-    // rebuilt (update_cell_pointers, :11453), so additional cell / neighbor
-    // items are updated again (e.g. a Center item after set_geometry)
-    Dccrg& balance_load(bool = true)
+    // dccrg.hpp:586-595: chained; throws when the geometry rejects the parameters
+    Dccrg& set_geometry(const typename Geometry::Parameters& p)
     {
-        if (!initialized_) return *this;  // weights stay: DCCRG_NO_LB skips initialize_balance_load's clear (:3839)
+        if (!geometry.set(p)) throw std::invalid_argument("Couldn't set geometry");
+        return *this;
+    }
+    int get_initial_partition() const { return partition_; }
+    // dccrg.hpp:1046-1064 as built with DCCRG_NO_LB (Zoltan stays out of the
+    // device path): the body is compiled out, so nothing moves and the
+    // iteration caches, additional items and references into `cells` stay
+    // as they are
+    Dccrg& balance_load(bool = true) { return *this; }
+    // facade extension, not in the reference: rebuild the iteration caches
+    // and run the additional items' update() again -- what a Zoltan build's
+    // balance_load does through update_cell_pointers (:4130-4144, :11453),
+    // e.g. to refresh a Center item after set_geometry.  Invalidates
+    // references into `cells`.
+    Dccrg& refresh_additional_items()
+    {
+        if (!initialized_) return *this;
         std::vector<int> ids;
         for (auto& kv : hoods_) ids.push_back(kv.first);
         for (int id : ids) build_hood(id);
@@ -1368,37 +1386,55 @@ public:
     {
         return hoods_.count(hood) ? hs(hood).remote_ids : std::vector<uint64_t>();
     }
-    // dccrg.hpp:6953-6975: the owner of every cell of the grid (built when
-    // called, from the replicated leaf set: as large as the grid) and the
-    // default neighborhood's boundary cells as sets
+    // dccrg.hpp:6953-6975: the owner of every cell of the grid (built from
+    // the replicated leaf set on the first call after a structural change,
+    // then kept: references stay valid until the next refine / load /
+    // neighborhood change) and the default neighborhood's boundary cells as
+    // sets.  A uniform grid never replicates cell_process, so a
+    // map of more than 2^27 cells is refused rather than built.
     const std::unordered_map<uint64_t, uint64_t>& get_cell_process() const
     {
+        if (cp_epoch_ == epoch_) return cell_process_;
+        size_t total = 0;
+        const int e = dccrgx_get_all_cells(grid_, nullptr, 0, &total);
+        detail::check(e == DCCRGX_ERANGE ? DCCRGX_OK : e, "get_all_cells");
+        if (total > (uint64_t(1) << 27))
+            throw std::length_error("get_cell_process: " + std::to_string(total) +
+                                    " cells; the map would be as large as the grid (owners are arithmetic: "
+                                    "get_process(cell))");
         const std::vector<uint64_t> all = get_all_cells();
         std::vector<int32_t> owner(all.size());
         if (!all.empty()) detail::check(dccrgx_get_process(grid_, all.data(), all.size(), owner.data()), "get_process");
         cell_process_.clear();
         cell_process_.reserve(all.size());
         for (size_t i = 0; i < all.size(); i++) cell_process_[all[i]] = uint64_t(owner[i]);
+        cp_epoch_ = epoch_;
         return cell_process_;
     }
     const std::unordered_set<uint64_t>& get_local_cells_on_process_boundary_internal() const
     {
-        const std::vector<uint64_t> v = get_local_cells_on_process_boundary();
-        local_bdy_ = std::unordered_set<uint64_t>(v.begin(), v.end());
+        if (lb_epoch_ != epoch_) {
+            const std::vector<uint64_t> v = get_local_cells_on_process_boundary();
+            local_bdy_ = std::unordered_set<uint64_t>(v.begin(), v.end());
+            lb_epoch_ = epoch_;
+        }
         return local_bdy_;
     }
     const std::unordered_set<uint64_t>& get_remote_cells_on_process_boundary_internal() const
     {
-        const std::vector<uint64_t> v = get_remote_cells_on_process_boundary();
-        remote_bdy_ = std::unordered_set<uint64_t>(v.begin(), v.end());
+        if (rb_epoch_ != epoch_) {
+            const std::vector<uint64_t> v = get_remote_cells_on_process_boundary();
+            remote_bdy_ = std::unordered_set<uint64_t>(v.begin(), v.end());
+            rb_epoch_ = epoch_;
+        }
         return remote_bdy_;
     }
-    // the three-phase balance_load (:3745-4150) as built with DCCRG_NO_LB: no
-    // cell moves, so nothing is added or removed; finishing rebuilds the
-    // iteration caches like balance_load
+    // the three-phase balance_load (:3745-4150) as built with DCCRG_NO_LB
+    // (:3982-4181 compiled out): no cell moves, nothing is added or removed,
+    // the caches stay
     Dccrg& initialize_balance_load(bool = true) { return *this; }
     Dccrg& continue_balance_load() { return *this; }
-    Dccrg& finish_balance_load() { return balance_load(); }
+    Dccrg& finish_balance_load() { return *this; }
     const std::unordered_set<uint64_t>& get_cells_added_by_balance_load() const { return no_cells_; }
     const std::unordered_set<uint64_t>& get_cells_removed_by_balance_load() const { return no_cells_; }
     // :3320-3390: an ASCII legacy-VTK unstructured grid of this rank's leaf
@@ -1454,6 +1490,7 @@ public:
         if (id == default_neighborhood_id) return *this;
         detail::check(dccrgx_remove_neighborhood(grid_, id), "remove_neighborhood");
         hoods_.erase(id);
+        ++epoch_;
         user_hood_of_.erase(id);
         user_hood_to_.erase(id);
         return *this;
@@ -1481,6 +1518,8 @@ public:
     // send / receive lists per process
     const std::unordered_map<int, std::unordered_set<uint64_t>>& get_user_local_cells_on_process_boundary() const
     {
+        if (ulb_epoch_ == epoch_) return user_local_bdy_;
+        ulb_epoch_ = epoch_;
         user_local_bdy_.clear();
         for (const auto& kv : hoods_)
             if (kv.first != default_neighborhood_id) {
@@ -1491,6 +1530,8 @@ public:
     }
     const std::unordered_map<int, std::unordered_set<uint64_t>>& get_user_remote_cells_on_process_boundary() const
     {
+        if (urb_epoch_ == epoch_) return user_remote_bdy_;
+        urb_epoch_ = epoch_;
         user_remote_bdy_.clear();
         for (const auto& kv : hoods_)
             if (kv.first != default_neighborhood_id)
@@ -1760,6 +1801,7 @@ private:
     // neighbors per cell as std::set-ordered [only_of][both][only_to]
     void build_hood(int hood)
     {
+        ++epoch_;  // the cached sets of the getters below are rebuilt on their next call
         HoodState S;
         const auto inner = query_cells(hood, DCCRGX_CELLS_INNER);
         const auto outer = query_cells(hood, DCCRGX_CELLS_OUTER);
@@ -1958,6 +2000,9 @@ private:
     // the user-neighborhood views, refreshed by their accessors
     mutable std::unordered_map<int, std::unordered_set<uint64_t>> user_local_bdy_, user_remote_bdy_;
     mutable std::unordered_map<uint64_t, uint64_t> cell_process_;
+    uint64_t epoch_ = 0;  // structural changes (build_hood, remove_neighborhood)
+    mutable uint64_t cp_epoch_ = ~uint64_t(0), lb_epoch_ = ~uint64_t(0), rb_epoch_ = ~uint64_t(0),
+                     ulb_epoch_ = ~uint64_t(0), urb_epoch_ = ~uint64_t(0);
     mutable std::unordered_set<uint64_t> local_bdy_, remote_bdy_;
     const std::unordered_set<uint64_t> no_cells_{};
     mutable std::unordered_map<int, std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>> user_send_,

@@ -13,7 +13,11 @@
  *    the ABI; dccrgx_last_error() returns a thread-local message;
  *  - plain pointers and sizes only; "_dev" pointers are HIP device memory,
  *    "_host" pointers are host memory; streams are hipStream_t passed as void*
- *    (NULL = the context's compute stream);
+ *    (NULL = the context's compute stream); work the library queues on a
+ *    caller's stream is ordered before the library's later frees, rebuilds
+ *    and destroys (the compute stream waits for it), but the caller's OWN
+ *    kernels that read grid memory (dccrgx_field_device_ptr) must be
+ *    synchronised by the caller before a structural or destroy call;
  *  - thread-compatible, not thread-safe: one context per host thread;
  *  - device memory of a grid is owned by the grid (SoA field pools).
  */
@@ -253,6 +257,8 @@ int dccrgx_get_peer_cells(const dccrgx_grid* grid, int32_t hood_id, int32_t send
  * remote_neighbors unordered_maps, dccrg.hpp:7238, 7330).
  * ------------------------------------------------------------------------ */
 int dccrgx_field_create(dccrgx_grid* grid, uint32_t elem_bytes, int32_t* field_id_out);
+/* valid until the next structural call (refine, load) or, for an advection
+ * density field, the next dccrgx_advect_step (double-buffered) */
 int dccrgx_field_device_ptr(const dccrgx_grid* grid, int32_t field_id, void** ptr_out,
                             uint64_t* n_slots_out);
 /* slot of each cell id in every field (-1: no slot on this rank) */
@@ -414,7 +420,11 @@ int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccr
                                   uint64_t* to_refine, uint64_t* not_to_unrefine, uint64_t* to_unrefine, size_t cap,
                                   size_t counts[3]);
 /* one step of tests/advection/2d.cpp:321-390: density halo start, inner
- * fluxes, halo wait, outer fluxes, apply */
+ * fluxes, halo wait, outer fluxes, apply -- fused: each cell's face fluxes
+ * and the apply are one kernel writing the new density into a second buffer
+ * (the same additions in the same order as fluxes + apply, flux left 0), and
+ * the two density buffers swap.  The density field's device pointer
+ * (dccrgx_field_device_ptr) therefore changes on every step. */
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt);
 /* velocities and lengths of every local cell, adapter.hpp:304-314 /
  * initialize.hpp:50-58: Cartesian_Geometry get_length / get_center

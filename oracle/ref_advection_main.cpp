@@ -81,7 +81,11 @@ int main(int argc, char** argv)
     grid.set_initial_length({{n, n, 1}}).set_periodic(true, true, false);
     grid.initialize(comm).set_geometry(geom_params);
     const int balance_n = 25;  // 2d.cpp's default (:114-115)
-    grid.balance_load();       // :254-256
+    grid.balance_load();       // :254-256 (DCCRG_NO_LB: a no-op)
+    // the Center items were computed before set_geometry; the reference's
+    // Zoltan build refreshes them in balance_load (update_cell_pointers), the
+    // facade does it on request
+    grid.refresh_additional_items();
 
     const bool dbg = std::getenv("REF_ADVECTION_DEBUG") != nullptr;
     Cell::transfer_all_data = true;

@@ -361,7 +361,7 @@ static int coords()
         .set_periodic(true, false, false)
         .initialize(MPI_COMM_WORLD);
     // x from -1 (4 cells of 0.5), y from 0 (4 of 1), z from 0 (2 of 2)
-    if (!grid.set_geometry(dccrg::Cartesian_Geometry::Parameters({{-1, 0, 0}}, {{0.5, 1, 2}}))) abort();
+    grid.set_geometry(dccrg::Cartesian_Geometry::Parameters({{-1, 0, 0}}, {{0.5, 1, 2}}));
     auto want = [](bool ok, const char* what) {
         if (!ok) {
             std::fprintf(stderr, "FAIL %s\n", what);
@@ -456,6 +456,10 @@ template <class G> static void check_remote_copies(const G& grid, double factor,
         cell_process.size() != grid.get_all_cells().size() ||
         grid.get_local_cells_on_process_boundary_internal().size() != grid.get_local_cells_on_process_boundary().size())
         abort();
+    // the sets are kept between calls: a second call returns the same object
+    if (&grid.get_cell_process() != &cell_process || &grid.get_remote_cells_on_process_boundary_internal() != &remote ||
+        grid.get_cell_process().size() != cell_process.size())
+        abort();
     for (uint64_t c : remote) {
         const auto* d = grid[c];
         if (d == nullptr || double(d->data) != factor * double(cell_process.at(c)) ||
@@ -486,7 +490,16 @@ static int copy()
         .set_maximum_refinement_level(1)
         .set_periodic(true, false, false)
         .initialize(MPI_COMM_WORLD);
-    want(grid1.set_geometry(dccrg::Cartesian_Geometry::Parameters({{-1, 0, 0}}, {{0.5, 1, 2}})), "geometry");
+    grid1.set_geometry(dccrg::Cartesian_Geometry::Parameters({{-1, 0, 0}}, {{0.5, 1, 2}}));
+    {
+        bool threw = false;
+        try {
+            grid1.set_geometry(dccrg::Cartesian_Geometry::Parameters({{-1, 0, 0}}, {{-0.5, 1, 2}}));
+        } catch (const std::invalid_argument&) {
+            threw = true;
+        }
+        want(threw, "set_geometry rejects a negative cell length (dccrg.hpp:586-595 throws)");
+    }
     if (grid1.is_local(456)) grid1.refine_completely(456);
     grid1.stop_refining();
     const std::vector<dccrg::Types<3>::neighborhood_item_t> items{{{0, 0, -1}}, {{0, 0, 1}}, {{1, 0, 0}}};
@@ -815,8 +828,11 @@ static int items()
             const_cast<uint64_t&>(cell.additional_cell_data4) = dccrg::error_cell;
             const_cast<double&>(cell.d1) -= 3;
         }
-        grid.balance_load();
-        check("cell items updated again by balance_load");
+        grid.balance_load();  // DCCRG_NO_LB: a no-op, the items keep what was written
+        for (const auto& cell : grid.cells)
+            want(cell.additional_cell_data1 == dccrg::error_cell, "balance_load left the cell items alone");
+        grid.refresh_additional_items();
+        check("cell items updated again by refresh_additional_items");
     }
     {  // neighbor_data1.cpp
         dccrg::Dccrg<empty_cell, dccrg::No_Geometry, std::tuple<>, std::tuple<ani_defaults>> grid;
@@ -893,7 +909,7 @@ static int vtk(int argc, char** argv)
     dccrg::Dccrg<int, dccrg::Cartesian_Geometry> grid;
     grid.set_initial_length({3, 2, 1}).set_neighborhood_length(1).set_maximum_refinement_level(1).initialize(
         MPI_COMM_WORLD);
-    if (!grid.set_geometry(dccrg::Cartesian_Geometry::Parameters({{-1, 0, 0}}, {{0.5, 1, 2}}))) abort();
+    grid.set_geometry(dccrg::Cartesian_Geometry::Parameters({{-1, 0, 0}}, {{0.5, 1, 2}}));
     if (grid.is_local(2)) grid.refine_completely(2);
     grid.stop_refining();
     grid.initialize_balance_load(true);

@@ -275,12 +275,15 @@ def sc_advection(ctx):
     for s in range(steps):
         g.update_copies_of_remote_neighbors(fields=["density"])
         sets = A.check_for_adaptation(g, rel / M, thr, sens)
-        g.start_remote_neighbor_copy_updates(fields=["density"])
-        g.calculate_fluxes(cfl * dt, True)
-        g.wait_remote_neighbor_copy_update_receives()
-        g.calculate_fluxes(cfl * dt, False)
-        g.wait_remote_neighbor_copy_update_sends()
-        g.apply_fluxes()
+        if s % 2:  # the fused step (one kernel per region, double-buffered density)
+            g.advect_step(cfl * dt)
+        else:  # the reference's calls one by one (2d.cpp:321-390)
+            g.start_remote_neighbor_copy_updates(fields=["density"])
+            g.calculate_fluxes(cfl * dt, True)
+            g.wait_remote_neighbor_copy_update_receives()
+            g.calculate_fluxes(cfl * dt, False)
+            g.wait_remote_neighbor_copy_update_sends()
+            g.apply_fluxes()
         A.adapt_grid(g, geom, *sets)
         dt = dt_min()
         ref.step()

@@ -89,6 +89,37 @@ def test_advection_parity(case, P):
         assert np.all(g.read_local("flux") == 0)
 
 
+@pytest.mark.parametrize("case", CASES)
+def test_fused_step_equals_fluxes_then_apply(case):
+    """dccrgx_advect_step (one kernel writing the new density into the other
+    buffer) against calculate_fluxes(all) + apply_fluxes: bit-identical
+    densities, flux 0 afterwards, also when flux starts non-zero; remote
+    ghost copies and the buffer swap survive many steps."""
+    uniform = case[4] is None
+    lists, (a,) = build(case, 1)
+    _, (b,) = build(case, 1)
+    state = O.advection_initial_state(O.Mapping(case[0], case[1]), lists.cells)
+    rng = np.random.default_rng(7)
+    flux0 = rng.standard_normal(len(lists.cells)) * 1e-3
+    for g in (a, b):
+        for name, arr in zip(NAMES, state):
+            g.write_local(name, arr)
+        g.write_local("flux", flux0)
+        exchange([g], NAMES, uniform)
+    dt = 0.5 * lists.max_time_step(state)
+    for k in range(7):
+        a.advect_step(dt)
+        b.update_copies_of_remote_neighbors(fields=["density"])
+        b.calculate_fluxes(dt, True, region=D._capi.REGION_ALL)
+        b.apply_fluxes()
+        da, db = a.read_local("density"), b.read_local("density")
+        assert np.array_equal(da, db), k
+        assert np.all(a.read_local("flux") == 0)
+        assert np.array_equal(a.read_remote("density"), b.read_remote("density"))
+    for g in (a, b):
+        g.close()
+
+
 def test_advection_mass_conserved_large():
     """Size-independent property at a larger size: 256 x 256 periodic, 20
     steps, total mass conserved to 1e-12 relative."""
