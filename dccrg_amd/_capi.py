@@ -13,6 +13,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdccrgx.so")
 
 DCCRGX_OK = 0
+DCCRGX_ENOMEM = 2
+DCCRGX_ESTATE = 6
 ERROR_CELL = 0
 ERROR_INDEX = 0xFFFFFFFFFFFFFFFF
 DEFAULT_NEIGHBORHOOD_ID = -0xDCC
@@ -178,6 +180,8 @@ SIGNATURES = {
     "dccrgx_dont_refine": (C.c_int, [_vp, C.c_uint64, _i32p]),
     "dccrgx_amr_requests": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _szp]),
     "dccrgx_stop_refining": (C.c_int, [_vp, C.POINTER(_u64p), _szp, _szp]),
+    "dccrgx_stop_refining_prepare": (C.c_int, [_vp, C.POINTER(_u64p), _szp, _szp]),
+    "dccrgx_stop_refining_finish": (C.c_int, [_vp, C.c_int32]),
     "dccrgx_get_new_cells": (C.c_int, [_vp, _u64p, C.c_size_t, _szp]),
     "dccrgx_get_removed_cells": (C.c_int, [_vp, _u64p, C.c_size_t, _szp]),
     "dccrgx_clear_refined_unrefined_data": (C.c_int, [_vp]),

@@ -27,6 +27,8 @@
 #include <algorithm>
 #include <cstring>
 #include <unordered_set>
+#include <cstdlib>
+#include <memory>
 
 #include "face.hpp"
 #include "grid.hpp"
@@ -263,12 +265,52 @@ __global__ void __launch_bounds__(256) k_level0_ids(uint64_t* __restrict__ out, 
 // Rebuild the grid on an ascending leaf list: device leaf state, every
 // neighborhood (which defines the ghost slots), and every field moved to the
 // new slots.  `retired` cells (ascending, local) get slots after the ghosts
-// and keep their old data.  Transactional: the new state and every new field
-// array are built first; on any failure they are freed and the old grid is
-// left exactly as it was.
-int rebuild(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired,
-            uint64_t* d_leaves = nullptr,  // leaves: moved into the grid
-            const uint32_t* gone_flags = nullptr)  // per old leaf, AMR_FLAG_GONE: lists rebuilt around the change
+// and keep their old data.  Transactional in two phases: rebuild_prepare
+// builds the new state and every new field array aside (the grid stays the
+// old one meanwhile; on failure everything new is freed), rebuild_commit
+// adopts it, rebuild_abort drops it.  Between the two every rank of a
+// collective stop_refining learns whether all ranks built theirs.
+void rebuild_abort(RebuildTxn& t)
+{
+    for (void* q : t.np) dx_free(q);
+    t.np.clear();
+    for (auto& kv : t.hoods) free_hood(kv.second);
+    t.hoods.clear();
+    explicit_free(t.ex);
+    t.ex = nullptr;
+}
+
+void rebuild_commit(dccrgx_grid* grid, RebuildTxn& t)
+{
+    Explicit* old_ex = grid->ex;
+    std::map<int32_t, Hood> old_hoods;
+    old_hoods.swap(grid->hoods);
+    grid->hoods.swap(t.hoods);
+    grid->ex = t.ex;
+    t.ex = nullptr;
+    grid->uniform = t.uniform;
+    grid->n_local = t.n_local;
+    grid->first_local = t.first_local;
+    grid->n_slots = t.n_slots;
+    // the old arrays become the spares of the next rebuild
+    for (auto& b : grid->spare_bufs) dx_free(b.first);
+    grid->spare_bufs.clear();
+    for (size_t i = 0; i < grid->fields.size(); i++) {
+        Field& F = grid->fields[i];
+        if (F.ptr) grid->spare_bufs.emplace_back(F.ptr, F.cap_bytes ? F.cap_bytes : t.old_n_slots * F.elem);
+        F.ptr = t.np[i];
+        F.cap_bytes = t.cap[i];
+    }
+    t.np.clear();
+    for (auto& kv : old_hoods) free_hood(kv.second);
+    explicit_recycle(grid, old_ex);
+    if (grid->amr) grid->amr->dev_current = false;  // request flags were over the old leaves
+}
+
+int rebuild_prepare(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired,
+                    uint64_t* d_leaves,  // leaves: moved into the new state
+                    const uint32_t* gone_flags,  // per old leaf, AMR_FLAG_GONE: lists rebuilt around the change
+                    RebuildTxn& t)
 {
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
@@ -390,20 +432,33 @@ int rebuild(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<
     }
     if (hipStreamSynchronize(st) != hipSuccess) return fail(set_error(DCCRGX_EHIP, "moving field data failed"));
     dx_free(d_from);
-    // commit; the old arrays become the spares of the next rebuild
-    for (auto& b : grid->spare_bufs) dx_free(b.first);
-    grid->spare_bufs.clear();
-    for (size_t i = 0; i < grid->fields.size(); i++) {
-        Field& F = grid->fields[i];
-        if (F.ptr) grid->spare_bufs.emplace_back(F.ptr, F.cap_bytes ? F.cap_bytes : old.n_slots * F.elem);
-        F.ptr = np[i];
-        F.cap_bytes = cap[i];
-    }
-    for (auto& kv : old_hoods) free_hood(kv.second);
-    explicit_recycle(grid, old.ex);
-    old.ex = nullptr;
-    if (grid->amr) grid->amr->dev_current = false;  // request flags were over the old leaves
+    // the new state goes aside; the grid is the old one until the commit
+    t.ex = grid->ex;
+    t.hoods.clear();
+    t.hoods.swap(grid->hoods);
+    t.uniform = grid->uniform;
+    t.n_local = grid->n_local;
+    t.first_local = grid->first_local;
+    t.n_slots = grid->n_slots;
+    t.old_n_slots = old.n_slots;
+    t.np.swap(np);
+    t.cap.swap(cap);
+    grid->hoods.swap(old_hoods);
+    grid->ex = old.ex;
+    grid->uniform = old.uniform;
+    grid->n_local = old.n_local;
+    grid->first_local = old.first_local;
+    grid->n_slots = old.n_slots;
     T.lap("fields moved");
+    return DCCRGX_OK;
+}
+
+int rebuild(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired,
+            uint64_t* d_leaves = nullptr, const uint32_t* gone_flags = nullptr)
+{
+    RebuildTxn t;
+    DX_TRY(rebuild_prepare(grid, leaves, retired, d_leaves, gone_flags, t));
+    rebuild_commit(grid, t);
     return DCCRGX_OK;
 }
 
@@ -446,12 +501,40 @@ int ensure_explicit(dccrgx_grid* grid)
     return rebuild(grid, leaves, {});
 }
 
+// DCCRGX_TEST_FAIL_STOP_REFINING=<rank>: the decisions of that rank's next
+// stop_refining report ENOMEM (the collective two-phase tests)
+bool amr_fail_injected(const dccrgx_grid* grid)
+{
+    const char* e = getenv("DCCRGX_TEST_FAIL_STOP_REFINING");
+    return e && *e && atoi(e) == grid->ctx->rank;
+}
+
 }  // namespace
+
+// stop_refining between prepare and finish: the rebuild held aside, the
+// request flags before the decisions, and (when the caller passed the union of
+// every rank's sets) this rank's own sets
+struct StopTxn {
+    RebuildTxn rb;
+    bool rebuilt = false;  // rb holds a new grid state
+    bool noop = false;     // a uniform grid without refines or unrefines
+    uint32_t* d_saved = nullptr;
+    bool from_sets = false;
+    FlatSet saved[4];
+    std::vector<uint64_t> nr;  // the new dont_refine closure
+};
 
 int amr_ensure_explicit(dccrgx_grid* grid) { return ensure_explicit(grid); }
 
 void amr_destroy(dccrgx_grid* grid)
 {
+    if (grid->amr && grid->amr->pending) {
+        StopTxn* X = grid->amr->pending;
+        grid->amr->pending = nullptr;
+        if (X->rebuilt) rebuild_abort(X->rb);
+        ds_free(X->d_saved, grid->ctx->compute);
+        delete X;
+    }
     delete grid->amr;
     grid->amr = nullptr;
 }
@@ -651,17 +734,25 @@ int dccrgx_amr_requests(const dccrgx_grid* grid, int32_t which, uint64_t* ids, s
     return DCCRGX_OK;
 }
 
-int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const size_t* counts, size_t* n_new)
+int dccrgx_stop_refining_prepare(dccrgx_grid* grid, const uint64_t* const* sets, const size_t* counts,
+                                 size_t* n_new)
 {
     DX_CHECK(grid && (!sets || counts), DCCRGX_EINVAL, "null argument");
     if (sets)
         for (int k = 0; k < 4; k++) DX_CHECK(sets[k] || !counts[k], DCCRGX_EINVAL, "null request set %d", k);
     Amr& A = amr_of(grid);
-    A.new_cells.clear();
-    A.removed.clear();
+    DX_CHECK(!A.pending, DCCRGX_ESTATE, "a prepared stop_refining awaits dccrgx_stop_refining_finish");
     if (n_new) *n_new = 0;
     PhaseTimer T("stop_refining");
+    auto txn = std::unique_ptr<StopTxn>(new StopTxn());
+    StopTxn& X = *txn;
     if (sets) {  // the union of every rank's requests (dccrg.hpp:10130-10236 gathers them)
+        DX_TRY(amr_host_sync(grid));
+        X.from_sets = true;
+        X.saved[0] = A.to_refine;
+        X.saved[1] = A.not_to_refine;
+        X.saved[2] = A.to_unrefine;
+        X.saved[3] = A.not_to_unrefine;
         A.to_refine = FlatSet(sets[0], sets[0] + counts[0]);
         A.not_to_refine = FlatSet(sets[1], sets[1] + counts[1]);
         A.to_unrefine = FlatSet(sets[2], sets[2] + counts[2]);
@@ -669,63 +760,126 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
         A.host_current = true;
         A.dev_current = false;
     }
+    // a failure before anything was decided: this rank's requests as they were
+    auto unwind_sets = [&](int code) {
+        if (X.from_sets) {
+            A.to_refine = std::move(X.saved[0]);
+            A.not_to_refine = std::move(X.saved[1]);
+            A.to_unrefine = std::move(X.saved[2]);
+            A.not_to_unrefine = std::move(X.saved[3]);
+            A.host_current = true;
+            A.dev_current = false;
+        }
+        return code;
+    };
     if (grid->uniform) {  // requests of a uniform grid live on the host (amr_dev.hip: explicit grids)
         if (A.to_refine.empty() && A.to_unrefine.empty()) {
             // nothing can change; on a level-0 grid the dont_refine closure is
             // the set itself, and it persists (:10188)
-            A.to_refine.clear();
-            A.not_to_unrefine.clear();
+            X.nr = A.not_to_refine.sorted();
+            X.noop = true;
+            A.pending = txn.release();
             return DCCRGX_OK;
         }
-        DX_TRY(ensure_explicit(grid));
+        const int e = ensure_explicit(grid);  // the same leaves in the explicit layout
+        if (e != DCCRGX_OK) return unwind_sets(e);
     }
     // override_refines (:10130-10236), induce_refines (:9730-9907),
     // override_unrefines (:9935-10124) and the new leaf set of
     // execute_refines (:10243-10693), on the device
     uint64_t* d_leaves = nullptr;
     uint64_t n_leaves = 0;
-    std::vector<uint64_t> leaves, retired, nr;
+    std::vector<uint64_t> leaves, retired;
     // the leaf list of two rebuilds ago lends its storage: a fresh 8 B-per-leaf
     // vector page-faults on first touch every step
     if (grid->spare_host) leaves.swap(grid->spare_host->leaves);
     bool changed = false;
-    // the request flags before the decisions: restored if the rebuild fails,
-    // so the requests stay pending
-    DX_TRY(amr_dev_sync(grid));
+    // the request flags before the decisions: restored if the rebuild fails
+    // or another rank's does, so the requests stay pending
+    int e = amr_dev_sync(grid);
+    if (e != DCCRGX_OK) return unwind_sets(e);
     hipStream_t st = grid->ctx->compute;
-    uint32_t* d_saved = nullptr;
-    DX_HIP(ds_malloc(&d_saved, std::max<uint64_t>(A.flags_n, 1) * 4, st));
-    DX_HIP(hipMemcpyAsync(d_saved, A.d_flags, A.flags_n * 4, hipMemcpyDeviceToDevice, st));
-    auto restore = [&](int code) {
-        (void)hipMemcpyAsync(A.d_flags, d_saved, A.flags_n * 4, hipMemcpyDeviceToDevice, st);
-        ds_free(d_saved, st);
-        A.dev_current = true;
-        A.new_cells.clear();
-        A.removed.clear();
-        return code;
-    };
-    int s = amr_dev_decide(grid, &d_leaves, &n_leaves, leaves, retired, nr, &changed);
-    if (s != DCCRGX_OK) return restore(s);
-    T.lap("decisions");
-    if (changed) {
-        // the previous round's refined / unrefined data goes first, as in
-        // execute_refines (dccrg.hpp:10266-10267)
-        explicit_clear_retired(grid->ex);
-        // transactional: on failure the grid is unchanged; the flags mark the old leaves that go
-        s = rebuild(grid, leaves, retired, d_leaves, A.flags_n == grid->ex->n ? A.d_flags : nullptr);
-        if (s != DCCRGX_OK) return restore(s);
+    if (ds_malloc(&X.d_saved, std::max<uint64_t>(A.flags_n, 1) * 4, st) != hipSuccess)
+        return unwind_sets(set_error(DCCRGX_ENOMEM, "out of device memory for the request flags"));
+    (void)hipMemcpyAsync(X.d_saved, A.d_flags, A.flags_n * 4, hipMemcpyDeviceToDevice, st);
+    A.pending = txn.release();
+    int s = amr_dev_decide(grid, &d_leaves, &n_leaves, leaves, retired, X.nr, &changed);
+    if (s == DCCRGX_OK && amr_fail_injected(grid)) {
+        ds_free(d_leaves, st);
+        s = set_error(DCCRGX_ENOMEM, "DCCRGX_TEST_FAIL_STOP_REFINING: injected failure on rank %d", grid->ctx->rank);
     }
-    ds_free(d_saved, st);
-    // the dont_refine closure persists (:10178), everything else is consumed
-    A.to_refine.clear();
-    A.to_unrefine.clear();
-    A.not_to_unrefine.clear();
-    A.not_to_refine = FlatSet(nr.data(), nr.data() + nr.size());
-    A.host_current = true;
-    A.dev_current = false;
-    T.lap("rebuild");
+    T.lap("decisions");
+    if (s == DCCRGX_OK && changed) {
+        // transactional: on failure the grid is unchanged; the flags mark the old leaves that go
+        s = rebuild_prepare(grid, leaves, retired, d_leaves, A.flags_n == grid->ex->n ? A.d_flags : nullptr, X.rb);
+        X.rebuilt = s == DCCRGX_OK;
+    }
+    if (s != DCCRGX_OK) {
+        (void)dccrgx_stop_refining_finish(grid, 0);
+        return s;
+    }
+    T.lap("rebuild prepared");
     if (n_new) *n_new = A.new_cells.size();
     return DCCRGX_OK;
+}
+
+int dccrgx_stop_refining_finish(dccrgx_grid* grid, int32_t commit)
+{
+    DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    Amr* Ap = grid->amr;
+    if (!Ap || !Ap->pending) {
+        // nothing prepared: this rank's prepare failed (and unwound) -- the
+        // abort every rank then makes is a no-op here
+        DX_CHECK(!commit, DCCRGX_ESTATE, "no prepared stop_refining to commit");
+        return DCCRGX_OK;
+    }
+    Amr& A = *Ap;
+    std::unique_ptr<StopTxn> txn(A.pending);
+    A.pending = nullptr;
+    StopTxn& X = *txn;
+    hipStream_t st = grid->ctx->compute;
+    if (commit) {
+        if (X.rebuilt) rebuild_commit(grid, X.rb);
+        ds_free(X.d_saved, st);
+        // the dont_refine closure persists (:10178), everything else is consumed
+        A.to_refine.clear();
+        A.to_unrefine.clear();
+        A.not_to_unrefine.clear();
+        A.not_to_refine = FlatSet(X.nr.data(), X.nr.data() + X.nr.size());
+        A.host_current = true;
+        A.dev_current = false;
+        if (X.noop) {
+            A.new_cells.clear();
+            A.removed.clear();
+        }
+        return DCCRGX_OK;
+    }
+    // abort: the grid stays the old one, every request stays pending
+    if (X.rebuilt) rebuild_abort(X.rb);
+    A.new_cells.clear();
+    A.removed.clear();
+    if (X.from_sets) {
+        A.to_refine = std::move(X.saved[0]);
+        A.not_to_refine = std::move(X.saved[1]);
+        A.to_unrefine = std::move(X.saved[2]);
+        A.not_to_unrefine = std::move(X.saved[3]);
+        A.host_current = true;
+        A.dev_current = false;
+        ds_free(X.d_saved, st);
+    } else if (X.d_saved) {
+        (void)hipMemcpyAsync(A.d_flags, X.d_saved, A.flags_n * 4, hipMemcpyDeviceToDevice, st);
+        ds_free(X.d_saved, st);
+        A.dev_current = true;
+        A.host_current = false;
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    return DCCRGX_OK;
+}
+
+int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const size_t* counts, size_t* n_new)
+{
+    DX_TRY(dccrgx_stop_refining_prepare(grid, sets, counts, n_new));
+    return dccrgx_stop_refining_finish(grid, 1);
 }
 
 int dccrgx_get_new_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, size_t* n)

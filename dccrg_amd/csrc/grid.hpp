@@ -249,6 +249,9 @@ struct Explicit {
     uint64_t n_ret = 0;
 };
 
+// stop_refining between its two phases (amr.hip)
+struct StopTxn;
+
 // pending refinement requests of this rank and the results of the last
 // stop_refining (dccrg.hpp:7355-7360, 3483-3543)
 struct LoadState;
@@ -265,6 +268,7 @@ struct Amr {
     std::vector<uint64_t> nr_other;
     bool host_current = true, dev_current = false;
     bool dev_unrefines = true;  // the flags may hold cells_to_unrefine (else erasing them is skipped)
+    StopTxn* pending = nullptr;  // a prepared stop_refining awaiting commit or abort
     ~Amr() { (void)dx_free(d_flags); }
 };
 // amr_dev.hip
@@ -343,6 +347,18 @@ struct Hood {
     uint32_t* d_st_slot = nullptr;
     int32_t* d_st_off = nullptr;     // x, y, z offset of each stencil entry
     std::shared_ptr<FaceCache> faces;  // advection face lists (explicit grids)
+};
+
+// a rebuild built but not yet adopted (amr.hip rebuild_prepare): the new leaf
+// state, neighborhoods and field arrays, held aside while the grid is still
+// the old one
+struct RebuildTxn {
+    Explicit* ex = nullptr;
+    std::map<int32_t, Hood> hoods;
+    bool uniform = false;
+    uint64_t n_local = 0, first_local = 0, n_slots = 0, old_n_slots = 0;
+    std::vector<void*> np;    // new array of each field
+    std::vector<size_t> cap;  // its capacity in bytes
 };
 
 }  // namespace dccrgx

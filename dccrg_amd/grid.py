@@ -25,6 +25,28 @@ from ._capi import check, lib
 DEFAULT_NEIGHBORHOOD_ID = X.DEFAULT_NEIGHBORHOOD_ID
 
 
+def _dist_ready() -> bool:
+    try:
+        import torch.distributed as dist
+        return dist.is_available() and dist.is_initialized()
+    except ImportError:
+        return False
+
+
+def stop_refining_all(grids, all_requests):
+    """The collective stop_refining of several ranks held in one process (the
+    tests' in-process ranks): every grid prepares, then all commit or, when
+    any failed, all keep the old grid with the requests pending."""
+    res = [g.stop_refining_prepare(all_requests) for g in grids]
+    ok = all(st == X.DCCRGX_OK for st, _ in res)
+    for g in grids:
+        g.stop_refining_finish(ok)
+    for st, err in res:
+        if st != X.DCCRGX_OK:
+            raise X.DccrgxError(st, err)
+    return [g.get_new_cells() for g in grids]
+
+
 def _u64(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.uint64)
 
@@ -349,27 +371,53 @@ class Dccrg:
     def stop_refining(self, sorted: bool = True, all_requests=None) -> np.ndarray:
         """Collective (dccrg.hpp:3483-3507).  all_requests: the union over all
         ranks of amr_requests(); gathered with torch.distributed when the
-        grid has several ranks and it is not given."""
-        if all_requests is None and self.ctx.comm_size == 1:
-            # one rank: its own requests are the union (they stay on the device)
-            n_new = C.c_size_t()
-            check(lib().dccrgx_stop_refining(self._h, None, None, C.byref(n_new)))
-            self._refresh_info()
-            return self.get_new_cells()
-        if all_requests is None:
+        grid has several ranks and it is not given.  Two phases: every rank
+        prepares its new grid, the statuses are all-reduced (torch.distributed,
+        when initialised), and all ranks adopt or all keep the old grid with
+        the requests pending -- a failure on any rank raises on every rank."""
+        multi = self.ctx.comm_size > 1
+        if multi and all_requests is None:
             import torch.distributed as dist
             mine = self.amr_requests()
             got = [None] * self.ctx.comm_size
             dist.all_gather_object(got, [a.tolist() for a in mine])
             all_requests = [np.unique(np.concatenate([np.asarray(g[k], dtype=np.uint64) for g in got]))
                             for k in range(4)]
-        sets = [_u64(a) for a in all_requests]
-        ptrs = (X._u64p * 4)(*[a.ctypes.data_as(X._u64p) for a in sets])
-        counts = (C.c_size_t * 4)(*[a.size for a in sets])
-        n_new = C.c_size_t()
-        check(lib().dccrgx_stop_refining(self._h, ptrs, counts, C.byref(n_new)))
-        self._refresh_info()
+        st, err = self.stop_refining_prepare(all_requests)
+        ok = st == X.DCCRGX_OK
+        all_ok = ok
+        if multi and _dist_ready():
+            import torch
+            import torch.distributed as dist
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            all_ok = bool(t.item())
+        self.stop_refining_finish(all_ok)
+        if not ok:
+            raise X.DccrgxError(st, err)
+        if not all_ok:
+            raise X.DccrgxError(X.DCCRGX_ESTATE, "stop_refining failed on another rank; requests stay pending")
         return self.get_new_cells()
+
+    def stop_refining_prepare(self, all_requests=None):
+        """Phase one (dccrgx_stop_refining_prepare): (status, error message);
+        the grid stays the old one until stop_refining_finish."""
+        n_new = C.c_size_t()
+        if all_requests is None:  # this rank's own requests (they stay on the device)
+            st = lib().dccrgx_stop_refining_prepare(self._h, None, None, C.byref(n_new))
+        else:
+            sets = [_u64(a) for a in all_requests]
+            ptrs = (X._u64p * 4)(*[a.ctypes.data_as(X._u64p) for a in sets])
+            counts = (C.c_size_t * 4)(*[a.size for a in sets])
+            st = lib().dccrgx_stop_refining_prepare(self._h, ptrs, counts, C.byref(n_new))
+        err = lib().dccrgx_last_error().decode(errors="replace") if st != X.DCCRGX_OK else ""
+        return st, err
+
+    def stop_refining_finish(self, commit: bool):
+        """Phase two: adopt the prepared grid (commit) or drop it."""
+        check(lib().dccrgx_stop_refining_finish(self._h, 1 if commit else 0))
+        self._refresh_info()
+        return self
 
     def get_new_cells(self) -> np.ndarray:
         return self._id_list(lib().dccrgx_get_new_cells)

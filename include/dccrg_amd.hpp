@@ -1128,14 +1128,17 @@ public:
         const uint64_t* ptrs[4] = {sets[0].data(), sets[1].data(), sets[2].data(), sets[3].data()};
         const size_t counts[4] = {sets[0].size(), sets[1].size(), sets[2].size(), sets[3].size()};
         size_t n_new = 0;
-        // every rank must reach the same leaf set: a rank whose rebuild failed
-        // (it keeps its old grid) takes all ranks down, as the reference aborts
-        const int st = dccrgx_stop_refining(grid_, ptrs, counts, &n_new);
+        // every rank must reach the same leaf set: each builds its new grid
+        // aside, the statuses are all-reduced, and all ranks adopt theirs or
+        // all keep the old grid with the requests pending
+        const int st = dccrgx_stop_refining_prepare(grid_, ptrs, counts, &n_new);
+        const std::string err = st == DCCRGX_OK ? std::string() : std::string(dccrgx_last_error());
         int ok = st == DCCRGX_OK ? 1 : 0, all_ok = 0;
         MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_MIN, comm_);
+        detail::check(dccrgx_stop_refining_finish(grid_, all_ok), "stop_refining_finish");
         if (!all_ok)
             throw std::runtime_error(std::string("stop_refining failed on ") + (ok ? "another rank" : "this rank: ") +
-                                     (ok ? "" : dccrgx_last_error()));
+                                     err + "; the grid is unchanged and the requests stay pending");
         std::vector<uint64_t> created = id_list(dccrgx_get_new_cells);
         // data moves as execute_refines moves it (dccrg.hpp:10266-10267,
         // 10354-10375, 10526-10590): previous refined/unrefined data dropped,

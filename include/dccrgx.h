@@ -468,6 +468,18 @@ int dccrgx_amr_requests(const dccrgx_grid* grid, int32_t which, uint64_t* ids, s
  * created on this rank */
 int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const size_t* counts,
                          size_t* n_new);
+/* stop_refining in two phases, so that ranks agree before any of them adopts
+ * a new leaf set (the reference reaches agreement by All_Gather after each
+ * decision phase, dccrg.hpp:9730-10236, and aborts on failure).  prepare =
+ * the decisions and the complete new grid state built aside (the grid stays
+ * the old one; on failure everything is unwound and the requests stay
+ * pending); then every rank all-reduces its status and calls finish with
+ * commit = 1 (adopt) when all ranks succeeded, else commit = 0 (drop: old
+ * grid, this rank's requests pending).  finish(0) without a prepared
+ * stop_refining is a no-op; dccrgx_stop_refining = prepare + finish(1). */
+int dccrgx_stop_refining_prepare(dccrgx_grid* grid, const uint64_t* const* sets, const size_t* counts,
+                                 size_t* n_new);
+int dccrgx_stop_refining_finish(dccrgx_grid* grid, int32_t commit);
 /* the cells the last stop_refining created on this rank (ascending; the
  * reference's return value of stop_refining(true)) */
 int dccrgx_get_new_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, size_t* n);

@@ -237,6 +237,53 @@ def sc_amr(ctx):
         g.close()
 
 
+def sc_amr_fail(ctx):
+    """The two-phase stop_refining: one rank's rebuild fails (injected
+    ENOMEM), every rank raises, keeps its old leaves and its own requests,
+    and the next stop_refining succeeds on all ranks with the oracle's result
+    (dccrg.hpp:3483-3507)."""
+    from oracle.dccrg_amr import AmrOracle
+    length, M, per, hood = (4, 4, 2), 2, (True, True, False), 1
+    o = AmrOracle(length, M, per, hood, P)
+    g = make(ctx, length, per, hood, M)
+    g.add_field("v", np.float64)
+    g.write_local("v", g.local_cells().astype(np.float64))
+    rng = np.random.default_rng(7)
+    for rnd in range(2):
+        cells = o.cells()
+        for c in rng.choice(cells, min(len(cells), 6), replace=False):
+            c = int(c)
+            r = o.owner(c)
+            fn = "refine_completely" if rnd == 0 else ("refine_completely", "unrefine_completely")[int(rng.integers(2))]
+            want = getattr(o, fn)(r, c)
+            if r == RANK:
+                assert getattr(g, fn)(c) == want, (fn, c)
+        before_local = [int(c) for c in g.local_cells()]
+        before_req = [a.tolist() for a in g.amr_requests()]
+        os.environ["DCCRGX_TEST_FAIL_STOP_REFINING"] = str(P - 1)
+        try:
+            g.stop_refining()
+            raise AssertionError("stop_refining did not fail")
+        except D.DccrgxError as e:
+            assert ("injected" in str(e)) == (RANK == P - 1), str(e)
+        finally:
+            del os.environ["DCCRGX_TEST_FAIL_STOP_REFINING"]
+        assert [int(c) for c in g.local_cells()] == before_local
+        assert [a.tolist() for a in g.amr_requests()] == before_req
+        assert np.array_equal(g.read_local("v"), g.local_cells().astype(np.float64))
+        new = g.stop_refining()
+        want = o.stop_refining()
+        assert [int(c) for c in new] == want[RANK]
+        g.clear_refined_unrefined_data()
+        allc = sorted(c for part in gather_all([int(c) for c in g.local_cells()]) for c in part)
+        assert allc == o.cells()
+        ref = o.grid.rank_view(RANK, P)
+        assert [int(c) for c in g.local_cells()] == ref["local"]
+        assert g.get_cells_to_send() == ref["send"] and g.get_cells_to_receive() == ref["recv"]
+        g.write_local("v", g.local_cells().astype(np.float64))
+    g.close()
+
+
 def sc_advection(ctx):
     """tests/advection/2d.cpp with adapt_n = 1: per-rank leaf sets and
     densities vs the oracle's P-rank run; dt reduced with MIN across ranks
@@ -345,7 +392,7 @@ def sc_poisson(ctx):
 
 
 SCENARIOS = {"gol": sc_gol, "gol_explicit": sc_gol_explicit, "halo_ids": sc_halo_ids, "variable": sc_variable,
-             "amr": sc_amr, "advection": sc_advection, "poisson": sc_poisson}
+             "amr": sc_amr, "amr_fail": sc_amr_fail, "advection": sc_advection, "poisson": sc_poisson}
 
 
 def main():

@@ -12,6 +12,7 @@ pytestmark = pytest.mark.gpu
 import dccrg_amd as D  # noqa: E402
 from oracle import dccrg_oracle as O  # noqa: E402
 from oracle.dccrg_amr import AmrOracle  # noqa: E402
+from dccrg_amd.grid import stop_refining_all  # noqa: E402
 
 
 def make_ranks(length, M, per, hood, P, leaves=None):
@@ -28,7 +29,7 @@ def make_ranks(length, M, per, hood, P, leaves=None):
 def stop_all(grids):
     reqs = [g.amr_requests() for g in grids]
     union = [np.unique(np.concatenate([r[k] for r in reqs])).astype(np.uint64) for k in range(4)]
-    return [g.stop_refining(all_requests=union) for g in grids]
+    return stop_refining_all(grids, union)
 
 
 def all_leaves(grids):
@@ -227,6 +228,53 @@ def test_own_requests_stop_refining(P):
         for r in range(P):
             assert [int(c) for c in got[r]] == want[r]
             grids[r].clear_refined_unrefined_data()
+        check_structure(grids, o)
+    for g in grids:
+        g.close()
+
+
+@pytest.mark.parametrize("P,fail_rank", [(1, 0), (2, 1), (3, 0)])
+def test_two_phase_stop_refining_failure(P, fail_rank, monkeypatch):
+    """One rank's stop_refining fails after its decisions (injected ENOMEM):
+    no rank adopts a new leaf set, every rank keeps its own requests and its
+    data, and the next stop_refining gives the oracle's result on all ranks
+    (the reference's collective decisions, dccrg.hpp:3483-3507).  P == 1 runs
+    the own-requests path (sets == NULL), P > 1 the union path."""
+    length, M, per, hood = (5, 4, 2), 2, (True, False, True), 1
+    rng = np.random.default_rng(11 + P)
+    o = AmrOracle(length, M, per, hood, P)
+    grids = make_ranks(length, M, per, hood, P)
+    for g in grids:
+        g.add_field("v", np.float64)
+        g.write_local("v", g.local_cells().astype(np.float64))
+    for rnd in range(3):
+        cells = o.cells()
+        for r in range(P):
+            mine = [c for c in cells if o.owner(c) == r]
+            ids = [int(c) for c in rng.choice(mine, min(len(mine), 5), replace=False)]
+            name, kind = KINDS[0] if rnd == 0 else KINDS[int(rng.integers(3))]
+            grids[r].request_cells(kind, np.array(ids, dtype=np.uint64))
+            for c in ids:
+                getattr(o, name)(r, c)
+        before = [[int(c) for c in g.local_cells()] for g in grids]
+        reqs = [[a.tolist() for a in g.amr_requests()] for g in grids]
+        monkeypatch.setenv("DCCRGX_TEST_FAIL_STOP_REFINING", str(fail_rank))
+        with pytest.raises(D.DccrgxError, match="injected"):
+            if P == 1:
+                grids[0].stop_refining()
+            else:
+                stop_all(grids)
+        monkeypatch.delenv("DCCRGX_TEST_FAIL_STOP_REFINING")
+        for r, g in enumerate(grids):
+            assert [int(c) for c in g.local_cells()] == before[r]
+            assert [a.tolist() for a in g.amr_requests()] == reqs[r]
+            assert np.array_equal(g.read_local("v"), g.local_cells().astype(np.float64))
+        got = [grids[0].stop_refining()] if P == 1 else stop_all(grids)
+        want = o.stop_refining()
+        for r in range(P):
+            assert [int(c) for c in got[r]] == want[r]
+            grids[r].clear_refined_unrefined_data()
+            grids[r].write_local("v", grids[r].local_cells().astype(np.float64))
         check_structure(grids, o)
     for g in grids:
         g.close()

@@ -14,7 +14,7 @@ import sys
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SCENARIOS = os.environ.get("MP_SCENARIOS", "gol,gol_explicit,halo_ids,variable,amr,advection,poisson").split(",")
+SCENARIOS = os.environ.get("MP_SCENARIOS", "gol,gol_explicit,halo_ids,variable,amr,amr_fail,advection,poisson").split(",")
 _RESULTS = {}
 
 
