@@ -180,6 +180,7 @@ SIGNATURES = {
     "dccrgx_dont_refine": (C.c_int, [_vp, C.c_uint64, _i32p]),
     "dccrgx_amr_requests": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _szp]),
     "dccrgx_stop_refining": (C.c_int, [_vp, C.POINTER(_u64p), _szp, _szp]),
+    "dccrgx_neighbor_list_stats": (C.c_int, [_vp, C.c_int32, C.POINTER(C.c_uint64)]),
     "dccrgx_stop_refining_prepare": (C.c_int, [_vp, C.POINTER(_u64p), _szp, _szp]),
     "dccrgx_stop_refining_finish": (C.c_int, [_vp, C.c_int32]),
     "dccrgx_get_new_cells": (C.c_int, [_vp, _u64p, C.c_size_t, _szp]),

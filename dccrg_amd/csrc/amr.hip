@@ -99,7 +99,7 @@ struct View {
         if (exists(map_cell(g->map, idx, l + 1))) return true;
         return !exists(c);
     }
-    // neighbors_of / neighbors_to of an existing leaf (default neighborhood):
+    // neighbors_of / neighbors_to of an existing leaf of this process (default neighborhood):
     // from the host copy of the lists when one was made, else from the row
     // cache (rows are prefetched in batches by prefetch(); a miss fetches one)
     template <class F>
@@ -108,11 +108,12 @@ struct View {
         const Hood& h = g->hoods.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
         const auto& L = E->hl.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
         const int64_t r = gidx(c);
-        if (r < 0) return;
+        if (r < 0 || E->row_of((uint64_t)r) < 0) return;  // rows are held for this process's cells
         if (L.host_valid) {
             const auto& row = to ? L.h_nto_row : L.h_nof_row;
             const auto& val = to ? L.h_nto_g : L.h_nof_g;
-            for (uint64_t e = row[r]; e < row[r + 1]; e++) f(E->leaves[val[e]]);
+            const int64_t rr = E->row_of((uint64_t)r);
+            for (uint64_t e = row[rr]; e < row[rr + 1]; e++) f(E->leaves[val[e]]);
             return;
         }
         auto it = L.row_at.find((uint32_t)r);
@@ -463,16 +464,17 @@ int rebuild(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<
 }
 
 // an estimate of the device memory the explicit form of the current grid
-// needs (replicated leaf ids, hash, slot map, every leaf's neighbor lists),
-// checked before a uniform grid is converted
+// needs (replicated leaf ids, hash, slot map; the neighbor lists of this
+// rank's cells), checked before a uniform grid is converted
 static int check_explicit_memory(const dccrgx_grid* grid, uint64_t N)
 {
     uint64_t cap = 16;
     while (cap < 2 * N) cap <<= 1;
     double need = (double)N * (8 + 4 + 4 + 1) + (double)cap * 12;
+    const double nl = (double)grid->n_local;
     for (const auto& kv : grid->hoods) {
         const double K = (double)(kv.second.items.size() / 3);
-        need += (double)N * (16 + K * (8 + 12 + 4 + 4));  // rows, neighbors_of (+ transpose)
+        need += nl * (16 + K * (8 + 12 + 4 + 4 + 16));  // rows, neighbors_of, neighbors_to, stencil rows
     }
     // memory the pool keeps for reuse and the spare field buffers of earlier
     // rebuilds are free for this purpose

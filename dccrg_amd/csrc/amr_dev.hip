@@ -50,11 +50,13 @@ struct AView {
     ExView v;
     const uint64_t* leaves;
     uint64_t n;
-    const uint64_t* nof_row;
+    const uint64_t* nof_row;  // the local cells' rows (row = local position = slot)
     const uint32_t* nof_g;
     const uint64_t* nto_row;
     const uint32_t* nto_g;
-    const int32_t* items;  // default neighborhood items (original axes)
+    const uint32_t* slot_of_g;  // leaf index -> slot (the row of a local cell)
+    const int32_t* items;     // default neighborhood items (original axes)
+    const int32_t* items_to;  // and their negation (neighborhood_to)
     int32_t K;
     uint32_t hood_len;
     Partition part;
@@ -194,7 +196,8 @@ __global__ void __launch_bounds__(256) k_req_refine(AView a, const uint64_t* __r
                 r = 1;  // dont_unrefine of an existing cell
             } else if (!(a.flags[g] & RF_NOT_REFINE)) {
                 bool blocked = false;
-                for (uint64_t e = a.nof_row[g]; e < a.nof_row[g + 1] && !blocked; e++) {
+                const uint32_t rw = a.slot_of_g[g];  // a local cell: its row
+                for (uint64_t e = a.nof_row[rw]; e < a.nof_row[rw + 1] && !blocked; e++) {
                     const uint32_t t = a.nof_g[e];
                     blocked = a_level(a, a.leaves[t]) < lvl && (a.flags[t] & RF_NOT_REFINE);
                 }
@@ -206,7 +209,7 @@ __global__ void __launch_bounds__(256) k_req_refine(AView a, const uint64_t* __r
                     for (int pass = 0; pass < 2; pass++) {
                         const uint64_t* row = pass ? a.nto_row : a.nof_row;
                         const uint32_t* val = pass ? a.nto_g : a.nof_g;
-                        for (uint64_t e = row[g]; e < row[g + 1]; e++) {
+                        for (uint64_t e = row[rw]; e < row[rw + 1]; e++) {
                             const uint64_t nb = a.leaves[val[e]];
                             if (a_level(a, nb) <= lvl) a_erase_sibling_unrefines(a, nb);
                         }
@@ -430,7 +433,10 @@ __global__ void __launch_bounds__(256) k_collect(AView a, uint32_t bit, uint32_t
 
 // one round of override_refines (finer = 1: every finer neighbor of a
 // dont_refine leaf joins, :10130-10177) or induce_refines (finer = 0: every
-// coarser neighbor of a refined leaf, :9730-9907); neighbors of / to
+// coarser neighbor of a refined leaf, :9730-9907); neighbors of / to.  The
+// frontier holds cells of every process: their neighbors are searched from
+// the replicated leaf lookup (nof_search / nto_search), not read from lists,
+// which a process keeps for its own cells only.
 __global__ void __launch_bounds__(256) k_spread(AView a, uint32_t bit, int finer, const uint32_t* __restrict__ front,
                                                 const uint32_t* __restrict__ front_n, uint32_t* __restrict__ next,
                                                 uint32_t* __restrict__ next_n)
@@ -439,18 +445,16 @@ __global__ void __launch_bounds__(256) k_spread(AView a, uint32_t bit, int finer
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint32_t g = front[i];
-        const int l = a_level(a, a.leaves[g]);
-        for (int pass = 0; pass < 2; pass++) {
-            const uint64_t* row = pass ? a.nto_row : a.nof_row;
-            const uint32_t* val = pass ? a.nto_g : a.nof_g;
-            for (uint64_t e = row[g]; e < row[g + 1]; e++) {
-                const uint32_t t = val[e];
-                const int lt = a_level(a, a.leaves[t]);
-                if (finer ? lt <= l : lt >= l) continue;
-                if (a.flags[t] & bit) continue;
-                if (!(atomicOr(&a.flags[t], bit) & bit)) next[atomicAdd(next_n, 1u)] = t;
-            }
-        }
+        const uint64_t c = a.leaves[g];
+        const int l = a_level(a, c);
+        auto visit = [&](uint32_t t) {
+            const int lt = a_level(a, a.leaves[t]);
+            if (finer ? lt <= l : lt >= l) return;
+            if (a.flags[t] & bit) return;
+            if (!(atomicOr(&a.flags[t], bit) & bit)) next[atomicAdd(next_n, 1u)] = t;
+        };
+        nof_search(a.v, a.items, a.K, c, visit);
+        nto_search(a.v, a.items_to, a.K, c, visit);
     }
 }
 
@@ -737,7 +741,9 @@ static AView aview(const dccrgx_grid* grid, uint32_t* flags)
     a.nof_g = h.d_nof_g;
     a.nto_row = h.d_nto_row;
     a.nto_g = h.d_nto_g;
+    a.slot_of_g = E->d_slot_of_g;
     a.items = h.d_of_c;
+    a.items_to = h.d_to_c;
     a.K = h.K;
     a.hood_len = grid->params.neighborhood_length;
     a.part = E->part;

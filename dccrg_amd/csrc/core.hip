@@ -744,8 +744,14 @@ hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_strea
             return hipSuccess;
         }
     }
-    hipError_t e = hipMallocAsync(p, cls ? cls : bytes, st);
-    if (e == hipSuccess && any_stream) e = hipStreamSynchronize(st);
+    // hipMalloc, not the stream-ordered pool: the copy engines (SDMA) keep
+    // stale translations for pool memory the pool re-maps, so a copy into or
+    // out of a fresh hipMallocAsync block can land in the wrong pages
+    // (tools/micro/pool_trim_copy.hip: wrong data in 24-39 of 40 rounds with
+    // hipMallocAsync on either runtime, none with hipMalloc or with
+    // HSA_ENABLE_SDMA=0).  The cache makes the runtime call rare.
+    (void)st;
+    hipError_t e = hipMalloc(p, cls ? cls : bytes);
     if (e == hipSuccess && cls) {
         std::lock_guard<std::mutex> lk(C.m);
         C.dev[current_device()].live[*p] = cls;
@@ -805,20 +811,46 @@ void dx_cache_free_many(void* const* ps, size_t n, hipStream_t st, bool any_stre
                 D.idle[b.second].push_back(b.first);
                 D.idle_bytes += b.second;
             }
-        } else if (D.idle_bytes + D.held_bytes > CACHE_MAX_TOTAL) {  // too much kept: wait and return them
+        } else if (D.idle_bytes + D.held_bytes > CACHE_MAX_TOTAL) {  // too much kept: return them
             lk.unlock();
-            (void)hipDeviceSynchronize();
-            for (auto& b : blocks) (void)hipFreeAsync(b.first, nullptr);
+            for (auto& b : blocks) (void)hipFree(b.first);  // waits for the device
             lk.lock();
         } else {
             defer(D, std::move(blocks));
         }
     }
     lk.unlock();
-    if (!large.empty()) {
-        if (any_stream) (void)hipDeviceSynchronize();
-        for (void* q : large) (void)hipFreeAsync(q, any_stream ? nullptr : st);
+    for (void* q : large) (void)hipFree(q);  // waits for the device
+}
+
+void dx_cache_trim()
+{
+    Cache& C = cache();
+    std::vector<void*> out;
+    {
+        std::lock_guard<std::mutex> lk(C.m);
+        DevCache& D = C.dev[current_device()];
+        if (D.idle_bytes == 0 && D.held_bytes == 0) return;
     }
+    (void)hipDeviceSynchronize();  // every pending free has passed
+    {
+        std::lock_guard<std::mutex> lk(C.m);
+        DevCache& D = C.dev[current_device()];
+        drain(D);
+        for (auto& kv : D.idle)
+            for (void* q : kv.second) out.push_back(q);
+        D.idle.clear();
+        D.idle_bytes = 0;
+        for (auto& sl : D.by_stream)
+            for (auto& kv : sl.second)
+                for (void* q : kv.second) {
+                    out.push_back(q);
+                    D.held_bytes -= kv.first;
+                }
+        D.by_stream.clear();
+        D.stream_bytes.clear();
+    }
+    for (void* q : out) (void)hipFree(q);
 }
 
 void dx_cache_streams(hipStream_t a, hipStream_t b, bool add)
@@ -872,17 +904,7 @@ size_t dx_cache_idle_bytes()
     return D.idle_bytes + D.held_bytes;
 }
 
-size_t dx_pool_idle_bytes()
-{
-    int dev = 0;
-    hipMemPool_t pool = nullptr;
-    uint64_t reserved = 0, used = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess ||
-        hipMemPoolGetAttribute(pool, hipMemPoolAttrReservedMemCurrent, &reserved) != hipSuccess ||
-        hipMemPoolGetAttribute(pool, hipMemPoolAttrUsedMemCurrent, &used) != hipSuccess)
-        return 0;
-    return (reserved > used ? (size_t)(reserved - used) : 0) + dx_cache_idle_bytes();
-}
+size_t dx_pool_idle_bytes() { return dx_cache_idle_bytes(); }
 }  // namespace dccrgx
 
 extern "C" {
@@ -896,12 +918,6 @@ int dccrgx_ctx_create(int device, int rank, int comm_size, dccrgx_ctx** out)
     DX_HIP(hipGetDeviceCount(&ndev));
     DX_CHECK(device >= 0 && device < ndev, DCCRGX_EINVAL, "device %d of %d", device, ndev);
     DX_HIP(hipSetDevice(device));
-    {  // keep freed pool memory for reuse (dx_malloc / dx_free)
-        hipMemPool_t pool = nullptr;
-        DX_HIP(hipDeviceGetDefaultMemPool(&pool, device));
-        uint64_t keep = UINT64_MAX;
-        DX_HIP(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
-    }
     auto* c = new dccrgx_ctx();
     c->device = device;
     c->rank = rank;
@@ -923,6 +939,7 @@ int dccrgx_ctx_destroy(dccrgx_ctx* c)
     hipStreamSynchronize(c->compute);
     hipStreamSynchronize(c->comm);
     dx_cache_streams(c->compute, c->comm, false);
+    dx_cache_trim();
     if (c->has_comm) ncclCommDestroy(c->nccl);
     hipEventDestroy(c->ev_compute);
     hipEventDestroy(c->ev_comm);

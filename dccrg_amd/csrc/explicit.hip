@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(256) k_ex_nof(ExView v, const int32_t* __restr
                                                 const uint64_t* __restrict__ cells, size_t n,
                                                 uint64_t* __restrict__ row, uint64_t* __restrict__ ids,
                                                 int32_t* __restrict__ off, uint32_t* __restrict__ gidx,
-                                                int32_t* __restrict__ err)
+                                                int32_t* __restrict__ err, uint64_t* __restrict__ codes = nullptr)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     const MapParams& p = v.mp;
@@ -84,6 +84,7 @@ __global__ void __launch_bounds__(256) k_ex_nof(ExView v, const int32_t* __restr
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t c = cells[i];
         uint64_t w = ids ? row[i] : 0;
+        uint64_t code = 0;  // count pass, K <= 32: each item's case in 2 bits (k_ex_nof_fill_codes)
         uint64_t idx[3];
         int l;
         if (ex_find(v, c) < 0 || !map_indices(p, c, idx, &l)) {
@@ -126,12 +127,14 @@ __global__ void __launch_bounds__(256) k_ex_nof(ExView v, const int32_t* __restr
             int64_t g = ex_find(v, W);
             if (g >= 0) {
                 emit(W, g, h[0] * L, h[1] * L, h[2] * L);
+                code |= 1ull << (2 * k);
                 continue;
             }
             if (l > 0) {
                 const uint64_t P = map_cell(p, wi, l - 1);
                 g = ex_find(v, P);
                 if (g >= 0) {
+                    code |= 2ull << (2 * k);
                     const int64_t L2 = 2 * L;
                     emit(P, g, h[0] * L - (int64_t)(wi[0] % L2), h[1] * L - (int64_t)(wi[1] % L2),
                          h[2] * L - (int64_t)(wi[2] % L2));
@@ -141,6 +144,7 @@ __global__ void __launch_bounds__(256) k_ex_nof(ExView v, const int32_t* __restr
             if (l < M) {
                 const int64_t hl = L / 2;
                 bool all = true;
+                code |= 3ull << (2 * k);
                 for (int dz = 0; dz < 2; dz++)
                     for (int dy = 0; dy < 2; dy++)
                         for (int dx = 0; dx < 2; dx++) {
@@ -155,6 +159,7 @@ __global__ void __launch_bounds__(256) k_ex_nof(ExView v, const int32_t* __restr
             atomicOr(err, 2);  // level difference > 1: outside the reference's assumptions
         }
         if (!ids) row[i + 1] = w;
+        if (codes) codes[i] = code;
     }
 }
 
@@ -168,22 +173,6 @@ __global__ void __launch_bounds__(256) k_ex_nof(ExView v, const int32_t* __restr
 // Entries beyond the LDS capacity are written by their lane directly.
 constexpr int NOF_REC_CAP = 1024;  // records per wave (8 KiB; four independent waves per workgroup)
 
-__device__ __forceinline__ bool nof_window(const MapParams& p, const int32_t* per, const uint64_t idx[3],
-                                           const int32_t* h, int64_t L, uint64_t wi[3])
-{
-    const int M = p.max_lvl;
-    for (int d = 0; d < 3; d++) {
-        const int64_t G = (int64_t)(p.length[d] << M);
-        int64_t x = (int64_t)idx[d] + (int64_t)h[d] * L;
-        if (x < 0 || x >= G) {
-            if (!per[d]) return false;
-            x %= G;
-            if (x < 0) x += G;
-        }
-        wi[d] = (uint64_t)x;
-    }
-    return true;
-}
 
 __device__ __forceinline__ void nof_entry(const MapParams& p, const uint64_t wi[3], int l, const int32_t* h, int64_t L,
                                           int cs, uint64_t& id, int32_t o[3])
@@ -301,6 +290,86 @@ __global__ void __launch_bounds__(256) k_ex_nof_fill(ExView v, const int32_t* __
             off[3 * (base + e) + 1] = o[1];
             off[3 * (base + e) + 2] = o[2];
         }
+    }
+}
+
+// Fill pass from the count pass's per-item cases (K <= 32), entry-parallel:
+// one wave per 64 cells whose rows form one output run.  The wave walks its
+// run 64 entries at a time; each lane finds its entry's cell (binary search
+// over the 65 row offsets in LDS) and item (the cell's 2-bit cases: 0
+// dropped, 1 the window's cell, 2 its parent, 3 its 8 children), rebuilds id
+// and offset from the cell's indices and looks up the leaf index.  Every
+// store is coalesced whatever the row lengths (k_ex_nof_fill stages 1024
+// records per wave and stores the rest per lane: 2.5x the output's bytes
+// written for 26-item neighborhoods), and an entry costs one lookup.
+__global__ void __launch_bounds__(256) k_ex_nof_fill_codes(ExView v, const int32_t* __restrict__ items, int K,
+                                                           const uint64_t* __restrict__ cells, size_t n,
+                                                           const uint64_t* __restrict__ row,
+                                                           const uint64_t* __restrict__ codes, uint64_t* __restrict__ ids,
+                                                           int32_t* __restrict__ off, uint32_t* __restrict__ gidx)
+{
+    __shared__ uint64_t s_row_all[4][65];
+    __shared__ uint64_t s_code_all[4][64];
+    __shared__ uint64_t s_idx_all[4][3][64];
+    __shared__ int32_t s_lvl_all[4][64];
+    const int wv = threadIdx.x >> 6;
+    uint64_t* s_row = s_row_all[wv];
+    uint64_t* s_code = s_code_all[wv];
+    uint64_t(*s_idx)[64] = s_idx_all[wv];
+    int32_t* s_lvl = s_lvl_all[wv];
+    const MapParams& p = v.mp;
+    const int M = p.max_lvl;
+    const int lane = threadIdx.x & 63;
+    const uint64_t r0 = ((uint64_t)blockIdx.x * 4 + wv) * 64;
+    const bool live = r0 < n;  // a wave past the end still meets the block barrier
+    const uint64_t last = r0 + 64 < n ? r0 + 64 : n;
+    const uint64_t i = r0 + lane;
+    if (live) {
+        const uint64_t end_row = row[last];
+        s_row[lane] = i < n ? row[i] : end_row;
+        if (lane == 0) s_row[64] = end_row;
+        uint64_t idx[3] = {0, 0, 0};
+        int l = 0;
+        if (i < n) map_indices(p, cells[i], idx, &l);  // cells the count pass refused have empty rows
+        for (int d = 0; d < 3; d++) s_idx[d][lane] = idx[d];
+        s_lvl[lane] = l;
+        s_code[lane] = i < n ? codes[i] : 0;
+    }
+    __syncthreads();
+    if (!live) return;
+    const uint64_t base = s_row[0], end = s_row[64];
+    for (uint64_t e = base + lane; e < end; e += 64) {
+        int lo = 0, hi = 64;  // the last cell whose row starts at or before e
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_row[mid] <= e) lo = mid;
+            else hi = mid;
+        }
+        uint64_t t = e - s_row[lo];
+        const uint64_t code = s_code[lo];
+        int k = 0, cs = 0;
+        for (; k < K; k++) {
+            const uint32_t c2 = (uint32_t)(code >> (2 * k)) & 3u;
+            const uint64_t cnt = c2 == 3u ? 8 : (c2 ? 1 : 0);
+            if (t < cnt) {
+                cs = c2 == 1u ? 0 : c2 == 2u ? 1 : 2 + (int)t;
+                break;
+            }
+            t -= cnt;
+        }
+        const uint64_t idx[3] = {s_idx[0][lo], s_idx[1][lo], s_idx[2][lo]};
+        const int l = s_lvl[lo];
+        const int64_t L = (int64_t)1 << (M - l);
+        uint64_t wi[3];
+        nof_window(p, v.per, idx, items + 3 * k, L, wi);
+        uint64_t id;
+        int32_t o[3];
+        nof_entry(p, wi, l, items + 3 * k, L, cs, id, o);
+        ids[e] = id;
+        gidx[e] = (uint32_t)ex_find(v, id);
+        off[3 * e + 0] = o[0];
+        off[3 * e + 1] = o[1];
+        off[3 * e + 2] = o[2];
     }
 }
 
@@ -431,6 +500,22 @@ __global__ void __launch_bounds__(256) k_stencil_slots(const uint64_t* __restric
 
 // the same per wavefront in LDS (rows up to WAVE_SORT_MAX; longer ones flagged
 // ~0 in ucnt for k_stencil_rows); defined after the wave helpers
+// count pass (out == null: row[i + 1] = entries) / fill pass (from row[i])
+__global__ void __launch_bounds__(256) k_ex_nto(ExView v, const int32_t* __restrict__ items_to, int K,
+                                                const uint64_t* __restrict__ cells, size_t n, uint64_t* __restrict__ row,
+                                                uint32_t* __restrict__ out)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t w = out ? row[i] : 0;
+        nto_search(v, items_to, K, cells[i], [&](uint32_t g) {
+            if (out) out[w] = g;
+            w++;
+        });
+        if (!out) row[i + 1] = w;
+    }
+}
+
 __global__ void __launch_bounds__(64) k_stencil_rows_wave(const uint64_t* __restrict__ nof_row,
                                                           const uint32_t* __restrict__ nof_g,
                                                           const int32_t* __restrict__ nof_off,
@@ -536,22 +621,26 @@ __global__ void __launch_bounds__(64) k_rows_gather_g(const uint32_t* __restrict
     }
 }
 
-// query cells -> their leaf index and row length in the stored CSR
+// query cells -> their row (local position) and its length in the stored
+// CSR; err bit 1: not a leaf, bit 4: a leaf of another process (no row here)
 __global__ void __launch_bounds__(256) k_ex_query_rows(ExView v, const uint64_t* __restrict__ cells, size_t n,
-                                                       const uint64_t* __restrict__ nof_row, uint32_t* __restrict__ gq,
-                                                       uint64_t* __restrict__ row, int32_t* __restrict__ err)
+                                                       const uint64_t* __restrict__ nof_row,
+                                                       const uint32_t* __restrict__ slot_of_g, uint64_t n_local,
+                                                       uint32_t* __restrict__ gq, uint64_t* __restrict__ row,
+                                                       int32_t* __restrict__ err)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const int64_t g = ex_find(v, cells[i]);
-        if (g < 0) {
-            atomicOr(err, 1);
+        const uint32_t r = g < 0 ? NO_SLOT : slot_of_g[g];
+        if (g < 0 || r >= n_local) {
+            atomicOr(err, g < 0 ? 1 : 4);
             row[i + 1] = 0;
             gq[i] = 0;
             continue;
         }
-        gq[i] = (uint32_t)g;
-        row[i + 1] = nof_row[g + 1] - nof_row[g];
+        gq[i] = r;
+        row[i + 1] = nof_row[r + 1] - nof_row[r];
     }
 }
 
@@ -890,9 +979,11 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     DX_HIP(ds_malloc(&d_err, 16, st));
     DX_HIP(hipMemsetAsync(d_err, 0, 16, st));
     DX_HIP(hipMemsetAsync(row, 0, 8, st));
+    uint64_t* d_codes = nullptr;  // per-item cases for the entry-parallel fill
+    if (ids && h.K <= 32 && n) DX_HIP(ds_malloc(&d_codes, n * 8, st));
     if (n)
         hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(n)), dim3(256), 0, st, v, h.d_of_c, h.K, cells, n, row,
-                           (uint64_t*)nullptr, (int32_t*)nullptr, (uint32_t*)nullptr, d_err);
+                           (uint64_t*)nullptr, (int32_t*)nullptr, (uint32_t*)nullptr, d_err, d_codes);
     DX_HIP(hipGetLastError());
     DX_TRY(device_scan_rows(row, n, st, nullptr));
     uint64_t back[2] = {0, 0};  // total, error word: one read-back
@@ -902,6 +993,7 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     const int32_t err = (int32_t)(back[0] & 0xffffffffu);
     if (err) {
         ds_free(d_err, st);
+        ds_free(d_codes, st);
         return set_error(err & 1 ? DCCRGX_ENOTFOUND : DCCRGX_EINTERNAL,
                          err & 1 ? "cell does not exist" : "neighbor more than one level apart");
     }
@@ -910,16 +1002,91 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
         DX_HIP(ds_malloc(ids, t * 8, st));
         DX_HIP(ds_malloc(off, t * 12, st));
         DX_HIP(ds_malloc(gidx, t * 4, st));
-        if (n)
+        if (n && d_codes)
+            hipLaunchKernelGGL(k_ex_nof_fill_codes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, h.d_of_c,
+                               h.K, cells, n, (const uint64_t*)row, (const uint64_t*)d_codes, *ids, *off, *gidx);
+        else if (n)
             hipLaunchKernelGGL(k_ex_nof_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, h.d_of_c, h.K,
                                cells, n, (const uint64_t*)row, *ids, *off, *gidx);
         DX_HIP(hipGetLastError());
     }
+    ds_free(d_codes, st);
     ds_free(d_err, st);
     return DCCRGX_OK;
 }
 
 static int sync_slots(dccrgx_grid* grid, bool slot_map_changed);
+int explicit_local_ids(const dccrgx_grid* grid, uint64_t* d_ids, hipStream_t st);
+
+// ids of the local cells, from the device leaf list
+__global__ void __launch_bounds__(256) k_local_ids(const uint64_t* __restrict__ leaves,
+                                                   const uint32_t* __restrict__ local_g, uint64_t n,
+                                                   uint64_t* __restrict__ out)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = leaves[local_g[i]];
+}
+
+// rows (row[n + 1], `tot` entries in v) sorted and made unique in place,
+// then copied compacted into a new CSR (*out_row, *out_v)
+static int sort_unique_compact(const uint64_t* row, uint32_t* v, uint64_t n, uint64_t tot, uint64_t** out_row,
+                               uint32_t** out_v, hipStream_t st)
+{
+    uint32_t* d_ucnt = nullptr;
+    DX_HIP(ds_malloc(&d_ucnt, std::max<uint64_t>(n, 1) * 4, st));
+    if (n) {
+        hipLaunchKernelGGL((k_sort_unique_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((n + 15) / 16, 16384)),
+                           dim3(256), 0, st, row, n, v, d_ucnt);
+        hipLaunchKernelGGL((k_sort_unique_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((n + 3) / 4, 4096)),
+                           dim3(256), 0, st, row, n, v, d_ucnt);
+        hipLaunchKernelGGL(k_sort_unique_rows_wave, dim3((unsigned)std::min<uint64_t>(n, 4096)), dim3(64), 0, st, row, n,
+                           v, d_ucnt);
+        hipLaunchKernelGGL(k_sort_unique_rows, dim3(grid_for(n)), dim3(256), 0, st, row, n, v, d_ucnt);
+    }
+    DX_HIP(hipGetLastError());
+    const int e = scan_counts_device(d_ucnt, n, out_row, nullptr, st);
+    if (e != DCCRGX_OK) {
+        ds_free(d_ucnt, st);
+        return e;
+    }
+    DX_HIP(ds_malloc(out_v, std::max<uint64_t>(tot, 1) * 4, st));  // unique entries: at most tot
+    if (n)
+        hipLaunchKernelGGL(k_copy_rows_wave, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, row, (const uint32_t*)v,
+                           (const uint64_t*)*out_row, n, *out_v);
+    DX_HIP(hipGetLastError());
+    ds_free(d_ucnt, st);
+    return DCCRGX_OK;
+}
+
+// neighbors_to rows (ascending leaf indices) of `cells` by the reference's
+// search (k_ex_nto): count, scan, fill, sort + unique
+static int nto_direct(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, uint64_t n, uint64_t** out_row,
+                      uint32_t** out_g, hipStream_t st)
+{
+    const ExView v = view(grid);
+    uint64_t* d_row = nullptr;
+    uint32_t* d_tmp = nullptr;
+    DX_HIP(ds_malloc(&d_row, (n + 1) * 8, st));
+    auto done = [&](int code) {
+        ds_free(d_row, st);
+        ds_free(d_tmp, st);
+        return code;
+    };
+    if (hipMemsetAsync(d_row, 0, 8, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
+    if (n)
+        hipLaunchKernelGGL(k_ex_nto, dim3(grid_for(n)), dim3(256), 0, st, v, (const int32_t*)h.d_to_c, h.K, cells,
+                           (size_t)n, d_row, (uint32_t*)nullptr);
+    uint64_t tot = 0;
+    int e = device_scan_rows(d_row, n, st, &tot);
+    if (e != DCCRGX_OK) return done(e);
+    if (ds_malloc(&d_tmp, std::max<uint64_t>(tot, 1) * 4, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "neighbors_to of %llu cells", (unsigned long long)n));
+    if (n)
+        hipLaunchKernelGGL(k_ex_nto, dim3(grid_for(n)), dim3(256), 0, st, v, (const int32_t*)h.d_to_c, h.K, cells,
+                           (size_t)n, d_row, d_tmp);
+    return done(sort_unique_compact(d_row, d_tmp, n, tot, out_row, out_g, st));
+}
+
 
 int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t* d_leaves,
                   std::vector<uint64_t>* take)
@@ -1267,7 +1434,7 @@ int explicit_host_lists(const dccrgx_grid* grid, const Hood& h)
     if (L.host_valid) return DCCRGX_OK;
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
-    const uint64_t N = E->n;
+    const uint64_t N = h.n_rows;  // the local cells' rows (row = local position)
     L.h_nof_row.resize(N + 1);
     L.h_nto_row.resize(N + 1);
     DX_TRY(dx_d2h(ctx, L.h_nof_row.data(), h.d_nof_row, (N + 1) * 8, st));
@@ -1313,12 +1480,14 @@ int explicit_fetch_rows(const dccrgx_grid* grid, const Hood& h, const std::vecto
     Explicit* E = grid->ex;
     Explicit::HoodLists& L = E->hl[h.id];
     if (L.host_valid) return DCCRGX_OK;  // the whole lists are on the host already
-    std::vector<uint32_t> want;
+    std::vector<uint32_t> want;  // leaves of this rank (the rows held here) not fetched yet
     for (uint32_t g : leaves)
-        if (g < E->n && !L.row_at.count(g)) want.push_back(g);
+        if (g < E->n && E->row_of(g) >= 0 && !L.row_at.count(g)) want.push_back(g);
     std::sort(want.begin(), want.end());
     want.erase(std::unique(want.begin(), want.end()), want.end());
     if (want.empty()) return DCCRGX_OK;
+    std::vector<uint32_t> rows(want.size());
+    for (size_t i = 0; i < want.size(); i++) rows[i] = (uint32_t)E->row_of(want[i]);
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
     const uint64_t n = want.size();
@@ -1333,7 +1502,7 @@ int explicit_fetch_rows(const dccrgx_grid* grid, const Hood& h, const std::vecto
         if (d_out) (void)ds_free(d_out, st);
         return code;
     };
-    int s = dx_h2d_async(ctx, d_g, want.data(), n * 4, st);
+    int s = dx_h2d_async(ctx, d_g, rows.data(), n * 4, st);
     if (s != DCCRGX_OK) return done(s);
     hipLaunchKernelGGL(k_rows_len, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)d_g, n, h.d_nof_row,
                        h.d_nto_row, d_row, d_row + n + 1);
@@ -1688,57 +1857,65 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     h.outer.clear();
     h.remote.clear();
     const uint64_t N = E->n;
-    h.n_rows = N;
-    // neighbors_of of every leaf (the reference also builds all of them)
-    DX_HIP(ds_malloc(&h.d_nof_row, (N + 1) * 8, st));
+    const uint64_t nl = E->local.size();
+    // The CSRs hold the rows of this rank's local cells, indexed by local
+    // position (= storage slot).  One process: every leaf, in leaf order.
+    // Several: only the local cells' rows -- the reference builds lists for
+    // every cell (dccrg.hpp:8371-8397); here a rank's list memory scales with
+    // its own cells, and rows of other cells are searched on demand from the
+    // replicated leaf lookup (queries, the refinement decisions).
+    const bool per_rank = ctx->comm_size > 1;
+    h.n_rows = nl;
+    DX_HIP(ds_malloc(&h.d_nof_row, (nl + 1) * 8, st));
     uint64_t tot = 0;
     IncMaps inc;
-    const bool inc_nof = hint && hint->old_h && hint->old_h->d_nof_row && hint->old_h->items == h.items &&
+    const bool inc_nof = !per_rank && hint && hint->old_h && hint->old_h->d_nof_row && hint->old_h->items == h.items &&
                          hint->old_ex && incremental_rebuild(hint->old_ex->n);
     // the stencil rows follow incrementally where slots are leaf indices before and after
-    const bool inc_st = inc_nof && ctx->comm_size == 1 && E->slot_identity && hint->old_ex->slot_identity &&
-                        hint->old_h->d_st_row && hint->old_ex->local.size() == hint->old_ex->n;
+    const bool inc_st = inc_nof && E->slot_identity && hint->old_ex->slot_identity && hint->old_h->d_st_row &&
+                        hint->old_ex->local.size() == hint->old_ex->n;
+    uint64_t* d_local_ids = nullptr;  // several processes: the local cells' ids
+    if (per_rank) {
+        DX_HIP(ds_malloc(&d_local_ids, std::max<uint64_t>(nl, 1) * 8, st));
+        DX_TRY(explicit_local_ids(grid, d_local_ids, st));
+    }
+    struct FreeIds {
+        uint64_t*& p;
+        hipStream_t st;
+        ~FreeIds() { ds_free(p, st); }
+    } free_ids{d_local_ids, st};
     if (inc_nof)
         DX_TRY(nof_incremental(grid, h, *hint, &tot, st, inc_st ? &inc : nullptr));
     else
-        DX_TRY(nof_device(grid, h, E->d_leaves, N, h.d_nof_row, &h.d_nof_id, &h.d_nof_off, &h.d_nof_g, &tot, st));
+        DX_TRY(nof_device(grid, h, per_rank ? d_local_ids : E->d_leaves, per_rank ? nl : N, h.d_nof_row, &h.d_nof_id,
+                          &h.d_nof_off, &h.d_nof_g, &tot, st));
     T.lap("neighbors_of");
-    // neighbors_to = transpose (rows: leaves)
-    uint32_t *d_cnt = nullptr, *d_cur = nullptr, *d_tmp = nullptr, *d_ucnt = nullptr;
-    DX_HIP(ds_malloc(&d_cnt, N * 4, st));
-    DX_HIP(ds_malloc(&d_cur, N * 4, st));
-    DX_HIP(hipMemsetAsync(d_cnt, 0, N * 4, st));
-    DX_HIP(hipMemsetAsync(d_cur, 0, N * 4, st));
-    hipLaunchKernelGGL(k_tr_count, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_cnt);
-    uint64_t* d_trow = nullptr;
-    const uint64_t ttot = tot;  // the transpose has as many entries as neighbors_of: no read-back
-    DX_TRY(scan_counts_device(d_cnt, N, &d_trow, nullptr, st));
-    DX_HIP(ds_malloc(&d_tmp, std::max<uint64_t>(ttot, 1) * 4, st));
-    hipLaunchKernelGGL(k_tr_scatter, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_trow,
-                       d_cur, d_tmp);
-    DX_HIP(ds_malloc(&d_ucnt, N * 4, st));
-    hipLaunchKernelGGL((k_sort_unique_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((N + 15) / 16, 16384)),
-                       dim3(256), 0, st, d_trow, N, d_tmp, d_ucnt);
-    hipLaunchKernelGGL((k_sort_unique_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((N + 3) / 4, 4096)),
-                       dim3(256), 0, st, d_trow, N, d_tmp, d_ucnt);
-    hipLaunchKernelGGL(k_sort_unique_rows_wave, dim3((unsigned)std::min<uint64_t>(N, 4096)), dim3(64), 0, st, d_trow,
-                       N, d_tmp, d_ucnt);
-    hipLaunchKernelGGL(k_sort_unique_rows, dim3(grid_for(N)), dim3(256), 0, st, d_trow, N, d_tmp, d_ucnt);
-    DX_HIP(hipGetLastError());
-    DX_TRY(scan_counts_device(d_ucnt, N, &h.d_nto_row, nullptr, st));
-    DX_HIP(ds_malloc(&h.d_nto_g, std::max<uint64_t>(ttot, 1) * 4, st));  // unique entries: at most ttot
-    hipLaunchKernelGGL(k_copy_rows_wave, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, d_trow, d_tmp, h.d_nto_row,
-                       N, h.d_nto_g);
-    DX_HIP(hipGetLastError());
-    ds_free(d_cnt, st);
-    ds_free(d_cur, st);
-    ds_free(d_tmp, st);
-    ds_free(d_ucnt, st);
-    ds_free(d_trow, st);
+    if (per_rank) {  // neighbors_to of the local cells by the reference's search
+        DX_TRY(nto_direct(grid, h, d_local_ids, nl, &h.d_nto_row, &h.d_nto_g, st));
+    } else {  // one process: the transpose of every leaf's neighbors_of (rows: leaves)
+        uint32_t *d_cnt = nullptr, *d_cur = nullptr, *d_tmp = nullptr;
+        DX_HIP(ds_malloc(&d_cnt, N * 4, st));
+        DX_HIP(ds_malloc(&d_cur, N * 4, st));
+        DX_HIP(hipMemsetAsync(d_cnt, 0, N * 4, st));
+        DX_HIP(hipMemsetAsync(d_cur, 0, N * 4, st));
+        hipLaunchKernelGGL(k_tr_count, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_cnt);
+        uint64_t* d_trow = nullptr;
+        const uint64_t ttot = tot;  // the transpose has as many entries as neighbors_of: no read-back
+        DX_TRY(scan_counts_device(d_cnt, N, &d_trow, nullptr, st));
+        DX_HIP(ds_malloc(&d_tmp, std::max<uint64_t>(ttot, 1) * 4, st));
+        hipLaunchKernelGGL(k_tr_scatter, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_trow,
+                           d_cur, d_tmp);
+        DX_HIP(hipGetLastError());
+        const int e = sort_unique_compact(d_trow, d_tmp, N, ttot, &h.d_nto_row, &h.d_nto_g, st);
+        ds_free(d_cnt, st);
+        ds_free(d_cur, st);
+        ds_free(d_tmp, st);
+        ds_free(d_trow, st);
+        DX_TRY(e);
+    }
 
     T.lap("neighbors_to");
     // per-rank bookkeeping from the device lists (dccrg.hpp:9131-9234, 8729-8891)
-    const uint64_t nl = E->local.size();
     Explicit::HoodLists& L = E->hl[h.id];
     for (uint32_t* p : {L.d_inner_pos, L.d_outer_pos, L.d_all_pos}) dx_free(p);
     L = Explicit::HoodLists{};
@@ -1757,7 +1934,7 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     std::map<int, std::set<uint64_t>> send, recv;
     L.inner_all = ctx->comm_size == 1;  // one process: every cell is inner, nothing remote
     for (uint64_t i = 0; ctx->comm_size > 1 && i < nl; i++) {
-        const uint32_t r = E->local_g[i];
+        const uint64_t r = i;  // rows by local position
         bool outer = false;
         for (uint64_t e = nof_row[r]; e < nof_row[r + 1]; e++) {
             const uint32_t t = L.h_nof_g[e];
@@ -1843,32 +2020,24 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
         Pair* d_pairs = nullptr;
         uint32_t* d_pc = nullptr;
         uint64_t tmp_tot = 0;
-        if (ctx->comm_size == 1) {  // every leaf is local, in leaf order: the rows are neighbors_of's
-            DX_HIP(ds_malloc(&d_tmp_row, (nl + 1) * 8, st));
-            DX_HIP(hipMemcpyAsync(d_tmp_row, h.d_nof_row, (nl + 1) * 8, hipMemcpyDeviceToDevice, st));
-            tmp_tot = tot;
-        } else {
-            std::vector<uint64_t> tmp_row(nl + 1, 0);
-            for (uint64_t i = 0; i < nl; i++) {
-                const uint32_t r = E->local_g[i];
-                tmp_row[i + 1] = tmp_row[i] + (nof_row[r + 1] - nof_row[r]);
-            }
-            DX_TRY(upload(grid->ctx, tmp_row, &d_tmp_row, st));
-            tmp_tot = tmp_row[nl];
-        }
+        // the rows are the local cells' neighbors_of rows, in local order
+        DX_HIP(ds_malloc(&d_tmp_row, (nl + 1) * 8, st));
+        DX_HIP(hipMemcpyAsync(d_tmp_row, h.d_nof_row, (nl + 1) * 8, hipMemcpyDeviceToDevice, st));
+        tmp_tot = tot;
+        if (!L.d_all_pos) DX_TRY(device_iota(&L.d_all_pos, nl, st));  // row of local position i: i
         DX_HIP(ds_malloc(&d_pairs, std::max<uint64_t>(tmp_tot, 1) * sizeof(Pair), st));
         DX_HIP(ds_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4, st));
         if (nl) {
             hipLaunchKernelGGL((k_stencil_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((nl + 15) / 16, 16384)),
-                               dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs,
+                               dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, L.d_all_pos, nl, d_tmp_row, d_pairs,
                                d_pc);
             hipLaunchKernelGGL((k_stencil_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((nl + 3) / 4, 4096)),
-                               dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs,
+                               dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, L.d_all_pos, nl, d_tmp_row, d_pairs,
                                d_pc);
             hipLaunchKernelGGL(k_stencil_rows_wave, dim3((unsigned)std::min<uint64_t>(nl, 4096)), dim3(64), 0, st,
-                               h.d_nof_row, h.d_nof_g, h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
+                               h.d_nof_row, h.d_nof_g, h.d_nof_off, L.d_all_pos, nl, d_tmp_row, d_pairs, d_pc);
             hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
-                               h.d_nof_off, E->d_local_g, nl, d_tmp_row, d_pairs, d_pc);
+                               h.d_nof_off, L.d_all_pos, nl, d_tmp_row, d_pairs, d_pc);
         }
         const uint64_t stot = tmp_tot;  // unique pairs: at most the rows' entries (no read-back)
         DX_TRY(scan_counts_device(d_pc, nl, &h.d_st_row, nullptr, st));
@@ -1920,7 +2089,7 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     if (ctx->comm_size == 1) DX_TRY(device_iota(&L.d_inner_pos, nl, st));  // every cell inner
     else DX_TRY(upload(grid->ctx, L.inner_pos, &L.d_inner_pos, st));
     DX_TRY(upload(grid->ctx, L.outer_pos, &L.d_outer_pos, st));
-    DX_TRY(device_iota(&L.d_all_pos, nl, st));
+    if (!L.d_all_pos) DX_TRY(device_iota(&L.d_all_pos, nl, st));
     return DCCRGX_OK;
 }
 
@@ -2066,8 +2235,9 @@ __global__ void __launch_bounds__(256) k_ex_gather_count(ExView v, const uint64_
             gidx[i] = 0;
             continue;
         }
-        gidx[i] = (uint32_t)g;
-        row[i + 1] = nof_row[g + 1] - nof_row[g];
+        const uint32_t r = slot_of_g[g];  // its row: local position
+        gidx[i] = r;
+        row[i + 1] = nof_row[r + 1] - nof_row[r];
     }
 }
 
@@ -2080,7 +2250,7 @@ __global__ void __launch_bounds__(256) k_ex_gather_fill(const uint32_t* __restri
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t g = gidx[i];
+        const uint32_t g = gidx[i];  // row of the query cell
         uint64_t w = row[i];
         for (uint64_t e = nof_row[g]; e < nof_row[g + 1]; e++, w++) {
             const uint8_t* src = field + (uint64_t)slot_of_g[nof_g[e]] * elem;
@@ -2149,15 +2319,33 @@ int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t
         return code;
     };
     if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
+    const Explicit* E = grid->ex;
     if (n)
-        hipLaunchKernelGGL(k_ex_query_rows, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nof_row, gq,
-                           row, d_err);
+        hipLaunchKernelGGL(k_ex_query_rows, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nof_row,
+                           (const uint32_t*)E->d_slot_of_g, (uint64_t)E->local.size(), gq, row, d_err);
     uint64_t total = 0;
     int s = device_scan_rows(row, n, st, &total);  // synchronises (total)
     if (s != DCCRGX_OK) return done(s);
     int32_t err = 0;
     if ((s = dx_d2h(grid->ctx, &err, d_err, 4, st)) != DCCRGX_OK) return done(s);
-    if (err) return done(set_error(DCCRGX_ENOTFOUND, "cell does not exist"));
+    if (err & 1) return done(set_error(DCCRGX_ENOTFOUND, "cell does not exist"));
+    if (err & 4) {  // rows of other processes' cells: searched now (the reference's lists of every cell)
+        if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess || hipMemsetAsync(row, 0, 8, st) != hipSuccess)
+            return done(set_error(DCCRGX_EHIP, "memset"));
+        hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(n)), dim3(256), 0, st, view(grid), (const int32_t*)h.d_of_c, h.K,
+                           cells, n, row, (uint64_t*)nullptr, (int32_t*)nullptr, (uint32_t*)nullptr, d_err,
+                           (uint64_t*)nullptr);
+        if ((s = device_scan_rows(row, n, st, &total)) != DCCRGX_OK) return done(s);
+        if ((s = dx_d2h(grid->ctx, &err, d_err, 4, st)) != DCCRGX_OK) return done(s);
+        if (err) return done(set_error(err & 1 ? DCCRGX_ENOTFOUND : DCCRGX_EINTERNAL,
+                                       err & 1 ? "cell does not exist" : "neighbor more than one level apart"));
+        if (!ids) return done(DCCRGX_OK);
+        if (cap < total) return done(set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total));
+        hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(n)), dim3(256), 0, st, view(grid), (const int32_t*)h.d_of_c, h.K,
+                           cells, n, row, ids, off3, (uint32_t*)nullptr, d_err, (uint64_t*)nullptr);
+        if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "neighbor list search failed"));
+        return done(DCCRGX_OK);
+    }
     if (!ids) return done(DCCRGX_OK);
     if (cap < total) return done(set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total));
     if (n)
@@ -2183,15 +2371,39 @@ int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t
         return code;
     };
     if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
+    const Explicit* E = grid->ex;
     if (n)
-        hipLaunchKernelGGL(k_ex_query_rows, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nto_row, gq,
-                           row, d_err);
+        hipLaunchKernelGGL(k_ex_query_rows, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nto_row,
+                           (const uint32_t*)E->d_slot_of_g, (uint64_t)E->local.size(), gq, row, d_err);
     uint64_t total = 0;
     int s = device_scan_rows(row, n, st, &total);  // synchronises (total)
     if (s != DCCRGX_OK) return done(s);
     int32_t err = 0;
     if ((s = dx_d2h(grid->ctx, &err, d_err, 4, st)) != DCCRGX_OK) return done(s);
-    if (err) return done(set_error(DCCRGX_ENOTFOUND, "cell does not exist"));
+    if (err & 1) return done(set_error(DCCRGX_ENOTFOUND, "cell does not exist"));
+    if (err & 4) {  // rows of other processes' cells: the reference's search, now
+        uint64_t* trow = nullptr;
+        uint32_t* tg = nullptr;
+        uint32_t* iota = nullptr;
+        auto done2 = [&](int code) {
+            ds_free(trow, st);
+            ds_free(tg, st);
+            ds_free(iota, st);
+            return done(code);
+        };
+        if ((s = nto_direct(grid, h, cells, n, &trow, &tg, st)) != DCCRGX_OK) return done2(s);
+        if (hipMemcpyAsync(row, trow, (n + 1) * 8, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return done2(set_error(DCCRGX_EHIP, "copy"));
+        if ((s = dx_d2h(grid->ctx, &total, trow + n, 8, st)) != DCCRGX_OK) return done2(s);
+        if (!ids) return done2(DCCRGX_OK);
+        if (cap < total) return done2(set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total));
+        if ((s = device_iota(&iota, n, st)) != DCCRGX_OK) return done2(s);
+        hipLaunchKernelGGL(k_rows_gather_g, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, (const uint32_t*)iota,
+                           (uint64_t)n, (const uint64_t*)trow, (const uint64_t*)row, (const uint32_t*)tg,
+                           (const uint64_t*)E->d_leaves, ids);
+        if (hipGetLastError() != hipSuccess) return done2(set_error(DCCRGX_EHIP, "neighbor list copy failed"));
+        return done2(DCCRGX_OK);
+    }
     if (!ids) return done(DCCRGX_OK);
     if (cap < total) return done(set_error(DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)total));
     if (n)
@@ -2258,9 +2470,13 @@ int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, boo
 // id of each local slot [0, nl): the ascending local ids
 int explicit_local_ids(const dccrgx_grid* grid, uint64_t* d_ids, hipStream_t st)
 {
-    const auto& L = grid->ex->local;
-    if (L.empty()) return DCCRGX_OK;
-    return dx_h2d(grid->ctx, d_ids, L.data(), L.size() * 8, st);
+    const Explicit* E = grid->ex;
+    const uint64_t n = E->local.size();
+    if (!n) return DCCRGX_OK;
+    hipLaunchKernelGGL(k_local_ids, dim3(grid_for(n)), dim3(256), 0, st, (const uint64_t*)E->d_leaves,
+                       (const uint32_t*)E->d_local_g, n, d_ids);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
 }
 
 }  // namespace dccrgx

@@ -54,6 +54,100 @@ __device__ inline int64_t ex_find(const ExView& v, uint64_t id)
     }
 }
 
+// the window of neighborhood item h around a cell at indices idx of length
+// L (in indices), wrapped where the grid is periodic; false outside a
+// non-periodic grid (dccrg.hpp:4670-4672, indices_from_neighborhood)
+__device__ inline bool nof_window(const MapParams& p, const int32_t* per, const uint64_t idx[3],
+                                           const int32_t* h, int64_t L, uint64_t wi[3])
+{
+    const int M = p.max_lvl;
+    for (int d = 0; d < 3; d++) {
+        const int64_t G = (int64_t)(p.length[d] << M);
+        int64_t x = (int64_t)idx[d] + (int64_t)h[d] * L;
+        if (x < 0 || x >= G) {
+            if (!per[d]) return false;
+            x %= G;
+            if (x < 0) x += G;
+        }
+        wi[d] = (uint64_t)x;
+    }
+    return true;
+}
+
+// neighbors_of of leaf c (find_neighbors_of, dccrg.hpp:4375-4716) as f(leaf
+// index) per entry, in the reference's list order: per item, the window's
+// cell, else its parent, else its existing children
+template <class F>
+__device__ inline void nof_search(const ExView& v, const int32_t* items, int K, uint64_t c, F f)
+{
+    const MapParams& p = v.mp;
+    const int M = p.max_lvl;
+    uint64_t idx[3];
+    int l;
+    if (!map_indices(p, c, idx, &l)) return;
+    const int64_t L = (int64_t)1 << (M - l);
+    for (int k = 0; k < K; k++) {
+        uint64_t wi[3];
+        if (!nof_window(p, v.per, idx, items + 3 * k, L, wi)) continue;
+        int64_t g = ex_find(v, map_cell(p, wi, l));
+        if (g >= 0) {
+            f((uint32_t)g);
+            continue;
+        }
+        if (l > 0 && (g = ex_find(v, map_cell(p, wi, l - 1))) >= 0) {
+            f((uint32_t)g);
+            continue;
+        }
+        if (l >= M) continue;
+        const uint64_t hl = (uint64_t)(L / 2);
+        for (int ch = 0; ch < 8; ch++) {
+            const uint64_t ci[3] = {wi[0] + (ch & 1) * hl, wi[1] + ((ch >> 1) & 1) * hl, wi[2] + ((ch >> 2) & 1) * hl};
+            const int64_t gc = ex_find(v, map_cell(p, ci, l + 1));
+            if (gc >= 0) f((uint32_t)gc);
+        }
+    }
+}
+
+// neighbors_to by the reference's own search (find_neighbors_to,
+// dccrg.hpp:4744-4897): the windows of the neighborhood_to items around the
+// cell's parent (one level coarser), around each of its children (one level
+// finer) and around the cell itself; a window whose cell at that level is an
+// existing leaf is a cell that has this one among its neighbors_of.  Rows of
+// any leaf from the replicated leaf lookup alone, so a rank builds them for
+// its own cells only (the transpose of neighbors_of needs every leaf's row).
+// Entries may repeat (sorted and made unique afterwards).
+template <class F>
+__device__ inline void nto_search(const ExView& v, const int32_t* items_to, int K, uint64_t c, F f)
+{
+    const MapParams& p = v.mp;
+    const int M = p.max_lvl;
+    uint64_t idx[3];
+    int l;
+    if (!map_indices(p, c, idx, &l)) return;
+    const int64_t L = (int64_t)1 << (M - l);
+    auto probe = [&](const uint64_t base[3], int lv, int64_t len) {
+        for (int k = 0; k < K; k++) {
+            uint64_t wi[3];
+            if (!nof_window(p, v.per, base, items_to + 3 * k, len, wi)) continue;
+            const int64_t g = ex_find(v, map_cell(p, wi, lv));
+            if (g >= 0) f((uint32_t)g);
+        }
+    };
+    if (l > 0) {  // larger cells: windows around the parent
+        const uint64_t pi[3] = {idx[0] - idx[0] % (uint64_t)(2 * L), idx[1] - idx[1] % (uint64_t)(2 * L),
+                                idx[2] - idx[2] % (uint64_t)(2 * L)};
+        probe(pi, l - 1, 2 * L);
+    }
+    if (l < M) {  // smaller cells: windows around each child
+        const uint64_t hl = (uint64_t)(L / 2);
+        for (int ch = 0; ch < 8; ch++) {
+            const uint64_t ci[3] = {idx[0] + (ch & 1) * hl, idx[1] + ((ch >> 1) & 1) * hl, idx[2] + ((ch >> 2) & 1) * hl};
+            probe(ci, l + 1, (int64_t)hl);
+        }
+    }
+    probe(idx, l, L);
+}
+
 // the lookups of an explicit grid (explicit.hip)
 ExView explicit_view(const dccrgx_grid* grid);
 

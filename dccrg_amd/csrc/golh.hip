@@ -122,7 +122,7 @@ struct XArgs {
     const uint64_t* leaves;      // global leaves (ascending)
     const uint32_t* local_g;     // local position -> global leaf index
     const uint32_t* local_slot;  // local position -> storage slot
-    const uint64_t* nof_row;     // neighbors_of CSR over global leaf indices, reference order
+    const uint64_t* nof_row;     // neighbors_of CSR of the local cells (row = local position), reference order
     const uint64_t* nof_id;
     const uint32_t* nof_g;
     const uint32_t* slot_of_g;   // global leaf index -> storage slot
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(256) k_golh_record_x(XArgs x, uint64_t* __rest
         const uint32_t gi = x.local_g[i];
         const uint64_t own_parent = l0_parent(x.map, x.leaves[gi]);
         uint64_t L[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (uint64_t e = x.nof_row[gi]; e < x.nof_row[gi + 1]; e++) {
+        for (uint64_t e = x.nof_row[i]; e < x.nof_row[i + 1]; e++) {  // rows by local position
             const uint64_t nid = x.nof_id[e];
             if (nid == 0) continue;
             const uint64_t np = l0_parent(x.map, nid);
@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(256) k_golh_spread_x(XArgs x, const uint64_t* 
         uint64_t L[8];
         const uint64_t* own = data + (uint64_t)x.local_slot[i] * W;
         for (int j = 0; j < 8; j++) L[j] = own[1 + j];
-        for (uint64_t e = x.nof_row[gi]; e < x.nof_row[gi + 1]; e++) {
+        for (uint64_t e = x.nof_row[i]; e < x.nof_row[i + 1]; e++) {  // rows by local position
             const uint64_t nid = x.nof_id[e];
             if (nid == 0 || l0_parent(x.map, nid) != own_parent) continue;
             const uint64_t* nd = data + (uint64_t)x.slot_of_g[x.nof_g[e]] * W;

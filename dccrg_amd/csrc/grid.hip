@@ -755,7 +755,8 @@ int dccrgx_grid_destroy(dccrgx_grid* grid)
     load_state_free(grid);
     hipEventDestroy(grid->t0);
     hipEventDestroy(grid->t1);
-    delete grid;  // its memory stays in the device pool for the next grid (dx_pool_idle_bytes)
+    delete grid;
+    dx_cache_trim();  // the grid's memory goes back to the device (torch or the user may need it)
     return DCCRGX_OK;
 }
 
@@ -899,6 +900,28 @@ int dccrgx_get_cells(const dccrgx_grid* grid, int32_t id, int32_t which, uint64_
     default:
         return set_error(DCCRGX_EINVAL, "unknown cell class %d", which);
     }
+}
+
+int dccrgx_neighbor_list_stats(const dccrgx_grid* grid, int32_t id, uint64_t out[4])
+{
+    DX_CHECK(grid && out, DCCRGX_EINVAL, "null argument");
+    const Hood* h = find_hood(grid, id);
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", id);
+    for (int k = 0; k < 4; k++) out[k] = 0;
+    if (grid->uniform || !h->d_nof_row) return DCCRGX_OK;  // closed-form rows: nothing stored
+    const uint64_t rows = h->n_rows, nl = grid->ex->local.size();
+    uint64_t e[3] = {0, 0, 0};  // neighbors_of, neighbors_to, stencil entries
+    hipStream_t st = grid->ctx->compute;
+    DX_TRY(dx_d2h(grid->ctx, &e[0], h->d_nof_row + rows, 8, st));
+    DX_TRY(dx_d2h(grid->ctx, &e[1], h->d_nto_row + rows, 8, st));
+    if (h->d_st_row) DX_TRY(dx_d2h(grid->ctx, &e[2], h->d_st_row + nl, 8, st));
+    out[0] = rows;
+    out[1] = e[0];
+    out[2] = e[1];
+    out[3] = (rows + 1) * 8 + e[0] * (8 + 12 + 4)  // neighbors_of: rows, ids, offsets, leaf indices
+             + (rows + 1) * 8 + e[1] * 4           // neighbors_to: rows, leaf indices
+             + (h->d_st_row ? (nl + 1) * 8 + e[2] * (4 + 12) : 0);  // stencil rows: slots, offsets
+    return DCCRGX_OK;
 }
 
 int dccrgx_get_peers(const dccrgx_grid* grid, int32_t id, int32_t send, int32_t* peers,

@@ -229,6 +229,14 @@ struct Explicit {
             while (b <= bi) dir[b++] = (uint32_t)i;
         }
     }
+    // row of leaf g in the neighborhood CSRs, which hold the local cells' rows
+    // by local position (= storage slot); -1 for a leaf of another process
+    int64_t row_of(uint64_t g) const
+    {
+        if (slot_identity) return (int64_t)g;
+        const uint32_t s = slot_of_g[g];
+        return s < local.size() ? (int64_t)s : -1;
+    }
     int64_t find(uint64_t c) const  // global index of a leaf, -1 if none
     {
         if (!dir_valid) build_dir();

@@ -41,31 +41,28 @@ int set_error(int code, const char* fmt, ...);
                                        #expr, ncclGetErrorString(r_));                   \
     } while (0)
 
-// Device allocations of the library come from the device's default memory
-// pool, which keeps freed memory for reuse (release threshold raised in
-// dccrgx_ctx_create): an adaptive run frees and allocates grid structures
+// Device allocations of the library go through a caching layer over
+// hipMalloc (core.hip): an adaptive run frees and allocates grid structures
 // every step, and returning them to the driver each time cost tens of ms.
-// dx_free waits for the device first, as hipFree does.
+// Blocks up to 256 MiB are kept in size classes when freed and handed out
+// again without a runtime call (hipFreeAsync cost ~35 us on torch's bundled
+// HIP runtime and an adaptive step freed ~60 scratch buffers -- 2 ms of the
+// step, tools/api_census.py).  A block freed with ds_free on a stream is
+// reused only by that stream (stream order keeps it safe); blocks freed with
+// dx_free / FreeBatch are reused by any stream once events recorded on every
+// library stream at the free have passed -- no host wait, so a free between a
+// halo's start and wait does not block on the exchange.  Larger blocks go
+// back with hipFree.  The stream-ordered pool (hipMallocAsync) is not used:
+// the copy engines keep stale translations for pool memory the pool re-maps,
+// and copies into fresh pool blocks landed in the wrong pages
+// (tools/micro/pool_trim_copy.hip).
 void dx_slow_note(const char* what, size_t bytes, double ms);  // DCCRGX_TIMING: allocations over 1 ms
 
-// memory the pool holds for reuse (reserved minus in use): free for the
-// library's purposes.  The pool is never trimmed: on /opt/rocm's 7.2 runtime
-// (a process that loads the library before torch, whose bundled runtime has
-// the same soname), after hipMemPoolTrimTo a pinned-host copy into a fresh
-// stream-ordered allocation could land nowhere (a grid's leaf upload read
-// back wrong, tools/rt_bisect.py), so freed memory stays in the pool.
+// idle bytes the cache holds (free for the library's purposes)
 size_t dx_pool_idle_bytes();
+// return every idle cached block to the device (grid and context teardown)
+void dx_cache_trim();
 
-// Library allocations go through a caching layer over the pool (core.hip):
-// blocks up to 256 MiB are kept in size classes when freed and handed out
-// again without a runtime call.  hipFreeAsync costs ~35 us on torch's bundled
-// HIP runtime (4 us on /opt/rocm's) and an adaptive step freed ~60 scratch
-// buffers -- 2 ms of the step (tools/api_census.py).  A block freed with
-// ds_free on a stream is reused only by that stream (stream order keeps it
-// safe); blocks freed with dx_free / FreeBatch are reused by any stream once
-// events recorded on every library stream at the free have passed -- no
-// host wait, so a free between a halo's start and wait does not block on
-// the exchange.
 hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_stream);
 // any_stream: the block becomes reusable by any stream once every library
 // stream of the device has passed the free (events, no host wait)

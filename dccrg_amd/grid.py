@@ -488,6 +488,12 @@ class Dccrg:
             check(lib().dccrgx_get_all_cells(self._h, out.ctypes.data_as(X._u64p), out.size, C.byref(n)))
         return out
 
+    def neighbor_list_stats(self, hood: int = DEFAULT_NEIGHBORHOOD_ID) -> dict:
+        """The device lists this rank holds (dccrgx_neighbor_list_stats)."""
+        out = (C.c_uint64 * 4)()
+        check(lib().dccrgx_neighbor_list_stats(self._h, hood, out))
+        return {"rows": int(out[0]), "nof_entries": int(out[1]), "nto_entries": int(out[2]), "bytes": int(out[3])}
+
     def neighbors_of(self, cells: np.ndarray, hood: int = DEFAULT_NEIGHBORHOOD_ID):
         """Batched get_neighbors_of: (row_ptr, ids, offsets[x,y,z]) as numpy."""
         import torch

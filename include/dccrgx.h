@@ -187,6 +187,13 @@ int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* params,
                        const uint64_t* leaves_host, size_t n_leaves, dccrgx_grid** out);
 int dccrgx_grid_destroy(dccrgx_grid* grid);
 int dccrgx_grid_get_info(const dccrgx_grid* grid, dccrgx_grid_info* out);
+/* the device neighbor lists neighborhood `hood_id` holds on this rank
+ * (explicit grids; the reference keeps neighbors_of / neighbors_to of every
+ * cell on every process, dccrg.hpp:8371-8397): out[0] = rows held (this
+ * rank's local cells), out[1] = neighbors_of entries, out[2] = neighbors_to
+ * entries, out[3] = device bytes of the lists and stencil rows.  Uniform
+ * grids store none (closed-form rows): zeros. */
+int dccrgx_neighbor_list_stats(const dccrgx_grid* grid, int32_t hood_id, uint64_t out[4]);
 
 /* Dccrg::get_process (dccrg.hpp:5886-5902) for n cells on the host: the
  * process owning each existing cell (the replicated cell_process), -1 for a

@@ -224,6 +224,13 @@ def sc_amr(ctx):
             assert [int(c) for c in g.inner_cells()] == ref["inner"]
             assert [int(c) for c in g.outer_cells()] == ref["outer"]
             assert g.get_cells_to_send() == ref["send"] and g.get_cells_to_receive() == ref["recv"]
+            # per-rank lists: this rank's rows only, bytes within 1.2x of (local + ghost) rows
+            st = g.neighbor_list_stats()
+            assert st["rows"] == (0 if g.info.uniform else len(ref["local"]))
+            tot = gather_all((st["rows"], st["bytes"]))
+            per_row = sum(t[1] for t in tot) / len(o.cells())
+            assert sum(t[0] for t in tot) in (0, len(o.cells()))
+            assert st["bytes"] <= 1.2 * (len(ref["local"]) + len(ref["remote"])) * per_row + 64, (st, per_row)
             # data moves with the new plans: surviving cells keep theirs, ghosts match
             loc = g.local_cells()
             vals = g.read_local("v")

@@ -98,6 +98,44 @@ def test_explicit_rank_structures(case, P):
         assert g.get_cells_to_receive() == ref["recv"]
 
 
+@pytest.mark.parametrize("P", [2, 3, 5])
+@pytest.mark.parametrize("case", CASES[2:])
+def test_per_rank_neighbor_lists(case, P):
+    """With several processes a rank holds the lists of its own cells only
+    (the reference keeps every cell's, dccrg.hpp:8371-8397): rows == local
+    cells, entries == the oracle's over the local cells, and list bytes
+    within 1.2x of (local + ghost cells) x the grid's mean bytes per row.
+    Queries of other ranks' cells are searched on demand and still equal the
+    oracle (find_neighbors_of / find_neighbors_to, :4375-4897)."""
+    leaves = leaves_for(case)
+    length, M, per, hood = case[:4]
+    og = O.Grid(length, M, per, hood, leaves)
+    g1 = make(case, leaves)
+    whole = g1.neighbor_list_stats()
+    assert whole["rows"] == len(leaves)
+    g1.close()
+    cells = np.array(leaves, dtype=np.uint64)
+    total = 0
+    for r in range(P):
+        g = make(case, leaves, r, P)
+        st = g.neighbor_list_stats()
+        loc = [int(c) for c in g.local_cells()]
+        assert st["rows"] == len(loc)
+        assert st["nof_entries"] == sum(len(og.find_neighbors_of(c)) for c in loc)
+        assert st["nto_entries"] == sum(len(og.find_neighbors_to(c)) for c in loc)
+        assert st["bytes"] <= 1.2 * (len(loc) + len(g.remote_cells())) * whole["bytes"] / len(leaves) + 64
+        total += st["rows"]
+        row, ids, off = g.neighbors_of(cells)  # every leaf: local rows stored, the others searched
+        for i, c in enumerate(leaves):
+            got = [(int(ids[k]), tuple(int(v) for v in off[k])) for k in range(int(row[i]), int(row[i + 1]))]
+            assert got == og.find_neighbors_of(c), (r, c)
+        row, ids = g.neighbors_to(cells)
+        for i, c in enumerate(leaves):
+            assert [int(v) for v in ids[int(row[i]):int(row[i + 1])]] == og.find_neighbors_to(c), (r, c)
+        g.close()
+    assert total == len(leaves)
+
+
 def loopback(grids, fields):
     msgs = {}
     for r, g in enumerate(grids):
