@@ -209,6 +209,71 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces(AdvPtrs p, double 
         for (uint64_t s = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < t1; s += stride) rho_out[s] = p.rho[s];
 }
 
+// k_ex_advect_faces with the per-cell and gathered loads as buffer loads:
+// one buffer resource per array and a 32-bit byte offset per lane, instead
+// of a 64-bit address per lane and load (the gathers' address arithmetic was
+// 68 of the kernel's ~400 VALU instructions per cell).  Arrays below 2 GiB.
+__device__ inline __amdgpu_buffer_rsrc_t adv_rsrc(const void* p)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+__device__ inline double adv_ld(__amdgpu_buffer_rsrc_t r, uint32_t i)
+{
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8u), 0, 0));
+}
+
+template <int WPE>
+__global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, double dt, FaceView fc,
+                                                             const uint32_t* __restrict__ pos, uint64_t n,
+                                                             double* __restrict__ rho_out, uint64_t t0, uint64_t t1)
+{
+#pragma clang fp contract(off)
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const __amdgpu_buffer_rsrc_t rr = adv_rsrc(p.rho), rl0 = adv_rsrc(p.l[0]), rl1 = adv_rsrc(p.l[1]),
+                                 rl2 = adv_rsrc(p.l[2]), rv0 = adv_rsrc(p.v[0]), rv1 = adv_rsrc(p.v[1]),
+                                 rv2 = adv_rsrc(p.v[2]), rf = adv_rsrc(p.flux);
+    const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(fc.ell_slot), 0, 0x7fffffff,
+                                                                        0x00020000);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t q = pos ? pos[i] : (uint32_t)i;
+        const uint32_t c = q;  // explicit local slots are [0, n_local)
+        uint32_t s[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++)
+            s[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (int)((uint32_t)(k * fc.n + q) * 4u), 0, 0);
+        const double lc3[3] = {adv_ld(rl0, c), adv_ld(rl1, c), adv_ld(rl2, c)};
+        const double vc3[3] = {adv_ld(rv0, c), adv_ld(rv1, c), adv_ld(rv2, c)};
+        const double rho_c = adv_ld(rr, c);
+        double acc = adv_ld(rf, c);
+        double ln0[6], ln1[6], ln2[6], vn[6], rn[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const uint32_t nb = s[k] != 0xffffffffu ? s[k] : c;
+            ln0[k] = adv_ld(rl0, nb);
+            ln1[k] = adv_ld(rl1, nb);
+            ln2[k] = adv_ld(rl2, nb);
+            vn[k] = adv_ld(k < 2 ? rv0 : k < 4 ? rv1 : rv2, nb);
+            rn[k] = adv_ld(rr, nb);
+        }
+        const double vol = lc3[0] * lc3[1] * lc3[2];
+#pragma unroll
+        for (int k = 0; k < 6; k++)
+            if (s[k] != 0xffffffffu)
+                acc += face_term_v((k & 1) ? (k >> 1) + 1 : -((k >> 1) + 1), dt, vol, lc3, vc3, rho_c, ln0[k], ln1[k],
+                                   ln2[k], vn[k], rn[k]);
+        if (fc.overflow)
+            for (uint64_t e = fc.o_row[q]; e < fc.o_row[q + 1]; e++) acc += face_term(p, c, fc.o_slot[e], fc.o_dir[e], dt, vol);
+        if (!rho_out) {
+            p.flux[c] = acc;
+        } else {
+            rho_out[c] = rho_c + acc;
+            if (adv_ld(rf, c) != 0.0) p.flux[c] = 0.0;
+        }
+    }
+    if (rho_out)
+        for (uint64_t s = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < t1; s += stride) rho_out[s] = p.rho[s];
+}
+
 // check_for_adaptation, tests/advection/adapter.hpp:66-103: max relative
 // density difference over the adapter's face neighbors, maximised into both
 // cells of a pair when the neighbor is local (atomic max on the bit pattern
@@ -587,10 +652,17 @@ int advect_launch(dccrgx_grid* grid, Hood& h, const AdvPtrs& p, double dt, int32
         const FaceView fv{F.n, F.ell_slot, F.o_row, F.o_slot, F.o_dir, F.overflow};
         // explicit grids store local cell q in slot q (explicit.hip): no slot loads
         static const int64_t wpe = getenv_int("DCCRGX_ADV_WPE", 4);  // sweep: waves per SIMD the kernel is built for
-        auto k = wpe >= 8 ? k_ex_advect_faces<8> : wpe >= 6 ? k_ex_advect_faces<6> : wpe >= 5 ? k_ex_advect_faces<5>
-                                                                                             : k_ex_advect_faces<1>;
-        hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv, (const uint32_t*)nullptr,
-                           region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos, R.n, rho_out, t0, t1);
+        const uint32_t* rpos = region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos;
+        static const int64_t use_buf = getenv_int("DCCRGX_ADV_BUF", 1);
+        if (use_buf && grid->n_slots < (1ull << 28) && 6 * F.n < (1ull << 29)) {  // byte offsets below 2 GiB
+            auto k = wpe >= 6 ? k_ex_advect_faces_buf<6> : wpe >= 5 ? k_ex_advect_faces_buf<5> : k_ex_advect_faces_buf<1>;
+            hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv, rpos, R.n, rho_out, t0, t1);
+        } else {
+            auto k = wpe >= 8 ? k_ex_advect_faces<8> : wpe >= 6 ? k_ex_advect_faces<6> : wpe >= 5 ? k_ex_advect_faces<5>
+                                                                                                 : k_ex_advect_faces<1>;
+            hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv, (const uint32_t*)nullptr, rpos,
+                               R.n, rho_out, t0, t1);
+        }
         DX_HIP(hipGetLastError());
         return DCCRGX_OK;
     }

@@ -55,6 +55,7 @@ struct AView {
     const uint64_t* nto_row;
     const uint32_t* nto_g;
     const uint32_t* slot_of_g;  // leaf index -> slot (the row of a local cell)
+    int rows_all;               // one process: the rows are every leaf's (row = leaf index)
     const int32_t* items;     // default neighborhood items (original axes)
     const int32_t* items_to;  // and their negation (neighborhood_to)
     int32_t K;
@@ -434,9 +435,10 @@ __global__ void __launch_bounds__(256) k_collect(AView a, uint32_t bit, uint32_t
 // one round of override_refines (finer = 1: every finer neighbor of a
 // dont_refine leaf joins, :10130-10177) or induce_refines (finer = 0: every
 // coarser neighbor of a refined leaf, :9730-9907); neighbors of / to.  The
-// frontier holds cells of every process: their neighbors are searched from
-// the replicated leaf lookup (nof_search / nto_search), not read from lists,
-// which a process keeps for its own cells only.
+// frontier holds cells of every process: with several processes their
+// neighbors are searched from the replicated leaf lookup (nof_search /
+// nto_search), since a process keeps lists for its own cells only; one
+// process reads its lists.
 __global__ void __launch_bounds__(256) k_spread(AView a, uint32_t bit, int finer, const uint32_t* __restrict__ front,
                                                 const uint32_t* __restrict__ front_n, uint32_t* __restrict__ next,
                                                 uint32_t* __restrict__ next_n)
@@ -453,8 +455,13 @@ __global__ void __launch_bounds__(256) k_spread(AView a, uint32_t bit, int finer
             if (a.flags[t] & bit) return;
             if (!(atomicOr(&a.flags[t], bit) & bit)) next[atomicAdd(next_n, 1u)] = t;
         };
-        nof_search(a.v, a.items, a.K, c, visit);
-        nto_search(a.v, a.items_to, a.K, c, visit);
+        if (a.rows_all) {  // one process holds every leaf's rows: read them
+            for (uint64_t e = a.nof_row[g]; e < a.nof_row[g + 1]; e++) visit(a.nof_g[e]);
+            for (uint64_t e = a.nto_row[g]; e < a.nto_row[g + 1]; e++) visit(a.nto_g[e]);
+        } else {
+            nof_search(a.v, a.items, a.K, c, visit);
+            nto_search(a.v, a.items_to, a.K, c, visit);
+        }
     }
 }
 
@@ -742,6 +749,7 @@ static AView aview(const dccrgx_grid* grid, uint32_t* flags)
     a.nto_row = h.d_nto_row;
     a.nto_g = h.d_nto_g;
     a.slot_of_g = E->d_slot_of_g;
+    a.rows_all = h.n_rows == E->n && E->slot_identity ? 1 : 0;
     a.items = h.d_of_c;
     a.items_to = h.d_to_c;
     a.K = h.K;
