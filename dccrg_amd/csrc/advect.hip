@@ -629,8 +629,7 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
                            R.local_slot, R.level, M, n, fc->ell_slot, (uint32_t*)nullptr, fc->o_row,
                            fc->o_slot, fc->o_dir);
     DX_HIP(hipGetLastError());
-    DX_HIP(hipStreamSynchronize(st));
-    h.faces = fc;
+    h.faces = fc;  // the lists are written in stream order before the kernels that read them
     return DCCRGX_OK;
 }
 

@@ -362,6 +362,11 @@ int rebuild_prepare(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std:
 
     // the new leaf state and neighborhoods (fields untouched meanwhile)
     PhaseTimer T("rebuild");
+    struct Rebuilding {
+        dccrgx_grid* g;
+        ~Rebuilding() { g->rebuilding = false; }
+    } rebuilding{grid};
+    grid->rebuilding = true;
     grid->ex = nullptr;
     grid->uniform = false;
     int s = explicit_init(grid, leaves.data(), leaves.size(), d_leaves, &leaves);  // adopts d_leaves

@@ -1068,22 +1068,26 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, tb, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
     DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, tb2, o.added, d_sorted, (int)cnt[0], 0, bits, st));
     DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, tb3, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
-    sort_lists();
-    uint64_t nk[2] = {0, 0};
-    DX_TRY(dx_d2h(ctx, nk, d_cnt64, 16, st));
-    T.lap("kept + sorted new");
-    const uint64_t n_new = nk[0] + nk[1];
+    // the merge reads both counts on the device, into a list sized for the
+    // most leaves there can be; counts and list come back in one read-back
+    const uint64_t n_max = N + cnt[0];
     uint64_t* d_new = nullptr;
-    DX_HIP(ds_malloc(&d_new, std::max<uint64_t>(n_new, 1) * 8, st));
-    hipLaunchKernelGGL(k_merge, dim3(blocks(n_new)), dim3(256), 0, st, (const uint64_t*)d_kept,
+    DX_HIP(ds_malloc(&d_new, std::max<uint64_t>(n_max, 1) * 8, st));
+    hipLaunchKernelGGL(k_merge, dim3(blocks(n_max)), dim3(256), 0, st, (const uint64_t*)d_kept,
                        (const uint64_t*)d_cnt64, (const uint64_t*)o.added, (const uint64_t*)(d_cnt64 + 1), d_new);
     DX_HIP(hipGetLastError());
-    leaves_host.resize(n_new);
-    const int e = dx_d2h(ctx, leaves_host.data(), d_new, n_new * 8, st);
+    sort_lists();
+    T.lap("kept + sorted new");
+    uint64_t nk[2] = {0, 0};
+    leaves_host.resize(n_max);
+    const D2H back[2] = {{nk, d_cnt64, 16}, {leaves_host.data(), d_new, n_max * 8}};
+    const int e = dx_d2h_many(ctx, back, 2, st);
     if (e != DCCRGX_OK) {
         ds_free(d_new, st);
         return e;
     }
+    const uint64_t n_new = nk[0] + nk[1];
+    leaves_host.resize(n_new);
     T.lap("new leaf list");
     *d_leaves_out = d_new;
     *n_out = n_new;
@@ -1316,11 +1320,12 @@ int amr_dev_codes_to_lists(dccrgx_grid* grid, const uint8_t* d_code, uint64_t n,
         DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, tb, d_ids, d_flags + k * n, d_out + k * n, d_cnt + k, (int)n, st));
     int cnt[3] = {0, 0, 0};
     DX_TRY(dx_d2h(grid->ctx, cnt, d_cnt, 12, st));
+    D2H v[3];
     for (int k = 0; k < 3; k++) {
         counts[k] = (size_t)cnt[k];
-        if (cnt[k]) DX_TRY(dx_d2h(grid->ctx, out[k], d_out + k * n, (size_t)cnt[k] * 8, st));
+        v[k] = D2H{out[k], d_out + k * n, (size_t)cnt[k] * 8};
     }
-    return DCCRGX_OK;
+    return dx_d2h_many(grid->ctx, v, 3, st);  // the three lists behind one synchronisation
 }
 
 }  // namespace dccrgx

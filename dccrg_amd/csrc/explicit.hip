@@ -1269,7 +1269,7 @@ static int sync_slots(dccrgx_grid* grid, bool slot_map_changed)
         DX_TRY(dx_h2d_async(grid->ctx, E->d_level + E->d_level_n, tail.data(), tail.size(), st));
         E->d_level_n = ns;
     }
-    DX_HIP(hipStreamSynchronize(st));
+    if (!grid->rebuilding) DX_HIP(hipStreamSynchronize(st));  // a rebuild synchronises once, at its end
     grid->n_slots = ns;
     return DCCRGX_OK;
 }

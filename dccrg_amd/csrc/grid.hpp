@@ -392,6 +392,7 @@ struct dccrgx_grid {
     // (their capacity: an adaptive run rebuilds every step at similar sizes,
     // and fresh multi-MB vectors cost page faults)
     dccrgx::Explicit* spare_host = nullptr;
+    bool rebuilding = false;  // inside amr.hip rebuild_prepare: intermediate synchronisations are skipped
     // SFC placement (params.partition): owner of each level-0 cell, id - 1
     std::vector<int32_t> sfc_owner;
     int32_t* d_sfc_owner = nullptr;  // its device copy (AMR decisions), made on first use
