@@ -970,13 +970,9 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     const unsigned waves = lds ? 4096 : 1024;
     uint64_t* d_scr = nullptr;
     if (!lds) DX_TRY(S.get(&d_scr, (size_t)waves * (Q + Sz)));
-    int32_t* d_err;
-    DX_TRY(S.get(&d_err, 1));
-    uint32_t *d_retry, *d_nretry;
+    int32_t* d_err = (int32_t*)(d_cnt + NC - 2);  // zeroed with the counters
+    uint32_t *d_retry, *d_nretry = d_cnt + NC - 1;
     DX_TRY(S.get(&d_retry, N));
-    DX_TRY(S.get(&d_nretry, 1));
-    DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
-    DX_HIP(hipMemsetAsync(d_nretry, 0, 4, st));
     // DCCRGX_OU_SMALL (tests): the first pass's queue length, to send walks to the second pass
     const uint32_t Q1 = (uint32_t)std::max<int64_t>(2, getenv_int("DCCRGX_OU_SMALL", 256));
     uint32_t S1 = 16;

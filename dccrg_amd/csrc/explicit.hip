@@ -977,8 +977,7 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     const ExView v = view(grid);
     int32_t* d_err = nullptr;  // error word, then (at +8) the total
     DX_HIP(ds_malloc(&d_err, 16, st));
-    DX_HIP(hipMemsetAsync(d_err, 0, 16, st));
-    DX_HIP(hipMemsetAsync(row, 0, 8, st));
+    DX_HIP(hipMemsetAsync(d_err, 0, 16, st));  // row[0] is written by the scan
     uint64_t* d_codes = nullptr;  // per-item cases for the entry-parallel fill
     if (ids && h.K <= 32 && n) DX_HIP(ds_malloc(&d_codes, n * 8, st));
     if (n)
@@ -1072,8 +1071,7 @@ static int nto_direct(const dccrgx_grid* grid, const Hood& h, const uint64_t* ce
         ds_free(d_tmp, st);
         return code;
     };
-    if (hipMemsetAsync(d_row, 0, 8, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
-    if (n)
+    if (n)  // row[0] is written by the scan
         hipLaunchKernelGGL(k_ex_nto, dim3(grid_for(n)), dim3(256), 0, st, v, (const int32_t*)h.d_to_c, h.K, cells,
                            (size_t)n, d_row, (uint32_t*)nullptr);
     uint64_t tot = 0;
@@ -2330,8 +2328,7 @@ int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t
     if ((s = dx_d2h(grid->ctx, &err, d_err, 4, st)) != DCCRGX_OK) return done(s);
     if (err & 1) return done(set_error(DCCRGX_ENOTFOUND, "cell does not exist"));
     if (err & 4) {  // rows of other processes' cells: searched now (the reference's lists of every cell)
-        if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess || hipMemsetAsync(row, 0, 8, st) != hipSuccess)
-            return done(set_error(DCCRGX_EHIP, "memset"));
+        if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
         hipLaunchKernelGGL(k_ex_nof, dim3(grid_for(n)), dim3(256), 0, st, view(grid), (const int32_t*)h.d_of_c, h.K,
                            cells, n, row, (uint64_t*)nullptr, (int32_t*)nullptr, (uint32_t*)nullptr, d_err,
                            (uint64_t*)nullptr);

@@ -43,9 +43,10 @@ __device__ __forceinline__ uint64_t block_inclusive(uint64_t& v, uint64_t* wtot)
 }
 
 __global__ void __launch_bounds__(ST) k_scan_tiles(uint64_t* __restrict__ x, uint64_t m,
-                                                   uint64_t* __restrict__ tile_sum)
+                                                   uint64_t* __restrict__ tile_sum, uint64_t* __restrict__ zero)
 {
     __shared__ uint64_t wtot[ST / 64];
+    if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;  // a CSR's row[0] (no separate memset launch)
     const uint64_t base = (uint64_t)blockIdx.x * STILE + (uint64_t)threadIdx.x * SE;
     uint64_t e[SE];
     uint64_t t = 0;
@@ -92,14 +93,17 @@ __global__ void __launch_bounds__(ST) k_scan_add(uint64_t* __restrict__ x, uint6
 
 }  // namespace
 
-int device_inclusive_scan(uint64_t* x, uint64_t m, hipStream_t st)
+static int inclusive_scan(uint64_t* x, uint64_t m, hipStream_t st, uint64_t* zero)
 {
-    if (!m) return DCCRGX_OK;
+    if (!m) {
+        if (zero) DX_HIP(hipMemsetAsync(zero, 0, 8, st));
+        return DCCRGX_OK;
+    }
     const uint64_t nt = (m + STILE - 1) / STILE;
     DX_CHECK(nt < (1ull << 31), DCCRGX_EINVAL, "scan of %llu elements", (unsigned long long)m);
     uint64_t* sums = nullptr;
     DX_HIP(ds_malloc(&sums, nt * 8, st));
-    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)nt), dim3(ST), 0, st, x, m, sums);
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)nt), dim3(ST), 0, st, x, m, sums, zero);
     if (nt > 1) {
         hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(ST), 0, st, sums, nt);
         hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nt), dim3(ST), 0, st, x, m, (const uint64_t*)sums);
@@ -109,10 +113,11 @@ int device_inclusive_scan(uint64_t* x, uint64_t m, hipStream_t st)
     return DCCRGX_OK;
 }
 
+int device_inclusive_scan(uint64_t* x, uint64_t m, hipStream_t st) { return inclusive_scan(x, m, st, nullptr); }
+
 int device_scan_rows(uint64_t* row, uint64_t n, hipStream_t st, uint64_t* total)
 {
-    DX_HIP(hipMemsetAsync(row, 0, 8, st));
-    DX_TRY(device_inclusive_scan(row + 1, n, st));
+    DX_TRY(inclusive_scan(row + 1, n, st, row));  // row[0] = 0 written by the first tile
     if (total) {  // through a pinned word: a pageable read-back costs a staging copy
         static thread_local uint64_t* word = nullptr;
         if (!word) DX_HIP(hipHostMalloc((void**)&word, 64, hipHostMallocDefault));
