@@ -408,8 +408,8 @@ __global__ void __launch_bounds__(256) k_flags_gather(AView a, uint64_t* __restr
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
         const uint32_t f = a.flags[g] & RF_SETS;
+        const uint32_t p = wave_reserve(cnt, f ? 1u : 0u);
         if (!f) continue;
-        const uint32_t p = atomicAdd(cnt, 1u);
         ids[p] = a.leaves[g];
         bits[p] = f;
     }
@@ -428,7 +428,8 @@ __global__ void __launch_bounds__(256) k_collect(AView a, uint32_t bit, uint32_t
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
         uint32_t f = a.flags[g];
         if (bit == RF_REFINE && (f & RF_NOT_REFINE) && (f & RF_REFINE)) a.flags[g] = f &= ~RF_REFINE;
-        if (f & bit) out[atomicAdd(cnt, 1u)] = (uint32_t)g;
+        const uint32_t p = wave_reserve(cnt, (f & bit) ? 1u : 0u);
+        if (f & bit) out[p] = (uint32_t)g;
     }
 }
 
@@ -634,35 +635,49 @@ __global__ void __launch_bounds__(256) k_exec(AView a, const uint32_t* __restric
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
         const uint32_t f = a.flags[g];
         const uint64_t c = a.leaves[g];
-        if (f & RF_REFINE) {
+        // what this leaf adds: children of a refined leaf; the parent of an
+        // unrefined group (by its walker, or by a lone request)
+        const bool ref = (f & RF_REFINE) != 0;
+        const bool ref_local = ref && a_owner(a, c) == a.rank;
+        bool fin = false, fin_local = false;
+        uint64_t par = 0, ch[8];
+        if (f & RF_FINAL) {
+            par = a_parent(a, c);
+            a_children(a, par, ch);
+            const int64_t g0 = ch[0] ? ex_find(a.v, ch[0]) : -1;
+            bool all = true;
+            for (int k = 0; k < 8 && all; k++) all = ch[k] && ex_find(a.v, ch[k]) >= 0;
+            fin = !(all && grp[(uint32_t)g0] != (uint32_t)g);  // the group's walker does it
+            fin_local = fin && a_owner(a, par) == a.rank;       // the children's process too
+        }
+        uint32_t nch = 0;
+        if (fin_local)
+            for (int k = 0; k < 8; k++) nch += ch[k] ? 1u : 0u;
+        const uint32_t p_add = wave_reserve(&o.cnt[0], (ref ? 8u : 0u) + (fin ? 1u : 0u));
+        const uint32_t p_new = wave_reserve(&o.cnt[1], ref_local ? 8u : 0u);
+        const uint32_t p_rem = wave_reserve(&o.cnt[2], nch);
+        uint32_t p_ret = wave_reserve(&o.cnt[3], (ref_local ? 1u : 0u) + nch);
+        if (ref) {
             atomicOr(&a.flags[g], RF_GONE);
-            uint64_t ch[8];
-            a_children(a, c, ch);
-            const uint32_t p = atomicAdd(&o.cnt[0], 8u);
-            for (int k = 0; k < 8; k++) o.added[p + k] = ch[k];
-            if (a_owner(a, c) == a.rank) {
-                const uint32_t q = atomicAdd(&o.cnt[1], 8u);
-                for (int k = 0; k < 8; k++) o.newc[q + k] = ch[k];
-                o.retired[atomicAdd(&o.cnt[3], 1u)] = c;
+            uint64_t cc[8];
+            a_children(a, c, cc);
+            for (int k = 0; k < 8; k++) o.added[p_add + k] = cc[k];
+            if (ref_local) {
+                for (int k = 0; k < 8; k++) o.newc[p_new + k] = cc[k];
+                o.retired[p_ret++] = c;
             }
         }
-        if (!(f & RF_FINAL)) continue;
-        const uint64_t par = a_parent(a, c);
-        uint64_t ch[8];
-        a_children(a, par, ch);
-        const int64_t g0 = ch[0] ? ex_find(a.v, ch[0]) : -1;
-        bool all = true;
-        for (int k = 0; k < 8 && all; k++) all = ch[k] && ex_find(a.v, ch[k]) >= 0;
-        if (all && grp[(uint32_t)g0] != (uint32_t)g) continue;  // the group's walker does it
-        o.added[atomicAdd(&o.cnt[0], 1u)] = par;
-        const bool local = a_owner(a, par) == a.rank;  // the children's process too
+        if (!fin) continue;
+        o.added[p_add + (ref ? 8u : 0u)] = par;
+        uint32_t w = 0;
         for (int k = 0; k < 8; k++) {
             if (!ch[k]) continue;
             const int64_t gc = ex_find(a.v, ch[k]);
             if (gc >= 0) atomicOr(&a.flags[gc], RF_GONE);
-            if (local) {
-                o.removed[atomicAdd(&o.cnt[2], 1u)] = ch[k];
-                o.retired[atomicAdd(&o.cnt[3], 1u)] = ch[k];
+            if (fin_local) {
+                o.removed[p_rem + w] = ch[k];
+                o.retired[p_ret + w] = ch[k];
+                w++;
             }
         }
     }
@@ -679,8 +694,11 @@ __global__ void __launch_bounds__(256) k_kept_flags(AView a, uint8_t* __restrict
 __global__ void __launch_bounds__(256) k_nr_ids(AView a, uint64_t* __restrict__ out, uint32_t* __restrict__ cnt)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride)
-        if (a.flags[g] & RF_NOT_REFINE) out[atomicAdd(cnt, 1u)] = a.leaves[g];
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
+        const bool hit = (a.flags[g] & RF_NOT_REFINE) != 0;
+        const uint32_t p = wave_reserve(cnt, hit ? 1u : 0u);
+        if (hit) out[p] = a.leaves[g];
+    }
 }
 
 __device__ inline uint64_t lower_bound_u64(const uint64_t* v, uint64_t n, uint64_t x)

@@ -44,13 +44,29 @@ __global__ void __launch_bounds__(256) k_hash_insert(const uint64_t* __restrict_
     }
 }
 
+// the bitmap of the ascending leaf list: lanes holding ids of the same 64-bit
+// word OR their bits together across the wave (a segmented doubling
+// reduction) and the first lane of each run stores them with one atomic --
+// one atomic per leaf on the same few words serialised (230 us on 3.5 M leaves)
 __global__ void __launch_bounds__(256) k_bits_set(const uint64_t* __restrict__ leaves, size_t n,
                                                   unsigned long long* bits)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t id = leaves[i];
-        atomicOr(&bits[id >> 6], 1ull << (id & 63));
+    const int lane = threadIdx.x & 63;
+    const size_t n64 = (n + 63) & ~(size_t)63;  // every lane of a wave runs every iteration
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n64; i += stride) {
+        const bool valid = i < n;
+        const uint64_t id = valid ? leaves[i] : 0;
+        const uint64_t w = valid ? id >> 6 : ~0ull;
+        unsigned long long b = valid ? 1ull << (id & 63) : 0ull;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long y = __shfl_down(b, d, 64);
+            const uint64_t yw = __shfl_down(w, d, 64);
+            if (lane + d < 64 && yw == w) b |= y;
+        }
+        const uint64_t pw = __shfl_up(w, 1, 64);
+        if (valid && (lane == 0 || pw != w)) atomicOr(&bits[w], b);
     }
 }
 
@@ -516,13 +532,6 @@ __global__ void __launch_bounds__(256) k_ex_nto(ExView v, const int32_t* __restr
     }
 }
 
-__global__ void __launch_bounds__(64) k_stencil_rows_wave(const uint64_t* __restrict__ nof_row,
-                                                          const uint32_t* __restrict__ nof_g,
-                                                          const int32_t* __restrict__ nof_off,
-                                                          const uint32_t* __restrict__ local_g, uint64_t nl,
-                                                          const uint64_t* __restrict__ tmp_row, Pair* __restrict__ tmp,
-                                                          uint32_t* __restrict__ ucnt);
-
 __global__ void __launch_bounds__(256) k_ex_gol(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                 uint32_t* __restrict__ cnt, const uint64_t* __restrict__ st_row,
                                                 const uint32_t* __restrict__ st_slot,
@@ -718,29 +727,67 @@ constexpr uint32_t ROW_PEND = 0xfffffffdu;  // row of 17..64 entries, for the 64
 // wave): the short rows of face neighborhoods fill a wave 4 at a time.  A
 // row longer than W is flagged -- for the 64-lane pass (PEND_ONLY: the
 // flagged rows only), then for the LDS / per-thread kernels.
+// rows handed from one pass to the next as compacted lists: the 16-lane pass
+// appends the rows it leaves for the 64-lane pass, which appends the rows it
+// leaves for the LDS pass (a pass that walked every row to find its few cost
+// ~250 us per pass on 3.5 M rows)
+struct RowLists {
+    uint32_t* pend;  // rows longer than 16 entries
+    uint32_t* med;   // rows of 65..WAVE_SORT_MAX entries
+    uint32_t* cnt;   // [0] pend, [1] med
+};
+
 template <int W, bool PEND_ONLY>
 __global__ void __launch_bounds__(256) k_sort_unique_rows_seg(const uint64_t* __restrict__ row, uint64_t n,
-                                                              uint32_t* __restrict__ v, uint32_t* __restrict__ ucnt)
+                                                              uint32_t* __restrict__ v, uint32_t* __restrict__ ucnt,
+                                                              RowLists L)
 {
     constexpr int R = 64 / W;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const int lane = threadIdx.x & 63, sl = lane & (W - 1), seg = lane / W;
     const uint64_t segmask = (W >= 64 ? ~0ull : ((1ull << (W & 63)) - 1ull)) << (seg * W);
+    if constexpr (PEND_ONLY) {  // W == 64: a wave per row the 16-lane pass left
+        const uint32_t np = L.cnt[0];
+        for (uint64_t k = wave; k < np; k += waves) {
+            const uint64_t r = L.pend[k];
+            const uint64_t b = row[r];
+            const int m = (int)(row[r + 1] - b);
+            if (m > 64) {
+                if (lane == 0) {
+                    ucnt[r] = m > WAVE_SORT_MAX ? ROW_LONG : ROW_MEDIUM;
+                    if (m <= WAVE_SORT_MAX) L.med[atomicAdd(&L.cnt[1], 1u)] = (uint32_t)r;
+                }
+                continue;
+            }
+            uint32_t x = lane < m ? v[b + lane] : 0xffffffffu;
+            x = seg_sort<64>(x, [](uint32_t a, uint32_t c) { return a < c; });
+            const uint32_t prev = __shfl_up(x, 1, 64);
+            const bool keep = lane < m && (lane == 0 || x != prev);
+            const uint64_t mask = __ballot(keep);
+            if (keep) v[b + __popcll(mask & ((1ull << lane) - 1ull))] = x;
+            if (lane == 0) ucnt[r] = (uint32_t)__popcll(mask);
+        }
+        return;
+    }
     for (uint64_t r0 = wave * R; r0 < n; r0 += waves * R) {
         const uint64_t r = r0 + seg;
-        bool active = r < n && (!PEND_ONLY || ucnt[r] == ROW_PEND);
+        bool active = r < n;
         uint64_t b = 0;
         int m = 0;
+        bool pend = false;
         if (active) {
             b = row[r];
             m = (int)(row[r + 1] - b);
             if (m > W) {
-                if (sl == 0) ucnt[r] = W < 64 ? ROW_PEND : (m > WAVE_SORT_MAX ? ROW_LONG : ROW_MEDIUM);
+                pend = true;
+                if (sl == 0) ucnt[r] = ROW_PEND;
                 active = false;
             }
         }
-        if (!__ballot(active)) continue;  // the whole wave idle (most rows in the 64-lane pass)
+        const uint32_t pk = wave_reserve(&L.cnt[0], pend && sl == 0 ? 1u : 0u);
+        if (pend && sl == 0) L.pend[pk] = (uint32_t)r;
+        if (!__ballot(active)) continue;
         uint32_t x = active && sl < m ? v[b + sl] : 0xffffffffu;
         x = seg_sort<W>(x, [](uint32_t a, uint32_t c) { return a < c; });
         const uint32_t prev = __shfl_up(x, 1, W);
@@ -752,11 +799,13 @@ __global__ void __launch_bounds__(256) k_sort_unique_rows_seg(const uint64_t* __
 }
 
 __global__ void __launch_bounds__(64) k_sort_unique_rows_wave(const uint64_t* __restrict__ row, uint64_t n,
-                                                              uint32_t* __restrict__ v, uint32_t* __restrict__ ucnt)
+                                                              uint32_t* __restrict__ v, uint32_t* __restrict__ ucnt,
+                                                              RowLists L)
 {
     __shared__ uint32_t a[WAVE_SORT_MAX];
-    for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
-        if (ucnt[r] != ROW_MEDIUM) continue;
+    const uint32_t nm = L.cnt[1];
+    for (uint32_t k = blockIdx.x; k < nm; k += gridDim.x) {
+        const uint64_t r = L.med[k];
         const uint64_t b = row[r];
         const int m = (int)(row[r + 1] - b);
         int m2 = 1;
@@ -765,7 +814,7 @@ __global__ void __launch_bounds__(64) k_sort_unique_rows_wave(const uint64_t* __
         __syncthreads();
         wave_bitonic(a, m2, [](uint32_t x, uint32_t y) { return x < y; });
         const uint32_t u = wave_unique(a, m, [](uint32_t x, uint32_t y) { return x == y; },
-                                       [&](uint32_t k, uint32_t x) { v[b + k] = x; });
+                                       [&](uint32_t kk, uint32_t x) { v[b + kk] = x; });
         if (threadIdx.x == 0) ucnt[r] = u;
         __syncthreads();
     }
@@ -796,11 +845,12 @@ __global__ void __launch_bounds__(64) k_stencil_rows_wave(const uint64_t* __rest
                                                           const int32_t* __restrict__ nof_off,
                                                           const uint32_t* __restrict__ local_g, uint64_t nl,
                                                           const uint64_t* __restrict__ tmp_row, Pair* __restrict__ tmp,
-                                                          uint32_t* __restrict__ ucnt)
+                                                          uint32_t* __restrict__ ucnt, RowLists L)
 {
     __shared__ Pair a[WAVE_SORT_MAX];
-    for (uint64_t i = blockIdx.x; i < nl; i += gridDim.x) {
-        if (ucnt[i] != ROW_MEDIUM) continue;
+    const uint32_t nm = L.cnt[1];
+    for (uint32_t k0 = blockIdx.x; k0 < nm; k0 += gridDim.x) {
+        const uint64_t i = L.med[k0];
         const uint32_t r = local_g[i];
         const uint64_t b = nof_row[r];
         const int m = (int)(nof_row[r + 1] - b);
@@ -831,28 +881,64 @@ __global__ void __launch_bounds__(256) k_stencil_rows_seg(const uint64_t* __rest
                                                           const int32_t* __restrict__ nof_off,
                                                           const uint32_t* __restrict__ local_g, uint64_t nl,
                                                           const uint64_t* __restrict__ tmp_row, Pair* __restrict__ tmp,
-                                                          uint32_t* __restrict__ ucnt)
+                                                          uint32_t* __restrict__ ucnt, RowLists L)
 {
     constexpr int R = 64 / W;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const int lane = threadIdx.x & 63, sl = lane & (W - 1), seg = lane / W;
     const uint64_t segmask = (W >= 64 ? ~0ull : ((1ull << (W & 63)) - 1ull)) << (seg * W);
+    if constexpr (PEND_ONLY) {  // W == 64: a wave per row the 16-lane pass left
+        const uint32_t np = L.cnt[0];
+        for (uint64_t k = wave; k < np; k += waves) {
+            const uint64_t i = L.pend[k];
+            const uint32_t r = local_g[i];
+            const uint64_t b = nof_row[r];
+            const int m = (int)(nof_row[r + 1] - b);
+            if (m > 64) {
+                if (lane == 0) {
+                    ucnt[i] = m > WAVE_SORT_MAX ? ROW_LONG : ROW_MEDIUM;
+                    if (m <= WAVE_SORT_MAX) L.med[atomicAdd(&L.cnt[1], 1u)] = (uint32_t)i;
+                }
+                continue;
+            }
+            Pair x{0xffffffffu, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+            if (lane < m) {
+                const uint64_t e = b + lane;
+                x = Pair{nof_g[e], nof_off[3 * e], nof_off[3 * e + 1], nof_off[3 * e + 2]};
+            }
+            x = seg_sort<64>(x, [](const Pair& a, const Pair& c) { return pair_less_(a, c); });
+            Pair prev;
+            prev.g = __shfl_up(x.g, 1, 64);
+            prev.x = __shfl_up(x.x, 1, 64);
+            prev.y = __shfl_up(x.y, 1, 64);
+            prev.z = __shfl_up(x.z, 1, 64);
+            const bool keep = lane < m && (lane == 0 || !pair_eq(x, prev));
+            const uint64_t mask = __ballot(keep);
+            if (keep) tmp[tmp_row[i] + __popcll(mask & ((1ull << lane) - 1ull))] = x;
+            if (lane == 0) ucnt[i] = (uint32_t)__popcll(mask);
+        }
+        return;
+    }
     for (uint64_t i0 = wave * R; i0 < nl; i0 += waves * R) {
         const uint64_t i = i0 + seg;
-        bool active = i < nl && (!PEND_ONLY || ucnt[i] == ROW_PEND);
+        bool active = i < nl;
         uint64_t b = 0;
         int m = 0;
+        bool pend = false;
         if (active) {
             const uint32_t r = local_g[i];
             b = nof_row[r];
             m = (int)(nof_row[r + 1] - b);
             if (m > W) {
-                if (sl == 0) ucnt[i] = W < 64 ? ROW_PEND : (m > WAVE_SORT_MAX ? ROW_LONG : ROW_MEDIUM);
+                pend = true;
+                if (sl == 0) ucnt[i] = ROW_PEND;
                 active = false;
             }
         }
-        if (!__ballot(active)) continue;  // the whole wave idle (most rows in the 64-lane pass)
+        const uint32_t pk = wave_reserve(&L.cnt[0], pend && sl == 0 ? 1u : 0u);
+        if (pend && sl == 0) L.pend[pk] = (uint32_t)i;
+        if (!__ballot(active)) continue;
         Pair x{0xffffffffu, 0x7fffffff, 0x7fffffff, 0x7fffffff};
         if (active && sl < m) {
             const uint64_t e = b + sl;
@@ -1026,6 +1112,25 @@ __global__ void __launch_bounds__(256) k_local_ids(const uint64_t* __restrict__ 
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = leaves[local_g[i]];
 }
 
+// the row lists of one sort (RowLists), freed with it
+struct RowListBufs {
+    RowLists L{};
+    hipStream_t st = nullptr;
+    int make(uint64_t n, hipStream_t s)
+    {
+        st = s;
+        DX_HIP(ds_malloc(&L.pend, std::max<uint64_t>(n, 1) * 4, st));
+        DX_HIP(ds_malloc(&L.med, std::max<uint64_t>(n, 1) * 4, st));
+        DX_HIP(ds_malloc(&L.cnt, 8, st));
+        DX_HIP(hipMemsetAsync(L.cnt, 0, 8, st));
+        return DCCRGX_OK;
+    }
+    ~RowListBufs()
+    {
+        for (void* q : {(void*)L.pend, (void*)L.med, (void*)L.cnt}) ds_free(q, st);
+    }
+};
+
 // rows (row[n + 1], `tot` entries in v) sorted and made unique in place,
 // then copied compacted into a new CSR (*out_row, *out_v)
 static int sort_unique_compact(const uint64_t* row, uint32_t* v, uint64_t n, uint64_t tot, uint64_t** out_row,
@@ -1033,13 +1138,15 @@ static int sort_unique_compact(const uint64_t* row, uint32_t* v, uint64_t n, uin
 {
     uint32_t* d_ucnt = nullptr;
     DX_HIP(ds_malloc(&d_ucnt, std::max<uint64_t>(n, 1) * 4, st));
+    RowListBufs RL;
+    DX_TRY(RL.make(n, st));
     if (n) {
         hipLaunchKernelGGL((k_sort_unique_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((n + 15) / 16, 16384)),
-                           dim3(256), 0, st, row, n, v, d_ucnt);
+                           dim3(256), 0, st, row, n, v, d_ucnt, RL.L);
         hipLaunchKernelGGL((k_sort_unique_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((n + 3) / 4, 4096)),
-                           dim3(256), 0, st, row, n, v, d_ucnt);
+                           dim3(256), 0, st, row, n, v, d_ucnt, RL.L);
         hipLaunchKernelGGL(k_sort_unique_rows_wave, dim3((unsigned)std::min<uint64_t>(n, 4096)), dim3(64), 0, st, row, n,
-                           v, d_ucnt);
+                           v, d_ucnt, RL.L);
         hipLaunchKernelGGL(k_sort_unique_rows, dim3(grid_for(n)), dim3(256), 0, st, row, n, v, d_ucnt);
     }
     DX_HIP(hipGetLastError());
@@ -1569,11 +1676,12 @@ __global__ void __launch_bounds__(256) k_inc_count(const uint32_t* __restrict__ 
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
         const uint32_t o = new2old[j];
-        if (o != NO_SLOT && !touched[o]) {
+        const bool copied = o != NO_SLOT && !touched[o];
+        const uint32_t k = wave_reserve(naff, copied ? 0u : 1u);
+        if (copied) {
             row[j + 1] = orow[o + 1] - orow[o];
             continue;
         }
-        const uint32_t k = atomicAdd(naff, 1u);
         aff[k] = (uint32_t)j;
         aff_ids[k] = leaves[j];
     }
@@ -1984,16 +2092,18 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
         if (e != DCCRGX_OK) return st_done(e);
         if (ds_malloc(&d_apairs, std::max<uint64_t>(atot, 1) * sizeof(Pair), st) != hipSuccess)
             return st_done(set_error(DCCRGX_ENOMEM, "incremental stencil rows"));
+        RowListBufs RL;
+        if (na && (e = RL.make(na, st)) != DCCRGX_OK) return st_done(e);
         if (na) {
             hipLaunchKernelGGL((k_stencil_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((na + 15) / 16, 16384)),
                                dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, (const uint32_t*)inc.aff, na,
-                               (const uint64_t*)d_arow, d_apairs, d_apc);
+                               (const uint64_t*)d_arow, d_apairs, d_apc, RL.L);
             hipLaunchKernelGGL((k_stencil_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((na + 3) / 4, 4096)),
                                dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, (const uint32_t*)inc.aff, na,
-                               (const uint64_t*)d_arow, d_apairs, d_apc);
+                               (const uint64_t*)d_arow, d_apairs, d_apc, RL.L);
             hipLaunchKernelGGL(k_stencil_rows_wave, dim3((unsigned)std::min<uint64_t>(na, 4096)), dim3(64), 0, st,
                                h.d_nof_row, h.d_nof_g, h.d_nof_off, (const uint32_t*)inc.aff, na,
-                               (const uint64_t*)d_arow, d_apairs, d_apc);
+                               (const uint64_t*)d_arow, d_apairs, d_apc, RL.L);
             hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(na)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
                                h.d_nof_off, (const uint32_t*)inc.aff, na, (const uint64_t*)d_arow, d_apairs, d_apc);
         }
@@ -2025,15 +2135,17 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
         if (!L.d_all_pos) DX_TRY(device_iota(&L.d_all_pos, nl, st));  // row of local position i: i
         DX_HIP(ds_malloc(&d_pairs, std::max<uint64_t>(tmp_tot, 1) * sizeof(Pair), st));
         DX_HIP(ds_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4, st));
+        RowListBufs RL;
+        if (nl) DX_TRY(RL.make(nl, st));
         if (nl) {
             hipLaunchKernelGGL((k_stencil_rows_seg<16, false>), dim3((unsigned)std::min<uint64_t>((nl + 15) / 16, 16384)),
                                dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, L.d_all_pos, nl, d_tmp_row, d_pairs,
-                               d_pc);
+                               d_pc, RL.L);
             hipLaunchKernelGGL((k_stencil_rows_seg<64, true>), dim3((unsigned)std::min<uint64_t>((nl + 3) / 4, 4096)),
                                dim3(256), 0, st, h.d_nof_row, h.d_nof_g, h.d_nof_off, L.d_all_pos, nl, d_tmp_row, d_pairs,
-                               d_pc);
+                               d_pc, RL.L);
             hipLaunchKernelGGL(k_stencil_rows_wave, dim3((unsigned)std::min<uint64_t>(nl, 4096)), dim3(64), 0, st,
-                               h.d_nof_row, h.d_nof_g, h.d_nof_off, L.d_all_pos, nl, d_tmp_row, d_pairs, d_pc);
+                               h.d_nof_row, h.d_nof_g, h.d_nof_off, L.d_all_pos, nl, d_tmp_row, d_pairs, d_pc, RL.L);
             hipLaunchKernelGGL(k_stencil_rows, dim3(grid_for(nl)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g,
                                h.d_nof_off, L.d_all_pos, nl, d_tmp_row, d_pairs, d_pc);
         }
