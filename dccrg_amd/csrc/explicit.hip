@@ -785,8 +785,10 @@ __global__ void __launch_bounds__(256) k_sort_unique_rows_seg(const uint64_t* __
                 active = false;
             }
         }
-        const uint32_t pk = wave_reserve(&L.cnt[0], pend && sl == 0 ? 1u : 0u);
-        if (pend && sl == 0) L.pend[pk] = (uint32_t)r;
+        if (__ballot(pend && sl == 0)) {  // rare: most rows fit the pass
+            const uint32_t pk = wave_reserve(&L.cnt[0], pend && sl == 0 ? 1u : 0u);
+            if (pend && sl == 0) L.pend[pk] = (uint32_t)r;
+        }
         if (!__ballot(active)) continue;
         uint32_t x = active && sl < m ? v[b + sl] : 0xffffffffu;
         x = seg_sort<W>(x, [](uint32_t a, uint32_t c) { return a < c; });
@@ -936,8 +938,10 @@ __global__ void __launch_bounds__(256) k_stencil_rows_seg(const uint64_t* __rest
                 active = false;
             }
         }
-        const uint32_t pk = wave_reserve(&L.cnt[0], pend && sl == 0 ? 1u : 0u);
-        if (pend && sl == 0) L.pend[pk] = (uint32_t)i;
+        if (__ballot(pend && sl == 0)) {
+            const uint32_t pk = wave_reserve(&L.cnt[0], pend && sl == 0 ? 1u : 0u);
+            if (pend && sl == 0) L.pend[pk] = (uint32_t)i;
+        }
         if (!__ballot(active)) continue;
         Pair x{0xffffffffu, 0x7fffffff, 0x7fffffff, 0x7fffffff};
         if (active && sl < m) {
