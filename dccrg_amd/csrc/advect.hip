@@ -71,47 +71,46 @@ __device__ inline int face_dir(int64_t cl, int64_t nl, const int32_t* off)
     return overlaps == 2 ? direction : 0;
 }
 
-// face lists of local cells from the stencil rows.  Column k of the first
-// six holds the cell's face neighbor in direction k = -x, +x, -y, +y, -z, +z
-// (the first one met in stencil order; 0xffffffff: none), so the kernels
-// know each column's axis and sign at compile time; further neighbors in a
-// direction (finer cells: 2 per face in 2-D, 4 in 3-D) go to the overflow
-// rows with their direction.  Pass 1 (o_row == null) writes the columns and
-// counts the overflow into o_cnt; pass 2 writes the overflow at o_row.
+// face lists of local cells from the stencil rows, in one pass.  Column k of
+// the first six holds the cell's face neighbor in direction k = -x, +x, -y,
+// +y, -z, +z (the first one met in stencil order; 0xffffffff: none), so the
+// kernels know each column's axis and sign at compile time; further
+// neighbors in a direction (finer cells: 2 per face in 2-D, 4 in 3-D) go to
+// the overflow with their direction, o_cnt[q] of them from the cell's
+// stencil row offset (a row's overflow is a subset of the row): no count
+// pass, scan or read-back.  *over = 1 when some cell has overflow.
 __global__ void __launch_bounds__(256) k_face_build(const uint64_t* __restrict__ st_row,
                                                     const uint32_t* __restrict__ st_slot,
                                                     const int32_t* __restrict__ st_off,
                                                     const uint32_t* __restrict__ local_g,
                                                     const uint8_t* __restrict__ level, int M, uint64_t n,
                                                     uint32_t* __restrict__ ell_slot, uint32_t* __restrict__ o_cnt,
-                                                    const uint64_t* __restrict__ o_row, uint32_t* __restrict__ o_slot,
-                                                    int8_t* __restrict__ o_dir)
+                                                    uint32_t* __restrict__ o_slot, int8_t* __restrict__ o_dir,
+                                                    uint32_t* __restrict__ over)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
         const int64_t cl = 1ll << (M - level[local_g[q]]);
         uint32_t used = 0, k = 0;
-        for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) {
+        const uint64_t base = st_row[q];
+        for (uint64_t e = base; e < st_row[q + 1]; e++) {
             const uint32_t nb = st_slot[e];
             const int dir = face_dir(cl, 1ll << (M - level[nb]), st_off + 3 * e);
             if (!dir) continue;
             const int col = 2 * ((dir > 0 ? dir : -dir) - 1) + (dir > 0 ? 1 : 0);
             if (!(used >> col & 1u)) {
                 used |= 1u << col;
-                if (!o_row) ell_slot[col * n + q] = nb;
+                ell_slot[col * n + q] = nb;
                 continue;
             }
-            if (o_row) {
-                o_slot[o_row[q] + k] = nb;
-                o_dir[o_row[q] + k] = (int8_t)dir;
-            }
+            o_slot[base + k] = nb;
+            o_dir[base + k] = (int8_t)dir;
             k++;
         }
-        if (!o_row) {
-            for (int col = 0; col < 6; col++)
-                if (!(used >> col & 1u)) ell_slot[col * n + q] = 0xffffffffu;
-            o_cnt[q] = k;
-        }
+        for (int col = 0; col < 6; col++)
+            if (!(used >> col & 1u)) ell_slot[col * n + q] = 0xffffffffu;
+        o_cnt[q] = k;
+        if (__ballot(k > 0) && (threadIdx.x & 63) == 0) atomicOr(over, 1u);
     }
 }
 
@@ -120,10 +119,11 @@ __global__ void __launch_bounds__(256) k_face_build(const uint64_t* __restrict__
 struct FaceView {  // trivially copyable kernel argument
     uint64_t n;
     const uint32_t* ell_slot;
-    const uint64_t* o_row;
+    const uint64_t* o_base;
+    const uint32_t* o_cnt;
     const uint32_t* o_slot;
     const int8_t* o_dir;
-    bool overflow;
+    const uint32_t* over;  // device flag (a scalar load per wave)
 };
 
 __device__ inline double sel3(int k, double x0, double x1, double x2) { return k == 0 ? x0 : (k == 1 ? x1 : x2); }
@@ -196,8 +196,9 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces(AdvPtrs p, double 
             if (s[k] != 0xffffffffu)
                 acc += face_term_v((k & 1) ? (k >> 1) + 1 : -((k >> 1) + 1), dt, vol, lc3, vc3, rho_c, ln0[k], ln1[k],
                                    ln2[k], vn[k], rn[k]);
-        if (fc.overflow)
-            for (uint64_t e = fc.o_row[q]; e < fc.o_row[q + 1]; e++) acc += face_term(p, c, fc.o_slot[e], fc.o_dir[e], dt, vol);
+        if (*fc.over)
+            for (uint64_t e = fc.o_base[q], e1 = e + fc.o_cnt[q]; e < e1; e++)
+                acc += face_term(p, c, fc.o_slot[e], fc.o_dir[e], dt, vol);
         if (!rho_out) {
             p.flux[c] = acc;
         } else {
@@ -261,8 +262,9 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, dou
             if (s[k] != 0xffffffffu)
                 acc += face_term_v((k & 1) ? (k >> 1) + 1 : -((k >> 1) + 1), dt, vol, lc3, vc3, rho_c, ln0[k], ln1[k],
                                    ln2[k], vn[k], rn[k]);
-        if (fc.overflow)
-            for (uint64_t e = fc.o_row[q]; e < fc.o_row[q + 1]; e++) acc += face_term(p, c, fc.o_slot[e], fc.o_dir[e], dt, vol);
+        if (*fc.over)
+            for (uint64_t e = fc.o_base[q], e1 = e + fc.o_cnt[q]; e < e1; e++)
+                acc += face_term(p, c, fc.o_slot[e], fc.o_dir[e], dt, vol);
         if (!rho_out) {
             p.flux[c] = acc;
         } else {
@@ -590,13 +592,9 @@ void uniform_local_run(const dccrgx_grid* grid, uint64_t* s0, uint64_t* n)
     *n = u.hi - u.lo;
 }
 
-__global__ void __launch_bounds__(256) k_cnt_to_row(const uint32_t* __restrict__ cnt, uint64_t n, uint64_t* __restrict__ row)
-{
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) row[i + 1] = cnt[i];
-}
 
-// build the face lists of a neighborhood's local cells (explicit grids)
+// build the face lists of a neighborhood's local cells (explicit grids):
+// one pass, no synchronisation
 int build_faces(const dccrgx_grid* grid, Hood& h)
 {
     ExRegion R;
@@ -605,29 +603,18 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
     auto fc = std::make_shared<FaceCache>();
     const uint64_t n = R.n;
     fc->n = n;
-    const size_t m = std::max<uint64_t>(n, 1);
+    const size_t m = std::max<uint64_t>(n, 1), cap = std::max<uint64_t>(h.st_cap, 1);
     DX_HIP(dx_malloc(&fc->ell_slot, 6 * m * 4));
-    DX_HIP(dx_malloc(&fc->o_row, (m + 1) * 8));
-    uint32_t* d_cnt = nullptr;
-    DX_HIP(dx_malloc(&d_cnt, m * 4));
+    DX_HIP(dx_malloc(&fc->o_cnt, m * 4));
+    DX_HIP(dx_malloc(&fc->o_slot, cap * 4));
+    DX_HIP(dx_malloc(&fc->o_dir, cap));
+    DX_HIP(dx_malloc(&fc->d_over, 4));
+    fc->o_base = h.d_st_row;
+    DX_HIP(hipMemsetAsync(fc->d_over, 0, 4, st));
     const int M = grid->map.max_lvl;
     if (n)
         hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
-                           R.local_slot, R.level, M, n, fc->ell_slot, d_cnt, (const uint64_t*)nullptr,
-                           (uint32_t*)nullptr, (int8_t*)nullptr);
-    DX_HIP(hipGetLastError());
-    // overflow rows by a device scan (one 8-byte read-back for the total)
-    if (n) hipLaunchKernelGGL(k_cnt_to_row, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)d_cnt, n, fc->o_row);
-    uint64_t total = 0;
-    DX_TRY(device_scan_rows(fc->o_row, n, st, &total));
-    ds_free(d_cnt, st);
-    fc->overflow = total > 0;
-    DX_HIP(dx_malloc(&fc->o_slot, std::max<uint64_t>(total, 1) * 4));
-    DX_HIP(dx_malloc(&fc->o_dir, std::max<uint64_t>(total, 1)));
-    if (fc->overflow)
-        hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
-                           R.local_slot, R.level, M, n, fc->ell_slot, (uint32_t*)nullptr, fc->o_row,
-                           fc->o_slot, fc->o_dir);
+                           R.local_slot, R.level, M, n, fc->ell_slot, fc->o_cnt, fc->o_slot, fc->o_dir, fc->d_over);
     DX_HIP(hipGetLastError());
     h.faces = fc;  // the lists are written in stream order before the kernels that read them
     return DCCRGX_OK;
@@ -648,7 +635,7 @@ int advect_launch(dccrgx_grid* grid, Hood& h, const AdvPtrs& p, double dt, int32
         if (!work) return DCCRGX_OK;
         if (!h.faces) DX_TRY(build_faces(grid, h));
         const FaceCache& F = *h.faces;
-        const FaceView fv{F.n, F.ell_slot, F.o_row, F.o_slot, F.o_dir, F.overflow};
+        const FaceView fv{F.n, F.ell_slot, F.o_base, F.o_cnt, F.o_slot, F.o_dir, F.d_over};
         // explicit grids store local cell q in slot q (explicit.hip): no slot loads
         static const int64_t wpe = getenv_int("DCCRGX_ADV_WPE", 4);  // sweep: waves per SIMD the kernel is built for
         const uint32_t* rpos = region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos;
@@ -719,7 +706,7 @@ int density_spare(dccrgx_grid* grid, double** out, size_t* bytes)
 FaceCache::~FaceCache()
 {
     FreeBatch fb;
-    for (void* q : {(void*)ell_slot, (void*)o_row, (void*)o_slot, (void*)o_dir}) fb.add(q);
+    for (void* q : {(void*)ell_slot, (void*)o_cnt, (void*)o_slot, (void*)o_dir, (void*)d_over}) fb.add(q);
 }
 
 }  // namespace dccrgx

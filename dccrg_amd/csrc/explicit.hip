@@ -2116,6 +2116,7 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
                            (const uint32_t*)d_apc, N, d_cnt2);
         if ((e = scan_counts_device(d_cnt2, N, &h.d_st_row, nullptr, st)) != DCCRGX_OK) return st_done(e);
         const uint64_t stot = tot;  // unique pairs: at most the rows' entries
+        h.st_cap = std::max<uint64_t>(stot, 1);
         if (ds_malloc(&h.d_st_slot, std::max<uint64_t>(stot, 1) * 4, st) != hipSuccess ||
             ds_malloc(&h.d_st_off, std::max<uint64_t>(stot, 1) * 12, st) != hipSuccess)
             return st_done(set_error(DCCRGX_ENOMEM, "stencil rows"));
@@ -2155,6 +2156,7 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
         }
         const uint64_t stot = tmp_tot;  // unique pairs: at most the rows' entries (no read-back)
         DX_TRY(scan_counts_device(d_pc, nl, &h.d_st_row, nullptr, st));
+        h.st_cap = std::max<uint64_t>(stot, 1);
         DX_HIP(ds_malloc(&h.d_st_slot, std::max<uint64_t>(stot, 1) * 4, st));
         DX_HIP(ds_malloc(&h.d_st_off, std::max<uint64_t>(stot, 1) * 12, st));
         if (nl)

@@ -307,10 +307,13 @@ struct CopySeg {
 struct FaceCache {
     uint64_t n = 0;
     uint32_t* ell_slot = nullptr;  // 6 columns: the face neighbor in direction -x, +x, -y, +y, -z, +z
-    uint64_t* o_row = nullptr;
+    // further face neighbors of cell q: o_cnt[q] entries from o_base[q] (the
+    // neighborhood's stencil row offsets: a row's overflow is a subset of it)
+    const uint64_t* o_base = nullptr;
+    uint32_t* o_cnt = nullptr;
     uint32_t* o_slot = nullptr;
     int8_t* o_dir = nullptr;
-    bool overflow = false;
+    uint32_t* d_over = nullptr;    // device flag: some cell has overflow
     ~FaceCache();
 };
 
@@ -353,6 +356,7 @@ struct Hood {
     // (id, offset) pairs, dccrg.hpp:11570-11712) as storage slots
     uint64_t* d_st_row = nullptr;
     uint32_t* d_st_slot = nullptr;
+    uint64_t st_cap = 0;             // entries d_st_slot / d_st_off hold (>= the rows' total)
     int32_t* d_st_off = nullptr;     // x, y, z offset of each stencil entry
     std::shared_ptr<FaceCache> faces;  // advection face lists (explicit grids)
 };
