@@ -1277,6 +1277,8 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
         dx_free(d_e);
         std::fprintf(stderr, "[dccrgx] check_init n %llu leaves differing %llu lookups failing %d first %d bitmap %d\n",
                      (unsigned long long)E->n, (unsigned long long)bad, e[0], e[1] - 1, E->d_bits != nullptr);
+        DX_CHECK(!bad && !e[0], DCCRGX_EINTERNAL, "DCCRGX_CHECK_INIT: %llu leaves of the host list differ from the "
+                 "device list, %d lookups fail", (unsigned long long)bad, e[0]);
     }
     // ownership: the process of the level-0 ancestor (no load balancing),
     // block partition or the grid's SFC table

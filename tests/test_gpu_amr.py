@@ -111,6 +111,8 @@ def rebuild_mode(request, monkeypatch):
     small_walks: override_unrefines' first pass gets a 4-entry queue, so the
     walks overflow into the second, full-size pass (amr_dev.hip k_ou_walk)."""
     monkeypatch.setenv("DCCRGX_INCREMENTAL", "1" if request.param == "incremental" else "0")
+    # every rebuild compares the host-merged leaf list with the device's (explicit.hip explicit_init)
+    monkeypatch.setenv("DCCRGX_CHECK_INIT", "1")
     if request.param == "small_walks":
         monkeypatch.setenv("DCCRGX_OU_SMALL", "4")
     else:
