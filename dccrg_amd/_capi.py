@@ -57,6 +57,16 @@ class FileInfo_t(C.Structure):
                 ("list_offset", C.c_uint64)]
 
 
+class StencilView_t(C.Structure):
+    """dccrgx_stencil_view (include/dccrgx.h): device data of a user stencil."""
+    _fields_ = [("kind", C.c_int32), ("n_items", C.c_int32), ("n_cells", C.c_uint64), ("stream", C.c_void_p),
+                ("la", C.c_uint64), ("lb", C.c_uint64), ("lc", C.c_uint64), ("lo", C.c_uint64), ("hi", C.c_uint64),
+                ("cbase", C.c_int64), ("s0", C.c_int64 * 2), ("s1", C.c_int64 * 2), ("per", C.c_int32 * 3),
+                ("perm", C.c_int32 * 3), ("scale", C.c_int32), ("reach", C.c_int32 * 3), ("reserved", C.c_int32 * 2),
+                ("items", C.c_void_p), ("pos", C.c_void_p), ("local_slot", C.c_void_p), ("local_g", C.c_void_p),
+                ("leaves", C.c_void_p), ("row", C.c_void_p), ("nbr_slot", C.c_void_p), ("nbr_off", C.c_void_p)]
+
+
 class AdvectFields_t(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("density", "flux", "vx", "vy", "vz",
                                          "length_x", "length_y", "length_z")]
@@ -181,6 +191,7 @@ SIGNATURES = {
     "dccrgx_amr_requests": (C.c_int, [_vp, C.c_int32, _u64p, C.c_size_t, _szp]),
     "dccrgx_stop_refining": (C.c_int, [_vp, C.POINTER(_u64p), _szp, _szp]),
     "dccrgx_neighbor_list_stats": (C.c_int, [_vp, C.c_int32, C.POINTER(C.c_uint64)]),
+    "dccrgx_stencil_view_get": (C.c_int, [_vp, C.c_int32, C.c_int32, C.POINTER(StencilView_t)]),
     "dccrgx_stop_refining_prepare": (C.c_int, [_vp, C.POINTER(_u64p), _szp, _szp]),
     "dccrgx_stop_refining_finish": (C.c_int, [_vp, C.c_int32]),
     "dccrgx_get_new_cells": (C.c_int, [_vp, _u64p, C.c_size_t, _szp]),

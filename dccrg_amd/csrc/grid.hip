@@ -296,6 +296,7 @@ void free_hood(Hood& h)
     h.d_nof_g = h.d_nto_g = h.d_st_slot = nullptr;
     h.n_rows = 0;
     h.faces.reset();
+    h.iter.reset();
 }
 
 Hood* find_hood(dccrgx_grid* g, int32_t id)

@@ -317,6 +317,16 @@ struct FaceCache {
     ~FaceCache();
 };
 
+// the device user-stencil view's data (stencil.hip, dccrgx_stencil_view_get),
+// made on first use after a structural change
+struct IterCache {
+    int32_t* items = nullptr;      // uniform: 4 per item (a, b, c, mirror), iteration order
+    int32_t reach[3] = {0, 0, 0};  // uniform: largest |item component| per canonical axis
+    uint32_t* slot = nullptr;      // explicit: stencil rows regrouped into iteration order
+    int32_t* off = nullptr;
+    ~IterCache();
+};
+
 struct Hood {
     int32_t id = 0;
     std::vector<int32_t> items;    // original (x, y, z) items, hood_of
@@ -359,6 +369,7 @@ struct Hood {
     uint64_t st_cap = 0;             // entries d_st_slot / d_st_off hold (>= the rows' total)
     int32_t* d_st_off = nullptr;     // x, y, z offset of each stencil entry
     std::shared_ptr<FaceCache> faces;  // advection face lists (explicit grids)
+    std::shared_ptr<IterCache> iter;   // user-stencil view (stencil.hip)
 };
 
 // a rebuild built but not yet adopted (amr.hip rebuild_prepare): the new leaf

@@ -1,0 +1,175 @@
+// stencil.hip -- the device user-stencil view (include/dccrgx_stencil.hpp):
+// what a caller's device functor needs to walk a region's cells and each
+// cell's neighbors_of in the reference's iteration-cache order
+// (dccrg.hpp:11590-11640: unique (id, offset) pairs, the ones whose id is not
+// also a neighbor_to first, each group ascending by (id, x, y, z)).
+//
+// Uniform grids: nothing per cell is stored.  The neighborhood's items are
+// sorted once into that order for a cell no periodic wrap reaches (ids then
+// grow with the canonical (c, b, a) offsets, and an entry is a neighbor_to
+// exactly when the mirrored item is in the neighborhood); cells near a
+// periodic wrap select their entries by key in the header.
+// Explicit grids: the stencil rows (sorted by (id, offset)) regrouped per cell
+// by membership in its neighbors_to row.
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <vector>
+
+#include "grid.hpp"
+
+namespace dccrgx {
+
+IterCache::~IterCache()
+{
+    FreeBatch fb;
+    for (void* q : {(void*)items, (void*)slot, (void*)off}) fb.add(q);
+}
+
+namespace {
+
+unsigned blocks_for(uint64_t n)
+{
+    const uint64_t b = (n + 255) / 256;
+    return (unsigned)(b < 8192 ? (b ? b : 1) : 8192);
+}
+
+// one thread per local cell: its stencil row, entries that are not in the
+// cell's neighbors_to row first, both groups in row order (ascending (id,
+// offset)); membership by slot (one slot per id)
+__global__ void __launch_bounds__(256) k_iter_rows(const uint64_t* __restrict__ st_row,
+                                                   const uint32_t* __restrict__ st_slot,
+                                                   const int32_t* __restrict__ st_off,
+                                                   const uint64_t* __restrict__ nto_row,
+                                                   const uint32_t* __restrict__ nto_g,
+                                                   const uint32_t* __restrict__ slot_of_g, uint64_t nl,
+                                                   uint32_t* __restrict__ it_slot, int32_t* __restrict__ it_off)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
+        const uint64_t e0 = st_row[i], e1 = st_row[i + 1], t0 = nto_row[i], t1 = nto_row[i + 1];
+        uint64_t w = e0;
+        for (int both = 0; both < 2; both++)
+            for (uint64_t e = e0; e < e1; e++) {
+                const uint32_t s = st_slot[e];
+                bool in_to = false;
+                for (uint64_t t = t0; t < t1 && !in_to; t++) in_to = slot_of_g[nto_g[t]] == s;
+                if (in_to != (both != 0)) continue;
+                it_slot[w] = s;
+                it_off[3 * w] = st_off[3 * e];
+                it_off[3 * w + 1] = st_off[3 * e + 1];
+                it_off[3 * w + 2] = st_off[3 * e + 2];
+                w++;
+            }
+    }
+}
+
+int build_iter(const dccrgx_grid* grid, Hood& h, hipStream_t st)
+{
+    auto ic = std::make_shared<IterCache>();
+    if (grid->uniform) {
+        const int K = h.K;
+        std::vector<std::array<int32_t, 4>> it(K);
+        for (int k = 0; k < K; k++) {
+            const int32_t* d = &h.of_c[3 * k];
+            bool mirror = false;
+            for (int j = 0; j < K && !mirror; j++)
+                mirror = h.of_c[3 * j] == -d[0] && h.of_c[3 * j + 1] == -d[1] && h.of_c[3 * j + 2] == -d[2];
+            it[k] = {d[0], d[1], d[2], mirror ? 1 : 0};
+            for (int a = 0; a < 3; a++) ic->reach[a] = std::max(ic->reach[a], std::abs(d[a]));
+        }
+        // only-neighbors_of entries first, then by id: canonical (c, b, a)
+        std::sort(it.begin(), it.end(), [](const std::array<int32_t, 4>& x, const std::array<int32_t, 4>& y) {
+            if (x[3] != y[3]) return x[3] < y[3];
+            if (x[2] != y[2]) return x[2] < y[2];
+            if (x[1] != y[1]) return x[1] < y[1];
+            return x[0] < y[0];
+        });
+        DX_HIP(dx_malloc(&ic->items, std::max(K, 1) * 16));
+        if (K) DX_TRY(dx_h2d(grid->ctx, ic->items, it.data(), (size_t)K * 16, st));
+    } else {
+        const Explicit* E = grid->ex;
+        const uint64_t nl = E->local.size();
+        DX_CHECK(!nl || (h.d_st_row && h.d_nto_row && E->d_slot_of_g), DCCRGX_EINTERNAL,
+                 "neighborhood %d has no stencil rows", h.id);
+        const uint64_t cap = std::max<uint64_t>(h.st_cap, 1);
+        DX_HIP(dx_malloc(&ic->slot, cap * 4));
+        DX_HIP(dx_malloc(&ic->off, cap * 12));
+        if (nl) {
+            hipLaunchKernelGGL(k_iter_rows, dim3(blocks_for(nl)), dim3(256), 0, st, (const uint64_t*)h.d_st_row,
+                               (const uint32_t*)h.d_st_slot, (const int32_t*)h.d_st_off, (const uint64_t*)h.d_nto_row,
+                               (const uint32_t*)h.d_nto_g, (const uint32_t*)E->d_slot_of_g, nl, ic->slot, ic->off);
+            DX_HIP(hipGetLastError());
+        }
+    }
+    h.iter = ic;
+    return DCCRGX_OK;
+}
+
+}  // namespace
+}  // namespace dccrgx
+
+using namespace dccrgx;
+
+extern "C" {
+
+int dccrgx_stencil_view_get(const dccrgx_grid* grid, int32_t hood_id, int32_t region, dccrgx_stencil_view* out)
+{
+    DX_CHECK(grid && out, DCCRGX_EINVAL, "null argument");
+    Hood* h = const_cast<Hood*>(find_hood(grid, hood_id));  // the view's data is made on first use
+    DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    DX_CHECK(region >= DCCRGX_REGION_ALL && region <= DCCRGX_REGION_OUTER, DCCRGX_EINVAL, "bad region %d", region);
+    DX_CHECK(!grid->load, DCCRGX_ESTATE, "grid data is being loaded");
+    hipStream_t st = grid->ctx->compute;
+    if (!h->iter) DX_TRY(build_iter(grid, *h, st));
+    const IterCache& ic = *h->iter;
+    dccrgx_stencil_view v;
+    std::memset(&v, 0, sizeof v);
+    v.stream = (void*)st;
+    v.scale = 1 << grid->map.max_lvl;
+    if (grid->uniform) {
+        const UGeom& g = grid->g;
+        v.kind = 0;
+        v.n_items = h->K;
+        v.items = ic.items;
+        for (int d = 0; d < 3; d++) v.reach[d] = ic.reach[d];
+        v.la = g.LA;
+        v.lb = g.LB;
+        v.lc = g.LC;
+        v.lo = g.lo;
+        v.hi = g.hi;
+        v.cbase = g.cbase;
+        v.per[0] = g.perA;
+        v.per[1] = g.perB;
+        v.per[2] = g.perC;
+        for (int d = 0; d < 3; d++) v.perm[d] = g.perm[d];
+        int64_t r[2][2];
+        region_slices(grid, *h, region, r);
+        for (int k = 0; k < 2; k++) {
+            v.s0[k] = r[k][0];
+            v.s1[k] = std::max(r[k][0], r[k][1]);
+            // the range's local cells: its slices' lin range within [lo, hi)
+            if (v.s1[k] <= v.s0[k]) continue;
+            const uint64_t a = (uint64_t)(v.s0[k] + g.cbase) * g.S, b = (uint64_t)(v.s1[k] + g.cbase) * g.S;
+            const uint64_t lo = std::max(a, g.lo), hi = std::min(b, g.hi);
+            if (hi > lo) v.n_cells += hi - lo;
+        }
+    } else {
+        ExRegion R;
+        DX_TRY(explicit_region(grid, *h, region, &R));
+        const Explicit* E = grid->ex;
+        v.kind = 1;
+        v.n_cells = R.n;
+        v.pos = R.pos;
+        v.local_slot = R.local_slot;
+        v.local_g = E->d_local_g;
+        v.leaves = E->d_leaves;
+        v.row = h->d_st_row;
+        v.nbr_slot = ic.slot;
+        v.nbr_off = ic.off;
+    }
+    *out = v;
+    return DCCRGX_OK;
+}
+
+}  // extern "C"

@@ -494,6 +494,15 @@ class Dccrg:
         check(lib().dccrgx_neighbor_list_stats(self._h, hood, out))
         return {"rows": int(out[0]), "nof_entries": int(out[1]), "nto_entries": int(out[2]), "bytes": int(out[3])}
 
+    def stencil_view(self, hood: int = DEFAULT_NEIGHBORHOOD_ID, region: int = X.REGION_ALL) -> "X.StencilView_t":
+        """The device data a user stencil walks (dccrgx_stencil_view_get; the
+        C++ side is include/dccrgx_stencil.hpp's for_each_cell): the region's
+        cell count, and for each cell its neighbors_of in the iteration cache's
+        order (dccrg.hpp:11590-11640)."""
+        v = X.StencilView_t()
+        check(lib().dccrgx_stencil_view_get(self._h, hood, region, C.byref(v)))
+        return v
+
     def neighbors_of(self, cells: np.ndarray, hood: int = DEFAULT_NEIGHBORHOOD_ID):
         """Batched get_neighbors_of: (row_ptr, ids, offsets[x,y,z]) as numpy."""
         import torch

@@ -1,0 +1,92 @@
+// user_stencil.hip -- user programs written against include/dccrgx_stencil.hpp:
+// the reference's game of life (examples/game_of_life.cpp:54-79: count the
+// live neighbors over cell.neighbors_of, then apply B3/S23) and a neighbor
+// walk that digests each cell's (neighbor id, x, y, z) sequence, as device
+// functors over a region's cells.  Built into examples/libuser_stencil.so
+// (extern "C", called by tests/test_gpu_user_stencil.py and bench.py).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I../include
+//         user_stencil.hip -o libuser_stencil.so -L../dccrg_amd -ldccrgx
+#include "dccrgx_stencil.hpp"
+
+namespace {
+
+template <class T>
+int field_ptr(const dccrgx_grid* grid, int32_t fid, T** p)
+{
+    void* v = nullptr;
+    uint64_t n = 0;
+    const int e = dccrgx_field_device_ptr(grid, fid, &v, &n);
+    *p = (T*)v;
+    return e;
+}
+
+__device__ inline uint64_t mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+}  // namespace
+
+extern "C" {
+
+// one game-of-life half step over the region: live-neighbor counts of the
+// cells into fcnt, the next state into fout (fin's ghosts must be current)
+int us_gol(const dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t fout, int32_t fcnt, int32_t region)
+{
+    const uint32_t* in;
+    uint32_t *out, *cnt;
+    int e = field_ptr(grid, fin, &in);
+    if (!e) e = field_ptr(grid, fout, &out);
+    if (!e) e = field_ptr(grid, fcnt, &cnt);
+    if (e) return e;
+    return dccrgx_user::for_each_cell(grid, hood_id, region, [=] __device__(const auto& cell) {
+        uint32_t n = 0;
+        cell.for_each_neighbor([&](const dccrgx_user::Neighbor& nb) { n += in[nb.slot] != 0u ? 1u : 0u; });
+        cnt[cell.slot] = n;
+        out[cell.slot] = n == 3u ? 1u : (n == 2u ? in[cell.slot] : 0u);
+    });
+}
+
+// per cell: cid = the cell's id as for_each_cell reports it, dig = a digest of
+// its neighbor sequence h = (h ^ (mix64(id) + x * K1 + y * K2 + z * K3)) * P
+// over the neighbors in order (ids read from field fids, whose ghosts must be
+// current), cnt = the number of neighbors
+int us_digest(const dccrgx_grid* grid, int32_t hood_id, int32_t region, int32_t fids, int32_t fcid, int32_t fdig,
+              int32_t fcnt)
+{
+    const uint64_t* ids;
+    uint64_t *cid, *dig;
+    uint32_t* cnt;
+    int e = field_ptr(grid, fids, &ids);
+    if (!e) e = field_ptr(grid, fcid, &cid);
+    if (!e) e = field_ptr(grid, fdig, &dig);
+    if (!e) e = field_ptr(grid, fcnt, &cnt);
+    if (e) return e;
+    return dccrgx_user::for_each_cell(grid, hood_id, region, [=] __device__(const auto& cell) {
+        uint64_t h = 0xCBF29CE484222325ull;
+        uint32_t n = 0;
+        cell.for_each_neighbor([&](const dccrgx_user::Neighbor& nb) {
+            const uint64_t v = mix64(ids[nb.slot]) + (uint64_t)(int64_t)nb.x * 0x100000001B3ull +
+                               (uint64_t)(int64_t)nb.y * 0x5851F42D4C957F2Dull +
+                               (uint64_t)(int64_t)nb.z * 0x14057B7EF767814Full;
+            h = (h ^ v) * 0x00000100000001B3ull;
+            n++;
+        });
+        cid[cell.slot] = cell.id;
+        dig[cell.slot] = h;
+        cnt[cell.slot] = n;
+    });
+}
+
+// cells a region holds (dccrgx_stencil_view_get's n_cells), -1 on error
+long long us_region_cells(const dccrgx_grid* grid, int32_t hood_id, int32_t region)
+{
+    dccrgx_stencil_view v;
+    if (dccrgx_stencil_view_get(grid, hood_id, region, &v) != DCCRGX_OK) return -1;
+    return (long long)v.n_cells;
+}
+
+}  // extern "C"

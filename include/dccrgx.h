@@ -232,6 +232,52 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
  * DCCRGX_ENOTFOUND if a cell is not local. */
 int dccrgx_gather_neighbors(const dccrgx_grid* grid, int32_t hood_id, int32_t field_id, const uint64_t* cells_dev,
                             size_t n, uint64_t* row_ptr_dev, void* out_dev, size_t cap_bytes, void* stream);
+/* Device user stencils: the reference's loop over a region's cells and each
+ * cell's neighbors_of (examples/game_of_life.cpp:54-79; the iteration cache's
+ * Cells_Item / Neighbors_Item {id, data, x, y, z}, dccrg.hpp:7395-7456 and
+ * the local/inner/outer cell ranges, :11570-11712) as plain device data that
+ * include/dccrgx_stencil.hpp's for_each_cell() launches a caller's device
+ * functor over, one thread per cell.  Neighbors come in the iteration cache's
+ * order: unique (id, offset) pairs, those that are not also neighbors_to
+ * first, each group by ascending (id, x, y, z) (dccrg.hpp:11590-11640).
+ * Uniform grids: neighbors in closed form from the canonical geometry
+ * (nothing stored); explicit grids: the stencil rows, regrouped into that
+ * order on the first call after a structural change.  Neighbor data
+ * is read from the field arrays of dccrgx_field_device_ptr at the neighbor's
+ * slot (remote neighbors: their ghost copies -- update them first).  Valid
+ * until the next structural call (refine, load, new neighborhood).  Regions
+ * as dccrgx_gol_compute's: on uniform grids DCCRGX_REGION_INNER is the whole
+ * slices whose cells read no ghost copy (a subset of the reference's inner
+ * cells) and DCCRGX_REGION_OUTER the rest of the local cells. */
+typedef struct dccrgx_stencil_view {
+    int32_t kind;     /* 0 uniform (closed form), 1 explicit (stored rows) */
+    int32_t n_items;  /* uniform: neighborhood items */
+    uint64_t n_cells; /* cells of the region */
+    void* stream;     /* the grid's compute stream */
+    /* uniform: canonical axes (a fastest, c the partitioned one) */
+    uint64_t la, lb, lc;
+    uint64_t lo, hi;       /* local range of id - 1 */
+    int64_t cbase;         /* canonical slice in storage slice 0 */
+    int64_t s0[2], s1[2];  /* storage slice ranges [s0, s1) of the region */
+    int32_t per[3];        /* canonical periodicity */
+    int32_t perm[3];       /* canonical axis -> x / y / z */
+    int32_t scale;         /* offsets in indices of the finest level: 2^max_ref_lvl */
+    int32_t reach[3];      /* largest |item component| per canonical axis */
+    int32_t reserved[2];
+    /* n_items x 4 int32, device: canonical (a, b, c) of each item and 1 if its
+     * mirror is an item too (the neighbor is also a neighbor_to), in the
+     * iteration cache's order for a cell no periodic wrap reaches */
+    const int32_t* items;
+    /* explicit: stencil rows in the iteration cache's order */
+    const uint32_t* pos;        /* local positions of the region's cells */
+    const uint32_t* local_slot; /* local position -> storage slot */
+    const uint32_t* local_g;    /* local position -> leaf index */
+    const uint64_t* leaves;     /* leaf ids, ascending */
+    const uint64_t* row;        /* stencil rows by local position (n_local + 1) */
+    const uint32_t* nbr_slot;   /* storage slot of each entry */
+    const int32_t* nbr_off;     /* x, y, z offset of each entry, in indices */
+} dccrgx_stencil_view;
+int dccrgx_stencil_view_get(const dccrgx_grid* grid, int32_t hood_id, int32_t region, dccrgx_stencil_view* out);
 /* Dccrg::get_face_neighbors_of (dccrg.hpp:2828-2955) for n cells: the face
  * graph (update_neighbors_, :9463-9597) neighbor in -x,+x,-y,+y,-z,+z order
  * plus, for a smaller neighbor, its 3 siblings sharing the face; dirs_dev
