@@ -516,10 +516,55 @@ def secondary(ctx, torch, D):
                       "achieved_GBs": 36 * nid / (ms * 1e-3) / 1e9,
                       "frac": 36 * nid / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_id": 36}
     del ids
+    out["user_stencil_gol"] = user_stencil_gol(ctx, D)
     out["advection_large"] = advection_large(ctx, D)
     out["mapping_reference_speed_test"] = mapping_speed_test(D, torch, dev)
     out["neighbor_lists"] = neighbor_lists(ctx, D, torch)
     return out
+
+
+def user_stencil_gol(ctx, D):
+    """The reference's game of life written as a user functor over
+    include/dccrgx_stencil.hpp (examples/user_stencil.hip us_gol: count over
+    cell.neighbors_of in iteration order, then B3/S23 -- examples/
+    game_of_life.cpp:54-79) on the headline grid, beside the library's own
+    kernel from the same state: the states and counts must agree."""
+    import ctypes as C
+    L = C.CDLL(os.path.join(ROOT, "examples", "libuser_stencil.so"))
+    L.us_gol.argtypes = [C.c_void_p] + [C.c_int32] * 5
+    n = 2048
+    g = (D.Dccrg().set_initial_length((n, n, n)).set_neighborhood_length(1)
+         .set_maximum_refinement_level(0).set_periodic(False, False, True).initialize(ctx))
+    try:
+        for f in ("a", "b", "n", "c", "d"):
+            g.add_field(f, np.uint32)
+        D.lib().dccrgx_field_init_hash(g._h, g.field_id("a"), 200)
+        hood = D.DEFAULT_NEIGHBORHOOD_ID
+        f = g.field_id
+        # one step each from the same state: the user functor a -> b (counts n),
+        # the library a -> c (counts d)
+        if L.us_gol(g._h, hood, f("a"), f("b"), f("n"), 0) != 0:
+            raise RuntimeError("us_gol failed")
+        g.gol_step("a", "c", "d")
+        ctx.synchronize()
+        same = g.checksum("b") == g.checksum("c") and g.checksum("n") == g.checksum("d")
+        steps = 5
+        cur, nxt = "b", "a"
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            L.us_gol(g._h, hood, f(cur), f(nxt), f("n"), 0)
+            cur, nxt = nxt, cur
+        ctx.synchronize()
+        dt = time.perf_counter() - t0
+        ach = BYTES_PER_CELL * n ** 3 * steps / dt / 1e9
+        return {"workload": "headline grid (2048^3, hood 1, periodic z) stepped by the game of life written "
+                            "as a device user functor (include/dccrgx_stencil.hpp for_each_cell, "
+                            "examples/user_stencil.hip us_gol), one launch per step",
+                "value": n ** 3 * steps / dt, "unit": "cell-updates/s", "steps": steps,
+                "ms_per_step": dt * 1e3 / steps, "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
+                "equals_library_step": same}
+    finally:
+        g.close()
 
 
 def advection_large(ctx, D):

@@ -90,3 +90,30 @@ long long us_region_cells(const dccrgx_grid* grid, int32_t hood_id, int32_t regi
 }
 
 }  // extern "C"
+
+extern "C" {
+// the neighbors of the cell at `slot` as the functor sees them: (id read from
+// fids, x, y, z) into out (4 x int64 per neighbor, at most cap), count returned
+// through *n (device); for debugging a walk
+int us_list(const dccrgx_grid* grid, int32_t hood_id, int32_t fids, uint64_t slot, int64_t* out, uint32_t cap,
+            uint32_t* n)
+{
+    const uint64_t* ids;
+    int e = field_ptr(grid, fids, &ids);
+    if (e) return e;
+    return dccrgx_user::for_each_cell(grid, hood_id, DCCRGX_REGION_ALL, [=] __device__(const auto& cell) {
+        if (cell.slot != slot) return;
+        uint32_t k = 0;
+        cell.for_each_neighbor([&](const dccrgx_user::Neighbor& nb) {
+            if (k < cap) {
+                out[4 * k] = (int64_t)ids[nb.slot];
+                out[4 * k + 1] = nb.x;
+                out[4 * k + 2] = nb.y;
+                out[4 * k + 3] = nb.z;
+            }
+            k++;
+        });
+        *n = k;
+    });
+}
+}  // extern "C"

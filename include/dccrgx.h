@@ -264,10 +264,14 @@ typedef struct dccrgx_stencil_view {
     int32_t scale;         /* offsets in indices of the finest level: 2^max_ref_lvl */
     int32_t reach[3];      /* largest |item component| per canonical axis */
     int32_t reserved[2];
-    /* n_items x 4 int32, device: canonical (a, b, c) of each item and 1 if its
-     * mirror is an item too (the neighbor is also a neighbor_to), in the
-     * iteration cache's order for a cell no periodic wrap reaches */
+    /* n_items x 8 int32, device, in the iteration cache's order for a cell no
+     * periodic wrap reaches: canonical (a, b, c) of each item, 1 if its mirror
+     * is an item too (the neighbor is also a neighbor_to), the x, y, z offset
+     * in indices, 0 */
     const int32_t* items;
+    /* n_items int64, device: the slot distance of each item for a cell no
+     * grid boundary reaches (a + la * b + la * lb * c) */
+    const int64_t* item_delta;
     /* explicit: stencil rows in the iteration cache's order */
     const uint32_t* pos;        /* local positions of the region's cells */
     const uint32_t* local_slot; /* local position -> storage slot */

@@ -53,11 +53,11 @@ namespace detail {
 struct UniformGeo {
     uint64_t la, lb, lc, S, lo, hi;
     int64_t cbase;
-    const int32_t* items; /* 4 per item: canonical a, b, c, mirror flag (iteration order) */
-    int32_t K, scale;
+    const int32_t* items; /* 8 per item: canonical a, b, c, mirror flag, x, y, z (iteration order) */
+    const int64_t* delta; /* slot distance per item */
+    int32_t K;
     int32_t pa, pb, pc;
     int32_t ra, rb, rc; /* reach per canonical axis */
-    int32_t ax, ay, az; /* canonical axis of x, y, z */
 };
 
 /* the iteration cache's order of two entries: (group, id, x, y, z) */
@@ -67,7 +67,7 @@ struct Key {
     int32_t x, y, z;
 };
 
-__device__ inline bool key_less(const Key& p, const Key& q)
+__host__ __device__ inline bool key_less(const Key& p, const Key& q)
 {
     if (p.grp != q.grp) return p.grp < q.grp;
     if (p.id != q.id) return p.id < q.id;
@@ -76,15 +76,10 @@ __device__ inline bool key_less(const Key& p, const Key& q)
     return p.z < q.z;
 }
 
-__device__ inline int64_t wrap(int64_t v, int64_t L)
+__host__ __device__ inline int64_t wrap(int64_t v, int64_t L)
 {
     const int64_t r = v % L;
     return r < 0 ? r + L : r;
-}
-
-__device__ inline int32_t pick(int32_t axis, int32_t da, int32_t db, int32_t dc)
-{
-    return axis == 0 ? da : (axis == 1 ? db : dc);
 }
 
 }  // namespace detail
@@ -100,7 +95,7 @@ struct UniformCell {
     /* neighbor of canonical (a0, b0, c0) at item (da, db, dc): false if it
      * falls outside a non-periodic grid (dccrg.hpp:4670-4672); else a + la * b
      * (wrapped), the wrapped and the unwrapped c */
-    __device__ inline bool step(int64_t a0, int64_t b0, int64_t c0, int32_t da, int32_t db, int32_t dc, uint64_t& ab,
+    __host__ __device__ inline bool step(int64_t a0, int64_t b0, int64_t c0, int32_t da, int32_t db, int32_t dc, uint64_t& ab,
                                 int64_t& cw, int64_t& cu) const
     {
         int64_t a2 = a0 + da, b2 = b0 + db;
@@ -122,32 +117,52 @@ struct UniformCell {
         return true;
     }
 
-    __device__ inline Neighbor make(uint64_t ab, int64_t cs, int32_t da, int32_t db, int32_t dc) const
+    __host__ __device__ inline Neighbor make(uint64_t nslot, int32_t k) const
     {
         Neighbor nb;
-        nb.slot = ab + g.S * (uint64_t)(cs - g.cbase);
-        nb.x = detail::pick(g.ax, da, db, dc) * g.scale;
-        nb.y = detail::pick(g.ay, da, db, dc) * g.scale;
-        nb.z = detail::pick(g.az, da, db, dc) * g.scale;
+        nb.slot = nslot;
+        nb.x = g.items[8 * k + 4];
+        nb.y = g.items[8 * k + 5];
+        nb.z = g.items[8 * k + 6];
         return nb;
     }
 
     template <class G>
-    __device__ inline void for_each_neighbor(G&& fn) const
+    __host__ __device__ inline void for_each_neighbor(G&& fn) const
     {
-        // no periodic wrap within twice the reach: the items' order is the
-        // iteration order (ids grow with (c, b, a); an entry is a neighbor_to
-        // exactly when the mirrored item exists)
-        const bool fast = (!g.pa || (a >= 2 * g.ra && a + 2 * g.ra < (int64_t)g.la)) &&
-                          (!g.pb || (b >= 2 * g.rb && b + 2 * g.rb < (int64_t)g.lb)) &&
-                          (!g.pc || (c >= 2 * g.rc && c + 2 * g.rc < (int64_t)g.lc));
-        if (fast) {
+        // no grid boundary within the reach: every item's neighbor exists at
+        // a fixed slot distance, in the items' order
+        const bool inside = a >= g.ra && a + g.ra < (int64_t)g.la && b >= g.rb && b + g.rb < (int64_t)g.lb &&
+                            c >= g.rc && c + g.rc < (int64_t)g.lc;
+        if (inside) {
+            // unrolled, so that the neighbors' loads of many items are in
+            // flight at once: fully for the default neighborhoods of length 1
+            // (26 items) and 0 (6 items)
+            if (g.K == 26) {
+#pragma unroll
+                for (int32_t k = 0; k < 26; k++) fn(make(slot + (uint64_t)g.delta[k], k));
+            } else if (g.K == 6) {
+#pragma unroll
+                for (int32_t k = 0; k < 6; k++) fn(make(slot + (uint64_t)g.delta[k], k));
+            } else {
+#pragma unroll 8
+                for (int32_t k = 0; k < g.K; k++) fn(make(slot + (uint64_t)g.delta[k], k));
+            }
+            return;
+        }
+        // no periodic wrap within twice the reach: the items' order is still
+        // the iteration order (ids grow with (c, b, a); an entry is a
+        // neighbor_to exactly when the mirrored item exists), items past a
+        // non-periodic boundary are dropped
+        const bool nowrap = (!g.pa || (a >= 2 * g.ra && a + 2 * g.ra < (int64_t)g.la)) &&
+                            (!g.pb || (b >= 2 * g.rb && b + 2 * g.rb < (int64_t)g.lb)) &&
+                            (!g.pc || (c >= 2 * g.rc && c + 2 * g.rc < (int64_t)g.lc));
+        if (nowrap) {
             for (int32_t k = 0; k < g.K; k++) {
-                const int32_t da = g.items[4 * k], db = g.items[4 * k + 1], dc = g.items[4 * k + 2];
                 uint64_t ab;
                 int64_t cw, cu;
-                if (!step(a, b, c, da, db, dc, ab, cw, cu)) continue;
-                fn(make(ab, cu, da, db, dc));  // no wrap: the slot of c + dc, local or ghost
+                if (!step(a, b, c, g.items[8 * k], g.items[8 * k + 1], g.items[8 * k + 2], ab, cw, cu)) continue;
+                fn(make(ab + g.S * (uint64_t)(cu - g.cbase), k));  // the slot of c + dc, local or ghost
             }
             return;
         }
@@ -155,38 +170,37 @@ struct UniformCell {
         const uint64_t self = (uint64_t)a + g.la * (uint64_t)b + g.S * (uint64_t)c;
         detail::Key prev{-1, 0, 0, 0, 0};
         for (int32_t pass = 0; pass < g.K; pass++) {
-            bool found = false;
+            int32_t bk = -1;
+            uint64_t bslot = 0;
             detail::Key best{0, 0, 0, 0, 0};
-            Neighbor bn{0, 0, 0, 0};
             for (int32_t k = 0; k < g.K; k++) {
-                const int32_t da = g.items[4 * k], db = g.items[4 * k + 1], dc = g.items[4 * k + 2];
                 uint64_t ab;
                 int64_t cw, cu;
-                if (!step(a, b, c, da, db, dc, ab, cw, cu)) continue;
+                if (!step(a, b, c, g.items[8 * k], g.items[8 * k + 1], g.items[8 * k + 2], ab, cw, cu)) continue;
                 const uint64_t nlin = ab + g.S * (uint64_t)cw;
                 // a local neighbor (also one reached through a periodic wrap)
                 // is read from its own slot, a remote one from its ghost slot
-                const Neighbor nb = make(ab, (nlin >= g.lo && nlin < g.hi) ? cw : cu, da, db, dc);
-                int32_t grp = g.items[4 * k + 3];
+                const int64_t cs = (nlin >= g.lo && nlin < g.hi) ? cw : cu;
+                int32_t grp = g.items[8 * k + 3];
                 if (!grp) {  // another item of the neighbor may reach this cell through a wrap
                     const int64_t na = (int64_t)(ab % g.la), nbb = (int64_t)(ab / g.la);
                     for (int32_t j = 0; j < g.K && !grp; j++) {
                         uint64_t ab2;
                         int64_t cw2, cu2;
-                        if (step(na, nbb, cw, g.items[4 * j], g.items[4 * j + 1], g.items[4 * j + 2], ab2, cw2, cu2))
+                        if (step(na, nbb, cw, g.items[8 * j], g.items[8 * j + 1], g.items[8 * j + 2], ab2, cw2, cu2))
                             grp = ab2 + g.S * (uint64_t)cw2 == self ? 1 : 0;
                     }
                 }
-                const detail::Key key{grp, nlin, nb.x, nb.y, nb.z};
+                const detail::Key key{grp, nlin, g.items[8 * k + 4], g.items[8 * k + 5], g.items[8 * k + 6]};
                 if (!detail::key_less(prev, key)) continue;
-                if (!found || detail::key_less(key, best)) {
+                if (bk < 0 || detail::key_less(key, best)) {
                     best = key;
-                    bn = nb;
-                    found = true;
+                    bk = k;
+                    bslot = ab + g.S * (uint64_t)(cs - g.cbase);
                 }
             }
-            if (!found) break;
-            fn(bn);
+            if (bk < 0) break;
+            fn(make(bslot, bk));
             prev = best;
         }
     }
@@ -202,7 +216,7 @@ struct ExplicitCell {
     uint32_t q; /* local position */
 
     template <class G>
-    __device__ inline void for_each_neighbor(G&& fn) const
+    __host__ __device__ inline void for_each_neighbor(G&& fn) const
     {
         const uint64_t e1 = row[q + 1];
         for (uint64_t e = row[q]; e < e1; e++) {
@@ -285,19 +299,14 @@ int for_each_cell(const dccrgx_stencil_view& v, F f, hipStream_t st)
         g.hi = v.hi;
         g.cbase = v.cbase;
         g.items = v.items;
+        g.delta = v.item_delta;
         g.K = v.n_items;
-        g.scale = v.scale;
         g.pa = v.per[0];
         g.pb = v.per[1];
         g.pc = v.per[2];
         g.ra = v.reach[0];
         g.rb = v.reach[1];
         g.rc = v.reach[2];
-        int32_t ax[3] = {0, 0, 0};  // perm: canonical axis d -> original axis perm[d]
-        for (int d = 0; d < 3; d++) ax[v.perm[d]] = d;
-        g.ax = ax[0];
-        g.ay = ax[1];
-        g.az = ax[2];
         const uint64_t tiles = (g.S + 255) / 256;
         if (tiles >= (1ull << 31)) return DCCRGX_EINVAL;
         for (int r = 0; r < 2; r++) {
