@@ -807,8 +807,10 @@ int adapt_marks_device(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_f
     DX_HIP(dx_malloc(&d_flag, ns));
     DX_HIP(dx_malloc(&d_marks, n));
     DX_HIP(dx_malloc(&d_diff, n * 8));
-    DX_HIP(hipMemsetAsync(d_max, 0, ns * 8, st));  // max_diff = 0 (:62-64)
-    DX_HIP(hipMemsetAsync(d_flag, 0, ns, st));
+    {
+        const Fill z[2] = {{d_max, ns * 8, 0}, {d_flag, ns, 0}};  // max_diff = 0 (:62-64)
+        DX_TRY(dx_fill_many(z, 2, st));
+    }
     hipLaunchKernelGGL(k_flag_slots, dim3(grid_for(n)), dim3(256), 0, st, R.local_slot, n, d_flag);
     hipLaunchKernelGGL(k_adapt_diff, dim3(grid_for(n)), dim3(256), 0, st, p.rho, h->d_st_row, h->d_st_slot,
                        h->d_st_off, R.local_slot, R.level, grid->map.max_lvl, n, (const uint8_t*)d_flag,

@@ -1002,8 +1002,10 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     DX_TRY(S.get(&d_fb, N));
     DX_TRY(S.get(&d_grp, N));
     DX_TRY(S.get(&d_key, N));
-    DX_HIP(hipMemsetAsync(d_cnt, 0, NC * 4, st));
-    DX_HIP(hipMemsetAsync(d_grp, 0xff, N * 4, st));
+    {
+        const Fill z[2] = {{d_cnt, (size_t)NC * 4, 0}, {d_grp, N * 4, 0xff}};
+        DX_TRY(dx_fill_many(z, 2, st));
+    }
     const unsigned bN = blocks(N);
     // override_refines then induce_refines: at most M rounds each
     for (int phase = 0; phase < 2; phase++) {

@@ -106,6 +106,50 @@ int dx_h2d_async(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t s
     return DCCRGX_OK;
 }
 
+struct FillArgs {
+    uint8_t* p[8];
+    uint64_t bytes[8];
+    uint32_t word[8];  // the value byte replicated
+};
+
+// blockIdx.y: the range; 4-byte stores over the aligned middle, bytes at the ends
+__global__ void __launch_bounds__(256) k_fill_many(FillArgs a)
+{
+    const int r = blockIdx.y;
+    uint8_t* p = a.p[r];
+    const uint64_t n = a.bytes[r];
+    const uint64_t head = std::min<uint64_t>(n, (4 - ((uintptr_t)p & 3)) & 3);
+    const uint64_t words = (n - head) / 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t* w = reinterpret_cast<uint32_t*>(p + head);
+    for (uint64_t i = t0; i < words; i += stride) w[i] = a.word[r];
+    if (t0 < head) p[t0] = (uint8_t)a.word[r];
+    const uint64_t tail = head + words * 4;
+    if (t0 < n - tail) p[tail + t0] = (uint8_t)a.word[r];
+}
+
+int dx_fill_many(const Fill* v, int n, hipStream_t st)
+{
+    DX_CHECK(n >= 0 && n <= 8, DCCRGX_EINTERNAL, "dx_fill_many: %d ranges", n);
+    FillArgs a{};
+    uint64_t most = 0;
+    int m = 0;
+    for (int i = 0; i < n; i++) {
+        if (!v[i].bytes) continue;
+        a.p[m] = (uint8_t*)v[i].p;
+        a.bytes[m] = v[i].bytes;
+        a.word[m] = 0x01010101u * v[i].value;
+        most = std::max<uint64_t>(most, v[i].bytes / 4 + 4);
+        m++;
+    }
+    if (!m) return DCCRGX_OK;
+    const unsigned gx = (unsigned)std::min<uint64_t>((most + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_fill_many, dim3(gx, m), dim3(256), 0, st, a);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
 int dx_d2h_many(Ctx* c, const D2H* v, size_t n, hipStream_t st)
 {
     size_t total = 0;

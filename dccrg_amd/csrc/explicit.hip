@@ -1811,14 +1811,14 @@ static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_
         ds_malloc(&d_touched, oN, st) != hipSuccess || ds_malloc(&d_aff_ids, N * 8, st) != hipSuccess ||
         ds_malloc(&d_err, 16, st) != hipSuccess)
         return done(set_error(DCCRGX_ENOMEM, "incremental neighbor lists"));
-    hipMemsetAsync(d_o2n, 0xff, oN * 4, st);
-    hipMemsetAsync(d_naff, 0, 16, st);
-    hipMemsetAsync(d_err, 0, 16, st);
+    {
+        const Fill z[4] = {{d_o2n, oN * 4, 0xff}, {d_naff, 16, 0}, {d_err, 16, 0}, {h.d_nof_row, 8, 0}};
+        if (dx_fill_many(z, 4, st) != DCCRGX_OK) return done(DCCRGX_EHIP);
+    }
     hipLaunchKernelGGL(k_inc_new2old, dim3(grid_for(N)), dim3(256), 0, st, ov, (const uint64_t*)E->d_leaves, N, d_n2o,
                        d_o2n);
     hipLaunchKernelGGL(k_inc_touched, dim3(grid_for(oN)), dim3(256), 0, st, (const uint64_t*)oh.d_nof_row,
                        (const uint32_t*)oh.d_nof_g, oN, H.old_flags, H.gone_bit, d_touched);
-    hipMemsetAsync(h.d_nof_row, 0, 8, st);
     hipLaunchKernelGGL(k_inc_count, dim3(grid_for(N)), dim3(256), 0, st, (const uint32_t*)d_n2o,
                        (const uint8_t*)d_touched, (const uint64_t*)oh.d_nof_row, (const uint64_t*)E->d_leaves, N,
                        h.d_nof_row, d_aff, d_aff_ids, d_naff);
@@ -2008,8 +2008,10 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
         uint32_t *d_cnt = nullptr, *d_cur = nullptr, *d_tmp = nullptr;
         DX_HIP(ds_malloc(&d_cnt, N * 4, st));
         DX_HIP(ds_malloc(&d_cur, N * 4, st));
-        DX_HIP(hipMemsetAsync(d_cnt, 0, N * 4, st));
-        DX_HIP(hipMemsetAsync(d_cur, 0, N * 4, st));
+        {
+            const Fill z[2] = {{d_cnt, N * 4, 0}, {d_cur, N * 4, 0}};
+            DX_TRY(dx_fill_many(z, 2, st));
+        }
         hipLaunchKernelGGL(k_tr_count, dim3(grid_for(N)), dim3(256), 0, st, h.d_nof_row, h.d_nof_g, N, d_cnt);
         uint64_t* d_trow = nullptr;
         const uint64_t ttot = tot;  // the transpose has as many entries as neighbors_of: no read-back
@@ -2088,8 +2090,10 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
             ds_malloc(&d_apc, std::max<uint64_t>(na, 1) * 4, st) != hipSuccess ||
             ds_malloc(&d_cnt2, std::max<uint64_t>(N, 1) * 4, st) != hipSuccess)
             return st_done(set_error(DCCRGX_ENOMEM, "incremental stencil rows"));
-        hipMemsetAsync(d_aidx, 0xff, N * 4, st);
-        hipMemsetAsync(d_arow, 0, 8, st);
+        {
+            const Fill z[2] = {{d_aidx, N * 4, 0xff}, {d_arow, 8, 0}};
+            if (dx_fill_many(z, 2, st) != DCCRGX_OK) return st_done(DCCRGX_EHIP);
+        }
         if (na)
             hipLaunchKernelGGL(k_st_aff_rows, dim3(grid_for(na)), dim3(256), 0, st, (const uint32_t*)inc.aff, na,
                                (const uint64_t*)h.d_nof_row, d_arow, d_aidx);

@@ -320,7 +320,8 @@ struct FaceCache {
 // the device user-stencil view's data (stencil.hip, dccrgx_stencil_view_get),
 // made on first use after a structural change
 struct IterCache {
-    int32_t* items = nullptr;      // uniform: 4 per item (a, b, c, mirror), iteration order
+    int32_t* items = nullptr;      // uniform: 8 per item (a, b, c, mirror, x, y, z, 0), iteration order
+    int64_t* delta = nullptr;      // uniform: slot distance of each item
     int32_t reach[3] = {0, 0, 0};  // uniform: largest |item component| per canonical axis
     uint32_t* slot = nullptr;      // explicit: stencil rows regrouped into iteration order
     int32_t* off = nullptr;

@@ -411,6 +411,15 @@ struct D2H {
     size_t bytes;
 };
 int dx_d2h_many(Ctx* c, const D2H* v, size_t n, hipStream_t st);
+// several memsets in one launch (each hipMemsetAsync is a launch of its own
+// and costs the host as much as a kernel): at most 8 byte ranges, each set
+// to one byte value
+struct Fill {
+    void* p;
+    size_t bytes;
+    uint8_t value;
+};
+int dx_fill_many(const Fill* v, int n, hipStream_t st);
 
 }  // namespace dccrgx
 

@@ -23,7 +23,7 @@ namespace dccrgx {
 IterCache::~IterCache()
 {
     FreeBatch fb;
-    for (void* q : {(void*)items, (void*)slot, (void*)off}) fb.add(q);
+    for (void* q : {(void*)items, (void*)delta, (void*)slot, (void*)off}) fb.add(q);
 }
 
 namespace {
@@ -85,8 +85,23 @@ int build_iter(const dccrgx_grid* grid, Hood& h, hipStream_t st)
             if (x[1] != y[1]) return x[1] < y[1];
             return x[0] < y[0];
         });
-        DX_HIP(dx_malloc(&ic->items, std::max(K, 1) * 16));
-        if (K) DX_TRY(dx_h2d(grid->ctx, ic->items, it.data(), (size_t)K * 16, st));
+        const UGeom& g = grid->g;
+        const int32_t sc = 1 << grid->map.max_lvl;
+        std::vector<int32_t> rec(std::max(K, 1) * 8, 0);
+        std::vector<int64_t> delta(std::max(K, 1), 0);
+        for (int k = 0; k < K; k++) {
+            int32_t o[3];
+            for (int d = 0; d < 3; d++) o[g.perm[d]] = it[k][d] * sc;  // canonical axis d is axis perm[d]
+            const int32_t r[8] = {it[k][0], it[k][1], it[k][2], it[k][3], o[0], o[1], o[2], 0};
+            std::memcpy(&rec[8 * k], r, sizeof r);
+            delta[k] = it[k][0] + (int64_t)g.LA * it[k][1] + (int64_t)g.S * it[k][2];
+        }
+        DX_HIP(dx_malloc(&ic->items, rec.size() * 4));
+        DX_HIP(dx_malloc(&ic->delta, delta.size() * 8));
+        if (K) {
+            DX_TRY(dx_h2d(grid->ctx, ic->items, rec.data(), (size_t)K * 32, st));
+            DX_TRY(dx_h2d(grid->ctx, ic->delta, delta.data(), (size_t)K * 8, st));
+        }
     } else {
         const Explicit* E = grid->ex;
         const uint64_t nl = E->local.size();
@@ -132,6 +147,7 @@ int dccrgx_stencil_view_get(const dccrgx_grid* grid, int32_t hood_id, int32_t re
         v.kind = 0;
         v.n_items = h->K;
         v.items = ic.items;
+        v.item_delta = ic.delta;
         for (int d = 0; d < 3; d++) v.reach[d] = ic.reach[d];
         v.la = g.LA;
         v.lb = g.LB;

@@ -897,8 +897,13 @@ class Dccrg:
 
     def _advect_fields(self, names=None):
         """names: mapping from the Cell::data members (cell.hpp:34-44) to
-        field names; default: fields named after the members."""
-        names = names or {}
+        field names; default: fields named after the members (made once: a
+        field keeps its id)."""
+        if not names:
+            f = getattr(self, "_adv_default", None)
+            if f is None:
+                f = self._adv_default = X.AdvectFields_t(*[self.field_id(m) for m in self.ADVECT_FIELDS])
+            return f
         return X.AdvectFields_t(*[self.field_id(names.get(m, m)) for m in self.ADVECT_FIELDS])
 
     def add_advection_fields(self):
@@ -926,7 +931,9 @@ class Dccrg:
 
     def advect_step(self, dt: float, hood: int = DEFAULT_NEIGHBORHOOD_ID, names=None):
         f = self._advect_fields(names)
-        check(lib().dccrgx_advect_step(self._h, hood, C.byref(f), dt))
+        s = lib().dccrgx_advect_step(self._h, hood, f, dt)
+        if s:
+            check(s)
 
     def kernel_timer(self, reset: int = 0):
         ms = C.c_double()

@@ -30,15 +30,34 @@ dt = g.max_time_step()
 g.update_copies_of_remote_neighbors(fields=list(A.ALL))
 steps = int(os.environ.get("ADAPT_STEPS", "20"))
 per = []
+seg = os.environ.get("ADAPT_SEG")  # per-phase times, synchronised after each phase (diagnosis)
+segs = []
 for _ in range(steps):
     t0 = time.perf_counter()
+    ts = [t0]
+
+    def mark():
+        if seg:
+            ctx.synchronize()
+            ts.append(time.perf_counter())
     g.update_copies_of_remote_neighbors(fields=["density"])
+    mark()
     sets = A.check_for_adaptation(g, rel / M, thr, sens)
+    mark()
     g.advect_step(cfl * dt)
+    mark()
     A.adapt_grid(g, geom, *sets)
+    mark()
     dt = g.max_time_step()
+    mark()
     per.append((time.perf_counter() - t0) * 1e3)
+    if seg:
+        segs.append([(b - a) * 1e3 for a, b in zip(ts, ts[1:])])
 ctx.synchronize()
+if seg:
+    n = max(len(segs) - 4, 1)
+    print("phases (ghost, check, advect, adapt, dt) ms: " + " ".join(
+        f"{sum(x[i] for x in segs[4:]) / n:.2f}" for i in range(5)), flush=True)
 print("ms/step " + " ".join(f"{x:.2f}" for x in per), flush=True)
 print(f"leaves {g.n_local} mean of last {max(steps - 4, 1)}: "
       f"{sum(per[4:]) / max(len(per[4:]), 1):.2f} ms", flush=True)
