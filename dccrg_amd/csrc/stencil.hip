@@ -155,6 +155,7 @@ int dccrgx_stencil_view_get(const dccrgx_grid* grid, int32_t hood_id, int32_t re
         v.lo = g.lo;
         v.hi = g.hi;
         v.cbase = g.cbase;
+        v.nslices = (int32_t)g.nslices;
         v.per[0] = g.perA;
         v.per[1] = g.perB;
         v.per[2] = g.perC;

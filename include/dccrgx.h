@@ -263,7 +263,8 @@ typedef struct dccrgx_stencil_view {
     int32_t perm[3];       /* canonical axis -> x / y / z */
     int32_t scale;         /* offsets in indices of the finest level: 2^max_ref_lvl */
     int32_t reach[3];      /* largest |item component| per canonical axis */
-    int32_t reserved[2];
+    int32_t nslices;       /* storage slices (local and ghost), la * lb slots each */
+    int32_t reserved;
     /* n_items x 8 int32, device, in the iteration cache's order for a cell no
      * periodic wrap reaches: canonical (a, b, c) of each item, 1 if its mirror
      * is an item too (the neighbor is also a neighbor_to), the x, y, z offset

@@ -215,3 +215,67 @@ def test_user_stencil_view_follows_refinement():
     finally:
         g.close()
         ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("length,per,hood_len", [((70, 40, 9), (True, False, True), 1),
+                                                 ((66, 36, 11), (False, True, False), 2),
+                                                 ((130, 33, 5), (True, True, True), 1)])
+def test_gol_functor_larger_grids(length, per, hood_len, P):
+    """The game-of-life functor over several steps on grids where most cells
+    take the fixed-distance walk (no boundary within reach), with wraps and
+    rank slabs: equal to the oracle's run (oracle gol_reference_run, the
+    reference's lists) on every rank."""
+    import torch
+
+    import dccrg_amd as D
+    from dccrg_amd import _capi as X
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    n = int(np.prod(length))
+    ids = np.arange(1, n + 1, dtype=np.uint64)
+    a0 = O.random_alive(ids, 300)
+    steps = 3
+    ref_a, ref_n = O.gol_reference_run(length, per, hood_len, a0, steps)
+    L = lib()
+    hood = D.DEFAULT_NEIGHBORHOOD_ID
+    ctxs, grids = [], []
+    for r in range(P):
+        ctx = D.Context(0, r, P)
+        g = (D.Dccrg().set_initial_length(length).set_periodic(*per).set_neighborhood_length(hood_len)
+             .initialize(ctx))
+        for f in ("a", "b", "n"):
+            g.add_field(f, np.uint32)
+        g.write_local("a", a0[g.local_cells().astype(np.int64) - 1])
+        ctxs.append(ctx)
+        grids.append(g)
+    try:
+        cur, nxt = "a", "b"
+        for _ in range(steps):
+            msgs = {}
+            for r, g in enumerate(grids):
+                for p in g.get_cells_to_send():
+                    buf = torch.empty(1 << 22, dtype=torch.uint8, device="cuda")
+                    torch.cuda.synchronize()
+                    msgs[(r, p)] = (buf, g.pack_to(p, buf.data_ptr(), buf.numel(), fields=[cur]))
+                    g.ctx.synchronize()
+            for r, g in enumerate(grids):
+                g.halo_self(fields=[cur])
+                for p in g.get_cells_to_receive():
+                    buf, nb = msgs[(p, r)]
+                    g.unpack_from(p, buf.data_ptr(), nb, fields=[cur])
+                g.ctx.synchronize()
+            for g in grids:
+                assert L.us_gol(g._h, hood, g.field_id(cur), g.field_id(nxt), g.field_id("n"),
+                                       X.REGION_ALL) == 0
+                g.ctx.synchronize()
+            cur, nxt = nxt, cur
+        for g in grids:
+            idx = g.local_cells().astype(np.int64) - 1
+            assert np.array_equal(g.read_local(cur), ref_a[idx])
+            assert np.array_equal(g.read_local("n"), ref_n[idx])
+    finally:
+        for g in grids:
+            g.close()
+        for ctx in ctxs:
+            ctx.close()
