@@ -136,7 +136,12 @@ int dccrgx_stencil_view_get(const dccrgx_grid* grid, int32_t hood_id, int32_t re
     DX_CHECK(region >= DCCRGX_REGION_ALL && region <= DCCRGX_REGION_OUTER, DCCRGX_EINVAL, "bad region %d", region);
     DX_CHECK(!grid->load, DCCRGX_ESTATE, "grid data is being loaded");
     hipStream_t st = grid->ctx->compute;
-    if (!h->iter) DX_TRY(build_iter(grid, *h, st));
+    if (!h->iter) {
+        DX_TRY(build_iter(grid, *h, st));
+        // the caller may launch on a stream of its own: the rows are complete
+        // before the view is handed out (once per structural change)
+        DX_HIP(hipStreamSynchronize(st));
+    }
     const IterCache& ic = *h->iter;
     dccrgx_stencil_view v;
     std::memset(&v, 0, sizeof v);

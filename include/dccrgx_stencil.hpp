@@ -25,7 +25,11 @@
  * A cell's or neighbor's data is the element at its `slot` in every field
  * array (dccrgx_field_device_ptr); a remote neighbor's slot holds its ghost
  * copy (dccrgx_halo_update / _start + _wait first).  Neighbor offsets are the
- * reference's x, y, z: indices of the finest level.  Neighbors come in the
+ * reference's x, y, z: indices of the finest level.  Launches go to the
+ * grid's compute stream unless a stream is passed; work on a stream of the
+ * caller's must be finished (or the stream synchronised) before the grid's
+ * next structural call (refine, load, new neighborhood, destroy), which frees
+ * what the view points to.  Neighbors come in the
  * iteration cache's order (dccrg.hpp:11590-11640): unique (id, offset) pairs,
  * those whose id is not also a neighbor_to first, each group ascending by
  * (id, x, y, z) -- so floating-point sums over them round as the reference's
