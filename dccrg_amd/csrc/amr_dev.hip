@@ -725,24 +725,17 @@ __global__ void __launch_bounds__(256) k_merge(const uint64_t* __restrict__ a, c
     }
 }
 
-// indices of the leaves that go (execute_refines), in no particular order
-__global__ void __launch_bounds__(256) k_gone_idx(AView a, uint32_t* __restrict__ out, uint32_t* __restrict__ cnt)
-{
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
-        const bool gone = (a.flags[g] & RF_GONE) != 0;
-        const uint32_t p = wave_reserve(cnt, gone ? 1u : 0u);
-        if (gone) out[p] = (uint32_t)g;
-    }
-}
+// a leaf goes: its keep flag is clear (the ordered selection of their indices)
+struct NotKept {
+    __host__ __device__ bool operator()(uint8_t k) const { return k == 0; }
+};
 
-// new = (old without the leaves at `gone`) merged with `added` (ascending,
-// disjoint from the kept leaves), on the host threads: each takes a run of
+// new = (old without the leaves at `gone`, ascending) merged with `added`
+// (ascending, disjoint from the kept leaves), on the host threads: each takes a run of
 // the old list, the new ids in its id range, and writes at its place
-static void merge_leaves_host(const std::vector<uint64_t>& old, std::vector<uint32_t>& gone,
+static void merge_leaves_host(const std::vector<uint64_t>& old, const std::vector<uint32_t>& gone,
                               const std::vector<uint64_t>& added, std::vector<uint64_t>& out)
 {
-    std::sort(gone.begin(), gone.end());
     const size_t N = old.size(), na = added.size();
     out.resize(N - gone.size() + na);
     if (!N) {
@@ -1082,20 +1075,20 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     T.lap("decisions");
     DX_CHECK(!err, DCCRGX_EINTERNAL, "override_unrefines walk exceeded its workspace");
     // the persisting dont_refine set (flagged leaves, and the ids that are not
-    // leaves) and this rank's new / removed / retired cells, in one read-back
+    // leaves) and this rank's new / removed / retired cells
     nr.resize(cnt[4]);
     A.new_cells.resize(cnt[1]);
     A.removed.resize(cnt[2]);
     retired.resize(cnt[3]);
-    const D2H lists[4] = {{nr.data(), d_nr, cnt[4] * 8ull},
-                          {A.new_cells.data(), o.newc, cnt[1] * 8ull},
-                          {A.removed.data(), o.removed, cnt[2] * 8ull},
-                          {retired.data(), o.retired, cnt[3] * 8ull}};
-    DX_TRY(dx_d2h_many(ctx, lists, 4, st));
-    nr.insert(nr.end(), A.nr_other.begin(), A.nr_other.end());
-    // the three lists sorted side by side on the host threads (after the
-    // device work of the new leaf list is queued, which they overlap)
-    auto sort_lists = [&] {
+    *changed = cnt[0] > 0;
+    T.lap("lists");
+    if (!*changed) {  // one read-back, sorted on the host threads
+        const D2H lists[4] = {{nr.data(), d_nr, cnt[4] * 8ull},
+                              {A.new_cells.data(), o.newc, cnt[1] * 8ull},
+                              {A.removed.data(), o.removed, cnt[2] * 8ull},
+                              {retired.data(), o.retired, cnt[3] * 8ull}};
+        DX_TRY(dx_d2h_many(ctx, lists, 4, st));
+        nr.insert(nr.end(), A.nr_other.begin(), A.nr_other.end());
         std::vector<uint64_t>* lv[3] = {&A.new_cells, &A.removed, &retired};
         const size_t nt = std::min<size_t>(3, host_threads());
         pool_run(nt, [&](size_t t) {
@@ -1105,11 +1098,6 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
                 v.erase(std::unique(v.begin(), v.end()), v.end());
             }
         });
-    };
-    *changed = cnt[0] > 0;
-    T.lap("lists");
-    if (!*changed) {
-        sort_lists();
         return DCCRGX_OK;
     }
     // the new leaf list: surviving leaves in order, merged with the sorted new ones
@@ -1119,19 +1107,48 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     DX_TRY(S.get(&d_kept, N));
     DX_TRY(S.get(&d_sorted, cnt[0]));
     DX_TRY(S.get(&d_cnt64, 2));
+    // the new / removed / retired lists sorted on the device (the host would
+    // sort them while the device waits), unique-d on the host after the read-back
+    uint64_t* d_ls[3];
+    const uint64_t* ls_in[3] = {o.newc, o.removed, o.retired};
+    const uint32_t ls_n[3] = {cnt[1], cnt[2], cnt[3]};
+    for (int k = 0; k < 3; k++) DX_TRY(S.get(&d_ls[k], std::max<uint32_t>(ls_n[k], 1)));
+    // the indices of the leaves that go, ascending: a selection over the
+    // leaf indices (the host merge needs them in order)
+    uint32_t* d_gone;
+    DX_TRY(S.get(&d_gone, N));
+    uint32_t* d_ngone = d_cnt + NC - 3;
     hipLaunchKernelGGL(k_kept_flags, dim3(bN), dim3(256), 0, st, a, d_keep);
-    size_t tb = 0, tb2 = 0, tb3 = 0;
-    DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
-    int bits = 1;  // ids are at most last_cell: sort only its bits
+    const hipcub::CountingInputIterator<uint32_t> leaf_idx(0);
+    const hipcub::TransformInputIterator<bool, NotKept, const uint8_t*> gone_flags(d_keep, NotKept{});
+    size_t tb[6] = {0, 0, 0, 0, 0, 0};
+    DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb[0], a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
+    int bits = 1;  // ids are at most last_cell: sort only their bits
     while (bits < 64 && (grid->map.last_cell >> bits)) bits++;
-    DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb2, o.added, d_sorted, (int)cnt[0], 0, bits, st));
-    DX_HIP(hipcub::DeviceSelect::Unique(nullptr, tb3, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
+    DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb[1], o.added, d_sorted, (int)cnt[0], 0, bits, st));
+    DX_HIP(hipcub::DeviceSelect::Unique(nullptr, tb[2], d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
+    DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb[3], leaf_idx, gone_flags, d_gone, d_ngone, (int)N, st));
+    for (int k = 0; k < 3; k++) {
+        size_t t = 0;
+        DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, t, ls_in[k], d_ls[k], (int)ls_n[k], 0, bits, st));
+        tb[4] = std::max(tb[4], t);
+    }
+    const size_t tmax = *std::max_element(tb, tb + 6);
     uint8_t* d_tmp;
-    DX_TRY(S.get(&d_tmp, std::max({tb, tb2, tb3})));
-    tb = tb2 = tb3 = std::max({tb, tb2, tb3});
-    DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, tb, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
-    DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, tb2, o.added, d_sorted, (int)cnt[0], 0, bits, st));
-    DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, tb3, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
+    DX_TRY(S.get(&d_tmp, std::max<size_t>(tmax, 1)));
+    size_t t = tmax;
+    DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, t, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
+    t = tmax;
+    DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, t, o.added, d_sorted, (int)cnt[0], 0, bits, st));
+    t = tmax;
+    DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, t, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
+    t = tmax;
+    DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, t, leaf_idx, gone_flags, d_gone, d_ngone, (int)N, st));
+    for (int k = 0; k < 3; k++) {
+        if (!ls_n[k]) continue;
+        t = tmax;
+        DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, t, ls_in[k], d_ls[k], (int)ls_n[k], 0, bits, st));
+    }
     // the merge reads both counts on the device, into a list sized for the
     // most leaves there can be
     const uint64_t n_max = N + cnt[0];
@@ -1139,33 +1156,36 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     DX_HIP(ds_malloc(&d_new, std::max<uint64_t>(n_max, 1) * 8, st));
     hipLaunchKernelGGL(k_merge, dim3(blocks(n_max)), dim3(256), 0, st, (const uint64_t*)d_kept,
                        (const uint64_t*)d_cnt64, (const uint64_t*)o.added, (const uint64_t*)(d_cnt64 + 1), d_new);
+    DX_HIP(hipGetLastError());
+    T.lap("kept + sorted new");
     // the host's copy of the new list is merged on the host from its copy of
     // the old one, the gone leaves and the new ids -- small lists instead of
     // the whole list over PCIe (28 MB at 3.5 M leaves, 0.5 ms of copy plus
     // the staging copy)
-    uint32_t* d_gone;
-    DX_TRY(S.get(&d_gone, N));
-    hipLaunchKernelGGL(k_gone_idx, dim3(bN), dim3(256), 0, st, a, d_gone, d_cnt + NC - 3);
-    DX_HIP(hipGetLastError());
-    sort_lists();
-    T.lap("kept + sorted new");
     uint64_t nk[2] = {0, 0};
     uint32_t ngone = 0;
     int e = DCCRGX_OK;
     {
-        const D2H c2[2] = {{nk, d_cnt64, 16}, {&ngone, d_cnt + NC - 3, 4}};
+        const D2H c2[2] = {{nk, d_cnt64, 16}, {&ngone, d_ngone, 4}};
         e = dx_d2h_many(ctx, c2, 2, st);
     }
     std::vector<uint64_t> added(nk[1]);
     std::vector<uint32_t> gone(ngone);
     if (e == DCCRGX_OK) {
-        const D2H l2[2] = {{added.data(), o.added, nk[1] * 8}, {gone.data(), d_gone, (size_t)ngone * 4}};
-        e = dx_d2h_many(ctx, l2, 2, st);
+        const D2H l2[6] = {{added.data(), o.added, nk[1] * 8},
+                           {gone.data(), d_gone, (size_t)ngone * 4},
+                           {nr.data(), d_nr, cnt[4] * 8ull},
+                           {A.new_cells.data(), d_ls[0], cnt[1] * 8ull},
+                           {A.removed.data(), d_ls[1], cnt[2] * 8ull},
+                           {retired.data(), d_ls[2], cnt[3] * 8ull}};
+        e = dx_d2h_many(ctx, l2, 6, st);
     }
     if (e != DCCRGX_OK) {
         ds_free(d_new, st);
         return e;
     }
+    nr.insert(nr.end(), A.nr_other.begin(), A.nr_other.end());
+    for (std::vector<uint64_t>* v : {&A.new_cells, &A.removed, &retired}) v->erase(std::unique(v->begin(), v->end()), v->end());
     const uint64_t n_new = nk[0] + nk[1];
     merge_leaves_host(grid->ex->leaves, gone, added, leaves_host);
     DX_CHECK(leaves_host.size() == n_new, DCCRGX_EINTERNAL, "host leaf list %zu, device %llu", leaves_host.size(),
