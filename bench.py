@@ -525,13 +525,17 @@ def secondary(ctx, torch, D):
 
 def user_stencil_gol(ctx, D):
     """The reference's game of life written as a user functor over
-    include/dccrgx_stencil.hpp (examples/user_stencil.hip us_gol: count over
+    include/dccrgx_stencil.hpp (examples/user_stencil.hip: count over
     cell.neighbors_of in iteration order, then B3/S23 -- examples/
     game_of_life.cpp:54-79) on the headline grid, beside the library's own
-    kernel from the same state: the states and counts must agree."""
+    kernel from the same state: the states and counts must agree.  Two forms:
+    for_each_cell_staged (the alive values staged through LDS and a register
+    window; the boundary shell walked in separate launches) and for_each_cell
+    (every neighbor read through its slot)."""
     import ctypes as C
     L = C.CDLL(os.path.join(ROOT, "examples", "libuser_stencil.so"))
     L.us_gol.argtypes = [C.c_void_p] + [C.c_int32] * 5
+    L.us_gol_staged.argtypes = [C.c_void_p] + [C.c_int32] * 6
     n = 2048
     g = (D.Dccrg().set_initial_length((n, n, n)).set_neighborhood_length(1)
          .set_maximum_refinement_level(0).set_periodic(False, False, True).initialize(ctx))
@@ -541,28 +545,40 @@ def user_stencil_gol(ctx, D):
         D.lib().dccrgx_field_init_hash(g._h, g.field_id("a"), 200)
         hood = D.DEFAULT_NEIGHBORHOOD_ID
         f = g.field_id
-        # one step each from the same state: the user functor a -> b (counts n),
-        # the library a -> c (counts d)
-        if L.us_gol(g._h, hood, f("a"), f("b"), f("n"), 0) != 0:
-            raise RuntimeError("us_gol failed")
-        g.gol_step("a", "c", "d")
+        g.gol_step("a", "c", "d")  # the library's step from the same state
         ctx.synchronize()
-        same = g.checksum("b") == g.checksum("c") and g.checksum("n") == g.checksum("d")
-        steps = 5
-        cur, nxt = "b", "a"
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            L.us_gol(g._h, hood, f(cur), f(nxt), f("n"), 0)
-            cur, nxt = nxt, cur
-        ctx.synchronize()
-        dt = time.perf_counter() - t0
-        ach = BYTES_PER_CELL * n ** 3 * steps / dt / 1e9
-        return {"workload": "headline grid (2048^3, hood 1, periodic z) stepped by the game of life written "
-                            "as a device user functor (include/dccrgx_stencil.hpp for_each_cell, "
-                            "examples/user_stencil.hip us_gol), one launch per step",
-                "value": n ** 3 * steps / dt, "unit": "cell-updates/s", "steps": steps,
-                "ms_per_step": dt * 1e3 / steps, "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
-                "equals_library_step": same}
+        ref = (g.checksum("c"), g.checksum("d"))
+
+        def run(step, steps):
+            # one step a -> b (counts n) checked against the library's, then
+            # `steps` timed steps
+            if step("a", "b") != 0:
+                raise RuntimeError("user stencil launch failed")
+            ctx.synchronize()
+            same = (g.checksum("b"), g.checksum("n")) == ref
+            cur, nxt = "b", "a"
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step(cur, nxt)
+                cur, nxt = nxt, cur
+            ctx.synchronize()
+            dt = time.perf_counter() - t0
+            D.lib().dccrgx_field_init_hash(g._h, g.field_id("a"), 200)  # back to the initial state
+            ach = BYTES_PER_CELL * n ** 3 * steps / dt / 1e9
+            return {"value": n ** 3 * steps / dt, "unit": "cell-updates/s", "steps": steps,
+                    "ms_per_step": dt * 1e3 / steps, "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
+                    "equals_library_step": same}
+
+        staged = run(lambda a, b: L.us_gol_staged(g._h, hood, f(a), f(b), f("n"), 0, 1), 10)
+        walk = run(lambda a, b: L.us_gol(g._h, hood, f(a), f(b), f("n"), 0), 3)
+        staged["workload"] = ("headline grid (2048^3, hood 1, periodic z) stepped by the game of life written as a "
+                              "device user functor over staged values (include/dccrgx_stencil.hpp "
+                              "for_each_cell_staged, examples/user_stencil.hip us_gol_staged): the staged kernel "
+                              "for the interior plus the boundary-shell walks, launches of one step")
+        walk["workload"] = ("the same functor reading every neighbor through its slot (for_each_cell, "
+                            "examples/user_stencil.hip us_gol)")
+        staged["walk"] = walk
+        return staged
     finally:
         g.close()
 

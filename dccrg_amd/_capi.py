@@ -62,7 +62,7 @@ class StencilView_t(C.Structure):
     _fields_ = [("kind", C.c_int32), ("n_items", C.c_int32), ("n_cells", C.c_uint64), ("stream", C.c_void_p),
                 ("la", C.c_uint64), ("lb", C.c_uint64), ("lc", C.c_uint64), ("lo", C.c_uint64), ("hi", C.c_uint64),
                 ("cbase", C.c_int64), ("s0", C.c_int64 * 2), ("s1", C.c_int64 * 2), ("per", C.c_int32 * 3),
-                ("perm", C.c_int32 * 3), ("scale", C.c_int32), ("reach", C.c_int32 * 3), ("nslices", C.c_int32), ("reserved", C.c_int32),
+                ("perm", C.c_int32 * 3), ("scale", C.c_int32), ("reach", C.c_int32 * 3), ("nslices", C.c_int32), ("shape", C.c_int32),
                 ("items", C.c_void_p), ("item_delta", C.c_void_p), ("pos", C.c_void_p), ("local_slot", C.c_void_p), ("local_g", C.c_void_p),
                 ("leaves", C.c_void_p), ("row", C.c_void_p), ("nbr_slot", C.c_void_p), ("nbr_off", C.c_void_p)]
 

@@ -323,6 +323,7 @@ struct IterCache {
     int32_t* items = nullptr;      // uniform: 8 per item (a, b, c, mirror, x, y, z, 0), iteration order
     int64_t* delta = nullptr;      // uniform: slot distance of each item
     int32_t reach[3] = {0, 0, 0};  // uniform: largest |item component| per canonical axis
+    int32_t shape = 0;             // uniform: DCCRGX_SHAPE_* flags of the items in iteration order
     uint32_t* slot = nullptr;      // explicit: stencil rows regrouped into iteration order
     int32_t* off = nullptr;
     ~IterCache();

@@ -85,6 +85,29 @@ int build_iter(const dccrgx_grid* grid, Hood& h, hipStream_t st)
             if (x[1] != y[1]) return x[1] < y[1];
             return x[0] < y[0];
         });
+        // shape flags: all mirrored; the 26-cube / 6 faces in ascending (c, b, a)
+        // order, which is the order the sort gives them when all are mirrored
+        bool sym = true;
+        for (int k = 0; k < K; k++) sym = sym && it[k][3] == 1;
+        ic->shape = sym ? DCCRGX_SHAPE_SYMMETRIC : 0;
+        if (sym && K == 26) {
+            bool cube = true;
+            for (int k = 0, dc = -1; dc <= 1; dc++)
+                for (int db = -1; db <= 1; db++)
+                    for (int da = -1; da <= 1; da++) {
+                        if (!da && !db && !dc) continue;
+                        cube = cube && it[k][0] == da && it[k][1] == db && it[k][2] == dc;
+                        k++;
+                    }
+            if (cube) ic->shape |= DCCRGX_SHAPE_CUBE1;
+        }
+        if (sym && K == 6) {
+            static const int32_t fc[6][3] = {{0, 0, -1}, {0, -1, 0}, {-1, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+            bool faces = true;
+            for (int k = 0; k < 6; k++)
+                faces = faces && it[k][0] == fc[k][0] && it[k][1] == fc[k][1] && it[k][2] == fc[k][2];
+            if (faces) ic->shape |= DCCRGX_SHAPE_FACES;
+        }
         const UGeom& g = grid->g;
         const int32_t sc = 1 << grid->map.max_lvl;
         std::vector<int32_t> rec(std::max(K, 1) * 8, 0);
@@ -154,6 +177,7 @@ int dccrgx_stencil_view_get(const dccrgx_grid* grid, int32_t hood_id, int32_t re
         v.items = ic.items;
         v.item_delta = ic.delta;
         for (int d = 0; d < 3; d++) v.reach[d] = ic.reach[d];
+        v.shape = ic.shape;
         v.la = g.LA;
         v.lb = g.LB;
         v.lc = g.LC;

@@ -50,6 +50,87 @@ int us_gol(const dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t fout, 
     });
 }
 
+// the same step with the neighbors' alive values staged
+// (dccrgx_user::for_each_cell_staged: LDS tiles and a register window on
+// uniform grids whose neighborhood is the cube or the faces); staged == 0
+// sends every cell through the walk with the values loaded at the slots
+int us_gol_staged(const dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t fout, int32_t fcnt, int32_t region,
+                  int32_t staged)
+{
+    const uint32_t* in;
+    uint32_t *out, *cnt;
+    int e = field_ptr(grid, fin, &in);
+    if (!e) e = field_ptr(grid, fout, &out);
+    if (!e) e = field_ptr(grid, fcnt, &cnt);
+    if (e) return e;
+    dccrgx_user::StagedOptions opt;
+    opt.staged = staged != 0;
+    return dccrgx_user::for_each_cell_staged(
+        grid, hood_id, region, dccrgx_user::Fields<uint32_t, 1>{{in}},
+        [=] __device__(const auto& cell) {
+            uint32_t n = 0;
+            cell.for_each_neighbor([&](const auto& nb) { n += nb.value(0) != 0u ? 1u : 0u; });
+            cnt[cell.slot] = n;
+            out[cell.slot] = n == 3u ? 1u : (n == 2u ? cell.value(0) : 0u);
+        },
+        nullptr, opt);
+}
+
+// us_digest with the neighbor ids as staged values (8-byte elements)
+int us_digest_staged(const dccrgx_grid* grid, int32_t hood_id, int32_t region, int32_t fids, int32_t fcid,
+                     int32_t fdig, int32_t fcnt)
+{
+    const uint64_t* ids;
+    uint64_t *cid, *dig;
+    uint32_t* cnt;
+    int e = field_ptr(grid, fids, &ids);
+    if (!e) e = field_ptr(grid, fcid, &cid);
+    if (!e) e = field_ptr(grid, fdig, &dig);
+    if (!e) e = field_ptr(grid, fcnt, &cnt);
+    if (e) return e;
+    return dccrgx_user::for_each_cell_staged(
+        grid, hood_id, region, dccrgx_user::Fields<uint64_t, 1>{{ids}}, [=] __device__(const auto& cell) {
+            uint64_t h = 0xCBF29CE484222325ull;
+            uint32_t n = 0;
+            cell.for_each_neighbor([&](const auto& nb) {
+                const uint64_t v = mix64(nb.value(0)) + (uint64_t)(int64_t)nb.x * 0x100000001B3ull +
+                                   (uint64_t)(int64_t)nb.y * 0x5851F42D4C957F2Dull +
+                                   (uint64_t)(int64_t)nb.z * 0x14057B7EF767814Full;
+                h = (h ^ v) * 0x00000100000001B3ull;
+                n++;
+            });
+            cid[cell.slot] = cell.value(0) == cell.id ? cell.id : 0;
+            dig[cell.slot] = h;
+            cnt[cell.slot] = n;
+        });
+}
+
+// an order-sensitive floating-point stencil over two staged f64 fields:
+// out = u + sum over the neighbors in order of (w_nb * u_nb - 0.25 * u)
+// (summed in the iteration order, so the rounding follows it); staged == 0:
+// the walk
+int us_fsum_staged(const dccrgx_grid* grid, int32_t hood_id, int32_t fu, int32_t fw, int32_t fout, int32_t region,
+                   int32_t staged)
+{
+    const double *u, *wt;
+    double* out;
+    int e = field_ptr(grid, fu, &u);
+    if (!e) e = field_ptr(grid, fw, &wt);
+    if (!e) e = field_ptr(grid, fout, &out);
+    if (e) return e;
+    dccrgx_user::StagedOptions opt;
+    opt.staged = staged != 0;
+    return dccrgx_user::for_each_cell_staged(
+        grid, hood_id, region, dccrgx_user::Fields<double, 2>{{u, wt}},
+        [=] __device__(const auto& cell) {
+            const double me = cell.value(0);
+            double s = me;
+            cell.for_each_neighbor([&](const auto& nb) { s += nb.value(1) * nb.value(0) - 0.25 * me; });
+            out[cell.slot] = s;
+        },
+        nullptr, opt);
+}
+
 // per cell: cid = the cell's id as for_each_cell reports it, dig = a digest of
 // its neighbor sequence h = (h ^ (mix64(id) + x * K1 + y * K2 + z * K3)) * P
 // over the neighbors in order (ids read from field fids, whose ghosts must be

@@ -249,6 +249,11 @@ int dccrgx_gather_neighbors(const dccrgx_grid* grid, int32_t hood_id, int32_t fi
  * as dccrgx_gol_compute's: on uniform grids DCCRGX_REGION_INNER is the whole
  * slices whose cells read no ghost copy (a subset of the reference's inner
  * cells) and DCCRGX_REGION_OUTER the rest of the local cells. */
+/* dccrgx_stencil_view.shape flags (uniform grids): every item's mirror is an
+ * item too (each neighbor is also a neighbor_to); the items are the 26-cell
+ * cube of reach 1 / the 6 face items, in their iteration order (the staged
+ * launches of include/dccrgx_stencil.hpp then use compile-time offsets) */
+enum { DCCRGX_SHAPE_SYMMETRIC = 1, DCCRGX_SHAPE_CUBE1 = 2, DCCRGX_SHAPE_FACES = 4 };
 typedef struct dccrgx_stencil_view {
     int32_t kind;     /* 0 uniform (closed form), 1 explicit (stored rows) */
     int32_t n_items;  /* uniform: neighborhood items */
@@ -264,7 +269,7 @@ typedef struct dccrgx_stencil_view {
     int32_t scale;         /* offsets in indices of the finest level: 2^max_ref_lvl */
     int32_t reach[3];      /* largest |item component| per canonical axis */
     int32_t nslices;       /* storage slices (local and ghost), la * lb slots each */
-    int32_t reserved;
+    int32_t shape;         /* uniform: DCCRGX_SHAPE_* flags of the items (staged launches) */
     /* n_items x 8 int32, device, in the iteration cache's order for a cell no
      * periodic wrap reaches: canonical (a, b, c) of each item, 1 if its mirror
      * is an item too (the neighbor is also a neighbor_to), the x, y, z offset

@@ -41,6 +41,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "dccrgx.h"
 
@@ -62,6 +63,7 @@ struct UniformGeo {
     int32_t K;
     int32_t pa, pb, pc;
     int32_t ra, rb, rc; /* reach per canonical axis */
+    int32_t sym;        /* every item's mirror is an item (DCCRGX_SHAPE_SYMMETRIC) */
 };
 
 /* the iteration cache's order of two entries: (group, id, x, y, z) */
@@ -154,13 +156,16 @@ struct UniformCell {
             }
             return;
         }
-        // no periodic wrap within twice the reach: the items' order is still
-        // the iteration order (ids grow with (c, b, a); an entry is a
-        // neighbor_to exactly when the mirrored item exists), items past a
-        // non-periodic boundary are dropped
-        const bool nowrap = (!g.pa || (a >= 2 * g.ra && a + 2 * g.ra < (int64_t)g.la)) &&
-                            (!g.pb || (b >= 2 * g.rb && b + 2 * g.rb < (int64_t)g.lb)) &&
-                            (!g.pc || (c >= 2 * g.rc && c + 2 * g.rc < (int64_t)g.lc));
+        // no periodic wrap within the reach: the items' order is still the
+        // iteration order (ids grow with (c, b, a)), items past a non-periodic
+        // boundary are dropped.  An entry is a neighbor_to exactly when the
+        // mirrored item exists -- always, for a symmetric neighborhood; else
+        // only if no wrap is within twice the reach (a neighbor's items could
+        // reach back through it)
+        const int64_t m = g.sym ? 1 : 2;
+        const bool nowrap = (!g.pa || (a >= m * g.ra && a + m * g.ra < (int64_t)g.la)) &&
+                            (!g.pb || (b >= m * g.rb && b + m * g.rb < (int64_t)g.lb)) &&
+                            (!g.pc || (c >= m * g.rc && c + m * g.rc < (int64_t)g.lc));
         if (nowrap) {
             for (int32_t k = 0; k < g.K; k++) {
                 uint64_t ab;
@@ -284,6 +289,48 @@ __global__ void __launch_bounds__(256) k_user_explicit(const uint32_t* __restric
     }
 }
 
+/* the uniform geometry of a view */
+inline UniformGeo uniform_geo(const dccrgx_stencil_view& v)
+{
+    UniformGeo g;
+    g.la = v.la;
+    g.lb = v.lb;
+    g.lc = v.lc;
+    g.S = v.la * v.lb;
+    g.lo = v.lo;
+    g.hi = v.hi;
+    g.cbase = v.cbase;
+    g.items = v.items;
+    g.delta = v.item_delta;
+    g.K = v.n_items;
+    g.pa = v.per[0];
+    g.pb = v.per[1];
+    g.pc = v.per[2];
+    g.ra = v.reach[0];
+    g.rb = v.reach[1];
+    g.rc = v.reach[2];
+    g.sym = (v.shape & DCCRGX_SHAPE_SYMMETRIC) != 0;
+    return g;
+}
+
+/* the walk over whole storage slices [s0, s1) of a uniform grid */
+template <class F>
+int launch_slices(const UniformGeo& g, int64_t s0, int64_t s1, F f, hipStream_t st)
+{
+    const int64_t nsl = s1 - s0;
+    if (nsl <= 0) return DCCRGX_OK;
+    const uint64_t tiles = (g.S + 255) / 256;
+    if (tiles >= (1ull << 31)) return DCCRGX_EINVAL;
+    // about 2^20 workgroups (4096 per CU) and never more than 2^31
+    uint64_t chunk = (tiles * (uint64_t)nsl + (1u << 20) - 1) >> 20;
+    if (chunk < 1) chunk = 1;
+    const uint64_t nch = ((uint64_t)nsl + chunk - 1) / chunk;
+    if (tiles * nch >= (1ull << 31)) return DCCRGX_EINVAL;
+    hipLaunchKernelGGL(k_user_uniform<F>, dim3((unsigned)(tiles * nch)), dim3(256), 0, st, g, s0, s1,
+                       (uint32_t)tiles, (uint32_t)chunk, f);
+    return DCCRGX_OK;
+}
+
 }  // namespace detail
 
 /* Launch f(cell) for every cell of the region described by v on stream st
@@ -294,35 +341,10 @@ int for_each_cell(const dccrgx_stencil_view& v, F f, hipStream_t st)
 {
     if (v.n_cells == 0) return DCCRGX_OK;
     if (v.kind == 0) {
-        detail::UniformGeo g;
-        g.la = v.la;
-        g.lb = v.lb;
-        g.lc = v.lc;
-        g.S = v.la * v.lb;
-        g.lo = v.lo;
-        g.hi = v.hi;
-        g.cbase = v.cbase;
-        g.items = v.items;
-        g.delta = v.item_delta;
-        g.K = v.n_items;
-        g.pa = v.per[0];
-        g.pb = v.per[1];
-        g.pc = v.per[2];
-        g.ra = v.reach[0];
-        g.rb = v.reach[1];
-        g.rc = v.reach[2];
-        const uint64_t tiles = (g.S + 255) / 256;
-        if (tiles >= (1ull << 31)) return DCCRGX_EINVAL;
+        const detail::UniformGeo g = detail::uniform_geo(v);
         for (int r = 0; r < 2; r++) {
-            const int64_t nsl = v.s1[r] - v.s0[r];
-            if (nsl <= 0) continue;
-            // about 2^20 workgroups (4096 per CU) and never more than 2^31
-            uint64_t chunk = (tiles * (uint64_t)nsl + (1u << 20) - 1) >> 20;
-            if (chunk < 1) chunk = 1;
-            const uint64_t nch = ((uint64_t)nsl + chunk - 1) / chunk;
-            if (tiles * nch >= (1ull << 31)) return DCCRGX_EINVAL;
-            hipLaunchKernelGGL(detail::k_user_uniform<F>, dim3((unsigned)(tiles * nch)), dim3(256), 0, st, g,
-                               (int64_t)v.s0[r], (int64_t)v.s1[r], (uint32_t)tiles, (uint32_t)chunk, f);
+            const int e = detail::launch_slices(g, (int64_t)v.s0[r], (int64_t)v.s1[r], f, st);
+            if (e != DCCRGX_OK) return e;
         }
     } else {
         uint64_t blocks = (v.n_cells + 255) / 256;
@@ -342,6 +364,732 @@ int for_each_cell(const dccrgx_grid* grid, int32_t hood_id, int32_t region, F f,
     const int e = dccrgx_stencil_view_get(grid, hood_id, region, &v);
     if (e != DCCRGX_OK) return e;
     return for_each_cell(v, f, st ? st : (hipStream_t)v.stream);
+}
+
+/* ------------------------------------------------------------------------
+ * Staged launches: the caller names the fields its functor reads at the
+ * neighbors (one element type T, NF fields), and the functor reads them as
+ * values -- cell.value(j), nb.value(j) -- instead of through slots:
+ *
+ *     dccrgx_user::for_each_cell_staged(grid, hood, region, dccrgx_user::Fields<uint32_t, 1>{{alive}},
+ *         [=] __device__ (const auto& cell) {
+ *             uint32_t n = 0;
+ *             cell.for_each_neighbor([&](const auto& nb) { n += nb.value(0) != 0; });
+ *             count[cell.slot] = n;
+ *         });
+ *
+ * Same cells, same neighbors in the same order as for_each_cell (nb.slot,
+ * x, y, z are there too).  On uniform grids whose neighborhood is the 26-cell
+ * cube or the 6 faces (DCCRGX_SHAPE_CUBE1 / _FACES: the default
+ * neighborhoods of length 1 and 0), the cells no grid boundary reaches run
+ * k_staged: a workgroup owns a 64 x (NW * NB) tile of the (A, B) plane and
+ * marches along C; each plane of the declared fields is read from HBM once
+ * (16-byte loads, +1 apron) into LDS, every lane reads the 3 x (NB + 2)
+ * values around its column of NB cells into a register window of three
+ * planes, and the functor's neighbor loop is unrolled over compile-time
+ * offsets into that window.  The cells within reach of a grid boundary (the
+ * ring of each slice, the slices next to a C boundary) run the exact-order
+ * walk in separate launches; so do other neighborhoods and refined grids.
+ * ---------------------------------------------------------------------- */
+
+template <class T, int NF>
+struct Fields {
+    const T* p[NF];
+};
+
+/* a neighbor with the values of the declared fields */
+template <class T, int NF>
+struct ValueNeighbor : Neighbor {
+    T v[NF];
+    __host__ __device__ inline T value(int j) const { return v[j]; }
+};
+
+/* a walk cell (UniformCell / ExplicitCell) whose values are loaded from the
+ * fields at the slots */
+template <class Cell, class T, int NF>
+struct LoadedCell {
+    Cell cell;
+    Fields<T, NF> fld;
+    uint64_t slot, id;
+
+    __host__ __device__ inline T value(int j) const { return fld.p[j][slot]; }
+
+    template <class G>
+    __host__ __device__ inline void for_each_neighbor(G&& fn) const
+    {
+        cell.for_each_neighbor([&](const Neighbor& nb) {
+            ValueNeighbor<T, NF> v;
+            v.slot = nb.slot;
+            v.x = nb.x;
+            v.y = nb.y;
+            v.z = nb.z;
+#pragma unroll
+            for (int j = 0; j < NF; j++) v.v[j] = fld.p[j][nb.slot];
+            fn(v);
+        });
+    }
+};
+
+namespace detail {
+
+/* the items of the staged shapes, canonical (a, b, c) of item k in the
+ * iteration order of a cell no periodic wrap reaches (ascending (c, b, a);
+ * every entry is also a neighbor_to) */
+template <int SHAPE>
+struct StagedItems;
+template <>
+struct StagedItems<DCCRGX_SHAPE_CUBE1> {
+    static constexpr int K = 26;
+    __host__ __device__ static constexpr int d(int k, int axis)
+    {
+        return ((k < 13 ? k : k + 1) / (axis == 0 ? 1 : (axis == 1 ? 3 : 9))) % 3 - 1;
+    }
+};
+template <>
+struct StagedItems<DCCRGX_SHAPE_FACES> {
+    static constexpr int K = 6;  // (0,0,-1) (0,-1,0) (-1,0,0) (1,0,0) (0,1,0) (0,0,1)
+    __host__ __device__ static constexpr int d(int k, int axis)
+    {
+        return axis == 2 ? (k == 0 ? -1 : (k == 5 ? 1 : 0))
+                         : (axis == 1 ? (k == 1 ? -1 : (k == 4 ? 1 : 0)) : (k == 2 ? -1 : (k == 3 ? 1 : 0)));
+    }
+};
+
+/* where a cell's plane sits on a periodic C axis: inside, or the first / last
+ * slice, whose neighbors across the wrap have the largest / smallest ids (so
+ * their c-groups come last / first in the iteration order) */
+enum { CLS_MID = 0, CLS_LOW = 1, CLS_HIGH = 2 };
+
+__host__ __device__ constexpr int class_dc(int cls, int grp)
+{
+    return cls == CLS_MID ? grp - 1 : (cls == CLS_LOW ? (grp == 2 ? -1 : grp) : (grp == 0 ? 1 : grp - 2));
+}
+
+struct StagedGeo {
+    uint64_t la, lb, lc, S, lo, hi;
+    int64_t cbase;
+    int64_t s0, s1;    // storage slices computed by the launch
+    int64_t chunk;     // slices per workgroup
+    int64_t wrap_lo;   // storage slice to read for the plane below canonical 0 (wrap launches)
+    int64_t wrap_hi;   // ... above canonical LC - 1
+    uint32_t tiles_a, tiles_b, nwg;
+    int32_t pa, pb, pc;
+    int32_t inv[3];    // x, y, z -> canonical axis
+    int32_t scale;
+};
+
+/* a cell of the staged kernels: values from the register window
+ * W[field][plane][row][col] (planes c - 1, c, c + 1, read from storage slices
+ * ps0..ps2); every neighbor exists (cells next to a grid boundary or a
+ * periodic wrap in A / B run the edge walk) */
+template <class T, int NF, int SHAPE, int NB, int CLS>
+struct StagedCell {
+    uint64_t slot, id;
+    const T (*w)[3][NB + 2][3];
+    int64_t la, S;
+    int64_t ps0, ps1, ps2;
+    int32_t inv[3], scale;
+    int r;  // the cell's row in the window is r + 1
+
+    __host__ __device__ inline T value(int j) const { return w[j][1][r + 1][1]; }
+
+    template <class G>
+    __host__ __device__ inline void for_each_neighbor(G&& fn) const
+    {
+        typedef StagedItems<SHAPE> It;
+#pragma unroll
+        for (int grp = 0; grp < 3; grp++) {
+            const int dcg = class_dc(CLS, grp);
+#pragma unroll
+            for (int k = 0; k < It::K; k++) {
+                const int da = It::d(k, 0), db = It::d(k, 1), dc = It::d(k, 2);
+                if (dc != dcg) continue;
+                ValueNeighbor<T, NF> nb;
+                const int64_t dps = dc < 0 ? ps0 - ps1 : (dc > 0 ? ps2 - ps1 : 0);
+                nb.slot = slot + (uint64_t)((int64_t)da + la * db + S * dps);
+                nb.x = (inv[0] == 0 ? da : (inv[0] == 1 ? db : dc)) * scale;
+                nb.y = (inv[1] == 0 ? da : (inv[1] == 1 ? db : dc)) * scale;
+                nb.z = (inv[2] == 0 ? da : (inv[2] == 1 ? db : dc)) * scale;
+#pragma unroll
+                for (int j = 0; j < NF; j++) nb.v[j] = w[j][dc + 1][r + 1 + db][da + 1];
+                fn(nb);
+            }
+        }
+    }
+};
+
+/* a cell of the edge walk (a cell of a staged shape next to a grid boundary
+ * or a periodic wrap): its neighbors in closed form, values read at their
+ * slots.  Per axis the neighbors' coordinates sort as -1, 0, +1, or -- at
+ * the first / last cell of a periodic axis of >= 3 cells -- as 0, +1, -1 /
+ * +1, -1, 0 (the wrapped one has the largest / smallest index), so nested
+ * loops over those orders give the iteration order (ids ascending by (c, b,
+ * a)); neighbors past a non-periodic boundary are dropped. */
+template <class T, int NF, int SHAPE>
+struct EdgeCell {
+    uint64_t slot, id;
+    Fields<T, NF> fld;
+    uint64_t la, lb, lc, S, lo, hi;
+    int64_t a, b, c, cbase;  // c canonical
+    int32_t pa, pb, pc;
+    int32_t inv[3], scale;
+
+    __host__ __device__ inline T value(int j) const { return fld.p[j][slot]; }
+
+    __host__ __device__ static inline int axis_class(int64_t x, uint64_t L, int32_t p)
+    {
+        return !p ? CLS_MID : (x == 0 ? CLS_LOW : (x == (int64_t)L - 1 ? CLS_HIGH : CLS_MID));
+    }
+
+    template <class G>
+    __host__ __device__ inline void for_each_neighbor(G&& fn) const
+    {
+        const int ka = axis_class(a, la, pa), kb = axis_class(b, lb, pb), kc = axis_class(c, lc, pc);
+#pragma unroll
+        for (int rc = 0; rc < 3; rc++) {
+#pragma unroll
+            for (int rb = 0; rb < 3; rb++) {
+#pragma unroll
+                for (int ra = 0; ra < 3; ra++) {
+                    const int da = class_dc(ka, ra), db = class_dc(kb, rb), dc = class_dc(kc, rc);
+                    const int nz = (da != 0) + (db != 0) + (dc != 0);
+                    if (nz == 0 || (SHAPE == DCCRGX_SHAPE_FACES && nz != 1)) continue;
+                    int64_t a2 = a + da, b2 = b + db, cu = c + dc, cw = cu;
+                    if (a2 < 0 || a2 >= (int64_t)la) {
+                        if (!pa) continue;
+                        a2 = a2 < 0 ? a2 + (int64_t)la : a2 - (int64_t)la;
+                    }
+                    if (b2 < 0 || b2 >= (int64_t)lb) {
+                        if (!pb) continue;
+                        b2 = b2 < 0 ? b2 + (int64_t)lb : b2 - (int64_t)lb;
+                    }
+                    if (cu < 0 || cu >= (int64_t)lc) {
+                        if (!pc) continue;
+                        cw = cu < 0 ? cu + (int64_t)lc : cu - (int64_t)lc;
+                    }
+                    const uint64_t ab = (uint64_t)a2 + la * (uint64_t)b2, nlin = ab + S * (uint64_t)cw;
+                    // a local neighbor (also one across a wrap) is read from its
+                    // own slot, a remote one from its ghost slot
+                    const int64_t cs = (nlin >= lo && nlin < hi) ? cw : cu;
+                    ValueNeighbor<T, NF> nb;
+                    nb.slot = ab + S * (uint64_t)(cs - cbase);
+                    nb.x = (inv[0] == 0 ? da : (inv[0] == 1 ? db : dc)) * scale;
+                    nb.y = (inv[1] == 0 ? da : (inv[1] == 1 ? db : dc)) * scale;
+                    nb.z = (inv[2] == 0 ? da : (inv[2] == 1 ? db : dc)) * scale;
+#pragma unroll
+                    for (int j = 0; j < NF; j++) nb.v[j] = fld.p[j][nb.slot];
+                    fn(nb);
+                }
+            }
+        }
+    }
+};
+
+template <int VEC, class T>
+struct StagedChunk {
+    typedef uint32_t type __attribute__((ext_vector_type(4)));  // VEC elements, 16 bytes
+};
+template <class T>
+struct StagedChunk<1, T> {
+    typedef T type;
+};
+
+template <class V>
+__device__ inline V buffer_load(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    if constexpr (sizeof(V) == 16) {
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+    } else if constexpr (sizeof(V) == 8) {
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+    } else if constexpr (sizeof(V) == 4) {
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+    } else if constexpr (sizeof(V) == 2) {
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b16(r, (int)off, 0, 0));
+    } else {
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b8(r, (int)off, 0, 0));
+    }
+}
+
+/* One workgroup's tile: 64 columns (lane l: column a0 + l) x NW * NB rows
+ * (wave w: rows w * NB ..) of the (A, B) plane, + 1 apron.  Planes go HBM ->
+ * registers (16-byte loads, VEC elements; VEC = 1: element loads) -> LDS ->
+ * each lane's 3 x (NB + 2) window of one plane. */
+template <class T, int NF, int NW, int NB, int VEC>
+struct StagedTile {
+    typedef typename StagedChunk<VEC, T>::type Chunk;
+    static constexpr int NT = 64 * NW, TB = NW * NB, WB = TB + 2;
+    static constexpr int X0 = VEC > 1 ? VEC : 1;  // LDS row: apron at X0 - 1, cells at X0.., apron at X0 + 64
+    static constexpr int RS = 64 + 2 * X0;
+    static constexpr int CR = 64 / VEC;           // chunks per tile row
+    static constexpr int NCH = (WB * CR + NT - 1) / NT;
+
+    uint32_t moff[NCH], mdst[NCH], mmask;
+    uint32_t eoff, edst;
+    bool eok;
+
+    __device__ inline void init(const StagedGeo& g, int64_t a0, int64_t b0, int t)
+    {
+        const int64_t LA = (int64_t)g.la, LB = (int64_t)g.lb;
+        mmask = 0;
+#pragma unroll
+        for (int i = 0; i < NCH; i++) {
+            const int e = t + NT * i;
+            const int row = e / CR, q = e - row * CR;
+            const int64_t a = a0 + VEC * q, b = b0 - 1 + row;
+            const bool ok = e < WB * CR && a < LA && b >= 0 && b < LB;
+            moff[i] = ok ? (uint32_t)((a + LA * b) * (int64_t)sizeof(T)) : 0u;  // bytes
+            mdst[i] = ok ? (uint32_t)(row * RS + X0 + VEC * q) : 0u;
+            mmask |= ok ? (1u << i) : 0u;
+        }
+        eoff = edst = 0;
+        eok = false;
+        if (t < 2 * WB) {
+            const int row = t >> 1;
+            const int64_t a = (t & 1) ? a0 + 64 : a0 - 1, b = b0 - 1 + row;
+            eok = a >= 0 && a < LA && b >= 0 && b < LB;
+            eoff = eok ? (uint32_t)((a + LA * b) * (int64_t)sizeof(T)) : 0u;
+            edst = (uint32_t)(row * RS + ((t & 1) ? X0 + 64 : X0 - 1));
+        }
+    }
+    __device__ inline void fetch(const Fields<T, NF>& fld, uint64_t S, int64_t sc, Chunk (&FM)[NF][NCH],
+                                 T (&FE)[NF]) const
+    {
+#pragma unroll
+        for (int j = 0; j < NF; j++) {
+            // buffer loads: a scalar resource per plane + a 32-bit byte
+            // offset per load; unconditional (a chunk outside the grid reads
+            // the plane's first bytes and is not stashed)
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<T*>(fld.p[j] + (uint64_t)sc * S), 0, (int)(S * sizeof(T)), 0x00020000);
+#pragma unroll
+            for (int i = 0; i < NCH; i++) FM[j][i] = buffer_load<Chunk>(rs, moff[i]);
+            FE[j] = buffer_load<T>(rs, eoff);
+        }
+    }
+    __device__ inline void stash(T* lds, const Chunk (&FM)[NF][NCH], const T (&FE)[NF]) const
+    {
+#pragma unroll
+        for (int j = 0; j < NF; j++) {
+            T* l = lds + j * WB * RS;
+#pragma unroll
+            for (int i = 0; i < NCH; i++)
+                if ((mmask >> i) & 1u) *reinterpret_cast<Chunk*>(l + mdst[i]) = FM[j][i];
+            if (eok) l[edst] = FE[j];
+        }
+    }
+    // the lane's 3 x (NB + 2) values of the plane in lds into W[.][pl]
+    __device__ static inline void window(const T* lds, int w, int lane, T (&W)[NF][3][NB + 2][3], int pl)
+    {
+#pragma unroll
+        for (int j = 0; j < NF; j++)
+#pragma unroll
+            for (int rr = 0; rr < NB + 2; rr++)
+#pragma unroll
+                for (int q = 0; q < 3; q++) W[j][pl][rr][q] = lds[(j * WB + w * NB + rr) * RS + X0 + lane + q - 1];
+    }
+};
+
+/* f(std::integral_constant<int, J>()) for J = 0 .. N - 1, unrolled at compile
+ * time (register arrays indexed by J stay registers) */
+template <int J, int N>
+struct StaticFor {
+    template <class G>
+    __device__ static inline void run(G& g)
+    {
+        g(std::integral_constant<int, J>());
+        StaticFor<J + 1, N>::run(g);
+    }
+};
+template <int N>
+struct StaticFor<N, N> {
+    template <class G>
+    __device__ static inline void run(G&)
+    {
+    }
+};
+
+/* XCD-aware workgroup order: each XCD takes a contiguous run of tiles
+ * (vertically adjacent tiles share apron rows through its L2) */
+__device__ inline uint32_t xcd_wgid(uint32_t nwg)
+{
+    const uint32_t bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+/* f on the NB cells of plane c of the lane's column (window planes read from
+ * storage slices ps); only cells with a in [1, LA - 1), b in [1, LB - 1) */
+template <class T, int NF, int SHAPE, int NB, int CLS, class F>
+__device__ inline void staged_cells(const StagedGeo& g, F& f, const T (&W)[NF][3][NB + 2][3], const int64_t (&ps)[3],
+                                    int64_t c, int64_t a, int64_t bw)
+{
+    const int64_t LA = (int64_t)g.la, LB = (int64_t)g.lb, cg = c + g.cbase;
+    if (a < 1 || a + 1 >= LA) return;
+    const uint64_t plin = g.S * (uint64_t)cg;
+    const bool plane_local = plin >= g.lo && plin + g.S <= g.hi;  // uniform
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+        const int64_t b = bw + k;
+        if (b < 1 || b + 1 >= LB) continue;
+        const uint64_t lin = plin + (uint64_t)a + g.la * (uint64_t)b;
+        if (!plane_local && (lin < g.lo || lin >= g.hi)) continue;
+        StagedCell<T, NF, SHAPE, NB, CLS> cell;
+        cell.slot = (uint64_t)c * g.S + (uint64_t)a + g.la * (uint64_t)b;
+        cell.id = lin + 1;
+        cell.w = W;
+        cell.la = LA;
+        cell.S = (int64_t)g.S;
+        cell.ps0 = ps[0];
+        cell.ps1 = ps[1];
+        cell.ps2 = ps[2];
+        cell.inv[0] = g.inv[0];
+        cell.inv[1] = g.inv[1];
+        cell.inv[2] = g.inv[2];
+        cell.scale = g.scale;
+        cell.r = k;
+        f(cell);
+    }
+}
+
+/* The staged kernel over storage slices [s0, s1), none of them the first or
+ * last slice of a periodic C: a workgroup marches its tile through `chunk`
+ * slices; plane q of the march is fetched PF planes ahead into its own
+ * registers (the loop is unrolled by PF so loads land where they are used),
+ * stashed to one of two LDS buffers, and read into the register window. */
+template <class T, int NF, int SHAPE, int NW, int NB, int VEC, int PF, class F>
+__global__ void __launch_bounds__(64 * NW) k_staged(StagedGeo g, Fields<T, NF> fld, F f)
+{
+    typedef StagedTile<T, NF, NW, NB, VEC> Tile;
+    typedef typename Tile::Chunk Chunk;
+    __shared__ __attribute__((aligned(16))) T P[2][NF][Tile::WB][Tile::RS];
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t wgid = xcd_wgid(g.nwg);
+    const uint32_t tiles = g.tiles_a * g.tiles_b;
+    const uint32_t tile_id = wgid % tiles;
+    const int64_t chunk_id = wgid / tiles;
+    const int64_t a0 = (int64_t)(tile_id % g.tiles_a) * 64;
+    const int64_t b0 = (int64_t)(tile_id / g.tiles_a) * Tile::TB;
+    const int64_t c0 = g.s0 + chunk_id * g.chunk;
+    const int64_t c1 = min(g.s1, c0 + g.chunk);
+    if (c0 >= c1) return;
+
+    Tile tile;
+    tile.init(g, a0, b0, t);
+    Chunk FM[PF][NF][Tile::NCH];
+    T FE[PF][NF];
+    T W[NF][3][NB + 2][3];
+    // plane q = storage slice c0 - 1 + q, q in [0, Q); computed: q in [2, Q) -> slice c0 + q - 2
+    const int64_t Q = c1 - c0 + 2;
+    auto pre = [&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if (j < Q) tile.fetch(fld, g.S, c0 - 1 + j, FM[j], FE[j]);
+    };
+    StaticFor<0, PF>::run(pre);
+    const int64_t a = a0 + lane, bw = b0 + w * NB;
+    const int64_t ps[3] = {0, 0, 0};  // unused by CLS_MID planes' slots (filled below)
+    (void)ps;
+    for (int64_t qb = 0; qb < Q; qb += PF) {
+        auto step = [&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            const int64_t q = qb + j;
+            if (q < Q) {
+                T* lds = &P[q & 1][0][0][0];
+                tile.stash(lds, FM[j], FE[j]);
+                if (q + PF < Q) tile.fetch(fld, g.S, c0 - 1 + q + PF, FM[j], FE[j]);
+                __syncthreads();
+                Tile::window(lds, w, lane, W, 2);
+                if (q >= 2) {
+                    const int64_t c = c0 + q - 2;
+                    const int64_t pls[3] = {c - 1, c, c + 1};
+                    staged_cells<T, NF, SHAPE, NB, CLS_MID>(g, f, W, pls, c, a, bw);
+                }
+#pragma unroll
+                for (int jj = 0; jj < NF; jj++)
+#pragma unroll
+                    for (int rr = 0; rr < NB + 2; rr++)
+#pragma unroll
+                        for (int qq = 0; qq < 3; qq++) {
+                            W[jj][0][rr][qq] = W[jj][1][rr][qq];
+                            W[jj][1][rr][qq] = W[jj][2][rr][qq];
+                        }
+            }
+        };
+        StaticFor<0, PF>::run(step);
+    }
+}
+
+/* The first (CLS_LOW) or last (CLS_HIGH) slice of a periodic C axis, storage
+ * slice g.s0: the plane across the wrap is read from storage slice
+ * g.wrap_lo / g.wrap_hi (the local slice itself when this rank holds it, as
+ * the walk reads it; else the ghost copy), one tile per workgroup. */
+template <class T, int NF, int SHAPE, int NW, int NB, int VEC, int CLS, class F>
+__global__ void __launch_bounds__(64 * NW) k_staged_wrap(StagedGeo g, Fields<T, NF> fld, F f)
+{
+    typedef StagedTile<T, NF, NW, NB, VEC> Tile;
+    typedef typename Tile::Chunk Chunk;
+    __shared__ __attribute__((aligned(16))) T P[3][NF][Tile::WB][Tile::RS];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t tile_id = blockIdx.x;
+    const int64_t a0 = (int64_t)(tile_id % g.tiles_a) * 64;
+    const int64_t b0 = (int64_t)(tile_id / g.tiles_a) * Tile::TB;
+    const int64_t c = g.s0;
+    const int64_t ps[3] = {CLS == CLS_LOW ? g.wrap_lo : c - 1, c, CLS == CLS_HIGH ? g.wrap_hi : c + 1};
+    Tile tile;
+    tile.init(g, a0, b0, t);
+    Chunk FM[NF][Tile::NCH];
+    T FE[NF];
+#pragma unroll
+    for (int pl = 0; pl < 3; pl++) {
+        tile.fetch(fld, g.S, ps[pl], FM, FE);
+        tile.stash(&P[pl][0][0][0], FM, FE);
+    }
+    __syncthreads();
+    T W[NF][3][NB + 2][3];
+#pragma unroll
+    for (int pl = 0; pl < 3; pl++) Tile::window(&P[pl][0][0][0], w, lane, W, pl);
+    staged_cells<T, NF, SHAPE, NB, CLS>(g, f, W, ps, c, a0 + lane, b0 + w * NB);
+}
+
+/* The edge walk over storage slices [s0, s1): the ring of each slice (rows
+ * b = 0 and LB - 1 whole, the other rows' cells a = 0 and LA - 1), or, with
+ * whole != 0, every cell of the slices; one thread per cell. */
+template <class T, int NF, int SHAPE, class F>
+__global__ void __launch_bounds__(256) k_staged_edge(StagedGeo g, Fields<T, NF> fld, int64_t s0, int64_t s1,
+                                                      int32_t whole, F f)
+{
+    const uint64_t per = whole ? g.S : 2 * g.la + 2 * (g.lb - 2);
+    const uint64_t n = per * (uint64_t)(s1 - s0);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t si = i / per, j = i - si * per;
+        uint64_t a, b;
+        if (whole) {
+            b = j / g.la;
+            a = j - b * g.la;
+        } else if (j < 2 * g.la) {
+            b = j < g.la ? 0 : g.lb - 1;
+            a = j < g.la ? j : j - g.la;
+        } else {
+            // column a = 0, then a = LA - 1: consecutive lanes on consecutive
+            // rows share their neighbors' lines
+            const uint64_t k = j - 2 * g.la, h = g.lb - 2;
+            b = 1 + (k < h ? k : k - h);
+            a = k < h ? 0 : g.la - 1;
+        }
+        const int64_t s = s0 + (int64_t)si, c = s + g.cbase;
+        const uint64_t lin = a + g.la * b + g.S * (uint64_t)c;
+        if (lin < g.lo || lin >= g.hi) continue;
+        EdgeCell<T, NF, SHAPE> cell;
+        cell.slot = a + g.la * b + g.S * (uint64_t)s;
+        cell.id = lin + 1;
+        cell.fld = fld;
+        cell.la = g.la;
+        cell.lb = g.lb;
+        cell.lc = g.lc;
+        cell.S = g.S;
+        cell.lo = g.lo;
+        cell.hi = g.hi;
+        cell.a = (int64_t)a;
+        cell.b = (int64_t)b;
+        cell.c = c;
+        cell.cbase = g.cbase;
+        cell.pa = g.pa;
+        cell.pb = g.pb;
+        cell.pc = g.pc;
+        cell.inv[0] = g.inv[0];
+        cell.inv[1] = g.inv[1];
+        cell.inv[2] = g.inv[2];
+        cell.scale = g.scale;
+        f(cell);
+    }
+}
+
+template <class T, int NF>
+struct StagedShape {
+    // the register window holds 9 (NB + 2) elements per field: NB rows per
+    // lane for 4-byte data, fewer (and more waves) for more bytes
+    static constexpr int units = (int)((NF * sizeof(T) + 3) / 4);
+    static constexpr int NB = units <= 1 ? 4 : (units == 2 ? 2 : 1);
+    static constexpr int NW = units <= 1 ? 4 : 8;
+    static constexpr int TB = NW * NB;
+    static constexpr int VEC = (int)(16 / sizeof(T));
+    static constexpr int PF = 1;  // planes in flight (deeper costs occupancy: tools/us_sweep.hip)
+};
+
+inline StagedGeo staged_geo(const dccrgx_stencil_view& v, int TB)
+{
+    StagedGeo g;
+    g.la = v.la;
+    g.lb = v.lb;
+    g.lc = v.lc;
+    g.S = v.la * v.lb;
+    g.lo = v.lo;
+    g.hi = v.hi;
+    g.cbase = v.cbase;
+    g.s0 = g.s1 = g.chunk = g.wrap_lo = g.wrap_hi = 0;
+    g.pa = v.per[0];
+    g.pb = v.per[1];
+    g.pc = v.per[2];
+    for (int d = 0; d < 3; d++) g.inv[v.perm[d]] = d;
+    g.scale = v.scale;
+    g.tiles_a = (uint32_t)((v.la + 63) / 64);
+    g.tiles_b = (uint32_t)((v.lb + TB - 1) / TB);
+    g.nwg = 0;
+    return g;
+}
+
+template <class T, int NF, int SHAPE, class F>
+int launch_staged(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, int64_t s1, F f, hipStream_t st,
+                  int64_t want)
+{
+    typedef StagedShape<T, NF> Sh;
+    StagedGeo g = staged_geo(v, Sh::TB);
+    g.s0 = s0;
+    g.s1 = s1;
+    const int64_t tiles = (int64_t)g.tiles_a * g.tiles_b, nsl = s1 - s0;
+    int64_t chunks = (want + tiles - 1) / tiles;
+    chunks = chunks < 1 ? 1 : (chunks > nsl ? nsl : chunks);
+    g.chunk = (nsl + chunks - 1) / chunks;
+    const int64_t nwg = tiles * ((nsl + g.chunk - 1) / g.chunk);
+    if (nwg >= (1ll << 31)) return DCCRGX_EINVAL;
+    g.nwg = (uint32_t)nwg;
+    if (v.la % Sh::VEC == 0)
+        hipLaunchKernelGGL((k_staged<T, NF, SHAPE, Sh::NW, Sh::NB, Sh::VEC, Sh::PF, F>), dim3(g.nwg),
+                           dim3(64 * Sh::NW), 0, st, g, fld, f);
+    else
+        hipLaunchKernelGGL((k_staged<T, NF, SHAPE, Sh::NW, Sh::NB, 1, Sh::PF, F>), dim3(g.nwg), dim3(64 * Sh::NW),
+                           0, st, g, fld, f);
+    return DCCRGX_OK;
+}
+
+/* the wrap slice s (canonical 0: CLS_LOW, LC - 1: CLS_HIGH), the plane across
+ * the wrap read from storage slice `across` */
+template <class T, int NF, int SHAPE, int CLS, class F>
+int launch_staged_wrap(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s, int64_t across, F f,
+                       hipStream_t st)
+{
+    typedef StagedShape<T, NF> Sh;
+    StagedGeo g = staged_geo(v, Sh::TB);
+    g.s0 = s;
+    g.s1 = s + 1;
+    g.wrap_lo = g.wrap_hi = across;
+    const int64_t tiles = (int64_t)g.tiles_a * g.tiles_b;
+    if (tiles >= (1ll << 31)) return DCCRGX_EINVAL;
+    if (v.la % Sh::VEC == 0)
+        hipLaunchKernelGGL((k_staged_wrap<T, NF, SHAPE, Sh::NW, Sh::NB, Sh::VEC, CLS, F>), dim3((unsigned)tiles),
+                           dim3(64 * Sh::NW), 0, st, g, fld, f);
+    else
+        hipLaunchKernelGGL((k_staged_wrap<T, NF, SHAPE, Sh::NW, Sh::NB, 1, CLS, F>), dim3((unsigned)tiles),
+                           dim3(64 * Sh::NW), 0, st, g, fld, f);
+    return DCCRGX_OK;
+}
+
+template <class T, int NF, int SHAPE, class F>
+int launch_edge(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, int64_t s1, bool whole, F f,
+                hipStream_t st)
+{
+    if (s1 <= s0) return DCCRGX_OK;
+    const StagedGeo g = staged_geo(v, 1);
+    const uint64_t per = whole ? v.la * v.lb : 2 * v.la + 2 * (v.lb - 2), n = per * (uint64_t)(s1 - s0);
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks)
+        hipLaunchKernelGGL((k_staged_edge<T, NF, SHAPE, F>), dim3((unsigned)blocks), dim3(256), 0, st, g, fld, s0, s1,
+                           (int32_t)whole, f);
+    return DCCRGX_OK;
+}
+
+/* the staged launches of one slice range [s0, s1) of a region: the staged
+ * kernel for the slices whose canonical c is in [1, LC - 1); the first and
+ * last slice of a periodic C by the wrap kernel when the slice across the
+ * wrap is held whole or not at all by this rank, else (and for a
+ * non-periodic C) by the edge walk; the ring of every other slice by the
+ * edge walk */
+template <class T, int NF, int SHAPE, class F>
+int staged_range(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, int64_t s1, F f, hipStream_t st,
+                 int64_t want)
+{
+    const int64_t lc = (int64_t)v.lc, cb = v.cbase;
+    const int64_t m0 = s0 > 1 - cb ? s0 : 1 - cb;
+    const int64_t m1 = s1 < lc - 1 - cb ? s1 : lc - 1 - cb;
+    int e = DCCRGX_OK;
+    if (m1 > m0) {
+        e = launch_staged<T, NF, SHAPE>(v, fld, m0, m1, f, st, want);
+        if (e == DCCRGX_OK) e = launch_edge<T, NF, SHAPE>(v, fld, m0, m1, false, f, st);
+        if (e != DCCRGX_OK) return e;
+    }
+    for (int side = 0; side < 2; side++) {
+        const int64_t s = side == 0 ? -cb : lc - 1 - cb;
+        if (s < s0 || s >= s1 || (side == 1 && lc == 1)) continue;
+        const uint64_t oc = side == 0 ? (uint64_t)(lc - 1) : 0;  // canonical slice across the wrap
+        const uint64_t o0 = oc * v.la * v.lb, o1 = o0 + v.la * v.lb;
+        const bool whole = o0 >= v.lo && o1 <= v.hi, none = o1 <= v.lo || o0 >= v.hi;
+        if (v.per[2] && lc >= 3 && (whole || none)) {
+            const int64_t across = whole ? (int64_t)oc - cb : (side == 0 ? s - 1 : s + 1);
+            e = side == 0 ? launch_staged_wrap<T, NF, SHAPE, CLS_LOW>(v, fld, s, across, f, st)
+                          : launch_staged_wrap<T, NF, SHAPE, CLS_HIGH>(v, fld, s, across, f, st);
+            if (e == DCCRGX_OK) e = launch_edge<T, NF, SHAPE>(v, fld, s, s + 1, false, f, st);
+        } else {
+            e = launch_edge<T, NF, SHAPE>(v, fld, s, s + 1, true, f, st);
+        }
+        if (e != DCCRGX_OK) return e;
+    }
+    return DCCRGX_OK;
+}
+
+}  // namespace detail
+
+/* options of the staged launches */
+struct StagedOptions {
+    int64_t workgroups = 131072;  // target workgroups of the staged kernel (tiles x slice chunks)
+    bool staged = true;          // false: every cell through the walk (for comparisons)
+};
+
+/* Launch f(cell) for every cell of the region described by v, the declared
+ * fields' values staged (see above).  Returns a DCCRGX_* code. */
+template <class T, int NF, class F>
+int for_each_cell_staged(const dccrgx_stencil_view& v, Fields<T, NF> fld, F f, hipStream_t st,
+                         const StagedOptions& opt = StagedOptions())
+{
+    static_assert(sizeof(T) == 1 || sizeof(T) == 2 || sizeof(T) == 4 || sizeof(T) == 8, "element of 1-8 bytes");
+    static_assert(NF >= 1 && NF <= 8, "1 to 8 staged fields");
+    if (v.n_cells == 0) return DCCRGX_OK;
+    auto walk = [=] __device__(const auto& cell) {
+        LoadedCell<typename std::decay<decltype(cell)>::type, T, NF> lc{cell, fld, cell.slot, cell.id};
+        f(lc);
+    };
+    if (v.kind != 0) return for_each_cell(v, walk, st);
+    const detail::UniformGeo g = detail::uniform_geo(v);
+    const int shape = v.shape & (DCCRGX_SHAPE_CUBE1 | DCCRGX_SHAPE_FACES);
+    // staged: the cube / the faces on axes of >= 3 cells (periodic axes of 1
+    // or 2 cells repeat neighbors across the wrap; shorter non-periodic ones
+    // leave no inner cells), planes of < 2^31 bytes
+    const bool fast = opt.staged && shape != 0 && v.la >= 3 && v.lb >= 3 && v.lc >= 3 &&
+                      v.la * v.lb * sizeof(T) < (1ull << 31);
+    for (int r = 0; r < 2; r++) {
+        const int64_t s0 = v.s0[r], s1 = v.s1[r];
+        if (s1 <= s0) continue;
+        int e;
+        if (!fast)
+            e = detail::launch_slices(g, s0, s1, walk, st);
+        else if (shape == DCCRGX_SHAPE_CUBE1)
+            e = detail::staged_range<T, NF, DCCRGX_SHAPE_CUBE1>(v, fld, s0, s1, f, st, opt.workgroups);
+        else
+            e = detail::staged_range<T, NF, DCCRGX_SHAPE_FACES>(v, fld, s0, s1, f, st, opt.workgroups);
+        if (e != DCCRGX_OK) return e;
+    }
+    return hipGetLastError() == hipSuccess ? DCCRGX_OK : DCCRGX_EHIP;
+}
+
+/* the same for neighborhood hood_id and region of a grid */
+template <class T, int NF, class F>
+int for_each_cell_staged(const dccrgx_grid* grid, int32_t hood_id, int32_t region, Fields<T, NF> fld, F f,
+                         hipStream_t st = nullptr, const StagedOptions& opt = StagedOptions())
+{
+    dccrgx_stencil_view v;
+    const int e = dccrgx_stencil_view_get(grid, hood_id, region, &v);
+    if (e != DCCRGX_OK) return e;
+    return for_each_cell_staged(v, fld, f, st ? st : (hipStream_t)v.stream, opt);
 }
 
 }  // namespace dccrgx_user

@@ -50,13 +50,16 @@ def lib():
     L.us_digest.argtypes = [C.c_void_p] + [C.c_int32] * 6
     L.us_region_cells.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
     L.us_region_cells.restype = C.c_longlong
+    L.us_gol_staged.argtypes = [C.c_void_p] + [C.c_int32] * 6
+    L.us_digest_staged.argtypes = [C.c_void_p] + [C.c_int32] * 6
+    L.us_fsum_staged.argtypes = [C.c_void_p] + [C.c_int32] * 6
     return L
 
 
 def test_example_library_exports():
     """CPU: build() made the user-stencil program and it exports its entry points."""
     L = C.CDLL(LIB)
-    for s in ("us_gol", "us_digest", "us_region_cells"):
+    for s in ("us_gol", "us_digest", "us_region_cells", "us_gol_staged", "us_digest_staged", "us_fsum_staged"):
         assert hasattr(L, s)
 
 
@@ -114,7 +117,8 @@ def test_user_stencil_iteration_order(case, P, user_hood):
         if user_hood:
             assert g.add_neighborhood(hood, USER_ITEMS[hood_len])
         for f, t in (("id", np.uint64), ("cid", np.uint64), ("dig", np.uint64), ("cnt", np.uint32),
-                     ("a", np.uint32), ("b", np.uint32), ("n", np.uint32)):
+                     ("a", np.uint32), ("b", np.uint32), ("n", np.uint32), ("scid", np.uint64),
+                     ("sdig", np.uint64), ("scnt", np.uint32), ("sb", np.uint32), ("sn", np.uint32)):
             g.add_field(f, t)
         loc = g.local_cells()
         g.write_local("id", loc)
@@ -158,19 +162,25 @@ def test_user_stencil_iteration_order(case, P, user_hood):
             assert L.us_digest(h, hood, X.REGION_OUTER, fid("id"), fid("cid"), fid("dig"), fid("cnt")) == 0
             for region in (X.REGION_INNER, X.REGION_OUTER):
                 assert L.us_gol(h, hood, fid("a"), fid("b"), fid("n"), region) == 0
+                # the staged launches: values instead of slots (the staged
+                # kernel where the neighborhood is the cube or the faces)
+                assert L.us_gol_staged(h, hood, fid("a"), fid("sb"), fid("sn"), region, 1) == 0
+                assert L.us_digest_staged(h, hood, region, fid("id"), fid("scid"), fid("sdig"), fid("scnt")) == 0
             g.ctx.synchronize()
             assert g.read_local("cid").tolist() == loc
-            got_cnt = g.read_local("cnt").tolist()
-            got_dig = g.read_local("dig").tolist()
-            got_n = g.read_local("n").tolist()
-            got_b = g.read_local("b").tolist()
-            for k, c in enumerate(loc):
-                want = lists[c]
-                assert got_cnt[k] == len(want), (c, got_cnt[k], want)
-                assert got_dig[k] == digest(want, mix), (c, want)
-                n = sum(alive[i] for i, _ in want)
-                assert got_n[k] == n, c
-                assert got_b[k] == (1 if n == 3 else (alive[c] if n == 2 else 0)), c
+            assert g.read_local("scid").tolist() == loc
+            for pre in ("", "s"):
+                got_cnt = g.read_local(pre + "cnt").tolist()
+                got_dig = g.read_local(pre + "dig").tolist()
+                got_n = g.read_local(pre + "n").tolist()
+                got_b = g.read_local(pre + "b").tolist()
+                for k, c in enumerate(loc):
+                    want = lists[c]
+                    assert got_cnt[k] == len(want), (pre, c, got_cnt[k], want)
+                    assert got_dig[k] == digest(want, mix), (pre, c, want)
+                    n = sum(alive[i] for i, _ in want)
+                    assert got_n[k] == n, (pre, c)
+                    assert got_b[k] == (1 if n == 3 else (alive[c] if n == 2 else 0)), (pre, c)
     finally:
         for g in grids:
             g.close()
@@ -217,16 +227,26 @@ def test_user_stencil_view_follows_refinement():
         ctx.close()
 
 
+LARGER = [((70, 40, 9), (True, False, True), 1),
+          ((66, 36, 11), (False, True, False), 2),
+          ((130, 33, 5), (True, True, True), 1),
+          # A % 4 == 0 (16-byte staged loads), several tiles along A and B
+          ((132, 37, 12), (False, True, True), 1),
+          ((128, 50, 7), (True, True, False), 0),
+          ((8, 20, 16), (True, False, False), 1)]
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("staged", [None, 0, 1])
 @pytest.mark.parametrize("P", [1, 3])
-@pytest.mark.parametrize("length,per,hood_len", [((70, 40, 9), (True, False, True), 1),
-                                                 ((66, 36, 11), (False, True, False), 2),
-                                                 ((130, 33, 5), (True, True, True), 1)])
-def test_gol_functor_larger_grids(length, per, hood_len, P):
+@pytest.mark.parametrize("length,per,hood_len", LARGER)
+def test_gol_functor_larger_grids(length, per, hood_len, P, staged):
     """The game-of-life functor over several steps on grids where most cells
     take the fixed-distance walk (no boundary within reach), with wraps and
     rank slabs: equal to the oracle's run (oracle gol_reference_run, the
-    reference's lists) on every rank."""
+    reference's lists) on every rank.  staged: None = for_each_cell (slots),
+    1 = for_each_cell_staged (the staged kernel for the cube / faces plus the
+    boundary walks), 0 = for_each_cell_staged with every cell walked."""
     import torch
 
     import dccrg_amd as D
@@ -266,14 +286,94 @@ def test_gol_functor_larger_grids(length, per, hood_len, P):
                     g.unpack_from(p, buf.data_ptr(), nb, fields=[cur])
                 g.ctx.synchronize()
             for g in grids:
-                assert L.us_gol(g._h, hood, g.field_id(cur), g.field_id(nxt), g.field_id("n"),
-                                       X.REGION_ALL) == 0
+                if staged is None:
+                    assert L.us_gol(g._h, hood, g.field_id(cur), g.field_id(nxt), g.field_id("n"),
+                                    X.REGION_ALL) == 0
+                else:
+                    for region in (X.REGION_INNER, X.REGION_OUTER):
+                        assert L.us_gol_staged(g._h, hood, g.field_id(cur), g.field_id(nxt), g.field_id("n"),
+                                               region, staged) == 0
                 g.ctx.synchronize()
             cur, nxt = nxt, cur
         for g in grids:
             idx = g.local_cells().astype(np.int64) - 1
             assert np.array_equal(g.read_local(cur), ref_a[idx])
             assert np.array_equal(g.read_local("n"), ref_n[idx])
+    finally:
+        for g in grids:
+            g.close()
+        for ctx in ctxs:
+            ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("length,per,hood_len", [((68, 40, 9), (True, False, True), 1),
+                                                 ((33, 20, 14), (False, True, True), 1),
+                                                 ((64, 18, 10), (True, True, True), 0),
+                                                 ((20, 16, 12), (True, False, True), 2)])
+def test_staged_f64_order(length, per, hood_len, P):
+    """A floating-point functor over two staged f64 fields, summed over the
+    neighbors in order (us_fsum_staged): the staged launch gives the same
+    bits as the walk (same neighbors, same order), and both are within
+    1e-12 of the sum in the reference's iteration order over the oracle's
+    lists (fp64 contraction may differ from numpy)."""
+    import torch
+
+    import dccrg_amd as D
+    from dccrg_amd import _capi as X
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    n = int(np.prod(length))
+    ids = np.arange(1, n + 1, dtype=np.uint64)
+    rng = np.random.default_rng(11)
+    u0, w0 = rng.standard_normal(n), rng.uniform(0.5, 1.5, n)
+    og = O.Grid(length, 0, per, hood_len, list(range(1, n + 1)))
+    L = lib()
+    hood = D.DEFAULT_NEIGHBORHOOD_ID
+    ctxs, grids = [], []
+    for r in range(P):
+        ctx = D.Context(0, r, P)
+        g = (D.Dccrg().set_initial_length(length).set_periodic(*per).set_neighborhood_length(hood_len)
+             .initialize(ctx))
+        for f in ("u", "w", "o1", "o0"):
+            g.add_field(f, np.float64)
+        idx = g.local_cells().astype(np.int64) - 1
+        g.write_local("u", u0[idx])
+        g.write_local("w", w0[idx])
+        ctxs.append(ctx)
+        grids.append(g)
+    try:
+        msgs = {}
+        for r, g in enumerate(grids):
+            for p in g.get_cells_to_send():
+                buf = torch.empty(1 << 22, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
+                msgs[(r, p)] = (buf, g.pack_to(p, buf.data_ptr(), buf.numel(), fields=["u", "w"]))
+                g.ctx.synchronize()
+        for r, g in enumerate(grids):
+            g.halo_self(fields=["u", "w"])
+            for p in g.get_cells_to_receive():
+                buf, nb = msgs[(p, r)]
+                g.unpack_from(p, buf.data_ptr(), nb, fields=["u", "w"])
+            g.ctx.synchronize()
+        for g in grids:
+            f = g.field_id
+            for region in (X.REGION_INNER, X.REGION_OUTER):
+                assert L.us_fsum_staged(g._h, hood, f("u"), f("w"), f("o1"), region, 1) == 0
+                assert L.us_fsum_staged(g._h, hood, f("u"), f("w"), f("o0"), region, 0) == 0
+            g.ctx.synchronize()
+            got1, got0 = g.read_local("o1"), g.read_local("o0")
+            assert np.array_equal(got1.view(np.uint64), got0.view(np.uint64))
+            loc = g.local_cells()
+            want = np.empty(loc.size)
+            for k, c in enumerate(loc):
+                c = int(c)
+                me = u0[c - 1]
+                s = me
+                for i, _ in O.iteration_cache_lists(og.find_neighbors_of(c), og.find_neighbors_to(c))[0]:
+                    s += w0[i - 1] * u0[i - 1] - 0.25 * me
+                want[k] = s
+            assert np.allclose(got1, want, rtol=1e-12, atol=1e-12)
     finally:
         for g in grids:
             g.close()

@@ -1,0 +1,65 @@
+#!/bin/bash
+# One GPU pass, steps chosen on the command line (each under its own time
+# limit; the pass stops at the first failing step):
+#   bash tools/gpu_pass.sh TAG STEP [STEP ...]
+# steps:
+#   tests[=PYTEST_ARGS]  pytest -m gpu (default: the whole GPU suite) -> TAG/tests.log
+#   smoke                __graft_entry__.smoke()                     -> TAG/smoke.log
+#   bench                bench.py --steps 20 --warmup 3               -> TAG/bench.log
+#   prof                 rocprofv3 --kernel-trace --stats of bench.py -> TAG/prof/
+#   pmc                  FETCH_SIZE / WRITE_SIZE passes of bench.py   -> TAG/pmc_*/
+#   us                   tools/user_stencil_bench.py (+ --stats)      -> TAG/us.log, TAG/us_prof/
+#   uspmc                FETCH/WRITE + SQ passes of the user stencil  -> TAG/uspmc_*/
+#   adapt / adaptbig     tools/adapt_loop.py at 218k / 3.5 M leaves   -> TAG/adapt*.log
+#   advlarge             tools/run_adv_large.py (+ --stats)           -> TAG/adv_large.log
+#   py=SCRIPT            python -u SCRIPT                              -> TAG/<script>.log
+set -o pipefail
+tag=$1; shift
+out=gpurun_out/$tag; mkdir -p $out
+export TMPDIR=/tmp
+fail() { echo "step $1 failed rc=$2"; tail -n 30 "$3"; exit 1; }
+for step in "$@"; do
+  case $step in
+    tests*)
+      args=${step#tests}; args=${args#=}; [ -z "$args" ] && args="tests"
+      timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $args > $out/tests.log 2>&1 || fail tests $? $out/tests.log
+      tail -n 2 $out/tests.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > $out/smoke.log 2>&1 || fail smoke $? $out/smoke.log
+      tail -n 1 $out/smoke.log ;;
+    bench)
+      timeout -k 10 600 python -u bench.py --steps 20 --warmup 3 > $out/bench.log 2>&1 || fail bench $? $out/bench.log
+      tail -n 1 $out/bench.log | cut -c1-600 ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python3 bench.py --steps 20 --warmup 3 > $out/prof.log 2>&1 || fail prof $? $out/prof.log ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $out/pmc_$c -o run -- python3 bench.py --steps 5 --warmup 1 --no-secondary > $out/pmc_$c.log 2>&1 || fail pmc_$c $? $out/pmc_$c.log
+      done ;;
+    us)
+      timeout -k 10 300 python -u tools/user_stencil_bench.py > $out/us.log 2>&1 || fail us $? $out/us.log
+      cat $out/us.log | cut -c1-1500
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/us_prof -o run -- python3 tools/user_stencil_bench.py > $out/us_prof.log 2>&1 || fail us_prof $? $out/us_prof.log ;;
+    uspmc)
+      i=0
+      for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY" "TCC_HIT_sum TCC_MISS_sum TA_BUSY_avr GRBM_GUI_ACTIVE"; do
+        i=$((i+1))
+        timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $out/uspmc_$i -o run -- python3 tools/user_stencil_bench.py > $out/uspmc_$i.log 2>&1 || fail uspmc_$i $? $out/uspmc_$i.log
+      done ;;
+    adapt)
+      timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt.log 2>&1 || fail adapt $? $out/adapt.log
+      tail -n 2 $out/adapt.log ;;
+    adaptbig)
+      ADAPT_N=1600 ADAPT_REL=0.006 timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_3p5M.log 2>&1 || fail adaptbig $? $out/adapt_3p5M.log
+      tail -n 2 $out/adapt_3p5M.log ;;
+    advlarge)
+      timeout -k 10 300 python -u tools/run_adv_large.py > $out/adv_large.log 2>&1 || fail advlarge $? $out/adv_large.log
+      tail -n 3 $out/adv_large.log ;;
+    py=*)
+      scr=${step#py=}; name=$(basename $scr .py)
+      timeout -k 10 600 python -u $scr > $out/$name.log 2>&1 || fail $name $? $out/$name.log
+      tail -n 5 $out/$name.log ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "pass $tag done"
