@@ -874,6 +874,9 @@ def main():
     ap.add_argument("--no-secondary", action="store_true", help="skip the other configs' lines (N = 1)")
     ap.add_argument("--no-halo-payload", action="store_true", help="skip the byte-payload halo line")
     ap.add_argument("--no-check", action="store_true", help="skip the self-check after the timed loop (profiling)")
+    ap.add_argument("--test-corrupt-ghost", action="store_true",
+                    help="tests: libdccrgx's corrupt_ghost test option (a bad ghost cell after every exchange); "
+                         "the self-check must fail")
     ap.add_argument("--stall-timeout", type=float, default=180.0,
                     help="seconds before a rank stuck in RCCL init or the first exchange ends the run (exit 3)")
     ap.add_argument("--dry-run", action="store_true",
@@ -903,6 +906,9 @@ def main():
     device = local_rank % max(ndev, 1)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.test_corrupt_ghost:
+        from dccrg_amd.grid import set_test_option
+        set_test_option("corrupt_ghost", 1)
     ctx = D.Context(device, rank, world)
     # ranks on the same physical GPU (a rehearsal on one GPU): RCCL refuses
     # that.  Decided from the devices' PCI ids, so a launcher that makes one

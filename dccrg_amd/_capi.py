@@ -110,6 +110,7 @@ SIGNATURES = {
     "dccrgx_get_unique_id": (C.c_int, [C.c_char_p]),
     "dccrgx_ctx_comm_init": (C.c_int, [_vp, C.c_char_p]),
     "dccrgx_ctx_route_self_through_rccl": (C.c_int, [_vp, C.c_int32]),
+    "dccrgx_test_option": (C.c_int, [C.c_char_p, C.c_int64, C.c_int32]),
     "dccrgx_ctx_compute_stream": (C.c_int, [_vp, C.POINTER(_vp)]),
     "dccrgx_ctx_set_host_transport": (C.c_int, [_vp, C.POINTER(HostTransport_t)]),
     "dccrgx_ctx_synchronize": (C.c_int, [_vp]),

@@ -131,14 +131,14 @@ def request_adaptation(grid: Dccrg, to_refine, not_to_unrefine, to_unrefine):
 
 
 def finish_adaptation(grid: Dccrg, geom: CartesianGeometry, all_requests=None,
-                      update: bool = True) -> Tuple[int, int]:
+                      update: bool = True, agreed: bool = False) -> Tuple[int, int]:
     """adapter.hpp:215-319: stop_refining (all_requests: the union of every
-    rank's requests, see Dccrg.stop_refining), data of new cells and of the
-    parents of removed cells, velocities and lengths, ghost update (skipped
-    with update=False)."""
+    rank's requests, agreed: see Dccrg.stop_refining), data of new cells and
+    of the parents of removed cells, velocities and lengths, ghost update
+    (skipped with update=False)."""
     if grid.get_maximum_refinement_level() == 0:
         return 0, 0
-    new = grid.stop_refining(all_requests=all_requests)
+    new = grid.stop_refining(all_requests=all_requests, agreed=agreed)
     removed = grid.get_removed_cells()
     # new cells are value-initialised by the rebuild (flux = 0); they take the
     # parent's density (:229-251).  Parents of removed cells: 0, then

@@ -637,17 +637,13 @@ int advect_launch(dccrgx_grid* grid, Hood& h, const AdvPtrs& p, double dt, int32
         const FaceCache& F = *h.faces;
         const FaceView fv{F.n, F.ell_slot, F.o_base, F.o_cnt, F.o_slot, F.o_dir, F.d_over};
         // explicit grids store local cell q in slot q (explicit.hip): no slot loads
-        static const int64_t wpe = getenv_int("DCCRGX_ADV_WPE", 4);  // sweep: waves per SIMD the kernel is built for
         const uint32_t* rpos = region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos;
-        static const int64_t use_buf = getenv_int("DCCRGX_ADV_BUF", 1);
-        if (use_buf && grid->n_slots < (1ull << 28) && 6 * F.n < (1ull << 29)) {  // byte offsets below 2 GiB
-            auto k = wpe >= 6 ? k_ex_advect_faces_buf<6> : wpe >= 5 ? k_ex_advect_faces_buf<5> : k_ex_advect_faces_buf<1>;
-            hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv, rpos, R.n, rho_out, t0, t1);
+        if (grid->n_slots < (1ull << 28) && 6 * F.n < (1ull << 29)) {  // buffer loads: byte offsets below 2 GiB
+            hipLaunchKernelGGL(k_ex_advect_faces_buf<1>, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv, rpos, R.n,
+                               rho_out, t0, t1);
         } else {
-            auto k = wpe >= 8 ? k_ex_advect_faces<8> : wpe >= 6 ? k_ex_advect_faces<6> : wpe >= 5 ? k_ex_advect_faces<5>
-                                                                                                 : k_ex_advect_faces<1>;
-            hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv, (const uint32_t*)nullptr, rpos,
-                               R.n, rho_out, t0, t1);
+            hipLaunchKernelGGL(k_ex_advect_faces<1>, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv,
+                               (const uint32_t*)nullptr, rpos, R.n, rho_out, t0, t1);
         }
         DX_HIP(hipGetLastError());
         return DCCRGX_OK;
@@ -718,6 +714,7 @@ extern "C" {
 int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt,
                          int32_t region)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -730,6 +727,7 @@ int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect
 
 int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     AdvPtrs p;
     DX_TRY(adv_ptrs(grid, f, &p));
@@ -750,6 +748,7 @@ int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f)
 
 int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f, double* local_min)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && local_min, DCCRGX_EINVAL, "null argument");
     AdvPtrs p;
     DX_TRY(adv_ptrs(grid, f, &p));
@@ -835,6 +834,7 @@ int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_a
                               double diff_increase, double diff_threshold, double unrefine_sensitivity,
                               int8_t* marks_out, double* max_diff_out)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && f && (marks_out || !grid->n_local), DCCRGX_EINVAL, "null argument");
     int8_t* d_marks = nullptr;
     DX_TRY(adapt_marks_device(grid, hood_id, f, diff_increase, diff_threshold, unrefine_sensitivity, &d_marks,
@@ -851,6 +851,7 @@ int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccr
                                   uint64_t* to_refine, uint64_t* not_to_unrefine, uint64_t* to_unrefine, size_t cap,
                                   size_t counts[3])
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && f && counts, DCCRGX_EINVAL, "null argument");
     counts[0] = counts[1] = counts[2] = 0;
     if (grid->map.max_lvl == 0) return DCCRGX_OK;  // adapter.hpp:57-59
@@ -890,6 +891,7 @@ int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccr
 int dccrgx_advect_set_geometry(dccrgx_grid* grid, const dccrgx_advect_fields* f, const double start[3],
                                const double level_0_cell_length[3])
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && f && start && level_0_cell_length, DCCRGX_EINVAL, "null argument");
     AdvPtrs p;
     DX_TRY(adv_ptrs(grid, f, &p));
@@ -925,6 +927,7 @@ int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t
 
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && f, DCCRGX_EINVAL, "null argument");
     // 2d.cpp:321-390: start density halo, inner fluxes, wait, outer fluxes,
     // apply -- fused: the flux kernels write the new density into the other

@@ -283,6 +283,13 @@ void rebuild_abort(RebuildTxn& t)
 
 void rebuild_commit(dccrgx_grid* grid, RebuildTxn& t)
 {
+    // every field was rebuilt (field creation is refused while a rebuild is
+    // prepared, DX_NOT_PENDING): anything else is a broken invariant
+    if (t.np.size() != grid->fields.size() || t.cap.size() != grid->fields.size()) {
+        fprintf(stderr, "dccrgx: rebuild prepared %zu field arrays for %zu fields\n", t.np.size(),
+                grid->fields.size());
+        std::abort();
+    }
     Explicit* old_ex = grid->ex;
     std::map<int32_t, Hood> old_hoods;
     old_hoods.swap(grid->hoods);
@@ -508,12 +515,11 @@ int ensure_explicit(dccrgx_grid* grid)
     return rebuild(grid, leaves, {});
 }
 
-// DCCRGX_TEST_FAIL_STOP_REFINING=<rank>: the decisions of that rank's next
+// test option fail_stop_refining = rank + 1: the decisions of that rank's
 // stop_refining report ENOMEM (the collective two-phase tests)
 bool amr_fail_injected(const dccrgx_grid* grid)
 {
-    const char* e = getenv("DCCRGX_TEST_FAIL_STOP_REFINING");
-    return e && *e && atoi(e) == grid->ctx->rank;
+    return test_opt(OPT_FAIL_STOP_REFINING, 0) == (int64_t)grid->ctx->rank + 1;
 }
 
 }  // namespace

@@ -1035,7 +1035,7 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     uint32_t *d_retry, *d_nretry = d_cnt + NC - 1;
     DX_TRY(S.get(&d_retry, N));
     // DCCRGX_OU_SMALL (tests): the first pass's queue length, to send walks to the second pass
-    const uint32_t Q1 = (uint32_t)std::max<int64_t>(2, getenv_int("DCCRGX_OU_SMALL", 256));
+    const uint32_t Q1 = (uint32_t)std::max<int64_t>(2, test_opt(OPT_OU_SMALL, 256));
     uint32_t S1 = 16;
     while (S1 < 2 * Q1) S1 <<= 1;  // 256 -> 512: 6 KiB per wave
     if (Q1 < Q && (size_t)(Q1 + S1) * 8 <= 48 * 1024) {

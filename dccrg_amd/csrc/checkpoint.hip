@@ -573,6 +573,7 @@ int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* 
 
 int dccrgx_load_cell_data(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     DX_CHECK(grid->load, DCCRGX_ESTATE, "the grid was not loaded from a file (or loading finished)");
     FDesc d;

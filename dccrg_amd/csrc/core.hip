@@ -2,6 +2,7 @@
 // mapping kernels (dccrg_mapping.hpp re-designed for gfx950: one lane per id,
 // magic-number 64-bit division, no loops over levels beyond a branch-free
 // compare chain).
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstring>
@@ -63,20 +64,9 @@ static void stage_copy(void* dst, const void* src, size_t k)
     });
 }
 
-static bool pageable_copies()  // DCCRGX_PAGEABLE=1: direct pageable copies (comparison runs)
-{
-    static const bool on = getenv_flag("DCCRGX_PAGEABLE");
-    return on;
-}
-
 int dx_h2d(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
 {
     if (!bytes) return DCCRGX_OK;
-    if (pageable_copies()) {
-        DX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
-        DX_HIP(hipStreamSynchronize(st));
-        return DCCRGX_OK;
-    }
     DX_TRY(stage_reserve(c, std::min(bytes, STAGE_CHUNK)));
     for (size_t off = 0; off < bytes; off += STAGE_CHUNK) {
         const size_t k = std::min(STAGE_CHUNK, bytes - off);
@@ -90,7 +80,7 @@ int dx_h2d(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
 int dx_h2d_async(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
 {
     if (!bytes) return DCCRGX_OK;
-    if (bytes > Ctx::UP_SLOT_BYTES || st != c->compute || pageable_copies()) return dx_h2d(c, dst, src, bytes, st);
+    if (bytes > Ctx::UP_SLOT_BYTES || st != c->compute) return dx_h2d(c, dst, src, bytes, st);
     if (!c->up) {
         DX_HIP(hipHostMalloc((void**)&c->up, Ctx::UP_SLOTS * Ctx::UP_SLOT_BYTES, hipHostMallocDefault));
         for (int k = 0; k < Ctx::UP_SLOTS; k++) DX_HIP(hipEventCreateWithFlags(&c->up_ev[k], hipEventDisableTiming));
@@ -177,11 +167,6 @@ int dx_d2h_many(Ctx* c, const D2H* v, size_t n, hipStream_t st)
 int dx_d2h(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
 {
     if (!bytes) return DCCRGX_OK;
-    if (pageable_copies()) {
-        DX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
-        DX_HIP(hipStreamSynchronize(st));
-        return DCCRGX_OK;
-    }
     DX_TRY(stage_reserve(c, std::min(bytes, STAGE_CHUNK)));
     for (size_t off = 0; off < bytes; off += STAGE_CHUNK) {
         const size_t k = std::min(STAGE_CHUNK, bytes - off);
@@ -843,19 +828,7 @@ void dx_cache_free_many(void* const* ps, size_t n, hipStream_t st, bool any_stre
             defer(D, std::move(all));
         }
     } else if (!blocks.empty()) {
-        // diagnosis: 1 wait for the device, 2 wait for the library's streams, 3 reuse at once (unsafe)
-        static const int64_t sync_free = getenv_int("DCCRGX_SYNC_FREE", 0);
-        if (sync_free) {
-            lk.unlock();
-            if (sync_free == 1) (void)hipDeviceSynchronize();
-            if (sync_free == 2)
-                for (hipStream_t s2 : D.streams) (void)hipStreamSynchronize(s2);
-            lk.lock();
-            for (auto& b : blocks) {
-                D.idle[b.second].push_back(b.first);
-                D.idle_bytes += b.second;
-            }
-        } else if (D.idle_bytes + D.held_bytes > CACHE_MAX_TOTAL) {  // too much kept: return them
+        if (D.idle_bytes + D.held_bytes > CACHE_MAX_TOTAL) {  // too much kept: return them
             lk.unlock();
             for (auto& b : blocks) (void)hipFree(b.first);  // waits for the device
             lk.lock();
@@ -1057,3 +1030,43 @@ int dccrgx_ctx_synchronize(dccrgx_ctx* c)
 }
 
 }  // extern "C"
+
+// ---- test options (internal.hpp) ------------------------------------------
+namespace dccrgx {
+namespace {
+std::atomic<int64_t> g_test_opt[OPT_COUNT];
+std::atomic<bool> g_test_set[OPT_COUNT];
+const char* const kTestOptName[OPT_COUNT] = {"gol_scalar",  "gol_chunk",      "poisson_multi",
+                                             "poisson_solo_global", "incremental", "ou_small",
+                                             "corrupt_ghost", "fail_stop_refining", "check_init"};
+}  // namespace
+
+int64_t test_opt(TestOpt o, int64_t dflt)
+{
+#ifdef DCCRGX_NO_TEST_OPTIONS
+    (void)o;
+    return dflt;
+#else
+    return g_test_set[o].load(std::memory_order_relaxed) ? g_test_opt[o].load(std::memory_order_relaxed) : dflt;
+#endif
+}
+}  // namespace dccrgx
+
+extern "C" int dccrgx_test_option(const char* name, int64_t value, int32_t set)
+{
+    using namespace dccrgx;
+    DX_CHECK(name, DCCRGX_EINVAL, "null name");
+#ifdef DCCRGX_NO_TEST_OPTIONS
+    (void)value;
+    (void)set;
+    return set_error(DCCRGX_EINVAL, "test options are compiled out of this build");
+#else
+    for (int o = 0; o < OPT_COUNT; o++)
+        if (std::strcmp(name, kTestOptName[o]) == 0) {
+            g_test_opt[o].store(value);
+            g_test_set[o].store(set != 0);
+            return DCCRGX_OK;
+        }
+    return set_error(DCCRGX_EINVAL, "unknown test option '%s'", name);
+#endif
+}

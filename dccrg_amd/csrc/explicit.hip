@@ -1263,7 +1263,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
     }
     DX_HIP(hipGetLastError());
     T.lap("leaves+lookup");
-    if (getenv_flag("DCCRGX_CHECK_INIT")) {  // diagnosis: device leaves and lookups against the host list
+    if (test_opt(OPT_CHECK_INIT, 0)) {  // device leaves and lookups against the host list
         std::vector<uint64_t> back(E->n);
         DX_TRY(dx_d2h(ctx, back.data(), E->d_leaves, E->n * 8, st));
         uint64_t bad = 0;
@@ -1277,7 +1277,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
         dx_free(d_e);
         std::fprintf(stderr, "[dccrgx] check_init n %llu leaves differing %llu lookups failing %d first %d bitmap %d\n",
                      (unsigned long long)E->n, (unsigned long long)bad, e[0], e[1] - 1, E->d_bits != nullptr);
-        DX_CHECK(!bad && !e[0], DCCRGX_EINTERNAL, "DCCRGX_CHECK_INIT: %llu leaves of the host list differ from the "
+        DX_CHECK(!bad && !e[0], DCCRGX_EINTERNAL, "check_init: %llu leaves of the host list differ from the "
                  "device list, %d lookups fail", (unsigned long long)bad, e[0]);
     }
     // ownership: the process of the level-0 ancestor (no load balancing),
@@ -1761,7 +1761,7 @@ __global__ void __launch_bounds__(64) k_inc_copy(const uint32_t* __restrict__ ne
 
 static bool incremental_rebuild(uint64_t n)
 {
-    const int64_t force = getenv_int("DCCRGX_INCREMENTAL", -1);  // 1 / 0: always / never (tests)
+    const int64_t force = test_opt(OPT_INCREMENTAL, -1);  // 1 / 0: always / never (tests)
     if (force >= 0) return force != 0;
     return n >= (1ull << 20);  // below, one full pass costs less than the extra launches
 }

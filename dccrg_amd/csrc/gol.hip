@@ -166,10 +166,10 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
     a.perA = u.perA;
     a.perB = u.perB;
     const int64_t nsl = s1 - s0;
-    // DCCRGX_GOL_CHUNK (tests): slices per workgroup, to put chunk seams in small grids
-    const int64_t chunk = getenv_int("DCCRGX_GOL_CHUNK", 0);
-    // DCCRGX_GOL_SCALAR (tests): the LDS-tiled scalar kernels on grids the vector kernels take
-    const bool vec = u.LA % 4 == 0 && u.S < (1ull << 31) && !getenv_flag("DCCRGX_GOL_SCALAR");
+    // test options: slices per workgroup (chunk seams in small grids); the
+    // LDS-tiled scalar kernels on grids the vector kernels take
+    const int64_t chunk = test_opt(OPT_GOL_CHUNK, 0);
+    const bool vec = u.LA % 4 == 0 && u.S < (1ull << 31) && !test_opt(OPT_GOL_SCALAR, 0);
     const uint32_t mult = u.perB ? 3u : 1u;
     if (u.LB == 1 && vec) {
         // 2-D / 1-D grids: k_gol26_rowv, 4 waves x 256 cells of a row per workgroup
@@ -290,6 +290,7 @@ static int gol_fields(dccrgx_grid* grid, int32_t a, int32_t b, int32_t c)
 int dccrgx_gol_compute(dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t fout, int32_t fcnt,
                        int32_t region)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     const Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -301,6 +302,7 @@ int dccrgx_gol_compute(dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t 
 
 int dccrgx_gol_step(dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t fout, int32_t fcnt)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     const Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -309,11 +311,10 @@ int dccrgx_gol_step(dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t fou
     DX_TRY(dccrgx_halo_start(grid, hood_id, &fin, 1));
     DX_TRY(dccrgx_gol_compute(grid, hood_id, fin, fout, fcnt, DCCRGX_REGION_INNER));
     DX_TRY(dccrgx_halo_wait(grid, hood_id, DCCRGX_WAIT_ALL));
-    // DCCRGX_TEST_CORRUPT_GHOST=1 (tests only): after every exchange, mark the
-    // ghost cell just below the rank's first local cell alive, as a lost or
-    // misplaced halo message would; bench.py's self-check must then fail
-    static const bool corrupt = getenv_flag("DCCRGX_TEST_CORRUPT_GHOST");
-    if (corrupt && grid->uniform && grid->n_local) {
+    // test option corrupt_ghost: after every exchange, mark the ghost cell
+    // just below the rank's first local cell alive, as a lost or misplaced
+    // halo message would; bench.py's self-check must then fail
+    if (test_opt(OPT_CORRUPT_GHOST, 0) && grid->uniform && grid->n_local) {
         const uint64_t slot0 = grid->g.lo + (uint64_t)(-grid->g.cbase * (int64_t)grid->g.S);
         if (slot0 > 0)
             DX_HIP(hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)grid->fields[fin].ptr + slot0 - 1), 1, 1,
@@ -325,6 +326,7 @@ int dccrgx_gol_step(dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t fou
 
 int dccrgx_field_init_hash(dccrgx_grid* grid, int32_t fid, uint32_t permille)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
     DX_CHECK(grid->fields[fid].elem == 4, DCCRGX_EINVAL, "4-byte field expected");
     DX_CHECK(grid->uniform, DCCRGX_EINVAL, "uniform grids only");

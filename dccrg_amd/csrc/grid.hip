@@ -783,6 +783,7 @@ int dccrgx_grid_get_info(const dccrgx_grid* grid, dccrgx_grid_info* out)
 
 int dccrgx_add_neighborhood(dccrgx_grid* grid, int32_t id, const int32_t* items, size_t n)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     // dccrg.hpp:6505-6618
     DX_CHECK(id != DCCRGX_DEFAULT_NEIGHBORHOOD_ID, DCCRGX_EINVAL, "default neighborhood id");
@@ -820,6 +821,7 @@ int dccrgx_add_neighborhood(dccrgx_grid* grid, int32_t id, const int32_t* items,
 
 int dccrgx_remove_neighborhood(dccrgx_grid* grid, int32_t id)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     if (id == DCCRGX_DEFAULT_NEIGHBORHOOD_ID) return DCCRGX_OK;  // dccrg.hpp:6685-6687
     Hood* h = find_hood(grid, id);

@@ -279,6 +279,12 @@ struct Amr {
     StopTxn* pending = nullptr;  // a prepared stop_refining awaiting commit or abort
     ~Amr() { (void)dx_free(d_flags); }
 };
+// a two-phase stop_refining is between prepare and finish: calls that would
+// change or read the fields, neighborhoods or halo plans the prepared rebuild
+// has already moved must wait for dccrgx_stop_refining_finish
+#define DX_NOT_PENDING(grid)                                                                           \
+    DX_CHECK(!((grid) && (grid)->amr && (grid)->amr->pending), DCCRGX_ESTATE,                                      \
+             "a prepared stop_refining awaits dccrgx_stop_refining_finish")
 // amr_dev.hip
 int amr_dev_sync(dccrgx_grid* grid);
 int amr_host_sync(dccrgx_grid* grid);

@@ -482,6 +482,7 @@ extern "C" {
 
 int dccrgx_field_create(dccrgx_grid* grid, uint32_t elem, int32_t* fid)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && fid && elem > 0, DCCRGX_EINVAL, "bad argument");
     DX_HIP(hipSetDevice(grid->ctx->device));
     Field F;
@@ -527,6 +528,7 @@ static uint64_t local_slot0(const dccrgx_grid* grid)
 
 int dccrgx_field_write_local(dccrgx_grid* grid, int32_t fid, const void* host, size_t n)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
     DX_CHECK(!grid->fields[fid].variable, DCCRGX_EINVAL, "variable-size field: use dccrgx_field_write_cells");
     DX_CHECK(n == grid->n_local && (host || !n), DCCRGX_EINVAL, "expected %llu local values",
@@ -588,6 +590,7 @@ int dccrgx_halo_self(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size_
 
 int dccrgx_halo_start(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size_t nf)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     Hood* h = find_hood(grid, hood_id);
     // the reference returns false for unknown ids (dccrg.hpp:5055-5060)
@@ -797,6 +800,7 @@ int dccrgx_halo_unpack_from(dccrgx_grid* grid, int32_t hood_id, const int32_t* f
 
 int dccrgx_field_create_variable(dccrgx_grid* grid, uint32_t elem, int32_t* fid)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && fid && elem > 0, DCCRGX_EINVAL, "bad argument");
     Field F;
     F.elem = elem;
@@ -813,6 +817,7 @@ int dccrgx_field_create_variable(dccrgx_grid* grid, uint32_t elem, int32_t* fid)
 
 int dccrgx_field_resize(dccrgx_grid* grid, int32_t fid, const uint64_t* ids, const uint32_t* counts, size_t n)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
     DX_CHECK((ids && counts) || !n, DCCRGX_EINVAL, "null argument");
     Field& F = grid->fields[fid];
@@ -885,6 +890,7 @@ static int cell_segments(const dccrgx_grid* grid, const Field& F, const uint64_t
 int dccrgx_field_write_cells(dccrgx_grid* grid, int32_t fid, const uint64_t* ids, size_t n, const void* data,
                              size_t bytes)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
     DX_CHECK(ids || !n, DCCRGX_EINVAL, "null argument");
     const Field& F = grid->fields[fid];

@@ -50,9 +50,12 @@ int set_error(int code, const char* fmt, ...);
 // step, tools/api_census.py).  A block freed with ds_free on a stream is
 // reused only by that stream (stream order keeps it safe); blocks freed with
 // dx_free / FreeBatch are reused by any stream once events recorded on every
-// library stream at the free have passed -- no host wait, so a free between a
-// halo's start and wait does not block on the exchange.  Larger blocks go
-// back with hipFree.  The stream-ordered pool (hipMallocAsync) is not used:
+// library stream at the free have passed -- no host wait, so such a free
+// between a halo's start and wait does not block on the exchange.  Blocks
+// over 256 MiB, and cached blocks freed while the cache holds more than its
+// total limit, go back with hipFree, which waits for the whole device: such a
+// free between a halo's start and wait stalls the host until the exchange is
+// done (grids free them only in structural calls).  The stream-ordered pool (hipMallocAsync) is not used:
 // the copy engines keep stale translations for pool memory the pool re-maps,
 // and copies into fresh pool blocks landed in the wrong pages
 // (tools/micro/pool_trim_copy.hip).
@@ -153,18 +156,24 @@ struct PhaseTimer {
     }
 };
 
-// test hooks and tuning knobs read from the environment (DCCRGX_GOL_CHUNK, ...)
-inline bool getenv_flag(const char* name)
-{
-    const char* v = std::getenv(name);
-    return v && *v && *v != '0';
-}
-
-inline int64_t getenv_int(const char* name, int64_t dflt)
-{
-    const char* v = std::getenv(name);
-    return (v && *v) ? std::atoll(v) : dflt;
-}
+// Test options (dccrgx_test_option, core.hip): switches the GPU tests use to
+// force a code path the library otherwise picks by size, and fault injection.
+// Set explicitly through the C-ABI, never read from the environment; all off
+// by default.  A product build may compile them out (-DDCCRGX_NO_TEST_OPTIONS:
+// test_opt() returns its default and dccrgx_test_option refuses).
+enum TestOpt {
+    OPT_GOL_SCALAR,          // LDS-tiled scalar GoL kernels on grids the vector kernels take
+    OPT_GOL_CHUNK,           // slices per workgroup of the GoL kernels (chunk seams in small grids)
+    OPT_POISSON_MULTI,       // the multi-kernel BiCG for systems one workgroup would take
+    OPT_POISSON_SOLO_GLOBAL, // k_solo over global memory instead of k_solo_lds
+    OPT_INCREMENTAL,         // 1 / 0: incremental / full neighbor-list rebuilds at any size
+    OPT_OU_SMALL,            // queue of override_unrefines' small first pass (overflow retries)
+    OPT_CORRUPT_GHOST,       // dccrgx_gol_step marks a ghost cell alive after each exchange
+    OPT_FAIL_STOP_REFINING,  // this rank's next stop_refining decisions report ENOMEM (rank + 1)
+    OPT_CHECK_INIT,          // explicit grids: check the device leaves and lookups against the host list
+    OPT_COUNT
+};
+int64_t test_opt(TestOpt o, int64_t dflt);
 
 // ---------------------------------------------------------------------------
 // host-side parallel loop for structural work that is independent per item

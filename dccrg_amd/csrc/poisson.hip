@@ -1029,6 +1029,7 @@ extern "C" {
 int dccrgx_poisson_create(dccrgx_grid* grid, const dccrgx_poisson_params* prm, const dccrgx_poisson_fields* f,
                           dccrgx_poisson** out)
 {
+    DX_NOT_PENDING(grid);
     DX_CHECK(grid && f && out, DCCRGX_EINVAL, "null argument");
     const int32_t uf[5] = {f->rhs, f->solution, f->length_x, f->length_y, f->length_z};
     for (int32_t id : uf) {
@@ -1077,6 +1078,7 @@ int dccrgx_poisson_solve(dccrgx_poisson* P, const uint64_t* cells, size_t n, con
                          int32_t cache_is_up_to_date, uint32_t* iterations, double* residual_min)
 {
     DX_CHECK(P && (cells || !n) && (skip || !n_skip), DCCRGX_EINVAL, "null argument");
+    DX_NOT_PENDING(P->grid);
     if (!cache_is_up_to_date || !P->cached) DX_TRY(build_cache(P, cells, n, skip, n_skip));
     hipStream_t st = P->grid->ctx->compute;
     const PPtrs p = P->ptrs();
@@ -1090,10 +1092,10 @@ int dccrgx_poisson_solve(dccrgx_poisson* P, const uint64_t* cells, size_t n, con
     PState hs{};
     const Hood* dh = find_hood(P->grid, DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
     const bool solo = !multi_rank(P->grid->ctx) && dh && dh->h_self.empty() && P->n_info <= (1u << 16) &&
-                      !getenv("DCCRGX_POISSON_MULTI");
+                      !test_opt(OPT_POISSON_MULTI, 0);
     if (solo) {
         const dccrgx_poisson_params& q = P->prm;
-        if (P->d_ej && pn == 2.0 && !getenv("DCCRGX_POISSON_SOLO_GLOBAL"))
+        if (P->d_ej && pn == 2.0 && !test_opt(OPT_POISSON_SOLO_GLOBAL, 0))
             hipLaunchKernelGGL(k_solo_lds, dim3(1), dim3(SL), 0, st, p, s, (const int32_t*)P->d_ej, P->d_state,
                                q.stop_residual, q.stop_after_residual_increase, q.min_iterations, q.max_iterations);
         else

@@ -33,6 +33,27 @@ def _dist_ready() -> bool:
         return False
 
 
+def set_test_option(name: str, value=None):
+    """dccrgx_test_option: force a code path or inject a fault (tests only);
+    value None returns the option to its default."""
+    check(lib().dccrgx_test_option(name.encode(), 0 if value is None else int(value), 0 if value is None else 1))
+
+
+class test_option:
+    """with test_option("gol_scalar", 1): ... -- set for the block, then reset."""
+
+    def __init__(self, name: str, value):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        set_test_option(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_test_option(self.name, None)
+        return False
+
+
 def stop_refining_all(grids, all_requests):
     """The collective stop_refining of several ranks held in one process (the
     tests' in-process ranks): every grid prepares, then all commit or, when
@@ -368,14 +389,20 @@ class Dccrg:
             out.append(a)
         return out
 
-    def stop_refining(self, sorted: bool = True, all_requests=None) -> np.ndarray:
+    def stop_refining(self, sorted: bool = True, all_requests=None, agreed: bool = False) -> np.ndarray:
         """Collective (dccrg.hpp:3483-3507).  all_requests: the union over all
         ranks of amr_requests(); gathered with torch.distributed when the
         grid has several ranks and it is not given.  Two phases: every rank
-        prepares its new grid, the statuses are all-reduced (torch.distributed,
-        when initialised), and all ranks adopt or all keep the old grid with
-        the requests pending -- a failure on any rank raises on every rank."""
+        prepares its new grid, the statuses are all-reduced (torch.distributed),
+        and all ranks adopt or all keep the old grid with the requests pending
+        -- a failure on any rank raises on every rank.  With several ranks and
+        no torch.distributed the agreement is impossible and this raises,
+        unless agreed=True: the caller holds every rank (stop_refining_all does
+        the two phases across them) and takes a failure as its own."""
         multi = self.ctx.comm_size > 1
+        if multi and not agreed and not _dist_ready():
+            raise X.DccrgxError(X.DCCRGX_ESTATE, "stop_refining with several ranks needs torch.distributed for the "
+                                                 "ranks' status agreement (or agreed=True, see stop_refining_all)")
         if multi and all_requests is None:
             import torch.distributed as dist
             mine = self.amr_requests()
@@ -386,7 +413,7 @@ class Dccrg:
         st, err = self.stop_refining_prepare(all_requests)
         ok = st == X.DCCRGX_OK
         all_ok = ok
-        if multi and _dist_ready():
+        if multi and not agreed:
             import torch
             import torch.distributed as dist
             t = torch.tensor([1 if ok else 0], dtype=torch.int32)

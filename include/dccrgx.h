@@ -78,6 +78,15 @@ int dccrgx_ctx_comm_init(dccrgx_ctx* ctx, const uint8_t uid[128]);
  * (a peer plan with peer == rank) instead of device copies, so the whole
  * multi-rank halo path runs on a single GPU.  Needs dccrgx_ctx_comm_init. */
 int dccrgx_ctx_route_self_through_rccl(dccrgx_ctx* ctx, int32_t on);
+/* Test options (no reference counterpart): process-wide switches the test
+ * suite uses to force a code path the library otherwise picks by size, and
+ * fault injection; never read from the environment, all off by default.
+ * name: "gol_scalar", "gol_chunk" (slices per workgroup), "poisson_multi",
+ * "poisson_solo_global", "incremental" (1 / 0), "ou_small" (queue entries),
+ * "corrupt_ghost", "fail_stop_refining" (rank + 1), "check_init"; set = 0
+ * returns the option to its default.  DCCRGX_EINVAL for an unknown name, or
+ * in a build compiled with -DDCCRGX_NO_TEST_OPTIONS. */
+int dccrgx_test_option(const char* name, int64_t value, int32_t set);
 /* Host-staged transport for ranks that cannot have an RCCL communicator --
  * several processes sharing one GPU, which RCCL refuses ("Duplicate GPU").
  * With no communicator and a transport set, every halo message of a peer is

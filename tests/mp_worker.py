@@ -28,6 +28,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import dccrg_amd as D  # noqa: E402
+from dccrg_amd.grid import set_test_option  # noqa: E402
 from dccrg_amd.transport import TorchDistTransport  # noqa: E402
 from oracle import dccrg_oracle as O  # noqa: E402
 
@@ -267,14 +268,14 @@ def sc_amr_fail(ctx):
                 assert getattr(g, fn)(c) == want, (fn, c)
         before_local = [int(c) for c in g.local_cells()]
         before_req = [a.tolist() for a in g.amr_requests()]
-        os.environ["DCCRGX_TEST_FAIL_STOP_REFINING"] = str(P - 1)
+        set_test_option("fail_stop_refining", P)  # rank P - 1
         try:
             g.stop_refining()
             raise AssertionError("stop_refining did not fail")
         except D.DccrgxError as e:
             assert ("injected" in str(e)) == (RANK == P - 1), str(e)
         finally:
-            del os.environ["DCCRGX_TEST_FAIL_STOP_REFINING"]
+            set_test_option("fail_stop_refining", None)
         assert [int(c) for c in g.local_cells()] == before_local
         assert [a.tolist() for a in g.amr_requests()] == before_req
         assert np.array_equal(g.read_local("v"), g.local_cells().astype(np.float64))

@@ -64,22 +64,24 @@ def test_window_ids_order():
     assert ids.tolist() == want
 
 
-def _bench(gpus, extra_env=None):
+def _bench(gpus, extra_env=None, n=256, extra_args=()):
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     env.update(extra_env or {})
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--n", "256",
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--n", str(n),
                         "--steps", "2", "--warmup", "1", "--no-secondary", "--no-cpu-baseline",
-                        "--no-halo-payload", "--stall-timeout", "100"],
+                        "--no-halo-payload", "--stall-timeout", "100", *extra_args],
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     return r, lines
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpus", [1, 2, 3])
-def test_bench_self_check_passes(gpus):
-    r, lines = _bench(gpus)
+@pytest.mark.parametrize("gpus,n", [(1, 256), (2, 256), (3, 256), (8, 128)])
+def test_bench_self_check_passes(gpus, n):
+    """8 ranks (the SCALE run's shape: 8 slab seams and the ring wrap) share
+    the one GPU through the host-staged transport."""
+    r, lines = _bench(gpus, n=n)
     assert r.returncode == 0, r.stderr[-3000:]
     (line,) = lines
     c = line["check"]
@@ -90,7 +92,7 @@ def test_bench_self_check_passes(gpus):
 
 @pytest.mark.gpu
 def test_bench_self_check_catches_a_bad_ghost_plane():
-    r, lines = _bench(2, {"DCCRGX_TEST_CORRUPT_GHOST": "1"})
+    r, lines = _bench(2, extra_args=["--test-corrupt-ghost"])
     assert r.returncode != 0
     (line,) = lines
     assert line["check"]["bit_exact"] is False

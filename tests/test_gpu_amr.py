@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 import dccrg_amd as D  # noqa: E402
 from oracle import dccrg_oracle as O  # noqa: E402
 from oracle.dccrg_amr import AmrOracle  # noqa: E402
-from dccrg_amd.grid import stop_refining_all  # noqa: E402
+from dccrg_amd.grid import stop_refining_all, test_option  # noqa: E402
 
 
 def make_ranks(length, M, per, hood, P, leaves=None):
@@ -104,19 +104,17 @@ SEQ_CASES = [  # length, M, periodic, hood, P, rounds, seed
 
 
 @pytest.fixture(params=["full", "incremental", "small_walks"])
-def rebuild_mode(request, monkeypatch):
+def rebuild_mode(request, lib_options):
     """The rebuild's neighbors_of: recomputed for every leaf, or copied for
     rows that reference no removed leaf (explicit.hip nof_incremental; the
-    library picks it above 2^20 leaves, DCCRGX_INCREMENTAL forces it).
+    library picks it above 2^20 leaves, the test option forces it).
     small_walks: override_unrefines' first pass gets a 4-entry queue, so the
     walks overflow into the second, full-size pass (amr_dev.hip k_ou_walk)."""
-    monkeypatch.setenv("DCCRGX_INCREMENTAL", "1" if request.param == "incremental" else "0")
+    lib_options("incremental", 1 if request.param == "incremental" else 0)
     # every rebuild compares the host-merged leaf list with the device's (explicit.hip explicit_init)
-    monkeypatch.setenv("DCCRGX_CHECK_INIT", "1")
+    lib_options("check_init", 1)
     if request.param == "small_walks":
-        monkeypatch.setenv("DCCRGX_OU_SMALL", "4")
-    else:
-        monkeypatch.delenv("DCCRGX_OU_SMALL", raising=False)
+        lib_options("ou_small", 4)
     return request.param
 
 
@@ -260,13 +258,11 @@ def test_two_phase_stop_refining_failure(P, fail_rank, monkeypatch):
                 getattr(o, name)(r, c)
         before = [[int(c) for c in g.local_cells()] for g in grids]
         reqs = [[a.tolist() for a in g.amr_requests()] for g in grids]
-        monkeypatch.setenv("DCCRGX_TEST_FAIL_STOP_REFINING", str(fail_rank))
-        with pytest.raises(D.DccrgxError, match="injected"):
+        with test_option("fail_stop_refining", fail_rank + 1), pytest.raises(D.DccrgxError, match="injected"):
             if P == 1:
                 grids[0].stop_refining()
             else:
                 stop_all(grids)
-        monkeypatch.delenv("DCCRGX_TEST_FAIL_STOP_REFINING")
         for r, g in enumerate(grids):
             assert [int(c) for c in g.local_cells()] == before[r]
             assert [a.tolist() for a in g.amr_requests()] == reqs[r]
@@ -509,7 +505,7 @@ def test_adaptive_advection_multirank(P):
         reqs = [g.amr_requests() for g in grids]
         union = [np.unique(np.concatenate([q[k] for q in reqs])).astype(np.uint64) for k in range(4)]
         for g, geom in zip(grids, geoms):
-            A.finish_adaptation(g, geom, all_requests=union, update=False)
+            A.finish_adaptation(g, geom, all_requests=union, update=False, agreed=True)
         loopback(grids, list(A.ALL))
 
     init_all()
@@ -546,3 +542,49 @@ def test_adaptive_advection_multirank(P):
         assert abs(dt - ref.dt) <= 1e-15 * ref.dt
     for g in grids:
         g.close()
+
+
+@pytest.mark.gpu
+def test_calls_between_prepare_and_finish_are_refused():
+    """while a two-phase stop_refining is prepared (the new fields
+    and neighborhoods are built aside, the data already moved), field creation,
+    field writes, new neighborhoods, halos, stencils and solvers return
+    DCCRGX_ESTATE; finishing then commits the oracle's grid."""
+    import torch
+
+    import dccrg_amd as D
+    from dccrg_amd import _capi as X
+    from oracle.dccrg_amr import AmrOracle
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    length, M, per, hood = (4, 3, 2), 1, (True, False, True), 1
+    o = AmrOracle(length, M, per, hood, 1)
+    ctx = D.Context(0, 0, 1)
+    g = (D.Dccrg().set_initial_length(length).set_maximum_refinement_level(M).set_periodic(*per)
+         .set_neighborhood_length(hood).initialize(ctx))
+    try:
+        for f in ("a", "b", "n"):
+            g.add_field(f, np.uint32)
+        g.write_local("a", np.ones(g.n_local, dtype=np.uint32))
+        for c in (3, 7, 20):
+            assert g.refine_completely(c) == o.refine_completely(0, c)
+        st, err = g.stop_refining_prepare()
+        assert st == X.DCCRGX_OK, err
+        with pytest.raises(D.DccrgxError) as e:
+            g.add_field("late", np.uint32)
+        assert e.value.code == X.DCCRGX_ESTATE
+        for call in (lambda: g.write_local("a", np.zeros(g.n_local, dtype=np.uint32)),
+                     lambda: g.add_neighborhood(7, [[1, 0, 0], [-1, 0, 0]]),
+                     lambda: g.start_remote_neighbor_copy_updates(fields=["a"]),
+                     lambda: g.gol_step("a", "b", "n")):
+            with pytest.raises(D.DccrgxError) as e:
+                call()
+            assert e.value.code == X.DCCRGX_ESTATE
+        g.stop_refining_finish(True)
+        want = o.stop_refining()
+        assert [int(c) for c in g.get_new_cells()] == want[0]
+        assert [int(c) for c in g.local_cells()] == o.cells()
+        g.add_field("late", np.uint32)  # allowed again
+        g.gol_step("a", "b", "n")
+    finally:
+        g.close()
+        ctx.close()

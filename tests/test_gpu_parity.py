@@ -377,14 +377,14 @@ VEC_CASES = [
 @pytest.mark.parametrize("variant", ["vector", "scalar"])
 @pytest.mark.parametrize("chunk", ["0", "1", "3"])
 @pytest.mark.parametrize("length,periodic,P", VEC_CASES)
-def test_gol_kernels_bit_exact(monkeypatch, variant, chunk, length, periodic, P):
+def test_gol_kernels_bit_exact(lib_options, variant, chunk, length, periodic, P):
     """The 26-neighbor stencil kernels the library launches (vector tiles and
     the scalar LDS kernels) against the oracle, including partial slabs, tile
     overhangs and chunk seams (the alternative tilings are checked against the
     vector kernel by tools/gol_sweep.hip)."""
     if variant == "scalar":
-        monkeypatch.setenv("DCCRGX_GOL_SCALAR", "1")
-    monkeypatch.setenv("DCCRGX_GOL_CHUNK", chunk)
+        lib_options("gol_scalar", 1)
+    lib_options("gol_chunk", int(chunk))
     n = int(np.prod(length))
     a0 = O.random_alive(np.arange(1, n + 1, dtype=np.uint64), 350)
     ref_a, ref_n = O.gol_reference_run(length, periodic, 1, a0, 4)
@@ -407,13 +407,13 @@ VEC2D_CASES = [
 @pytest.mark.parametrize("variant", ["vector", "scalar"])
 @pytest.mark.parametrize("chunk", ["0", "3", "11"])
 @pytest.mark.parametrize("length,periodic,P", VEC2D_CASES)
-def test_gol2d_kernels_bit_exact(monkeypatch, variant, chunk, length, periodic, P):
+def test_gol2d_kernels_bit_exact(lib_options, variant, chunk, length, periodic, P):
     """The 2-D (LB == 1) kernels: the vector LDS row kernel and the scalar
     row kernel, over several chunk lengths, partial slabs, strip overhangs and
     periodic wraps."""
     if variant == "scalar":
-        monkeypatch.setenv("DCCRGX_GOL_SCALAR", "1")
-    monkeypatch.setenv("DCCRGX_GOL_CHUNK", chunk)
+        lib_options("gol_scalar", 1)
+    lib_options("gol_chunk", int(chunk))
     n = int(np.prod(length))
     a0 = O.random_alive(np.arange(1, n + 1, dtype=np.uint64), 350)
     ref_a, ref_n = O.gol_reference_run(length, periodic, 1, a0, 4)

@@ -19,19 +19,17 @@ TOL = 1e-12
 
 
 @pytest.fixture(params=["solo", "solo_global", "multi", "rccl"])
-def path(request, monkeypatch):
+def path(request, monkeypatch, lib_options):
     """Every iteration driver: one workgroup for small single-rank systems
     (LDS-resident up to 1024 cells with the 2-norm, else over global memory),
     the batched multi-kernel path used across ranks, and that path through a
     real RCCL communicator (ncclAllReduce of every scalar, periodic images
     as RCCL messages to the rank itself)."""
-    monkeypatch.delenv("DCCRGX_POISSON_MULTI", raising=False)
     monkeypatch.delenv("DCCRGX_TEST_RCCL", raising=False)
-    monkeypatch.delenv("DCCRGX_POISSON_SOLO_GLOBAL", raising=False)
     if request.param == "solo_global":
-        monkeypatch.setenv("DCCRGX_POISSON_SOLO_GLOBAL", "1")
+        lib_options("poisson_solo_global", 1)
     elif request.param == "multi":
-        monkeypatch.setenv("DCCRGX_POISSON_MULTI", "1")
+        lib_options("poisson_multi", 1)
     elif request.param == "rccl":
         monkeypatch.setenv("DCCRGX_TEST_RCCL", "1")
     return request.param

@@ -89,12 +89,12 @@ def test_device_matches_reference_solver(tmp_path, n, M, steps, adapt_n):
 
 @pytest.mark.skipif(not os.path.exists(BIN), reason="oracle/_ref/ref_advection is built where /root/reference is")
 @pytest.mark.parametrize("n,M,steps,adapt_n", [(20, 2, 12, 1), (64, 2, 24, 1), (400, 2, 8, 1)])
-def test_incremental_rebuild_matches_reference_solver(tmp_path, monkeypatch, n, M, steps, adapt_n):
+def test_incremental_rebuild_matches_reference_solver(tmp_path, lib_options, n, M, steps, adapt_n):
     """The same runs with the incremental rebuild forced (the library picks it
     above 2^20 leaves): neighbors_of rows and, on one rank, the stencil rows
     the face lists come from are copied for untouched leaves and remapped
     (explicit.hip nof_incremental, k_st_inc_fill)."""
-    monkeypatch.setenv("DCCRGX_INCREMENTAL", "1")
+    lib_options("incremental", 1)
     ref = reference_run(n, M, steps, adapt_n, str(tmp_path / "ref.bin"))
     dev = device_run(n, M, steps, adapt_n)
     assert len(ref) == len(dev) == steps + 1

@@ -6,8 +6,8 @@
 #   tests[=PYTEST_ARGS]  pytest -m gpu (default: the whole GPU suite) -> TAG/tests.log
 #   smoke                __graft_entry__.smoke()                     -> TAG/smoke.log
 #   bench                bench.py --steps 20 --warmup 3               -> TAG/bench.log
-#   prof                 rocprofv3 --kernel-trace --stats of bench.py -> TAG/prof/
-#   pmc                  FETCH_SIZE / WRITE_SIZE passes of bench.py   -> TAG/pmc_*/
+#   prof                 rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE passes of the
+#                        headline (summarize: python tools/summarize_prof.py TAG/prof ...)
 #   us                   tools/user_stencil_bench.py (+ --stats)      -> TAG/us.log, TAG/us_prof/
 #   uspmc                FETCH/WRITE + SQ passes of the user stencil  -> TAG/uspmc_*/
 #   adapt / adaptbig     tools/adapt_loop.py at 218k / 3.5 M leaves   -> TAG/adapt*.log
@@ -31,11 +31,12 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py --steps 20 --warmup 3 > $out/bench.log 2>&1 || fail bench $? $out/bench.log
       tail -n 1 $out/bench.log | cut -c1-600 ;;
     prof)
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python3 bench.py --steps 20 --warmup 3 > $out/prof.log 2>&1 || fail prof $? $out/prof.log ;;
-    pmc)
-      for c in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $out/pmc_$c -o run -- python3 bench.py --steps 5 --warmup 1 --no-secondary > $out/pmc_$c.log 2>&1 || fail pmc_$c $? $out/pmc_$c.log
-      done ;;
+      # kernel trace + stats, then FETCH_SIZE / WRITE_SIZE in passes of their own
+      # (the layout tools/summarize_prof.py reads: prof/trace, prof/fetch, prof/write)
+      q="--no-secondary --no-halo-payload --no-cpu-baseline --no-check"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof/trace -o run -- python3 bench.py --steps 5 --warmup 1 $q > $out/prof_trace.log 2>&1 || fail prof_trace $? $out/prof_trace.log
+      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $out/prof/fetch -o run -- python3 bench.py --steps 3 --warmup 1 $q > $out/prof_fetch.log 2>&1 || fail prof_fetch $? $out/prof_fetch.log
+      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $out/prof/write -o run -- python3 bench.py --steps 3 --warmup 1 $q > $out/prof_write.log 2>&1 || fail prof_write $? $out/prof_write.log ;;
     us)
       timeout -k 10 300 python -u tools/user_stencil_bench.py > $out/us.log 2>&1 || fail us $? $out/us.log
       cat $out/us.log | cut -c1-1500

@@ -14,14 +14,13 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import dccrg_amd as D  # noqa: E402
 import test_gpu_poisson as T  # noqa: E402
 
+from dccrg_amd.grid import set_test_option  # noqa: E402
+
 for path in ("solo", "solo_global", "multi", "rccl"):
-    for k in ("DCCRGX_POISSON_MULTI", "DCCRGX_TEST_RCCL", "DCCRGX_POISSON_SOLO_GLOBAL"):
-        os.environ.pop(k, None)
-    if path == "solo_global":
-        os.environ["DCCRGX_POISSON_SOLO_GLOBAL"] = "1"
-    elif path == "multi":
-        os.environ["DCCRGX_POISSON_MULTI"] = "1"
-    elif path == "rccl":
+    os.environ.pop("DCCRGX_TEST_RCCL", None)
+    set_test_option("poisson_solo_global", 1 if path == "solo_global" else None)
+    set_test_option("poisson_multi", 1 if path == "multi" else None)
+    if path == "rccl":
         os.environ["DCCRGX_TEST_RCCL"] = "1"
     for name in sorted(T.CASES):
         g, sysm, cells, rhs, guess, solve, skip = T.build(name)
