@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces(AdvPtrs p, double 
 {
 #pragma clang fp contract(off)
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    for (size_t i = (size_t)xcd_block() * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint32_t q = pos ? pos[i] : (uint32_t)i;
         const uint32_t c = local_g ? local_g[q] : q;  // null: identity (explicit local slots are [0, n_local))
         uint32_t s[6];
@@ -235,7 +235,9 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, dou
                                  rv2 = adv_rsrc(p.v[2]), rf = adv_rsrc(p.flux);
     const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(fc.ell_slot), 0, 0x7fffffff,
                                                                         0x00020000);
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    // XCD-contiguous cells: a cell's neighbors one level-row away were loaded
+    // into the same XCD's L2 by the blocks just before it
+    for (size_t i = (size_t)xcd_block() * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint32_t q = pos ? pos[i] : (uint32_t)i;
         const uint32_t c = q;  // explicit local slots are [0, n_local)
         uint32_t s[6];

@@ -228,6 +228,18 @@ inline Divider make_divider(uint64_t d)
     return r;
 }
 
+#ifdef __HIPCC__
+// XCD-aware block order: the dispatcher deals workgroups round-robin over the
+// 8 XCDs (block b runs on XCD b % 8); this bijection gives each XCD a
+// contiguous run of blocks, so work that reads its neighbors' lines (rows of
+// a grid, a stencil's apron) finds them in its own L2
+__device__ inline uint32_t xcd_block()
+{
+    const uint32_t bid = blockIdx.x, nwg = gridDim.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+#endif
+
 __host__ __device__ inline uint64_t mulhi64(uint64_t a, uint64_t b)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
