@@ -501,17 +501,23 @@ static int check_explicit_memory(const dccrgx_grid* grid, uint64_t N)
     return DCCRGX_OK;
 }
 
-// refinement requests need the explicit form (neighbor lists of every leaf on
-// the host); a uniform grid is converted on its first request
+// refinement requests need the explicit form (neighbor lists of the local
+// leaves, the leaf list replicated); a uniform grid is converted on its first
+// request.  The memory check refuses long before the 32-bit leaf indices
+// would: the lists of the 26-cell neighborhood take ~1.2 kB per local cell, so
+// 288 GB hold about 2.4e8 cells ("Mixed-level grids")
 int ensure_explicit(dccrgx_grid* grid)
 {
     if (!grid->uniform) return DCCRGX_OK;
     const uint64_t N = grid->g.N;
+    DX_TRY(check_explicit_memory(grid, N));
     DX_CHECK(N < (1ull << 32), DCCRGX_EINVAL, "grid of %llu cells is too large to refine",
              (unsigned long long)N);
-    DX_TRY(check_explicit_memory(grid, N));
     std::vector<uint64_t> leaves(N);
-    for (uint64_t i = 0; i < N; i++) leaves[i] = i + 1;
+    uint64_t* lv = leaves.data();
+    parallel_ranges(N, 1u << 20, [lv](size_t b, size_t e) {
+        for (size_t i = b; i < e; i++) lv[i] = i + 1;
+    });
     return rebuild(grid, leaves, {});
 }
 

@@ -34,15 +34,27 @@ unsigned blocks_for(uint64_t n)
     return (unsigned)(b < 8192 ? (b ? b : 1) : 8192);
 }
 
+// the leaf index held by each slot of a leaf (local and ghost slots)
+__global__ void __launch_bounds__(256) k_slot_leaf(const uint32_t* __restrict__ slot_of_g, uint64_t n,
+                                                   uint32_t* __restrict__ slot_g)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += stride) {
+        const uint32_t s = slot_of_g[g];
+        if (s != NO_SLOT) slot_g[s] = (uint32_t)g;
+    }
+}
+
 // one thread per local cell: its stencil row, entries that are not in the
 // cell's neighbors_to row first, both groups in row order (ascending (id,
-// offset)); membership by slot (one slot per id)
+// offset)).  Both rows ascend by leaf index (ids ascend with it), so
+// membership is one merge: O(row + neighbors_to row) per cell.
 __global__ void __launch_bounds__(256) k_iter_rows(const uint64_t* __restrict__ st_row,
                                                    const uint32_t* __restrict__ st_slot,
                                                    const int32_t* __restrict__ st_off,
                                                    const uint64_t* __restrict__ nto_row,
                                                    const uint32_t* __restrict__ nto_g,
-                                                   const uint32_t* __restrict__ slot_of_g, uint64_t nl,
+                                                   const uint32_t* __restrict__ slot_g, uint64_t nl,
                                                    uint32_t* __restrict__ it_slot, int32_t* __restrict__ it_off)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -50,10 +62,10 @@ __global__ void __launch_bounds__(256) k_iter_rows(const uint64_t* __restrict__ 
         const uint64_t e0 = st_row[i], e1 = st_row[i + 1], t0 = nto_row[i], t1 = nto_row[i + 1];
         uint64_t w = e0;
         for (int both = 0; both < 2; both++)
-            for (uint64_t e = e0; e < e1; e++) {
-                const uint32_t s = st_slot[e];
-                bool in_to = false;
-                for (uint64_t t = t0; t < t1 && !in_to; t++) in_to = slot_of_g[nto_g[t]] == s;
+            for (uint64_t e = e0, t = t0; e < e1; e++) {
+                const uint32_t s = st_slot[e], ge = slot_g[s];
+                while (t < t1 && nto_g[t] < ge) t++;
+                const bool in_to = t < t1 && nto_g[t] == ge;
                 if (in_to != (both != 0)) continue;
                 it_slot[w] = s;
                 it_off[3 * w] = st_off[3 * e];
@@ -134,10 +146,15 @@ int build_iter(const dccrgx_grid* grid, Hood& h, hipStream_t st)
         DX_HIP(dx_malloc(&ic->slot, cap * 4));
         DX_HIP(dx_malloc(&ic->off, cap * 12));
         if (nl) {
+            uint32_t* slot_g = nullptr;
+            DX_HIP(ds_malloc(&slot_g, std::max<uint64_t>(grid->n_slots, 1) * 4, st));
+            hipLaunchKernelGGL(k_slot_leaf, dim3(blocks_for(E->n)), dim3(256), 0, st, (const uint32_t*)E->d_slot_of_g,
+                               (uint64_t)E->n, slot_g);
             hipLaunchKernelGGL(k_iter_rows, dim3(blocks_for(nl)), dim3(256), 0, st, (const uint64_t*)h.d_st_row,
                                (const uint32_t*)h.d_st_slot, (const int32_t*)h.d_st_off, (const uint64_t*)h.d_nto_row,
-                               (const uint32_t*)h.d_nto_g, (const uint32_t*)E->d_slot_of_g, nl, ic->slot, ic->off);
+                               (const uint32_t*)h.d_nto_g, (const uint32_t*)slot_g, nl, ic->slot, ic->off);
             DX_HIP(hipGetLastError());
+            ds_free(slot_g, st);
         }
     }
     h.iter = ic;
