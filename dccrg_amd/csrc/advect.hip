@@ -16,8 +16,6 @@
 #include <cfloat>
 #include <cstring>
 
-#include <hipcub/hipcub.hpp>
-
 #include "grid.hpp"
 
 namespace dccrgx {
@@ -597,59 +595,6 @@ void uniform_local_run(const dccrgx_grid* grid, uint64_t* s0, uint64_t* n)
 }
 
 
-__device__ inline uint64_t spread3(uint64_t v)  // 21 bits -> every third bit
-{
-    v &= 0x1fffffull;
-    v = (v | v << 32) & 0x1f00000000ffffull;
-    v = (v | v << 16) & 0x1f0000ff0000ffull;
-    v = (v | v << 8) & 0x100f00f00f00f00full;
-    v = (v | v << 4) & 0x10c30c30c30c30c3ull;
-    v = (v | v << 2) & 0x1249249249249249ull;
-    return v;
-}
-
-// Morton key of each local cell's min corner (finest-level indices)
-__global__ void __launch_bounds__(256) k_morton_keys(MapParams mp, const uint64_t* __restrict__ leaves,
-                                                     const uint32_t* __restrict__ local_g, uint64_t n,
-                                                     uint64_t* __restrict__ keys, uint32_t* __restrict__ vals)
-{
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
-        uint64_t idx[3];
-        map_indices(mp, leaves[local_g[q]], idx, nullptr);
-        keys[q] = spread3(idx[0]) | spread3(idx[1]) << 1 | spread3(idx[2]) << 2;
-        vals[q] = (uint32_t)q;
-    }
-}
-
-constexpr uint64_t ADV_ORDER_MIN = 1u << 20;  // below: launch-bound, the order does not pay for its sort
-
-int build_order(const dccrgx_grid* grid, FaceCache& fc, uint64_t n, hipStream_t st)
-{
-    const MapParams& mp = grid->map;
-    const int64_t forced = test_opt(OPT_ADV_ORDER, -1);
-    if (forced == 0 || (forced < 0 && n < ADV_ORDER_MIN)) return DCCRGX_OK;
-    int bits = 0;  // finest-level index bits in use (21 per axis fit a 64-bit key)
-    for (int d = 0; d < 3; d++)
-        while (bits < 64 && (mp.length[d] << mp.max_lvl) > (1ull << bits)) bits++;
-    if (bits > 21 || n >= (1ull << 31)) return DCCRGX_OK;
-    const Explicit* E = grid->ex;
-    uint64_t *k0 = nullptr, *k1 = nullptr;
-    uint32_t* v0 = nullptr;
-    void* tmp = nullptr;
-    size_t tb = 0;
-    DX_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v0, (int)n, 0, 3 * bits, st));
-    DX_HIP(ds_malloc(&k0, n * 8, st));
-    DX_HIP(ds_malloc(&k1, n * 8, st));
-    DX_HIP(ds_malloc(&v0, n * 4, st));
-    DX_HIP(ds_malloc(&tmp, std::max<size_t>(tb, 1), st));
-    DX_HIP(dx_malloc(&fc.order, n * 4));
-    hipLaunchKernelGGL(k_morton_keys, dim3(grid_for(n)), dim3(256), 0, st, mp, E->d_leaves, E->d_local_g, n, k0, v0);
-    DX_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, fc.order, (int)n, 0, 3 * bits, st));
-    for (void* q : {(void*)k0, (void*)k1, (void*)v0, tmp}) ds_free(q, st);
-    return DCCRGX_OK;
-}
-
 // build the face lists of a neighborhood's local cells (explicit grids):
 // one pass, no synchronisation
 int build_faces(const dccrgx_grid* grid, Hood& h)
@@ -673,7 +618,6 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
         hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
                            R.local_slot, R.level, M, n, fc->ell_slot, fc->o_cnt, fc->o_slot, fc->o_dir, fc->d_over);
     DX_HIP(hipGetLastError());
-    DX_TRY(build_order(grid, *fc, n, st));
     h.faces = fc;  // the lists are written in stream order before the kernels that read them
     return DCCRGX_OK;
 }
@@ -695,7 +639,7 @@ int advect_launch(dccrgx_grid* grid, Hood& h, const AdvPtrs& p, double dt, int32
         const FaceCache& F = *h.faces;
         const FaceView fv{F.n, F.ell_slot, F.o_base, F.o_cnt, F.o_slot, F.o_dir, F.d_over};
         // explicit grids store local cell q in slot q (explicit.hip): no slot loads
-        const uint32_t* rpos = region == DCCRGX_REGION_ALL ? (const uint32_t*)F.order : R.pos;
+        const uint32_t* rpos = region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos;
         if (grid->n_slots < (1ull << 28) && 6 * F.n < (1ull << 29)) {  // buffer loads: byte offsets below 2 GiB
             hipLaunchKernelGGL(k_ex_advect_faces_buf<1>, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv, rpos, R.n,
                                rho_out, t0, t1);
@@ -760,8 +704,7 @@ int density_spare(dccrgx_grid* grid, double** out, size_t* bytes)
 FaceCache::~FaceCache()
 {
     FreeBatch fb;
-    for (void* q : {(void*)ell_slot, (void*)o_cnt, (void*)o_slot, (void*)o_dir, (void*)d_over, (void*)order})
-        fb.add(q);
+    for (void* q : {(void*)ell_slot, (void*)o_cnt, (void*)o_slot, (void*)o_dir, (void*)d_over}) fb.add(q);
 }
 
 }  // namespace dccrgx

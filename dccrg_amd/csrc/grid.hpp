@@ -320,12 +320,6 @@ struct FaceCache {
     uint32_t* o_slot = nullptr;
     int8_t* o_dir = nullptr;
     uint32_t* d_over = nullptr;    // device flag: some cell has overflow
-    // the local positions in the Morton order of the cells' min corners
-    // (finest-level indices): the solver visits every level of a region
-    // together, so a cell's coarser / finer face neighbors, which sit in
-    // another level's id block, are gathered while their lines are in L2;
-    // null below ADV_ORDER_MIN cells
-    uint32_t* order = nullptr;
     ~FaceCache();
 };
 

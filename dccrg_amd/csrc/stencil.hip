@@ -45,34 +45,76 @@ __global__ void __launch_bounds__(256) k_slot_leaf(const uint32_t* __restrict__ 
     }
 }
 
-// one thread per local cell: its stencil row, entries that are not in the
+// one wave per local cell: its stencil row, entries that are not in the
 // cell's neighbors_to row first, both groups in row order (ascending (id,
-// offset)).  Both rows ascend by leaf index (ids ascend with it), so
-// membership is one merge: O(row + neighbors_to row) per cell.
-__global__ void __launch_bounds__(256) k_iter_rows(const uint64_t* __restrict__ st_row,
-                                                   const uint32_t* __restrict__ st_slot,
-                                                   const int32_t* __restrict__ st_off,
-                                                   const uint64_t* __restrict__ nto_row,
-                                                   const uint32_t* __restrict__ nto_g,
-                                                   const uint32_t* __restrict__ slot_g, uint64_t nl,
-                                                   uint32_t* __restrict__ it_slot, int32_t* __restrict__ it_off)
+// offset)).  Both rows ascend by leaf index (ids ascend with it); the
+// neighbors_to row goes to LDS (up to NTO_LDS entries, else it is searched in
+// place), each lane takes one entry of a 64-entry chunk and finds its leaf
+// there by binary search, and the wave's ballots place the entries: a count
+// pass, then a write pass.  Reads and writes of a chunk are coalesced.
+// (Per-entry group flags instead of the copy made this 2.4x faster and the
+// walks over the view 2x slower: profiles/r5g_iter_view_time_groupflags.log.)
+constexpr int ITER_WAVES = 4, NTO_LDS = 1024;
+
+__device__ inline bool in_sorted(const uint32_t* a, uint32_t n, uint32_t x)
 {
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (a[m] < x) lo = m + 1;
+        else hi = m;
+    }
+    return lo < n && a[lo] == x;
+}
+
+__global__ void __launch_bounds__(64 * ITER_WAVES) k_iter_rows(const uint64_t* __restrict__ st_row,
+                                                               const uint32_t* __restrict__ st_slot,
+                                                               const int32_t* __restrict__ st_off,
+                                                               const uint64_t* __restrict__ nto_row,
+                                                               const uint32_t* __restrict__ nto_g,
+                                                               const uint32_t* __restrict__ slot_g, uint64_t nl,
+                                                               uint32_t* __restrict__ it_slot,
+                                                               int32_t* __restrict__ it_off)
+{
+    __shared__ uint32_t lds[ITER_WAVES][NTO_LDS];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t* L = lds[w];
+    for (uint64_t i = (uint64_t)blockIdx.x * ITER_WAVES + w; i < nl; i += (uint64_t)gridDim.x * ITER_WAVES) {
         const uint64_t e0 = st_row[i], e1 = st_row[i + 1], t0 = nto_row[i], t1 = nto_row[i + 1];
-        uint64_t w = e0;
-        for (int both = 0; both < 2; both++)
-            for (uint64_t e = e0, t = t0; e < e1; e++) {
-                const uint32_t s = st_slot[e], ge = slot_g[s];
-                while (t < t1 && nto_g[t] < ge) t++;
-                const bool in_to = t < t1 && nto_g[t] == ge;
-                if (in_to != (both != 0)) continue;
-                it_slot[w] = s;
-                it_off[3 * w] = st_off[3 * e];
-                it_off[3 * w + 1] = st_off[3 * e + 1];
-                it_off[3 * w + 2] = st_off[3 * e + 2];
-                w++;
+        const uint32_t nt = (uint32_t)(t1 - t0);
+        const bool local = nt <= NTO_LDS;
+        if (local)
+            for (uint32_t k = lane; k < nt; k += 64) L[k] = nto_g[t0 + k];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const uint32_t* T = local ? L : nto_g + t0;
+        auto member = [&](uint64_t e) { return in_sorted(T, nt, slot_g[st_slot[e]]); };
+        // count pass: entries not in the neighbors_to row
+        uint32_t n_out = 0;
+        for (uint64_t c = e0; c < e1; c += 64) {
+            const uint64_t e = c + lane;
+            const bool out = e < e1 && !member(e);
+            n_out += (uint32_t)__popcll(__ballot(out));
+        }
+        // write pass
+        uint64_t w0 = e0, w1 = e0 + n_out;
+        for (uint64_t c = e0; c < e1; c += 64) {
+            const uint64_t e = c + lane;
+            const bool valid = e < e1;
+            const bool in = valid && member(e);
+            const uint64_t m_out = __ballot(valid && !in), m_in = __ballot(in);
+            const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+            if (valid) {
+                const uint64_t d = in ? w1 + __popcll(m_in & below) : w0 + __popcll(m_out & below);
+                it_slot[d] = st_slot[e];
+                it_off[3 * d] = st_off[3 * e];
+                it_off[3 * d + 1] = st_off[3 * e + 1];
+                it_off[3 * d + 2] = st_off[3 * e + 2];
             }
+            w0 += __popcll(m_out);
+            w1 += __popcll(m_in);
+        }
+        __builtin_amdgcn_wave_barrier();  // L is rewritten for the next row
     }
 }
 
@@ -150,7 +192,8 @@ int build_iter(const dccrgx_grid* grid, Hood& h, hipStream_t st)
             DX_HIP(ds_malloc(&slot_g, std::max<uint64_t>(grid->n_slots, 1) * 4, st));
             hipLaunchKernelGGL(k_slot_leaf, dim3(blocks_for(E->n)), dim3(256), 0, st, (const uint32_t*)E->d_slot_of_g,
                                (uint64_t)E->n, slot_g);
-            hipLaunchKernelGGL(k_iter_rows, dim3(blocks_for(nl)), dim3(256), 0, st, (const uint64_t*)h.d_st_row,
+            const unsigned nb = (unsigned)std::min<uint64_t>((nl + ITER_WAVES - 1) / ITER_WAVES, 16384);
+            hipLaunchKernelGGL(k_iter_rows, dim3(nb), dim3(64 * ITER_WAVES), 0, st, (const uint64_t*)h.d_st_row,
                                (const uint32_t*)h.d_st_slot, (const int32_t*)h.d_st_off, (const uint64_t*)h.d_nto_row,
                                (const uint32_t*)h.d_nto_g, (const uint32_t*)slot_g, nl, ic->slot, ic->off);
             DX_HIP(hipGetLastError());

@@ -56,14 +56,9 @@ def exchange(grids, fields, uniform):
         loopback(grids, list(fields))
 
 
-@pytest.mark.parametrize("order", [None, 1])
 @pytest.mark.parametrize("P", [1, 3])
 @pytest.mark.parametrize("case", CASES)
-def test_advection_parity(case, P, order, lib_options):
-    """order 1: the explicit-grid kernels visit the cells in the Morton order
-    of their min corners (the library does so above 2^20 leaves)."""
-    if order is not None:
-        lib_options("adv_order", order)
+def test_advection_parity(case, P):
     uniform = case[4] is None
     lists, grids = build(case, P)
     state = O.advection_initial_state(O.Mapping(case[0], case[1]), lists.cells)

@@ -11,7 +11,8 @@
 #   us                   tools/user_stencil_bench.py (+ --stats)      -> TAG/us.log, TAG/us_prof/
 #   uspmc                FETCH/WRITE + SQ passes of the user stencil  -> TAG/uspmc_*/
 #   adapt / adaptbig     tools/adapt_loop.py at 218k / 3.5 M leaves   -> TAG/adapt*.log
-#   advlarge             tools/run_adv_large.py (+ --stats)           -> TAG/adv_large.log
+#   advlarge             tools/run_adv_large.py                        -> TAG/adv_large.log
+#   adapttrace           3.5 M-leaf adaptive loop: phases, trace, idle gaps -> TAG/adapt_*
 #   py=SCRIPT            python -u SCRIPT                              -> TAG/<script>.log
 set -o pipefail
 tag=$1; shift
@@ -53,6 +54,13 @@ for step in "$@"; do
     adaptbig)
       ADAPT_N=1600 ADAPT_REL=0.006 timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_3p5M.log 2>&1 || fail adaptbig $? $out/adapt_3p5M.log
       tail -n 2 $out/adapt_3p5M.log ;;
+    adapttrace)
+      # the 3.5 M-leaf adaptive loop: library phase timers, then a kernel +
+      # HIP-runtime trace (no counters) and its device-idle report
+      ADAPT_N=1600 ADAPT_REL=0.006 DCCRGX_TIMING=1 timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_big_phases.log 2>&1 || fail adapt_phases $? $out/adapt_big_phases.log
+      tail -n 2 $out/adapt_big_phases.log
+      ADAPT_N=1600 ADAPT_REL=0.006 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $out/adapt_trace -o run -- python3 tools/adapt_loop.py > $out/adapt_trace.log 2>&1 || fail adapt_trace $? $out/adapt_trace.log
+      python3 tools/idle_gaps.py $out/adapt_trace > $out/adapt_gaps.txt 2>&1; tail -n 25 $out/adapt_gaps.txt ;;
     advlarge)
       timeout -k 10 300 python -u tools/run_adv_large.py > $out/adv_large.log 2>&1 || fail advlarge $? $out/adv_large.log
       tail -n 3 $out/adv_large.log ;;
