@@ -16,6 +16,7 @@
 #include <cfloat>
 #include <cstring>
 
+#include "exview.hpp"
 #include "grid.hpp"
 
 namespace dccrgx {
@@ -330,37 +331,6 @@ __global__ void __launch_bounds__(256) k_adapt_marks(const unsigned long long* _
     }
 }
 
-// the 8 siblings of every local cell (dccrg_mapping.hpp:450-471: the
-// parent's children, x fastest; a level-0 cell is its own only sibling)
-__global__ void __launch_bounds__(256) k_sibling_ids(MapParams mp, const uint64_t* __restrict__ leaves,
-                                                     const uint32_t* __restrict__ local_g, uint64_t n,
-                                                     uint64_t* __restrict__ sib, int8_t* __restrict__ lvl_out)
-{
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
-        const uint64_t c = leaves[local_g[q]];
-        uint64_t idx[3];
-        int l = 0;
-        map_indices(mp, c, idx, &l);
-        lvl_out[q] = (int8_t)l;
-        if (l == 0) {
-            sib[8 * q] = c;
-            for (int k = 1; k < 8; k++) sib[8 * q + k] = 0;
-            continue;
-        }
-        const uint64_t h = (uint64_t)1 << (mp.max_lvl - l);
-        uint64_t p[3];
-        for (int d = 0; d < 3; d++) p[d] = idx[d] - idx[d] % (2 * h);
-        int k = 0;
-        for (int dz = 0; dz < 2; dz++)
-            for (int dy = 0; dy < 2; dy++)
-                for (int dx = 0; dx < 2; dx++) {
-                    const uint64_t ci[3] = {p[0] + dx * h, p[1] + dy * h, p[2] + dz * h};
-                    sib[8 * q + k++] = map_cell(mp, ci, l);
-                }
-    }
-}
-
 // adapter.hpp:109-176 per sibling group.  The reference's loop inserts and
 // erases while it walks the local cells; its outcome per group is: refine
 // every cell marked 2; if any sibling is marked 2 nothing else; else keep
@@ -370,22 +340,36 @@ __global__ void __launch_bounds__(256) k_sibling_ids(MapParams mp, const uint64_
 // never kept or unrefined (:152, :173).  Local positions are in ascending id
 // order and siblings are local (same level-0 ancestor), so "first" is the
 // smallest position.  Codes: 0 none, 1 refine, 2 dont_unrefine, 3 unrefine.
-__global__ void __launch_bounds__(256) k_adapt_codes(const int8_t* __restrict__ marks,
-                                                     const int64_t* __restrict__ sib_pos,
-                                                     const int8_t* __restrict__ lvl, uint64_t n,
+// The siblings (dccrg_mapping.hpp:450-471: the parent's children, x fastest)
+// are looked up in the leaf bitmap / hash directly; a sibling that is not a
+// leaf (refined) or not local takes no part.
+__global__ void __launch_bounds__(256) k_adapt_codes(ExView v, const uint64_t* __restrict__ leaves,
+                                                     const uint32_t* __restrict__ slot_of_g,
+                                                     const uint32_t* __restrict__ local_g,
+                                                     const int8_t* __restrict__ marks, uint64_t n,
                                                      uint8_t* __restrict__ code)
 {
+    const MapParams& mp = v.mp;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
         const int m = marks[q];
-        if (lvl[q] == 0) {
+        const uint64_t c = leaves[local_g[q]];
+        uint64_t idx[3];
+        int l = 0;
+        map_indices(mp, c, idx, &l);
+        if (l == 0) {
             code[q] = m == 2 ? 1 : 0;
             continue;
         }
+        const uint64_t h = (uint64_t)1 << (mp.max_lvl - l);
+        uint64_t p[3];
+        for (int d = 0; d < 3; d++) p[d] = idx[d] - idx[d] % (2 * h);
         bool g_ref = false, g_keep = false, earlier_keep = false;
         for (int k = 0; k < 8; k++) {
-            const int64_t s = sib_pos[8 * q + k];
-            if (s < 0 || (uint64_t)s >= n) continue;  // refined sibling (not a leaf)
+            const uint64_t ci[3] = {p[0] + (k & 1) * h, p[1] + ((k >> 1) & 1) * h, p[2] + ((k >> 2) & 1) * h};
+            const int64_t g = ex_find(v, map_cell(mp, ci, l));
+            const uint32_t s = g < 0 ? NO_SLOT : slot_of_g[g];
+            if (s >= n) continue;  // refined sibling (not a leaf), or not local
             const int ms = marks[s];
             g_ref |= ms == 2;
             g_keep |= ms == 1;
@@ -741,7 +725,7 @@ int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f)
     else {
         // local cell q lives in slot q on explicit grids (explicit.hip)
         s0 = 0;
-        n = grid->ex->local.size();
+        n = grid->ex->n_local();
     }
     hipLaunchKernelGGL(k_apply_slots, dim3(grid_for(n)), dim3(256), 0, st, (double*)p.rho, p.flux, s0, n, slots);
     DX_HIP(hipGetLastError());
@@ -861,32 +845,27 @@ int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccr
     DX_CHECK(cap >= n, DCCRGX_ERANGE, "capacity %zu < %llu local cells", cap, (unsigned long long)n);
     DX_CHECK((to_refine && not_to_unrefine && to_unrefine) || !n, DCCRGX_EINVAL, "null output");
     int8_t* d_marks = nullptr;
+    PhaseTimer T("adaptation_sets");
     DX_TRY(adapt_marks_device(grid, hood_id, f, diff_increase, diff_threshold, unrefine_sensitivity, &d_marks,
                               nullptr));
     if (!d_marks) return DCCRGX_OK;
+    T.lap("marks");
     hipStream_t st = grid->ctx->compute;
     const Explicit* E = grid->ex;
-    uint64_t* d_sib = nullptr;
-    int64_t* d_pos = nullptr;
-    int8_t* d_lvl = nullptr;
     uint8_t* d_code = nullptr;
     int s = DCCRGX_OK;
-    if (dx_malloc(&d_sib, n * 64) != hipSuccess || dx_malloc(&d_pos, n * 64) != hipSuccess ||
-        dx_malloc(&d_lvl, n) != hipSuccess || dx_malloc(&d_code, n) != hipSuccess)
-        s = set_error(DCCRGX_ENOMEM, "out of device memory for the adaptation sets");
+    if (dx_malloc(&d_code, n) != hipSuccess) s = set_error(DCCRGX_ENOMEM, "out of device memory for the adaptation sets");
     if (s == DCCRGX_OK) {
-        hipLaunchKernelGGL(k_sibling_ids, dim3(grid_for(n)), dim3(256), 0, st, grid->map, E->d_leaves, E->d_local_g,
-                           n, d_sib, d_lvl);
-        s = explicit_slots_of(grid, d_sib, 8 * n, d_pos, st);
-    }
-    if (s == DCCRGX_OK) {
-        hipLaunchKernelGGL(k_adapt_codes, dim3(grid_for(n)), dim3(256), 0, st, (const int8_t*)d_marks,
-                           (const int64_t*)d_pos, (const int8_t*)d_lvl, n, d_code);
+        hipLaunchKernelGGL(k_adapt_codes, dim3(grid_for(n)), dim3(256), 0, st, explicit_view(grid),
+                           (const uint64_t*)E->d_leaves, (const uint32_t*)E->d_slot_of_g, (const uint32_t*)E->d_local_g, (const int8_t*)d_marks, n,
+                           d_code);
         if (hipGetLastError() != hipSuccess) s = set_error(DCCRGX_EHIP, "adaptation sets failed");
+        T.lap("codes");
         uint64_t* out[3] = {to_refine, not_to_unrefine, to_unrefine};
         if (s == DCCRGX_OK) s = amr_dev_codes_to_lists(grid, d_code, n, out, counts);
     }
-    for (void* q : {(void*)d_marks, (void*)d_sib, (void*)d_pos, (void*)d_lvl, (void*)d_code}) dx_free(q);
+    for (void* q : {(void*)d_marks, (void*)d_code}) dx_free(q);
+    T.lap("lists");
     return s;
 }
 

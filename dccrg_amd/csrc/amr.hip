@@ -113,7 +113,7 @@ struct View {
             const auto& row = to ? L.h_nto_row : L.h_nof_row;
             const auto& val = to ? L.h_nto_g : L.h_nof_g;
             const int64_t rr = E->row_of((uint64_t)r);
-            for (uint64_t e = row[rr]; e < row[rr + 1]; e++) f(E->leaves[val[e]]);
+            for (uint64_t e = row[rr]; e < row[rr + 1]; e++) f(E->leaves()[val[e]]);
             return;
         }
         auto it = L.row_at.find((uint32_t)r);
@@ -122,7 +122,7 @@ struct View {
             it = L.row_at.find((uint32_t)r);
         }
         const uint64_t off = it->second[to ? 2 : 0], len = it->second[to ? 3 : 1];
-        for (uint64_t e = off; e < off + len; e++) f(E->leaves[L.row_vals[e]]);
+        for (uint64_t e = off; e < off + len; e++) f(E->leaves()[L.row_vals[e]]);
     }
     template <class F>
     void for_nof(uint64_t c, F f) const { for_row(c, false, f); }
@@ -318,7 +318,8 @@ void rebuild_commit(dccrgx_grid* grid, RebuildTxn& t)
 int rebuild_prepare(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std::vector<uint64_t>& retired,
                     uint64_t* d_leaves,  // leaves: moved into the new state
                     const uint32_t* gone_flags,  // per old leaf, AMR_FLAG_GONE: lists rebuilt around the change
-                    RebuildTxn& t)
+                    RebuildTxn& t,
+                    uint64_t n_dev = 0, uint64_t first_dev = 0)  // leaves empty: d_leaves' count, first leaf
 {
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
@@ -376,7 +377,9 @@ int rebuild_prepare(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std:
     grid->rebuilding = true;
     grid->ex = nullptr;
     grid->uniform = false;
-    int s = explicit_init(grid, leaves.data(), leaves.size(), d_leaves, &leaves);  // adopts d_leaves
+    int s = leaves.empty() && d_leaves  // one rank: the device list only
+                ? explicit_init(grid, nullptr, n_dev, d_leaves, nullptr, first_dev)
+                : explicit_init(grid, leaves.data(), leaves.size(), d_leaves, &leaves);  // adopts d_leaves
     T.lap("explicit_init");
     if (s == DCCRGX_OK) grid->ex->defer_fields = true;
     for (auto it = grid->hoods.begin(); s == DCCRGX_OK && it != grid->hoods.end(); ++it) {
@@ -384,14 +387,13 @@ int rebuild_prepare(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std:
         s = explicit_build_hood_async(grid, it->second, gone_flags && !old.uniform && old.ex ? &hint : nullptr);
     }
     T.lap("neighborhoods");
-    if (s == DCCRGX_OK) s = explicit_add_slots(grid, retired, true);  // retired cells are not leaves
+    if (s == DCCRGX_OK) s = explicit_add_retired(grid, retired);
     if (s != DCCRGX_OK) return rollback(s);
     T.lap("retired slots");
     Explicit* E = grid->ex;
     E->defer_fields = false;
-    E->retired = retired;
     if ((s = amr_dev_retired_table(grid)) != DCCRGX_OK) return rollback(s);
-    const uint64_t ns = E->slot_ids.size();
+    const uint64_t ns = E->n_slot_ids();
 
     // old slot of every new slot: on the device from the old leaf hash and
     // slot map when the old grid was explicit (its retired cells were
@@ -409,7 +411,7 @@ int rebuild_prepare(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std:
         if (e != DCCRGX_OK) return fail(e);
     } else {
         std::vector<int64_t> from(ns);
-        for (uint64_t k = 0; k < ns; k++) from[k] = host_primary_slot(&old, E->slot_ids[k]);
+        for (uint64_t k = 0; k < ns; k++) from[k] = host_primary_slot(&old, E->slot_id(k));
         const int e = dx_h2d(ctx, d_from, from.data(), ns * 8, st);
         if (e != DCCRGX_OK) return fail(e);
     }
@@ -439,9 +441,15 @@ int rebuild_prepare(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std:
     }
     // every new slot written once: surviving data moved, new cells
     // value-initialised (dccrg.hpp:10375, 10590)
-    for (size_t i = 0; i < grid->fields.size(); i++) {
-        const Field& F = grid->fields[i];
-        if (launch_move(F.ptr, d_from, ns, F.elem, np[i], st) != DCCRGX_OK) return fail(DCCRGX_EHIP);
+    {
+        std::vector<const void*> src;
+        std::vector<uint32_t> elem;
+        for (const Field& F : grid->fields) {
+            src.push_back(F.ptr);
+            elem.push_back(F.elem);
+        }
+        if (launch_move_many(src.data(), np.data(), elem.data(), src.size(), d_from, ns, st) != DCCRGX_OK)
+            return fail(DCCRGX_EHIP);
     }
     if (hipStreamSynchronize(st) != hipSuccess) return fail(set_error(DCCRGX_EHIP, "moving field data failed"));
     dx_free(d_from);
@@ -807,11 +815,12 @@ int dccrgx_stop_refining_prepare(dccrgx_grid* grid, const uint64_t* const* sets,
     // override_unrefines (:9935-10124) and the new leaf set of
     // execute_refines (:10243-10693), on the device
     uint64_t* d_leaves = nullptr;
-    uint64_t n_leaves = 0;
+    uint64_t n_leaves = 0, first_leaf = 0;
     std::vector<uint64_t> leaves, retired;
     // the leaf list of two rebuilds ago lends its storage: a fresh 8 B-per-leaf
     // vector page-faults on first touch every step
-    if (grid->spare_host) leaves.swap(grid->spare_host->leaves);
+    // (several ranks: one rank's new list stays on the device)
+    if (grid->spare_host && grid->ctx->comm_size > 1) leaves.swap(grid->spare_host->leaves_);
     bool changed = false;
     // the request flags before the decisions: restored if the rebuild fails
     // or another rank's does, so the requests stay pending
@@ -822,15 +831,19 @@ int dccrgx_stop_refining_prepare(dccrgx_grid* grid, const uint64_t* const* sets,
         return unwind_sets(set_error(DCCRGX_ENOMEM, "out of device memory for the request flags"));
     (void)hipMemcpyAsync(X.d_saved, A.d_flags, A.flags_n * 4, hipMemcpyDeviceToDevice, st);
     A.pending = txn.release();
-    int s = amr_dev_decide(grid, &d_leaves, &n_leaves, leaves, retired, X.nr, &changed);
+    int s = amr_dev_decide(grid, &d_leaves, &n_leaves, &first_leaf, leaves, retired, X.nr, &changed);
     if (s == DCCRGX_OK && amr_fail_injected(grid)) {
         ds_free(d_leaves, st);
         s = set_error(DCCRGX_ENOMEM, "DCCRGX_TEST_FAIL_STOP_REFINING: injected failure on rank %d", grid->ctx->rank);
     }
     T.lap("decisions");
+    if (T.on)
+        std::fprintf(stderr, "[dccrgx] stop_refining leaves %llu new %zu removed %zu retired %zu\n",
+                     (unsigned long long)n_leaves, A.new_cells.size(), A.removed.size(), retired.size());
     if (s == DCCRGX_OK && changed) {
         // transactional: on failure the grid is unchanged; the flags mark the old leaves that go
-        s = rebuild_prepare(grid, leaves, retired, d_leaves, A.flags_n == grid->ex->n ? A.d_flags : nullptr, X.rb);
+        s = rebuild_prepare(grid, leaves, retired, d_leaves, A.flags_n == grid->ex->n ? A.d_flags : nullptr, X.rb,
+                            n_leaves, first_leaf);
         X.rebuilt = s == DCCRGX_OK;
     }
     if (s != DCCRGX_OK) {

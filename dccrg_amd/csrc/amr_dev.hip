@@ -970,12 +970,14 @@ int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_
 }
 
 // override_refines, induce_refines and override_unrefines on the flags, then
-// the new leaf list (device, ascending, and its host copy), this rank's new /
+// the new leaf list (device, ascending, its first leaf, and with several
+// ranks its host copy -- left empty on one rank), this rank's new /
 // removed cells (A.new_cells / A.removed) and retired cells (ascending), and
 // the dont_refine ids that persist (`nr`).  The grid is not changed; the
 // flags hold the decisions afterwards (the caller restores them if the
 // rebuild fails).
-int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, std::vector<uint64_t>& leaves_host,
+int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, uint64_t* first_out,
+                   std::vector<uint64_t>& leaves_host,
                    std::vector<uint64_t>& retired, std::vector<uint64_t>& nr, bool* changed)
 {
     Amr& A = *grid->amr;
@@ -1143,7 +1145,8 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     t = tmax;
     DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, t, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
     t = tmax;
-    DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, t, leaf_idx, gone_flags, d_gone, d_ngone, (int)N, st));
+    if (grid->ctx->comm_size > 1)  // for the host merge
+        DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, t, leaf_idx, gone_flags, d_gone, d_ngone, (int)N, st));
     for (int k = 0; k < 3; k++) {
         if (!ls_n[k]) continue;
         t = tmax;
@@ -1158,41 +1161,48 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
                        (const uint64_t*)d_cnt64, (const uint64_t*)o.added, (const uint64_t*)(d_cnt64 + 1), d_new);
     DX_HIP(hipGetLastError());
     T.lap("kept + sorted new");
-    // the host's copy of the new list is merged on the host from its copy of
-    // the old one, the gone leaves and the new ids -- small lists instead of
-    // the whole list over PCIe (28 MB at 3.5 M leaves, 0.5 ms of copy plus
-    // the staging copy)
-    uint64_t nk[2] = {0, 0};
+    // several ranks: the host's copy of the new list is merged on the host
+    // from its copy of the old one, the gone leaves and the new ids -- small
+    // lists instead of the whole list over PCIe (28 MB at 3.5 M leaves, 0.5 ms
+    // of copy plus the staging copy).  One rank keeps the list on the device
+    // only (Explicit::leaves() fetches it if host code asks).
+    const bool host_list = grid->ctx->comm_size > 1;
+    uint64_t nk[2] = {0, 0}, first_leaf = 0;
     uint32_t ngone = 0;
     int e = DCCRGX_OK;
     {
-        const D2H c2[2] = {{nk, d_cnt64, 16}, {&ngone, d_ngone, 4}};
-        e = dx_d2h_many(ctx, c2, 2, st);
+        const D2H c2[3] = {{nk, d_cnt64, 16}, {&ngone, d_ngone, 4}, {&first_leaf, d_new, 8}};
+        e = dx_d2h_many(ctx, c2, 3, st);
     }
-    std::vector<uint64_t> added(nk[1]);
-    std::vector<uint32_t> gone(ngone);
+    std::vector<uint64_t> added(host_list ? nk[1] : 0);
+    std::vector<uint32_t> gone(host_list ? ngone : 0);
     if (e == DCCRGX_OK) {
-        const D2H l2[6] = {{added.data(), o.added, nk[1] * 8},
-                           {gone.data(), d_gone, (size_t)ngone * 4},
-                           {nr.data(), d_nr, cnt[4] * 8ull},
+        const D2H l2[6] = {{nr.data(), d_nr, cnt[4] * 8ull},
                            {A.new_cells.data(), d_ls[0], cnt[1] * 8ull},
                            {A.removed.data(), d_ls[1], cnt[2] * 8ull},
-                           {retired.data(), d_ls[2], cnt[3] * 8ull}};
+                           {retired.data(), d_ls[2], cnt[3] * 8ull},
+                           {added.data(), o.added, added.size() * 8},
+                           {gone.data(), d_gone, gone.size() * 4}};
         e = dx_d2h_many(ctx, l2, 6, st);
     }
     if (e != DCCRGX_OK) {
         ds_free(d_new, st);
         return e;
     }
+    T.lap("lists read back");
     nr.insert(nr.end(), A.nr_other.begin(), A.nr_other.end());
     for (std::vector<uint64_t>* v : {&A.new_cells, &A.removed, &retired}) v->erase(std::unique(v->begin(), v->end()), v->end());
     const uint64_t n_new = nk[0] + nk[1];
-    merge_leaves_host(grid->ex->leaves, gone, added, leaves_host);
-    DX_CHECK(leaves_host.size() == n_new, DCCRGX_EINTERNAL, "host leaf list %zu, device %llu", leaves_host.size(),
-             (unsigned long long)n_new);
+    leaves_host.clear();
+    if (host_list) {
+        merge_leaves_host(grid->ex->leaves(), gone, added, leaves_host);
+        DX_CHECK(leaves_host.size() == n_new, DCCRGX_EINTERNAL, "host leaf list %zu, device %llu",
+                 leaves_host.size(), (unsigned long long)n_new);
+    }
     T.lap("new leaf list");
     *d_leaves_out = d_new;
     *n_out = n_new;
+    *first_out = first_leaf;
     return DCCRGX_OK;
 }
 
@@ -1234,10 +1244,8 @@ int amr_dev_retired_table(dccrgx_grid* grid)
     if (!n) return DCCRGX_OK;
     std::vector<uint64_t> t(2 * n);
     for (uint64_t i = 0; i < n; i++) {
-        const uint32_t* x = E->extra.find(E->retired[i]);
-        DX_CHECK(x, DCCRGX_EINTERNAL, "retired cell %llu has no slot", (unsigned long long)E->retired[i]);
         t[i] = E->retired[i];
-        t[n + i] = *x;
+        t[n + i] = E->ret_slot0 + i;
     }
     hipStream_t st = grid->ctx->compute;
     ds_free(E->d_ret, st);

@@ -102,7 +102,7 @@ uint64_t local_s0(const dccrgx_grid* g)
     return g->g.lo + (uint64_t)(-g->g.cbase * (int64_t)g->g.S);
 }
 
-uint64_t local_id(const dccrgx_grid* g, uint64_t i) { return g->uniform ? g->first_local + i : g->ex->local[i]; }
+uint64_t local_id(const dccrgx_grid* g, uint64_t i) { return g->uniform ? g->first_local + i : g->ex->local()[i]; }
 
 // record bytes of local cell i
 uint64_t record_bytes(const dccrgx_grid* g, const int32_t* f, size_t nf, uint64_t s0, uint64_t i)
@@ -558,8 +558,9 @@ int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* 
         int64_t i;
         if (g->uniform) i = (int64_t)(c - g->first_local);
         else {
-            auto it = std::lower_bound(g->ex->local.begin(), g->ex->local.end(), c);
-            i = (it != g->ex->local.end() && *it == c) ? (int64_t)(it - g->ex->local.begin()) : -1;
+            const std::vector<uint64_t>& loc = g->ex->local();
+            auto it = std::lower_bound(loc.begin(), loc.end(), c);
+            i = (it != loc.end() && *it == c) ? (int64_t)(it - loc.begin()) : -1;
         }
         DX_CHECK(i >= 0 && (uint64_t)i < g->n_local && L->disp[i] == ~0ull, DCCRGX_EINVAL,
                  "cell %llu is listed twice or is not a local leaf", (unsigned long long)c);

@@ -17,6 +17,7 @@
 // are replicated; field storage is per rank: local cells, then ghosts, then
 // retired cells (grid.hpp, Explicit).
 #include <algorithm>
+#include <mutex>
 #include <cstring>
 #include <set>
 
@@ -1198,13 +1199,15 @@ static int nto_direct(const dccrgx_grid* grid, const Hood& h, const uint64_t* ce
 
 
 int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t* d_leaves,
-                  std::vector<uint64_t>* take)
+                  std::vector<uint64_t>* take, uint64_t first_leaf)
 {
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
     auto* E = new Explicit();
     E->d_leaves = d_leaves;  // adopted (ascending, unique, = leaves): freed with E from here on
-    if (n == 0 || n >= (1ull << 32)) {
+    E->ctx = ctx;
+    E->one_rank = ctx->comm_size == 1;
+    if (n == 0 || n >= (1ull << 32) || (!leaves && (!d_leaves || !E->one_rank))) {
         explicit_free(E);
         return set_error(DCCRGX_EINVAL, "leaf count %zu", n);
     }
@@ -1212,37 +1215,39 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
     uint64_t ident = 0;  // leading identity entries of the reused one-rank maps
     if (grid->spare_host) {  // the previous state's host arrays: their capacity is reused
         Explicit* S = grid->spare_host;
-        E->leaves.swap(S->leaves);
-        E->local.swap(S->local);
+        E->leaves_.swap(S->leaves_);
+        E->local_.swap(S->local_);
         E->local_g.swap(S->local_g);
         E->owner.swap(S->owner);
-        E->slot_ids.swap(S->slot_ids);
+        E->slot_ids_.swap(S->slot_ids_);
         E->slot_of_g.swap(S->slot_of_g);
         E->dir.swap(S->dir);
-        if (ctx->comm_size > 1) {  // rebuilt by push_back; one rank overwrites them in place
-            E->local.clear();
-            E->local_g.clear();
-            E->slot_ids.clear();
-        } else {
-            ident = S->ident_n;
-        }
+        E->local_.clear();
+        E->slot_ids_.clear();
+        if (E->one_rank) ident = S->ident_n;
         delete S;
         grid->spare_host = nullptr;
     }
     grid->ex = E;
-    if (take && take->data() == leaves && take->size() == n) E->leaves.swap(*take);  // the caller's list, moved
-    else E->leaves.assign(leaves, leaves + n);
-    if (!d_leaves) {
-        if (!std::is_sorted(E->leaves.begin(), E->leaves.end())) std::sort(E->leaves.begin(), E->leaves.end());
-        E->leaves.erase(std::unique(E->leaves.begin(), E->leaves.end()), E->leaves.end());
+    if (!leaves) {  // one rank, the device's list (amr_dev_decide): fetched if host code asks
+        E->host_leaves = false;
+        E->n = n;
+    } else {
+        if (take && take->data() == leaves && take->size() == n) E->leaves_.swap(*take);  // the caller's list, moved
+        else E->leaves_.assign(leaves, leaves + n);
+        if (!d_leaves) {
+            if (!std::is_sorted(E->leaves_.begin(), E->leaves_.end())) std::sort(E->leaves_.begin(), E->leaves_.end());
+            E->leaves_.erase(std::unique(E->leaves_.begin(), E->leaves_.end()), E->leaves_.end());
+        }
+        DX_CHECK(E->leaves_[0] > 0 && E->leaves_.back() <= grid->map.last_cell, DCCRGX_EINVAL, "invalid cell %llu",
+                 (unsigned long long)(E->leaves_[0] == 0 ? 0 : E->leaves_.back()));
+        E->n = E->leaves_.size();
+        first_leaf = E->leaves_[0];
     }
-    DX_CHECK(E->leaves[0] > 0 && E->leaves.back() <= grid->map.last_cell, DCCRGX_EINVAL, "invalid cell %llu",
-             (unsigned long long)(E->leaves[0] == 0 ? 0 : E->leaves.back()));
-    E->n = E->leaves.size();
     E->dir_valid = false;  // built on the first host lookup
     uint64_t cap = 16;
     while (cap < 2 * E->n) cap <<= 1;
-    if (!E->d_leaves) DX_TRY(upload(grid->ctx, E->leaves, &E->d_leaves, st));
+    if (!E->d_leaves) DX_TRY(upload(grid->ctx, E->leaves_, &E->d_leaves, st));
     // the rank bitmap when it is small (at most 1 GiB, and at most 16x the hash)
     const uint64_t nw = (grid->map.last_cell >> 6) + 1;
     if (nw <= (1ull << 26) && nw * 12 <= 16 * cap * 12) {
@@ -1264,10 +1269,11 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
     DX_HIP(hipGetLastError());
     T.lap("leaves+lookup");
     if (test_opt(OPT_CHECK_INIT, 0)) {  // device leaves and lookups against the host list
+        const std::vector<uint64_t>& L = E->leaves();
         std::vector<uint64_t> back(E->n);
         DX_TRY(dx_d2h(ctx, back.data(), E->d_leaves, E->n * 8, st));
         uint64_t bad = 0;
-        for (uint64_t i = 0; i < E->n; i++) bad += back[i] != E->leaves[i];
+        for (uint64_t i = 0; i < E->n; i++) bad += back[i] != L[i];
         int32_t* d_e = nullptr;
         DX_HIP(dx_malloc(&d_e, 8));
         DX_HIP(hipMemsetAsync(d_e, 0, 8, st));
@@ -1283,48 +1289,46 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
     // ownership: the process of the level-0 ancestor (no load balancing),
     // block partition or the grid's SFC table
     E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
-    E->owner.resize(E->n);
-    if (ctx->comm_size == 1) {  // one process owns every leaf: identity maps, filled by the host threads
+    if (E->one_rank) {  // one process owns every leaf: identity maps, filled by the host threads
         // (reused maps already hold the identity up to `ident`: only the tail is written)
         ident = std::min<uint64_t>({ident, E->owner.size(), E->local_g.size(), E->slot_of_g.size()});
         E->owner.resize(E->n);
-        E->local.resize(E->n);
         E->local_g.resize(E->n);
-        E->slot_ids.resize(E->n);
         E->slot_of_g.resize(E->n);
-        parallel_ranges(E->n, 1u << 16, [E, ident](size_t b, size_t e) {
-            std::copy(E->leaves.begin() + b, E->leaves.begin() + e, E->local.begin() + b);
-            std::copy(E->leaves.begin() + b, E->leaves.begin() + e, E->slot_ids.begin() + b);
-            for (size_t i = std::max<size_t>(b, ident); i < e; i++) {
-                E->owner[i] = 0;
-                E->local_g[i] = E->slot_of_g[i] = (uint32_t)i;
-            }
-        });
+        if (ident < E->n)
+            parallel_ranges(E->n - ident, 1u << 16, [E, ident](size_t b, size_t e) {
+                for (size_t i = ident + b; i < ident + e; i++) {
+                    E->owner[i] = 0;
+                    E->local_g[i] = E->slot_of_g[i] = (uint32_t)i;
+                }
+            });
         E->slot_identity = true;
         E->ident_n = E->n;
-    }
-    for (uint64_t i = 0; ctx->comm_size > 1 && i < E->n; i++) {
-        uint64_t idx[3];
-        int l;
-        map_indices(grid->map, E->leaves[i], idx, &l);
-        const uint64_t l0 = l == 0 ? E->leaves[i] : map_cell(grid->map, idx, 0);
-        E->owner[i] = level0_owner(grid, E->part, l0);
-        if (E->owner[i] == ctx->rank) {
-            E->local.push_back(E->leaves[i]);
-            E->local_g.push_back((uint32_t)i);
+        DX_TRY(device_iota(&E->d_local_g, E->n, st));
+    } else {
+        const std::vector<uint64_t>& L = E->leaves_;
+        E->local_g.clear();
+        E->owner.resize(E->n);
+        for (uint64_t i = 0; i < E->n; i++) {
+            uint64_t idx[3];
+            int l;
+            map_indices(grid->map, L[i], idx, &l);
+            const uint64_t l0 = l == 0 ? L[i] : map_cell(grid->map, idx, 0);
+            E->owner[i] = level0_owner(grid, E->part, l0);
+            if (E->owner[i] == ctx->rank) {
+                E->local_.push_back(L[i]);
+                E->local_g.push_back((uint32_t)i);
+            }
         }
-    }
-    if (ctx->comm_size == 1) DX_TRY(device_iota(&E->d_local_g, E->n, st));
-    else DX_TRY(upload(grid->ctx, E->local_g, &E->d_local_g, st));
-    grid->n_local = E->local.size();
-    grid->first_local = E->local.empty() ? 0 : E->local[0];
-    // storage: the local cells first (ghosts are added by the neighborhoods)
-    if (ctx->comm_size > 1) {
-        E->slot_ids = E->local;
+        DX_TRY(upload(grid->ctx, E->local_g, &E->d_local_g, st));
+        // storage: the local cells first (ghosts are added by the neighborhoods)
+        E->slot_ids_ = E->local_;
         E->slot_of_g.assign(E->n, NO_SLOT);
-        for (uint64_t i = 0; i < E->local.size(); i++) E->slot_of_g[E->local_g[i]] = (uint32_t)i;
+        for (uint64_t i = 0; i < E->local_.size(); i++) E->slot_of_g[E->local_g[i]] = (uint32_t)i;
     }
-    DX_TRY(device_iota(&E->d_local_slot, E->local.size(), st));  // local position -> slot: identity
+    grid->n_local = E->n_local();
+    grid->first_local = !grid->n_local ? 0 : E->one_rank ? first_leaf : E->local_[0];
+    DX_TRY(device_iota(&E->d_local_slot, grid->n_local, st));  // local position -> slot: identity
     T.lap("owners+local");
     DX_TRY(sync_slots(grid, true));
     T.lap("sync_slots");
@@ -1348,7 +1352,7 @@ static int sync_slots(dccrgx_grid* grid, bool slot_map_changed)
 {
     Explicit* E = grid->ex;
     hipStream_t st = grid->ctx->compute;
-    const uint64_t ns = E->slot_ids.size(), nl = E->local.size();
+    const uint64_t ns = E->n_slot_ids(), nl = E->n_local();
     if (slot_map_changed || !E->d_slot_of_g) {
         dx_free(E->d_slot_of_g);
         E->d_slot_of_g = nullptr;
@@ -1375,7 +1379,7 @@ static int sync_slots(dccrgx_grid* grid, bool slot_map_changed)
         std::vector<uint8_t> tail(ns - E->d_level_n);
         const uint64_t k0 = E->d_level_n;
         parallel_ranges(ns - k0, 1u << 15, [&](size_t b, size_t e) {
-            for (size_t k = b; k < e; k++) tail[k] = (uint8_t)map_level(grid->map, E->slot_ids[k0 + k]);
+            for (size_t k = b; k < e; k++) tail[k] = (uint8_t)map_level(grid->map, E->slot_id(k0 + k));
         });
         DX_TRY(dx_h2d_async(grid->ctx, E->d_level + E->d_level_n, tail.data(), tail.size(), st));
         E->d_level_n = ns;
@@ -1425,18 +1429,18 @@ static int grow_fields(dccrgx_grid* grid, uint64_t old_ns, uint64_t ns)
     return DCCRGX_OK;
 }
 
-int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids, bool not_leaves)
+int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
 {
     Explicit* E = grid->ex;
-    const uint64_t old_ns = E->slot_ids.size();
+    const uint64_t old_ns = E->n_slot_ids();
     bool leaf_slot = false;  // a leaf got a (ghost) slot: the slot map changes
     E->extra.reserve(E->extra.size() + ids.size());
-    E->slot_ids.reserve(old_ns + ids.size());
+    uint64_t ns = old_ns;
     for (uint64_t c : ids) {
-        const int64_t g = not_leaves ? -1 : E->find(c);  // retired cells are no leaves: no host lookup
+        const int64_t g = E->find(c);
         if ((g >= 0 && E->slot_of_g[g] != NO_SLOT) || E->extra.count(c)) continue;  // has a slot
-        const uint32_t s = (uint32_t)E->slot_ids.size();
-        E->slot_ids.push_back(c);
+        const uint32_t s = (uint32_t)ns++;
+        E->push_slot(c);
         E->extra.set(c, s);
         if (g >= 0) {
             E->slot_of_g[g] = s;
@@ -1445,14 +1449,13 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids, bool
             E->ident_n = 0;
         }
     }
-    const uint64_t ns = E->slot_ids.size();
     DX_CHECK(ns < NO_SLOT, DCCRGX_EINVAL, "%llu storage slots on one rank", (unsigned long long)ns);
     if (ns == old_ns) return DCCRGX_OK;
     if (!E->defer_fields) {
         const int s = grow_fields(grid, old_ns, ns);
         if (s != DCCRGX_OK) {  // undo the new slots
             for (uint64_t k = old_ns; k < ns; k++) {
-                const uint64_t c = E->slot_ids[k];
+                const uint64_t c = E->slot_id(k);
                 E->extra.erase(c);
                 const int64_t g = E->find(c);
                 if (g >= 0) {
@@ -1460,11 +1463,25 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids, bool
                     E->ident_n = 0;
                 }
             }
-            E->slot_ids.resize(old_ns);
+            E->truncate_slots(old_ns);
             return s;
         }
     }
     return sync_slots(grid, leaf_slot);
+}
+
+int explicit_add_retired(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
+{
+    Explicit* E = grid->ex;
+    E->retired.clear();
+    if (ids.empty()) return DCCRGX_OK;
+    const uint64_t ns = E->n_slot_ids() + ids.size();
+    DX_CHECK(ns < NO_SLOT, DCCRGX_EINVAL, "%llu storage slots on one rank", (unsigned long long)ns);
+    DX_CHECK(E->defer_fields, DCCRGX_EINTERNAL, "retired slots outside a rebuild");
+    E->retired = ids;
+    E->ret_slot0 = E->n_slot_ids();
+    for (uint64_t c : ids) E->push_slot(c);
+    return sync_slots(grid, false);
 }
 
 int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
@@ -1488,15 +1505,30 @@ int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
     return explicit_build_hood(grid, grid->hoods[h.id]);
 }
 
+// Explicit::leaves() of a list held on the device only: one copy, made once
+// (a lookup may ask from several host threads)
+void explicit_fetch_leaves(const Explicit* E)
+{
+    static std::mutex m;
+    std::lock_guard<std::mutex> g(m);
+    if (E->host_leaves) return;
+    E->leaves_.resize(E->n);
+    if (dx_d2h(E->ctx, E->leaves_.data(), E->d_leaves, E->n * 8, E->ctx->compute) != DCCRGX_OK) {
+        std::fprintf(stderr, "dccrgx: reading the leaf list from the device failed: %s\n", dccrgx_last_error());
+        std::abort();
+    }
+    E->host_leaves = true;
+}
+
 void explicit_recycle(dccrgx_grid* grid, Explicit* E)
 {
     if (!E) return;
     auto* S = new Explicit();
-    S->leaves.swap(E->leaves);
-    S->local.swap(E->local);
+    S->leaves_.swap(E->leaves_);  // (empty while the leaves are on the device only)
+    S->local_.swap(E->local_);
     S->local_g.swap(E->local_g);
     S->owner.swap(E->owner);
-    S->slot_ids.swap(E->slot_ids);
+    S->slot_ids_.swap(E->slot_ids_);
     S->slot_of_g.swap(E->slot_of_g);
     S->dir.swap(E->dir);
     S->ident_n = E->ident_n;
@@ -1523,7 +1555,6 @@ void explicit_free(Explicit* E)
 // the next rebuild)
 void explicit_clear_retired(Explicit* E)
 {
-    for (uint64_t c : E->retired) E->extra.erase(c);
     E->retired.clear();
     E->n_ret = 0;  // the table stays allocated until E is freed
 }
@@ -1969,7 +2000,7 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     h.outer.clear();
     h.remote.clear();
     const uint64_t N = E->n;
-    const uint64_t nl = E->local.size();
+    const uint64_t nl = E->n_local();
     // The CSRs hold the rows of this rank's local cells, indexed by local
     // position (= storage slot).  One process: every leaf, in leaf order.
     // Several: only the local cells' rows -- the reference builds lists for
@@ -1985,7 +2016,7 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
                          hint->old_ex && incremental_rebuild(hint->old_ex->n);
     // the stencil rows follow incrementally where slots are leaf indices before and after
     const bool inc_st = inc_nof && E->slot_identity && hint->old_ex->slot_identity && hint->old_h->d_st_row &&
-                        hint->old_ex->local.size() == hint->old_ex->n;
+                        hint->old_ex->n_local() == hint->old_ex->n;
     uint64_t* d_local_ids = nullptr;  // several processes: the local cells' ids
     if (per_rank) {
         DX_HIP(ds_malloc(&d_local_ids, std::max<uint64_t>(nl, 1) * 8, st));
@@ -2054,20 +2085,20 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
             const uint32_t t = L.h_nof_g[e];
             if (owner[t] != me) {
                 outer = true;
-                remote.insert(E->leaves[t]);
-                recv[owner[t]].insert(E->leaves[t]);
+                remote.insert(E->leaves_[t]);
+                recv[owner[t]].insert(E->leaves_[t]);
             }
         }
         for (uint64_t e = nto_row[r]; e < nto_row[r + 1]; e++) {
             const uint32_t t = L.h_nto_g[e];
             if (owner[t] != me) {
                 outer = true;
-                remote.insert(E->leaves[t]);
-                send[owner[t]].insert(E->local[i]);
+                remote.insert(E->leaves_[t]);
+                send[owner[t]].insert(E->local_[i]);
             }
         }
         (outer ? L.outer_pos : L.inner_pos).push_back((uint32_t)i);
-        if (outer) h.outer.push_back(E->local[i]);
+        if (outer) h.outer.push_back(E->local_[i]);
     }
     h.remote.assign(remote.begin(), remote.end());
     T.lap("classification");
@@ -2184,7 +2215,8 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     for (auto& kv : send) peers.insert(kv.first);
     for (auto& kv : recv) peers.insert(kv.first);
     auto local_pos = [&](uint64_t id) {
-        return (uint64_t)(std::lower_bound(E->local.begin(), E->local.end(), id) - E->local.begin());
+        const std::vector<uint64_t>& loc = E->local();
+        return (uint64_t)(std::lower_bound(loc.begin(), loc.end(), id) - loc.begin());
     };
     for (int p : peers) {
         PeerPlan pp;
@@ -2229,13 +2261,13 @@ int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, ui
     const std::vector<uint64_t>* v = nullptr;
     std::vector<uint64_t> inner;
     switch (which) {
-    case DCCRGX_CELLS_LOCAL: v = &E->local; break;
+    case DCCRGX_CELLS_LOCAL: v = &E->local(); break;
     case DCCRGX_CELLS_OUTER: v = &h.outer; break;
     case DCCRGX_CELLS_REMOTE: v = &h.remote; break;
     case DCCRGX_CELLS_INNER: {
         const auto& L = E->hl.at(h.id);
-        if (L.inner_all) inner = E->local;
-        for (uint32_t p : L.inner_pos) inner.push_back(E->local[p]);
+        if (L.inner_all) inner = E->local();
+        for (uint32_t p : L.inner_pos) inner.push_back(E->local()[p]);
         v = &inner;
         break;
     }
@@ -2255,18 +2287,20 @@ int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id)
     // ghosts, and data of refined / unrefined cells kept until
     // clear_refined_unrefined_data
     const uint32_t* x = E->extra.find(id);
-    return x ? (int64_t)*x : -1;
+    return x ? (int64_t)*x : E->retired_slot(id);
 }
 
 // rebuild(): new slot k takes old slot src[k] (-1: value-initialised), looked
 // up in the old leaf hash and slot map on the device
+// (ids of slots [0, na) from `ids`, of the rest from `tail`)
 __global__ void __launch_bounds__(256) k_old_slots(ExView old, const uint32_t* __restrict__ old_slot_of_g,
-                                                   const uint64_t* __restrict__ ids, uint64_t n,
+                                                   const uint64_t* __restrict__ ids, uint64_t na,
+                                                   const uint64_t* __restrict__ tail, uint64_t n,
                                                    int64_t* __restrict__ src)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
-        const int64_t g = ex_find(old, ids[k]);
+        const int64_t g = ex_find(old, k < na ? ids[k] : tail[k - na]);
         const uint32_t s = g < 0 ? NO_SLOT : old_slot_of_g[g];
         src[k] = s == NO_SLOT ? -1 : (int64_t)s;
     }
@@ -2288,20 +2322,29 @@ __global__ void __launch_bounds__(256) k_move(const T* __restrict__ src, const i
 int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_src, hipStream_t st)
 {
     const Explicit* E = grid->ex;
-    const uint64_t n = E->slot_ids.size();
+    const uint64_t n = E->n_slot_ids();
     if (!n) return DCCRGX_OK;
     uint64_t* d_ids = nullptr;
+    const uint64_t *ids = nullptr, *tail = nullptr;
+    uint64_t na = n;
     // one rank: the slot ids are the device leaf list, then the retired cells
     // in the order of the device retired table -- no upload of the host copy
     const uint64_t nr = n > E->n ? n - E->n : 0;
-    if (E->slot_identity && E->d_leaves && nr == E->n_ret && (!nr || E->d_ret) && E->retired.size() == nr &&
-        std::equal(E->slot_ids.begin() + E->n, E->slot_ids.end(), E->retired.begin())) {
-        DX_HIP(ds_malloc(&d_ids, n * 8, st));
-        DX_HIP(hipMemcpyAsync(d_ids, E->d_leaves, E->n * 8, hipMemcpyDeviceToDevice, st));
-        if (nr) DX_HIP(hipMemcpyAsync(d_ids + E->n, E->d_ret, nr * 8, hipMemcpyDeviceToDevice, st));
+    if (E->one_rank && E->slot_identity && E->d_leaves && nr == E->n_ret && (!nr || E->d_ret) &&
+        E->retired.size() == nr && std::equal(E->slot_ids_.begin(), E->slot_ids_.end(), E->retired.begin())) {
+        ids = E->d_leaves;
+        na = E->n;
+        tail = E->d_ret;
     } else {
         DX_HIP(ds_malloc(&d_ids, n * 8, st));
-        DX_TRY(dx_h2d(grid->ctx, d_ids, E->slot_ids.data(), n * 8, st));
+        std::vector<uint64_t> h_ids(n);
+        for (uint64_t k = 0; k < n; k++) h_ids[k] = E->slot_id(k);
+        const int e = dx_h2d(grid->ctx, d_ids, h_ids.data(), n * 8, st);
+        if (e != DCCRGX_OK) {
+            ds_free(d_ids, st);
+            return e;
+        }
+        ids = d_ids;
     }
     ExView v{};
     v.mp = grid->map;
@@ -2310,14 +2353,55 @@ int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_
     v.mask = old->mask;
     v.bits = old->d_bits;
     v.rank = old->d_rank;
-    hipLaunchKernelGGL(k_old_slots, dim3(grid_for(n)), dim3(256), 0, st, v, old->d_slot_of_g, d_ids, n, d_src);
+    hipLaunchKernelGGL(k_old_slots, dim3(grid_for(n)), dim3(256), 0, st, v, old->d_slot_of_g, ids, na, tail, n,
+                       d_src);
     const hipError_t e = hipGetLastError();
-    ds_free(d_ids, st);  // after the kernel, in stream order
+    if (d_ids) ds_free(d_ids, st);  // after the kernel, in stream order
     DX_HIP(e);
     return DCCRGX_OK;
 }
 
 // dst[k] = src[from[k]] (or zero), elements of `elem` bytes
+// up to 8 fields of 8-byte elements moved behind one read of `from`
+struct MoveSet {
+    const uint64_t* src[8];
+    uint64_t* dst[8];
+    int n;
+};
+
+__global__ void __launch_bounds__(256) k_move_many(MoveSet m, const int64_t* __restrict__ from, uint64_t n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+        const int64_t f = from[k];
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (j < m.n) m.dst[j][k] = f >= 0 ? m.src[j][f] : 0;
+    }
+}
+
+int launch_move_many(const void* const* src, void* const* dst, const uint32_t* elem, size_t nf, const int64_t* from,
+                     uint64_t n, hipStream_t st)
+{
+    MoveSet m{};
+    auto flush = [&]() {
+        if (m.n) hipLaunchKernelGGL(k_move_many, dim3(grid_for(n)), dim3(256), 0, st, m, from, n);
+        m.n = 0;
+    };
+    for (size_t i = 0; i < nf && n; i++) {
+        if (elem[i] != 8) {
+            DX_TRY(launch_move(src[i], from, n, elem[i], dst[i], st));
+            continue;
+        }
+        m.src[m.n] = (const uint64_t*)src[i];
+        m.dst[m.n++] = (uint64_t*)dst[i];
+        if (m.n == 8) flush();
+    }
+    flush();
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
 int launch_move(const void* src, const int64_t* from, uint64_t n, uint32_t elem, void* dst, hipStream_t st)
 {
     if (!n) return DCCRGX_OK;
@@ -2403,7 +2487,7 @@ int explicit_gather_neighbors(const dccrgx_grid* grid, const Hood& h, const Fiel
     if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
     if (n)
         hipLaunchKernelGGL(k_ex_gather_count, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nof_row,
-                           E->d_slot_of_g, (uint64_t)E->local.size(), gidx, row, d_err);
+                           E->d_slot_of_g, E->n_local(), gidx, row, d_err);
     uint64_t total = 0;
     int s = device_scan_rows(row, n, st, &total);
     if (s != DCCRGX_OK) return done(s);
@@ -2444,7 +2528,7 @@ int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t
     const Explicit* E = grid->ex;
     if (n)
         hipLaunchKernelGGL(k_ex_query_rows, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nof_row,
-                           (const uint32_t*)E->d_slot_of_g, (uint64_t)E->local.size(), gq, row, d_err);
+                           (const uint32_t*)E->d_slot_of_g, E->n_local(), gq, row, d_err);
     uint64_t total = 0;
     int s = device_scan_rows(row, n, st, &total);  // synchronises (total)
     if (s != DCCRGX_OK) return done(s);
@@ -2495,7 +2579,7 @@ int explicit_neighbors_to(const dccrgx_grid* grid, const Hood& h, const uint64_t
     const Explicit* E = grid->ex;
     if (n)
         hipLaunchKernelGGL(k_ex_query_rows, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nto_row,
-                           (const uint32_t*)E->d_slot_of_g, (uint64_t)E->local.size(), gq, row, d_err);
+                           (const uint32_t*)E->d_slot_of_g, E->n_local(), gq, row, d_err);
     uint64_t total = 0;
     int s = device_scan_rows(row, n, st, &total);  // synchronises (total)
     if (s != DCCRGX_OK) return done(s);
@@ -2557,8 +2641,8 @@ int explicit_region(const dccrgx_grid* grid, const Hood& h, int32_t region, ExRe
     const auto& L = it->second;
     out->pos = region == DCCRGX_REGION_INNER ? L.d_inner_pos
                : region == DCCRGX_REGION_OUTER ? L.d_outer_pos : L.d_all_pos;
-    out->n = region == DCCRGX_REGION_INNER ? (L.inner_all ? E->local.size() : L.inner_pos.size())
-             : region == DCCRGX_REGION_OUTER ? L.outer_pos.size() : E->local.size();
+    out->n = region == DCCRGX_REGION_INNER ? (L.inner_all ? E->n_local() : L.inner_pos.size())
+             : region == DCCRGX_REGION_OUTER ? L.outer_pos.size() : E->n_local();
     out->local_slot = E->d_local_slot;
     out->level = E->d_level;
     return DCCRGX_OK;
@@ -2579,7 +2663,7 @@ int explicit_gol(dccrgx_grid* grid, const Hood& h, const Field& in, const Field&
 // local values in ascending id order <-> slots [0, nl)
 int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device)
 {
-    const uint64_t n = grid->ex->local.size();
+    const uint64_t n = grid->ex->n_local();
     if (!n) return DCCRGX_OK;
     hipStream_t st = grid->ctx->compute;
     if (to_device) DX_TRY(dx_h2d(grid->ctx, F.ptr, host, n * F.elem, st));
@@ -2592,7 +2676,7 @@ int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, boo
 int explicit_local_ids(const dccrgx_grid* grid, uint64_t* d_ids, hipStream_t st)
 {
     const Explicit* E = grid->ex;
-    const uint64_t n = E->local.size();
+    const uint64_t n = E->n_local();
     if (!n) return DCCRGX_OK;
     hipLaunchKernelGGL(k_local_ids, dim3(grid_for(n)), dim3(256), 0, st, (const uint64_t*)E->d_leaves,
                        (const uint32_t*)E->d_local_g, n, d_ids);

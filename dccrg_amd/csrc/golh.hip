@@ -223,7 +223,7 @@ int xargs(const dccrgx_grid* grid, const Hood& h, XArgs* x)
     x->nof_id = h.d_nof_id;
     x->nof_g = h.d_nof_g;
     x->slot_of_g = E->d_slot_of_g;
-    x->n = E->local.size();
+    x->n = E->n_local();
     return DCCRGX_OK;
 }
 

@@ -850,7 +850,7 @@ int dccrgx_get_all_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, siz
 {
     DX_CHECK(grid && n, DCCRGX_EINVAL, "null argument");
     if (!grid->uniform) {
-        const std::vector<uint64_t>& L = grid->ex->leaves;
+        const std::vector<uint64_t>& L = grid->ex->leaves();
         *n = L.size();
         DX_CHECK(cap >= *n && (ids || !*n), DCCRGX_ERANGE, "capacity");
         std::copy(L.begin(), L.end(), ids);
@@ -912,7 +912,7 @@ int dccrgx_neighbor_list_stats(const dccrgx_grid* grid, int32_t id, uint64_t out
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", id);
     for (int k = 0; k < 4; k++) out[k] = 0;
     if (grid->uniform || !h->d_nof_row) return DCCRGX_OK;  // closed-form rows: nothing stored
-    const uint64_t rows = h->n_rows, nl = grid->ex->local.size();
+    const uint64_t rows = h->n_rows, nl = grid->ex->n_local();
     uint64_t e[3] = {0, 0, 0};  // neighbors_of, neighbors_to, stencil entries
     hipStream_t st = grid->ctx->compute;
     DX_TRY(dx_d2h(grid->ctx, &e[0], h->d_nof_row + rows, 8, st));

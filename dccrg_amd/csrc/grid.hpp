@@ -6,6 +6,7 @@
 #include "internal.hpp"
 
 #include <array>
+#include <atomic>
 #include <map>
 #include <set>
 #include <unordered_map>
@@ -153,9 +154,27 @@ struct PeerPlan {
     VarPlans var_send, var_recv;
 };
 
+struct Explicit;
+// the host copy of a leaf list kept on the device (Explicit::leaves())
+void explicit_fetch_leaves(const Explicit* E);
+
 struct Explicit {
     uint64_t n = 0;                 // global leaves
-    std::vector<uint64_t> leaves;   // ascending
+    // Host copies of the leaf list, the local cells and the slot ids.  On one
+    // rank the local cells are the leaves and slot k < n holds leaf k, so
+    // `local_` stays empty and `slot_ids_` holds only the slots after the
+    // leaves (retired cells); after a rebuild decided on the device the leaf
+    // list itself stays on the device until host code asks for it (an
+    // adaptive step needs none: 3 copies of 8 B per leaf saved per step).
+    mutable std::vector<uint64_t> leaves_;  // ascending (valid when host_leaves)
+    mutable std::atomic<bool> host_leaves{true};
+    Ctx* ctx = nullptr;                     // for the lazy fetch
+    bool one_rank = false;                  // local = leaves, slots [0, n) = leaves
+    const std::vector<uint64_t>& leaves() const
+    {
+        if (!host_leaves) explicit_fetch_leaves(this);
+        return leaves_;
+    }
     uint64_t* d_leaves = nullptr;
     uint64_t* d_keys = nullptr;     // hash keys (0 = empty)
     uint32_t* d_vals = nullptr;     // global index
@@ -164,7 +183,9 @@ struct Explicit {
     uint32_t* d_rank = nullptr;     // leaves before each 64-bit word
     uint64_t nwords = 0;
     Partition part;                 // over level-0 cells
-    std::vector<uint64_t> local;    // ascending local ids
+    std::vector<uint64_t> local_;   // ascending local ids (several ranks)
+    const std::vector<uint64_t>& local() const { return one_rank ? leaves() : local_; }
+    uint64_t n_local() const { return one_rank ? n : local_.size(); }
     std::vector<uint32_t> local_g;  // their global indices
     std::vector<int32_t> owner;     // process of each leaf (level-0 ancestor's, dccrg.hpp:8098-8145)
     uint32_t* d_local_g = nullptr;
@@ -173,8 +194,16 @@ struct Explicit {
     // neighborhood), then the data of retired cells.  Fields are sized for
     // these slots only, as the reference stores data only for local cells and
     // remote neighbors (dccrg.hpp:7238, 7330).
-    std::vector<uint64_t> slot_ids;                 // id held by each slot
-    FlatMap32 extra;                                // ghost / retired id -> slot
+    std::vector<uint64_t> slot_ids_;                // id held by each slot (one rank: by each slot >= n)
+    uint64_t n_slot_ids() const { return one_rank ? n + slot_ids_.size() : slot_ids_.size(); }
+    uint64_t slot_id(uint64_t k) const
+    {
+        if (!one_rank) return slot_ids_[k];
+        return k < n ? leaves()[k] : slot_ids_[k - n];
+    }
+    void push_slot(uint64_t c) { slot_ids_.push_back(c); }
+    void truncate_slots(uint64_t ns) { slot_ids_.resize(one_rank ? ns - n : ns); }
+    FlatMap32 extra;                                // ghost id -> slot
     std::vector<uint32_t> slot_of_g;                // global leaf index -> slot (NO_SLOT)
     bool slot_identity = false;                     // slot_of_g[g] == g (one rank, no ghost leaves)
     uint64_t ident_n = 0;                           // one rank: owner[i] == 0, local_g[i] == slot_of_g[i] == i
@@ -214,6 +243,7 @@ struct Explicit {
     {
         dir_valid = true;
         dir.clear();
+        const std::vector<uint64_t>& leaves = this->leaves();
         if (leaves.empty()) return;
         dir_base = leaves.front();
         const uint64_t span = leaves.back() - dir_base + 1;
@@ -235,11 +265,12 @@ struct Explicit {
     {
         if (slot_identity) return (int64_t)g;
         const uint32_t s = slot_of_g[g];
-        return s < local.size() ? (int64_t)s : -1;
+        return s < n_local() ? (int64_t)s : -1;
     }
     int64_t find(uint64_t c) const  // global index of a leaf, -1 if none
     {
         if (!dir_valid) build_dir();
+        const std::vector<uint64_t>& leaves = this->leaves();
         if (dir.empty() || c < dir_base || c > leaves.back()) return -1;
         const uint64_t b = (c - dir_base) >> dir_shift;
         const auto lo = leaves.begin() + dir[b], hi = leaves.begin() + dir[b + 1];
@@ -251,6 +282,12 @@ struct Explicit {
     // clear_refined_unrefined_data (dccrg.hpp:3519-3543, 5550-5567): ascending
     // ids, stored in slots after the ghosts
     std::vector<uint64_t> retired;
+    uint64_t ret_slot0 = 0;  // retired[i] is in slot ret_slot0 + i
+    int64_t retired_slot(uint64_t id) const
+    {
+        const auto it = std::lower_bound(retired.begin(), retired.end(), id);
+        return it != retired.end() && *it == id ? (int64_t)(ret_slot0 + (it - retired.begin())) : -1;
+    }
     // their device copy for slot lookups (amr_dev.hip): ids ascending, then
     // the slot of each (n_ret of each), made by the rebuild that retired them
     uint64_t* d_ret = nullptr;
@@ -289,7 +326,8 @@ struct Amr {
 int amr_dev_sync(dccrgx_grid* grid);
 int amr_host_sync(dccrgx_grid* grid);
 int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results);
-int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, std::vector<uint64_t>& leaves_host,
+int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, uint64_t* first_out,
+                   std::vector<uint64_t>& leaves_host,
                    std::vector<uint64_t>& retired, std::vector<uint64_t>& nr, bool* changed);
 // the retired cells' device lookup table (after their slots were assigned)
 int amr_dev_retired_table(dccrgx_grid* grid);
@@ -463,11 +501,17 @@ void explicit_recycle(dccrgx_grid* grid, Explicit* E);
 void explicit_clear_retired(Explicit* E);
 // explicit grids: give `ids` (leaves or retired cells) storage slots if they
 // have none, growing every field unless a rebuild defers that
-int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids, bool not_leaves = false);
+int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids);
+// rebuild(): slots after the ghosts for the retired cells (ascending, unique,
+// no leaves), in their order; E->retired becomes `ids`
+int explicit_add_retired(dccrgx_grid* grid, const std::vector<uint64_t>& ids);
 // rebuild(): old slot (or -1) of every slot of the new layout, device output
 int explicit_old_slots(const dccrgx_grid* grid, const Explicit* old, int64_t* d_src, hipStream_t st);
 // dst[k] = src[from[k]], or zero where from[k] < 0
 int launch_move(const void* src, const int64_t* from, uint64_t n, uint32_t elem, void* dst, hipStream_t st);
+// the same for several fields (8-byte elements share one pass over `from`)
+int launch_move_many(const void* const* src, void* const* dst, const uint32_t* elem, size_t nf, const int64_t* from,
+                     uint64_t n, hipStream_t st);
 // the previous leaf set's lists of the same neighborhood and which of its
 // leaves are gone (flags & gone_bit): rows of kept leaves that reference no
 // gone leaf are copied from `old_h` instead of recomputed (amr.hip rebuild)
@@ -491,9 +535,12 @@ int explicit_get_cells(const dccrgx_grid* grid, const Hood& h, int32_t which, ui
                        size_t cap, size_t* n);
 int explicit_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device);
 // explicit grid state over an ascending leaf list (no neighborhoods built);
-// d_leaves: the same list on the device, adopted by the grid (amr_dev.hip)
+// d_leaves: the same list on the device, adopted by the grid (amr_dev.hip);
+// on one rank `leaves` may be null: the device list alone, whose first leaf
+// is `first_leaf` (the host copy is fetched when host code asks for it)
 int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t* d_leaves = nullptr,
-                  std::vector<uint64_t>* take = nullptr);  // take: the vector holding `leaves`, moved from
+                  std::vector<uint64_t>* take = nullptr,  // take: the vector holding `leaves`, moved from
+                  uint64_t first_leaf = 0);
 int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id);
 // the slot read and written for a cell on this rank (-1: none), halo.hip
 int64_t host_primary_slot(const dccrgx_grid* grid, uint64_t id);

@@ -135,20 +135,23 @@ inline hipError_t ds_free(void* p, hipStream_t st)
 
 // ---------------------------------------------------------------------------
 // host phase timing of structural calls (AMR rebuild, neighbor builds):
-// DCCRGX_TIMING=1 prints one line per phase to stderr
+// DCCRGX_TIMING=1 prints one line per phase to stderr; =2 waits for the
+// device before each lap (device time lands in the phase that queued it)
 // ---------------------------------------------------------------------------
 struct PhaseTimer {
     const char* scope;
     std::chrono::steady_clock::time_point t;
-    bool on;
+    bool on, sync;
     explicit PhaseTimer(const char* s) : scope(s), t(std::chrono::steady_clock::now())
     {
         const char* e = std::getenv("DCCRGX_TIMING");
         on = e && *e && *e != '0';
+        sync = on && *e == '2';
     }
     void lap(const char* what)
     {
         if (!on) return;
+        if (sync) (void)hipDeviceSynchronize();
         const auto now = std::chrono::steady_clock::now();
         std::fprintf(stderr, "[dccrgx] %s %s %.3f ms\n", scope, what,
                      std::chrono::duration<double, std::milli>(now - t).count());

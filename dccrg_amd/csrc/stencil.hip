@@ -181,7 +181,7 @@ int build_iter(const dccrgx_grid* grid, Hood& h, hipStream_t st)
         }
     } else {
         const Explicit* E = grid->ex;
-        const uint64_t nl = E->local.size();
+        const uint64_t nl = E->n_local();
         DX_CHECK(!nl || (h.d_st_row && h.d_nto_row && E->d_slot_of_g), DCCRGX_EINTERNAL,
                  "neighborhood %d has no stencil rows", h.id);
         const uint64_t cap = std::max<uint64_t>(h.st_cap, 1);

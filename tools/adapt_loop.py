@@ -13,6 +13,9 @@ if not os.environ.get("ADAPT_NO_TORCH"):
     import torch  # noqa: F401
 import dccrg_amd as D  # noqa: E402
 from dccrg_amd import advection as A  # noqa: E402
+from dccrg_amd import _capi as X  # noqa: E402
+from dccrg_amd._capi import check, lib  # noqa: E402
+import numpy as np  # noqa: E402
 
 ctx = D.Context(0, 0, 1)
 rel, thr, sens, cfl, M = 0.025, 0.25, 0.5, 0.5, 2
@@ -30,7 +33,7 @@ dt = g.max_time_step()
 g.update_copies_of_remote_neighbors(fields=list(A.ALL))
 steps = int(os.environ.get("ADAPT_STEPS", "20"))
 per = []
-seg = os.environ.get("ADAPT_SEG")  # per-phase times, synchronised after each phase (diagnosis)
+seg = os.environ.get("ADAPT_SEG")  # per-phase times, synchronised after each phase (diagnosis; 2: adapt split)
 segs = []
 for _ in range(steps):
     t0 = time.perf_counter()
@@ -46,8 +49,27 @@ for _ in range(steps):
     mark()
     g.advect_step(cfl * dt)
     mark()
-    A.adapt_grid(g, geom, *sets)
-    mark()
+    if seg == "2":  # adapt_grid in its parts
+        A.request_adaptation(g, *sets)
+        mark()
+        g.stop_refining()
+        mark()
+        g.get_removed_cells()
+        fd = np.array([g.field_id("density")], dtype=np.int32)
+        mark()
+        check(lib().dccrgx_amr_copy_from_parents(g._h, fd.ctypes.data_as(X._i32p), fd.size))
+        mark()
+        check(lib().dccrgx_amr_average_children(g._h, fd.ctypes.data_as(X._i32p), fd.size))
+        mark()
+        g.clear_refined_unrefined_data()
+        mark()
+        A._velocities_lengths(g, geom)
+        mark()
+        g.update_copies_of_remote_neighbors(fields=list(A.ALL))
+        mark()
+    else:
+        A.adapt_grid(g, geom, *sets)
+        mark()
     dt = g.max_time_step()
     mark()
     per.append((time.perf_counter() - t0) * 1e3)
@@ -56,8 +78,11 @@ for _ in range(steps):
 ctx.synchronize()
 if seg:
     n = max(len(segs) - 4, 1)
-    print("phases (ghost, check, advect, adapt, dt) ms: " + " ".join(
-        f"{sum(x[i] for x in segs[4:]) / n:.2f}" for i in range(5)), flush=True)
+    names = ("ghost", "check", "advect") + (("request", "stop_refining", "removed list", "from parents",
+                                                                 "average", "clear", "geometry", "update")
+                                            if seg == "2" else ("adapt",)) + ("dt",)
+    print(f"phases ({', '.join(names)}) ms: " + " ".join(
+        f"{sum(x[i] for x in segs[4:]) / n:.3f}" for i in range(len(names))), flush=True)
 print("ms/step " + " ".join(f"{x:.2f}" for x in per), flush=True)
 print(f"leaves {g.n_local} mean of last {max(steps - 4, 1)}: "
       f"{sum(per[4:]) / max(len(per[4:]), 1):.2f} ms", flush=True)

@@ -12,6 +12,7 @@
 #   uspmc                FETCH/WRITE + SQ passes of the user stencil  -> TAG/uspmc_*/
 #   adapt / adaptbig     tools/adapt_loop.py at 218k / 3.5 M leaves   -> TAG/adapt*.log
 #   advlarge             tools/run_adv_large.py                        -> TAG/adv_large.log
+#   adaptsplit           adapt_grid split into its parts; sync phase timers -> TAG/adapt_*split*.log
 #   adapttrace           3.5 M-leaf adaptive loop: phases, trace, idle gaps -> TAG/adapt_*
 #   py=SCRIPT            python -u SCRIPT                              -> TAG/<script>.log
 set -o pipefail
@@ -61,6 +62,15 @@ for step in "$@"; do
       tail -n 2 $out/adapt_big_phases.log
       ADAPT_N=1600 ADAPT_REL=0.006 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $out/adapt_trace -o run -- python3 tools/adapt_loop.py > $out/adapt_trace.log 2>&1 || fail adapt_trace $? $out/adapt_trace.log
       python3 tools/idle_gaps.py $out/adapt_trace > $out/adapt_gaps.txt 2>&1; tail -n 25 $out/adapt_gaps.txt ;;
+    adaptsplit)
+      # adapt_grid in its parts (synchronised after each), at 218 k and 3.5 M
+      # leaves, then the library's phase timers waiting for the device per lap
+      ADAPT_SEG=2 timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_split.log 2>&1 || fail adapt_split $? $out/adapt_split.log
+      tail -n 3 $out/adapt_split.log
+      ADAPT_SEG=2 ADAPT_N=1600 ADAPT_REL=0.006 timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_big_split.log 2>&1 || fail adapt_big_split $? $out/adapt_big_split.log
+      tail -n 3 $out/adapt_big_split.log
+      ADAPT_N=1600 ADAPT_REL=0.006 DCCRGX_TIMING=2 timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_big_sync_phases.log 2>&1 || fail adapt_sync_phases $? $out/adapt_big_sync_phases.log
+      tail -n 2 $out/adapt_big_sync_phases.log ;;
     advlarge)
       timeout -k 10 300 python -u tools/run_adv_large.py > $out/adv_large.log 2>&1 || fail advlarge $? $out/adv_large.log
       tail -n 3 $out/adv_large.log ;;
