@@ -1396,15 +1396,62 @@ int amr_dev_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf
     return run_rule(grid, grid->amr->removed, fields, nf, true);
 }
 
-__global__ void __launch_bounds__(256) k_code_ids(const uint64_t* __restrict__ leaves, const uint32_t* __restrict__ local_g,
-                                                  const uint8_t* __restrict__ code, uint64_t n, uint64_t* __restrict__ ids,
-                                                  uint8_t* __restrict__ flags)
+// codes 1..3 of the local cells (k_adapt_codes) into three id lists, each in
+// local (ascending id) order, back to back in one buffer: per block of CODE_R
+// * 256 cells the count of each code, one scan over the [code][block] counts,
+// then each block writes its cells at the scanned offsets (wave ballots keep
+// the order inside a block)
+constexpr int CODE_R = 4;
+
+__global__ void __launch_bounds__(256) k_code_count(const uint8_t* __restrict__ code, uint64_t n, uint32_t nb,
+                                                    uint32_t* __restrict__ cnt)
 {
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
-        ids[q] = leaves[local_g[q]];
-        const uint8_t c = code[q];
-        for (int k = 0; k < 3; k++) flags[k * n + q] = c == k + 1;
+    __shared__ uint32_t c3[3];
+    if (threadIdx.x < 3) c3[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t q0 = (uint64_t)blockIdx.x * 256 * CODE_R;
+    uint32_t m[3] = {0, 0, 0};
+    for (int r = 0; r < CODE_R; r++) {
+        const uint64_t q = q0 + r * 256 + threadIdx.x;
+        const uint8_t c = q < n ? code[q] : 0;
+        for (int k = 0; k < 3; k++) m[k] += __popcll(__ballot(c == k + 1));
+    }
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 3; k++) atomicAdd(&c3[k], m[k]);
+    __syncthreads();
+    if (threadIdx.x < 3) cnt[threadIdx.x * nb + blockIdx.x] = c3[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) k_code_scatter(const uint8_t* __restrict__ code, const uint64_t* __restrict__ leaves,
+                                                      const uint32_t* __restrict__ local_g, uint64_t n, uint32_t nb,
+                                                      const uint32_t* __restrict__ off, uint64_t* __restrict__ out)
+{
+    __shared__ uint32_t wsum[3][4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t base[3];
+    for (int k = 0; k < 3; k++) base[k] = off[k * nb + blockIdx.x];
+    const uint64_t q0 = (uint64_t)blockIdx.x * 256 * CODE_R;
+    for (int r = 0; r < CODE_R; r++) {
+        const uint64_t q = q0 + r * 256 + threadIdx.x;
+        const uint8_t c = q < n ? code[q] : 0;
+        uint64_t m[3];
+        for (int k = 0; k < 3; k++) m[k] = __ballot(c == k + 1);
+        if (lane == 0)
+            for (int k = 0; k < 3; k++) wsum[k][w] = (uint32_t)__popcll(m[k]);
+        __syncthreads();
+        uint32_t pre[3] = {0, 0, 0}, tot[3] = {0, 0, 0};
+        for (int k = 0; k < 3; k++)
+            for (int j = 0; j < 4; j++) {
+                pre[k] += j < w ? wsum[k][j] : 0;
+                tot[k] += wsum[k][j];
+            }
+        if (c >= 1 && c <= 3) {
+            const int k = c - 1;
+            out[base[k] + pre[k] + (uint32_t)__popcll(m[k] & below)] = leaves[local_g[q]];
+        }
+        for (int k = 0; k < 3; k++) base[k] += tot[k];
+        __syncthreads();
     }
 }
 
@@ -1412,28 +1459,35 @@ int amr_dev_codes_to_lists(dccrgx_grid* grid, const uint8_t* d_code, uint64_t n,
 {
     hipStream_t st = grid->ctx->compute;
     const Explicit* E = grid->ex;
+    DX_CHECK(n < (1ull << 32), DCCRGX_EINVAL, "%llu local cells", (unsigned long long)n);
     Scratch S(st);
-    uint64_t *d_ids, *d_out;
-    uint8_t* d_flags;
-    int* d_cnt;
-    DX_TRY(S.get(&d_ids, n));
-    DX_TRY(S.get(&d_out, 3 * n));
-    DX_TRY(S.get(&d_flags, 3 * n));
-    DX_TRY(S.get(&d_cnt, 4));
-    hipLaunchKernelGGL(k_code_ids, dim3(blocks(n)), dim3(256), 0, st, (const uint64_t*)E->d_leaves,
-                       (const uint32_t*)E->d_local_g, d_code, n, d_ids, d_flags);
+    const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (n + 256 * CODE_R - 1) / (256 * CODE_R));
+    uint32_t *d_cnt, *d_off;
+    uint64_t* d_out;
+    DX_TRY(S.get(&d_cnt, 3ull * nb + 1));
+    DX_TRY(S.get(&d_off, 3ull * nb + 1));
+    DX_TRY(S.get(&d_out, std::max<uint64_t>(n, 1)));
+    DX_HIP(hipMemsetAsync(d_cnt + 3ull * nb, 0, 4, st));  // the scan's last entry: the total
+    hipLaunchKernelGGL(k_code_count, dim3(nb), dim3(256), 0, st, d_code, n, nb, d_cnt);
     size_t tb = 0;
-    DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, d_ids, d_flags, d_out, d_cnt, (int)n, st));
+    DX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, d_cnt, d_off, (int)(3 * nb + 1), st));
     uint8_t* d_tmp;
-    DX_TRY(S.get(&d_tmp, tb));
-    for (int k = 0; k < 3; k++)  // order preserving: ascending like the local cells
-        DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, tb, d_ids, d_flags + k * n, d_out + k * n, d_cnt + k, (int)n, st));
-    int cnt[3] = {0, 0, 0};
-    DX_TRY(dx_d2h(grid->ctx, cnt, d_cnt, 12, st));
+    DX_TRY(S.get(&d_tmp, std::max<size_t>(tb, 1)));
+    DX_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, d_cnt, d_off, (int)(3 * nb + 1), st));
+    hipLaunchKernelGGL(k_code_scatter, dim3(nb), dim3(256), 0, st, d_code, (const uint64_t*)E->d_leaves,
+                       (const uint32_t*)E->d_local_g, n, nb, (const uint32_t*)d_off, d_out);
+    DX_HIP(hipGetLastError());
+    // the lists start at the scanned offsets of their first blocks
+    uint32_t start[4] = {0, 0, 0, 0};
+    {
+        const D2H c[4] = {{&start[0], d_off, 4}, {&start[1], d_off + nb, 4}, {&start[2], d_off + 2ull * nb, 4},
+                          {&start[3], d_off + 3ull * nb, 4}};
+        DX_TRY(dx_d2h_many(grid->ctx, c, 4, st));
+    }
     D2H v[3];
     for (int k = 0; k < 3; k++) {
-        counts[k] = (size_t)cnt[k];
-        v[k] = D2H{out[k], d_out + k * n, (size_t)cnt[k] * 8};
+        counts[k] = (size_t)(start[k + 1] - start[k]);
+        v[k] = D2H{out[k], d_out + start[k], counts[k] * 8};
     }
     return dx_d2h_many(grid->ctx, v, 3, st);  // the three lists behind one synchronisation
 }
