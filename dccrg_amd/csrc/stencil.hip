@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(256) k_slot_leaf(const uint32_t* __restrict__ 
 // pass, then a write pass.  Reads and writes of a chunk are coalesced.
 // (Per-entry group flags instead of the copy made this 2.4x faster and the
 // walks over the view 2x slower: profiles/r5g_iter_view_time_groupflags.log.)
-constexpr int ITER_WAVES = 4, NTO_LDS = 1024;
+constexpr int ITER_WAVES = 4, NTO_LDS = 1024, ITER_MASKS = 16, ITER_CH = 3;
 
 __device__ inline bool in_sorted(const uint32_t* a, uint32_t n, uint32_t x)
 {
@@ -73,35 +73,103 @@ __global__ void __launch_bounds__(64 * ITER_WAVES) k_iter_rows(const uint64_t* _
                                                                const uint64_t* __restrict__ nto_row,
                                                                const uint32_t* __restrict__ nto_g,
                                                                const uint32_t* __restrict__ slot_g, uint64_t nl,
+                                                               int identity,  // slot_g[s] == s (one rank)
                                                                uint32_t* __restrict__ it_slot,
                                                                int32_t* __restrict__ it_off)
 {
     __shared__ uint32_t lds[ITER_WAVES][NTO_LDS];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __shared__ uint64_t msk[ITER_WAVES][ITER_MASKS];  // membership ballots of the first chunks
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     uint32_t* L = lds[w];
-    for (uint64_t i = (uint64_t)blockIdx.x * ITER_WAVES + w; i < nl; i += (uint64_t)gridDim.x * ITER_WAVES) {
-        const uint64_t e0 = st_row[i], e1 = st_row[i + 1], t0 = nto_row[i], t1 = nto_row[i + 1];
+    uint64_t* M = msk[w];
+    const uint64_t step = (uint64_t)gridDim.x * ITER_WAVES;
+    uint64_t i = (uint64_t)blockIdx.x * ITER_WAVES + w;
+    // the next row's bounds are loaded while this row is processed
+    uint64_t n_e0 = 0, n_e1 = 0, n_t0 = 0, n_t1 = 0;
+    if (i < nl) {
+        n_e0 = st_row[i];
+        n_e1 = st_row[i + 1];
+        n_t0 = nto_row[i];
+        n_t1 = nto_row[i + 1];
+    }
+    for (; i < nl; i += step) {
+        const uint64_t e0 = n_e0, e1 = n_e1, t0 = n_t0, t1 = n_t1;
+        if (i + step < nl) {
+            n_e0 = st_row[i + step];
+            n_e1 = st_row[i + step + 1];
+            n_t0 = nto_row[i + step];
+            n_t1 = nto_row[i + step + 1];
+        }
         const uint32_t nt = (uint32_t)(t1 - t0);
+        if (e1 - e0 <= 64 * ITER_CH && nt <= NTO_LDS) {
+            // short row (most): every load of the row issued at once and held
+            // in registers -- the row costs three dependent memory round trips
+            uint32_t sl[ITER_CH], lg[ITER_CH];
+            int32_t o[ITER_CH][3];
+            bool valid[ITER_CH];
+#pragma unroll
+            for (int j = 0; j < ITER_CH; j++) {
+                const uint64_t e = e0 + 64 * j + lane;
+                valid[j] = e < e1;
+                sl[j] = valid[j] ? st_slot[e] : 0;
+                for (int a = 0; a < 3; a++) o[j][a] = valid[j] ? st_off[3 * e + a] : 0;
+            }
+            for (uint32_t k = lane; k < nt; k += 64) L[k] = nto_g[t0 + k];
+#pragma unroll
+            for (int j = 0; j < ITER_CH; j++) lg[j] = identity ? sl[j] : valid[j] ? slot_g[sl[j]] : 0;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            uint64_t m[ITER_CH];
+            uint32_t n_in = 0;
+#pragma unroll
+            for (int j = 0; j < ITER_CH; j++) {
+                m[j] = __ballot(valid[j] && in_sorted(L, nt, lg[j]));
+                n_in += (uint32_t)__popcll(m[j]);
+            }
+            uint64_t w0 = e0, w1 = e1 - n_in;
+            const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+            for (int j = 0; j < ITER_CH; j++) {
+                const uint64_t m_in = m[j], m_out = __ballot(valid[j]) & ~m_in;
+                if (valid[j]) {
+                    const bool in = (m_in >> lane) & 1;
+                    const uint64_t d = in ? w1 + __popcll(m_in & below) : w0 + __popcll(m_out & below);
+                    it_slot[d] = sl[j];
+                    for (int a = 0; a < 3; a++) it_off[3 * d + a] = o[j][a];
+                }
+                w0 += __popcll(m_out);
+                w1 += __popcll(m_in);
+            }
+            __builtin_amdgcn_wave_barrier();  // L is rewritten for the next row
+            continue;
+        }
         const bool local = nt <= NTO_LDS;
         if (local)
             for (uint32_t k = lane; k < nt; k += 64) L[k] = nto_g[t0 + k];
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         const uint32_t* T = local ? L : nto_g + t0;
-        auto member = [&](uint64_t e) { return in_sorted(T, nt, slot_g[st_slot[e]]); };
-        // count pass: entries not in the neighbors_to row
-        uint32_t n_out = 0;
-        for (uint64_t c = e0; c < e1; c += 64) {
+        auto member = [&](uint64_t e) {
+            const uint32_t s = st_slot[e];
+            return in_sorted(T, nt, identity ? s : slot_g[s]);
+        };
+        // count pass: entries in the neighbors_to row (the first chunks'
+        // ballots are kept for the write pass)
+        uint32_t n_in = 0;
+        for (uint64_t c = e0, j = 0; c < e1; c += 64, j++) {
             const uint64_t e = c + lane;
-            const bool out = e < e1 && !member(e);
-            n_out += (uint32_t)__popcll(__ballot(out));
+            const uint64_t m = __ballot(e < e1 && member(e));
+            if (j < ITER_MASKS && lane == 0) M[j] = m;
+            n_in += (uint32_t)__popcll(m);
         }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         // write pass
-        uint64_t w0 = e0, w1 = e0 + n_out;
-        for (uint64_t c = e0; c < e1; c += 64) {
+        uint64_t w0 = e0, w1 = e1 - n_in;
+        for (uint64_t c = e0, j = 0; c < e1; c += 64, j++) {
             const uint64_t e = c + lane;
             const bool valid = e < e1;
-            const bool in = valid && member(e);
+            const bool in = valid && (j < ITER_MASKS ? (M[j] >> lane) & 1 : member(e));
             const uint64_t m_out = __ballot(valid && !in), m_in = __ballot(in);
             const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
             if (valid) {
@@ -185,19 +253,26 @@ int build_iter(const dccrgx_grid* grid, Hood& h, hipStream_t st)
         DX_CHECK(!nl || (h.d_st_row && h.d_nto_row && E->d_slot_of_g), DCCRGX_EINTERNAL,
                  "neighborhood %d has no stencil rows", h.id);
         const uint64_t cap = std::max<uint64_t>(h.st_cap, 1);
+        PhaseTimer T("build_iter");
         DX_HIP(dx_malloc(&ic->slot, cap * 4));
         DX_HIP(dx_malloc(&ic->off, cap * 12));
+        T.lap("allocations");
         if (nl) {
+            // the leaf of each slot (one rank: slot s holds leaf s)
             uint32_t* slot_g = nullptr;
-            DX_HIP(ds_malloc(&slot_g, std::max<uint64_t>(grid->n_slots, 1) * 4, st));
-            hipLaunchKernelGGL(k_slot_leaf, dim3(blocks_for(E->n)), dim3(256), 0, st, (const uint32_t*)E->d_slot_of_g,
-                               (uint64_t)E->n, slot_g);
+            const int identity = E->slot_identity ? 1 : 0;
+            if (!identity) {
+                DX_HIP(ds_malloc(&slot_g, std::max<uint64_t>(grid->n_slots, 1) * 4, st));
+                hipLaunchKernelGGL(k_slot_leaf, dim3(blocks_for(E->n)), dim3(256), 0, st,
+                                   (const uint32_t*)E->d_slot_of_g, (uint64_t)E->n, slot_g);
+            }
             const unsigned nb = (unsigned)std::min<uint64_t>((nl + ITER_WAVES - 1) / ITER_WAVES, 16384);
             hipLaunchKernelGGL(k_iter_rows, dim3(nb), dim3(64 * ITER_WAVES), 0, st, (const uint64_t*)h.d_st_row,
                                (const uint32_t*)h.d_st_slot, (const int32_t*)h.d_st_off, (const uint64_t*)h.d_nto_row,
-                               (const uint32_t*)h.d_nto_g, (const uint32_t*)slot_g, nl, ic->slot, ic->off);
+                               (const uint32_t*)h.d_nto_g, (const uint32_t*)slot_g, nl, identity, ic->slot, ic->off);
             DX_HIP(hipGetLastError());
-            ds_free(slot_g, st);
+            if (slot_g) ds_free(slot_g, st);
+            T.lap("rows");
         }
     }
     h.iter = ic;
