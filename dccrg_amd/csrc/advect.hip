@@ -252,6 +252,12 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, dou
         double ln0[6], ln1[6], ln2[6], vn[6], rn[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) {
+            // a direction no lane of the wave has a face in (z of level-0
+            // cells of a one-cell-thick grid) issues no loads
+            if (!__ballot(s[k] != 0xffffffffu)) {
+                ln0[k] = ln1[k] = ln2[k] = vn[k] = rn[k] = 0.0;
+                continue;
+            }
             const uint32_t nb = s[k] != 0xffffffffu ? s[k] : c;
             ln0[k] = adv_ld(rl0, nb);
             ln1[k] = adv_ld(rl1, nb);
