@@ -249,28 +249,36 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, dou
         const double vc3[3] = {adv_ld(rv0, c), adv_ld(rv1, c), adv_ld(rv2, c)};
         const double rho_c = adv_ld(rr, c);
         double acc = adv_ld(rf, c);
-        double ln0[6], ln1[6], ln2[6], vn[6], rn[6];
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-            // a direction no lane of the wave has a face in (z of level-0
-            // cells of a one-cell-thick grid) issues no loads
-            if (!__ballot(s[k] != 0xffffffffu)) {
-                ln0[k] = ln1[k] = ln2[k] = vn[k] = rn[k] = 0.0;
-                continue;
-            }
-            const uint32_t nb = s[k] != 0xffffffffu ? s[k] : c;
-            ln0[k] = adv_ld(rl0, nb);
-            ln1[k] = adv_ld(rl1, nb);
-            ln2[k] = adv_ld(rl2, nb);
-            vn[k] = adv_ld(k < 2 ? rv0 : k < 4 ? rv1 : rv2, nb);
-            rn[k] = adv_ld(rr, nb);
-        }
         const double vol = lc3[0] * lc3[1] * lc3[2];
+        // one axis at a time: its two faces' 10 gathers in flight together,
+        // then their terms (10 live neighbor values instead of 30: more waves
+        // per SIMD to hide the gathers' latency); the terms are added in face
+        // order as before.  An axis no lane of the wave has a face on (z of
+        // level-0 cells of a one-cell-thick grid) issues no loads.
 #pragma unroll
-        for (int k = 0; k < 6; k++)
-            if (s[k] != 0xffffffffu)
-                acc += face_term_v((k & 1) ? (k >> 1) + 1 : -((k >> 1) + 1), dt, vol, lc3, vc3, rho_c, ln0[k], ln1[k],
-                                   ln2[k], vn[k], rn[k]);
+        for (int ax = 0; ax < 3; ax++) {
+            if (!__ballot(s[2 * ax] != 0xffffffffu || s[2 * ax + 1] != 0xffffffffu)) continue;
+            const __amdgpu_buffer_rsrc_t rv = ax == 0 ? rv0 : ax == 1 ? rv1 : rv2;
+            double ln0[2], ln1[2], ln2[2], vn[2], rn[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int k = 2 * ax + h;
+                const uint32_t nb = s[k] != 0xffffffffu ? s[k] : c;
+                ln0[h] = adv_ld(rl0, nb);
+                ln1[h] = adv_ld(rl1, nb);
+                ln2[h] = adv_ld(rl2, nb);
+                vn[h] = adv_ld(rv, nb);
+                rn[h] = adv_ld(rr, nb);
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int k = 2 * ax + h;
+                if (s[k] != 0xffffffffu)
+                    acc += face_term_v(h ? ax + 1 : -(ax + 1), dt, vol, lc3, vc3, rho_c, ln0[h], ln1[h], ln2[h], vn[h],
+                                       rn[h]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
         if (*fc.over)
             for (uint64_t e = fc.o_base[q], e1 = e + fc.o_cnt[q]; e < e1; e++)
                 acc += face_term(p, c, fc.o_slot[e], fc.o_dir[e], dt, vol);
