@@ -1984,6 +1984,156 @@ __global__ void __launch_bounds__(64) k_st_inc_fill(const uint32_t* __restrict__
     }
 }
 
+// Incremental neighbors_to (one rank, after nof_incremental).  A kept leaf's
+// row -- the leaves whose neighbors_of holds it -- can change only through a
+// row that changed: it is marked if it appears in the new row of a recomputed
+// neighbors_of row or in the old row of a recomputed or removed leaf (new
+// leaves are recomputed rows themselves).  Every unmarked row is its old row
+// with the indices remapped (each leaf in it is kept with a copied row, so it
+// still holds the leaf; the remap keeps the order).  Marked rows are searched
+// anew by the reference's three-level search (nto_direct).  No symmetry of
+// the neighborhood is assumed.
+__global__ void __launch_bounds__(256) k_nto_mark_new(const uint32_t* __restrict__ aff, uint64_t naff,
+                                                      const uint64_t* __restrict__ row, const uint32_t* __restrict__ g,
+                                                      uint32_t* __restrict__ mark)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < naff; k += stride) {
+        const uint32_t j = aff[k];
+        mark[j] = 1;
+        for (uint64_t e = row[j]; e < row[j + 1]; e++) mark[g[e]] = 1;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_nto_mark_old(const uint8_t* __restrict__ touched, uint64_t on,
+                                                      const uint64_t* __restrict__ orow, const uint32_t* __restrict__ og,
+                                                      const uint32_t* __restrict__ o2n, uint32_t* __restrict__ mark)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < on; o += stride) {
+        if (!touched[o]) continue;
+        for (uint64_t e = orow[o]; e < orow[o + 1]; e++) {
+            const uint32_t t = o2n[og[e]];
+            if (t != NO_SLOT) mark[t] = 1;
+        }
+    }
+}
+
+// ids of the marked rows, in order (pos: exclusive scan of the marks)
+__global__ void __launch_bounds__(256) k_nto_marked_ids(const uint32_t* __restrict__ mark, const uint64_t* __restrict__ pos,
+                                                        uint64_t n, const uint64_t* __restrict__ leaves,
+                                                        uint64_t* __restrict__ ids)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride)
+        if (mark[j]) ids[pos[j]] = leaves[j];
+}
+
+__global__ void __launch_bounds__(256) k_nto_inc_counts(const uint32_t* __restrict__ mark,
+                                                        const uint64_t* __restrict__ pos,
+                                                        const uint64_t* __restrict__ mrow,
+                                                        const uint32_t* __restrict__ n2o,
+                                                        const uint64_t* __restrict__ orow, uint64_t n,
+                                                        uint32_t* __restrict__ cnt)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+        if (mark[j]) {
+            const uint64_t k = pos[j];
+            cnt[j] = (uint32_t)(mrow[k + 1] - mrow[k]);
+        } else {
+            const uint32_t o = n2o[j];
+            cnt[j] = (uint32_t)(orow[o + 1] - orow[o]);
+        }
+    }
+}
+
+// one wave per 64 rows, consecutive lanes on consecutive entries (k_st_inc_fill)
+__global__ void __launch_bounds__(64) k_nto_inc_fill(const uint32_t* __restrict__ mark, const uint64_t* __restrict__ pos,
+                                                     const uint64_t* __restrict__ mrow, const uint32_t* __restrict__ mval,
+                                                     const uint32_t* __restrict__ n2o, const uint32_t* __restrict__ o2n,
+                                                     const uint64_t* __restrict__ orow, const uint32_t* __restrict__ og,
+                                                     uint64_t n, const uint64_t* __restrict__ row,
+                                                     uint32_t* __restrict__ out)
+{
+    __shared__ uint64_t s_dst[65], s_src[64];
+    __shared__ uint32_t s_new[64];
+    const int lane = threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * 64;
+    const uint64_t last = r0 + 64 < n ? r0 + 64 : n;
+    s_dst[lane] = row[r0 + lane < last ? r0 + lane : last];
+    if (lane == 0) s_dst[64] = row[last];
+    uint32_t fresh = 0;
+    uint64_t src = 0;
+    if (r0 + lane < n) {
+        const uint64_t j = r0 + lane;
+        fresh = mark[j];
+        src = fresh ? mrow[pos[j]] : orow[n2o[j]];
+    }
+    s_new[lane] = fresh;
+    s_src[lane] = src;
+    __syncthreads();
+    const uint64_t end = s_dst[64];
+    for (uint64_t o = s_dst[0] + lane; o < end; o += 64) {
+        const int j = wave_row_of(s_dst, o);
+        const uint64_t e = s_src[j] + (o - s_dst[j]);
+        out[o] = s_new[j] ? mval[e] : o2n[og[e]];
+    }
+}
+
+static int nto_direct(const dccrgx_grid* grid, const Hood& h, const uint64_t* cells, uint64_t n, uint64_t** out_row,
+                      uint32_t** out_g, hipStream_t st);
+
+// the new neighbors_to CSR of every leaf (rows: leaves) from the old one; tot:
+// the new neighbors_of's entries (a bound on the transpose's)
+static int nto_incremental(dccrgx_grid* grid, Hood& h, const Hood& oh, const IncMaps& inc, uint64_t old_n,
+                           uint64_t tot, hipStream_t st)
+{
+    Explicit* E = grid->ex;
+    const uint64_t N = E->n;
+    uint32_t *d_mark = nullptr, *d_mval = nullptr, *d_cnt = nullptr;
+    uint64_t *d_pos = nullptr, *d_ids = nullptr, *d_mrow = nullptr;
+    auto done = [&](int code) {
+        for (void* q : {(void*)d_mark, (void*)d_mval, (void*)d_cnt, (void*)d_pos, (void*)d_ids, (void*)d_mrow})
+            ds_free(q, st);
+        return code;
+    };
+    if (ds_malloc(&d_mark, std::max<uint64_t>(N, 1) * 4, st) != hipSuccess ||
+        ds_malloc(&d_cnt, std::max<uint64_t>(N, 1) * 4, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "incremental neighbors_to"));
+    {
+        const Fill z[1] = {{d_mark, N * 4, 0}};
+        if (dx_fill_many(z, 1, st) != DCCRGX_OK) return done(DCCRGX_EHIP);
+    }
+    if (inc.naff)
+        hipLaunchKernelGGL(k_nto_mark_new, dim3(grid_for(inc.naff)), dim3(256), 0, st, (const uint32_t*)inc.aff,
+                           inc.naff, (const uint64_t*)h.d_nof_row, (const uint32_t*)h.d_nof_g, d_mark);
+    hipLaunchKernelGGL(k_nto_mark_old, dim3(grid_for(old_n)), dim3(256), 0, st, (const uint8_t*)inc.touched, old_n,
+                       (const uint64_t*)oh.d_nof_row, (const uint32_t*)oh.d_nof_g, (const uint32_t*)inc.o2n, d_mark);
+    uint64_t nm = 0;
+    int e = scan_counts_device(d_mark, N, &d_pos, &nm, st);  // the marked rows' places (one read-back)
+    if (e != DCCRGX_OK) return done(e);
+    if (ds_malloc(&d_ids, std::max<uint64_t>(nm, 1) * 8, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "incremental neighbors_to"));
+    hipLaunchKernelGGL(k_nto_marked_ids, dim3(grid_for(N)), dim3(256), 0, st, (const uint32_t*)d_mark,
+                       (const uint64_t*)d_pos, N, (const uint64_t*)E->d_leaves, d_ids);
+    if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "incremental neighbors_to"));
+    if ((e = nto_direct(grid, h, d_ids, nm, &d_mrow, &d_mval, st)) != DCCRGX_OK) return done(e);
+    hipLaunchKernelGGL(k_nto_inc_counts, dim3(grid_for(N)), dim3(256), 0, st, (const uint32_t*)d_mark,
+                       (const uint64_t*)d_pos, (const uint64_t*)d_mrow, (const uint32_t*)inc.n2o,
+                       (const uint64_t*)oh.d_nto_row, N, d_cnt);
+    if ((e = scan_counts_device(d_cnt, N, &h.d_nto_row, nullptr, st)) != DCCRGX_OK) return done(e);
+    if (ds_malloc(&h.d_nto_g, std::max<uint64_t>(tot, 1) * 4, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "neighbors_to lists"));
+    if (N)
+        hipLaunchKernelGGL(k_nto_inc_fill, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, (const uint32_t*)d_mark,
+                           (const uint64_t*)d_pos, (const uint64_t*)d_mrow, (const uint32_t*)d_mval,
+                           (const uint32_t*)inc.n2o, (const uint32_t*)inc.o2n, (const uint64_t*)oh.d_nto_row,
+                           (const uint32_t*)oh.d_nto_g, N, (const uint64_t*)h.d_nto_row, h.d_nto_g);
+    if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "incremental neighbors_to"));
+    return done(DCCRGX_OK);
+}
+
 int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
 {
     Explicit* E = grid->ex;
@@ -2028,13 +2178,16 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
         ~FreeIds() { ds_free(p, st); }
     } free_ids{d_local_ids, st};
     if (inc_nof)
-        DX_TRY(nof_incremental(grid, h, *hint, &tot, st, inc_st ? &inc : nullptr));
+        DX_TRY(nof_incremental(grid, h, *hint, &tot, st, &inc));
     else
         DX_TRY(nof_device(grid, h, per_rank ? d_local_ids : E->d_leaves, per_rank ? nl : N, h.d_nof_row, &h.d_nof_id,
                           &h.d_nof_off, &h.d_nof_g, &tot, st));
     T.lap("neighbors_of");
     if (per_rank) {  // neighbors_to of the local cells by the reference's search
         DX_TRY(nto_direct(grid, h, d_local_ids, nl, &h.d_nto_row, &h.d_nto_g, st));
+    } else if (inc.n2o && hint->old_h->d_nto_row && hint->old_h->d_nto_g && !test_opt(OPT_FULL_NTO, 0)) {
+        // one process after an incremental neighbors_of: the old transpose, remapped, around the changes
+        DX_TRY(nto_incremental(grid, h, *hint->old_h, inc, hint->old_ex->n, tot, st));
     } else {  // one process: the transpose of every leaf's neighbors_of (rows: leaves)
         uint32_t *d_cnt = nullptr, *d_cur = nullptr, *d_tmp = nullptr;
         DX_HIP(ds_malloc(&d_cnt, N * 4, st));
@@ -2107,7 +2260,7 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     T.lap("ghost slots");
 
     // stencil rows of local cells (iteration-cache neighbors_of: unique pairs)
-    if (inc.n2o) {  // one rank after an incremental neighbors_of: old rows remapped, the rest sorted
+    if (inc_st && inc.n2o) {  // one rank after an incremental neighbors_of: old rows remapped, the rest sorted
         const Hood& oh = *hint->old_h;
         const uint64_t na = inc.naff;
         uint64_t* d_arow = nullptr;

@@ -174,6 +174,7 @@ enum TestOpt {
     OPT_CORRUPT_GHOST,       // dccrgx_gol_step marks a ghost cell alive after each exchange
     OPT_FAIL_STOP_REFINING,  // this rank's next stop_refining decisions report ENOMEM (rank + 1)
     OPT_CHECK_INIT,          // explicit grids: check the device leaves and lookups against the host list
+    OPT_FULL_NTO,            // one rank: the full neighbors_to transpose after an incremental neighbors_of
     OPT_COUNT
 };
 int64_t test_opt(TestOpt o, int64_t dflt);

@@ -103,15 +103,20 @@ SEQ_CASES = [  # length, M, periodic, hood, P, rounds, seed
 ]
 
 
-@pytest.fixture(params=["full", "incremental", "small_walks"])
+@pytest.fixture(params=["full", "incremental", "incremental_full_nto", "small_walks"])
 def rebuild_mode(request, lib_options):
     """The rebuild's neighbors_of: recomputed for every leaf, or copied for
     rows that reference no removed leaf (explicit.hip nof_incremental; the
-    library picks it above 2^20 leaves, the test option forces it).
+    library picks it above 2^20 leaves, the test option forces it).  After
+    an incremental neighbors_of one rank also updates neighbors_to around the
+    changes (nto_incremental); incremental_full_nto keeps the full transpose.
     small_walks: override_unrefines' first pass gets a 4-entry queue, so the
     walks overflow into the second, full-size pass (amr_dev.hip k_ou_walk)."""
-    lib_options("incremental", 1 if request.param == "incremental" else 0)
-    # every rebuild compares the host-merged leaf list with the device's (explicit.hip explicit_init)
+    lib_options("incremental", 1 if request.param.startswith("incremental") else 0)
+    if request.param == "incremental_full_nto":
+        lib_options("full_nto", 1)
+    # every rebuild checks the device leaf lookups against the host leaf list (several ranks: the
+    # host-merged list; one rank: the list fetched from the device) (explicit.hip explicit_init)
     lib_options("check_init", 1)
     if request.param == "small_walks":
         lib_options("ou_small", 4)
