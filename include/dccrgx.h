@@ -548,7 +548,13 @@ int dccrgx_stop_refining(dccrgx_grid* grid, const uint64_t* const* sets, const s
  * pending); then every rank all-reduces its status and calls finish with
  * commit = 1 (adopt) when all ranks succeeded, else commit = 0 (drop: old
  * grid, this rank's requests pending).  finish(0) without a prepared
- * stop_refining is a no-op; dccrgx_stop_refining = prepare + finish(1). */
+ * stop_refining is a no-op; dccrgx_stop_refining = prepare + finish(1).
+ * A uniform grid with refine or unrefine requests switches to the explicit
+ * layout at prepare, before the decisions, and stays explicit when the
+ * stop_refining is then dropped: same leaves and data, but field device
+ * pointers and slots change (take dccrgx_field_device_ptr again).  Between
+ * prepare and finish every call that reads or changes the grid's structure
+ * or data returns DCCRGX_ESTATE. */
 int dccrgx_stop_refining_prepare(dccrgx_grid* grid, const uint64_t* const* sets, const size_t* counts,
                                  size_t* n_new);
 int dccrgx_stop_refining_finish(dccrgx_grid* grid, int32_t commit);
