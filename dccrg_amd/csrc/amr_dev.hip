@@ -766,6 +766,25 @@ static void merge_leaves_host(const std::vector<uint64_t>& old, const std::vecto
     else pool_run(nt, job);
 }
 
+// four id lists into one array of sort keys, list k tagged k above the ids' bits
+struct TagLists {
+    const uint64_t* in[4];
+    uint32_t n[4];
+    int bits;
+};
+
+__global__ void __launch_bounds__(256) k_tag_lists(TagLists t, uint64_t* __restrict__ keys)
+{
+    const uint64_t tot = (uint64_t)t.n[0] + t.n[1] + t.n[2] + t.n[3];
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += stride) {
+        uint64_t j = i;
+        int k = 0;
+        while (k < 3 && j >= t.n[k]) j -= t.n[k++];
+        keys[i] = ((uint64_t)k << t.bits) | t.in[k][j];
+    }
+}
+
 static unsigned blocks(uint64_t n, unsigned cap = 4096)
 {
     uint64_t g = (n + 255) / 256;
@@ -1104,17 +1123,25 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     }
     // the new leaf list: surviving leaves in order, merged with the sorted new ones
     uint8_t* d_keep;
-    uint64_t *d_kept, *d_sorted, *d_cnt64;
+    uint64_t *d_kept, *d_cnt64;
     DX_TRY(S.get(&d_keep, N));
     DX_TRY(S.get(&d_kept, N));
-    DX_TRY(S.get(&d_sorted, cnt[0]));
     DX_TRY(S.get(&d_cnt64, 2));
-    // the new / removed / retired lists sorted on the device (the host would
-    // sort them while the device waits), unique-d on the host after the read-back
-    uint64_t* d_ls[3];
-    const uint64_t* ls_in[3] = {o.newc, o.removed, o.retired};
-    const uint32_t ls_n[3] = {cnt[1], cnt[2], cnt[3]};
-    for (int k = 0; k < 3; k++) DX_TRY(S.get(&d_ls[k], std::max<uint32_t>(ls_n[k], 1)));
+    // the new ids and the new / removed / retired lists sorted on the device
+    // (the host would sort them while the device waits) in one radix sort:
+    // each list tagged in the two bits above the ids' bits, so the sorted
+    // keys are the four lists one after the other; the three lists are
+    // untagged and unique-d on the host after the read-back
+    int bits = 1;  // ids are at most last_cell: sort only their bits
+    while (bits < 64 && (grid->map.last_cell >> bits)) bits++;
+    DX_CHECK(bits <= 62, DCCRGX_EINTERNAL, "cell ids of %d bits", bits);
+    const uint64_t n_all = (uint64_t)cnt[0] + cnt[1] + cnt[2] + cnt[3];
+    uint64_t *d_keys, *d_all;
+    DX_TRY(S.get(&d_keys, std::max<uint64_t>(n_all, 1)));
+    DX_TRY(S.get(&d_all, std::max<uint64_t>(n_all, 1)));
+    TagLists tl{{o.added, o.newc, o.removed, o.retired}, {cnt[0], cnt[1], cnt[2], cnt[3]}, bits};
+    if (n_all) hipLaunchKernelGGL(k_tag_lists, dim3(blocks(n_all)), dim3(256), 0, st, tl, d_keys);
+    const uint64_t off_ls[3] = {cnt[0], (uint64_t)cnt[0] + cnt[1], (uint64_t)cnt[0] + cnt[1] + cnt[2]};
     // the indices of the leaves that go, ascending: a selection over the
     // leaf indices (the host merge needs them in order)
     uint32_t* d_gone;
@@ -1123,35 +1150,23 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     hipLaunchKernelGGL(k_kept_flags, dim3(bN), dim3(256), 0, st, a, d_keep);
     const hipcub::CountingInputIterator<uint32_t> leaf_idx(0);
     const hipcub::TransformInputIterator<bool, NotKept, const uint8_t*> gone_flags(d_keep, NotKept{});
-    size_t tb[6] = {0, 0, 0, 0, 0, 0};
+    size_t tb[4] = {0, 0, 0, 0};
     DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb[0], a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
-    int bits = 1;  // ids are at most last_cell: sort only their bits
-    while (bits < 64 && (grid->map.last_cell >> bits)) bits++;
-    DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb[1], o.added, d_sorted, (int)cnt[0], 0, bits, st));
-    DX_HIP(hipcub::DeviceSelect::Unique(nullptr, tb[2], d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
+    DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb[1], d_keys, d_all, (int)n_all, 0, bits + 2, st));
+    DX_HIP(hipcub::DeviceSelect::Unique(nullptr, tb[2], d_all, o.added, d_cnt64 + 1, (int)cnt[0], st));
     DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb[3], leaf_idx, gone_flags, d_gone, d_ngone, (int)N, st));
-    for (int k = 0; k < 3; k++) {
-        size_t t = 0;
-        DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, t, ls_in[k], d_ls[k], (int)ls_n[k], 0, bits, st));
-        tb[4] = std::max(tb[4], t);
-    }
-    const size_t tmax = *std::max_element(tb, tb + 6);
+    const size_t tmax = *std::max_element(tb, tb + 4);
     uint8_t* d_tmp;
     DX_TRY(S.get(&d_tmp, std::max<size_t>(tmax, 1)));
     size_t t = tmax;
     DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, t, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
     t = tmax;
-    DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, t, o.added, d_sorted, (int)cnt[0], 0, bits, st));
+    if (n_all) DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, t, d_keys, d_all, (int)n_all, 0, bits + 2, st));
     t = tmax;
-    DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, t, d_sorted, o.added, d_cnt64 + 1, (int)cnt[0], st));
+    DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, t, d_all, o.added, d_cnt64 + 1, (int)cnt[0], st));
     t = tmax;
     if (grid->ctx->comm_size > 1)  // for the host merge
         DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, t, leaf_idx, gone_flags, d_gone, d_ngone, (int)N, st));
-    for (int k = 0; k < 3; k++) {
-        if (!ls_n[k]) continue;
-        t = tmax;
-        DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, t, ls_in[k], d_ls[k], (int)ls_n[k], 0, bits, st));
-    }
     // the merge reads both counts on the device, into a list sized for the
     // most leaves there can be
     const uint64_t n_max = N + cnt[0];
@@ -1178,9 +1193,9 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     std::vector<uint32_t> gone(host_list ? ngone : 0);
     if (e == DCCRGX_OK) {
         const D2H l2[6] = {{nr.data(), d_nr, cnt[4] * 8ull},
-                           {A.new_cells.data(), d_ls[0], cnt[1] * 8ull},
-                           {A.removed.data(), d_ls[1], cnt[2] * 8ull},
-                           {retired.data(), d_ls[2], cnt[3] * 8ull},
+                           {A.new_cells.data(), d_all + off_ls[0], cnt[1] * 8ull},
+                           {A.removed.data(), d_all + off_ls[1], cnt[2] * 8ull},
+                           {retired.data(), d_all + off_ls[2], cnt[3] * 8ull},
                            {added.data(), o.added, added.size() * 8},
                            {gone.data(), d_gone, gone.size() * 4}};
         e = dx_d2h_many(ctx, l2, 6, st);
@@ -1191,7 +1206,11 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     }
     T.lap("lists read back");
     nr.insert(nr.end(), A.nr_other.begin(), A.nr_other.end());
-    for (std::vector<uint64_t>* v : {&A.new_cells, &A.removed, &retired}) v->erase(std::unique(v->begin(), v->end()), v->end());
+    const uint64_t id_mask = (1ull << bits) - 1;
+    for (std::vector<uint64_t>* v : {&A.new_cells, &A.removed, &retired}) {
+        for (uint64_t& x : *v) x &= id_mask;  // the sort's list tags
+        v->erase(std::unique(v->begin(), v->end()), v->end());
+    }
     const uint64_t n_new = nk[0] + nk[1];
     leaves_host.clear();
     if (host_list) {

@@ -683,6 +683,20 @@ void* take(Lists& m, size_t cls)
     return p;
 }
 
+// large blocks (over CACHE_MAX_BLOCK) are kept at their own size and handed
+// out for requests of 80-100 % of it; *got = the block's size
+void* take_fit(Lists& m, size_t need, size_t* got)
+{
+    for (auto it = m.lower_bound(need); it != m.end() && it->first <= need + need / 4; ++it)
+        if (!it->second.empty()) {
+            void* p = it->second.back();
+            it->second.pop_back();
+            *got = it->first;
+            return p;
+        }
+    return nullptr;
+}
+
 // pending groups whose events have all passed become idle (oldest first)
 void drain(DevCache& D)
 {
@@ -751,12 +765,17 @@ void defer(DevCache& D, std::vector<std::pair<void*, size_t>>&& blocks)
 hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_stream)
 {
     Cache& C = cache();
-    const size_t cls = bytes <= CACHE_MAX_BLOCK ? size_class(bytes) : 0;
-    if (cls) {
+    // small blocks in size classes; large ones (a view's iteration rows, big
+    // grids' lists) at their size rounded to 2 MiB, reused for requests of
+    // 80-100 % of a kept block -- a large hipFree waits for the whole device
+    const bool large = bytes > CACHE_MAX_BLOCK;
+    const size_t cls = large ? (bytes + (2ull << 20) - 1) & ~((2ull << 20) - 1) : size_class(bytes);
+    {
         std::lock_guard<std::mutex> lk(C.m);
         DevCache& D = C.dev[current_device()];
         void* q = nullptr;
-        if (!any_stream) {
+        size_t got = cls;
+        if (!any_stream && !large) {
             auto it = D.by_stream.find(st);
             if (it != D.by_stream.end() && (q = take(it->second, cls))) {
                 D.stream_bytes[st] -= cls;
@@ -765,10 +784,10 @@ hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_strea
         }
         if (!q) {
             drain(D);
-            if ((q = take(D.idle, cls))) D.idle_bytes -= cls;
+            if ((q = large ? take_fit(D.idle, cls, &got) : take(D.idle, cls))) D.idle_bytes -= got;
         }
         if (q) {
-            D.live[q] = cls;
+            D.live[q] = got;
             *p = q;
             return hipSuccess;
         }
@@ -780,8 +799,22 @@ hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_strea
     // hipMallocAsync on either runtime, none with hipMalloc or with
     // HSA_ENABLE_SDMA=0).  The cache makes the runtime call rare.
     (void)st;
-    hipError_t e = hipMalloc(p, cls ? cls : bytes);
-    if (e == hipSuccess && cls) {
+    hipError_t e = hipMalloc(p, cls);
+    if (e == hipErrorOutOfMemory) {  // the cache's idle blocks back to the device, then once more
+        (void)hipGetLastError();
+        dx_cache_trim();
+        e = hipMalloc(p, cls);
+    }
+    if (e != hipSuccess && large) {  // the rounding must not make the difference
+        (void)hipGetLastError();
+        e = hipMalloc(p, bytes);
+        if (e == hipSuccess) {
+            std::lock_guard<std::mutex> lk(C.m);
+            C.dev[current_device()].live[*p] = bytes;
+        }
+        return e;
+    }
+    if (e == hipSuccess) {
         std::lock_guard<std::mutex> lk(C.m);
         C.dev[current_device()].live[*p] = cls;
     }
@@ -801,15 +834,29 @@ void dx_cache_free_many(void* const* ps, size_t n, hipStream_t st, bool any_stre
     DevCache& D = C.dev[current_device()];
     std::vector<std::pair<void*, size_t>> blocks;
     std::vector<void*> large;
+    std::vector<std::pair<void*, size_t>> big;  // large blocks: fenced for any stream
     for (size_t i = 0; i < n; i++) {
         if (!ps[i]) continue;
         auto it = D.live.find(ps[i]);
-        if (it == D.live.end()) {  // an uncached (large) block: back to the pool
+        if (it == D.live.end()) {  // not the cache's: back to the pool
             large.push_back(ps[i]);
             continue;
         }
-        blocks.emplace_back(ps[i], it->second);
+        (it->second > CACHE_MAX_BLOCK ? big : blocks).emplace_back(ps[i], it->second);
         D.live.erase(it);
+    }
+    if (!big.empty()) {
+        std::vector<std::pair<void*, size_t>> keep;
+        size_t kept = D.idle_bytes + D.held_bytes;
+        for (auto& b : big) {
+            if (kept + b.second > CACHE_MAX_TOTAL) {  // the cache stays within its total
+                large.push_back(b.first);
+                continue;
+            }
+            kept += b.second;
+            keep.push_back(b);
+        }
+        if (!keep.empty()) defer(D, std::move(keep));
     }
     if (!any_stream) {  // ds_free: reused by `st` in stream order
         size_t& sb = D.stream_bytes[st];

@@ -47,15 +47,18 @@ int set_error(int code, const char* fmt, ...);
 // Blocks up to 256 MiB are kept in size classes when freed and handed out
 // again without a runtime call (hipFreeAsync cost ~35 us on torch's bundled
 // HIP runtime and an adaptive step freed ~60 scratch buffers -- 2 ms of the
-// step, tools/api_census.py).  A block freed with ds_free on a stream is
-// reused only by that stream (stream order keeps it safe); blocks freed with
-// dx_free / FreeBatch are reused by any stream once events recorded on every
-// library stream at the free have passed -- no host wait, so such a free
-// between a halo's start and wait does not block on the exchange.  Blocks
-// over 256 MiB, and cached blocks freed while the cache holds more than its
-// total limit, go back with hipFree, which waits for the whole device: such a
-// free between a halo's start and wait stalls the host until the exchange is
-// done (grids free them only in structural calls).  The stream-ordered pool (hipMallocAsync) is not used:
+// step, tools/api_census.py); larger blocks are kept at their size (rounded
+// to 2 MiB) and reused for requests of 80-100 % of it.  A block freed with
+// ds_free on a stream is reused only by that stream (stream order keeps it
+// safe); blocks freed with dx_free / FreeBatch (and every large block) are
+// reused by any stream once events recorded on every library stream at the
+// free have passed -- no host wait, so such a free between a halo's start
+// and wait does not block on the exchange.  Blocks freed while the cache
+// holds its total limit (8 GiB idle) go back with hipFree, which waits for
+// the whole device: such a free between a halo's start and wait stalls the
+// host until the exchange is done (grids free them only in structural
+// calls).  A hipMalloc that runs out of memory returns the idle blocks first
+// and tries again.  The stream-ordered pool (hipMallocAsync) is not used:
 // the copy engines keep stale translations for pool memory the pool re-maps,
 // and copies into fresh pool blocks landed in the wrong pages
 // (tools/micro/pool_trim_copy.hip).
