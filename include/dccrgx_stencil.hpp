@@ -228,14 +228,38 @@ struct ExplicitCell {
     __host__ __device__ inline void for_each_neighbor(G&& fn) const
     {
         const uint64_t e1 = row[q + 1];
-        for (uint64_t e = row[q]; e < e1; e++) {
+        uint64_t e = row[q];
+        auto one = [&](uint64_t k) {
             Neighbor nb;
-            nb.slot = nbr_slot[e];
-            nb.x = nbr_off[3 * e];
-            nb.y = nbr_off[3 * e + 1];
-            nb.z = nbr_off[3 * e + 2];
+            nb.slot = nbr_slot[k];
+            nb.x = nbr_off[3 * k];
+            nb.y = nbr_off[3 * k + 1];
+            nb.z = nbr_off[3 * k + 2];
             fn(nb);
+        };
+        // each lane walks its own row: four entries per 16-byte load (slots)
+        // and three (offsets) once the row is at a multiple of four -- a
+        // quarter of the load instructions, each line used for more entries
+        for (; e < e1 && (e & 3); e++) one(e);
+        for (; e + 4 <= e1; e += 4) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            typedef int32_t i4 __attribute__((ext_vector_type(4)));
+            const u4 s = *reinterpret_cast<const u4*>(nbr_slot + e);
+            const i4* po = reinterpret_cast<const i4*>(nbr_off + 3 * e);
+            const i4 o0 = po[0], o1 = po[1], o2 = po[2];
+            const int32_t o[12] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w, o2.x, o2.y, o2.z, o2.w};
+            const uint32_t sl[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                Neighbor nb;
+                nb.slot = sl[k];
+                nb.x = o[3 * k];
+                nb.y = o[3 * k + 1];
+                nb.z = o[3 * k + 2];
+                fn(nb);
+            }
         }
+        for (; e < e1; e++) one(e);
     }
 };
 
