@@ -94,20 +94,20 @@ __global__ void __launch_bounds__(256) k_face_build(const uint64_t* __restrict__
         const int64_t cl = 1ll << (M - level[local_g[q]]);
         uint32_t used = 0, k = 0;
         const uint64_t base = st_row[q];
-        for (uint64_t e = base; e < st_row[q + 1]; e++) {
-            const uint32_t nb = st_slot[e];
-            const int dir = face_dir(cl, 1ll << (M - level[nb]), st_off + 3 * e);
-            if (!dir) continue;
+        row_walk4(base, st_row[q + 1], st_slot, st_off, [&](uint64_t, uint32_t nb, int32_t x, int32_t y, int32_t z) {
+            const int32_t o[3] = {x, y, z};
+            const int dir = face_dir(cl, 1ll << (M - level[nb]), o);
+            if (!dir) return;
             const int col = 2 * ((dir > 0 ? dir : -dir) - 1) + (dir > 0 ? 1 : 0);
             if (!(used >> col & 1u)) {
                 used |= 1u << col;
                 ell_slot[col * n + q] = nb;
-                continue;
+                return;
             }
             o_slot[base + k] = nb;
             o_dir[base + k] = (int8_t)dir;
             k++;
-        }
+        });
         for (int col = 0; col < 6; col++)
             if (!(used >> col & 1u)) ell_slot[col * n + q] = 0xffffffffu;
         o_cnt[q] = k;
@@ -310,22 +310,20 @@ __global__ void __launch_bounds__(256) k_adapt_diff(const double* __restrict__ r
         const uint32_t c = local_g[q];
         const int64_t lc = 1ll << (M - level[c]);
         const double rc = rho[c];
-        for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) {
-            const uint32_t nb = st_slot[e];
+        row_walk4(st_row[q], st_row[q + 1], st_slot, st_off, [&](uint64_t, uint32_t nb, int64_t x, int64_t y, int64_t z) {
             const int64_t ln = 1ll << (M - level[nb]);
-            const int64_t x = st_off[3 * e], y = st_off[3 * e + 1], z = st_off[3 * e + 2];
             const bool face = ((x == lc || x == -ln) && y == 0 && z == 0) || ((y == lc || y == -ln) && x == 0 && z == 0) ||
                               ((z == lc || z == -ln) && x == 0 && y == 0);
-            if (!face) continue;
+            if (!face) return;
             const double rn = rho[nb];
             const double diff = fabs(rc - rn) / ((rc < rn ? rc : rn) + thr);
             // the bit pattern orders like the value only for diff >= 0; a
             // non-positive diff never raises the reference's max from 0
-            if (!(diff > 0.0)) continue;
+            if (!(diff > 0.0)) return;
             const unsigned long long k = (unsigned long long)__double_as_longlong(diff);
             atomicMax(&maxd[c], k);
             if (slot_local[nb]) atomicMax(&maxd[nb], k);
-        }
+        });
     }
 }
 

@@ -400,7 +400,7 @@ __global__ void __launch_bounds__(256) k_tr_count(const uint64_t* __restrict__ r
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += stride)
-        for (uint64_t e = row[s]; e < row[s + 1]; e++) atomicAdd(&cnt[tgt[e]], 1u);
+        row_walk4(row[s], row[s + 1], tgt, [&](uint64_t, uint32_t t) { atomicAdd(&cnt[t], 1u); });
 }
 
 __global__ void __launch_bounds__(256) k_tr_scatter(const uint64_t* __restrict__ row, const uint32_t* __restrict__ tgt,
@@ -409,10 +409,8 @@ __global__ void __launch_bounds__(256) k_tr_scatter(const uint64_t* __restrict__
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += stride)
-        for (uint64_t e = row[s]; e < row[s + 1]; e++) {
-            const uint32_t t = tgt[e];
-            out[trow[t] + atomicAdd(&cursor[t], 1u)] = (uint32_t)s;
-        }
+        row_walk4(row[s], row[s + 1], tgt,
+                  [&](uint64_t, uint32_t t) { out[trow[t] + atomicAdd(&cursor[t], 1u)] = (uint32_t)s; });
 }
 
 // per row: insertion sort + unique in place; unique count -> ucnt
@@ -543,7 +541,7 @@ __global__ void __launch_bounds__(256) k_ex_gol(const uint32_t* __restrict__ in,
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint32_t q = pos[i];
         uint32_t c = 0;
-        for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) c += in[st_slot[e]] != 0u ? 1u : 0u;
+        row_walk4(st_row[q], st_row[q + 1], st_slot, [&](uint64_t, uint32_t sl) { c += in[sl] != 0u ? 1u : 0u; });
         const uint32_t s = local_slot[q];
         cnt[s] = c;
         out[s] = c == 3u ? 1u : (c == 2u ? in[s] : 0u);

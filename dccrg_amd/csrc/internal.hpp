@@ -245,6 +245,46 @@ __device__ inline uint32_t xcd_block()
     const uint32_t bid = blockIdx.x, nwg = gridDim.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 }
+
+// One thread's walk over its own row [e, e1) of a stencil row CSR (4-byte
+// slots, 3 x 4-byte offsets): once the position is a multiple of four, four
+// entries per 16-byte load of slots and three of offsets (lanes on different
+// rows: each load is a line per lane, so fewer, wider loads use each line
+// for more entries).  fn(entry, slot, x, y, z) in row order.
+template <class F>
+__device__ inline void row_walk4(uint64_t e, uint64_t e1, const uint32_t* __restrict__ slot,
+                                 const int32_t* __restrict__ off, F&& fn)
+{
+    for (; e < e1 && (e & 3); e++) fn(e, slot[e], off[3 * e], off[3 * e + 1], off[3 * e + 2]);
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    typedef int32_t i4 __attribute__((ext_vector_type(4)));
+    for (; e + 4 <= e1; e += 4) {
+        const u4 s = *reinterpret_cast<const u4*>(slot + e);
+        const i4* po = reinterpret_cast<const i4*>(off + 3 * e);
+        const i4 o0 = po[0], o1 = po[1], o2 = po[2];
+        fn(e, s.x, o0.x, o0.y, o0.z);
+        fn(e + 1, s.y, o0.w, o1.x, o1.y);
+        fn(e + 2, s.z, o1.z, o1.w, o2.x);
+        fn(e + 3, s.w, o2.y, o2.z, o2.w);
+    }
+    for (; e < e1; e++) fn(e, slot[e], off[3 * e], off[3 * e + 1], off[3 * e + 2]);
+}
+
+// the same over a row of 4-byte values alone: fn(entry, value)
+template <class F>
+__device__ inline void row_walk4(uint64_t e, uint64_t e1, const uint32_t* __restrict__ val, F&& fn)
+{
+    for (; e < e1 && (e & 3); e++) fn(e, val[e]);
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    for (; e + 4 <= e1; e += 4) {
+        const u4 v = *reinterpret_cast<const u4*>(val + e);
+        fn(e, v.x);
+        fn(e + 1, v.y);
+        fn(e + 2, v.z);
+        fn(e + 3, v.w);
+    }
+    for (; e < e1; e++) fn(e, val[e]);
+}
 #endif
 
 __host__ __device__ inline uint64_t mulhi64(uint64_t a, uint64_t b)
