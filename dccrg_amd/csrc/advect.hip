@@ -279,9 +279,14 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, dou
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (*fc.over)
-            for (uint64_t e = fc.o_base[q], e1 = e + fc.o_cnt[q]; e < e1; e++)
-                acc += face_term(p, c, fc.o_slot[e], fc.o_dir[e], dt, vol);
+        if (*fc.over)  // further faces (finer neighbors), over the values already loaded
+            for (uint64_t e = fc.o_base[q], e1 = e + fc.o_cnt[q]; e < e1; e++) {
+                const uint32_t nb = fc.o_slot[e];
+                const int dir = fc.o_dir[e], ax = (dir > 0 ? dir : -dir) - 1;
+                const double ln0 = adv_ld(rl0, nb), ln1 = adv_ld(rl1, nb), ln2 = adv_ld(rl2, nb);
+                const double vn = adv_ld(ax == 0 ? rv0 : ax == 1 ? rv1 : rv2, nb), rn = adv_ld(rr, nb);
+                acc += face_term_v(dir, dt, vol, lc3, vc3, rho_c, ln0, ln1, ln2, vn, rn);
+            }
         if (!rho_out) {
             p.flux[c] = acc;
         } else {
