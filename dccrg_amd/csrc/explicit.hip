@@ -1688,37 +1688,57 @@ __global__ void __launch_bounds__(256) k_inc_new2old(ExView oldv, const uint64_t
     }
 }
 
-// old leaves whose row references a gone leaf (or that are gone)
+// Rows are the local cells' by local position; with one process position
+// == leaf index (the maps below are null: identity), with several a local
+// position maps to its leaf through local_g and a leaf to its position
+// through slot_of_g (local slots are [0, n_local)).  A kept leaf local
+// before is local after (owners follow the level-0 ancestor).
+__device__ inline uint32_t pos_map(const uint32_t* m, uint64_t i) { return m ? m[i] : (uint32_t)i; }
+
+// old rows that reference a gone leaf (or whose cell is gone)
 __global__ void __launch_bounds__(256) k_inc_touched(const uint64_t* __restrict__ row, const uint32_t* __restrict__ g,
-                                                     uint64_t n, const uint32_t* __restrict__ flags, uint32_t gone,
+                                                     uint64_t n, const uint32_t* __restrict__ old_pos_leaf,
+                                                     const uint32_t* __restrict__ flags, uint32_t gone,
                                                      uint8_t* __restrict__ touched)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += stride) {
-        bool t = (flags[o] & gone) != 0;
+        bool t = (flags[pos_map(old_pos_leaf, o)] & gone) != 0;
         for (uint64_t e = row[o]; e < row[o + 1] && !t; e++) t = (flags[g[e]] & gone) != 0;
         touched[o] = t ? 1 : 0;
     }
+}
+
+// the old row of new row j, or NO_SLOT: recomputed
+__device__ inline uint32_t inc_src_row(uint64_t j, const uint32_t* new_pos_leaf, const uint32_t* new2old,
+                                       const uint32_t* old_leaf_pos, uint64_t old_rows, const uint8_t* touched)
+{
+    const uint32_t o = new2old[pos_map(new_pos_leaf, j)];
+    if (o == NO_SLOT) return NO_SLOT;
+    const uint32_t p = pos_map(old_leaf_pos, o);
+    return p < old_rows && !touched[p] ? p : NO_SLOT;
 }
 
 // counts of copied rows; the other leaves listed for recomputation
 __global__ void __launch_bounds__(256) k_inc_count(const uint32_t* __restrict__ new2old,
                                                    const uint8_t* __restrict__ touched, const uint64_t* __restrict__ orow,
                                                    const uint64_t* __restrict__ leaves, uint64_t n,
+                                                   const uint32_t* __restrict__ new_pos_leaf,
+                                                   const uint32_t* __restrict__ old_leaf_pos, uint64_t old_rows,
                                                    uint64_t* __restrict__ row, uint32_t* __restrict__ aff,
                                                    uint64_t* __restrict__ aff_ids, uint32_t* __restrict__ naff)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
-        const uint32_t o = new2old[j];
-        const bool copied = o != NO_SLOT && !touched[o];
+        const uint32_t o = inc_src_row(j, new_pos_leaf, new2old, old_leaf_pos, old_rows, touched);
+        const bool copied = o != NO_SLOT;
         const uint32_t k = wave_reserve(naff, copied ? 0u : 1u);
         if (copied) {
             row[j + 1] = orow[o + 1] - orow[o];
             continue;
         }
         aff[k] = (uint32_t)j;
-        aff_ids[k] = leaves[j];
+        aff_ids[k] = leaves[pos_map(new_pos_leaf, j)];
     }
 }
 
@@ -1735,7 +1755,9 @@ __global__ void __launch_bounds__(256) k_inc_aff_rows(const uint32_t* __restrict
 
 // copied rows: one wave per 64 new leaves, consecutive lanes on consecutive entries
 __global__ void __launch_bounds__(64) k_inc_copy(const uint32_t* __restrict__ new2old, const uint8_t* __restrict__ touched,
-                                                 uint64_t n, const uint64_t* __restrict__ orow,
+                                                 uint64_t n, const uint32_t* __restrict__ new_pos_leaf,
+                                                 const uint32_t* __restrict__ old_leaf_pos, uint64_t old_rows,
+                                                 const uint64_t* __restrict__ orow,
                                                  const uint64_t* __restrict__ oid, const int32_t* __restrict__ ooff,
                                                  const uint32_t* __restrict__ og, const uint32_t* __restrict__ old2new,
                                                  const uint64_t* __restrict__ row, uint64_t* __restrict__ ids,
@@ -1748,8 +1770,8 @@ __global__ void __launch_bounds__(64) k_inc_copy(const uint32_t* __restrict__ ne
     // rows of recomputed leaves take no entries here (empty source runs)
     uint64_t len = 0, src = 0;
     if (j < n) {
-        const uint32_t o = new2old[j];
-        if (o != NO_SLOT && !touched[o]) {
+        const uint32_t o = inc_src_row(j, new_pos_leaf, new2old, old_leaf_pos, old_rows, touched);
+        if (o != NO_SLOT) {
             src = orow[o];
             len = orow[o + 1] - src;
         }
@@ -1818,6 +1840,12 @@ static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_
     Ctx* ctx = grid->ctx;
     const uint64_t N = E->n, oN = H.old_ex->n;
     const Hood& oh = *H.old_h;
+    // rows: local positions (several processes: through the position maps)
+    const bool per_rank = ctx->comm_size > 1;
+    const uint64_t R = per_rank ? E->n_local() : N, oR = per_rank ? oh.n_rows : oN;
+    const uint32_t* new_pos_leaf = per_rank ? E->d_local_g : nullptr;
+    const uint32_t* old_pos_leaf = per_rank ? H.old_ex->d_local_g : nullptr;
+    const uint32_t* old_leaf_pos = per_rank ? H.old_ex->d_slot_of_g : nullptr;
     const ExView v = view(grid);
     ExView ov = v;
     ov.keys = H.old_ex->d_keys;
@@ -1836,8 +1864,9 @@ static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_
         return code;
     };
     if (ds_malloc(&d_n2o, N * 4, st) != hipSuccess || ds_malloc(&d_o2n, oN * 4, st) != hipSuccess ||
-        ds_malloc(&d_aff, N * 4, st) != hipSuccess || ds_malloc(&d_naff, 16, st) != hipSuccess ||
-        ds_malloc(&d_touched, oN, st) != hipSuccess || ds_malloc(&d_aff_ids, N * 8, st) != hipSuccess ||
+        ds_malloc(&d_aff, std::max<uint64_t>(R, 1) * 4, st) != hipSuccess || ds_malloc(&d_naff, 16, st) != hipSuccess ||
+        ds_malloc(&d_touched, std::max<uint64_t>(oR, 1), st) != hipSuccess ||
+        ds_malloc(&d_aff_ids, std::max<uint64_t>(R, 1) * 8, st) != hipSuccess ||
         ds_malloc(&d_err, 16, st) != hipSuccess)
         return done(set_error(DCCRGX_ENOMEM, "incremental neighbor lists"));
     {
@@ -1846,11 +1875,13 @@ static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_
     }
     hipLaunchKernelGGL(k_inc_new2old, dim3(grid_for(N)), dim3(256), 0, st, ov, (const uint64_t*)E->d_leaves, N, d_n2o,
                        d_o2n);
-    hipLaunchKernelGGL(k_inc_touched, dim3(grid_for(oN)), dim3(256), 0, st, (const uint64_t*)oh.d_nof_row,
-                       (const uint32_t*)oh.d_nof_g, oN, H.old_flags, H.gone_bit, d_touched);
-    hipLaunchKernelGGL(k_inc_count, dim3(grid_for(N)), dim3(256), 0, st, (const uint32_t*)d_n2o,
-                       (const uint8_t*)d_touched, (const uint64_t*)oh.d_nof_row, (const uint64_t*)E->d_leaves, N,
-                       h.d_nof_row, d_aff, d_aff_ids, d_naff);
+    if (oR)
+        hipLaunchKernelGGL(k_inc_touched, dim3(grid_for(oR)), dim3(256), 0, st, (const uint64_t*)oh.d_nof_row,
+                           (const uint32_t*)oh.d_nof_g, oR, old_pos_leaf, H.old_flags, H.gone_bit, d_touched);
+    if (R)
+        hipLaunchKernelGGL(k_inc_count, dim3(grid_for(R)), dim3(256), 0, st, (const uint32_t*)d_n2o,
+                           (const uint8_t*)d_touched, (const uint64_t*)oh.d_nof_row, (const uint64_t*)E->d_leaves, R,
+                           new_pos_leaf, old_leaf_pos, oR, h.d_nof_row, d_aff, d_aff_ids, d_naff);
     if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "incremental neighbor lists"));
     uint32_t naff = 0;
     int s = dx_d2h(ctx, &naff, d_naff, 4, st);
@@ -1865,9 +1896,9 @@ static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_
         hipLaunchKernelGGL(k_inc_aff_rows, dim3(grid_for(naff)), dim3(256), 0, st, (const uint32_t*)d_aff,
                            (uint64_t)naff, (const uint64_t*)d_crow, h.d_nof_row, d_start, 0);
     }
-    if ((s = device_scan_rows(h.d_nof_row, N, st, nullptr)) != DCCRGX_OK) return done(s);
+    if ((s = device_scan_rows(h.d_nof_row, R, st, nullptr)) != DCCRGX_OK) return done(s);
     uint64_t back[2] = {0, 0};  // error word, total
-    hipMemcpyAsync(d_err + 2, h.d_nof_row + N, 8, hipMemcpyDeviceToDevice, st);
+    hipMemcpyAsync(d_err + 2, h.d_nof_row + R, 8, hipMemcpyDeviceToDevice, st);
     if ((s = dx_d2h(ctx, back, d_err, 16, st)) != DCCRGX_OK) return done(s);
     if (back[0] & 0xffffffffu)
         return done(set_error(back[0] & 1 ? DCCRGX_ENOTFOUND : DCCRGX_EINTERNAL,
@@ -1877,8 +1908,10 @@ static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_
     if (ds_malloc(&h.d_nof_id, t * 8, st) != hipSuccess || ds_malloc(&h.d_nof_off, t * 12, st) != hipSuccess ||
         ds_malloc(&h.d_nof_g, t * 4, st) != hipSuccess)
         return done(set_error(DCCRGX_ENOMEM, "neighbor lists of %llu entries", (unsigned long long)*total));
-    hipLaunchKernelGGL(k_inc_copy, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, (const uint32_t*)d_n2o,
-                       (const uint8_t*)d_touched, N, (const uint64_t*)oh.d_nof_row, (const uint64_t*)oh.d_nof_id,
+    if (R)
+        hipLaunchKernelGGL(k_inc_copy, dim3((unsigned)((R + 63) / 64)), dim3(64), 0, st, (const uint32_t*)d_n2o,
+                       (const uint8_t*)d_touched, R, new_pos_leaf, old_leaf_pos, oR, (const uint64_t*)oh.d_nof_row,
+                       (const uint64_t*)oh.d_nof_id,
                        (const int32_t*)oh.d_nof_off, (const uint32_t*)oh.d_nof_g, (const uint32_t*)d_o2n,
                        (const uint64_t*)h.d_nof_row, h.d_nof_id, h.d_nof_off, h.d_nof_g);
     if (naff) {  // the recomputed rows, each thread at its row's place
@@ -2160,7 +2193,7 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     DX_HIP(ds_malloc(&h.d_nof_row, (nl + 1) * 8, st));
     uint64_t tot = 0;
     IncMaps inc;
-    const bool inc_nof = !per_rank && hint && hint->old_h && hint->old_h->d_nof_row && hint->old_h->items == h.items &&
+    const bool inc_nof = hint && hint->old_h && hint->old_h->d_nof_row && hint->old_h->items == h.items &&
                          hint->old_ex && incremental_rebuild(hint->old_ex->n);
     // the stencil rows follow incrementally where slots are leaf indices before and after
     const bool inc_st = inc_nof && E->slot_identity && hint->old_ex->slot_identity && hint->old_h->d_st_row &&
