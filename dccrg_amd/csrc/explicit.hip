@@ -597,6 +597,16 @@ __global__ void __launch_bounds__(64) k_rows_gather(const uint32_t* __restrict__
     if (r0 + lane < n) s_src[lane] = src_row[gq[r0 + lane]];
     __syncthreads();
     const uint64_t end = s_dst[64];
+    // the 64 rows one run of the source (queries of consecutive cells: every
+    // leaf, a slab): a straight copy, no row search per entry
+    const bool run = r0 + lane + 1 >= last || s_src[lane + 1] == s_src[lane] + (s_dst[lane + 1] - s_dst[lane]);
+    if (__all(run)) {
+        const uint64_t d0 = s_dst[0], s0 = s_src[0];
+        for (uint64_t e = d0 + lane; e < end; e += 64) ids[e] = src_id[s0 + (e - d0)];
+        if (off3)
+            for (uint64_t w = lane; w < 3 * (end - d0); w += 64) off3[3 * d0 + w] = src_off[3 * s0 + w];
+        return;
+    }
     for (uint64_t e = s_dst[0] + lane; e < end; e += 64) {
         const int j = wave_row_of(s_dst, e);
         const uint64_t src = s_src[j] + (e - s_dst[j]);
@@ -623,6 +633,12 @@ __global__ void __launch_bounds__(64) k_rows_gather_g(const uint32_t* __restrict
     if (r0 + lane < n) s_src[lane] = src_row[gq[r0 + lane]];
     __syncthreads();
     const uint64_t end = s_dst[64];
+    const bool run = r0 + lane + 1 >= last || s_src[lane + 1] == s_src[lane] + (s_dst[lane + 1] - s_dst[lane]);
+    if (__all(run)) {  // one run of the source (see k_rows_gather)
+        const uint64_t d0 = s_dst[0], s0 = s_src[0];
+        for (uint64_t e = d0 + lane; e < end; e += 64) ids[e] = leaves[src_g[s0 + (e - d0)]];
+        return;
+    }
     for (uint64_t e = s_dst[0] + lane; e < end; e += 64) {
         const int j = wave_row_of(s_dst, e);
         ids[e] = leaves[src_g[s_src[j] + (e - s_dst[j])]];
