@@ -2730,10 +2730,13 @@ int explicit_neighbors_of(const dccrgx_grid* grid, const Hood& h, const uint64_t
         hipLaunchKernelGGL(k_ex_query_rows, dim3(grid_for(n)), dim3(256), 0, st, view(grid), cells, n, h.d_nof_row,
                            (const uint32_t*)E->d_slot_of_g, E->n_local(), gq, row, d_err);
     uint64_t total = 0;
-    int s = device_scan_rows(row, n, st, &total);  // synchronises (total)
+    int s = device_scan_rows(row, n, st, nullptr);
     if (s != DCCRGX_OK) return done(s);
     int32_t err = 0;
-    if ((s = dx_d2h(grid->ctx, &err, d_err, 4, st)) != DCCRGX_OK) return done(s);
+    {  // the total and the error word behind one synchronisation
+        const D2H rb[2] = {{&total, row + n, 8}, {&err, d_err, 4}};
+        if ((s = dx_d2h_many(grid->ctx, rb, 2, st)) != DCCRGX_OK) return done(s);
+    }
     if (err & 1) return done(set_error(DCCRGX_ENOTFOUND, "cell does not exist"));
     if (err & 4) {  // rows of other processes' cells: searched now (the reference's lists of every cell)
         if (hipMemsetAsync(d_err, 0, 4, st) != hipSuccess) return done(set_error(DCCRGX_EHIP, "memset"));
