@@ -2076,11 +2076,15 @@ __global__ void __launch_bounds__(256) k_nto_marked_ids(const uint32_t* __restri
         if (mark[j]) ids[pos[j]] = leaves[j];
 }
 
+// (rows: local positions; new_pos_leaf / old_leaf_pos: the position maps of
+// several processes, null with one -- see k_inc_touched)
 __global__ void __launch_bounds__(256) k_nto_inc_counts(const uint32_t* __restrict__ mark,
                                                         const uint64_t* __restrict__ pos,
                                                         const uint64_t* __restrict__ mrow,
                                                         const uint32_t* __restrict__ n2o,
                                                         const uint64_t* __restrict__ orow, uint64_t n,
+                                                        const uint32_t* __restrict__ new_pos_leaf,
+                                                        const uint32_t* __restrict__ old_leaf_pos,
                                                         uint32_t* __restrict__ cnt)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -2089,7 +2093,7 @@ __global__ void __launch_bounds__(256) k_nto_inc_counts(const uint32_t* __restri
             const uint64_t k = pos[j];
             cnt[j] = (uint32_t)(mrow[k + 1] - mrow[k]);
         } else {
-            const uint32_t o = n2o[j];
+            const uint32_t o = pos_map(old_leaf_pos, n2o[pos_map(new_pos_leaf, j)]);
             cnt[j] = (uint32_t)(orow[o + 1] - orow[o]);
         }
     }
@@ -2100,8 +2104,9 @@ __global__ void __launch_bounds__(64) k_nto_inc_fill(const uint32_t* __restrict_
                                                      const uint64_t* __restrict__ mrow, const uint32_t* __restrict__ mval,
                                                      const uint32_t* __restrict__ n2o, const uint32_t* __restrict__ o2n,
                                                      const uint64_t* __restrict__ orow, const uint32_t* __restrict__ og,
-                                                     uint64_t n, const uint64_t* __restrict__ row,
-                                                     uint32_t* __restrict__ out)
+                                                     uint64_t n, const uint32_t* __restrict__ new_pos_leaf,
+                                                     const uint32_t* __restrict__ old_leaf_pos,
+                                                     const uint64_t* __restrict__ row, uint32_t* __restrict__ out)
 {
     __shared__ uint64_t s_dst[65], s_src[64];
     __shared__ uint32_t s_new[64];
@@ -2115,7 +2120,7 @@ __global__ void __launch_bounds__(64) k_nto_inc_fill(const uint32_t* __restrict_
     if (r0 + lane < n) {
         const uint64_t j = r0 + lane;
         fresh = mark[j];
-        src = fresh ? mrow[pos[j]] : orow[n2o[j]];
+        src = fresh ? mrow[pos[j]] : orow[pos_map(old_leaf_pos, n2o[pos_map(new_pos_leaf, j)])];
     }
     s_new[lane] = fresh;
     s_src[lane] = src;
@@ -2168,7 +2173,7 @@ static int nto_incremental(dccrgx_grid* grid, Hood& h, const Hood& oh, const Inc
     if ((e = nto_direct(grid, h, d_ids, nm, &d_mrow, &d_mval, st)) != DCCRGX_OK) return done(e);
     hipLaunchKernelGGL(k_nto_inc_counts, dim3(grid_for(N)), dim3(256), 0, st, (const uint32_t*)d_mark,
                        (const uint64_t*)d_pos, (const uint64_t*)d_mrow, (const uint32_t*)inc.n2o,
-                       (const uint64_t*)oh.d_nto_row, N, d_cnt);
+                       (const uint64_t*)oh.d_nto_row, N, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_cnt);
     if ((e = scan_counts_device(d_cnt, N, &h.d_nto_row, nullptr, st)) != DCCRGX_OK) return done(e);
     if (ds_malloc(&h.d_nto_g, std::max<uint64_t>(tot, 1) * 4, st) != hipSuccess)
         return done(set_error(DCCRGX_ENOMEM, "neighbors_to lists"));
@@ -2176,7 +2181,137 @@ static int nto_incremental(dccrgx_grid* grid, Hood& h, const Hood& oh, const Inc
         hipLaunchKernelGGL(k_nto_inc_fill, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, st, (const uint32_t*)d_mark,
                            (const uint64_t*)d_pos, (const uint64_t*)d_mrow, (const uint32_t*)d_mval,
                            (const uint32_t*)inc.n2o, (const uint32_t*)inc.o2n, (const uint64_t*)oh.d_nto_row,
-                           (const uint32_t*)oh.d_nto_g, N, (const uint64_t*)h.d_nto_row, h.d_nto_g);
+                           (const uint32_t*)oh.d_nto_g, N, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                           (const uint64_t*)h.d_nto_row, h.d_nto_g);
+    if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "incremental neighbors_to"));
+    return done(DCCRGX_OK);
+}
+
+// Several processes: a local cell's neighbors_to row holds cells of any
+// process, whose neighbors_of rows this rank does not keep, so the marks
+// come from the leaves instead.  Whether a kept leaf c is in the neighbors_of
+// of a kept leaf d depends on those two cells alone (d's windows and c's
+// extent), so a kept cell's row changes only by leaves that are gone (they
+// drop out of it) or new (they may name it).  Marked: new cells, kept cells
+// whose old row holds a gone leaf, and cells some new leaf (of any process:
+// the leaf set is replicated) names in its neighbors_of; they are searched
+// anew (nto_direct), every other row is its old row remapped.
+__global__ void __launch_bounds__(256) k_nto_is_new(const uint32_t* __restrict__ n2o, uint64_t n,
+                                                    uint32_t* __restrict__ flag)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) flag[j] = n2o[j] == NO_SLOT;
+}
+
+__global__ void __launch_bounds__(256) k_nto_mark_ranks(const uint32_t* __restrict__ local_g, uint64_t nl,
+                                                        const uint32_t* __restrict__ n2o,
+                                                        const uint32_t* __restrict__ slot_of_g,
+                                                        const uint32_t* __restrict__ tgt, uint64_t nt,
+                                                        const uint64_t* __restrict__ orow,
+                                                        const uint32_t* __restrict__ og,
+                                                        const uint32_t* __restrict__ old_local_g, uint64_t onl,
+                                                        const uint32_t* __restrict__ flags, uint32_t gone,
+                                                        const uint32_t* __restrict__ o2n, uint32_t* __restrict__ mark)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (size_t q = t0; q < nl; q += stride)  // new cells
+        if (n2o[local_g[q]] == NO_SLOT) mark[q] = 1;
+    for (size_t e = t0; e < nt; e += stride) {  // named by a new leaf
+        const uint32_t sl = slot_of_g[tgt[e]];
+        if (sl < nl) mark[sl] = 1;
+    }
+    for (size_t p = t0; p < onl; p += stride) {  // old rows holding a gone leaf
+        bool g = false;
+        for (uint64_t e = orow[p]; e < orow[p + 1] && !g; e++) g = (flags[og[e]] & gone) != 0;
+        if (!g) continue;
+        const uint32_t j = o2n[old_local_g[p]];
+        const uint32_t sl = j == NO_SLOT ? NO_SLOT : slot_of_g[j];
+        if (sl < nl) mark[sl] = 1;
+    }
+}
+
+// marked positions' ids, in order (pos: exclusive scan of the marks)
+__global__ void __launch_bounds__(256) k_nto_marked_pos_ids(const uint32_t* __restrict__ mark,
+                                                            const uint64_t* __restrict__ pos, uint64_t n,
+                                                            const uint32_t* __restrict__ local_g,
+                                                            const uint64_t* __restrict__ leaves,
+                                                            uint64_t* __restrict__ ids)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride)
+        if (mark[q]) ids[pos[q]] = leaves[local_g[q]];
+}
+
+static int nto_incremental_ranks(dccrgx_grid* grid, Hood& h, const NofHint& H, const IncMaps& inc, hipStream_t st)
+{
+    Explicit* E = grid->ex;
+    const Explicit* O = H.old_ex;
+    const Hood& oh = *H.old_h;
+    const uint64_t N = E->n, nl = E->n_local(), onl = oh.n_rows;
+    uint32_t *d_isnew = nullptr, *d_mark = nullptr, *d_cnt = nullptr, *d_mval = nullptr, *d_ng = nullptr;
+    uint64_t *d_npos = nullptr, *d_nids = nullptr, *d_nrow = nullptr, *d_nid = nullptr, *d_mpos = nullptr,
+             *d_mids = nullptr, *d_mrow = nullptr;
+    int32_t* d_noff = nullptr;
+    auto done = [&](int code) {
+        for (void* q : {(void*)d_isnew, (void*)d_mark, (void*)d_cnt, (void*)d_mval, (void*)d_ng, (void*)d_npos,
+                        (void*)d_nids, (void*)d_nrow, (void*)d_nid, (void*)d_mpos, (void*)d_mids, (void*)d_mrow,
+                        (void*)d_noff})
+            ds_free(q, st);
+        return code;
+    };
+    // the new leaves of every process and their neighbors_of
+    if (ds_malloc(&d_isnew, std::max<uint64_t>(N, 1) * 4, st) != hipSuccess ||
+        ds_malloc(&d_mark, std::max<uint64_t>(nl, 1) * 4, st) != hipSuccess ||
+        ds_malloc(&d_cnt, std::max<uint64_t>(nl, 1) * 4, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "incremental neighbors_to"));
+    hipLaunchKernelGGL(k_nto_is_new, dim3(grid_for(N)), dim3(256), 0, st, (const uint32_t*)inc.n2o, N, d_isnew);
+    uint64_t n_new = 0;
+    int e = scan_counts_device(d_isnew, N, &d_npos, &n_new, st);
+    if (e != DCCRGX_OK) return done(e);
+    if (ds_malloc(&d_nids, std::max<uint64_t>(n_new, 1) * 8, st) != hipSuccess ||
+        ds_malloc(&d_nrow, (n_new + 1) * 8, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "incremental neighbors_to"));
+    hipLaunchKernelGGL(k_nto_marked_ids, dim3(grid_for(N)), dim3(256), 0, st, (const uint32_t*)d_isnew,
+                       (const uint64_t*)d_npos, N, (const uint64_t*)E->d_leaves, d_nids);
+    uint64_t nt = 0;
+    if ((e = nof_device(grid, h, d_nids, n_new, d_nrow, &d_nid, &d_noff, &d_ng, &nt, st)) != DCCRGX_OK)
+        return done(e);
+    {
+        const Fill z[1] = {{d_mark, nl * 4, 0}};
+        if (nl && dx_fill_many(z, 1, st) != DCCRGX_OK) return done(DCCRGX_EHIP);
+    }
+    const uint64_t most = std::max<uint64_t>({nl, nt, onl, 1});
+    hipLaunchKernelGGL(k_nto_mark_ranks, dim3(grid_for(most)), dim3(256), 0, st, (const uint32_t*)E->d_local_g, nl,
+                       (const uint32_t*)inc.n2o, (const uint32_t*)E->d_slot_of_g, (const uint32_t*)d_ng, nt,
+                       (const uint64_t*)oh.d_nto_row, (const uint32_t*)oh.d_nto_g, (const uint32_t*)O->d_local_g, onl,
+                       H.old_flags, H.gone_bit, (const uint32_t*)inc.o2n, d_mark);
+    // the marked cells searched anew
+    uint64_t nm = 0;
+    if ((e = scan_counts_device(d_mark, nl, &d_mpos, &nm, st)) != DCCRGX_OK) return done(e);
+    if (ds_malloc(&d_mids, std::max<uint64_t>(nm, 1) * 8, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "incremental neighbors_to"));
+    if (nl)
+        hipLaunchKernelGGL(k_nto_marked_pos_ids, dim3(grid_for(nl)), dim3(256), 0, st, (const uint32_t*)d_mark,
+                           (const uint64_t*)d_mpos, nl, (const uint32_t*)E->d_local_g, (const uint64_t*)E->d_leaves,
+                           d_mids);
+    if ((e = nto_direct(grid, h, d_mids, nm, &d_mrow, &d_mval, st)) != DCCRGX_OK) return done(e);
+    // every row: marked ones from the search, the others from the old rows
+    if (nl)
+        hipLaunchKernelGGL(k_nto_inc_counts, dim3(grid_for(nl)), dim3(256), 0, st, (const uint32_t*)d_mark,
+                           (const uint64_t*)d_mpos, (const uint64_t*)d_mrow, (const uint32_t*)inc.n2o,
+                           (const uint64_t*)oh.d_nto_row, nl, (const uint32_t*)E->d_local_g,
+                           (const uint32_t*)O->d_slot_of_g, d_cnt);
+    uint64_t total = 0;
+    if ((e = scan_counts_device(d_cnt, nl, &h.d_nto_row, &total, st)) != DCCRGX_OK) return done(e);
+    if (ds_malloc(&h.d_nto_g, std::max<uint64_t>(total, 1) * 4, st) != hipSuccess)
+        return done(set_error(DCCRGX_ENOMEM, "neighbors_to lists"));
+    if (nl)
+        hipLaunchKernelGGL(k_nto_inc_fill, dim3((unsigned)((nl + 63) / 64)), dim3(64), 0, st, (const uint32_t*)d_mark,
+                           (const uint64_t*)d_mpos, (const uint64_t*)d_mrow, (const uint32_t*)d_mval,
+                           (const uint32_t*)inc.n2o, (const uint32_t*)inc.o2n, (const uint64_t*)oh.d_nto_row,
+                           (const uint32_t*)oh.d_nto_g, nl, (const uint32_t*)E->d_local_g,
+                           (const uint32_t*)O->d_slot_of_g, (const uint64_t*)h.d_nto_row, h.d_nto_g);
     if (hipGetLastError() != hipSuccess) return done(set_error(DCCRGX_EHIP, "incremental neighbors_to"));
     return done(DCCRGX_OK);
 }
@@ -2230,7 +2365,10 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
         DX_TRY(nof_device(grid, h, per_rank ? d_local_ids : E->d_leaves, per_rank ? nl : N, h.d_nof_row, &h.d_nof_id,
                           &h.d_nof_off, &h.d_nof_g, &tot, st));
     T.lap("neighbors_of");
-    if (per_rank) {  // neighbors_to of the local cells by the reference's search
+    if (per_rank && inc.n2o && hint->old_h->d_nto_row && hint->old_h->d_nto_g && !test_opt(OPT_FULL_NTO, 0)) {
+        // several processes after an incremental neighbors_of: the old rows around the changes
+        DX_TRY(nto_incremental_ranks(grid, h, *hint, inc, st));
+    } else if (per_rank) {  // neighbors_to of the local cells by the reference's search
         DX_TRY(nto_direct(grid, h, d_local_ids, nl, &h.d_nto_row, &h.d_nto_g, st));
     } else if (inc.n2o && hint->old_h->d_nto_row && hint->old_h->d_nto_g && !test_opt(OPT_FULL_NTO, 0)) {
         // one process after an incremental neighbors_of: the old transpose, remapped, around the changes
