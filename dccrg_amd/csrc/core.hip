@@ -799,6 +799,9 @@ hipError_t dx_cache_alloc(void** p, size_t bytes, hipStream_t st, bool any_strea
     // hipMallocAsync on either runtime, none with hipMalloc or with
     // HSA_ENABLE_SDMA=0).  The cache makes the runtime call rare.
     (void)st;
+    // a huge array (a headline-size field): the idle cached blocks go back
+    // first, so that it is not placed around them
+    if (bytes >= (4ull << 30)) dx_cache_trim();
     hipError_t e = hipMalloc(p, cls);
     if (e == hipErrorOutOfMemory) {  // the cache's idle blocks back to the device, then once more
         (void)hipGetLastError();
