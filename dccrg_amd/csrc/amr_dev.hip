@@ -781,7 +781,7 @@ __global__ void __launch_bounds__(256) k_tag_lists(TagLists t, uint64_t* __restr
         uint64_t j = i;
         int k = 0;
         while (k < 3 && j >= t.n[k]) j -= t.n[k++];
-        keys[i] = ((uint64_t)k << t.bits) | t.in[k][j];
+        keys[i] = (t.bits < 64 ? (uint64_t)k << t.bits : 0) | t.in[k][j];
     }
 }
 
@@ -1134,14 +1134,18 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     // untagged and unique-d on the host after the read-back
     int bits = 1;  // ids are at most last_cell: sort only their bits
     while (bits < 64 && (grid->map.last_cell >> bits)) bits++;
-    DX_CHECK(bits <= 62, DCCRGX_EINTERNAL, "cell ids of %d bits", bits);
+    // (ids of more than 62 bits leave no room for the tags: the four lists
+    // are then sorted one by one into the same places)
+    const bool tagged = bits <= 62;
+    const int sort_bits = tagged ? bits + 2 : bits;
     const uint64_t n_all = (uint64_t)cnt[0] + cnt[1] + cnt[2] + cnt[3];
     uint64_t *d_keys, *d_all;
     DX_TRY(S.get(&d_keys, std::max<uint64_t>(n_all, 1)));
     DX_TRY(S.get(&d_all, std::max<uint64_t>(n_all, 1)));
-    TagLists tl{{o.added, o.newc, o.removed, o.retired}, {cnt[0], cnt[1], cnt[2], cnt[3]}, bits};
+    TagLists tl{{o.added, o.newc, o.removed, o.retired}, {cnt[0], cnt[1], cnt[2], cnt[3]}, tagged ? bits : 64};
     if (n_all) hipLaunchKernelGGL(k_tag_lists, dim3(blocks(n_all)), dim3(256), 0, st, tl, d_keys);
     const uint64_t off_ls[3] = {cnt[0], (uint64_t)cnt[0] + cnt[1], (uint64_t)cnt[0] + cnt[1] + cnt[2]};
+    const uint64_t off4[5] = {0, off_ls[0], off_ls[1], off_ls[2], n_all};
     // the indices of the leaves that go, ascending: a selection over the
     // leaf indices (the host merge needs them in order)
     uint32_t* d_gone;
@@ -1152,7 +1156,7 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     const hipcub::TransformInputIterator<bool, NotKept, const uint8_t*> gone_flags(d_keep, NotKept{});
     size_t tb[4] = {0, 0, 0, 0};
     DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb[0], a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
-    DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb[1], d_keys, d_all, (int)n_all, 0, bits + 2, st));
+    DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb[1], d_keys, d_all, (int)n_all, 0, sort_bits, st));
     DX_HIP(hipcub::DeviceSelect::Unique(nullptr, tb[2], d_all, o.added, d_cnt64 + 1, (int)cnt[0], st));
     DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb[3], leaf_idx, gone_flags, d_gone, d_ngone, (int)N, st));
     const size_t tmax = *std::max_element(tb, tb + 4);
@@ -1161,7 +1165,17 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     size_t t = tmax;
     DX_HIP(hipcub::DeviceSelect::Flagged(d_tmp, t, a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
     t = tmax;
-    if (n_all) DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, t, d_keys, d_all, (int)n_all, 0, bits + 2, st));
+    if (tagged && n_all) {
+        DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, t, d_keys, d_all, (int)n_all, 0, sort_bits, st));
+    } else {
+        for (int k = 0; k < 4; k++) {
+            const uint64_t nk = off4[k + 1] - off4[k];
+            if (!nk) continue;
+            t = tmax;
+            DX_HIP(hipcub::DeviceRadixSort::SortKeys(d_tmp, t, d_keys + off4[k], d_all + off4[k], (int)nk, 0,
+                                                     sort_bits, st));
+        }
+    }
     t = tmax;
     DX_HIP(hipcub::DeviceSelect::Unique(d_tmp, t, d_all, o.added, d_cnt64 + 1, (int)cnt[0], st));
     t = tmax;
@@ -1206,7 +1220,7 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     }
     T.lap("lists read back");
     nr.insert(nr.end(), A.nr_other.begin(), A.nr_other.end());
-    const uint64_t id_mask = (1ull << bits) - 1;
+    const uint64_t id_mask = tagged ? (1ull << bits) - 1 : ~0ull;
     for (std::vector<uint64_t>* v : {&A.new_cells, &A.removed, &retired}) {
         for (uint64_t& x : *v) x &= id_mask;  // the sort's list tags
         v->erase(std::unique(v->begin(), v->end()), v->end());

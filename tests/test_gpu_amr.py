@@ -593,3 +593,29 @@ def test_calls_between_prepare_and_finish_are_refused():
     finally:
         g.close()
         ctx.close()
+
+
+def test_ids_of_64_bits():
+    """A 1x1x1 grid at the largest refinement level it allows (21): its ids
+    need all 64 bits, so the device decisions sort their id lists without
+    the list tags (amr_dev.hip amr_dev_decide); refines and an unrefine
+    against the oracle."""
+    o = AmrOracle((1, 1, 1), -1, hood_length=1, comm_size=1)
+    assert o.M == 21
+    grids = make_ranks((1, 1, 1), -1, (False, False, False), 1, 1)
+    g = grids[0]
+    for rnd in range(4):
+        cells = o.cells()
+        if rnd < 3:
+            c = max(cells)  # the deepest cell
+            assert g.refine_completely(c) == o.refine_completely(0, c)
+        else:
+            c = cells[-1]
+            assert g.unrefine_completely(c) == o.unrefine_completely(0, c)
+        got = stop_all(grids)
+        want = o.stop_refining()
+        assert [int(x) for x in got[0]] == want[0]
+        assert [int(x) for x in g.get_removed_cells()] == o.get_removed_cells(0)
+        g.clear_refined_unrefined_data()
+        check_structure(grids, o)
+    g.close()
