@@ -257,10 +257,21 @@ int host_sets(dccrgx_grid* grid, Amr** out)
     return DCCRGX_OK;
 }
 
+// grid-stride launches: at most 16 workgroups per CU
+unsigned grid_for(uint64_t n) { return (unsigned)std::max<uint64_t>(std::min<uint64_t>((n + 255) / 256, 256 * 16), 1); }
+
 __global__ void __launch_bounds__(256) k_level0_ids(uint64_t* __restrict__ out, uint64_t n)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = i + 1;
+}
+
+// old slot of every new slot when a one-rank uniform grid turns explicit:
+// leaf k is cell k + 1, held in the uniform slot k + off
+__global__ void __launch_bounds__(256) k_uniform_from(int64_t* __restrict__ from, uint64_t n, int64_t off)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) from[k] = (int64_t)k + off;
 }
 
 // Rebuild the grid on an ascending leaf list: device leaf state, every
@@ -406,9 +417,16 @@ int rebuild_prepare(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std:
     };
     if (dx_malloc(&d_from, std::max<uint64_t>(ns, 1) * 8) != hipSuccess)
         return fail(set_error(DCCRGX_ENOMEM, "out of device memory for the rebuild plan"));
+    const int64_t off1 = old.uniform ? host_primary_slot(&old, 1) : -1;
     if (!old.uniform && old.ex) {
         const int e = explicit_old_slots(grid, old.ex, d_from, st);
         if (e != DCCRGX_OK) return fail(e);
+    } else if (E->one_rank && ns == E->n && ns == old.g.N && off1 >= 0 &&
+               host_primary_slot(&old, ns) == (int64_t)ns - 1 + off1) {
+        // one rank, every level-0 cell a leaf in id order (ensure_explicit):
+        // the uniform slots are one run
+        hipLaunchKernelGGL(k_uniform_from, dim3(grid_for(ns)), dim3(256), 0, st, d_from, ns, off1);
+        if (hipGetLastError() != hipSuccess) return fail(set_error(DCCRGX_EHIP, "move plan launch failed"));
     } else {
         std::vector<int64_t> from(ns);
         for (uint64_t k = 0; k < ns; k++) from[k] = host_primary_slot(&old, E->slot_id(k));
@@ -521,6 +539,20 @@ int ensure_explicit(dccrgx_grid* grid)
     DX_TRY(check_explicit_memory(grid, N));
     DX_CHECK(N < (1ull << 32), DCCRGX_EINVAL, "grid of %llu cells is too large to refine",
              (unsigned long long)N);
+    if (grid->ctx->comm_size == 1) {
+        // one rank: the leaf list 1..N is generated on the device and the host
+        // copy is made only if host code asks for it (explicit_fetch_leaves)
+        hipStream_t st = grid->ctx->compute;
+        uint64_t* d_leaves = nullptr;
+        DX_HIP(ds_malloc(&d_leaves, N * 8, st));
+        hipLaunchKernelGGL(k_level0_ids, dim3(grid_for(N)), dim3(256), 0, st, d_leaves, N);
+        DX_HIP(hipGetLastError());
+        std::vector<uint64_t> none;
+        RebuildTxn t;
+        DX_TRY(rebuild_prepare(grid, none, {}, d_leaves, nullptr, t, N, 1));  // adopts d_leaves
+        rebuild_commit(grid, t);
+        return DCCRGX_OK;
+    }
     std::vector<uint64_t> leaves(N);
     uint64_t* lv = leaves.data();
     parallel_ranges(N, 1u << 20, [lv](size_t b, size_t e) {

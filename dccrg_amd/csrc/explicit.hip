@@ -1226,7 +1226,6 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
         return set_error(DCCRGX_EINVAL, "leaf count %zu", n);
     }
     PhaseTimer T("explicit_init");
-    uint64_t ident = 0;  // leading identity entries of the reused one-rank maps
     if (grid->spare_host) {  // the previous state's host arrays: their capacity is reused
         Explicit* S = grid->spare_host;
         E->leaves_.swap(S->leaves_);
@@ -1238,7 +1237,6 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
         E->dir.swap(S->dir);
         E->local_.clear();
         E->slot_ids_.clear();
-        if (E->one_rank) ident = S->ident_n;
         delete S;
         grid->spare_host = nullptr;
     }
@@ -1303,21 +1301,11 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
     // ownership: the process of the level-0 ancestor (no load balancing),
     // block partition or the grid's SFC table
     E->part = make_partition(grid->map.nlevel0, ctx->comm_size);
-    if (E->one_rank) {  // one process owns every leaf: identity maps, filled by the host threads
-        // (reused maps already hold the identity up to `ident`: only the tail is written)
-        ident = std::min<uint64_t>({ident, E->owner.size(), E->local_g.size(), E->slot_of_g.size()});
-        E->owner.resize(E->n);
-        E->local_g.resize(E->n);
-        E->slot_of_g.resize(E->n);
-        if (ident < E->n)
-            parallel_ranges(E->n - ident, 1u << 16, [E, ident](size_t b, size_t e) {
-                for (size_t i = ident + b; i < ident + e; i++) {
-                    E->owner[i] = 0;
-                    E->local_g[i] = E->slot_of_g[i] = (uint32_t)i;
-                }
-            });
+    if (E->one_rank) {  // one process owns every leaf: owner 0 and identity maps, so no host arrays
+        E->owner.clear();
+        E->local_g.clear();
+        E->slot_of_g.clear();
         E->slot_identity = true;
-        E->ident_n = E->n;
         DX_TRY(device_iota(&E->d_local_g, E->n, st));
     } else {
         const std::vector<uint64_t>& L = E->leaves_;
@@ -1452,7 +1440,9 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
     uint64_t ns = old_ns;
     for (uint64_t c : ids) {
         const int64_t g = E->find(c);
-        if ((g >= 0 && E->slot_of_g[g] != NO_SLOT) || E->extra.count(c)) continue;  // has a slot
+        if ((g >= 0 && (E->slot_identity || E->slot_of_g[g] != NO_SLOT)) || E->extra.count(c)) continue;  // has a slot
+        DX_CHECK(g < 0 || g < (int64_t)E->slot_of_g.size(), DCCRGX_EINTERNAL, "no slot map for leaf %llu",
+                 (unsigned long long)c);
         const uint32_t s = (uint32_t)ns++;
         E->push_slot(c);
         E->extra.set(c, s);
@@ -1460,7 +1450,6 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
             E->slot_of_g[g] = s;
             leaf_slot = true;
             E->slot_identity = false;
-            E->ident_n = 0;
         }
     }
     DX_CHECK(ns < NO_SLOT, DCCRGX_EINVAL, "%llu storage slots on one rank", (unsigned long long)ns);
@@ -1472,10 +1461,7 @@ int explicit_add_slots(dccrgx_grid* grid, const std::vector<uint64_t>& ids)
                 const uint64_t c = E->slot_id(k);
                 E->extra.erase(c);
                 const int64_t g = E->find(c);
-                if (g >= 0) {
-                    E->slot_of_g[g] = NO_SLOT;
-                    E->ident_n = 0;
-                }
+                if (g >= 0) E->slot_of_g[g] = NO_SLOT;
             }
             E->truncate_slots(old_ns);
             return s;
@@ -1545,7 +1531,6 @@ void explicit_recycle(dccrgx_grid* grid, Explicit* E)
     S->slot_ids_.swap(E->slot_ids_);
     S->slot_of_g.swap(E->slot_of_g);
     S->dir.swap(E->dir);
-    S->ident_n = E->ident_n;
     explicit_free(E);
     delete grid->spare_host;
     grid->spare_host = S;
@@ -2621,6 +2606,7 @@ int64_t explicit_host_slot(const dccrgx_grid* grid, uint64_t id)
 {
     const Explicit* E = grid->ex;
     const int64_t g = E->find(id);  // a leaf: local or ghost slot, if any
+    if (g >= 0 && E->slot_identity) return g;  // one rank
     if (g >= 0 && E->slot_of_g[g] != NO_SLOT) return (int64_t)E->slot_of_g[g];
     // ghosts, and data of refined / unrefined cells kept until
     // clear_refined_unrefined_data

@@ -735,7 +735,7 @@ int dccrgx_get_process(const dccrgx_grid* grid, const uint64_t* cells, size_t n,
         }
         const Explicit* E = grid->ex;
         const int64_t g = E->find(c);
-        out[i] = g >= 0 ? E->owner[g] : -1;
+        out[i] = g < 0 ? -1 : E->one_rank ? 0 : E->owner[g];
     }
     return DCCRGX_OK;
 }

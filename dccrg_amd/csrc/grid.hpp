@@ -186,8 +186,9 @@ struct Explicit {
     std::vector<uint64_t> local_;   // ascending local ids (several ranks)
     const std::vector<uint64_t>& local() const { return one_rank ? leaves() : local_; }
     uint64_t n_local() const { return one_rank ? n : local_.size(); }
-    std::vector<uint32_t> local_g;  // their global indices
-    std::vector<int32_t> owner;     // process of each leaf (level-0 ancestor's, dccrg.hpp:8098-8145)
+    std::vector<uint32_t> local_g;  // their global indices (several ranks)
+    std::vector<int32_t> owner;     // process of each leaf (level-0 ancestor's, dccrg.hpp:8098-8145;
+                                    // several ranks: with one every leaf is rank 0's)
     uint32_t* d_local_g = nullptr;
     // Storage (per rank, not replicated): slots [0, nl) hold the local cells
     // in ascending id order, then ghost copies of remote neighbors (of every
@@ -204,10 +205,8 @@ struct Explicit {
     void push_slot(uint64_t c) { slot_ids_.push_back(c); }
     void truncate_slots(uint64_t ns) { slot_ids_.resize(one_rank ? ns - n : ns); }
     FlatMap32 extra;                                // ghost id -> slot
-    std::vector<uint32_t> slot_of_g;                // global leaf index -> slot (NO_SLOT)
-    bool slot_identity = false;                     // slot_of_g[g] == g (one rank, no ghost leaves)
-    uint64_t ident_n = 0;                           // one rank: owner[i] == 0, local_g[i] == slot_of_g[i] == i
-                                                    // hold for i < ident_n (kept by explicit_recycle)
+    std::vector<uint32_t> slot_of_g;                // global leaf index -> slot (NO_SLOT; several ranks)
+    bool slot_identity = false;                     // one rank: leaf g in slot g, local_g[g] == g (no host maps)
     uint32_t* d_slot_of_g = nullptr;
     uint32_t* d_local_slot = nullptr;               // local position -> slot (identity)
     uint8_t* d_level = nullptr;                     // refinement level of each slot
