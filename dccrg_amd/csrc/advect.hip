@@ -224,7 +224,10 @@ __device__ inline double adv_ld(__amdgpu_buffer_rsrc_t r, uint32_t i)
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8u), 0, 0));
 }
 
-template <int WPE>
+// SERIAL: one axis at a time (large grids: fewer live registers, more waves
+// per SIMD); otherwise all 30 gathers in flight together (small grids, where
+// the cell count and not the registers limits the waves in flight)
+template <int WPE, bool SERIAL>
 __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, double dt, FaceView fc,
                                                              const uint32_t* __restrict__ pos, uint64_t n,
                                                              double* __restrict__ rho_out, uint64_t t0, uint64_t t1)
@@ -249,44 +252,89 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, dou
         const double vc3[3] = {adv_ld(rv0, c), adv_ld(rv1, c), adv_ld(rv2, c)};
         const double rho_c = adv_ld(rr, c);
         double acc = adv_ld(rf, c);
+        // the overflow's row (faces next to finer cells beyond the first per
+        // direction) is read with the first loads and its first entry with the
+        // gathers, so a refined cell's chain of dependent loads stays three
+        // long instead of five
+        const bool over = *fc.over != 0;
+        uint64_t ob = 0;
+        uint32_t oc = 0;
+        if (over) {
+            ob = fc.o_base[q];
+            oc = fc.o_cnt[q];
+        }
         const double vol = lc3[0] * lc3[1] * lc3[2];
-        // one axis at a time: its two faces' 10 gathers in flight together,
-        // then their terms (10 live neighbor values instead of 30: more waves
-        // per SIMD to hide the gathers' latency); the terms are added in face
-        // order as before.  An axis no lane of the wave has a face on (z of
-        // level-0 cells of a one-cell-thick grid) issues no loads.
+        // SERIAL: one axis at a time, its two faces' 10 gathers in flight
+        // together, then their terms (10 live neighbor values instead of 30);
+        // the terms are added in face order either way.  An axis no lane of
+        // the wave has a face on (z of level-0 cells of a one-cell-thick grid)
+        // issues no loads.
+        constexpr int NA = SERIAL ? 1 : 3;
+        double ln0[NA][2], ln1[NA][2], ln2[NA][2], vn[NA][2], rn[NA][2];
+        bool any[3];
+        uint32_t nb0 = c;
+        int dir0 = 1;
+        if (oc) {
+            nb0 = fc.o_slot[ob];
+            dir0 = fc.o_dir[ob];
+        }
 #pragma unroll
         for (int ax = 0; ax < 3; ax++) {
-            if (!__ballot(s[2 * ax] != 0xffffffffu || s[2 * ax + 1] != 0xffffffffu)) continue;
-            const __amdgpu_buffer_rsrc_t rv = ax == 0 ? rv0 : ax == 1 ? rv1 : rv2;
-            double ln0[2], ln1[2], ln2[2], vn[2], rn[2];
+            const int a = SERIAL ? 0 : ax;
+            any[ax] = __ballot(s[2 * ax] != 0xffffffffu || s[2 * ax + 1] != 0xffffffffu) != 0;
+            if (any[ax]) {
+                const __amdgpu_buffer_rsrc_t rv = ax == 0 ? rv0 : ax == 1 ? rv1 : rv2;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int k = 2 * ax + h;
-                const uint32_t nb = s[k] != 0xffffffffu ? s[k] : c;
-                ln0[h] = adv_ld(rl0, nb);
-                ln1[h] = adv_ld(rl1, nb);
-                ln2[h] = adv_ld(rl2, nb);
-                vn[h] = adv_ld(rv, nb);
-                rn[h] = adv_ld(rr, nb);
-            }
+                for (int h = 0; h < 2; h++) {
+                    const int k = 2 * ax + h;
+                    const uint32_t nb = s[k] != 0xffffffffu ? s[k] : c;
+                    ln0[a][h] = adv_ld(rl0, nb);
+                    ln1[a][h] = adv_ld(rl1, nb);
+                    ln2[a][h] = adv_ld(rl2, nb);
+                    vn[a][h] = adv_ld(rv, nb);
+                    rn[a][h] = adv_ld(rr, nb);
+                }
+                if (SERIAL) {
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int k = 2 * ax + h;
-                if (s[k] != 0xffffffffu)
-                    acc += face_term_v(h ? ax + 1 : -(ax + 1), dt, vol, lc3, vc3, rho_c, ln0[h], ln1[h], ln2[h], vn[h],
-                                       rn[h]);
+                    for (int h = 0; h < 2; h++) {
+                        const int k = 2 * ax + h;
+                        if (s[k] != 0xffffffffu)
+                            acc += face_term_v(h ? ax + 1 : -(ax + 1), dt, vol, lc3, vc3, rho_c, ln0[a][h], ln1[a][h],
+                                               ln2[a][h], vn[a][h], rn[a][h]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
-            __builtin_amdgcn_sched_barrier(0);
         }
-        if (*fc.over)  // further faces (finer neighbors), over the values already loaded
-            for (uint64_t e = fc.o_base[q], e1 = e + fc.o_cnt[q]; e < e1; e++) {
+        if (!SERIAL) {
+#pragma unroll
+            for (int ax = 0; ax < 3; ax++) {
+                if (!any[ax]) continue;
+                const int a = SERIAL ? 0 : ax;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int k = 2 * ax + h;
+                    if (s[k] != 0xffffffffu)
+                        acc += face_term_v(h ? ax + 1 : -(ax + 1), dt, vol, lc3, vc3, rho_c, ln0[a][h], ln1[a][h],
+                                           ln2[a][h], vn[a][h], rn[a][h]);
+                }
+            }
+        }
+        if (oc) {  // further faces (finer neighbors), in row order after the six above
+            {
+                const int ax = (dir0 > 0 ? dir0 : -dir0) - 1;
+                const double ln0 = adv_ld(rl0, nb0), ln1 = adv_ld(rl1, nb0), ln2 = adv_ld(rl2, nb0);
+                const double vn = adv_ld(ax == 0 ? rv0 : ax == 1 ? rv1 : rv2, nb0), rn = adv_ld(rr, nb0);
+                acc += face_term_v(dir0, dt, vol, lc3, vc3, rho_c, ln0, ln1, ln2, vn, rn);
+            }
+            for (uint64_t e = ob + 1, e1 = ob + oc; e < e1; e++) {
                 const uint32_t nb = fc.o_slot[e];
                 const int dir = fc.o_dir[e], ax = (dir > 0 ? dir : -dir) - 1;
                 const double ln0 = adv_ld(rl0, nb), ln1 = adv_ld(rl1, nb), ln2 = adv_ld(rl2, nb);
                 const double vn = adv_ld(ax == 0 ? rv0 : ax == 1 ? rv1 : rv2, nb), rn = adv_ld(rr, nb);
                 acc += face_term_v(dir, dt, vol, lc3, vc3, rho_c, ln0, ln1, ln2, vn, rn);
             }
+        }
         if (!rho_out) {
             p.flux[c] = acc;
         } else {
@@ -645,8 +693,13 @@ int advect_launch(dccrgx_grid* grid, Hood& h, const AdvPtrs& p, double dt, int32
         // explicit grids store local cell q in slot q (explicit.hip): no slot loads
         const uint32_t* rpos = region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos;
         if (grid->n_slots < (1ull << 28) && 6 * F.n < (1ull << 29)) {  // buffer loads: byte offsets below 2 GiB
-            hipLaunchKernelGGL(k_ex_advect_faces_buf<1>, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv, rpos, R.n,
-                               rho_out, t0, t1);
+            // below ~8 waves per SIMD of cells the registers do not limit the waves in flight
+            if ((int64_t)R.n < test_opt(OPT_ADV_SERIAL_MIN, 1 << 19))
+                hipLaunchKernelGGL((k_ex_advect_faces_buf<1, false>), dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv,
+                                   rpos, R.n, rho_out, t0, t1);
+            else
+                hipLaunchKernelGGL((k_ex_advect_faces_buf<1, true>), dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv,
+                                   rpos, R.n, rho_out, t0, t1);
         } else {
             hipLaunchKernelGGL(k_ex_advect_faces<1>, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv,
                                (const uint32_t*)nullptr, rpos, R.n, rho_out, t0, t1);

@@ -1,0 +1,38 @@
+"""bench.py's gol2d line alone (configs[1]: 2-D game of life 16384^2, hood 1,
+periodic x, y): wall and kernel-timer time per step; run under rocprofv3
+--kernel-trace --stats for the launches of a step."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+
+import dccrg_amd as D  # noqa: E402
+
+ctx = D.Context(0, 0, 1)
+n = 16384
+g = (D.Dccrg().set_initial_length((n, n, 1)).set_neighborhood_length(1)
+     .set_maximum_refinement_level(0).set_periodic(True, True, False).initialize(ctx))
+for f in ("a", "b", "c"):
+    g.add_field(f, np.uint32)
+D.lib().dccrgx_field_init_hash(g._h, g.field_id("a"), 200)
+cur, nxt = "a", "b"
+g.gol_step(cur, nxt, "c")
+ctx.synchronize()
+for rep in range(3):
+    steps = 50
+    g.kernel_timer(reset=1)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.gol_step(cur, nxt, "c")
+        cur, nxt = nxt, cur
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    kms, nk = g.kernel_timer(reset=0)
+    g.kernel_timer(reset=-1)
+    print(f"wall {dt / steps * 1e3:.4f} ms/step, kernel timer {kms / steps:.4f} ms/step ({nk} timed), "
+          f"{12 * n * n / (kms / steps * 1e-3) / 1e9:.0f} GB/s", flush=True)
+g.close()
+ctx.close()
