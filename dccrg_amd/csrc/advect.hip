@@ -224,10 +224,7 @@ __device__ inline double adv_ld(__amdgpu_buffer_rsrc_t r, uint32_t i)
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8u), 0, 0));
 }
 
-// SERIAL: one axis at a time (large grids: fewer live registers, more waves
-// per SIMD); otherwise all 30 gathers in flight together (small grids, where
-// the cell count and not the registers limits the waves in flight)
-template <int WPE, bool SERIAL>
+template <int WPE>
 __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, double dt, FaceView fc,
                                                              const uint32_t* __restrict__ pos, uint64_t n,
                                                              double* __restrict__ rho_out, uint64_t t0, uint64_t t1)
@@ -263,62 +260,43 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, dou
             ob = fc.o_base[q];
             oc = fc.o_cnt[q];
         }
-        const double vol = lc3[0] * lc3[1] * lc3[2];
-        // SERIAL: one axis at a time, its two faces' 10 gathers in flight
-        // together, then their terms (10 live neighbor values instead of 30);
-        // the terms are added in face order either way.  An axis no lane of
-        // the wave has a face on (z of level-0 cells of a one-cell-thick grid)
-        // issues no loads.
-        constexpr int NA = SERIAL ? 1 : 3;
-        double ln0[NA][2], ln1[NA][2], ln2[NA][2], vn[NA][2], rn[NA][2];
-        bool any[3];
         uint32_t nb0 = c;
         int dir0 = 1;
         if (oc) {
             nb0 = fc.o_slot[ob];
             dir0 = fc.o_dir[ob];
         }
+        const double vol = lc3[0] * lc3[1] * lc3[2];
+        // one axis at a time: its two faces' 10 gathers in flight together,
+        // then their terms (10 live neighbor values instead of 30: more waves
+        // per SIMD to hide the gathers' latency); the terms are added in face
+        // order as before.  An axis no lane of the wave has a face on (z of
+        // level-0 cells of a one-cell-thick grid) issues no loads.  (All 30
+        // gathers in flight at once measured the same at 183k cells and 7 %
+        // slower at 2.56 M.)
 #pragma unroll
         for (int ax = 0; ax < 3; ax++) {
-            const int a = SERIAL ? 0 : ax;
-            any[ax] = __ballot(s[2 * ax] != 0xffffffffu || s[2 * ax + 1] != 0xffffffffu) != 0;
-            if (any[ax]) {
-                const __amdgpu_buffer_rsrc_t rv = ax == 0 ? rv0 : ax == 1 ? rv1 : rv2;
+            if (!__ballot(s[2 * ax] != 0xffffffffu || s[2 * ax + 1] != 0xffffffffu)) continue;
+            const __amdgpu_buffer_rsrc_t rv = ax == 0 ? rv0 : ax == 1 ? rv1 : rv2;
+            double ln0[2], ln1[2], ln2[2], vn[2], rn[2];
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int k = 2 * ax + h;
-                    const uint32_t nb = s[k] != 0xffffffffu ? s[k] : c;
-                    ln0[a][h] = adv_ld(rl0, nb);
-                    ln1[a][h] = adv_ld(rl1, nb);
-                    ln2[a][h] = adv_ld(rl2, nb);
-                    vn[a][h] = adv_ld(rv, nb);
-                    rn[a][h] = adv_ld(rr, nb);
-                }
-                if (SERIAL) {
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const int k = 2 * ax + h;
-                        if (s[k] != 0xffffffffu)
-                            acc += face_term_v(h ? ax + 1 : -(ax + 1), dt, vol, lc3, vc3, rho_c, ln0[a][h], ln1[a][h],
-                                               ln2[a][h], vn[a][h], rn[a][h]);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
+            for (int h = 0; h < 2; h++) {
+                const int k = 2 * ax + h;
+                const uint32_t nb = s[k] != 0xffffffffu ? s[k] : c;
+                ln0[h] = adv_ld(rl0, nb);
+                ln1[h] = adv_ld(rl1, nb);
+                ln2[h] = adv_ld(rl2, nb);
+                vn[h] = adv_ld(rv, nb);
+                rn[h] = adv_ld(rr, nb);
             }
-        }
-        if (!SERIAL) {
 #pragma unroll
-            for (int ax = 0; ax < 3; ax++) {
-                if (!any[ax]) continue;
-                const int a = SERIAL ? 0 : ax;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int k = 2 * ax + h;
-                    if (s[k] != 0xffffffffu)
-                        acc += face_term_v(h ? ax + 1 : -(ax + 1), dt, vol, lc3, vc3, rho_c, ln0[a][h], ln1[a][h],
-                                           ln2[a][h], vn[a][h], rn[a][h]);
-                }
+            for (int h = 0; h < 2; h++) {
+                const int k = 2 * ax + h;
+                if (s[k] != 0xffffffffu)
+                    acc += face_term_v(h ? ax + 1 : -(ax + 1), dt, vol, lc3, vc3, rho_c, ln0[h], ln1[h], ln2[h], vn[h],
+                                       rn[h]);
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (oc) {  // further faces (finer neighbors), in row order after the six above
             {
@@ -693,13 +671,8 @@ int advect_launch(dccrgx_grid* grid, Hood& h, const AdvPtrs& p, double dt, int32
         // explicit grids store local cell q in slot q (explicit.hip): no slot loads
         const uint32_t* rpos = region == DCCRGX_REGION_ALL ? (const uint32_t*)nullptr : R.pos;
         if (grid->n_slots < (1ull << 28) && 6 * F.n < (1ull << 29)) {  // buffer loads: byte offsets below 2 GiB
-            // below ~8 waves per SIMD of cells the registers do not limit the waves in flight
-            if ((int64_t)R.n < test_opt(OPT_ADV_SERIAL_MIN, 1 << 19))
-                hipLaunchKernelGGL((k_ex_advect_faces_buf<1, false>), dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv,
-                                   rpos, R.n, rho_out, t0, t1);
-            else
-                hipLaunchKernelGGL((k_ex_advect_faces_buf<1, true>), dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv,
-                                   rpos, R.n, rho_out, t0, t1);
+            hipLaunchKernelGGL(k_ex_advect_faces_buf<1>, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv, rpos, R.n,
+                               rho_out, t0, t1);
         } else {
             hipLaunchKernelGGL(k_ex_advect_faces<1>, dim3(grid_for(work)), dim3(256), 0, st, p, dt, fv,
                                (const uint32_t*)nullptr, rpos, R.n, rho_out, t0, t1);

@@ -1088,7 +1088,7 @@ std::atomic<int64_t> g_test_opt[OPT_COUNT];
 std::atomic<bool> g_test_set[OPT_COUNT];
 const char* const kTestOptName[OPT_COUNT] = {"gol_scalar",  "gol_chunk",      "poisson_multi",
                                              "poisson_solo_global", "incremental", "ou_small",
-                                             "corrupt_ghost", "fail_stop_refining", "check_init", "full_nto", "adv_serial_min"};
+                                             "corrupt_ghost", "fail_stop_refining", "check_init", "full_nto"};
 }  // namespace
 
 int64_t test_opt(TestOpt o, int64_t dflt)

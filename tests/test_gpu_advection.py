@@ -56,20 +56,9 @@ def exchange(grids, fields, uniform):
         loopback(grids, list(fields))
 
 
-@pytest.fixture(params=["gathers_together", "axis_by_axis"])
-def gather_order(request):
-    """The explicit-grid flux kernel's two schedules (advect.hip
-    k_ex_advect_faces_buf: every gather in flight at once below 2^19 cells,
-    one axis at a time above): the same terms in the same order."""
-    from dccrg_amd.grid import set_test_option
-    set_test_option("adv_serial_min", 0 if request.param == "axis_by_axis" else None)
-    yield request.param
-    set_test_option("adv_serial_min", None)
-
-
 @pytest.mark.parametrize("P", [1, 3])
 @pytest.mark.parametrize("case", CASES)
-def test_advection_parity(case, P, gather_order):
+def test_advection_parity(case, P):
     uniform = case[4] is None
     lists, grids = build(case, P)
     state = O.advection_initial_state(O.Mapping(case[0], case[1]), lists.cells)
