@@ -544,6 +544,7 @@ class Dccrg:
         total = int(row[-1].item())
         ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
         off = torch.zeros((max(total, 1), 3), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)  # the zero fills (torch's stream) before the library's writes (its own)
         check(lib().dccrgx_neighbors_of(self._h, hood, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
                                         off.data_ptr(), total, None))
         self.ctx.synchronize()
@@ -565,8 +566,10 @@ class Dccrg:
         row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         torch.cuda.synchronize(dev)
         check(lib().dccrgx_gather_neighbors(self._h, hood, fid, ct.data_ptr(), n, row.data_ptr(), None, 0, None))
+        self.ctx.synchronize()
         total = int(row[-1].item())
         out = torch.zeros(max(total, 1) * dt.itemsize, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
         check(lib().dccrgx_gather_neighbors(self._h, hood, fid, ct.data_ptr(), n, row.data_ptr(), out.data_ptr(),
                                             out.numel(), None))
         self.ctx.synchronize()
@@ -583,6 +586,7 @@ class Dccrg:
         self.ctx.synchronize()
         total = int(row[-1].item())
         ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
         check(lib().dccrgx_neighbors_to(self._h, hood, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
                                         total, None))
         self.ctx.synchronize()
