@@ -493,7 +493,7 @@ def secondary(ctx, torch, D):
     ach = BYTES_PER_CELL * n * n * steps / (kms * 1e-3) / 1e9
     out["gol2d"] = {"workload": "configs[1] 2-D game of life 16384x16384, hood 1, periodic x,y",
                     "value": n * n * steps / dt, "unit": "cell-updates/s", "steps": steps,
-                    "kernel": "k_gol26_rowv<4>", "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS}
+                    "kernel": "k_gol26_rowv<4, true>", "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS}
     g.close()
 
     # mapping kernel: ids -> indices + level, 2048^3 grid at max level 10

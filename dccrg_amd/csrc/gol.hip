@@ -172,10 +172,12 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
     const bool vec = u.LA % 4 == 0 && u.S < (1ull << 31) && !test_opt(OPT_GOL_SCALAR, 0);
     const uint32_t mult = u.perB ? 3u : 1u;
     if (u.LB == 1 && vec) {
-        // 2-D / 1-D grids: k_gol26_rowv, 4 waves x 256 cells of a row per workgroup
+        // 2-D / 1-D grids: k_gol26_rowv, 4 waves x 256 cells of a row per
+        // workgroup, non-temporal stores (1-2 % faster than plain stores in
+        // every A/B pairing, profiles/r7c_gol2d_nts_ab.log)
         Gol4Args v = gol4_plan(a, 1024, 1, nsl, chunk);
         DX_CHECK(v.nwg, DCCRGX_EINVAL, "grid too large for one launch");
-        hipLaunchKernelGGL((k_gol26_rowv<4>), dim3(v.nwg), dim3(256), 0, st, v, mult);
+        hipLaunchKernelGGL((k_gol26_rowv<4, true>), dim3(v.nwg), dim3(256), 0, st, v, mult);
     } else if (u.LB == 1) {
         constexpr int TA = 1024, NA = 4;
         a.tiles_a = (uint32_t)((u.LA + TA - 1) / TA);

@@ -9,6 +9,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401
 
+from dccrg_amd import _capi  # noqa: E402
+
+if os.environ.get("MAP_LIB"):  # A/B runs against another build of the library
+    _capi.LIB_PATH = os.environ["MAP_LIB"]
 import dccrg_amd as D  # noqa: E402
 
 ctx = D.Context(0, 0, 1)
@@ -32,7 +36,7 @@ for rep in range(3):
     dt = time.perf_counter() - t0
     kms, nk = g.kernel_timer(reset=0)
     g.kernel_timer(reset=-1)
-    print(f"wall {dt / steps * 1e3:.4f} ms/step, kernel timer {kms / steps:.4f} ms/step ({nk} timed), "
+    print(f"{os.path.basename(_capi.LIB_PATH)} wall {dt / steps * 1e3:.4f} ms/step, kernel timer {kms / steps:.4f} ms/step ({nk} timed), "
           f"{12 * n * n / (kms / steps * 1e-3) / 1e9:.0f} GB/s", flush=True)
 g.close()
 ctx.close()
