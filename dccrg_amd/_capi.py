@@ -166,6 +166,7 @@ SIGNATURES = {
     "dccrgx_gather_neighbors": (C.c_int, [_vp, C.c_int32, C.c_int32, _vp, C.c_size_t, _vp, _vp, C.c_size_t,
                                           _vp]),
     "dccrgx_sfc_owners": (C.c_int, [_vp, _u64p, C.c_int32, _i32p]),
+    "dccrgx_sfc_cuts": (C.c_int, [_u64p, C.c_int32, _u64p]),
     "dccrgx_hilbert_keys_host": (C.c_int, [_u64p, _u64p]),
     "dccrgx_gol_amr_phase": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int32]),
     "dccrgx_gol_amr_step": (C.c_int, [_vp, C.c_int32, C.c_int32]),

@@ -131,14 +131,28 @@ def request_adaptation(grid: Dccrg, to_refine, not_to_unrefine, to_unrefine):
 
 
 def finish_adaptation(grid: Dccrg, geom: CartesianGeometry, all_requests=None,
-                      update: bool = True, agreed: bool = False) -> Tuple[int, int]:
+                      update: bool = True) -> Tuple[int, int]:
     """adapter.hpp:215-319: stop_refining (all_requests: the union of every
-    rank's requests, agreed: see Dccrg.stop_refining), data of new cells and
-    of the parents of removed cells, velocities and lengths, ghost update
-    (skipped with update=False)."""
+    rank's requests), data of new cells and of the parents of removed cells,
+    velocities and lengths, ghost update (skipped with update=False)."""
     if grid.get_maximum_refinement_level() == 0:
         return 0, 0
-    new = grid.stop_refining(all_requests=all_requests, agreed=agreed)
+    new = grid.stop_refining(all_requests=all_requests)
+    return _after_stop_refining(grid, geom, new, update)
+
+
+def finish_adaptation_all(grids, geoms, all_requests, update: bool = False):
+    """finish_adaptation of several ranks held in one process: the
+    collective stop_refining across them (stop_refining_all: all adopt the new
+    grid or all keep the old one), then each rank's data rules."""
+    from .grid import stop_refining_all
+    if grids[0].get_maximum_refinement_level() == 0:
+        return [(0, 0) for _ in grids]
+    news = stop_refining_all(grids, all_requests)
+    return [_after_stop_refining(g, geom, new, update) for g, geom, new in zip(grids, geoms, news)]
+
+
+def _after_stop_refining(grid: Dccrg, geom: CartesianGeometry, new, update: bool) -> Tuple[int, int]:
     removed = grid.get_removed_cells()
     # new cells are value-initialised by the rebuild (flux = 0); they take the
     # parent's density (:229-251).  Parents of removed cells: 0, then

@@ -761,6 +761,7 @@ int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f)
 {
     DX_NOT_PENDING(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    DX_TRY(explicit_host_leaves(grid));
     AdvPtrs p;
     DX_TRY(adv_ptrs(grid, f, &p));
     if (!grid->n_local) return DCCRGX_OK;
@@ -941,6 +942,7 @@ int dccrgx_advect_set_geometry(dccrgx_grid* grid, const dccrgx_advect_fields* f,
 int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 {
     DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
+    DX_NOT_PENDING(grid);
     if (!grid->amr || grid->amr->new_cells.empty()) return DCCRGX_OK;
     return amr_dev_copy_from_parents(grid, fields, nf);
 }
@@ -948,6 +950,7 @@ int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_
 int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 {
     DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
+    DX_NOT_PENDING(grid);
     if (!grid->amr || grid->amr->removed.empty()) return DCCRGX_OK;
     return amr_dev_average_children(grid, fields, nf);
 }

@@ -607,6 +607,8 @@ extern "C" {
 int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 {
     DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
+    DX_NOT_PENDING(grid);
+    DX_TRY(explicit_host_leaves(grid));
     *result = 0;
     if (cell == 0) return DCCRGX_OK;
     if (grid->map.max_lvl == 0 && grid->uniform) {  // level == max: dont_unrefine, a no-op at level 0
@@ -663,6 +665,8 @@ int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 {
     DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
+    DX_NOT_PENDING(grid);
+    DX_TRY(explicit_host_leaves(grid));
     *result = 0;
     if (cell == 0) return DCCRGX_OK;
     if (grid->uniform) {  // every cell is at level 0: true for existing local cells (:2600-2602)
@@ -709,6 +713,8 @@ int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result
 int dccrgx_dont_unrefine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 {
     DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
+    DX_NOT_PENDING(grid);
+    DX_TRY(explicit_host_leaves(grid));
     *result = 0;
     if (cell == 0) return DCCRGX_OK;
     if (grid->uniform) {  // level 0: true for any existing cell (:2731-2733)
@@ -735,6 +741,8 @@ int dccrgx_dont_unrefine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 {
     DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
+    DX_NOT_PENDING(grid);
+    DX_TRY(explicit_host_leaves(grid));
     *result = 0;
     if (cell == 0) return DCCRGX_OK;
     const int lvl = map_level(grid->map, cell);
@@ -757,6 +765,7 @@ int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 int dccrgx_amr_request_cells(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results)
 {
     DX_CHECK(grid && (ids || !n) && kind >= 0 && kind < 4, DCCRGX_EINVAL, "bad argument");
+    DX_NOT_PENDING(grid);
     if (!grid->uniform) {  // the batch on the device (amr_dev.hip), results as the calls in this order
         amr_of(grid);
         return amr_dev_requests(grid, kind, ids, n, results);
@@ -969,6 +978,7 @@ int dccrgx_get_removed_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap,
 int dccrgx_clear_refined_unrefined_data(dccrgx_grid* grid)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    DX_NOT_PENDING(grid);
     if (grid->ex) explicit_clear_retired(grid->ex);
     if (grid->amr) grid->amr->removed.clear();
     return DCCRGX_OK;

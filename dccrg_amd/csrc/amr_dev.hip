@@ -61,7 +61,7 @@ struct AView {
     int32_t K;
     uint32_t hood_len;
     Partition part;
-    const int32_t* sfc;  // SFC owner table of the level-0 cells, or null (block partition)
+    SfcCuts sfc;  // SFC placement (device cut keys), or sfc.cut null (block partition)
     int32_t rank;
     uint32_t* flags;
 };
@@ -114,7 +114,7 @@ __device__ inline int a_owner(const AView& a, uint64_t c)
     int l;
     map_indices(a.v.mp, c, idx, &l);
     const uint64_t l0 = map_cell(a.v.mp, idx, 0);
-    return a.sfc ? a.sfc[l0 - 1] : part_owner(a.part, l0);
+    return a.sfc.cut ? sfc_owner(a.sfc, l0) : part_owner(a.part, l0);
 }
 
 // c != get_child(c), dccrg.hpp:9694-9718
@@ -833,7 +833,8 @@ static AView aview(const dccrgx_grid* grid, uint32_t* flags)
     a.K = h.K;
     a.hood_len = grid->params.neighborhood_length;
     a.part = E->part;
-    a.sfc = grid->d_sfc_owner;
+    a.sfc = SfcCuts{};
+    if (grid->sfc.on()) a.sfc = grid->sfc.view(grid->d_sfc_cut);
     a.rank = grid->ctx->rank;
     a.flags = flags;
     return a;
@@ -846,9 +847,11 @@ int amr_dev_sync(dccrgx_grid* grid)
     Amr& A = *grid->amr;
     Explicit* E = grid->ex;
     hipStream_t st = grid->ctx->compute;
-    if (!grid->sfc_owner.empty() && !grid->d_sfc_owner) {
-        DX_HIP(dx_malloc(&grid->d_sfc_owner, grid->sfc_owner.size() * 4));
-        DX_TRY(dx_h2d(grid->ctx, grid->d_sfc_owner, grid->sfc_owner.data(), grid->sfc_owner.size() * 4, st));
+    if (grid->sfc.on() && !grid->d_sfc_cut) {  // P - 1 cut keys
+        const size_t bytes = std::max<size_t>(8, grid->sfc.cut.size() * 8);
+        DX_HIP(dx_malloc(&grid->d_sfc_cut, bytes));
+        if (!grid->sfc.cut.empty())
+            DX_TRY(dx_h2d(grid->ctx, grid->d_sfc_cut, grid->sfc.cut.data(), grid->sfc.cut.size() * 8, st));
     }
     if (A.dev_current && A.flags_n == E->n && A.d_flags) return DCCRGX_OK;
     if (A.flags_cap < E->n) {

@@ -282,6 +282,7 @@ int dccrgx_save_sizes(const dccrgx_grid* grid, const int32_t* fields, size_t nf,
                       uint64_t* n_bytes)
 {
     DX_CHECK(grid && n_cells && n_bytes, DCCRGX_EINVAL, "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     FDesc d;
     bool var = false;
     DX_TRY(fdesc(grid, fields, nf, &d, &var));
@@ -367,6 +368,7 @@ int dccrgx_save_grid_data(const dccrgx_grid* grid, const char* path, uint64_t of
 {
     DX_CHECK(grid && path && (header || !header_bytes) && geometry && geometry_bytes >= 4, DCCRGX_EINVAL,
              "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     FDesc d;
     bool var = false;
     DX_TRY(fdesc(grid, fields, nf, &d, &var));
@@ -475,9 +477,9 @@ int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* 
     // the file records no placement: the loading grid's own (block, or the
     // SFC table of info->params) decides which rank reads which cells, as the
     // reference's load places cells by the new grid's partition
-    std::vector<int32_t> sfc;
-    if (info->params.partition == DCCRGX_PARTITION_SFC)
-        DX_TRY(sfc_owners(info->params.length, ctx->comm_size, ctx->compute, sfc));
+    SfcPlan sfc;
+    if (info->params.partition == DCCRGX_PARTITION_SFC) DX_TRY(sfc_plan(info->params.length, ctx->comm_size, sfc));
+    const SfcCuts sfc_cuts = sfc.view();
     // every cell in the list (:2033-2057); this rank loads the cells whose
     // level-0 ancestor is local (cell_overlaps_local, :2059-2071).  Pass 1
     // streams the list: are all cells level 0, and are this rank's cells
@@ -499,7 +501,7 @@ int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* 
         uint64_t idx[3];
         if (c == 0 || !map_indices(mp, c, idx, lvl)) return -1;
         const uint64_t l0 = *lvl == 0 ? c : map_cell(mp, idx, 0);
-        return sfc.empty() ? part_owner(part, l0) : (int)sfc[l0 - 1];
+        return sfc.on() ? sfc_owner(sfc_cuts, l0) : part_owner(part, l0);
     };
     bool all_level0 = true, simple = true;
     uint64_t n_mine = 0, first = 0, d0 = 0, stride = 0;
@@ -523,7 +525,7 @@ int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* 
         return DCCRGX_OK;
     }));
     // SFC grids always use the explicit layout (their local cells are not a slab)
-    const bool uniform = all_level0 && total == mp.nlevel0 && sfc.empty();
+    const bool uniform = all_level0 && total == mp.nlevel0 && !sfc.on();
     std::vector<uint64_t> leaves;
     if (!uniform) {
         leaves.reserve(total);
@@ -666,6 +668,7 @@ int dccrgx_save_grid_data_host(const dccrgx_grid* grid, const char* path, uint64
     DX_CHECK(grid && path && (header || !header_bytes) && geometry && geometry_bytes >= 4 &&
                  (record_bytes || !grid->n_local) && (records || !bytes),
              DCCRGX_EINVAL, "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     uint64_t tot = 0;
     for (uint64_t i = 0; i < grid->n_local; i++) tot += record_bytes[i];
     DX_CHECK(tot == bytes, DCCRGX_EINVAL, "records hold %zu bytes, their sizes add up to %llu", bytes,

@@ -618,7 +618,14 @@ void pool_run(size_t nt, const std::function<void(size_t)>& job)
 // caching allocator (internal.hpp)
 // ---------------------------------------------------------------------------
 namespace {
-constexpr size_t CACHE_MAX_BLOCK = 256ull << 20;   // larger blocks go straight back to the pool
+// blocks up to this size are kept in size classes; larger ones are kept at
+// their own size (a view's rows, a rebuild's field arrays), within
+// CACHE_MAX_TOTAL, and reused once the library's stream events recorded at the
+// free have passed -- work a caller queued on its own stream is not fenced, so
+// caller-stream kernels over library buffers must finish before the next
+// structural call, which frees and may hand out the block again (as
+// include/dccrgx_stencil.hpp states for user stencils)
+constexpr size_t CACHE_MAX_BLOCK = 256ull << 20;
 constexpr size_t CACHE_MAX_TOTAL = 8ull << 30;     // idle bytes kept at most per device
 constexpr size_t STREAM_LIST_MAX = 256ull << 20;   // a stream's own list is made common beyond this
 constexpr int MAX_DEV = 64;
@@ -994,6 +1001,7 @@ int dccrgx_ctx_create(int device, int rank, int comm_size, dccrgx_ctx** out)
     DX_HIP(hipEventCreateWithFlags(&c->ev_compute, hipEventDisableTiming));
     DX_HIP(hipEventCreateWithFlags(&c->ev_comm, hipEventDisableTiming));
     DX_HIP(hipEventCreateWithFlags(&c->ev_caller, hipEventDisableTiming));
+    DX_HIP(hipEventCreateWithFlags(&c->ev_enter, hipEventDisableTiming));
     dx_cache_streams(c->compute, c->comm, true);  // frees are fenced on these streams
     *out = c;
     return DCCRGX_OK;
@@ -1011,6 +1019,7 @@ int dccrgx_ctx_destroy(dccrgx_ctx* c)
     hipEventDestroy(c->ev_compute);
     hipEventDestroy(c->ev_comm);
     hipEventDestroy(c->ev_caller);
+    hipEventDestroy(c->ev_enter);
     for (hipEvent_t e : c->up_ev)  // recorded on the compute stream, which is idle now
         if (e) hipEventDestroy(e);
     hipStreamDestroy(c->compute);

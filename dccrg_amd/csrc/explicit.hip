@@ -1507,17 +1507,32 @@ int explicit_create(dccrgx_grid* grid, const uint64_t* leaves, size_t n)
 
 // Explicit::leaves() of a list held on the device only: one copy, made once
 // (a lookup may ask from several host threads)
-void explicit_fetch_leaves(const Explicit* E)
+static int fetch_leaves(const Explicit* E)
 {
     static std::mutex m;
     std::lock_guard<std::mutex> g(m);
-    if (E->host_leaves) return;
+    if (E->host_leaves) return DCCRGX_OK;
     E->leaves_.resize(E->n);
-    if (dx_d2h(E->ctx, E->leaves_.data(), E->d_leaves, E->n * 8, E->ctx->compute) != DCCRGX_OK) {
+    DX_TRY(dx_d2h(E->ctx, E->leaves_.data(), E->d_leaves, E->n * 8, E->ctx->compute));
+    E->host_leaves = true;
+    return DCCRGX_OK;
+}
+
+int explicit_host_leaves(const dccrgx_grid* grid)
+{
+    if (!grid || grid->uniform || !grid->ex || grid->ex->host_leaves) return DCCRGX_OK;
+    return fetch_leaves(grid->ex);
+}
+
+// the backstop of Explicit::leaves(): every public entry point that reaches
+// host lookups fetches first through explicit_host_leaves, which returns
+// the error instead (DCCRGX_EHIP); reaching this with a failing copy is a bug
+void explicit_fetch_leaves(const Explicit* E)
+{
+    if (fetch_leaves(E) != DCCRGX_OK) {
         std::fprintf(stderr, "dccrgx: reading the leaf list from the device failed: %s\n", dccrgx_last_error());
         std::abort();
     }
-    E->host_leaves = true;
 }
 
 void explicit_recycle(dccrgx_grid* grid, Explicit* E)

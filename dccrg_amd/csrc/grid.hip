@@ -669,7 +669,7 @@ int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uin
              "unknown partition %d", (int)prm->partition);
     std::vector<uint64_t> all_level0;
     if (prm->partition == DCCRGX_PARTITION_SFC) {
-        DX_TRY(sfc_owners(prm->length, ctx->comm_size, ctx->compute, grid->sfc_owner));
+        DX_TRY(sfc_plan(prm->length, ctx->comm_size, grid->sfc));
         if (!leaves) {  // every level-0 cell, on the explicit layout
             all_level0.resize(grid->map.nlevel0);
             for (uint64_t i = 0; i < all_level0.size(); i++) all_level0[i] = i + 1;
@@ -727,6 +727,7 @@ int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uin
 int dccrgx_get_process(const dccrgx_grid* grid, const uint64_t* cells, size_t n, int32_t* out)
 {
     DX_CHECK(grid && (cells || !n) && (out || !n), DCCRGX_EINVAL, "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     for (size_t i = 0; i < n; i++) {
         const uint64_t c = cells[i];
         if (grid->uniform) {
@@ -749,7 +750,7 @@ int dccrgx_grid_destroy(dccrgx_grid* grid)
     for (auto& kv : grid->hoods) free_hood(kv.second);
     for (Field& f : grid->fields) dx_free(f.ptr);
     for (auto& b : grid->spare_bufs) dx_free(b.first);
-    dx_free(grid->d_sfc_owner);
+    dx_free(grid->d_sfc_cut);
     if (!grid->uniform) explicit_destroy(grid);
     delete grid->spare_host;
     amr_destroy(grid);
@@ -849,6 +850,7 @@ int dccrgx_get_neighborhood(const dccrgx_grid* grid, int32_t id, int32_t* items,
 int dccrgx_get_all_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, size_t* n)
 {
     DX_CHECK(grid && n, DCCRGX_EINVAL, "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     if (!grid->uniform) {
         const std::vector<uint64_t>& L = grid->ex->leaves();
         *n = L.size();
@@ -868,6 +870,7 @@ int dccrgx_get_cells(const dccrgx_grid* grid, int32_t id, int32_t which, uint64_
                      size_t* n)
 {
     DX_CHECK(grid && n, DCCRGX_EINVAL, "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     const Hood* h = find_hood(grid, id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", id);
     if (!grid->uniform) return explicit_get_cells(grid, *h, which, ids, cap, n);
@@ -908,6 +911,7 @@ int dccrgx_get_cells(const dccrgx_grid* grid, int32_t id, int32_t which, uint64_
 int dccrgx_neighbor_list_stats(const dccrgx_grid* grid, int32_t id, uint64_t out[4])
 {
     DX_CHECK(grid && out, DCCRGX_EINVAL, "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     const Hood* h = find_hood(grid, id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", id);
     for (int k = 0; k < 4; k++) out[k] = 0;
@@ -952,6 +956,7 @@ int dccrgx_get_peer_cells(const dccrgx_grid* grid, int32_t id, int32_t send, int
                           uint64_t* ids, size_t cap, size_t* n)
 {
     DX_CHECK(grid && n, DCCRGX_EINVAL, "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     const Hood* h = find_hood(grid, id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", id);
     *n = 0;

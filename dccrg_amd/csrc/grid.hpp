@@ -157,6 +157,10 @@ struct PeerPlan {
 struct Explicit;
 // the host copy of a leaf list kept on the device (Explicit::leaves())
 void explicit_fetch_leaves(const Explicit* E);
+// the host copy of an explicit grid's leaf list (fetched once after a device
+// rebuild): public entry points that use host lookups call this first, so a
+// failing copy is an error code, not an abort (no-op for uniform grids)
+int explicit_host_leaves(const dccrgx_grid* grid);
 
 struct Explicit {
     uint64_t n = 0;                 // global leaves
@@ -417,6 +421,32 @@ struct Hood {
     std::shared_ptr<IterCache> iter;   // user-stencil view (stencil.hip)
 };
 
+// the SFC placement of a grid (sfc.hip): O(P) state, no per-cell table
+struct SfcPlan {
+    std::vector<uint64_t> cut;  // cut[r-1]: Hilbert key of process r's first level-0 cell
+    int32_t bits = 0;
+    uint64_t length[3] = {0, 0, 0};
+    Divider div_lx{}, div_lxly{};
+    bool enabled = false;
+    bool on() const { return enabled; }
+    // the cuts as kernels and host code read them (cut_ptr: host or device copy)
+    SfcCuts view(const uint64_t* cut_ptr = nullptr) const
+    {
+        SfcCuts s{};
+        s.cut = cut_ptr ? cut_ptr : cut.data();
+        s.ncut = (int32_t)cut.size();
+        s.bits = bits;
+        s.lx = length[0];
+        s.ly = length[1];
+        s.div_lx = div_lx;
+        s.div_lxly = div_lxly;
+        return s;
+    }
+};
+// the placement of `length`'s level-0 cells over comm_size processes (host
+// arithmetic over the curve, no device work and no per-cell memory)
+int sfc_plan(const uint64_t length[3], int comm_size, SfcPlan& out);
+
 // a rebuild built but not yet adopted (amr.hip rebuild_prepare): the new leaf
 // state, neighborhoods and field arrays, held aside while the grid is still
 // the old one
@@ -453,9 +483,9 @@ struct dccrgx_grid {
     // and fresh multi-MB vectors cost page faults)
     dccrgx::Explicit* spare_host = nullptr;
     bool rebuilding = false;  // inside amr.hip rebuild_prepare: intermediate synchronisations are skipped
-    // SFC placement (params.partition): owner of each level-0 cell, id - 1
-    std::vector<int32_t> sfc_owner;
-    int32_t* d_sfc_owner = nullptr;  // its device copy (AMR decisions), made on first use
+    // SFC placement (params.partition): the P - 1 cut keys along the curve
+    dccrgx::SfcPlan sfc;
+    uint64_t* d_sfc_cut = nullptr;  // their device copy (AMR decisions), made on first use
     // kernel timing (dccrgx_kernel_timer)
     hipEvent_t t0 = nullptr, t1 = nullptr;
     double timed_ms = 0;
@@ -463,14 +493,12 @@ struct dccrgx_grid {
 };
 
 namespace dccrgx {
-// process of a level-0 cell: the SFC table if the grid has one, else the
+// process of a level-0 cell: the SFC cuts if the grid has them, else the
 // block partition P (dccrg.hpp:8098-8145)
 inline int level0_owner(const dccrgx_grid* g, const Partition& P, uint64_t l0)
 {
-    return g->sfc_owner.empty() ? part_owner(P, l0) : g->sfc_owner[l0 - 1];
+    return g->sfc.on() ? sfc_owner(g->sfc.view(), l0) : part_owner(P, l0);
 }
-// owner table of the SFC placement (sfc.hip)
-int sfc_owners(const uint64_t length[3], int comm_size, hipStream_t st, std::vector<int32_t>& owner);
 Hood* find_hood(dccrgx_grid* g, int32_t id);
 const Hood* find_hood(const dccrgx_grid* g, int32_t id);
 int build_hood(dccrgx_grid* g, Hood& h);

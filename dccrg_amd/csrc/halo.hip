@@ -582,6 +582,7 @@ int dccrgx_field_read_remote(const dccrgx_grid* grid, int32_t hood_id, int32_t f
 int dccrgx_halo_self(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size_t nf)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    DX_NOT_PENDING(grid);
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     DX_TRY(check_fields(grid, f, nf, nullptr));
@@ -682,6 +683,7 @@ int dccrgx_exchange_start(dccrgx_grid* grid, int32_t hood_id, const void* const*
                           const uint64_t* send_bytes, void* const* recv_host, const uint64_t* recv_bytes)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    DX_NOT_PENDING(grid);
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     DX_CHECK(!h->pending, DCCRGX_ESTATE, "transfer of neighborhood %d already started", hood_id);
@@ -762,6 +764,7 @@ int dccrgx_halo_pack_to(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, si
                         void* dst, size_t cap, size_t* bytes)
 {
     DX_CHECK(grid && bytes, DCCRGX_EINVAL, "null argument");
+    DX_NOT_PENDING(grid);
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     size_t bpc = 0;
@@ -780,6 +783,7 @@ int dccrgx_halo_unpack_from(dccrgx_grid* grid, int32_t hood_id, const int32_t* f
                             int32_t peer, const void* src, size_t bytes)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null argument");
+    DX_NOT_PENDING(grid);
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     size_t bpc = 0;

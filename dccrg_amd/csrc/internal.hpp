@@ -409,6 +409,73 @@ inline uint64_t part_count(const Partition& P, int rank)
 }
 
 // ---------------------------------------------------------------------------
+// SFC placement, dccrg.hpp:8147-8220 (USE_SFC; sfc.hip): the level-0 cells in
+// Hilbert order get the block partition's per-process counts.  Process r's
+// cells are the ones whose key lies in [cut[r-1], cut[r]), so the P-1 cut keys
+// are the whole placement: owner = number of cut keys <= the cell's key.
+// ---------------------------------------------------------------------------
+
+// Hilbert index of (x, y, z) with `b` bits per axis (Skilling, "Programming
+// the Hilbert curve", AIP Conf. Proc. 707, 2004: axes -> transpose, read out
+// most significant bit first, X[0] X[1] X[2] per bit; x = X[0])
+__host__ __device__ inline uint64_t hilbert3(uint32_t x, uint32_t y, uint32_t z, int b)
+{
+    uint32_t X[3] = {x, y, z};
+    const uint32_t M = 1u << (b - 1);
+    for (uint32_t Q = M; Q > 1; Q >>= 1) {  // inverse undo
+        const uint32_t P = Q - 1;
+        for (int i = 0; i < 3; i++) {
+            if (X[i] & Q) {
+                X[0] ^= P;
+            } else {
+                const uint32_t t = (X[0] ^ X[i]) & P;
+                X[0] ^= t;
+                X[i] ^= t;
+            }
+        }
+    }
+    X[1] ^= X[0];  // Gray encode
+    X[2] ^= X[1];
+    uint32_t t = 0;
+    for (uint32_t Q = M; Q > 1; Q >>= 1)
+        if (X[2] & Q) t ^= Q - 1;
+    for (int i = 0; i < 3; i++) X[i] ^= t;
+    uint64_t key = 0;
+    for (int bit = b - 1; bit >= 0; bit--)
+        for (int i = 0; i < 3; i++) key = (key << 1) | ((X[i] >> bit) & 1u);
+    return key;
+}
+
+struct SfcCuts {
+    const uint64_t* cut;  // ascending; cut[r-1] = key of process r's first cell (r = 1 .. ncut); null: no SFC
+    int32_t ncut;         // comm_size - 1
+    int32_t bits;         // bits per axis of the Hilbert cube (smallest power of two holding the grid)
+    Divider div_lx, div_lxly;  // level-0 extents: x = i % lx, y = (i / lx) % ly, z = i / (lx * ly)
+    uint64_t lx, ly;
+};
+
+__host__ __device__ inline uint64_t sfc_key(const SfcCuts& s, uint64_t level0_id)
+{
+    const uint64_t i = level0_id - 1;
+    const uint64_t q = divide(i, s.div_lx), z = divide(i, s.div_lxly);
+    return hilbert3((uint32_t)(i - q * s.lx), (uint32_t)(q - z * s.ly), (uint32_t)z, s.bits);
+}
+
+__host__ __device__ inline int sfc_owner(const SfcCuts& s, uint64_t level0_id)
+{
+    const uint64_t key = sfc_key(s, level0_id);
+    int lo = 0, hi = s.ncut;  // first cut > key
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s.cut[mid] <= key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------
 struct Ctx {
@@ -416,6 +483,7 @@ struct Ctx {
     hipStream_t compute = nullptr, comm = nullptr;
     hipEvent_t ev_compute = nullptr, ev_comm = nullptr;
     hipEvent_t ev_caller = nullptr;  // CallerStream
+    hipEvent_t ev_enter = nullptr;   // CallerStream
     ncclComm_t nccl = nullptr;
     bool has_comm = false;
     // test mode (dccrgx_ctx_route_self_through_rccl): a rank's own periodic
@@ -451,7 +519,14 @@ struct Ctx {
 struct CallerStream {
     Ctx* c;
     hipStream_t st;
-    CallerStream(Ctx* c_, hipStream_t s) : c(c_), st(s) {}
+    // the call's work on a caller's stream follows the library's queued work
+    // (field writes, steps on the compute stream), and later library work
+    // follows it: stream order on both sides, no device-wide wait
+    CallerStream(Ctx* c_, hipStream_t s) : c(c_), st(s)
+    {
+        if (!c || !st || st == c->compute || st == c->comm) return;
+        if (hipEventRecord(c->ev_enter, c->compute) == hipSuccess) (void)hipStreamWaitEvent(st, c->ev_enter, 0);
+    }
     ~CallerStream()
     {
         if (!c || !st || st == c->compute || st == c->comm) return;

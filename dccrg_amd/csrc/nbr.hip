@@ -513,6 +513,7 @@ int dccrgx_face_neighbors_of_host(const dccrgx_grid* grid, const uint64_t* cells
                                   uint64_t* ids, int32_t* dirs, size_t cap)
 {
     DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_cells = nullptr, *d_row = nullptr, *d_ids = nullptr;
     int32_t* d_dirs = nullptr;
@@ -598,6 +599,7 @@ int dccrgx_neighbors_of_host(const dccrgx_grid* grid, int32_t hood_id, const uin
                              uint64_t* row, uint64_t* ids, int32_t* off3, size_t cap)
 {
     DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_cells = nullptr, *d_row = nullptr, *d_ids = nullptr;
     int32_t* d_off = nullptr;
@@ -635,6 +637,7 @@ int dccrgx_neighbors_to_host(const dccrgx_grid* grid, int32_t hood_id, const uin
                              uint64_t* row, uint64_t* ids, size_t cap)
 {
     DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    DX_TRY(explicit_host_leaves(grid));
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_cells = nullptr, *d_row = nullptr, *d_ids = nullptr;
     DX_HIP(dx_malloc(&d_cells, std::max<size_t>(n, 1) * 8));

@@ -68,6 +68,40 @@ def stop_refining_all(grids, all_requests):
     return [g.get_new_cells() for g in grids]
 
 
+class _OnLibraryStream:
+    """Stream order between torch and the library without device-wide waits:
+    the library's compute stream (as a torch ExternalStream) first waits for
+    torch's current stream (the query's input tensors), torch allocates and
+    fills the result tensors on it inside the block, the exports run on it
+    (stream None), and afterwards torch's current stream waits for it, so the
+    results are ordered before whatever the caller queues next.  (torch's
+    default stream is the null stream, which the C-ABI cannot name: its NULL
+    means the grid's compute stream.)"""
+
+    def __init__(self, ctx, dev):
+        import torch
+        self.cur = torch.cuda.current_stream(dev)
+        self.ls = torch.cuda.ExternalStream(ctx.stream, device=dev)
+
+    def __enter__(self):
+        import torch
+        self.ls.wait_stream(self.cur)
+        self._cm = torch.cuda.stream(self.ls)
+        self._cm.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        self._cm.__exit__(*exc)
+        self.cur.wait_stream(self.ls)
+        return False
+
+    def hand_over(self, *tensors):
+        """tensors made inside the block and returned to the caller: their
+        memory is in use on the caller's stream too (torch's record_stream)"""
+        for t in tensors:
+            t.record_stream(self.cur)
+
+
 def _u64(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.uint64)
 
@@ -389,20 +423,20 @@ class Dccrg:
             out.append(a)
         return out
 
-    def stop_refining(self, sorted: bool = True, all_requests=None, agreed: bool = False) -> np.ndarray:
+    def stop_refining(self, sorted: bool = True, all_requests=None) -> np.ndarray:
         """Collective (dccrg.hpp:3483-3507).  all_requests: the union over all
         ranks of amr_requests(); gathered with torch.distributed when the
         grid has several ranks and it is not given.  Two phases: every rank
         prepares its new grid, the statuses are all-reduced (torch.distributed),
         and all ranks adopt or all keep the old grid with the requests pending
         -- a failure on any rank raises on every rank.  With several ranks and
-        no torch.distributed the agreement is impossible and this raises,
-        unless agreed=True: the caller holds every rank (stop_refining_all does
-        the two phases across them) and takes a failure as its own."""
+        no torch.distributed the agreement is impossible and this raises:
+        ranks held in one process go through stop_refining_all, which runs
+        the two phases across them."""
         multi = self.ctx.comm_size > 1
-        if multi and not agreed and not _dist_ready():
+        if multi and not _dist_ready():
             raise X.DccrgxError(X.DCCRGX_ESTATE, "stop_refining with several ranks needs torch.distributed for the "
-                                                 "ranks' status agreement (or agreed=True, see stop_refining_all)")
+                                                 "ranks' status agreement (ranks in one process: stop_refining_all)")
         if multi and all_requests is None:
             import torch.distributed as dist
             mine = self.amr_requests()
@@ -413,7 +447,7 @@ class Dccrg:
         st, err = self.stop_refining_prepare(all_requests)
         ok = st == X.DCCRGX_OK
         all_ok = ok
-        if multi and not agreed:
+        if multi:
             import torch
             import torch.distributed as dist
             t = torch.tensor([1 if ok else 0], dtype=torch.int32)
@@ -536,20 +570,16 @@ class Dccrg:
         dev = torch.device("cuda", self.ctx.device)
         c = torch.from_numpy(_u64(cells).view(np.int64)).to(dev)
         n = c.numel()
-        row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        torch.cuda.synchronize(dev)
-        check(lib().dccrgx_neighbors_of(self._h, hood, c.data_ptr(), n, row.data_ptr(), None, None, 0,
-                                        None))
-        self.ctx.synchronize()
-        total = int(row[-1].item())
-        ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
-        off = torch.zeros((max(total, 1), 3), dtype=torch.int32, device=dev)
-        torch.cuda.synchronize(dev)  # the zero fills (torch's stream) before the library's writes (its own)
-        check(lib().dccrgx_neighbors_of(self._h, hood, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
-                                        off.data_ptr(), total, None))
-        self.ctx.synchronize()
-        return (row.cpu().numpy().astype(np.uint64), ids[:total].cpu().numpy().view(np.uint64),
-                off[:total].cpu().numpy())
+        with _OnLibraryStream(self.ctx, dev):
+            row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            check(lib().dccrgx_neighbors_of(self._h, hood, c.data_ptr(), n, row.data_ptr(), None, None, 0, None))
+            total = int(row[-1].item())
+            ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
+            off = torch.zeros((max(total, 1), 3), dtype=torch.int32, device=dev)
+            check(lib().dccrgx_neighbors_of(self._h, hood, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
+                                            off.data_ptr(), total, None))
+            return (row.cpu().numpy().astype(np.uint64), ids[:total].cpu().numpy().view(np.uint64),
+                    off[:total].cpu().numpy())
 
     def gather_neighbors(self, name: str, cells=None, hood: int = DEFAULT_NEIGHBORHOOD_ID):
         """Neighbor gather for user stencils (dccrgx_gather_neighbors): for
@@ -563,16 +593,14 @@ class Dccrg:
         c = self.local_cells() if cells is None else cells
         ct = torch.from_numpy(_u64(c).view(np.int64)).to(dev)
         n = ct.numel()
-        row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        torch.cuda.synchronize(dev)
-        check(lib().dccrgx_gather_neighbors(self._h, hood, fid, ct.data_ptr(), n, row.data_ptr(), None, 0, None))
-        self.ctx.synchronize()
-        total = int(row[-1].item())
-        out = torch.zeros(max(total, 1) * dt.itemsize, dtype=torch.uint8, device=dev)
-        torch.cuda.synchronize(dev)
-        check(lib().dccrgx_gather_neighbors(self._h, hood, fid, ct.data_ptr(), n, row.data_ptr(), out.data_ptr(),
-                                            out.numel(), None))
-        self.ctx.synchronize()
+        with _OnLibraryStream(self.ctx, dev) as ls:
+            row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            check(lib().dccrgx_gather_neighbors(self._h, hood, fid, ct.data_ptr(), n, row.data_ptr(), None, 0, None))
+            total = int(row[-1].item())
+            out = torch.zeros(max(total, 1) * dt.itemsize, dtype=torch.uint8, device=dev)
+            check(lib().dccrgx_gather_neighbors(self._h, hood, fid, ct.data_ptr(), n, row.data_ptr(),
+                                                out.data_ptr(), out.numel(), None))
+            ls.hand_over(row, out)
         return row, out[:total * dt.itemsize]
 
     def neighbors_to(self, cells: np.ndarray, hood: int = DEFAULT_NEIGHBORHOOD_ID):
@@ -580,17 +608,14 @@ class Dccrg:
         dev = torch.device("cuda", self.ctx.device)
         c = torch.from_numpy(_u64(cells).view(np.int64)).to(dev)
         n = c.numel()
-        row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        torch.cuda.synchronize(dev)
-        check(lib().dccrgx_neighbors_to(self._h, hood, c.data_ptr(), n, row.data_ptr(), None, 0, None))
-        self.ctx.synchronize()
-        total = int(row[-1].item())
-        ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
-        torch.cuda.synchronize(dev)
-        check(lib().dccrgx_neighbors_to(self._h, hood, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
-                                        total, None))
-        self.ctx.synchronize()
-        return row.cpu().numpy().astype(np.uint64), ids[:total].cpu().numpy().view(np.uint64)
+        with _OnLibraryStream(self.ctx, dev):
+            row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            check(lib().dccrgx_neighbors_to(self._h, hood, c.data_ptr(), n, row.data_ptr(), None, 0, None))
+            total = int(row[-1].item())
+            ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
+            check(lib().dccrgx_neighbors_to(self._h, hood, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
+                                            total, None))
+            return row.cpu().numpy().astype(np.uint64), ids[:total].cpu().numpy().view(np.uint64)
 
     def get_neighbors_of(self, cell: int, hood: int = DEFAULT_NEIGHBORHOOD_ID):
         """dccrg.hpp:836-883 for one cell: [(id, (x, y, z)), ...] in reference order."""
@@ -604,16 +629,16 @@ class Dccrg:
         dev = torch.device("cuda", self.ctx.device)
         c = torch.from_numpy(_u64(cells).view(np.int64)).to(dev)
         n = c.numel()
-        row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        cap = 24 * max(n, 1)
-        ids = torch.zeros(cap, dtype=torch.int64, device=dev)
-        dirs = torch.zeros(cap, dtype=torch.int32, device=dev)
-        torch.cuda.synchronize(dev)
-        check(lib().dccrgx_face_neighbors_of(self._h, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
-                                             dirs.data_ptr(), cap, None))
-        total = int(row[-1].item())
-        return (row.cpu().numpy().astype(np.uint64), ids[:total].cpu().numpy().view(np.uint64),
-                dirs[:total].cpu().numpy())
+        with _OnLibraryStream(self.ctx, dev):
+            row = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            cap = 24 * max(n, 1)
+            ids = torch.zeros(cap, dtype=torch.int64, device=dev)
+            dirs = torch.zeros(cap, dtype=torch.int32, device=dev)
+            check(lib().dccrgx_face_neighbors_of(self._h, c.data_ptr(), n, row.data_ptr(), ids.data_ptr(),
+                                                 dirs.data_ptr(), cap, None))
+            total = int(row[-1].item())
+            return (row.cpu().numpy().astype(np.uint64), ids[:total].cpu().numpy().view(np.uint64),
+                    dirs[:total].cpu().numpy())
 
     def get_face_neighbors_of(self, cell: int):
         """dccrg.hpp:2828-2955 for one cell: [(id, direction), ...]."""

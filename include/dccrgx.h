@@ -83,6 +83,7 @@ int dccrgx_ctx_route_self_through_rccl(dccrgx_ctx* ctx, int32_t on);
  * fault injection; never read from the environment, all off by default.
  * name: "gol_scalar", "gol_chunk" (slices per workgroup), "poisson_multi",
  * "poisson_solo_global", "incremental" (1 / 0), "ou_small" (queue entries),
+ * "full_nto" (1: the full neighbors_to transpose in incremental rebuilds),
  * "corrupt_ghost", "fail_stop_refining" (rank + 1), "check_init"; set = 0
  * returns the option to its default.  DCCRGX_EINVAL for an unknown name, or
  * in a build compiled with -DDCCRGX_NO_TEST_OPTIONS. */
@@ -169,11 +170,19 @@ typedef struct {
 /* Placement of the level-0 cells at initialize (create_level_0_cells,
  * dccrg.hpp:8089-8224).  BLOCK: contiguous ids (:8116-8145, the reference's
  * build without USE_SFC).  SFC: the same per-process counts taken along a
- * space-filling curve (the USE_SFC branch :8147-8220; Hilbert curve computed on
- * the device, sfc.hip; sfc++'s own curve is not in the reference tree).  An
- * SFC grid always uses the explicit (replicated leaf list) layout. */
+ * space-filling curve (the USE_SFC branch :8147-8220; a Hilbert curve, sfc.hip;
+ * sfc++'s own curve is not in the reference tree).  The placement is held as
+ * the comm_size - 1 cut keys along the curve, not as a per-cell owner table
+ * (the reference's replicated cell_process, :7311): a cell's process is the
+ * number of cuts <= the Hilbert key of its level-0 ancestor, on the host and
+ * on the device.  An SFC grid always uses the explicit layout. */
 enum { DCCRGX_PARTITION_BLOCK = 0, DCCRGX_PARTITION_SFC = 1 };
-/* owner of every level-0 cell (index id - 1) under the SFC placement */
+/* the comm_size - 1 cut keys of the SFC placement: cuts_out[r - 1] = the
+ * Hilbert key of process r's first level-0 cell (UINT64_MAX if it has none);
+ * host arithmetic over the curve, no per-cell work */
+int dccrgx_sfc_cuts(const uint64_t length[3], int32_t comm_size, uint64_t* cuts_out);
+/* owner of every level-0 cell (index id - 1) under the SFC placement, from the
+ * cuts (a listing for tests and tools; ctx is not used) */
 int dccrgx_sfc_owners(dccrgx_ctx* ctx, const uint64_t length[3], int32_t comm_size, int32_t* owner_host);
 /* the Hilbert key of every level-0 cell (index id - 1), host computation */
 int dccrgx_hilbert_keys_host(const uint64_t length[3], uint64_t* keys_out);

@@ -727,6 +727,16 @@ int dox_num_threads(void)
 #endif
 }
 
+/* the thread count of the parallel loops (the CPU baseline's sweep) */
+void dox_set_num_threads(int n)
+{
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
 long dox_build_uniform_slot_lists(const dox_grid* g, unsigned hood_length, uint64_t* row_ptr,
                                   uint32_t* nbr_slot, size_t cap)
 {

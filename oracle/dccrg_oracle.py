@@ -91,6 +91,7 @@ def lib():
         L.dox_gol_count.argtypes = [C.c_size_t, u64p, u32p, u32p, u32p]
         L.dox_gol_apply.argtypes = [C.c_size_t, u32p, u32p]
         L.dox_num_threads.restype = C.c_int
+        L.dox_set_num_threads.argtypes = [C.c_int]
         L.dox_build_uniform_slot_lists.restype = C.c_long
         L.dox_build_uniform_slot_lists.argtypes = [C.c_void_p, C.c_uint, u64p, u32p, C.c_size_t]
         f64p = C.POINTER(C.c_double)

@@ -509,8 +509,7 @@ def test_adaptive_advection_multirank(P):
             A.request_adaptation(g, *s)
         reqs = [g.amr_requests() for g in grids]
         union = [np.unique(np.concatenate([q[k] for q in reqs])).astype(np.uint64) for k in range(4)]
-        for g, geom in zip(grids, geoms):
-            A.finish_adaptation(g, geom, all_requests=union, update=False, agreed=True)
+        A.finish_adaptation_all(grids, geoms, union)
         loopback(grids, list(A.ALL))
 
     init_all()
@@ -584,6 +583,33 @@ def test_calls_between_prepare_and_finish_are_refused():
             with pytest.raises(D.DccrgxError) as e:
                 call()
             assert e.value.code == X.DCCRGX_ESTATE
+        # every other entry point that writes field data, request
+        # flags or retired data is refused too (the C-ABI directly)
+        L, h = D.lib(), g._h
+        fid = np.array([g.field_id("a")], dtype=np.int32)
+        fp = fid.ctypes.data_as(X._i32p)
+        res = np.zeros(4, dtype=np.int32)
+        rp = res.ctypes.data_as(X._i32p)
+        ids = np.array([5, 6], dtype=np.uint64)
+        buf = np.zeros(4096, dtype=np.uint8)
+        nbytes = np.zeros(1, dtype=np.uintp)
+        refused = {
+            "halo_self": lambda: L.dccrgx_halo_self(h, 0, fp, 1),
+            "halo_pack_to": lambda: L.dccrgx_halo_pack_to(h, 0, fp, 1, 0, buf.ctypes.data, buf.size,
+                                                          nbytes.ctypes.data_as(X._szp)),
+            "halo_unpack_from": lambda: L.dccrgx_halo_unpack_from(h, 0, fp, 1, 0, buf.ctypes.data, 0),
+            "exchange_start": lambda: L.dccrgx_exchange_start(h, 0, None, None, None, None),
+            "refine_completely": lambda: L.dccrgx_refine_completely(h, 5, rp),
+            "unrefine_completely": lambda: L.dccrgx_unrefine_completely(h, 5, rp),
+            "dont_unrefine": lambda: L.dccrgx_dont_unrefine(h, 5, rp),
+            "dont_refine": lambda: L.dccrgx_dont_refine(h, 5, rp),
+            "amr_request_cells": lambda: L.dccrgx_amr_request_cells(h, 0, ids.ctypes.data_as(X._u64p), 2, rp),
+            "amr_copy_from_parents": lambda: L.dccrgx_amr_copy_from_parents(h, fp, 1),
+            "amr_average_children": lambda: L.dccrgx_amr_average_children(h, fp, 1),
+            "clear_refined_unrefined_data": lambda: L.dccrgx_clear_refined_unrefined_data(h),
+        }
+        for name, call in refused.items():
+            assert call() == X.DCCRGX_ESTATE, name
         g.stop_refining_finish(True)
         want = o.stop_refining()
         assert [int(c) for c in g.get_new_cells()] == want[0]

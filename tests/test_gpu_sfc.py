@@ -112,7 +112,7 @@ def test_refinement_keeps_sfc_owners(length, M, per, hood, P, seed):
             assert grids[r].refine_completely(c) == o.refine_completely(r, c)
         reqs = [g.amr_requests() for g in grids]
         union = [np.unique(np.concatenate([q[k] for q in reqs])).astype(np.uint64) for k in range(4)]
-        got = [g.stop_refining(all_requests=union, agreed=True) for g in grids]
+        got = D.stop_refining_all(grids, union)
         want = o.stop_refining()
         for r in range(P):
             assert [int(c) for c in got[r]] == want[r]
