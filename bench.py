@@ -411,10 +411,13 @@ def secondary_host_heavy(ctx, D):
     for _ in range(steps):
         cells_steps += g.n_local
         g.update_copies_of_remote_neighbors(fields=["density"])
-        sets = A.check_for_adaptation(g, rel / M, thr, sens)
+        # check_for_adaptation + the adapter's requests, the sets kept on the
+        # device (A.check_and_request; the same request state as 2d.cpp's
+        # check, then adapt_grid's request loops)
+        A.check_and_request(g, rel / M, thr, sens)
         g.advect_step(cfl * dt_adv)
         ta = time.perf_counter()
-        A.adapt_grid(g, geom, *sets)
+        A.finish_adaptation(g, geom)
         dt_adv = g.max_time_step()
         t_adapt += time.perf_counter() - ta
     ctx.synchronize()

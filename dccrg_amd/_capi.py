@@ -217,6 +217,9 @@ SIGNATURES = {
                                              C.POINTER(C.c_double)]),
     "dccrgx_amr_copy_from_parents": (C.c_int, [_vp, _i32p, C.c_size_t]),
     "dccrgx_amr_average_children": (C.c_int, [_vp, _i32p, C.c_size_t]),
+    "dccrgx_amr_adapter_data_rules": (C.c_int, [_vp, _i32p, C.c_size_t]),
+    "dccrgx_advect_adapt_requests": (C.c_int, [_vp, C.c_int32, _vp, C.c_double, C.c_double, C.c_double,
+                                               C.POINTER(C.c_size_t)]),
 }
 
 _lib = None

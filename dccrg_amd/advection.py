@@ -105,6 +105,24 @@ def check_for_adaptation(grid: Dccrg, diff_increase: float, diff_threshold: floa
     return tuple(a[:k].copy() for a, k in zip(out, counts))
 
 
+def check_and_request(grid: Dccrg, diff_increase: float, diff_threshold: float,
+                      unrefine_sensitivity: float) -> Tuple[int, int, int]:
+    """check_for_adaptation followed by request_adaptation with the three
+    sets kept on the device (dccrgx_advect_adapt_requests): the same request
+    state, without the sets' round trip through host memory.  The requests
+    read only the leaf structure, not the density, so they may be made before
+    the solver step that 2d.cpp runs between the check and adapt_grid; finish
+    with finish_adaptation.  Returns the three set sizes."""
+    if grid.get_maximum_refinement_level() == 0:
+        return 0, 0, 0
+    counts = (C.c_size_t * 3)()
+    f = grid._advect_fields()
+    check(lib().dccrgx_advect_adapt_requests(grid._h, X.DEFAULT_NEIGHBORHOOD_ID, C.byref(f), diff_increase,
+                                             diff_threshold, unrefine_sensitivity, counts))
+    grid._refresh_info()
+    return tuple(int(c) for c in counts)
+
+
 def _request(grid: Dccrg, kind: int, ids: np.ndarray):
     ids = np.ascontiguousarray(ids, dtype=np.uint64)
     check(lib().dccrgx_amr_request_cells(grid._h, kind, ids.ctypes.data_as(X._u64p), ids.size, None))
@@ -137,8 +155,11 @@ def finish_adaptation(grid: Dccrg, geom: CartesianGeometry, all_requests=None,
     velocities and lengths, ghost update (skipped with update=False)."""
     if grid.get_maximum_refinement_level() == 0:
         return 0, 0
-    new = grid.stop_refining(all_requests=all_requests)
-    return _after_stop_refining(grid, geom, new, update)
+    if grid.ctx.comm_size == 1 and all_requests is None:
+        n_new = grid.stop_refining_count()  # the new cells' count only (no copy of the list)
+    else:
+        n_new = grid.stop_refining(all_requests=all_requests).size
+    return _after_stop_refining(grid, geom, n_new, update)
 
 
 def finish_adaptation_all(grids, geoms, all_requests, update: bool = False):
@@ -149,24 +170,26 @@ def finish_adaptation_all(grids, geoms, all_requests, update: bool = False):
     if grids[0].get_maximum_refinement_level() == 0:
         return [(0, 0) for _ in grids]
     news = stop_refining_all(grids, all_requests)
-    return [_after_stop_refining(g, geom, new, update) for g, geom, new in zip(grids, geoms, news)]
+    return [_after_stop_refining(g, geom, new.size, update) for g, geom, new in zip(grids, geoms, news)]
 
 
-def _after_stop_refining(grid: Dccrg, geom: CartesianGeometry, new, update: bool) -> Tuple[int, int]:
-    removed = grid.get_removed_cells()
+def _after_stop_refining(grid: Dccrg, geom: CartesianGeometry, n_new: int, update: bool) -> Tuple[int, int]:
+    n_removed = C.c_size_t()
+    check(lib().dccrgx_get_removed_cells(grid._h, None, 0, C.byref(n_removed)))
     # new cells are value-initialised by the rebuild (flux = 0); they take the
     # parent's density (:229-251).  Parents of removed cells: 0, then
     # += child / 8 over the children in ascending order (:253-300).  Both on
-    # the device, from the retired cells' data.
-    fd = np.array([grid.field_id("density")], dtype=np.int32)
-    check(lib().dccrgx_amr_copy_from_parents(grid._h, fd.ctypes.data_as(X._i32p), fd.size))
-    check(lib().dccrgx_amr_average_children(grid._h, fd.ctypes.data_as(X._i32p), fd.size))
+    # the device, from the retired cells' data, in one call.
+    fd = getattr(grid, "_adv_density_fid", None)
+    if fd is None:
+        fd = grid._adv_density_fid = np.array([grid.field_id("density")], dtype=np.int32)
+    check(lib().dccrgx_amr_adapter_data_rules(grid._h, fd.ctypes.data_as(X._i32p), fd.size))
     grid.clear_refined_unrefined_data()
     # velocities and lengths of every local cell (:303-313)
     _velocities_lengths(grid, geom)
     if update:
         grid.update_copies_of_remote_neighbors(fields=list(ALL))
-    return int(new.size), int(removed.size)
+    return int(n_new), int(n_removed.value)
 
 
 def max_time_step(grid: Dccrg) -> float:

@@ -916,6 +916,49 @@ int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccr
     return s;
 }
 
+int dccrgx_advect_adapt_requests(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
+                                 double diff_increase, double diff_threshold, double unrefine_sensitivity,
+                                 size_t counts[3])
+{
+    DX_NOT_PENDING(grid);
+    DX_CHECK(grid && f && counts, DCCRGX_EINVAL, "null argument");
+    counts[0] = counts[1] = counts[2] = 0;
+    if (grid->map.max_lvl == 0) return DCCRGX_OK;  // adapter.hpp:57-59, :190-192
+    const uint64_t n = grid->n_local;
+    int8_t* d_marks = nullptr;
+    PhaseTimer T("adapt_requests");
+    DX_TRY(adapt_marks_device(grid, hood_id, f, diff_increase, diff_threshold, unrefine_sensitivity, &d_marks,
+                              nullptr));
+    if (!d_marks) return DCCRGX_OK;
+    hipStream_t st = grid->ctx->compute;
+    const Explicit* E = grid->ex;
+    uint8_t* d_code = nullptr;
+    uint64_t* d_lists = nullptr;
+    int s = DCCRGX_OK;
+    if (ds_malloc(&d_code, n, st) != hipSuccess || ds_malloc(&d_lists, n * 8, st) != hipSuccess)
+        s = set_error(DCCRGX_ENOMEM, "out of device memory for the adaptation sets");
+    uint64_t* dev[3] = {nullptr, nullptr, nullptr};
+    if (s == DCCRGX_OK) {
+        hipLaunchKernelGGL(k_adapt_codes, dim3(grid_for(n)), dim3(256), 0, st, explicit_view(grid),
+                           (const uint64_t*)E->d_leaves, (const uint32_t*)E->d_slot_of_g,
+                           (const uint32_t*)E->d_local_g, (const int8_t*)d_marks, n, d_code);
+        if (hipGetLastError() != hipSuccess) s = set_error(DCCRGX_EHIP, "adaptation sets failed");
+        if (s == DCCRGX_OK) s = amr_dev_codes_to_device_lists(grid, d_code, n, d_lists, dev, counts);
+    }
+    T.lap("lists");
+    // adapter.hpp:197-213: refine, dont_unrefine, unrefine requests in this
+    // order, each a batch over its ascending device list (the calls' outcome)
+    const int32_t kinds[3] = {DCCRGX_AMR_REFINE, DCCRGX_AMR_DONT_UNREFINE, DCCRGX_AMR_UNREFINE};
+    if (s == DCCRGX_OK) amr_state(grid);
+    for (int k = 0; k < 3 && s == DCCRGX_OK; k++)
+        if (counts[k]) s = amr_dev_requests_ex(grid, kinds[k], nullptr, dev[k], counts[k], nullptr);
+    T.lap("requests");
+    ds_free(d_code, st);
+    ds_free(d_lists, st);
+    dx_free(d_marks);
+    return s;
+}
+
 int dccrgx_advect_set_geometry(dccrgx_grid* grid, const dccrgx_advect_fields* f, const double start[3],
                                const double level_0_cell_length[3])
 {
@@ -953,6 +996,14 @@ int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t
     DX_NOT_PENDING(grid);
     if (!grid->amr || grid->amr->removed.empty()) return DCCRGX_OK;
     return amr_dev_average_children(grid, fields, nf);
+}
+
+int dccrgx_amr_adapter_data_rules(dccrgx_grid* grid, const int32_t* fields, size_t nf)
+{
+    DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
+    DX_NOT_PENDING(grid);
+    if (!grid->amr || (grid->amr->new_cells.empty() && grid->amr->removed.empty())) return DCCRGX_OK;
+    return amr_dev_data_rules(grid, fields, nf);
 }
 
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt)

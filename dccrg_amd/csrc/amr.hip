@@ -570,6 +570,9 @@ bool amr_fail_injected(const dccrgx_grid* grid)
 
 }  // namespace
 
+// the grid's refinement state, made on first use (other translation units)
+Amr& amr_state(dccrgx_grid* grid) { return amr_of(grid); }
+
 // stop_refining between prepare and finish: the rebuild held aside, the
 // request flags before the decisions, and (when the caller passed the union of
 // every rank's sets) this rank's own sets

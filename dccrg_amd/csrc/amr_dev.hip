@@ -938,6 +938,14 @@ int amr_host_sync(dccrgx_grid* grid)
 // a batch of request calls of one kind in call order (explicit grids)
 int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results)
 {
+    return amr_dev_requests_ex(grid, kind, ids, nullptr, n, results);
+}
+
+// ids on the host, or dev_ids already on the device (stream-ordered on the
+// compute stream: the adaptation lists of dccrgx_advect_adapt_requests)
+int amr_dev_requests_ex(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, const uint64_t* dev_ids, size_t n,
+                        int32_t* results)
+{
     Amr& A = *grid->amr;
     DX_TRY(amr_dev_sync(grid));
     if (!n) return DCCRGX_OK;
@@ -947,12 +955,16 @@ int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_
     uint64_t *d_ids, *d_du;
     int32_t* d_res = nullptr;
     uint32_t *d_grp, *d_key, *d_ord, *d_dun;
-    DX_TRY(S.get(&d_ids, n));
+    if (dev_ids) {
+        d_ids = const_cast<uint64_t*>(dev_ids);
+    } else {
+        DX_TRY(S.get(&d_ids, n));
+        DX_TRY(dx_h2d_async(grid->ctx, d_ids, ids, n * 8, st));
+    }
     if (results) DX_TRY(S.get(&d_res, n));
     DX_TRY(S.get(&d_grp, a.n));
     DX_TRY(S.get(&d_key, n));
     DX_HIP(hipMemsetAsync(d_grp, 0xff, a.n * 4, st));
-    DX_TRY(dx_h2d_async(grid->ctx, d_ids, ids, n * 8, st));
     const unsigned b = blocks(n);
     if (kind == DCCRGX_AMR_UNREFINE) A.dev_unrefines = true;
     const int erase = A.dev_unrefines ? 1 : 0;
@@ -1251,9 +1263,41 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
 struct SlotView {
     ExView v;
     const uint32_t* slot_of_g;
-    const uint64_t* ret;
+    const uint64_t* ret;   // retired ids ascending, then their slots
     uint64_t n_ret;
+    const uint64_t* hkey;  // id -> slot table of the retired cells (hcap keys, then hcap slots)
+    uint64_t hmask;        // hcap - 1
 };
+
+__host__ __device__ inline uint64_t ret_hash(uint64_t id)  // splitmix64 finaliser
+{
+    id ^= id >> 31;
+    id *= 0x7fb5d329728ea185ull;
+    id ^= id >> 27;
+    id *= 0x81dadef4bc2dd44dull;
+    return id ^ (id >> 33);
+}
+
+// the table's value of a retired cell: its slot, with RET_REMOVED set if the
+// cell is one of the removed cells (a child of an unrefined parent, not a
+// refined leaf); ~0 if the id is not retired
+constexpr uint64_t RET_REMOVED = 1ull << 63;
+__device__ inline uint64_t ret_entry(const SlotView& s, uint64_t id)
+{
+    if (!s.n_ret) return ~0ull;
+    for (uint64_t h = ret_hash(id) & s.hmask;; h = (h + 1) & s.hmask) {
+        const uint64_t k = s.hkey[h];
+        if (k == id) return s.hkey[s.hmask + 1 + h];
+        if (k == 0) return ~0ull;
+    }
+}
+
+// slot of a retired cell, -1 if it is not one
+__device__ inline int64_t ret_slot(const SlotView& s, uint64_t id)
+{
+    const uint64_t e = ret_entry(s, id);
+    return e == ~0ull ? -1 : (int64_t)(e & ~RET_REMOVED);
+}
 
 __device__ inline int64_t slot_lookup(const SlotView& s, uint64_t id)
 {
@@ -1262,14 +1306,14 @@ __device__ inline int64_t slot_lookup(const SlotView& s, uint64_t id)
         const uint32_t x = s.slot_of_g[g];
         return x == NO_SLOT ? -1 : (int64_t)x;
     }
-    const uint64_t k = lower_bound_u64(s.ret, s.n_ret, id);
-    return k < s.n_ret && s.ret[k] == id ? (int64_t)s.ret[s.n_ret + k] : -1;
+    return ret_slot(s, id);
 }
 
 static SlotView slot_view(const dccrgx_grid* grid)
 {
     const Explicit* E = grid->ex;
-    return SlotView{explicit_view(grid), E->d_slot_of_g, E->d_ret, E->n_ret};
+    const uint64_t* hk = E->d_ret ? E->d_ret + 2 * E->n_ret : nullptr;
+    return SlotView{explicit_view(grid), E->d_slot_of_g, E->d_ret, E->n_ret, hk, E->ret_hcap ? E->ret_hcap - 1 : 0};
 }
 
 int amr_dev_retired_table(dccrgx_grid* grid)
@@ -1277,18 +1321,35 @@ int amr_dev_retired_table(dccrgx_grid* grid)
     Explicit* E = grid->ex;
     const uint64_t n = E->retired.size();
     E->n_ret = 0;
+    E->ret_hcap = 0;
     if (!n) return DCCRGX_OK;
-    std::vector<uint64_t> t(2 * n);
+    uint64_t cap = 64;
+    while (cap < 2 * n) cap <<= 1;  // load factor <= 1/2
+    std::vector<uint64_t> t(2 * n + 2 * cap, 0);
+    uint64_t* hk = t.data() + 2 * n;
+    uint64_t* hv = hk + cap;
+    // the removed cells among them (both lists ascending): marked in the table
+    static const std::vector<uint64_t> none;
+    const std::vector<uint64_t>& rem = grid->amr ? grid->amr->removed : none;
+    size_t r = 0;
     for (uint64_t i = 0; i < n; i++) {
-        t[i] = E->retired[i];
-        t[n + i] = E->ret_slot0 + i;
+        const uint64_t id = E->retired[i], slot = E->ret_slot0 + i;
+        t[i] = id;
+        t[n + i] = slot;
+        while (r < rem.size() && rem[r] < id) r++;
+        const bool removed = r < rem.size() && rem[r] == id;
+        uint64_t h = ret_hash(id) & (cap - 1);
+        while (hk[h]) h = (h + 1) & (cap - 1);
+        hk[h] = id;
+        hv[h] = slot | (removed ? RET_REMOVED : 0);
     }
     hipStream_t st = grid->ctx->compute;
     ds_free(E->d_ret, st);
     E->d_ret = nullptr;
-    DX_HIP(ds_malloc(&E->d_ret, 16 * n, st));
-    DX_TRY(dx_h2d_async(grid->ctx, E->d_ret, t.data(), 16 * n, st));
+    DX_HIP(ds_malloc(&E->d_ret, t.size() * 8, st));
+    DX_TRY(dx_h2d_async(grid->ctx, E->d_ret, t.data(), t.size() * 8, st));
     E->n_ret = n;
+    E->ret_hcap = cap;
     return DCCRGX_OK;
 }
 
@@ -1349,11 +1410,18 @@ __global__ void __launch_bounds__(256) k_average_children(SlotView sv, MapParams
             const uint64_t ci[3] = {pi[0] + (k & 1) * h, pi[1] + ((k >> 1) & 1) * h, pi[2] + ((k >> 2) & 1) * h};
             ch[k] = map_cell(mp, ci, l);
         }
+        // the first removed child of the parent does the sum, over the
+        // parent's removed children in ascending order.  Membership in the
+        // removed list and the children's slots come from the retired cells'
+        // table (removed cells are retired and marked there): eight
+        // independent probes instead of binary searches of the list
+        uint64_t ent[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) ent[k] = ret_entry(sv, ch[k]);
         bool first = true;
-        for (int k = 0; k < 8 && ch[k] < c; k++) {
-            const uint64_t j = lower_bound_u64(removed, n, ch[k]);
-            first &= !(j < n && removed[j] == ch[k]);
-        }
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (ch[k] < c && ent[k] != ~0ull && (ent[k] & RET_REMOVED)) first = false;
         if (!first) continue;
         const int64_t ps = slot_lookup(sv, par);
         if (ps < 0) {
@@ -1361,10 +1429,10 @@ __global__ void __launch_bounds__(256) k_average_children(SlotView sv, MapParams
             continue;
         }
         int64_t cs[8];
+#pragma unroll
         for (int k = 0; k < 8; k++) {
-            const uint64_t j = lower_bound_u64(removed, n, ch[k]);
-            cs[k] = j < n && removed[j] == ch[k] ? slot_lookup(sv, ch[k]) : -2;
-            if (cs[k] == -1) atomicOr(err, 1);
+            const bool in = ch[k] >= c && ent[k] != ~0ull && (ent[k] & RET_REMOVED);
+            cs[k] = in ? (int64_t)(ent[k] & ~RET_REMOVED) : -2;
         }
         for (int f = 0; f < fs.n; f++) {
             double* d = reinterpret_cast<double*>(fs.p[f]);
@@ -1392,44 +1460,55 @@ static int field_sets(const dccrgx_grid* grid, const int32_t* fields, size_t nf,
     return DCCRGX_OK;
 }
 
-static int run_rule(dccrgx_grid* grid, const std::vector<uint64_t>& cells, const int32_t* fields, size_t nf, bool avg)
+// the rules over `new_cells` (copy from parents) and then `removed`
+// (average of children; f64 fields), either list may be empty: one upload,
+// one error word read back
+static int run_rules(dccrgx_grid* grid, const std::vector<uint64_t>* new_cells, const std::vector<uint64_t>* removed,
+                     const int32_t* fields, size_t nf)
 {
     DX_CHECK(!grid->uniform, DCCRGX_ESTATE, "no refinement happened");
-    std::vector<FieldSet> sets;
-    DX_TRY(field_sets(grid, fields, nf, avg, sets));
+    const size_t nn = new_cells ? new_cells->size() : 0, nr = removed ? removed->size() : 0;
+    if (!nn && !nr) return DCCRGX_OK;
+    std::vector<FieldSet> copy_sets, avg_sets;
+    if (nn) DX_TRY(field_sets(grid, fields, nf, false, copy_sets));
+    if (nr) DX_TRY(field_sets(grid, fields, nf, true, avg_sets));
     hipStream_t st = grid->ctx->compute;
     Scratch S(st);
     uint64_t* d_cells;
     int32_t* d_err;
-    DX_TRY(S.get(&d_cells, cells.size()));
-    DX_TRY(S.get(&d_err, 1));
-    DX_HIP(hipMemsetAsync(d_err, 0, 4, st));
-    DX_TRY(dx_h2d_async(grid->ctx, d_cells, cells.data(), cells.size() * 8, st));
+    DX_TRY(S.get(&d_cells, nn + nr + 1));
+    d_err = reinterpret_cast<int32_t*>(d_cells + nn + nr);
+    std::vector<uint64_t> up(nn + nr + 1, 0);  // the lists and a zeroed error word in one upload
+    if (nn) std::copy(new_cells->begin(), new_cells->end(), up.begin());
+    if (nr) std::copy(removed->begin(), removed->end(), up.begin() + nn);
+    DX_TRY(dx_h2d_async(grid->ctx, d_cells, up.data(), up.size() * 8, st));
     const SlotView sv = slot_view(grid);
-    for (const FieldSet& fs : sets) {
-        if (avg)
-            hipLaunchKernelGGL(k_average_children, dim3(blocks(cells.size())), dim3(256), 0, st, sv, grid->map,
-                               (const uint64_t*)d_cells, (uint64_t)cells.size(), fs, d_err);
-        else
-            hipLaunchKernelGGL(k_copy_from_parents, dim3(blocks(cells.size())), dim3(256), 0, st, sv, grid->map,
-                               (const uint64_t*)d_cells, (uint64_t)cells.size(), fs, d_err);
-    }
+    for (const FieldSet& fs : copy_sets)
+        hipLaunchKernelGGL(k_copy_from_parents, dim3(blocks(nn)), dim3(256), 0, st, sv, grid->map,
+                           (const uint64_t*)d_cells, (uint64_t)nn, fs, d_err);
+    for (const FieldSet& fs : avg_sets)  // after the copies (the reference's order, adapter.hpp:229-300)
+        hipLaunchKernelGGL(k_average_children, dim3(blocks(nr)), dim3(256), 0, st, sv, grid->map,
+                           (const uint64_t*)d_cells + nn, (uint64_t)nr, fs, d_err);
     DX_HIP(hipGetLastError());
     int32_t err = 0;
     DX_TRY(dx_d2h(grid->ctx, &err, d_err, 4, st));
-    DX_CHECK(!err, DCCRGX_ENOTFOUND, "no data for a %s cell or its %s", avg ? "removed" : "new",
-             avg ? "parent" : "parent");
+    DX_CHECK(!err, DCCRGX_ENOTFOUND, "no data for a new or removed cell or its parent");
     return DCCRGX_OK;
 }
 
 int amr_dev_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 {
-    return run_rule(grid, grid->amr->new_cells, fields, nf, false);
+    return run_rules(grid, &grid->amr->new_cells, nullptr, fields, nf);
 }
 
 int amr_dev_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 {
-    return run_rule(grid, grid->amr->removed, fields, nf, true);
+    return run_rules(grid, nullptr, &grid->amr->removed, fields, nf);
+}
+
+int amr_dev_data_rules(dccrgx_grid* grid, const int32_t* fields, size_t nf)
+{
+    return run_rules(grid, &grid->amr->new_cells, &grid->amr->removed, fields, nf);
 }
 
 // codes 1..3 of the local cells (k_adapt_codes) into three id lists, each in
@@ -1493,16 +1572,29 @@ __global__ void __launch_bounds__(256) k_code_scatter(const uint8_t* __restrict_
 
 int amr_dev_codes_to_lists(dccrgx_grid* grid, const uint8_t* d_code, uint64_t n, uint64_t* out[3], size_t counts[3])
 {
+    Scratch S(grid->ctx->compute);
+    uint64_t* d_out;
+    DX_TRY(S.get(&d_out, std::max<uint64_t>(n, 1)));
+    uint64_t* dev[3];
+    DX_TRY(amr_dev_codes_to_device_lists(grid, d_code, n, d_out, dev, counts));
+    D2H v[3];
+    for (int k = 0; k < 3; k++) v[k] = D2H{out[k], dev[k], counts[k] * 8};
+    return dx_d2h_many(grid->ctx, v, 3, grid->ctx->compute);  // the three lists behind one synchronisation
+}
+
+// the same lists left on the device in d_out (n entries): dev[k] = list k,
+// counts[k] its length (one small read-back of the offsets)
+int amr_dev_codes_to_device_lists(dccrgx_grid* grid, const uint8_t* d_code, uint64_t n, uint64_t* d_out,
+                                  uint64_t* dev[3], size_t counts[3])
+{
     hipStream_t st = grid->ctx->compute;
     const Explicit* E = grid->ex;
     DX_CHECK(n < (1ull << 32), DCCRGX_EINVAL, "%llu local cells", (unsigned long long)n);
     Scratch S(st);
     const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (n + 256 * CODE_R - 1) / (256 * CODE_R));
     uint32_t *d_cnt, *d_off;
-    uint64_t* d_out;
     DX_TRY(S.get(&d_cnt, 3ull * nb + 1));
     DX_TRY(S.get(&d_off, 3ull * nb + 1));
-    DX_TRY(S.get(&d_out, std::max<uint64_t>(n, 1)));
     DX_HIP(hipMemsetAsync(d_cnt + 3ull * nb, 0, 4, st));  // the scan's last entry: the total
     hipLaunchKernelGGL(k_code_count, dim3(nb), dim3(256), 0, st, d_code, n, nb, d_cnt);
     size_t tb = 0;
@@ -1520,12 +1612,11 @@ int amr_dev_codes_to_lists(dccrgx_grid* grid, const uint8_t* d_code, uint64_t n,
                           {&start[3], d_off + 3ull * nb, 4}};
         DX_TRY(dx_d2h_many(grid->ctx, c, 4, st));
     }
-    D2H v[3];
     for (int k = 0; k < 3; k++) {
         counts[k] = (size_t)(start[k + 1] - start[k]);
-        v[k] = D2H{out[k], d_out + start[k], counts[k] * 8};
+        dev[k] = d_out + start[k];
     }
-    return dx_d2h_many(grid->ctx, v, 3, st);  // the three lists behind one synchronisation
+    return DCCRGX_OK;
 }
 
 }  // namespace dccrgx

@@ -295,6 +295,11 @@ struct Explicit {
     // the slot of each (n_ret of each), made by the rebuild that retired them
     uint64_t* d_ret = nullptr;
     uint64_t n_ret = 0;
+    // after them in the same allocation: an open-addressing table id -> slot
+    // of the same cells (ret_hcap keys, 0 = empty, then ret_hcap slots), so a
+    // kernel finds a retired cell's slot in one or two probes instead of a
+    // binary search (the data rules of new and removed cells)
+    uint64_t ret_hcap = 0;
 };
 
 // stop_refining between its two phases (amr.hip)
@@ -325,10 +330,14 @@ struct Amr {
 #define DX_NOT_PENDING(grid)                                                                           \
     DX_CHECK(!((grid) && (grid)->amr && (grid)->amr->pending), DCCRGX_ESTATE,                                      \
              "a prepared stop_refining awaits dccrgx_stop_refining_finish")
+// amr.hip: the grid's refinement state, made on first use
+Amr& amr_state(dccrgx_grid* grid);
 // amr_dev.hip
 int amr_dev_sync(dccrgx_grid* grid);
 int amr_host_sync(dccrgx_grid* grid);
 int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results);
+int amr_dev_requests_ex(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, const uint64_t* dev_ids, size_t n,
+                        int32_t* results);
 int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, uint64_t* first_out,
                    std::vector<uint64_t>& leaves_host,
                    std::vector<uint64_t>& retired, std::vector<uint64_t>& nr, bool* changed);
@@ -338,8 +347,12 @@ int amr_dev_retired_table(dccrgx_grid* grid);
 // of their children, on the device (tests/advection/adapter.hpp:229-300)
 int amr_dev_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_t nf);
 int amr_dev_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf);
+// both, copies first (one upload, one error read-back)
+int amr_dev_data_rules(dccrgx_grid* grid, const int32_t* fields, size_t nf);
 // ordered compaction of local cells by code (1..3) into three host lists
 int amr_dev_codes_to_lists(dccrgx_grid* grid, const uint8_t* d_code, uint64_t n, uint64_t* out[3], size_t counts[3]);
+int amr_dev_codes_to_device_lists(dccrgx_grid* grid, const uint8_t* d_code, uint64_t n, uint64_t* d_out,
+                                  uint64_t* dev[3], size_t counts[3]);
 
 
 struct CopySeg {

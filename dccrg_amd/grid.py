@@ -460,6 +460,16 @@ class Dccrg:
             raise X.DccrgxError(X.DCCRGX_ESTATE, "stop_refining failed on another rank; requests stay pending")
         return self.get_new_cells()
 
+    def stop_refining_count(self) -> int:
+        """stop_refining of a one-rank grid from its own requests, returning
+        the number of new cells instead of the list (get_new_cells has it)."""
+        if self.ctx.comm_size != 1:
+            raise X.DccrgxError(X.DCCRGX_ESTATE, "stop_refining_count is the one-rank form")
+        n_new = C.c_size_t()
+        check(lib().dccrgx_stop_refining(self._h, None, None, C.byref(n_new)))
+        self._refresh_info()
+        return int(n_new.value)
+
     def stop_refining_prepare(self, all_requests=None):
         """Phase one (dccrgx_stop_refining_prepare): (status, error message);
         the grid stays the old one until stop_refining_finish."""

@@ -500,6 +500,17 @@ int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccr
                                   double diff_increase, double diff_threshold, double unrefine_sensitivity,
                                   uint64_t* to_refine, uint64_t* not_to_unrefine, uint64_t* to_unrefine, size_t cap,
                                   size_t counts[3]);
+/* check_for_adaptation followed by the adapter's request loops
+ * (tests/advection/adapter.hpp:43-176, then :197-213: refine_completely of
+ * to_refine, dont_unrefine of not_to_unrefine, unrefine_completely of
+ * to_unrefine, in that order), with the three sets kept on the device: the
+ * same request state as dccrgx_advect_adaptation_sets plus
+ * dccrgx_amr_request_cells of each set, without the sets' round trip through
+ * host memory.  counts[3] receives the three set sizes.  Nothing on a grid
+ * with maximum level 0. */
+int dccrgx_advect_adapt_requests(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f,
+                                 double diff_increase, double diff_threshold, double unrefine_sensitivity,
+                                 size_t counts[3]);
 /* one step of tests/advection/2d.cpp:321-390: density halo start, inner
  * fluxes, halo wait, outer fluxes, apply -- fused: each cell's face fluxes
  * and the apply are one kernel writing the new density into a second buffer
@@ -582,6 +593,9 @@ int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_
  * then += child / 8 over its children in ascending id order, for each f64
  * field (adapter.hpp:253-300) */
 int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf);
+/* both rules above in one call, copies first (the adapter's order,
+ * adapter.hpp:229-300): one upload of the two lists, one error read-back */
+int dccrgx_amr_adapter_data_rules(dccrgx_grid* grid, const int32_t* fields, size_t nf);
 
 /* ------------------------------------------------------------------------ *
  * Poisson, tests/poisson/poisson_solve.hpp: Poisson_Solve (BiCG over face

@@ -45,7 +45,9 @@ def reference_run(n, M, steps, adapt_n, out):
     return states
 
 
-def device_run(n, M, steps, adapt_n):
+def device_run(n, M, steps, adapt_n, fused=False):
+    """fused: the adaptation sets stay on the device (A.check_and_request,
+    then finish_adaptation after the solve), as bench.py's adaptive loop."""
     rel, thr, sens, cfl = 0.025, 0.25, 0.5, 0.5
     ctx = D.Context(0, 0, 1)
     g = (D.Dccrg().set_initial_length((n, n, 1)).set_maximum_refinement_level(M)
@@ -61,10 +63,17 @@ def device_run(n, M, steps, adapt_n):
     for step in range(steps):
         g.update_copies_of_remote_neighbors(fields=["density"])
         adapt = adapt_n > 0 and step % adapt_n == 0
-        sets = A.check_for_adaptation(g, rel / M, thr, sens) if adapt else None
+        sets = None
+        if adapt and fused:
+            A.check_and_request(g, rel / M, thr, sens)
+        elif adapt:
+            sets = A.check_for_adaptation(g, rel / M, thr, sens)
         g.advect_step(cfl * dt)
-        if adapt:
+        if adapt and fused:
+            A.finish_adaptation(g, geom)
+        elif adapt:
             A.adapt_grid(g, geom, *sets)
+        if adapt:
             dt = g.max_time_step()
         states.append((step + 1, dt, g.local_cells().copy(), g.read_local("density").copy()))
     g.close()
@@ -102,3 +111,31 @@ def test_incremental_rebuild_matches_reference_solver(tmp_path, lib_options, n, 
         assert np.array_equal(ids0, ids1), f"leaf sets differ after step {s0}"
         scale = max(np.abs(rho0).max(), 1e-300)
         assert np.abs(rho0 - rho1).max() <= 1e-12 * scale, f"density after step {s0}"
+
+
+@pytest.mark.skipif(not os.path.exists(BIN), reason="oracle/_ref/ref_advection is built where /root/reference is")
+@pytest.mark.parametrize("n,M,steps,adapt_n", [(20, 2, 12, 1), (64, 2, 24, 1), (400, 2, 8, 1)])
+def test_device_resident_requests_match_reference_solver(tmp_path, n, M, steps, adapt_n):
+    """The adaptive loop as bench.py runs it: check_for_adaptation and the
+    request loops with the sets on the device (dccrgx_advect_adapt_requests),
+    the data rules in one call (dccrgx_amr_adapter_data_rules)."""
+    ref = reference_run(n, M, steps, adapt_n, str(tmp_path / "ref.bin"))
+    dev = device_run(n, M, steps, adapt_n, fused=True)
+    assert len(ref) == len(dev) == steps + 1
+    for (s0, dt0, ids0, rho0), (s1, dt1, ids1, rho1) in zip(ref, dev):
+        assert np.array_equal(ids0, ids1), f"leaf sets differ after step {s0}"
+        scale = max(np.abs(rho0).max(), 1e-300)
+        assert np.abs(rho0 - rho1).max() <= 1e-12 * scale, f"density after step {s0}"
+        assert abs(dt0 - dt1) <= 1e-12 * abs(dt0), f"dt after step {s0}"
+
+
+@pytest.mark.parametrize("n,M,steps", [(40, 2, 10), (128, 2, 6)])
+def test_device_resident_requests_equal_host_sets(n, M, steps):
+    """Bit for bit: the device-resident sets give the same leaves and
+    densities as the sets through host memory (no reference binary needed)."""
+    a = device_run(n, M, steps, 1, fused=False)
+    b = device_run(n, M, steps, 1, fused=True)
+    for (s0, dt0, ids0, rho0), (s1, dt1, ids1, rho1) in zip(a, b):
+        assert np.array_equal(ids0, ids1), s0
+        assert np.array_equal(rho0.view(np.uint64), rho1.view(np.uint64)), s0
+        assert dt0 == dt1

@@ -45,12 +45,17 @@ for _ in range(steps):
             ts.append(time.perf_counter())
     g.update_copies_of_remote_neighbors(fields=["density"])
     mark()
-    sets = A.check_for_adaptation(g, rel / M, thr, sens)
+    if os.environ.get("ADAPT_HOST_SETS"):  # the sets through host memory (check_for_adaptation)
+        sets = A.check_for_adaptation(g, rel / M, thr, sens)
+    else:
+        sets = None
+        A.check_and_request(g, rel / M, thr, sens)
     mark()
     g.advect_step(cfl * dt)
     mark()
     if seg == "2":  # adapt_grid in its parts
-        A.request_adaptation(g, *sets)
+        if sets is not None:
+            A.request_adaptation(g, *sets)
         mark()
         g.stop_refining()
         mark()
@@ -67,8 +72,11 @@ for _ in range(steps):
         mark()
         g.update_copies_of_remote_neighbors(fields=list(A.ALL))
         mark()
-    else:
+    elif sets is not None:
         A.adapt_grid(g, geom, *sets)
+        mark()
+    else:
+        A.finish_adaptation(g, geom)
         mark()
     dt = g.max_time_step()
     mark()

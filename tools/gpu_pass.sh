@@ -62,6 +62,21 @@ for step in "$@"; do
       tail -n 2 $out/adapt_big_phases.log
       ADAPT_N=1600 ADAPT_REL=0.006 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $out/adapt_trace -o run -- python3 tools/adapt_loop.py > $out/adapt_trace.log 2>&1 || fail adapt_trace $? $out/adapt_trace.log
       python3 tools/idle_gaps.py $out/adapt_trace > $out/adapt_gaps.txt 2>&1; tail -n 25 $out/adapt_gaps.txt ;;
+    adaptsmall)
+      # configs[2]'s 218k-leaf adaptive loop: split timing, phase timers that
+      # wait per lap, then a kernel + HIP-runtime trace and its census
+      timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_plain.log 2>&1 || fail adapt_plain $? $out/adapt_plain.log
+      tail -n 1 $out/adapt_plain.log
+      ADAPT_HOST_SETS=1 timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_host_sets.log 2>&1 || fail adapt_host_sets $? $out/adapt_host_sets.log
+      tail -n 1 $out/adapt_host_sets.log
+      ADAPT_SEG=2 timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_split.log 2>&1 || fail adapt_split $? $out/adapt_split.log
+      tail -n 3 $out/adapt_split.log
+      DCCRGX_TIMING=2 ADAPT_STEPS=8 timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_sync_phases.log 2>&1 || fail adapt_sync_phases $? $out/adapt_sync_phases.log
+      timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $out/adapt_trace -o run -- python3 tools/adapt_loop.py > $out/adapt_trace.log 2>&1 || fail adapt_trace $? $out/adapt_trace.log
+      tail -n 2 $out/adapt_trace.log
+      python3 tools/api_census.py $out/adapt_trace > $out/adapt_census.txt 2>&1 || true
+      python3 tools/idle_gaps.py $out/adapt_trace > $out/adapt_gaps.txt 2>&1 || true
+      tail -n 40 $out/adapt_census.txt ;;
     adaptsplit)
       # adapt_grid in its parts (synchronised after each), at 218 k and 3.5 M
       # leaves, then the library's phase timers waiting for the device per lap
