@@ -604,6 +604,7 @@ def user_stencil_gol(ctx, D):
                     "equals_library_step": same}
 
         staged = run(lambda a, b: L.us_gol_staged(g._h, hood, f(a), f(b), f("n"), 0, 1), 10)
+        one_stream = run(lambda a, b: L.us_gol_staged(g._h, hood, f(a), f(b), f("n"), 0, 2), 10)
         walk = run(lambda a, b: L.us_gol(g._h, hood, f(a), f(b), f("n"), 0), 3)
         staged["workload"] = ("headline grid (2048^3, hood 1, periodic z) stepped by the game of life written as a "
                               "device user functor over staged values (include/dccrgx_stencil.hpp "
@@ -612,6 +613,8 @@ def user_stencil_gol(ctx, D):
         walk["workload"] = ("the same functor reading every neighbor through its slot (for_each_cell, "
                             "examples/user_stencil.hip us_gol)")
         staged["walk"] = walk
+        one_stream["workload"] = "the staged launches with the edge walks on the caller's stream (no side stream)"
+        staged["one_stream"] = one_stream
         return staged
     finally:
         g.close()

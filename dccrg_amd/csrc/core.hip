@@ -302,6 +302,70 @@ __global__ void __launch_bounds__(256) k_ids_to_indices_u(MapParams p, const uin
     }
 }
 
+// k_ids_to_indices_u with the next pass's ids loaded before this pass is
+// computed and stored (one HBM round trip per pass was exposed: the stores
+// of a pass wait for the LDS exchange, and the next loads waited for them),
+// and the levels staged in LDS too, leaving as 16-byte stores
+template <int U>
+__global__ void __launch_bounds__(256) k_ids_to_indices_p(MapParams p, const uint64_t* __restrict__ ids,
+                                                          size_t n, uint64_t* __restrict__ idx3,
+                                                          int32_t* __restrict__ lvl)
+{
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    constexpr int B = 256 * U;
+    __shared__ __attribute__((aligned(16))) uint64_t s[3 * B];
+    __shared__ __attribute__((aligned(16))) int32_t sl[B];
+    const size_t step = (size_t)gridDim.x * B;
+    size_t base = (size_t)blockIdx.x * B;
+    uint64_t c[U];
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+        const size_t i = base + k * 256 + threadIdx.x;
+        c[k] = i < n ? __builtin_nontemporal_load(ids + i) : 0;
+    }
+    for (; base < n; base += step) {
+        uint64_t nx[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {  // the next pass's ids, in flight while this pass is finished
+            const size_t i = base + step + k * 256 + threadIdx.x;
+            nx[k] = i < n ? __builtin_nontemporal_load(ids + i) : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            uint64_t o[3] = {0, 0, 0};
+            int l = -1;
+            if (base + k * 256 + threadIdx.x < n) map_indices(p, c[k], o, &l);
+            const int j = k * 256 + threadIdx.x;
+            s[3 * j + 0] = o[0];
+            s[3 * j + 1] = o[1];
+            s[3 * j + 2] = o[2];
+            sl[j] = l;
+        }
+        __syncthreads();
+        const size_t cnt = n - base < (size_t)B ? n - base : (size_t)B;
+        if (cnt == (size_t)B) {
+            u64x2* dst = (u64x2*)(idx3 + 3 * base);
+            for (int k = threadIdx.x; k < 3 * B / 2; k += 256) {
+                const u64x2 v = {s[2 * k], s[2 * k + 1]};
+                __builtin_nontemporal_store(v, dst + k);
+            }
+            if (lvl)
+                for (int k = threadIdx.x; k < B / 4; k += 256) {
+                    const i32x4 v = {sl[4 * k], sl[4 * k + 1], sl[4 * k + 2], sl[4 * k + 3]};
+                    __builtin_nontemporal_store(v, (i32x4*)(lvl + base) + k);
+                }
+        } else {
+            for (size_t k = threadIdx.x; k < 3 * cnt; k += 256) idx3[3 * base + k] = s[k];
+            if (lvl)
+                for (size_t k = threadIdx.x; k < cnt; k += 256) lvl[base + k] = sl[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < U; k++) c[k] = nx[k];
+    }
+}
+
 __global__ void __launch_bounds__(256) k_indices_to_ids(MapParams p, const uint64_t* __restrict__ idx3,
                                                         const int32_t* __restrict__ lvl, size_t n,
                                                         uint64_t* __restrict__ ids)
@@ -380,7 +444,15 @@ int dccrgx_map_ids_to_indices(const dccrgx_mapping* map, const uint64_t* ids, si
     DX_TRY(make_map_params(map, &p));
     if (n == 0) return DCCRGX_OK;
     DX_CHECK(ids, DCCRGX_EINVAL, "null ids");
-    if (idx3 && ((uintptr_t)idx3 & 15) == 0) {
+    if (idx3 && ((uintptr_t)idx3 & 15) == 0 && ((uintptr_t)lvl & 15) == 0) {
+        // one pass per workgroup up to 2^20 workgroups: 2^26 ids 0.475 -> 0.42 ms
+        // against 2048 workgroups of 64 passes (tools/map_bench.py A/B,
+        // profiles/s11_map_grid_ab.log); the pass prefetch serves larger n
+        constexpr size_t per = 256 * 2;
+        const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>((n + per - 1) / per, 1u << 20));
+        hipLaunchKernelGGL(k_ids_to_indices_p<2>, dim3(g), dim3(256), 0, (hipStream_t)stream, p, ids, n, idx3,
+                           lvl);
+    } else if (idx3 && ((uintptr_t)idx3 & 15) == 0) {
         constexpr size_t per = 256 * 2;
         const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>((n + per - 1) / per, 256 * 8));
         hipLaunchKernelGGL(k_ids_to_indices_u<2>, dim3(g), dim3(256), 0, (hipStream_t)stream, p, ids, n, idx3,

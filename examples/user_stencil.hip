@@ -65,6 +65,7 @@ int us_gol_staged(const dccrgx_grid* grid, int32_t hood_id, int32_t fin, int32_t
     if (e) return e;
     dccrgx_user::StagedOptions opt;
     opt.staged = staged != 0;
+    opt.side_stream = staged != 2;  // 2: the edge launches on the caller's stream too
     return dccrgx_user::for_each_cell_staged(
         grid, hood_id, region, dccrgx_user::Fields<uint32_t, 1>{{in}},
         [=] __device__(const auto& cell) {

@@ -41,6 +41,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <type_traits>
 
 #include "dccrgx.h"
@@ -1148,15 +1149,17 @@ int launch_edge(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, int
  * edge walk */
 template <class T, int NF, int SHAPE, class F>
 int staged_range(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, int64_t s1, F f, hipStream_t st,
-                 int64_t want)
+                 int64_t want, hipStream_t se)
 {
+    // st: the staged kernel; se: the edge walks and wrap slices (cells
+    // disjoint from the staged kernel's, run beside it when se != st)
     const int64_t lc = (int64_t)v.lc, cb = v.cbase;
     const int64_t m0 = s0 > 1 - cb ? s0 : 1 - cb;
     const int64_t m1 = s1 < lc - 1 - cb ? s1 : lc - 1 - cb;
     int e = DCCRGX_OK;
     if (m1 > m0) {
         e = launch_staged<T, NF, SHAPE>(v, fld, m0, m1, f, st, want);
-        if (e == DCCRGX_OK) e = launch_edge<T, NF, SHAPE>(v, fld, m0, m1, false, f, st);
+        if (e == DCCRGX_OK) e = launch_edge<T, NF, SHAPE>(v, fld, m0, m1, false, f, se);
         if (e != DCCRGX_OK) return e;
     }
     for (int side = 0; side < 2; side++) {
@@ -1167,15 +1170,43 @@ int staged_range(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, in
         const bool whole = o0 >= v.lo && o1 <= v.hi, none = o1 <= v.lo || o0 >= v.hi;
         if (v.per[2] && lc >= 3 && (whole || none)) {
             const int64_t across = whole ? (int64_t)oc - cb : (side == 0 ? s - 1 : s + 1);
-            e = side == 0 ? launch_staged_wrap<T, NF, SHAPE, CLS_LOW>(v, fld, s, across, f, st)
-                          : launch_staged_wrap<T, NF, SHAPE, CLS_HIGH>(v, fld, s, across, f, st);
-            if (e == DCCRGX_OK) e = launch_edge<T, NF, SHAPE>(v, fld, s, s + 1, false, f, st);
+            e = side == 0 ? launch_staged_wrap<T, NF, SHAPE, CLS_LOW>(v, fld, s, across, f, se)
+                          : launch_staged_wrap<T, NF, SHAPE, CLS_HIGH>(v, fld, s, across, f, se);
+            if (e == DCCRGX_OK) e = launch_edge<T, NF, SHAPE>(v, fld, s, s + 1, false, f, se);
         } else {
-            e = launch_edge<T, NF, SHAPE>(v, fld, s, s + 1, true, f, st);
+            e = launch_edge<T, NF, SHAPE>(v, fld, s, s + 1, true, f, se);
         }
         if (e != DCCRGX_OK) return e;
     }
     return DCCRGX_OK;
+}
+
+/* a second stream per device for the edge launches of a staged launch (they
+ * run beside the staged kernel: edge walks are latency-bound on few waves),
+ * with the events that fork it from and join it to the caller's stream;
+ * made on first use, kept for the process */
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    bool ok = false;
+};
+
+inline SideStream* side_stream()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    static SideStream ss[64];
+    static std::mutex m;
+    std::lock_guard<std::mutex> lk(m);
+    SideStream& x = ss[dev];
+    if (!x.ok) {
+        if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess)
+            return nullptr;
+        x.ok = true;
+    }
+    return &x;
 }
 
 }  // namespace detail
@@ -1184,6 +1215,7 @@ int staged_range(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, in
 struct StagedOptions {
     int64_t workgroups = 131072;  // target workgroups of the staged kernel (tiles x slice chunks)
     bool staged = true;          // false: every cell through the walk (for comparisons)
+    bool side_stream = true;     // edge launches on a second stream beside the staged kernel
 };
 
 /* Launch f(cell) for every cell of the region described by v, the declared
@@ -1207,18 +1239,33 @@ int for_each_cell_staged(const dccrgx_stencil_view& v, Fields<T, NF> fld, F f, h
     // leave no inner cells), planes of < 2^31 bytes
     const bool fast = opt.staged && shape != 0 && v.la >= 3 && v.lb >= 3 && v.lc >= 3 &&
                       v.la * v.lb * sizeof(T) < (1ull << 31);
-    for (int r = 0; r < 2; r++) {
+    // the edge launches fork onto a second stream and join back, so the
+    // caller's stream orders everything as one launch would
+    detail::SideStream* side = fast && opt.side_stream ? detail::side_stream() : nullptr;
+    std::unique_lock<std::mutex> side_lock;
+    if (side) {
+        static std::mutex side_m;  // one staged launch at a time uses the side stream's events
+        side_lock = std::unique_lock<std::mutex>(side_m);
+        if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
+            return DCCRGX_EHIP;
+    }
+    hipStream_t se = side ? side->s : st;
+    int err = DCCRGX_OK;
+    for (int r = 0; r < 2 && err == DCCRGX_OK; r++) {
         const int64_t s0 = v.s0[r], s1 = v.s1[r];
         if (s1 <= s0) continue;
-        int e;
         if (!fast)
-            e = detail::launch_slices(g, s0, s1, walk, st);
+            err = detail::launch_slices(g, s0, s1, walk, st);
         else if (shape == DCCRGX_SHAPE_CUBE1)
-            e = detail::staged_range<T, NF, DCCRGX_SHAPE_CUBE1>(v, fld, s0, s1, f, st, opt.workgroups);
+            err = detail::staged_range<T, NF, DCCRGX_SHAPE_CUBE1>(v, fld, s0, s1, f, st, opt.workgroups, se);
         else
-            e = detail::staged_range<T, NF, DCCRGX_SHAPE_FACES>(v, fld, s0, s1, f, st, opt.workgroups);
-        if (e != DCCRGX_OK) return e;
+            err = detail::staged_range<T, NF, DCCRGX_SHAPE_FACES>(v, fld, s0, s1, f, st, opt.workgroups, se);
     }
+    if (side) {  // joined also after a failed launch: the caller's stream never runs ahead of the side stream
+        if (hipEventRecord(side->join, side->s) != hipSuccess || hipStreamWaitEvent(st, side->join, 0) != hipSuccess)
+            return DCCRGX_EHIP;
+    }
+    if (err != DCCRGX_OK) return err;
     return hipGetLastError() == hipSuccess ? DCCRGX_OK : DCCRGX_EHIP;
 }
 

@@ -237,7 +237,7 @@ LARGER = [((70, 40, 9), (True, False, True), 1),
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("staged", [None, 0, 1])
+@pytest.mark.parametrize("staged", [None, 0, 1, 2])
 @pytest.mark.parametrize("P", [1, 3])
 @pytest.mark.parametrize("length,per,hood_len", LARGER)
 def test_gol_functor_larger_grids(length, per, hood_len, P, staged):
@@ -246,7 +246,8 @@ def test_gol_functor_larger_grids(length, per, hood_len, P, staged):
     rank slabs: equal to the oracle's run (oracle gol_reference_run, the
     reference's lists) on every rank.  staged: None = for_each_cell (slots),
     1 = for_each_cell_staged (the staged kernel for the cube / faces plus the
-    boundary walks), 0 = for_each_cell_staged with every cell walked."""
+    boundary walks on a second stream), 2 = the same on the caller's stream
+    alone, 0 = for_each_cell_staged with every cell walked."""
     import torch
 
     import dccrg_amd as D

@@ -5,6 +5,7 @@
 //   ./us_sweep [n]
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "dccrgx_stencil.hpp"
