@@ -174,8 +174,11 @@ int gol_launch(dccrgx_grid* grid, const Hood& h, const Field& in, const Field& o
     if (u.LB == 1 && vec) {
         // 2-D / 1-D grids: k_gol26_rowv, 4 waves x 256 cells of a row per
         // workgroup, non-temporal stores (1-2 % faster than plain stores in
-        // every A/B pairing, profiles/r7c_gol2d_nts_ab.log)
-        Gol4Args v = gol4_plan(a, 1024, 1, nsl, chunk);
+        // every A/B pairing, profiles/r7c_gol2d_nts_ab.log); 65536 workgroups
+        // (4 rows each at 16384^2): 5.20 -> 5.46-5.56 TB/s against 8192, in
+        // both of two A/B rounds on one box (2048 / 4096 / 16384 / 32768 /
+        // 131072 in between or slower, profiles/s13_gol2d_want_ab.log)
+        Gol4Args v = gol4_plan(a, 1024, 1, nsl, chunk, 65536);
         DX_CHECK(v.nwg, DCCRGX_EINVAL, "grid too large for one launch");
         hipLaunchKernelGGL((k_gol26_rowv<4, true>), dim3(v.nwg), dim3(256), 0, st, v, mult);
     } else if (u.LB == 1) {
