@@ -17,6 +17,9 @@ from dccrg_amd import _capi as X  # noqa: E402
 from dccrg_amd._capi import check, lib  # noqa: E402
 import numpy as np  # noqa: E402
 
+if os.environ.get("ADAPT_INCREMENTAL"):  # force the incremental (1) or the full (0) list rebuild
+    from dccrg_amd.grid import set_test_option
+    set_test_option("incremental", int(os.environ["ADAPT_INCREMENTAL"]))
 ctx = D.Context(0, 0, 1)
 rel, thr, sens, cfl, M = 0.025, 0.25, 0.5, 0.5, 2
 rel = float(os.environ.get("ADAPT_REL", rel))  # larger grids: smaller differences between neighbors
