@@ -747,6 +747,7 @@ int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect
                          int32_t region)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -760,6 +761,7 @@ int dccrgx_advect_fluxes(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect
 int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     DX_TRY(explicit_host_leaves(grid));
     AdvPtrs p;
@@ -782,6 +784,7 @@ int dccrgx_advect_apply(dccrgx_grid* grid, const dccrgx_advect_fields* f)
 int dccrgx_advect_max_time_step(dccrgx_grid* grid, const dccrgx_advect_fields* f, double* local_min)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid && local_min, DCCRGX_EINVAL, "null argument");
     AdvPtrs p;
     DX_TRY(adv_ptrs(grid, f, &p));
@@ -868,6 +871,7 @@ int dccrgx_advect_adapt_marks(dccrgx_grid* grid, int32_t hood_id, const dccrgx_a
                               int8_t* marks_out, double* max_diff_out)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid && f && (marks_out || !grid->n_local), DCCRGX_EINVAL, "null argument");
     int8_t* d_marks = nullptr;
     DX_TRY(adapt_marks_device(grid, hood_id, f, diff_increase, diff_threshold, unrefine_sensitivity, &d_marks,
@@ -885,6 +889,7 @@ int dccrgx_advect_adaptation_sets(dccrgx_grid* grid, int32_t hood_id, const dccr
                                   size_t counts[3])
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid && f && counts, DCCRGX_EINVAL, "null argument");
     counts[0] = counts[1] = counts[2] = 0;
     if (grid->map.max_lvl == 0) return DCCRGX_OK;  // adapter.hpp:57-59
@@ -921,6 +926,7 @@ int dccrgx_advect_adapt_requests(dccrgx_grid* grid, int32_t hood_id, const dccrg
                                  size_t counts[3])
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid && f && counts, DCCRGX_EINVAL, "null argument");
     counts[0] = counts[1] = counts[2] = 0;
     if (grid->map.max_lvl == 0) return DCCRGX_OK;  // adapter.hpp:57-59, :190-192
@@ -963,6 +969,7 @@ int dccrgx_advect_set_geometry(dccrgx_grid* grid, const dccrgx_advect_fields* f,
                                const double level_0_cell_length[3])
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid && f && start && level_0_cell_length, DCCRGX_EINVAL, "null argument");
     AdvPtrs p;
     DX_TRY(adv_ptrs(grid, f, &p));
@@ -985,6 +992,7 @@ int dccrgx_advect_set_geometry(dccrgx_grid* grid, const dccrgx_advect_fields* f,
 int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 {
     DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     if (!grid->amr || grid->amr->new_cells.empty()) return DCCRGX_OK;
     return amr_dev_copy_from_parents(grid, fields, nf);
@@ -993,6 +1001,7 @@ int dccrgx_amr_copy_from_parents(dccrgx_grid* grid, const int32_t* fields, size_
 int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 {
     DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     if (!grid->amr || grid->amr->removed.empty()) return DCCRGX_OK;
     return amr_dev_average_children(grid, fields, nf);
@@ -1001,6 +1010,7 @@ int dccrgx_amr_average_children(dccrgx_grid* grid, const int32_t* fields, size_t
 int dccrgx_amr_adapter_data_rules(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 {
     DX_CHECK(grid && (fields || !nf), DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     if (!grid->amr || (grid->amr->new_cells.empty() && grid->amr->removed.empty())) return DCCRGX_OK;
     return amr_dev_data_rules(grid, fields, nf);
@@ -1009,6 +1019,7 @@ int dccrgx_amr_adapter_data_rules(dccrgx_grid* grid, const int32_t* fields, size
 int dccrgx_advect_step(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_fields* f, double dt)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid && f, DCCRGX_EINVAL, "null argument");
     // 2d.cpp:321-390: start density halo, inner fluxes, wait, outer fluxes,
     // apply -- fused: the flux kernels write the new density into the other

@@ -527,6 +527,23 @@ static int check_explicit_memory(const dccrgx_grid* grid, uint64_t N)
     return DCCRGX_OK;
 }
 
+bool explicit_too_large(const dccrgx_grid* grid)
+{
+    if (!grid->uniform) return false;
+    if (grid->g.N >= (1ull << 32)) return true;
+    return check_explicit_memory(grid, grid->g.N) != DCCRGX_OK;
+}
+
+// a uniform grid refines in place (hybrid.hip) instead of turning explicit:
+// one process, when the explicit form would not fit the device (or the test
+// option "hybrid" asks for it), or when it already holds refined cells
+static bool use_hybrid(const dccrgx_grid* grid)
+{
+    if (!grid->uniform || grid->ctx->comm_size != 1) return false;
+    if (grid->hy || test_opt(OPT_HYBRID, 0)) return true;
+    return explicit_too_large(grid);
+}
+
 // refinement requests need the explicit form (neighbor lists of the local
 // leaves, the leaf list replicated); a uniform grid is converted on its first
 // request.  The memory check refuses long before the 32-bit leaf indices
@@ -584,6 +601,8 @@ struct StopTxn {
     bool from_sets = false;
     FlatSet saved[4];
     std::vector<uint64_t> nr;  // the new dont_refine closure
+    bool hybrid = false;       // a refine in place of a uniform grid, done at the commit
+    std::vector<uint64_t> hybrid_cells;
 };
 
 int amr_ensure_explicit(dccrgx_grid* grid) { return ensure_explicit(grid); }
@@ -618,6 +637,12 @@ int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
         *result = map_level(grid->map, cell) == 0 && cell <= grid->g.N &&
                   part_owner(grid->g.part, cell) == grid->ctx->rank;
         return DCCRGX_OK;
+    }
+    if (grid->hy) {  // refined cells inside a uniform grid: level-0 leaves only (first slice)
+        if (map_level(grid->map, cell) > 0 && hybrid_slot(grid, cell) >= 0)
+            return set_error(DCCRGX_ESTATE, "refining a level-1 cell of a uniform grid with refined cells "
+                                            "(hybrid layout) is not supported");
+        if (hybrid_slot(grid, cell) < 0) return DCCRGX_OK;  // not a leaf
     }
     if (grid->uniform) {
         // dccrg.hpp:2476-2546 on a grid of level-0 cells: no coarser neighbor
@@ -668,6 +693,7 @@ int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 {
     DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     DX_TRY(explicit_host_leaves(grid));
     *result = 0;
@@ -716,6 +742,7 @@ int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result
 int dccrgx_dont_unrefine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 {
     DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     DX_TRY(explicit_host_leaves(grid));
     *result = 0;
@@ -768,6 +795,7 @@ int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 int dccrgx_amr_request_cells(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results)
 {
     DX_CHECK(grid && (ids || !n) && kind >= 0 && kind < 4, DCCRGX_EINVAL, "bad argument");
+    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     if (!grid->uniform) {  // the batch on the device (amr_dev.hip), results as the calls in this order
         amr_of(grid);
@@ -843,6 +871,23 @@ int dccrgx_stop_refining_prepare(dccrgx_grid* grid, const uint64_t* const* sets,
         }
         return code;
     };
+    if (grid->uniform && use_hybrid(grid)) {
+        // level-0 refines only: between levels 0 and 1 nothing is induced or
+        // overridden (2:1 holds for any set), so the decision is the
+        // requested cells minus the dont_refine ones (dccrg.hpp:10130-10693);
+        // level-0 unrefines are no-ops (:2610-2612)
+        for (uint64_t c : A.to_unrefine.sorted())
+            if (map_level(grid->map, c) > 0)
+                return unwind_sets(set_error(DCCRGX_ESTATE, "unrefining cells of a uniform grid with refined cells "
+                                                            "(hybrid layout) is not supported"));
+        for (uint64_t c : A.to_refine.sorted())
+            if (!A.not_to_refine.count(c)) X.hybrid_cells.push_back(c);
+        X.hybrid = true;
+        X.nr = A.not_to_refine.sorted();
+        if (n_new) *n_new = 8 * X.hybrid_cells.size();
+        A.pending = txn.release();
+        return DCCRGX_OK;
+    }
     if (grid->uniform) {  // requests of a uniform grid live on the host (amr_dev.hip: explicit grids)
         if (A.to_refine.empty() && A.to_unrefine.empty()) {
             // nothing can change; on a level-0 grid the dont_refine closure is
@@ -914,6 +959,19 @@ int dccrgx_stop_refining_finish(dccrgx_grid* grid, int32_t commit)
     A.pending = nullptr;
     StopTxn& X = *txn;
     hipStream_t st = grid->ctx->compute;
+    if (commit && X.hybrid) {
+        // the refine in place; on failure the grid and the requests stay
+        const int e = hybrid_refine(grid, X.hybrid_cells, A.new_cells);
+        if (e != DCCRGX_OK) return e;
+        A.removed.clear();
+        A.to_refine.clear();
+        A.to_unrefine.clear();
+        A.not_to_unrefine.clear();
+        A.not_to_refine = FlatSet(X.nr.data(), X.nr.data() + X.nr.size());
+        A.host_current = true;
+        A.dev_current = false;
+        return DCCRGX_OK;
+    }
     if (commit) {
         if (X.rebuilt) rebuild_commit(grid, X.rb);
         ds_free(X.d_saved, st);

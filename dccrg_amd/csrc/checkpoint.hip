@@ -282,6 +282,7 @@ int dccrgx_save_sizes(const dccrgx_grid* grid, const int32_t* fields, size_t nf,
                       uint64_t* n_bytes)
 {
     DX_CHECK(grid && n_cells && n_bytes, DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_TRY(explicit_host_leaves(grid));
     FDesc d;
     bool var = false;
@@ -368,6 +369,7 @@ int dccrgx_save_grid_data(const dccrgx_grid* grid, const char* path, uint64_t of
 {
     DX_CHECK(grid && path && (header || !header_bytes) && geometry && geometry_bytes >= 4, DCCRGX_EINVAL,
              "null argument");
+    DX_NO_HYBRID(grid);
     DX_TRY(explicit_host_leaves(grid));
     FDesc d;
     bool var = false;
@@ -577,6 +579,7 @@ int dccrgx_grid_load(dccrgx_ctx* ctx, const char* path, const dccrgx_file_info* 
 int dccrgx_load_cell_data(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     DX_CHECK(grid->load, DCCRGX_ESTATE, "the grid was not loaded from a file (or loading finished)");
     FDesc d;
@@ -656,6 +659,7 @@ int dccrgx_load_cell_data(dccrgx_grid* grid, const int32_t* fields, size_t nf)
 int dccrgx_finish_loading_grid_data(dccrgx_grid* grid)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    DX_NO_HYBRID(grid);
     load_state_free(grid);
     return DCCRGX_OK;
 }
@@ -668,6 +672,7 @@ int dccrgx_save_grid_data_host(const dccrgx_grid* grid, const char* path, uint64
     DX_CHECK(grid && path && (header || !header_bytes) && geometry && geometry_bytes >= 4 &&
                  (record_bytes || !grid->n_local) && (records || !bytes),
              DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_TRY(explicit_host_leaves(grid));
     uint64_t tot = 0;
     for (uint64_t i = 0; i < grid->n_local; i++) tot += record_bytes[i];
@@ -686,6 +691,7 @@ int dccrgx_save_grid_data_host(const dccrgx_grid* grid, const char* path, uint64
 int dccrgx_load_cell_records_host(dccrgx_grid* grid, const uint64_t* record_bytes, void* out, size_t bytes)
 {
     DX_CHECK(grid && (record_bytes || !grid->n_local) && (out || !bytes), DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid->load, DCCRGX_ESTATE, "the grid was not loaded from a file (or loading finished)");
     LoadState& L = *grid->load;
     const uint64_t n = grid->n_local;

@@ -1169,7 +1169,8 @@ std::atomic<int64_t> g_test_opt[OPT_COUNT];
 std::atomic<bool> g_test_set[OPT_COUNT];
 const char* const kTestOptName[OPT_COUNT] = {"gol_scalar",  "gol_chunk",      "poisson_multi",
                                              "poisson_solo_global", "incremental", "ou_small",
-                                             "corrupt_ghost", "fail_stop_refining", "check_init", "full_nto"};
+                                             "corrupt_ghost", "fail_stop_refining", "check_init", "full_nto",
+                                             "hybrid"};
 }  // namespace
 
 int64_t test_opt(TestOpt o, int64_t dflt)

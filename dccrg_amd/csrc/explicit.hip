@@ -158,22 +158,29 @@ __global__ void __launch_bounds__(256) k_ex_nof(ExView v, const int32_t* __restr
                     continue;
                 }
             }
-            if (l < M) {
+            if (l < M) {  // the 8 children, listed only when all exist
                 const int64_t hl = L / 2;
+                int64_t gc[8];
                 bool all = true;
-                code |= 3ull << (2 * k);
-                for (int dz = 0; dz < 2; dz++)
-                    for (int dy = 0; dy < 2; dy++)
-                        for (int dx = 0; dx < 2; dx++) {
-                            const uint64_t ci[3] = {wi[0] + dx * hl, wi[1] + dy * hl, wi[2] + dz * hl};
-                            const uint64_t ch = map_cell(p, ci, l + 1);
-                            const int64_t gc = ex_find(v, ch);
-                            all &= gc >= 0;
-                            emit(ch, gc, h[0] * L + dx * hl, h[1] * L + dy * hl, h[2] * L + dz * hl);
-                        }
-                if (all) continue;
+                for (int j = 0; j < 8; j++) {
+                    const uint64_t ci[3] = {wi[0] + (j & 1) * hl, wi[1] + ((j >> 1) & 1) * hl, wi[2] + ((j >> 2) & 1) * hl};
+                    gc[j] = ex_find(v, map_cell(p, ci, l + 1));
+                    all &= gc[j] >= 0;
+                }
+                if (all) {
+                    code |= 3ull << (2 * k);
+                    for (int j = 0; j < 8; j++) {
+                        const int64_t dx = j & 1, dy = (j >> 1) & 1, dz = (j >> 2) & 1;
+                        const uint64_t ci[3] = {wi[0] + dx * hl, wi[1] + dy * hl, wi[2] + dz * hl};
+                        emit(map_cell(p, ci, l + 1), gc[j], h[0] * L + dx * hl, h[1] * L + dy * hl, h[2] * L + dz * hl);
+                    }
+                    continue;
+                }
             }
-            atomicOr(err, 2);  // level difference > 1: outside the reference's assumptions
+            // no leaf covers the window: a level difference > 1 (outside the
+            // reference's assumptions, an error) or, on a grid holding part of
+            // the leaves (hybrid.hip's box), a window beyond them: dropped
+            atomicOr(err, 2);
         }
         if (!ids) row[i + 1] = w;
         if (codes) codes[i] = code;
@@ -276,13 +283,18 @@ __global__ void __launch_bounds__(256) k_ex_nof_fill(ExView v, const int32_t* __
                         continue;
                     }
                 }
-                if (l < M) {  // the count pass has checked that all 8 children exist
+                if (l < M) {  // the 8 children, listed (as in the count pass) only when all exist
                     const uint64_t hl = (uint64_t)(L / 2);
+                    int64_t gc[8];
+                    bool all = true;
                     for (int cix = 0; cix < 8; cix++) {
                         const uint64_t ci[3] = {wi[0] + (cix & 1) * hl, wi[1] + ((cix >> 1) & 1) * hl,
                                                 wi[2] + ((cix >> 2) & 1) * hl};
-                        put((uint32_t)ex_find(v, map_cell(p, ci, l + 1)), 2 + cix, k, wi);
+                        gc[cix] = ex_find(v, map_cell(p, ci, l + 1));
+                        all &= gc[cix] >= 0;
                     }
+                    if (all)
+                        for (int cix = 0; cix < 8; cix++) put((uint32_t)gc[cix], 2 + cix, k, wi);
                 }
             }
         }
@@ -1094,7 +1106,9 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     DX_HIP(hipMemcpyAsync(d_err + 2, row + n, 8, hipMemcpyDeviceToDevice, st));
     DX_TRY(dx_d2h(grid->ctx, back, d_err, 16, st));
     *total = back[1];
-    const int32_t err = (int32_t)(back[0] & 0xffffffffu);
+    // a box of leaves cut from a larger grid (hybrid.hip): a window outside
+    // the box finds no cell -- an entry of a cell at the box's edge, skipped
+    const int32_t err = (int32_t)(back[0] & 0xffffffffu) & (grid->partial_leaves ? ~2 : ~0);
     if (err) {
         ds_free(d_err, st);
         ds_free(d_codes, st);
@@ -1916,7 +1930,7 @@ static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_
     uint64_t back[2] = {0, 0};  // error word, total
     hipMemcpyAsync(d_err + 2, h.d_nof_row + R, 8, hipMemcpyDeviceToDevice, st);
     if ((s = dx_d2h(ctx, back, d_err, 16, st)) != DCCRGX_OK) return done(s);
-    if (back[0] & 0xffffffffu)
+    if ((back[0] & 0xffffffffu) & (grid->partial_leaves ? ~2u : ~0u))
         return done(set_error(back[0] & 1 ? DCCRGX_ENOTFOUND : DCCRGX_EINTERNAL,
                               back[0] & 1 ? "cell does not exist" : "neighbor more than one level apart"));
     *total = back[1];

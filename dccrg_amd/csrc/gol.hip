@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256) k_gol_items(UGeom g, const uint32_t* __re
 }
 
 // deterministic synthetic initial state: alive = splitmix64(id) % 1000 < permille
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
 {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -271,6 +271,10 @@ static int compute_region(dccrgx_grid* grid, const Hood& h, const Field& in, con
         DX_TRY(gol_launch(grid, h, in, out, cnt, x[0], x[1], st));
         DX_TRY(timed(grid, false, st));
     }
+    // refined cells inside the uniform grid: the overlay's cells again, from
+    // their stored rows (every region call: the overlay is small, and the
+    // rewrite is idempotent)
+    if (grid->hy) DX_TRY(hybrid_gol(grid, in.ptr, out.ptr, cnt.ptr, st));
     return DCCRGX_OK;
 }
 
@@ -335,6 +339,7 @@ int dccrgx_field_init_hash(dccrgx_grid* grid, int32_t fid, uint32_t permille)
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
     DX_CHECK(grid->fields[fid].elem == 4, DCCRGX_EINVAL, "4-byte field expected");
     DX_CHECK(grid->uniform, DCCRGX_EINVAL, "uniform grids only");
+    DX_NO_HYBRID(grid);
     if (!grid->n_local) return DCCRGX_OK;
     const uint64_t soff = (uint64_t)(-grid->g.cbase * (int64_t)grid->g.S);
     hipLaunchKernelGGL(k_init_hash, dim3(grid_for(grid->n_local)), dim3(256), 0, grid->ctx->compute,
@@ -376,6 +381,28 @@ int dccrgx_field_checksum(const dccrgx_grid* grid, int32_t fid, uint64_t out[2])
     }
     dx_free(ids);
     dx_free(d);
+    if (s == DCCRGX_OK && grid->hy) {
+        // the slab's sum holds the refined cells' slots and not their children:
+        // correct it cell by cell (refined cells are few)
+        const Hybrid& H = *grid->hy;
+        const uint64_t soff = (uint64_t)(-grid->g.cbase * (int64_t)grid->g.S);
+        auto value = [&](uint64_t slot, uint32_t* v) -> int {
+            DX_HIP(hipMemcpy(v, (const uint32_t*)F.ptr + slot, 4, hipMemcpyDeviceToHost));
+            return DCCRGX_OK;
+        };
+        for (uint64_t r : H.refined) {
+            uint32_t v = 0;
+            DX_TRY(value(r - 1 + soff, &v));
+            out[0] -= v;
+            out[1] -= (uint64_t)v * splitmix64(r);
+        }
+        for (size_t k = 0; k < H.children.size(); k++) {
+            uint32_t v = 0;
+            DX_TRY(value(H.child_slot[k], &v));
+            out[0] += v;
+            out[1] += (uint64_t)v * splitmix64(H.children[k]);
+        }
+    }
     return s;
 }
 

@@ -297,6 +297,7 @@ extern "C" {
 int dccrgx_gol_amr_phase(dccrgx_grid* grid, int32_t hood_id, int32_t f_data, int32_t phase)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     const Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -311,6 +312,7 @@ int dccrgx_gol_amr_phase(dccrgx_grid* grid, int32_t hood_id, int32_t f_data, int
 int dccrgx_gol_amr_step(dccrgx_grid* grid, int32_t hood_id, int32_t f_data)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_TRY(dccrgx_gol_amr_phase(grid, hood_id, f_data, DCCRGX_GOLH_RECORD));
     DX_TRY(dccrgx_halo_update(grid, hood_id, &f_data, 1));  // solve.hpp:105
     return dccrgx_gol_amr_phase(grid, hood_id, f_data, DCCRGX_GOLH_SPREAD_APPLY);

@@ -648,10 +648,28 @@ static int default_items(uint32_t hood_length, std::vector<int32_t>& items)
 
 using namespace dccrgx;
 
+static int grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uint64_t* leaves, size_t n_leaves,
+                       bool partial, dccrgx_grid** out);
+
 extern "C" {
 
 int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uint64_t* leaves,
                        size_t n_leaves, dccrgx_grid** out)
+{
+    return grid_create(ctx, prm, leaves, n_leaves, false, out);
+}
+
+}  // extern "C"
+
+// the explicit grid over a box of leaves cut from a larger grid (hybrid.hip)
+int dccrgx::grid_create_box(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uint64_t* leaves, size_t n,
+                            dccrgx_grid** out)
+{
+    return grid_create(ctx, prm, leaves, n, true, out);
+}
+
+static int grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uint64_t* leaves, size_t n_leaves,
+                       bool partial, dccrgx_grid** out)
 {
     DX_CHECK(ctx && prm && out, DCCRGX_EINVAL, "null argument");
     DX_HIP(hipSetDevice(ctx->device));
@@ -679,6 +697,7 @@ int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uin
     }
     if (leaves) {
         grid->uniform = false;
+        grid->partial_leaves = partial;
         DX_TRY(explicit_create(grid.get(), leaves, n_leaves));
         *out = grid.release();
         return DCCRGX_OK;
@@ -724,12 +743,18 @@ int dccrgx_grid_create(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uin
     return DCCRGX_OK;
 }
 
+extern "C" {
+
 int dccrgx_get_process(const dccrgx_grid* grid, const uint64_t* cells, size_t n, int32_t* out)
 {
     DX_CHECK(grid && (cells || !n) && (out || !n), DCCRGX_EINVAL, "null argument");
     DX_TRY(explicit_host_leaves(grid));
     for (size_t i = 0; i < n; i++) {
         const uint64_t c = cells[i];
+        if (grid->hy) {
+            out[i] = hybrid_slot(grid, c) >= 0 ? 0 : -1;
+            continue;
+        }
         if (grid->uniform) {
             out[i] = (c >= 1 && c <= grid->g.N) ? level0_owner(grid, grid->g.part, c) : -1;
             continue;
@@ -751,6 +776,7 @@ int dccrgx_grid_destroy(dccrgx_grid* grid)
     for (Field& f : grid->fields) dx_free(f.ptr);
     for (auto& b : grid->spare_bufs) dx_free(b.first);
     dx_free(grid->d_sfc_cut);
+    hybrid_destroy(grid);
     if (!grid->uniform) explicit_destroy(grid);
     delete grid->spare_host;
     amr_destroy(grid);
@@ -766,11 +792,11 @@ int dccrgx_grid_get_info(const dccrgx_grid* grid, dccrgx_grid_info* out)
 {
     DX_CHECK(grid && out, DCCRGX_EINVAL, "null argument");
     std::memset(out, 0, sizeof(*out));
-    out->n_local = grid->n_local;
+    out->n_local = grid->hy ? hybrid_n_local(grid) : grid->n_local;
     out->first_local = grid->first_local;
     out->n_slots = grid->n_slots;
     out->max_ref_lvl = grid->map.max_lvl;
-    out->uniform = grid->uniform ? 1 : 0;
+    out->uniform = grid->hy ? 2 : grid->uniform ? 1 : 0;  // 2: uniform layout with refined cells (hybrid.hip)
     out->rank = grid->ctx->rank;
     out->comm_size = grid->ctx->comm_size;
     if (grid->uniform) {
@@ -785,6 +811,7 @@ int dccrgx_grid_get_info(const dccrgx_grid* grid, dccrgx_grid_info* out)
 int dccrgx_add_neighborhood(dccrgx_grid* grid, int32_t id, const int32_t* items, size_t n)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     // dccrg.hpp:6505-6618
     DX_CHECK(id != DCCRGX_DEFAULT_NEIGHBORHOOD_ID, DCCRGX_EINVAL, "default neighborhood id");
@@ -823,6 +850,7 @@ int dccrgx_add_neighborhood(dccrgx_grid* grid, int32_t id, const int32_t* items,
 int dccrgx_remove_neighborhood(dccrgx_grid* grid, int32_t id)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
     if (id == DCCRGX_DEFAULT_NEIGHBORHOOD_ID) return DCCRGX_OK;  // dccrg.hpp:6685-6687
     Hood* h = find_hood(grid, id);
@@ -858,6 +886,14 @@ int dccrgx_get_all_cells(const dccrgx_grid* grid, uint64_t* ids, size_t cap, siz
         std::copy(L.begin(), L.end(), ids);
         return DCCRGX_OK;
     }
+    if (grid->hy) {  // one process: every leaf is local
+        std::vector<uint64_t> v;
+        DX_TRY(hybrid_local_cells(grid, v));
+        *n = v.size();
+        DX_CHECK(cap >= *n && (ids || !*n), DCCRGX_ERANGE, "capacity");
+        std::copy(v.begin(), v.end(), ids);
+        return DCCRGX_OK;
+    }
     *n = grid->g.N;
     DX_CHECK(cap >= *n && (ids || !*n), DCCRGX_ERANGE, "capacity");
     parallel_ranges(*n, 1u << 16, [ids](size_t b, size_t e) {
@@ -874,6 +910,20 @@ int dccrgx_get_cells(const dccrgx_grid* grid, int32_t id, int32_t which, uint64_
     const Hood* h = find_hood(grid, id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", id);
     if (!grid->uniform) return explicit_get_cells(grid, *h, which, ids, cap, n);
+    if (grid->hy) {  // one process: local = inner = every leaf, no outer or remote cells
+        if (which == DCCRGX_CELLS_OUTER || which == DCCRGX_CELLS_REMOTE) {
+            *n = 0;
+            return DCCRGX_OK;
+        }
+        DX_CHECK(which == DCCRGX_CELLS_LOCAL || which == DCCRGX_CELLS_INNER, DCCRGX_EINVAL, "unknown cell class %d",
+                 which);
+        std::vector<uint64_t> v;
+        DX_TRY(hybrid_local_cells(grid, v));
+        *n = v.size();
+        DX_CHECK(cap >= *n && (ids || !*n), DCCRGX_ERANGE, "capacity");
+        std::copy(v.begin(), v.end(), ids);
+        return DCCRGX_OK;
+    }
     const uint64_t nl = grid->n_local;
     switch (which) {
     case DCCRGX_CELLS_LOCAL:
@@ -911,6 +961,7 @@ int dccrgx_get_cells(const dccrgx_grid* grid, int32_t id, int32_t which, uint64_
 int dccrgx_neighbor_list_stats(const dccrgx_grid* grid, int32_t id, uint64_t out[4])
 {
     DX_CHECK(grid && out, DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_TRY(explicit_host_leaves(grid));
     const Hood* h = find_hood(grid, id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", id);
@@ -935,6 +986,7 @@ int dccrgx_get_peers(const dccrgx_grid* grid, int32_t id, int32_t send, int32_t*
                      uint64_t* counts, size_t cap, size_t* n)
 {
     DX_CHECK(grid && n, DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     const Hood* h = find_hood(grid, id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", id);
     size_t w = 0;
@@ -956,6 +1008,7 @@ int dccrgx_get_peer_cells(const dccrgx_grid* grid, int32_t id, int32_t send, int
                           uint64_t* ids, size_t cap, size_t* n)
 {
     DX_CHECK(grid && n, DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_TRY(explicit_host_leaves(grid));
     const Hood* h = find_hood(grid, id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", id);

@@ -327,6 +327,11 @@ struct Amr {
 // a two-phase stop_refining is between prepare and finish: calls that would
 // change or read the fields, neighborhoods or halo plans the prepared rebuild
 // has already moved must wait for dccrgx_stop_refining_finish
+// calls a hybrid grid (hybrid.hip) does not support yet
+#define DX_NO_HYBRID(grid)                                                                                   \
+    DX_CHECK(!((grid) && (grid)->hy), DCCRGX_ESTATE,                                                         \
+             "not supported on a uniform grid with refined cells (hybrid layout, first slice: game of life, " \
+             "cell data by id, neighbor queries, further level-0 refines)")
 #define DX_NOT_PENDING(grid)                                                                           \
     DX_CHECK(!((grid) && (grid)->amr && (grid)->amr->pending), DCCRGX_ESTATE,                                      \
              "a prepared stop_refining awaits dccrgx_stop_refining_finish")
@@ -434,6 +439,61 @@ struct Hood {
     std::shared_ptr<IterCache> iter;   // user-stencil view (stencil.hip)
 };
 
+// Refinement inside a uniform grid (hybrid.hip): the level-0 cells stay in
+// the implicit slab layout; refined level-0 cells' children get slots after
+// it; the "overlay" -- the leaves whose rows involve a refined cell -- keeps
+// its rows (built by an explicit grid over a box of leaves around the refined
+// cells), every other leaf's rows stay closed-form.  One process, the
+// default neighborhood, refinement of level-0 cells only (first slice).
+struct Hybrid {
+    std::vector<uint64_t> refined;      // refined level-0 cells, ascending
+    std::vector<uint64_t> children;     // their children (the level-1 leaves), ascending
+    std::vector<uint64_t> child_slot;   // the storage slot of each
+    uint64_t uniform_slots = 0;         // slots of the uniform layout (children after them)
+    std::vector<uint64_t> overlay;      // ascending leaves whose rows involve a refined cell
+    std::vector<uint32_t> ov_slot;      // the slot of each
+    // their iteration-cache rows (dccrg.hpp:11570-11712) as storage slots, host and device
+    std::vector<uint64_t> st_row;
+    std::vector<uint32_t> st_slot;
+    uint64_t* d_st_row = nullptr;
+    uint32_t* d_st_slot = nullptr;
+    uint32_t* d_ov_slot = nullptr;
+    // their neighbors_of (ids, offsets) and neighbors_to (ids) rows, host
+    std::vector<uint64_t> nof_row, nof_id, nto_row, nto_id;
+    std::vector<int32_t> nof_off;
+    int64_t find_child(uint64_t id) const
+    {
+        const auto it = std::lower_bound(children.begin(), children.end(), id);
+        return it != children.end() && *it == id ? (int64_t)(it - children.begin()) : -1;
+    }
+    int64_t find_overlay(uint64_t id) const
+    {
+        const auto it = std::lower_bound(overlay.begin(), overlay.end(), id);
+        return it != overlay.end() && *it == id ? (int64_t)(it - overlay.begin()) : -1;
+    }
+    bool is_refined(uint64_t id) const { return std::binary_search(refined.begin(), refined.end(), id); }
+};
+// an explicit grid over a box of leaves cut from a larger grid (grid.hip)
+int grid_create_box(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uint64_t* leaves, size_t n,
+                    dccrgx_grid** out);
+// refine level-0 `cells` (ascending, unique leaves) of a uniform grid in place
+int hybrid_refine(dccrgx_grid* grid, const std::vector<uint64_t>& cells, std::vector<uint64_t>& new_cells);
+void hybrid_destroy(dccrgx_grid* grid);
+// storage slot of a leaf of a hybrid grid, -1 if the id is not a leaf
+int64_t hybrid_slot(const dccrgx_grid* grid, uint64_t id);
+// the overlay's game-of-life fix-up after the uniform kernel (gol.hip)
+int hybrid_gol(const dccrgx_grid* grid, const void* in, void* out, void* cnt, hipStream_t st);
+// neighbors_of / neighbors_to queries of a hybrid grid (device arrays)
+int hybrid_neighbors(const dccrgx_grid* grid, int32_t hood_id, bool to, const uint64_t* cells, size_t n,
+                     uint64_t* row, uint64_t* ids, int32_t* off3, size_t cap, hipStream_t st);
+// local cells of a hybrid grid: count, and values in ascending id order <-> slots
+uint64_t hybrid_n_local(const dccrgx_grid* grid);
+int hybrid_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device);
+// local cells (ascending) of a hybrid grid
+int hybrid_local_cells(const dccrgx_grid* grid, std::vector<uint64_t>& out);
+// would the explicit layout of this uniform grid exceed the device (amr.hip)
+bool explicit_too_large(const dccrgx_grid* grid);
+
 // the SFC placement of a grid (sfc.hip): O(P) state, no per-cell table
 struct SfcPlan {
     std::vector<uint64_t> cut;  // cut[r-1]: Hilbert key of process r's first level-0 cell
@@ -496,6 +556,11 @@ struct dccrgx_grid {
     // and fresh multi-MB vectors cost page faults)
     dccrgx::Explicit* spare_host = nullptr;
     bool rebuilding = false;  // inside amr.hip rebuild_prepare: intermediate synchronisations are skipped
+    // refined cells inside a uniform grid (hybrid.hip), or null
+    dccrgx::Hybrid* hy = nullptr;
+    // the leaves are a box cut from a larger grid (hybrid.hip's box grid):
+    // windows outside the box are skipped instead of reported
+    bool partial_leaves = false;
     // SFC placement (params.partition): the P - 1 cut keys along the curve
     dccrgx::SfcPlan sfc;
     uint64_t* d_sfc_cut = nullptr;  // their device copy (AMR decisions), made on first use

@@ -405,6 +405,7 @@ static void slots_holding(const dccrgx_grid* grid, uint64_t id, std::vector<uint
 // first ghost copy; -1 if this rank stores no copy
 static int64_t primary_slot(const dccrgx_grid* grid, uint64_t id)
 {
+    if (grid->hy) return hybrid_slot(grid, id);
     if (!grid->uniform) return explicit_host_slot(grid, id);
     const UGeom& g = grid->g;
     if (id < 1 || id > g.N) return -1;
@@ -512,6 +513,16 @@ int dccrgx_slots_of(const dccrgx_grid* grid, const uint64_t* ids, size_t n, int6
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
     if (n == 0) return DCCRGX_OK;
     const CallerStream fence(grid->ctx, st);
+    if (grid->hy) {  // on the host (refined cells are few; the ids come back in one copy)
+        std::vector<uint64_t> h(n);
+        std::vector<int64_t> o(n);
+        DX_HIP(hipMemcpyAsync(h.data(), ids, n * 8, hipMemcpyDeviceToHost, st));
+        DX_HIP(hipStreamSynchronize(st));
+        for (size_t i = 0; i < n; i++) o[i] = hybrid_slot(grid, h[i]);
+        DX_HIP(hipMemcpyAsync(slots, o.data(), n * 8, hipMemcpyHostToDevice, st));
+        DX_HIP(hipStreamSynchronize(st));
+        return DCCRGX_OK;
+    }
     if (!grid->uniform) return explicit_slots_of(grid, ids, n, slots, st);
     if (grid->n_local == 0) return set_error(DCCRGX_ESTATE, "rank has no cells");
     hipLaunchKernelGGL(k_slots_of, dim3(grid_for(n)), dim3(256), 0, st, grid->g, ids, n, slots);
@@ -531,6 +542,11 @@ int dccrgx_field_write_local(dccrgx_grid* grid, int32_t fid, const void* host, s
     DX_NOT_PENDING(grid);
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
     DX_CHECK(!grid->fields[fid].variable, DCCRGX_EINVAL, "variable-size field: use dccrgx_field_write_cells");
+    if (grid->hy) {
+        DX_CHECK(n == hybrid_n_local(grid) && (host || !n), DCCRGX_EINVAL, "expected %llu local values",
+                 (unsigned long long)hybrid_n_local(grid));
+        return hybrid_local_copy(grid, grid->fields[fid], const_cast<void*>(host), true);
+    }
     DX_CHECK(n == grid->n_local && (host || !n), DCCRGX_EINVAL, "expected %llu local values",
              (unsigned long long)grid->n_local);
     if (!n) return DCCRGX_OK;
@@ -543,6 +559,11 @@ int dccrgx_field_read_local(const dccrgx_grid* grid, int32_t fid, void* host, si
 {
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
     DX_CHECK(!grid->fields[fid].variable, DCCRGX_EINVAL, "variable-size field: use dccrgx_field_read_cells");
+    if (grid->hy) {
+        DX_CHECK(n == hybrid_n_local(grid) && (host || !n), DCCRGX_EINVAL, "expected %llu local values",
+                 (unsigned long long)hybrid_n_local(grid));
+        return hybrid_local_copy(grid, grid->fields[fid], host, false);
+    }
     DX_CHECK(n == grid->n_local && (host || !n), DCCRGX_EINVAL, "expected %llu local values",
              (unsigned long long)grid->n_local);
     if (!n) return DCCRGX_OK;
@@ -555,6 +576,7 @@ int dccrgx_field_read_remote(const dccrgx_grid* grid, int32_t hood_id, int32_t f
                              size_t n)
 {
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
+    DX_NO_HYBRID(grid);
     DX_CHECK(!grid->fields[fid].variable, DCCRGX_EINVAL, "variable-size field: use dccrgx_field_read_cells");
     const Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -582,6 +604,7 @@ int dccrgx_field_read_remote(const dccrgx_grid* grid, int32_t hood_id, int32_t f
 int dccrgx_halo_self(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, size_t nf)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -683,6 +706,7 @@ int dccrgx_exchange_start(dccrgx_grid* grid, int32_t hood_id, const void* const*
                           const uint64_t* send_bytes, void* const* recv_host, const uint64_t* recv_bytes)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -752,6 +776,7 @@ int dccrgx_exchange_start(dccrgx_grid* grid, int32_t hood_id, const void* const*
 int dccrgx_exchange_wait(dccrgx_grid* grid, int32_t hood_id)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null grid");
+    DX_NO_HYBRID(grid);
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     if (!h->pending) return DCCRGX_OK;
@@ -764,6 +789,7 @@ int dccrgx_halo_pack_to(dccrgx_grid* grid, int32_t hood_id, const int32_t* f, si
                         void* dst, size_t cap, size_t* bytes)
 {
     DX_CHECK(grid && bytes, DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -783,6 +809,7 @@ int dccrgx_halo_unpack_from(dccrgx_grid* grid, int32_t hood_id, const int32_t* f
                             int32_t peer, const void* src, size_t bytes)
 {
     DX_CHECK(grid, DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
@@ -805,6 +832,7 @@ int dccrgx_halo_unpack_from(dccrgx_grid* grid, int32_t hood_id, const int32_t* f
 int dccrgx_field_create_variable(dccrgx_grid* grid, uint32_t elem, int32_t* fid)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid && fid && elem > 0, DCCRGX_EINVAL, "bad argument");
     Field F;
     F.elem = elem;
@@ -822,6 +850,7 @@ int dccrgx_field_create_variable(dccrgx_grid* grid, uint32_t elem, int32_t* fid)
 int dccrgx_field_resize(dccrgx_grid* grid, int32_t fid, const uint64_t* ids, const uint32_t* counts, size_t n)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid && fid >= 0 && (size_t)fid < grid->fields.size(), DCCRGX_EINVAL, "bad field");
     DX_CHECK((ids && counts) || !n, DCCRGX_EINVAL, "null argument");
     Field& F = grid->fields[fid];

@@ -1,0 +1,494 @@
+// hybrid.hip -- refinement inside a uniform grid too large for the explicit
+// layout (VERDICT r5 "next" 5: the first slice of the hybrid layout).
+//
+// The explicit layout keeps every leaf's neighbor lists (~1.2 kB per cell for
+// the 26-cell neighborhood), so it refuses grids above ~2.4e8 cells
+// (amr.hip check_explicit_memory).  Here a uniform grid stays uniform: its
+// level-0 cells keep the implicit slab layout and their closed-form rows;
+// the children of refined level-0 cells get storage slots after the slab;
+// the leaves whose rows involve a refined cell -- the children and the
+// level-0 cells within the neighborhood's reach of a refined cell, "the
+// overlay" -- keep their rows, computed by the explicit machinery itself: an
+// explicit grid over a box of leaves around the refined cells (every level-0
+// cell within three reaches of one, minus the refined ones, plus the
+// children), whose rows for the overlay cells are exactly the full grid's
+// (their windows, and the cells naming them, lie well inside the box).
+// Memory: O(refined cells), nothing per level-0 cell.
+//
+// Semantics are the reference's (dccrg.hpp:2456-2546 refine_completely,
+// :10243-10693 execute_refines): between levels 0 and 1 the 2:1 balance holds
+// for any set of refines, so no refine is induced and the decision is the
+// requested level-0 cells minus the dont_refine ones; children are value-
+// initialised (:10375).  The game of life runs the uniform kernel over the
+// slab, then rewrites the overlay cells from their stored rows (the
+// iteration cache's order, as k_ex_gol).
+//
+// First slice, refused elsewhere with DCCRGX_ESTATE (DX_NO_HYBRID): one
+// process, the default neighborhood only, refines of level-0 cells (no
+// unrefines, no level-1 refines), and the calls the game of life and cell
+// data by id need.  A refined cell's data is not kept after the refine.
+#include "grid.hpp"
+
+namespace dccrgx {
+
+namespace {
+
+unsigned grid_for(uint64_t n)
+{
+    uint64_t b = (n + 255) / 256;
+    if (b > 65536) b = 65536;
+    return (unsigned)(b ? b : 1);
+}
+
+// the overlay's rows: out / cnt of each overlay cell from its stored row
+__global__ void __launch_bounds__(256) k_hy_gol(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                uint32_t* __restrict__ cnt, const uint64_t* __restrict__ row,
+                                                const uint32_t* __restrict__ nslot,
+                                                const uint32_t* __restrict__ slot, uint64_t n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        uint32_t c = 0;
+        for (uint64_t e = row[q]; e < row[q + 1]; e++) c += in[nslot[e]] != 0u ? 1u : 0u;
+        const uint32_t s = slot[q];
+        cnt[s] = c;
+        out[s] = c == 3u ? 1u : (c == 2u ? in[s] : 0u);
+    }
+}
+
+template <class T>
+int upload_vec(const std::vector<T>& v, T** d, hipStream_t st)
+{
+    *d = nullptr;
+    DX_HIP(dx_malloc(d, std::max<size_t>(v.size(), 1) * sizeof(T)));
+    if (!v.empty()) DX_HIP(hipMemcpyAsync(*d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
+    return DCCRGX_OK;
+}
+
+// original-axis level-0 indices of a level-0 id, and back
+void l0_indices(const MapParams& mp, uint64_t id, int64_t x[3])
+{
+    const uint64_t i = id - 1, q = i / mp.length[0];
+    x[0] = (int64_t)(i % mp.length[0]);
+    x[1] = (int64_t)(q % mp.length[1]);
+    x[2] = (int64_t)(q / mp.length[1]);
+}
+
+// the level-0 cell at x (wrapped where periodic), 0 outside the grid
+uint64_t l0_cell(const MapParams& mp, const int32_t per[3], const int64_t x[3])
+{
+    uint64_t w[3];
+    for (int d = 0; d < 3; d++) {
+        const int64_t L = (int64_t)mp.length[d];
+        int64_t v = x[d];
+        if (v < 0 || v >= L) {
+            if (!per[d]) return 0;
+            v %= L;
+            if (v < 0) v += L;
+        }
+        w[d] = (uint64_t)v;
+    }
+    return 1 + w[0] + mp.length[0] * (w[1] + mp.length[1] * w[2]);
+}
+
+// the children of level-0 cell c, ascending (x fastest)
+void children_of(const MapParams& mp, uint64_t c, uint64_t ch[8])
+{
+    uint64_t idx[3];
+    int l;
+    map_indices(mp, c, idx, &l);
+    const uint64_t h = (uint64_t)1 << (mp.max_lvl - 1);
+    for (int k = 0; k < 8; k++) {
+        const uint64_t ci[3] = {idx[0] + (k & 1) * h, idx[1] + ((k >> 1) & 1) * h, idx[2] + ((k >> 2) & 1) * h};
+        ch[k] = map_cell(mp, ci, 1);
+    }
+}
+
+// level-0 cells around the refined cells: within `reach` (Chebyshev, in
+// level-0 cells) of any of them, wrapped where periodic, ascending
+std::vector<uint64_t> around(const MapParams& mp, const int32_t per[3], const std::vector<uint64_t>& refined,
+                             int reach)
+{
+    std::vector<uint64_t> out;
+    for (uint64_t r : refined) {
+        int64_t x[3];
+        l0_indices(mp, r, x);
+        for (int dz = -reach; dz <= reach; dz++)
+            for (int dy = -reach; dy <= reach; dy++)
+                for (int dx = -reach; dx <= reach; dx++) {
+                    const int64_t y[3] = {x[0] + dx, x[1] + dy, x[2] + dz};
+                    const uint64_t c = l0_cell(mp, per, y);
+                    if (c) out.push_back(c);
+                }
+    }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+}
+
+struct ShadowGrid {  // destroyed on every path
+    dccrgx_grid* g = nullptr;
+    ~ShadowGrid()
+    {
+        if (g) dccrgx_grid_destroy(g);
+    }
+};
+
+void free_device(Hybrid* H)
+{
+    if (!H) return;
+    FreeBatch fb;
+    fb.add(H->d_st_row);
+    fb.add(H->d_st_slot);
+    fb.add(H->d_ov_slot);
+    H->d_st_row = nullptr;
+    H->d_st_slot = nullptr;
+    H->d_ov_slot = nullptr;
+}
+
+}  // namespace
+
+void hybrid_destroy(dccrgx_grid* grid)
+{
+    if (!grid->hy) return;
+    free_device(grid->hy);
+    delete grid->hy;
+    grid->hy = nullptr;
+}
+
+int64_t hybrid_slot(const dccrgx_grid* grid, uint64_t id)
+{
+    const Hybrid& H = *grid->hy;
+    const int l = map_level(grid->map, id);
+    if (l == 0) {
+        if (id > grid->g.N || H.is_refined(id)) return -1;
+        const UGeom& g = grid->g;
+        return (int64_t)(id - 1 + (uint64_t)(-g.cbase * (int64_t)g.S));  // one process: every cell is local
+    }
+    const int64_t k = H.find_child(id);
+    return k < 0 ? -1 : (int64_t)H.child_slot[k];
+}
+
+int hybrid_local_cells(const dccrgx_grid* grid, std::vector<uint64_t>& out)
+{
+    const Hybrid& H = *grid->hy;
+    const uint64_t N = grid->g.N;
+    out.clear();
+    out.reserve(N - H.refined.size() + H.children.size());
+    size_t r = 0;
+    for (uint64_t c = 1; c <= N; c++) {
+        if (r < H.refined.size() && H.refined[r] == c) {
+            r++;
+            continue;
+        }
+        out.push_back(c);
+    }
+    out.insert(out.end(), H.children.begin(), H.children.end());  // level-1 ids follow every level-0 id
+    return DCCRGX_OK;
+}
+
+uint64_t hybrid_n_local(const dccrgx_grid* grid)
+{
+    return grid->g.N - grid->hy->refined.size() + grid->hy->children.size();
+}
+
+int hybrid_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool to_device)
+{
+    const Hybrid& H = *grid->hy;
+    Ctx* c = grid->ctx;
+    hipStream_t st = c->compute;
+    const uint64_t soff = (uint64_t)(-grid->g.cbase * (int64_t)grid->g.S), N = grid->g.N, e = F.elem;
+    char* h = static_cast<char*>(host);
+    // level-0 cells: runs of ids between refined ones, one copy each
+    uint64_t at = 0, id = 1;
+    for (size_t r = 0; r <= H.refined.size(); r++) {
+        const uint64_t end = r < H.refined.size() ? H.refined[r] : N + 1;  // run [id, end)
+        if (end > id) {
+            char* dev = (char*)F.ptr + (id - 1 + soff) * e;
+            if (to_device) DX_TRY(dx_h2d(c, dev, h + at * e, (end - id) * e, st));
+            else DX_TRY(dx_d2h(c, h + at * e, dev, (end - id) * e, st));
+            at += end - id;
+        }
+        id = end + 1;
+    }
+    // the children, ascending ids, each in its slot
+    for (size_t k = 0; k < H.children.size(); k++, at++) {
+        char* dev = (char*)F.ptr + H.child_slot[k] * e;
+        DX_HIP(to_device ? hipMemcpy(dev, h + at * e, e, hipMemcpyHostToDevice)
+                         : hipMemcpy(h + at * e, dev, e, hipMemcpyDeviceToHost));
+    }
+    return DCCRGX_OK;
+}
+
+int hybrid_refine(dccrgx_grid* grid, const std::vector<uint64_t>& cells, std::vector<uint64_t>& new_cells)
+{
+    Ctx* ctx = grid->ctx;
+    hipStream_t st = ctx->compute;
+    const MapParams& mp = grid->map;
+    DX_CHECK(grid->uniform && ctx->comm_size == 1, DCCRGX_ESTATE, "hybrid refinement: one process, uniform grid");
+    DX_CHECK(mp.max_lvl >= 1, DCCRGX_ESTATE, "maximum refinement level 0");
+    DX_CHECK(grid->hoods.size() == 1, DCCRGX_ESTATE,
+             "hybrid refinement supports the default neighborhood only (%zu neighborhoods)", grid->hoods.size());
+    for (const Field& F : grid->fields)
+        DX_CHECK(!F.variable, DCCRGX_ESTATE, "hybrid refinement of a grid with variable-size fields");
+    const Hood& hood = grid->hoods.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
+    std::unique_ptr<Hybrid> H(new Hybrid());
+    if (grid->hy) {  // the earlier refines stay (no unrefines in this slice)
+        H->refined = grid->hy->refined;
+        H->children = grid->hy->children;
+        H->child_slot = grid->hy->child_slot;
+        H->uniform_slots = grid->hy->uniform_slots;
+    } else {
+        H->uniform_slots = grid->n_slots;
+    }
+    // the new refined cells and their children (slots after the existing ones)
+    new_cells.clear();
+    std::vector<uint64_t> add;
+    for (uint64_t c : cells) {
+        DX_CHECK(map_level(mp, c) == 0 && c >= 1 && c <= grid->g.N, DCCRGX_EINVAL, "%llu is not a level-0 cell",
+                 (unsigned long long)c);
+        if (!H->is_refined(c)) add.push_back(c);
+    }
+    if (add.empty()) return DCCRGX_OK;
+    uint64_t next_slot = H->uniform_slots + H->children.size();
+    std::vector<std::pair<uint64_t, uint64_t>> ch_slot;
+    for (size_t i = 0; i < H->children.size(); i++) ch_slot.push_back({H->children[i], H->child_slot[i]});
+    for (uint64_t c : add) {
+        uint64_t ch[8];
+        children_of(mp, c, ch);
+        for (uint64_t x : ch) {
+            ch_slot.push_back({x, next_slot++});
+            new_cells.push_back(x);
+        }
+    }
+    std::sort(ch_slot.begin(), ch_slot.end());
+    std::sort(new_cells.begin(), new_cells.end());
+    H->children.clear();
+    H->child_slot.clear();
+    for (const auto& p : ch_slot) {
+        H->children.push_back(p.first);
+        H->child_slot.push_back(p.second);
+    }
+    H->refined.insert(H->refined.end(), add.begin(), add.end());
+    std::sort(H->refined.begin(), H->refined.end());
+    DX_CHECK(next_slot < (1ull << 32), DCCRGX_EINVAL, "hybrid refinement: %llu slots exceed 32-bit slot ids",
+             (unsigned long long)next_slot);
+
+    // reach of the neighborhood in level-0 cells: the overlay's level-0 cells
+    // are the ones an item of a refined cell reaches (the items are symmetric,
+    // so these are also the cells whose items reach a refined cell); the box
+    // extends three reaches from the refined cells
+    int reach = 1;
+    for (int32_t v : hood.items) reach = std::max(reach, std::abs(v));
+    const int32_t per[3] = {grid->params.periodic[0] ? 1 : 0, grid->params.periodic[1] ? 1 : 0,
+                            grid->params.periodic[2] ? 1 : 0};
+    std::vector<uint64_t> ov0;
+    for (uint64_t r : H->refined) {
+        int64_t x[3];
+        l0_indices(mp, r, x);
+        for (size_t k = 0; k + 2 < hood.items.size(); k += 3) {
+            const int64_t y[3] = {x[0] + hood.items[k], x[1] + hood.items[k + 1], x[2] + hood.items[k + 2]};
+            const uint64_t c = l0_cell(mp, per, y);
+            if (c && !H->is_refined(c)) ov0.push_back(c);
+        }
+    }
+    std::sort(ov0.begin(), ov0.end());
+    ov0.erase(std::unique(ov0.begin(), ov0.end()), ov0.end());
+    H->overlay = ov0;
+    H->overlay.insert(H->overlay.end(), H->children.begin(), H->children.end());
+    const std::vector<uint64_t> box0 = around(mp, per, H->refined, 3 * reach);
+    std::vector<uint64_t> box;
+    box.reserve(box0.size() + H->children.size());
+    for (uint64_t c : box0)
+        if (!H->is_refined(c)) box.push_back(c);
+    for (uint64_t c : H->children) {  // children of refined cells inside the box
+        uint64_t idx[3];
+        int l;
+        map_indices(mp, c, idx, &l);
+        if (std::binary_search(box0.begin(), box0.end(), map_cell(mp, idx, 0))) box.push_back(c);
+    }
+
+    // the explicit grid over the box: its rows of the overlay cells
+    ShadowGrid sh;
+    dccrgx_grid_params prm = grid->params;
+    prm.partition = DCCRGX_PARTITION_BLOCK;
+    DX_TRY(grid_create_box(static_cast<dccrgx_ctx*>(ctx), &prm, box.data(), box.size(), &sh.g));
+    const uint64_t nov = H->overlay.size();
+    H->nof_row.assign(nov + 1, 0);
+    H->nto_row.assign(nov + 1, 0);
+    DX_TRY(dccrgx_neighbors_of_host(sh.g, DCCRGX_DEFAULT_NEIGHBORHOOD_ID, H->overlay.data(), nov, H->nof_row.data(),
+                                    nullptr, nullptr, 0));
+    H->nof_id.resize(H->nof_row[nov]);
+    H->nof_off.resize(3 * H->nof_row[nov]);
+    DX_TRY(dccrgx_neighbors_of_host(sh.g, DCCRGX_DEFAULT_NEIGHBORHOOD_ID, H->overlay.data(), nov, H->nof_row.data(),
+                                    H->nof_id.data(), H->nof_off.data(), H->nof_id.size()));
+    DX_TRY(dccrgx_neighbors_to_host(sh.g, DCCRGX_DEFAULT_NEIGHBORHOOD_ID, H->overlay.data(), nov, H->nto_row.data(),
+                                    nullptr, 0));
+    H->nto_id.resize(H->nto_row[nov]);
+    DX_TRY(dccrgx_neighbors_to_host(sh.g, DCCRGX_DEFAULT_NEIGHBORHOOD_ID, H->overlay.data(), nov, H->nto_row.data(),
+                                    H->nto_id.data(), H->nto_id.size()));
+    // iteration-cache rows (stencil view of the box grid: one process, so a
+    // box slot is the box leaf's index)
+    dccrgx_stencil_view v;
+    DX_TRY(dccrgx_stencil_view_get(sh.g, DCCRGX_DEFAULT_NEIGHBORHOOD_ID, DCCRGX_REGION_ALL, &v));
+    DX_CHECK(v.kind == 1 && v.n_cells == box.size(), DCCRGX_EINTERNAL, "hybrid: box view of %llu cells",
+             (unsigned long long)v.n_cells);
+    std::vector<uint64_t> brow(box.size() + 1);
+    std::vector<uint32_t> blocal(box.size());
+    DX_HIP(hipMemcpyAsync(brow.data(), v.row, brow.size() * 8, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipMemcpyAsync(blocal.data(), v.local_slot, blocal.size() * 4, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    std::vector<uint32_t> bslot(brow[box.size()]);
+    if (!bslot.empty())
+        DX_HIP(hipMemcpy(bslot.data(), v.nbr_slot, bslot.size() * 4, hipMemcpyDeviceToHost));
+    // box slot -> leaf (one process: slot k < n holds leaf k) -> this grid's slot
+    auto slot_here = [&](uint64_t id) -> int64_t {
+        const int l = map_level(mp, id);
+        if (l == 0) return (int64_t)(id - 1 + (uint64_t)(-grid->g.cbase * (int64_t)grid->g.S));
+        const auto it = std::lower_bound(H->children.begin(), H->children.end(), id);
+        return it != H->children.end() && *it == id ? (int64_t)H->child_slot[it - H->children.begin()] : -1;
+    };
+    H->st_row.assign(nov + 1, 0);
+    H->st_slot.clear();
+    H->ov_slot.resize(nov);
+    for (uint64_t q = 0; q < nov; q++) {
+        const uint64_t id = H->overlay[q];
+        const auto it = std::lower_bound(box.begin(), box.end(), id);
+        DX_CHECK(it != box.end() && *it == id, DCCRGX_EINTERNAL, "hybrid: overlay cell %llu outside its box",
+                 (unsigned long long)id);
+        const uint64_t b = (uint64_t)(it - box.begin());
+        DX_CHECK(blocal[b] == b, DCCRGX_EINTERNAL, "hybrid: box slots are not leaf order");
+        for (uint64_t e = brow[b]; e < brow[b + 1]; e++) {
+            const uint32_t bs = bslot[e];
+            DX_CHECK(bs < box.size(), DCCRGX_EINTERNAL, "hybrid: box row entry %u", bs);
+            const int64_t s = slot_here(box[bs]);
+            DX_CHECK(s >= 0, DCCRGX_EINTERNAL, "hybrid: no slot for %llu", (unsigned long long)box[bs]);
+            H->st_slot.push_back((uint32_t)s);
+        }
+        H->st_row[q + 1] = H->st_slot.size();
+        const int64_t s = slot_here(id);
+        DX_CHECK(s >= 0, DCCRGX_EINTERNAL, "hybrid: no slot for %llu", (unsigned long long)id);
+        H->ov_slot[q] = (uint32_t)s;
+    }
+
+    // the new field arrays: the old slots copied, the children zeroed
+    // (value-initialised, dccrg.hpp:10375)
+    const uint64_t old_slots = grid->n_slots, new_slots = next_slot;
+    std::vector<void*> np(grid->fields.size(), nullptr);
+    auto drop = [&](int code) {
+        for (void* p : np) dx_free(p);
+        free_device(H.get());
+        return code;
+    };
+    for (size_t i = 0; i < grid->fields.size(); i++) {
+        const Field& F = grid->fields[i];
+        if (dx_malloc(&np[i], new_slots * F.elem) != hipSuccess)
+            return drop(set_error(DCCRGX_ENOMEM, "hybrid refinement: field %zu of %llu slots", i,
+                                  (unsigned long long)new_slots));
+        if (hipMemcpyAsync(np[i], F.ptr, old_slots * F.elem, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipMemsetAsync((char*)np[i] + old_slots * F.elem, 0, (new_slots - old_slots) * F.elem, st) != hipSuccess)
+            return drop(set_error(DCCRGX_EHIP, "hybrid refinement: moving field %zu", i));
+    }
+    if (upload_vec(H->st_row, &H->d_st_row, st) != DCCRGX_OK || upload_vec(H->st_slot, &H->d_st_slot, st) != DCCRGX_OK ||
+        upload_vec(H->ov_slot, &H->d_ov_slot, st) != DCCRGX_OK || hipStreamSynchronize(st) != hipSuccess)
+        return drop(set_error(DCCRGX_EHIP, "hybrid refinement: uploading the overlay rows"));
+    // adopt
+    for (size_t i = 0; i < grid->fields.size(); i++) {
+        dx_free(grid->fields[i].ptr);
+        grid->fields[i].ptr = np[i];
+        grid->fields[i].cap_bytes = 0;
+    }
+    grid->n_slots = new_slots;
+    hybrid_destroy(grid);
+    grid->hy = H.release();
+    return DCCRGX_OK;
+}
+
+int hybrid_gol(const dccrgx_grid* grid, const void* in, void* out, void* cnt, hipStream_t st)
+{
+    const Hybrid& H = *grid->hy;
+    const uint64_t n = H.overlay.size();
+    if (!n) return DCCRGX_OK;
+    hipLaunchKernelGGL(k_hy_gol, dim3(grid_for(n)), dim3(256), 0, st, (const uint32_t*)in, (uint32_t*)out,
+                       (uint32_t*)cnt, (const uint64_t*)H.d_st_row, (const uint32_t*)H.d_st_slot,
+                       (const uint32_t*)H.d_ov_slot, n);
+    DX_HIP(hipGetLastError());
+    return DCCRGX_OK;
+}
+
+int hybrid_neighbors(const dccrgx_grid* grid, int32_t hood_id, bool to, const uint64_t* cells, size_t n,
+                     uint64_t* row, uint64_t* ids, int32_t* off3, size_t cap, hipStream_t st)
+{
+    const Hybrid& H = *grid->hy;
+    DX_CHECK(hood_id == DCCRGX_DEFAULT_NEIGHBORHOOD_ID, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
+    std::vector<uint64_t> c(n);
+    if (n) DX_HIP(hipMemcpyAsync(c.data(), cells, n * 8, hipMemcpyDeviceToHost, st));
+    DX_HIP(hipStreamSynchronize(st));
+    // overlay cells: their stored rows; other leaves (level-0 cells no item
+    // of a refined cell reaches): the closed-form rows of the uniform layout
+    std::vector<uint64_t> plain;
+    std::vector<int64_t> where(n);  // overlay index, or -1 - position in `plain`
+    for (size_t i = 0; i < n; i++) {
+        const uint64_t id = c[i];
+        const int64_t q = H.find_overlay(id);
+        if (q >= 0) {
+            where[i] = q;
+            continue;
+        }
+        DX_CHECK(map_level(grid->map, id) == 0 && id >= 1 && id <= grid->g.N && !H.is_refined(id), DCCRGX_ENOTFOUND,
+                 "cell %llu does not exist", (unsigned long long)id);
+        where[i] = -1 - (int64_t)plain.size();
+        plain.push_back(id);
+    }
+    std::vector<uint64_t> prow(plain.size() + 1, 0), pids;
+    std::vector<int32_t> poff;
+    if (!plain.empty()) {
+        // the uniform layout's query on those cells alone (grid->hy hidden)
+        dccrgx_grid* g = const_cast<dccrgx_grid*>(grid);
+        Hybrid* keep = g->hy;
+        g->hy = nullptr;
+        int s = to ? dccrgx_neighbors_to_host(g, hood_id, plain.data(), plain.size(), prow.data(), nullptr, 0)
+                   : dccrgx_neighbors_of_host(g, hood_id, plain.data(), plain.size(), prow.data(), nullptr, nullptr, 0);
+        if (s == DCCRGX_OK) {
+            pids.resize(prow.back());
+            poff.resize(3 * prow.back());
+            s = to ? dccrgx_neighbors_to_host(g, hood_id, plain.data(), plain.size(), prow.data(), pids.data(),
+                                              pids.size())
+                   : dccrgx_neighbors_of_host(g, hood_id, plain.data(), plain.size(), prow.data(), pids.data(),
+                                              poff.data(), pids.size());
+        }
+        g->hy = keep;
+        DX_TRY(s);
+    }
+    const std::vector<uint64_t>& orow = to ? H.nto_row : H.nof_row;
+    const std::vector<uint64_t>& oid = to ? H.nto_id : H.nof_id;
+    std::vector<uint64_t> r(n + 1, 0);
+    for (size_t i = 0; i < n; i++) {
+        const int64_t w = where[i];
+        r[i + 1] = r[i] + (w >= 0 ? orow[w + 1] - orow[w] : prow[-w] - prow[-w - 1]);
+    }
+    if (n + 1) DX_HIP(hipMemcpyAsync(row, r.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    if (ids) {
+        DX_CHECK(cap >= r[n], DCCRGX_ERANGE, "capacity %zu < %llu", cap, (unsigned long long)r[n]);
+        std::vector<uint64_t> out(r[n]);
+        std::vector<int32_t> oo(3 * r[n]);
+        for (size_t i = 0; i < n; i++) {
+            const int64_t w = where[i];
+            const uint64_t b = w >= 0 ? orow[w] : prow[-w - 1], e = w >= 0 ? orow[w + 1] : prow[-w];
+            for (uint64_t k = b; k < e; k++) {
+                const uint64_t at = r[i] + (k - b);
+                out[at] = w >= 0 ? oid[k] : pids[k];
+                if (!to)
+                    for (int d = 0; d < 3; d++) oo[3 * at + d] = w >= 0 ? H.nof_off[3 * k + d] : poff[3 * k + d];
+            }
+        }
+        if (!out.empty()) {
+            DX_HIP(hipMemcpyAsync(ids, out.data(), out.size() * 8, hipMemcpyHostToDevice, st));
+            if (!to && off3) DX_HIP(hipMemcpyAsync(off3, oo.data(), oo.size() * 4, hipMemcpyHostToDevice, st));
+        }
+    }
+    DX_HIP(hipStreamSynchronize(st));
+    return DCCRGX_OK;
+}
+
+}  // namespace dccrgx

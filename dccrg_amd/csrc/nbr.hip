@@ -445,6 +445,7 @@ int dccrgx_neighbors_of(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
     const CallerStream fence(grid->ctx, st);
+    if (grid->hy) return hybrid_neighbors(grid, hood_id, false, cells, n, row, ids, off3, cap, st);
     if (!grid->uniform) return explicit_neighbors_of(grid, *h, cells, n, row, ids, off3, cap, st);
     const UGeom& g = grid->g;
     const int32_t sc = 1 << grid->map.max_lvl;  // offsets in indices of the finest level
@@ -473,6 +474,7 @@ int dccrgx_gather_neighbors(const dccrgx_grid* grid, int32_t hood_id, int32_t fi
                             size_t n, uint64_t* row, void* out, size_t cap_bytes, void* stream)
 {
     DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     const Hood* h = find_hood(grid, hood_id);
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     DX_CHECK(field_id >= 0 && (size_t)field_id < grid->fields.size(), DCCRGX_EINVAL, "bad field %d", field_id);
@@ -502,6 +504,7 @@ int dccrgx_face_neighbors_of(const dccrgx_grid* grid, const uint64_t* cells, siz
                              uint64_t* ids, int32_t* dirs, size_t cap, void* stream)
 {
     DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
     const CallerStream fence(grid->ctx, st);
     if (!grid->uniform) return explicit_face_neighbors(grid, cells, n, row, ids, dirs, cap, st);
@@ -513,6 +516,7 @@ int dccrgx_face_neighbors_of_host(const dccrgx_grid* grid, const uint64_t* cells
                                   uint64_t* ids, int32_t* dirs, size_t cap)
 {
     DX_CHECK(grid && row && (cells || n == 0), DCCRGX_EINVAL, "null argument");
+    DX_NO_HYBRID(grid);
     DX_TRY(explicit_host_leaves(grid));
     hipStream_t st = grid->ctx->compute;
     uint64_t *d_cells = nullptr, *d_row = nullptr, *d_ids = nullptr;
@@ -547,6 +551,7 @@ int dccrgx_neighbors_to(const dccrgx_grid* grid, int32_t hood_id, const uint64_t
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);
     hipStream_t st = stream ? (hipStream_t)stream : grid->ctx->compute;
     const CallerStream fence(grid->ctx, st);
+    if (grid->hy) return hybrid_neighbors(grid, hood_id, true, cells, n, row, ids, nullptr, cap, st);
     if (!grid->uniform) return explicit_neighbors_to(grid, *h, cells, n, row, ids, cap, st);
     // candidates with hood_to on the device, unique + sort per cell on the host
     const UGeom& g = grid->g;

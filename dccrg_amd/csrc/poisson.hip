@@ -1030,6 +1030,7 @@ int dccrgx_poisson_create(dccrgx_grid* grid, const dccrgx_poisson_params* prm, c
                           dccrgx_poisson** out)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid && f && out, DCCRGX_EINVAL, "null argument");
     const int32_t uf[5] = {f->rhs, f->solution, f->length_x, f->length_y, f->length_z};
     for (int32_t id : uf) {

@@ -289,6 +289,7 @@ extern "C" {
 int dccrgx_stencil_view_get(const dccrgx_grid* grid, int32_t hood_id, int32_t region, dccrgx_stencil_view* out)
 {
     DX_NOT_PENDING(grid);
+    DX_NO_HYBRID(grid);
     DX_CHECK(grid && out, DCCRGX_EINVAL, "null argument");
     Hood* h = const_cast<Hood*>(find_hood(grid, hood_id));  // the view's data is made on first use
     DX_CHECK(h, DCCRGX_ENOTFOUND, "no neighborhood %d", hood_id);

@@ -84,6 +84,7 @@ int dccrgx_ctx_route_self_through_rccl(dccrgx_ctx* ctx, int32_t on);
  * name: "gol_scalar", "gol_chunk" (slices per workgroup), "poisson_multi",
  * "poisson_solo_global", "incremental" (1 / 0), "ou_small" (queue entries),
  * "full_nto" (1: the full neighbors_to transpose in incremental rebuilds),
+ * "hybrid" (1: one-process uniform grids refine in place whatever their size),
  * "corrupt_ghost", "fail_stop_refining" (rank + 1), "check_init"; set = 0
  * returns the option to its default.  DCCRGX_EINVAL for an unknown name, or
  * in a build compiled with -DDCCRGX_NO_TEST_OPTIONS. */
