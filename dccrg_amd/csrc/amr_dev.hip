@@ -177,49 +177,53 @@ __device__ inline void a_erase_sibling_unrefines(const AView& a, uint64_t c)
 
 // refine_completely, dccrg.hpp:2476-2546.  Requests at the maximum level are
 // dont_unrefine calls (:2486-2488): they are queued for the dont_unrefine
-// kernels with their call index.
+// kernels with their call index.  One wave per request, its lanes over the
+// cell's rows (the blocking test, then the sibling unrefines erased around it).
 __global__ void __launch_bounds__(256) k_req_refine(AView a, const uint64_t* __restrict__ ids, uint64_t n,
                                                     int32_t* __restrict__ res, uint64_t* __restrict__ du_ids,
                                                     uint32_t* __restrict__ du_ord, uint32_t* __restrict__ du_n, int erase)
 {
     const int M = a.v.mp.max_lvl;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t c = ids[i];
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += nwave) {
+        const uint64_t c = ids[i];  // wave-uniform from here on
         int32_t r = 0;
         const int64_t g = ex_find(a.v, c);
         if (g >= 0 && a_owner(a, c) == a.rank) {
             const int lvl = a_level(a, c);
             if (lvl == M) {
-                const uint32_t p = atomicAdd(du_n, 1u);
-                du_ids[p] = c;
-                du_ord[p] = (uint32_t)i;
+                if (lane == 0) {
+                    const uint32_t p = atomicAdd(du_n, 1u);
+                    du_ids[p] = c;
+                    du_ord[p] = (uint32_t)i;
+                }
                 r = 1;  // dont_unrefine of an existing cell
             } else if (!(a.flags[g] & RF_NOT_REFINE)) {
-                bool blocked = false;
                 const uint32_t rw = a.slot_of_g[g];  // a local cell: its row
-                for (uint64_t e = a.nof_row[rw]; e < a.nof_row[rw + 1] && !blocked; e++) {
+                bool blk = false;
+                for (uint64_t e = a.nof_row[rw] + lane; e < a.nof_row[rw + 1]; e += 64) {
                     const uint32_t t = a.nof_g[e];
-                    blocked = a_level(a, a.leaves[t]) < lvl && (a.flags[t] & RF_NOT_REFINE);
+                    blk |= a_level(a, a.leaves[t]) < lvl && (a.flags[t] & RF_NOT_REFINE);
                 }
-                if (!blocked) {
+                if (!__ballot(blk)) {
                     r = 1;
-                    atomicOr(&a.flags[g], RF_REFINE);
-                    if (!erase) goto done;  // no cells_to_unrefine to erase (the adapter refines first)
-                    a_erase_sibling_unrefines(a, c);
-                    for (int pass = 0; pass < 2; pass++) {
-                        const uint64_t* row = pass ? a.nto_row : a.nof_row;
-                        const uint32_t* val = pass ? a.nto_g : a.nof_g;
-                        for (uint64_t e = row[rw]; e < row[rw + 1]; e++) {
-                            const uint64_t nb = a.leaves[val[e]];
-                            if (a_level(a, nb) <= lvl) a_erase_sibling_unrefines(a, nb);
+                    if (lane == 0) atomicOr(&a.flags[g], RF_REFINE);
+                    if (erase) {  // (no cells_to_unrefine to erase when the adapter refines first)
+                        if (lane == 0) a_erase_sibling_unrefines(a, c);
+                        for (int pass = 0; pass < 2; pass++) {
+                            const uint64_t* row = pass ? a.nto_row : a.nof_row;
+                            const uint32_t* val = pass ? a.nto_g : a.nof_g;
+                            for (uint64_t e = row[rw] + lane; e < row[rw + 1]; e += 64) {
+                                const uint64_t nb = a.leaves[val[e]];
+                                if (a_level(a, nb) <= lvl) a_erase_sibling_unrefines(a, nb);
+                            }
                         }
                     }
                 }
             }
         }
-    done:
-        if (res) res[i] = r;
+        if (lane == 0 && res) res[i] = r;
     }
 }
 
@@ -279,86 +283,98 @@ __global__ void __launch_bounds__(256) k_req_du_b(AView a, const uint64_t* __res
 // A window W at the parent's level is covered by W itself, by W's parent, by
 // a coarser ancestor (no leaf inside W) or by W's children; a child that is
 // not a leaf is refined, so its leaves are finer than plvl + 1.
-__device__ inline bool a_window_blocks(const AView& a, uint64_t parent)
+// does the window of item k of a parent at indices pi, level pl block it?
+__device__ inline bool a_item_blocks(const AView& a, const uint64_t pi[3], int pl, int k)
 {
     const MapParams& mp = a.v.mp;
     const int M = mp.max_lvl;
-    uint64_t pi[3];
-    int pl;
-    map_indices(mp, parent, pi, &pl);
     const int64_t L = (int64_t)1 << (M - pl);
-    for (int k = 0; k < a.K; k++) {
-        uint64_t wi[3];
-        bool ok = true;
-        for (int d = 0; d < 3; d++) {
-            const int64_t G = (int64_t)(mp.length[d] << M);
-            int64_t x = (int64_t)pi[d] + (int64_t)a.items[3 * k + d] * L;
-            if (x < 0 || x >= G) {
-                if (!a.v.per[d]) {
-                    ok = false;
-                    break;
-                }
-                x %= G;
-                if (x < 0) x += G;
-            }
-            wi[d] = (uint64_t)x;
+    uint64_t wi[3];
+    for (int d = 0; d < 3; d++) {
+        const int64_t G = (int64_t)(mp.length[d] << M);
+        int64_t x = (int64_t)pi[d] + (int64_t)a.items[3 * k + d] * L;
+        if (x < 0 || x >= G) {
+            if (!a.v.per[d]) return false;
+            x %= G;
+            if (x < 0) x += G;
         }
-        if (!ok) continue;
-        const uint64_t W = map_cell(mp, wi, pl);
-        const int64_t gw = ex_find(a.v, W);
-        if (gw >= 0) continue;  // a leaf of the parent's level: never blocks
-        if (pl > 0 && ex_find(a.v, map_cell(mp, wi, pl - 1)) >= 0) continue;  // coarser
-        bool covered = false;  // by a coarser ancestor: no leaf inside W
-        for (int l = pl - 2; l >= 0 && !covered; l--) covered = ex_find(a.v, map_cell(mp, wi, l)) >= 0;
-        if (covered || pl >= M) continue;
-        uint64_t ch[8];
-        a_children(a, W, ch);
-        for (int j = 0; j < 8; j++) {
-            const int64_t gc = ex_find(a.v, ch[j]);
-            if (gc < 0) return true;                            // refined: leaves at plvl + 2 or finer
-            if (a.flags[gc] & RF_REFINE) return true;           // plvl + 1 and about to be refined
-        }
+        wi[d] = (uint64_t)x;
+    }
+    const uint64_t W = map_cell(mp, wi, pl);
+    if (ex_find(a.v, W) >= 0) return false;                                      // a leaf of the parent's level
+    if (pl > 0 && ex_find(a.v, map_cell(mp, wi, pl - 1)) >= 0) return false;  // coarser
+    for (int l = pl - 2; l >= 0; l--)  // covered by a coarser ancestor: no leaf inside W
+        if (ex_find(a.v, map_cell(mp, wi, l)) >= 0) return false;
+    if (pl >= M) return false;
+    uint64_t ch[8];
+    a_children(a, W, ch);
+    for (int j = 0; j < 8; j++) {
+        const int64_t gc = ex_find(a.v, ch[j]);
+        if (gc < 0) return true;                   // refined: leaves at plvl + 2 or finer
+        if (a.flags[gc] & RF_REFINE) return true;  // plvl + 1 and about to be refined
     }
     return false;
 }
 
-// unrefine_completely, dccrg.hpp:2596-2675, phase 1 (reads the flags only)
+// unrefine_completely, dccrg.hpp:2596-2675, phase 1 (reads the flags only).
+// One wave per request: lanes 0-7 test the siblings (their outcome in the
+// reference's order, :2617-2633, is the first sibling that stops the loop,
+// found by ballot), then the lanes share the parent's window items (a serial
+// walk of them was a chain of ~100 dependent lookups per request).
 __global__ void __launch_bounds__(256) k_req_unref_a(AView a, const uint64_t* __restrict__ ids, uint64_t n,
                                                      int32_t* __restrict__ res, uint32_t* __restrict__ grp,
                                                      uint32_t* __restrict__ key)
 {
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t c = ids[i];
-        key[i] = NONE32;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += nwave) {
+        const uint64_t c = ids[i];  // wave-uniform from here on
         int32_t r = 0;
+        uint32_t kk = NONE32;
         const int64_t g = ex_find(a.v, c);
         if (g >= 0 && a_owner(a, c) == a.rank) {
             r = 1;
-            if (a_level(a, c) > 0) {
-                uint64_t s[8];
-                a_siblings(a, c, s);
-                bool stop = false;
-                for (int k = 0; k < 8 && !stop; k++) {  // in the reference's order (:2617-2633)
-                    if (!s[k]) continue;
-                    if (a_has_children(a, s[k])) {
-                        r = 0;
-                        stop = true;
-                        break;
+            uint64_t pi[3];
+            int pl;
+            const uint64_t parent = a_parent(a, c);
+            if (a_level(a, c) > 0 && map_indices(a.v.mp, parent, pi, &pl)) {
+                const uint64_t h = (uint64_t)1 << (a.v.mp.max_lvl - pl - 1);
+                bool hc = false, fl = false, un = false;
+                int64_t gk = -1;
+                if (lane < 8) {  // sibling `lane` (x fastest, Mapping::get_all_children)
+                    const uint64_t ci[3] = {pi[0] + (lane & 1) * h, pi[1] + ((lane >> 1) & 1) * h,
+                                            pi[2] + ((lane >> 2) & 1) * h};
+                    const uint64_t sk = map_cell(a.v.mp, ci, pl + 1);
+                    hc = a_has_children(a, sk);
+                    if (!hc) {  // no children: a leaf
+                        gk = ex_find(a.v, sk);
+                        const uint32_t f = a.flags[gk];
+                        fl = (f & (RF_REFINE | RF_NOT_UNREFINE)) != 0;
+                        un = (f & RF_UNREFINE) != 0;
                     }
-                    const uint32_t f = a.flags[ex_find(a.v, s[k])];
-                    stop = (f & (RF_REFINE | RF_NOT_UNREFINE)) != 0;
                 }
-                for (int k = 0; k < 8 && !stop; k++)  // a sibling already recorded (amr.hip)
-                    stop = s[k] && (a.flags[ex_find(a.v, s[k])] & RF_UNREFINE);
-                if (!stop && !a_window_blocks(a, a_parent(a, c))) {
-                    const uint32_t k0 = (uint32_t)ex_find(a.v, s[0]);
-                    key[i] = k0;
-                    atomicMin(&grp[k0], (uint32_t)i);
+                const uint64_t stop1 = __ballot(hc || fl);
+                bool stop = stop1 != 0;
+                if (stop) {
+                    if ((__ballot(hc) >> (__ffsll((unsigned long long)stop1) - 1)) & 1) r = 0;  // first stop: children
+                } else {
+                    stop = __ballot(un) != 0;  // a sibling already recorded (amr.hip)
+                }
+                if (!stop) {
+                    bool blk = false;
+                    for (int k = lane; k < a.K; k += 64) blk |= a_item_blocks(a, pi, pl, k);
+                    if (!__ballot(blk)) {
+                        const uint32_t k0 = (uint32_t)__shfl(gk, 0, 64);  // sibling 0, a leaf
+                        kk = k0;
+                        if (lane == 0) atomicMin(&grp[k0], (uint32_t)i);
+                    }
                 }
             }
         }
-        if (res) res[i] = r;
+        if (lane == 0) {
+            key[i] = kk;
+            if (res) res[i] = r;
+        }
     }
 }
 
@@ -462,6 +478,31 @@ __global__ void __launch_bounds__(256) k_spread(AView a, uint32_t bit, int finer
         } else {
             nof_search(a.v, a.items, a.K, c, visit);
             nto_search(a.v, a.items_to, a.K, c, visit);
+        }
+    }
+}
+
+// k_spread on one process (every leaf's rows held): one wave per frontier
+// cell, its lanes over the cell's rows (the per-cell loop over ~50 entries
+// was a latency chain with a few hundred cells in flight)
+__global__ void __launch_bounds__(256) k_spread_rows(AView a, uint32_t bit, int finer, const uint32_t* __restrict__ front,
+                                                     const uint32_t* __restrict__ front_n, uint32_t* __restrict__ next,
+                                                     uint32_t* __restrict__ next_n)
+{
+    const uint32_t n = *front_n;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += nwave) {
+        const uint32_t g = front[i];
+        const int l = a_level(a, a.leaves[g]);
+        const uint64_t b0 = a.nof_row[g], n0 = a.nof_row[g + 1] - b0;
+        const uint64_t b1 = a.nto_row[g], n1 = a.nto_row[g + 1] - b1;
+        for (uint64_t e = lane; e < n0 + n1; e += 64) {
+            const uint32_t t = e < n0 ? a.nof_g[b0 + e] : a.nto_g[b1 + (e - n0)];
+            const int lt = a_level(a, a.leaves[t]);
+            if (finer ? lt <= l : lt >= l) continue;
+            if (a.flags[t] & bit) continue;
+            if (!(atomicOr(&a.flags[t], bit) & bit)) next[atomicAdd(next_n, 1u)] = t;
         }
     }
 }
@@ -602,6 +643,48 @@ __global__ void __launch_bounds__(64) k_ou_walk(AView a, const uint32_t* __restr
             else if (!fail) atomicOr(&a.flags[k != NONE32 ? k : g], RF_KEEP);
         }
         __syncthreads();
+    }
+}
+
+// override_unrefines as a window test (the default; k_ou_walk, the
+// reference's walk, under the test option "ou_walk").  The walk of
+// dccrg.hpp:9975-10040 starts at the unrefined cell's face neighbors and
+// spreads through face neighbors that are is_neighbor(parent, .) (:9603-9683),
+// failing at a leaf finer than the unrefined cell or at one of its level to
+// be refined.  Those leaves are the ones overlapping the parent's
+// neighborhood box (the parent-sized windows at the neighborhood's offsets,
+// and the parent itself); leaves tiling a box are face-connected inside it
+// and the start cells lie in it, so the walk reaches every one of them and
+// no other: it fails exactly when a sibling is not a leaf (finer leaves
+// inside the parent) or is to be refined, or a window holds such leaves
+// (a_item_blocks, the request-time test of unrefine_completely, :2638-2670).
+// One wave per group walker / lone request: lanes 0-7 the siblings, then the
+// lanes over the window items.
+__global__ void __launch_bounds__(256) k_ou_check(AView a, const uint32_t* __restrict__ us,
+                                                  const uint32_t* __restrict__ nu, const uint32_t* __restrict__ grp,
+                                                  const uint32_t* __restrict__ key)
+{
+    const uint32_t n = *nu;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += nwave) {
+        const uint32_t g = us[i];
+        const uint32_t k = key[i];
+        if (k != NONE32 && grp[k] != g) continue;  // not the group's walker (wave-uniform)
+        uint64_t pi[3];
+        int pl;
+        if (!map_indices(a.v.mp, a_parent(a, a.leaves[g]), pi, &pl)) continue;
+        bool bad = false;
+        if (lane < 8) {  // a sibling that is not a leaf, or is to be refined or kept (:9960-9975)
+            const uint64_t h = (uint64_t)1 << (a.v.mp.max_lvl - pl - 1);
+            const uint64_t ci[3] = {pi[0] + (lane & 1) * h, pi[1] + ((lane >> 1) & 1) * h,
+                                    pi[2] + ((lane >> 2) & 1) * h};
+            const int64_t gs = ex_find(a.v, map_cell(a.v.mp, ci, pl + 1));
+            bad = gs < 0 || (a.flags[gs] & (RF_REFINE | RF_NOT_UNREFINE)) != 0;
+        }
+        if (__ballot(bad)) continue;
+        for (int q = lane; q < a.K; q += 64) bad |= a_item_blocks(a, pi, pl, q);
+        if (!__ballot(bad) && lane == 0) atomicOr(&a.flags[k != NONE32 ? k : g], RF_KEEP);
     }
 }
 
@@ -974,7 +1057,7 @@ int amr_dev_requests_ex(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, co
         DX_TRY(S.get(&d_ord, n));
         DX_TRY(S.get(&d_dun, 1));
         DX_HIP(hipMemsetAsync(d_dun, 0, 4, st));
-        hipLaunchKernelGGL(k_req_refine, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n, d_res, d_du,
+        hipLaunchKernelGGL(k_req_refine, dim3(blocks(64 * (uint64_t)n)), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n, d_res, d_du,
                            d_ord, d_dun, erase);
         hipLaunchKernelGGL(k_req_du_a, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_du, (const uint32_t*)d_ord,
                            (const uint32_t*)d_dun, (uint64_t)0, (int32_t*)nullptr, d_grp, d_key);
@@ -988,8 +1071,8 @@ int amr_dev_requests_ex(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, co
                            (const uint32_t*)nullptr, (uint64_t)n, (const uint32_t*)d_grp, (const uint32_t*)d_key, erase);
         break;
     case DCCRGX_AMR_UNREFINE:
-        hipLaunchKernelGGL(k_req_unref_a, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n, d_res,
-                           d_grp, d_key);
+        hipLaunchKernelGGL(k_req_unref_a, dim3(blocks(64 * (uint64_t)n)), dim3(256), 0, st, a, (const uint64_t*)d_ids,
+                           (uint64_t)n, d_res, d_grp, d_key);
         hipLaunchKernelGGL(k_req_unref_b, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n,
                            (const uint32_t*)d_grp, (const uint32_t*)d_key);
         break;
@@ -1043,8 +1126,12 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
         hipLaunchKernelGGL(k_collect, dim3(bN), dim3(256), 0, st, a, bit, d_fa, c);
         uint32_t *f = d_fa, *nx = d_fb;
         for (int r = 0; r < M; r++) {
-            hipLaunchKernelGGL(k_spread, dim3(bN), dim3(256), 0, st, a, bit, phase == 0 ? 1 : 0, (const uint32_t*)f,
-                               (const uint32_t*)(c + r), nx, c + r + 1);
+            if (a.rows_all)
+                hipLaunchKernelGGL(k_spread_rows, dim3(blocks(64 * N, 1024)), dim3(256), 0, st, a, bit, phase == 0 ? 1 : 0,
+                                   (const uint32_t*)f, (const uint32_t*)(c + r), nx, c + r + 1);
+            else
+                hipLaunchKernelGGL(k_spread, dim3(bN), dim3(256), 0, st, a, bit, phase == 0 ? 1 : 0, (const uint32_t*)f,
+                                   (const uint32_t*)(c + r), nx, c + r + 1);
             std::swap(f, nx);
         }
     }
@@ -1054,40 +1141,45 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     hipLaunchKernelGGL(k_collect, dim3(bN), dim3(256), 0, st, a, RF_UNREFINE, d_fa, cu);
     hipLaunchKernelGGL(k_ou_group, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_fa, (const uint32_t*)cu, d_grp,
                        d_key);
-    // the walks: first with a small LDS workspace (a walk visits tens of
-    // cells; many waves per CU), the few that overflow it again with one
-    // sized for the largest possible closure
-    const uint32_t hl = grid->params.neighborhood_length;
-    const uint64_t P = 8ull * (2 * hl + 3) * (2 * hl + 3) * (2 * hl + 3);
-    const uint32_t Q = (uint32_t)(6 * P + 8);
-    uint32_t Sz = 16;
-    while (Sz < 2 * Q) Sz <<= 1;
-    const size_t ws = (size_t)(Q + Sz) * 8;
-    const bool lds = ws <= 48 * 1024;
-    const unsigned waves = lds ? 4096 : 1024;
-    uint64_t* d_scr = nullptr;
-    if (!lds) DX_TRY(S.get(&d_scr, (size_t)waves * (Q + Sz)));
-    int32_t* d_err = (int32_t*)(d_cnt + NC - 2);  // zeroed with the counters
-    uint32_t *d_retry, *d_nretry = d_cnt + NC - 1;
-    DX_TRY(S.get(&d_retry, N));
-    // DCCRGX_OU_SMALL (tests): the first pass's queue length, to send walks to the second pass
-    const uint32_t Q1 = (uint32_t)std::max<int64_t>(2, test_opt(OPT_OU_SMALL, 256));
-    uint32_t S1 = 16;
-    while (S1 < 2 * Q1) S1 <<= 1;  // 256 -> 512: 6 KiB per wave
-    if (Q1 < Q && (size_t)(Q1 + S1) * 8 <= 48 * 1024) {
-        hipLaunchKernelGGL(k_ou_walk, dim3(8192), dim3(64), (Q1 + S1) * 8, st, a, (const uint32_t*)d_fa,
-                           (const uint32_t*)cu, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
-                           (const uint32_t*)d_grp, (const uint32_t*)d_key, Q1, S1, 1, (uint64_t*)nullptr, d_retry,
-                           d_nretry, d_err);
-        hipLaunchKernelGGL(k_ou_walk, dim3(waves), dim3(64), lds ? ws : 0, st, a, (const uint32_t*)d_fa,
-                           (const uint32_t*)cu, (const uint32_t*)d_retry, (const uint32_t*)d_nretry,
-                           (const uint32_t*)d_grp, (const uint32_t*)d_key, Q, Sz, lds ? 1 : 0, d_scr,
-                           (uint32_t*)nullptr, (uint32_t*)nullptr, d_err);
+    int32_t* d_err = (int32_t*)(d_cnt + NC - 2);  // zeroed with the counters (walk overflow)
+    if (!test_opt(OPT_OU_WALK, 0)) {
+        hipLaunchKernelGGL(k_ou_check, dim3(blocks(64 * N, 2048)), dim3(256), 0, st, a, (const uint32_t*)d_fa,
+                           (const uint32_t*)cu, (const uint32_t*)d_grp, (const uint32_t*)d_key);
     } else {
-        hipLaunchKernelGGL(k_ou_walk, dim3(waves), dim3(64), lds ? ws : 0, st, a, (const uint32_t*)d_fa,
-                           (const uint32_t*)cu, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
-                           (const uint32_t*)d_grp, (const uint32_t*)d_key, Q, Sz, lds ? 1 : 0, d_scr,
-                           (uint32_t*)nullptr, (uint32_t*)nullptr, d_err);
+        // the walks: first with a small LDS workspace (a walk visits tens of
+        // cells; many waves per CU), the few that overflow it again with one
+        // sized for the largest possible closure
+        const uint32_t hl = grid->params.neighborhood_length;
+        const uint64_t P = 8ull * (2 * hl + 3) * (2 * hl + 3) * (2 * hl + 3);
+        const uint32_t Q = (uint32_t)(6 * P + 8);
+        uint32_t Sz = 16;
+        while (Sz < 2 * Q) Sz <<= 1;
+        const size_t ws = (size_t)(Q + Sz) * 8;
+        const bool lds = ws <= 48 * 1024;
+        const unsigned waves = lds ? 4096 : 1024;
+        uint64_t* d_scr = nullptr;
+        if (!lds) DX_TRY(S.get(&d_scr, (size_t)waves * (Q + Sz)));
+        uint32_t *d_retry, *d_nretry = d_cnt + NC - 1;
+        DX_TRY(S.get(&d_retry, N));
+        // DCCRGX_OU_SMALL (tests): the first pass's queue length, to send walks to the second pass
+        const uint32_t Q1 = (uint32_t)std::max<int64_t>(2, test_opt(OPT_OU_SMALL, 256));
+        uint32_t S1 = 16;
+        while (S1 < 2 * Q1) S1 <<= 1;  // 256 -> 512: 6 KiB per wave
+        if (Q1 < Q && (size_t)(Q1 + S1) * 8 <= 48 * 1024) {
+            hipLaunchKernelGGL(k_ou_walk, dim3(8192), dim3(64), (Q1 + S1) * 8, st, a, (const uint32_t*)d_fa,
+                               (const uint32_t*)cu, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                               (const uint32_t*)d_grp, (const uint32_t*)d_key, Q1, S1, 1, (uint64_t*)nullptr, d_retry,
+                               d_nretry, d_err);
+            hipLaunchKernelGGL(k_ou_walk, dim3(waves), dim3(64), lds ? ws : 0, st, a, (const uint32_t*)d_fa,
+                               (const uint32_t*)cu, (const uint32_t*)d_retry, (const uint32_t*)d_nretry,
+                               (const uint32_t*)d_grp, (const uint32_t*)d_key, Q, Sz, lds ? 1 : 0, d_scr,
+                               (uint32_t*)nullptr, (uint32_t*)nullptr, d_err);
+        } else {
+            hipLaunchKernelGGL(k_ou_walk, dim3(waves), dim3(64), lds ? ws : 0, st, a, (const uint32_t*)d_fa,
+                               (const uint32_t*)cu, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                               (const uint32_t*)d_grp, (const uint32_t*)d_key, Q, Sz, lds ? 1 : 0, d_scr,
+                               (uint32_t*)nullptr, (uint32_t*)nullptr, d_err);
+        }
     }
     hipLaunchKernelGGL(k_ou_final, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_fa, (const uint32_t*)cu,
                        (const uint32_t*)d_key);

@@ -1170,7 +1170,7 @@ std::atomic<bool> g_test_set[OPT_COUNT];
 const char* const kTestOptName[OPT_COUNT] = {"gol_scalar",  "gol_chunk",      "poisson_multi",
                                              "poisson_solo_global", "incremental", "ou_small",
                                              "corrupt_ghost", "fail_stop_refining", "check_init", "full_nto",
-                                             "hybrid"};
+                                             "hybrid", "ou_walk"};
 }  // namespace
 
 int64_t test_opt(TestOpt o, int64_t dflt)

@@ -179,6 +179,7 @@ enum TestOpt {
     OPT_CHECK_INIT,          // explicit grids: check the device leaves and lookups against the host list
     OPT_FULL_NTO,            // one rank: the full neighbors_to transpose after an incremental neighbors_of
     OPT_HYBRID,              // 1: one-process uniform grids refine in place (hybrid.hip) whatever their size
+    OPT_OU_WALK,             // 1: override_unrefines walks the face graph (k_ou_walk) instead of k_ou_check
     OPT_COUNT
 };
 int64_t test_opt(TestOpt o, int64_t dflt);

@@ -85,6 +85,8 @@ int dccrgx_ctx_route_self_through_rccl(dccrgx_ctx* ctx, int32_t on);
  * "poisson_solo_global", "incremental" (1 / 0), "ou_small" (queue entries),
  * "full_nto" (1: the full neighbors_to transpose in incremental rebuilds),
  * "hybrid" (1: one-process uniform grids refine in place whatever their size),
+ * "ou_walk" (1: override_unrefines walks the face graph, the reference's
+ * literal algorithm, instead of the equivalent window test),
  * "corrupt_ghost", "fail_stop_refining" (rank + 1), "check_init"; set = 0
  * returns the option to its default.  DCCRGX_EINVAL for an unknown name, or
  * in a build compiled with -DDCCRGX_NO_TEST_OPTIONS. */

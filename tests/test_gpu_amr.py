@@ -110,8 +110,10 @@ def rebuild_mode(request, lib_options):
     library picks it above 2^20 leaves, the test option forces it).  After
     an incremental neighbors_of one rank also updates neighbors_to around the
     changes (nto_incremental); incremental_full_nto keeps the full transpose.
-    small_walks: override_unrefines' first pass gets a 4-entry queue, so the
-    walks overflow into the second, full-size pass (amr_dev.hip k_ou_walk)."""
+    small_walks: override_unrefines walks the face graph as the reference
+    does (amr_dev.hip k_ou_walk, test option ou_walk; the default is the
+    equivalent window test k_ou_check) and the walk's first pass gets a
+    4-entry queue, so the walks overflow into the second, full-size pass."""
     lib_options("incremental", 1 if request.param.startswith("incremental") else 0)
     if request.param == "incremental_full_nto":
         lib_options("full_nto", 1)
@@ -119,6 +121,7 @@ def rebuild_mode(request, lib_options):
     # host-merged list; one rank: the list fetched from the device) (explicit.hip explicit_init)
     lib_options("check_init", 1)
     if request.param == "small_walks":
+        lib_options("ou_walk", 1)
         lib_options("ou_small", 4)
     return request.param
 

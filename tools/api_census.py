@@ -33,8 +33,9 @@ kc, kd = collections.Counter(), collections.Counter()
 for k in kt:
     t = int(k["Start_Timestamp"])
     if lo <= t < hi:
-        kc[k["Kernel_Name"].split("(")[0][-48:]] += 1
-        kd[k["Kernel_Name"].split("(")[0][-48:]] += int(k["End_Timestamp"]) - t
+        name = k["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-60:]
+        kc[name] += 1
+        kd[name] += int(k["End_Timestamp"]) - t
 print(f"kernels: {sum(kc.values()) / steps:.0f} launches/step, {sum(kd.values()) / 1e6 / steps:.3f} ms/step busy")
-for f, n in kd.most_common(12):
-    print(f"  {f:48s} {kc[f] / steps:5.1f}/step {n / 1e3 / steps:8.1f} us/step")
+for f, n in kd.most_common(int(sys.argv[4]) if len(sys.argv) > 4 else 40):
+    print(f"  {f:60s} {kc[f] / steps:5.1f}/step {n / 1e3 / steps:8.1f} us/step  avg {n / 1e3 / kc[f]:6.1f} us")

@@ -77,6 +77,13 @@ for step in "$@"; do
       python3 tools/api_census.py $out/adapt_trace > $out/adapt_census.txt 2>&1 || true
       python3 tools/idle_gaps.py $out/adapt_trace > $out/adapt_gaps.txt 2>&1 || true
       tail -n 40 $out/adapt_census.txt ;;
+    adaptprof)
+      # the 218k-leaf loop: plain timing, then a kernel + HIP-runtime trace and its census
+      timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_plain.log 2>&1 || fail adapt_plain $? $out/adapt_plain.log
+      tail -n 1 $out/adapt_plain.log
+      timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $out/adapt_trace -o run -- python3 tools/adapt_loop.py > $out/adapt_trace.log 2>&1 || fail adapt_trace $? $out/adapt_trace.log
+      python3 tools/api_census.py $out/adapt_trace > $out/adapt_census.txt 2>&1 || true
+      head -n 30 $out/adapt_census.txt ;;
     adaptsplit)
       # adapt_grid in its parts (synchronised after each), at 218 k and 3.5 M
       # leaves, then the library's phase timers waiting for the device per lap
