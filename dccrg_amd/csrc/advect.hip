@@ -956,8 +956,10 @@ int dccrgx_advect_adapt_requests(dccrgx_grid* grid, int32_t hood_id, const dccrg
     // order, each a batch over its ascending device list (the calls' outcome)
     const int32_t kinds[3] = {DCCRGX_AMR_REFINE, DCCRGX_AMR_DONT_UNREFINE, DCCRGX_AMR_UNREFINE};
     if (s == DCCRGX_OK) amr_state(grid);
-    for (int k = 0; k < 3 && s == DCCRGX_OK; k++)
-        if (counts[k]) s = amr_dev_requests_ex(grid, kinds[k], nullptr, dev[k], counts[k], nullptr);
+    if (s == DCCRGX_OK && (counts[0] || counts[1] || counts[2])) {
+        const uint64_t* dv[3] = {dev[0], dev[1], dev[2]};
+        s = amr_dev_requests_many(grid, 3, kinds, nullptr, dv, counts, nullptr);
+    }
     T.lap("requests");
     ds_free(d_code, st);
     ds_free(d_lists, st);

@@ -1029,59 +1029,91 @@ int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_
 int amr_dev_requests_ex(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, const uint64_t* dev_ids, size_t n,
                         int32_t* results)
 {
+    return amr_dev_requests_many(grid, 1, &kind, &ids, &dev_ids, &n, &results);
+}
+
+// several request batches in call order: their scratch cleared by one fill
+// and their results read back behind one synchronisation (each batch's
+// kernels follow the previous batch's on the stream, as separate calls do)
+int amr_dev_requests_many(dccrgx_grid* grid, int nk, const int32_t* kinds, const uint64_t* const* ids,
+                          const uint64_t* const* dev_ids, const size_t* counts, int32_t* const* results)
+{
     Amr& A = *grid->amr;
     DX_TRY(amr_dev_sync(grid));
-    if (!n) return DCCRGX_OK;
+    DX_CHECK(nk >= 0 && nk <= 3, DCCRGX_EINTERNAL, "%d request batches", nk);
     hipStream_t st = grid->ctx->compute;
     const AView a = aview(grid, A.d_flags);
     Scratch S(st);
-    uint64_t *d_ids, *d_du;
-    int32_t* d_res = nullptr;
-    uint32_t *d_grp, *d_key, *d_ord, *d_dun;
-    if (dev_ids) {
-        d_ids = const_cast<uint64_t*>(dev_ids);
-    } else {
-        DX_TRY(S.get(&d_ids, n));
-        DX_TRY(dx_h2d_async(grid->ctx, d_ids, ids, n * 8, st));
+    struct Batch {
+        uint64_t *ids = nullptr, *du = nullptr;
+        int32_t* res = nullptr;
+        uint32_t *grp = nullptr, *key = nullptr, *ord = nullptr, *dun = nullptr;
+    } B[3];
+    Fill z[8];
+    int nz = 0;
+    for (int k = 0; k < nk; k++) {
+        const size_t n = counts[k];
+        if (!n) continue;
+        Batch& b = B[k];
+        if (dev_ids && dev_ids[k]) {
+            b.ids = const_cast<uint64_t*>(dev_ids[k]);
+        } else {
+            DX_TRY(S.get(&b.ids, n));
+            DX_TRY(dx_h2d_async(grid->ctx, b.ids, ids[k], n * 8, st));
+        }
+        if (results && results[k]) DX_TRY(S.get(&b.res, n));
+        DX_TRY(S.get(&b.grp, a.n));
+        DX_TRY(S.get(&b.key, n));
+        z[nz++] = Fill{b.grp, a.n * 4, 0xff};
+        if (kinds[k] == DCCRGX_AMR_REFINE) {
+            DX_TRY(S.get(&b.du, n));
+            DX_TRY(S.get(&b.ord, n));
+            DX_TRY(S.get(&b.dun, 1));
+            z[nz++] = Fill{b.dun, 4, 0};
+        }
     }
-    if (results) DX_TRY(S.get(&d_res, n));
-    DX_TRY(S.get(&d_grp, a.n));
-    DX_TRY(S.get(&d_key, n));
-    DX_HIP(hipMemsetAsync(d_grp, 0xff, a.n * 4, st));
-    const unsigned b = blocks(n);
-    if (kind == DCCRGX_AMR_UNREFINE) A.dev_unrefines = true;
-    const int erase = A.dev_unrefines ? 1 : 0;
-    switch (kind) {
-    case DCCRGX_AMR_REFINE:
-        DX_TRY(S.get(&d_du, n));
-        DX_TRY(S.get(&d_ord, n));
-        DX_TRY(S.get(&d_dun, 1));
-        DX_HIP(hipMemsetAsync(d_dun, 0, 4, st));
-        hipLaunchKernelGGL(k_req_refine, dim3(blocks(64 * (uint64_t)n)), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n, d_res, d_du,
-                           d_ord, d_dun, erase);
-        hipLaunchKernelGGL(k_req_du_a, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_du, (const uint32_t*)d_ord,
-                           (const uint32_t*)d_dun, (uint64_t)0, (int32_t*)nullptr, d_grp, d_key);
-        hipLaunchKernelGGL(k_req_du_b, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_du, (const uint32_t*)d_ord,
-                           (const uint32_t*)d_dun, (uint64_t)0, (const uint32_t*)d_grp, (const uint32_t*)d_key, erase);
-        break;
-    case DCCRGX_AMR_DONT_UNREFINE:
-        hipLaunchKernelGGL(k_req_du_a, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (const uint32_t*)nullptr,
-                           (const uint32_t*)nullptr, (uint64_t)n, d_res, d_grp, d_key);
-        hipLaunchKernelGGL(k_req_du_b, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (const uint32_t*)nullptr,
-                           (const uint32_t*)nullptr, (uint64_t)n, (const uint32_t*)d_grp, (const uint32_t*)d_key, erase);
-        break;
-    case DCCRGX_AMR_UNREFINE:
-        hipLaunchKernelGGL(k_req_unref_a, dim3(blocks(64 * (uint64_t)n)), dim3(256), 0, st, a, (const uint64_t*)d_ids,
-                           (uint64_t)n, d_res, d_grp, d_key);
-        hipLaunchKernelGGL(k_req_unref_b, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n,
-                           (const uint32_t*)d_grp, (const uint32_t*)d_key);
-        break;
-    default:
-        hipLaunchKernelGGL(k_req_dont_refine, dim3(b), dim3(256), 0, st, a, (const uint64_t*)d_ids, (uint64_t)n, d_res);
-        break;
+    DX_TRY(dx_fill_many(z, nz, st));
+    std::vector<D2H> back;
+    for (int k = 0; k < nk; k++) {
+        const size_t n = counts[k];
+        if (!n) continue;
+        const Batch& b = B[k];
+        const unsigned bl = blocks(n), bw = blocks(64 * (uint64_t)n);  // a thread / a wave per request
+        if (kinds[k] == DCCRGX_AMR_UNREFINE) A.dev_unrefines = true;
+        const int erase = A.dev_unrefines ? 1 : 0;
+        switch (kinds[k]) {
+        case DCCRGX_AMR_REFINE:
+            hipLaunchKernelGGL(k_req_refine, dim3(bw), dim3(256), 0, st, a, (const uint64_t*)b.ids, (uint64_t)n,
+                               b.res, b.du, b.ord, b.dun, erase);
+            hipLaunchKernelGGL(k_req_du_a, dim3(bl), dim3(256), 0, st, a, (const uint64_t*)b.du,
+                               (const uint32_t*)b.ord, (const uint32_t*)b.dun, (uint64_t)0, (int32_t*)nullptr, b.grp,
+                               b.key);
+            hipLaunchKernelGGL(k_req_du_b, dim3(bl), dim3(256), 0, st, a, (const uint64_t*)b.du,
+                               (const uint32_t*)b.ord, (const uint32_t*)b.dun, (uint64_t)0, (const uint32_t*)b.grp,
+                               (const uint32_t*)b.key, erase);
+            break;
+        case DCCRGX_AMR_DONT_UNREFINE:
+            hipLaunchKernelGGL(k_req_du_a, dim3(bl), dim3(256), 0, st, a, (const uint64_t*)b.ids,
+                               (const uint32_t*)nullptr, (const uint32_t*)nullptr, (uint64_t)n, b.res, b.grp, b.key);
+            hipLaunchKernelGGL(k_req_du_b, dim3(bl), dim3(256), 0, st, a, (const uint64_t*)b.ids,
+                               (const uint32_t*)nullptr, (const uint32_t*)nullptr, (uint64_t)n,
+                               (const uint32_t*)b.grp, (const uint32_t*)b.key, erase);
+            break;
+        case DCCRGX_AMR_UNREFINE:
+            hipLaunchKernelGGL(k_req_unref_a, dim3(bw), dim3(256), 0, st, a, (const uint64_t*)b.ids, (uint64_t)n,
+                               b.res, b.grp, b.key);
+            hipLaunchKernelGGL(k_req_unref_b, dim3(bl), dim3(256), 0, st, a, (const uint64_t*)b.ids, (uint64_t)n,
+                               (const uint32_t*)b.grp, (const uint32_t*)b.key);
+            break;
+        default:
+            hipLaunchKernelGGL(k_req_dont_refine, dim3(bl), dim3(256), 0, st, a, (const uint64_t*)b.ids, (uint64_t)n,
+                               b.res);
+            break;
+        }
+        DX_HIP(hipGetLastError());
+        if (b.res) back.push_back(D2H{results[k], b.res, n * 4});
     }
-    DX_HIP(hipGetLastError());
-    if (results) DX_TRY(dx_d2h(grid->ctx, results, d_res, n * 4, st));
+    if (!back.empty()) DX_TRY(dx_d2h_many(grid->ctx, back.data(), back.size(), st));
     A.host_current = false;
     return DCCRGX_OK;
 }

@@ -43,9 +43,12 @@ static int stage_reserve(Ctx* c, size_t bytes)
     size_t want = std::min<size_t>(std::max<size_t>({bytes, 2 * c->stage_bytes, 4u << 20}), 64ull << 20);
     if (c->stage) DX_HIP(hipHostFree(c->stage));
     c->stage = nullptr;
+    c->stage_dev = nullptr;
     c->stage_bytes = 0;
-    DX_HIP(hipHostMalloc(&c->stage, want, hipHostMallocDefault));
+    // coherent: the gather kernel's stores reach host memory without a cache flush
+    DX_HIP(hipHostMalloc(&c->stage, want, hipHostMallocMapped | hipHostMallocCoherent));
     c->stage_bytes = want;
+    DX_HIP(hipHostGetDevicePointer(&c->stage_dev, c->stage, 0));
     return DCCRGX_OK;
 }
 
@@ -140,10 +143,42 @@ int dx_fill_many(const Fill* v, int n, hipStream_t st)
     return DCCRGX_OK;
 }
 
+constexpr int GATHER_RANGES = 16;
+constexpr size_t GATHER_MAX = 1u << 20;
+
+struct GatherArgs {
+    const uint8_t* src[GATHER_RANGES];
+    uint8_t* dst[GATHER_RANGES];  // in the pinned stage (device address)
+    uint64_t bytes[GATHER_RANGES];
+};
+
+// blockIdx.y: the range; 4-byte loads / stores when both ends and the size
+// allow, bytes otherwise (read-backs of counters and short id lists)
+__global__ void __launch_bounds__(256) k_gather_d2h(GatherArgs a)
+{
+    const int r = blockIdx.y;
+    const uint8_t* s = a.src[r];
+    uint8_t* d = a.dst[r];
+    const uint64_t n = a.bytes[r];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((((uintptr_t)s | (uintptr_t)d | n) & 3) == 0) {
+        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s);
+        uint32_t* d4 = reinterpret_cast<uint32_t*>(d);
+        for (uint64_t i = t0; i < n / 4; i += stride) d4[i] = s4[i];
+    } else {
+        for (uint64_t i = t0; i < n; i += stride) d[i] = s[i];
+    }
+}
+
 int dx_d2h_many(Ctx* c, const D2H* v, size_t n, hipStream_t st)
 {
-    size_t total = 0;
-    for (size_t i = 0; i < n; i++) total += (v[i].bytes + 15) & ~(size_t)15;
+    size_t total = 0, nz = 0, most = 0;
+    for (size_t i = 0; i < n; i++) {
+        total += (v[i].bytes + 15) & ~(size_t)15;
+        nz += v[i].bytes ? 1 : 0;
+        most = std::max(most, v[i].bytes);
+    }
     if (!total) return DCCRGX_OK;
     if (total > STAGE_CHUNK) {  // large: one at a time
         for (size_t i = 0; i < n; i++) DX_TRY(dx_d2h(c, v[i].dst, v[i].src, v[i].bytes, st));
@@ -151,9 +186,27 @@ int dx_d2h_many(Ctx* c, const D2H* v, size_t n, hipStream_t st)
     }
     DX_TRY(stage_reserve(c, total));
     size_t at = 0;
-    for (size_t i = 0; i < n; i++) {
-        if (v[i].bytes) DX_HIP(hipMemcpyAsync((char*)c->stage + at, v[i].src, v[i].bytes, hipMemcpyDeviceToHost, st));
-        at += (v[i].bytes + 15) & ~(size_t)15;
+    if (total <= GATHER_MAX && nz <= (size_t)GATHER_RANGES && c->stage_dev) {
+        GatherArgs a{};
+        int m = 0;
+        for (size_t i = 0; i < n; i++) {
+            if (v[i].bytes) {
+                a.src[m] = static_cast<const uint8_t*>(v[i].src);
+                a.dst[m] = static_cast<uint8_t*>(c->stage_dev) + at;
+                a.bytes[m] = v[i].bytes;
+                m++;
+            }
+            at += (v[i].bytes + 15) & ~(size_t)15;
+        }
+        const unsigned gx = (unsigned)std::min<uint64_t>((most / 4 + 255) / 256 + 1, 256);
+        hipLaunchKernelGGL(k_gather_d2h, dim3(gx, m), dim3(256), 0, st, a);
+        DX_HIP(hipGetLastError());
+    } else {
+        for (size_t i = 0; i < n; i++) {
+            if (v[i].bytes)
+                DX_HIP(hipMemcpyAsync((char*)c->stage + at, v[i].src, v[i].bytes, hipMemcpyDeviceToHost, st));
+            at += (v[i].bytes + 15) & ~(size_t)15;
+        }
     }
     DX_HIP(hipStreamSynchronize(st));
     at = 0;
@@ -162,6 +215,39 @@ int dx_d2h_many(Ctx* c, const D2H* v, size_t n, hipStream_t st)
         at += (v[i].bytes + 15) & ~(size_t)15;
     }
     return DCCRGX_OK;
+}
+
+__global__ void __launch_bounds__(256) k_ident(uint32_t* __restrict__ out, uint64_t n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = (uint32_t)i;
+}
+
+int ctx_identity(Ctx* c, uint64_t n, uint32_t** out, hipStream_t st)
+{
+    if (n > c->ident_n || !c->ident) {
+        const uint64_t cap = std::max<uint64_t>({n + n / 4, 2 * c->ident_n, 1024});
+        uint32_t* d = nullptr;
+        DX_HIP(dx_malloc(&d, cap * 4));
+        hipLaunchKernelGGL(k_ident, dim3((unsigned)std::min<uint64_t>((cap + 255) / 256, 65536)), dim3(256), 0, st, d,
+                           cap);
+        DX_HIP(hipGetLastError());
+        // other streams read it only after this one (the structural calls end in a synchronisation)
+        if (c->ident) c->ident_old.push_back(c->ident);
+        c->ident = d;
+        c->ident_n = cap;
+    }
+    *out = c->ident;
+    return DCCRGX_OK;
+}
+
+bool ctx_is_identity(const Ctx* c, const void* p)
+{
+    if (!p) return false;
+    if (p == c->ident) return true;
+    for (const uint32_t* q : c->ident_old)
+        if (p == q) return true;
+    return false;
 }
 
 int dx_d2h(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st)
@@ -1086,6 +1172,8 @@ int dccrgx_ctx_destroy(dccrgx_ctx* c)
     hipStreamSynchronize(c->compute);
     hipStreamSynchronize(c->comm);
     dx_cache_streams(c->compute, c->comm, false);
+    dx_free(c->ident);
+    for (uint32_t* q : c->ident_old) dx_free(q);
     dx_cache_trim();
     if (c->has_comm) ncclCommDestroy(c->nccl);
     hipEventDestroy(c->ev_compute);

@@ -71,9 +71,10 @@ __global__ void __launch_bounds__(256) k_bits_set(const uint64_t* __restrict__ l
     }
 }
 
-// rank[w] = number of leaves with id < 64 w (binary search in the ascending list)
+// rank[w] = number of leaves with id < 64 w (binary search in the ascending
+// list), and bits[w] cleared for k_bits_set (no memset launch)
 __global__ void __launch_bounds__(256) k_bits_rank(const uint64_t* __restrict__ leaves, uint64_t n, uint64_t nw,
-                                                   uint32_t* __restrict__ rank)
+                                                   uint32_t* __restrict__ rank, uint64_t* __restrict__ bits)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
@@ -85,6 +86,7 @@ __global__ void __launch_bounds__(256) k_bits_rank(const uint64_t* __restrict__ 
             else hi = mid;
         }
         rank[w] = (uint32_t)lo;
+        bits[w] = 0;
     }
 }
 
@@ -1047,21 +1049,13 @@ static ExView view(const dccrgx_grid* grid)
 
 ExView explicit_view(const dccrgx_grid* grid) { return view(grid); }
 
-__global__ void __launch_bounds__(256) k_counts_to_row(const uint32_t* __restrict__ cnt, uint64_t n,
-                                                       uint64_t* __restrict__ row)
-{
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) row[i + 1] = cnt[i];
-}
-
 // CSR row offsets (n + 1, device, allocated here) of per-row counts on the
 // device; *total (host) = row[n]
 static int scan_counts_device(const uint32_t* d_cnt, uint64_t n, uint64_t** d_row, uint64_t* total, hipStream_t st)
 {
     DX_HIP(ds_malloc(d_row, (n + 1) * 8, st));
-    if (n) hipLaunchKernelGGL(k_counts_to_row, dim3(grid_for(n)), dim3(256), 0, st, d_cnt, n, *d_row);
-    DX_HIP(hipGetLastError());
-    return device_scan_rows(*d_row, n, st, total);
+    DX_TRY(device_scan_counts(d_cnt, n, *d_row, st));
+    return total ? device_scan_rows_total(*d_row, n, st, total) : DCCRGX_OK;
 }
 
 __global__ void __launch_bounds__(256) k_iota(uint32_t* __restrict__ out, uint64_t n)
@@ -1103,8 +1097,10 @@ static int nof_device(dccrgx_grid* grid, const Hood& h, const uint64_t* cells, s
     DX_HIP(hipGetLastError());
     DX_TRY(device_scan_rows(row, n, st, nullptr));
     uint64_t back[2] = {0, 0};  // total, error word: one read-back
-    DX_HIP(hipMemcpyAsync(d_err + 2, row + n, 8, hipMemcpyDeviceToDevice, st));
-    DX_TRY(dx_d2h(grid->ctx, back, d_err, 16, st));
+    {
+        const D2H rb[2] = {{&back[0], d_err, 8}, {&back[1], row + n, 8}};
+        DX_TRY(dx_d2h_many(grid->ctx, rb, 2, st));
+    }
     *total = back[1];
     // a box of leaves cut from a larger grid (hybrid.hip): a window outside
     // the box finds no cell -- an entry of a cell at the box's edge, skipped
@@ -1280,10 +1276,10 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
         E->nwords = nw;
         DX_HIP(ds_malloc(&E->d_bits, nw * 8, st));
         DX_HIP(ds_malloc(&E->d_rank, nw * 4, st));
-        DX_HIP(hipMemsetAsync(E->d_bits, 0, nw * 8, st));
+        hipLaunchKernelGGL(k_bits_rank, dim3(grid_for(nw)), dim3(256), 0, st, E->d_leaves, E->n, nw, E->d_rank,
+                           E->d_bits);
         hipLaunchKernelGGL(k_bits_set, dim3(grid_for(E->n)), dim3(256), 0, st, E->d_leaves, E->n,
                            (unsigned long long*)E->d_bits);
-        hipLaunchKernelGGL(k_bits_rank, dim3(grid_for(nw)), dim3(256), 0, st, E->d_leaves, E->n, nw, E->d_rank);
     } else {
         E->mask = cap - 1;
         DX_HIP(ds_malloc(&E->d_keys, cap * 8, st));
@@ -1320,7 +1316,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
         E->local_g.clear();
         E->slot_of_g.clear();
         E->slot_identity = true;
-        DX_TRY(device_iota(&E->d_local_g, E->n, st));
+        DX_TRY(ctx_identity(ctx, E->n, &E->d_local_g, st));
     } else {
         const std::vector<uint64_t>& L = E->leaves_;
         E->local_g.clear();
@@ -1344,7 +1340,7 @@ int explicit_init(dccrgx_grid* grid, const uint64_t* leaves, size_t n, uint64_t*
     }
     grid->n_local = E->n_local();
     grid->first_local = !grid->n_local ? 0 : E->one_rank ? first_leaf : E->local_[0];
-    DX_TRY(device_iota(&E->d_local_slot, grid->n_local, st));  // local position -> slot: identity
+    DX_TRY(ctx_identity(ctx, grid->n_local, &E->d_local_slot, st));  // local position -> slot: identity
     T.lap("owners+local");
     DX_TRY(sync_slots(grid, true));
     T.lap("sync_slots");
@@ -1370,9 +1366,9 @@ static int sync_slots(dccrgx_grid* grid, bool slot_map_changed)
     hipStream_t st = grid->ctx->compute;
     const uint64_t ns = E->n_slot_ids(), nl = E->n_local();
     if (slot_map_changed || !E->d_slot_of_g) {
-        dx_free(E->d_slot_of_g);
+        if (!ctx_is_identity(grid->ctx, E->d_slot_of_g)) dx_free(E->d_slot_of_g);
         E->d_slot_of_g = nullptr;
-        if (E->slot_identity) DX_TRY(device_iota(&E->d_slot_of_g, E->n, st));  // one rank: leaf g in slot g
+        if (E->slot_identity) DX_TRY(ctx_identity(grid->ctx, E->n, &E->d_slot_of_g, st));  // one rank: leaf g in slot g
         else DX_TRY(upload(grid->ctx, E->slot_of_g, &E->d_slot_of_g, st));
     }
     if (ns > E->d_level_cap || !E->d_level) {
@@ -1572,10 +1568,10 @@ void explicit_free(Explicit* E)
     for (void* q : {(void*)E->d_leaves, (void*)E->d_keys, (void*)E->d_vals, (void*)E->d_bits, (void*)E->d_rank,
                     (void*)E->d_local_g, (void*)E->d_level, (void*)E->d_slot_of_g, (void*)E->d_local_slot,
                     (void*)E->d_ret})
-        fb.add(q);
+        if (!ctx_is_identity(E->ctx, q)) fb.add(q);
     for (auto& kv : E->hl)
         for (void* q : {(void*)kv.second.d_inner_pos, (void*)kv.second.d_outer_pos, (void*)kv.second.d_all_pos})
-            fb.add(q);
+            if (!ctx_is_identity(E->ctx, q)) fb.add(q);
     delete E;
 }
 
@@ -1928,8 +1924,10 @@ static int nof_incremental(dccrgx_grid* grid, Hood& h, const NofHint& H, uint64_
     }
     if ((s = device_scan_rows(h.d_nof_row, R, st, nullptr)) != DCCRGX_OK) return done(s);
     uint64_t back[2] = {0, 0};  // error word, total
-    hipMemcpyAsync(d_err + 2, h.d_nof_row + R, 8, hipMemcpyDeviceToDevice, st);
-    if ((s = dx_d2h(ctx, back, d_err, 16, st)) != DCCRGX_OK) return done(s);
+    {
+        const D2H rb[2] = {{&back[0], d_err, 8}, {&back[1], h.d_nof_row + R, 8}};
+        if ((s = dx_d2h_many(ctx, rb, 2, st)) != DCCRGX_OK) return done(s);
+    }
     if ((back[0] & 0xffffffffu) & (grid->partial_leaves ? ~2u : ~0u))
         return done(set_error(back[0] & 1 ? DCCRGX_ENOTFOUND : DCCRGX_EINTERNAL,
                               back[0] & 1 ? "cell does not exist" : "neighbor more than one level apart"));
@@ -2414,7 +2412,8 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
     T.lap("neighbors_to");
     // per-rank bookkeeping from the device lists (dccrg.hpp:9131-9234, 8729-8891)
     Explicit::HoodLists& L = E->hl[h.id];
-    for (uint32_t* p : {L.d_inner_pos, L.d_outer_pos, L.d_all_pos}) dx_free(p);
+    for (uint32_t* p : {L.d_inner_pos, L.d_outer_pos, L.d_all_pos})
+        if (!ctx_is_identity(ctx, p)) dx_free(p);
     L = Explicit::HoodLists{};
     // host copies of the lists only where host code reads them: the
     // classification of several ranks here; refinement requests and
@@ -2526,7 +2525,7 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
         DX_HIP(ds_malloc(&d_tmp_row, (nl + 1) * 8, st));
         DX_HIP(hipMemcpyAsync(d_tmp_row, h.d_nof_row, (nl + 1) * 8, hipMemcpyDeviceToDevice, st));
         tmp_tot = tot;
-        if (!L.d_all_pos) DX_TRY(device_iota(&L.d_all_pos, nl, st));  // row of local position i: i
+        if (!L.d_all_pos) DX_TRY(ctx_identity(ctx, nl, &L.d_all_pos, st));  // row of local position i: i
         DX_HIP(ds_malloc(&d_pairs, std::max<uint64_t>(tmp_tot, 1) * sizeof(Pair), st));
         DX_HIP(ds_malloc(&d_pc, std::max<uint64_t>(nl, 1) * 4, st));
         RowListBufs RL;
@@ -2592,10 +2591,10 @@ int explicit_build_hood_async(dccrgx_grid* grid, Hood& h, const NofHint* hint)
         h.peers.push_back(std::move(pp));
     }
 
-    if (ctx->comm_size == 1) DX_TRY(device_iota(&L.d_inner_pos, nl, st));  // every cell inner
+    if (ctx->comm_size == 1) DX_TRY(ctx_identity(ctx, nl, &L.d_inner_pos, st));  // every cell inner
     else DX_TRY(upload(grid->ctx, L.inner_pos, &L.d_inner_pos, st));
     DX_TRY(upload(grid->ctx, L.outer_pos, &L.d_outer_pos, st));
-    if (!L.d_all_pos) DX_TRY(device_iota(&L.d_all_pos, nl, st));
+    if (!L.d_all_pos) DX_TRY(ctx_identity(ctx, nl, &L.d_all_pos, st));
     return DCCRGX_OK;
 }
 

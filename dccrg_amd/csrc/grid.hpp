@@ -343,6 +343,8 @@ int amr_host_sync(dccrgx_grid* grid);
 int amr_dev_requests(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results);
 int amr_dev_requests_ex(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, const uint64_t* dev_ids, size_t n,
                         int32_t* results);
+int amr_dev_requests_many(dccrgx_grid* grid, int nk, const int32_t* kinds, const uint64_t* const* ids,
+                          const uint64_t* const* dev_ids, const size_t* counts, int32_t* const* results);
 int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, uint64_t* first_out,
                    std::vector<uint64_t>& leaves_host,
                    std::vector<uint64_t>& retired, std::vector<uint64_t>& nr, bool* changed);
@@ -657,6 +659,9 @@ int amr_ensure_explicit(dccrgx_grid* grid);
 // (counts in row[1..n] -> row pointers, row[0] = 0, *total = row[n] if given)
 int device_inclusive_scan(uint64_t* x, uint64_t m, hipStream_t st);
 int device_scan_rows(uint64_t* row, uint64_t n, hipStream_t st, uint64_t* total);
+// row[0] = 0, row[i + 1] = cnt[0] + ... + cnt[i] (row: n + 1 entries)
+int device_scan_counts(const uint32_t* cnt, uint64_t n, uint64_t* row, hipStream_t st);
+int device_scan_rows_total(const uint64_t* row, uint64_t n, hipStream_t st, uint64_t* total);
 int launch_gather_ext(const void* src, const uint64_t* idx, uint64_t n, uint32_t elem, void* dst,
                       hipStream_t st);
 int launch_scatter_ext(const void* src, const uint64_t* sidx, const uint64_t* didx, uint64_t n,

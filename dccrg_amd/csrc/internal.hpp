@@ -497,9 +497,17 @@ struct Ctx {
     // a communicator
     dccrgx_host_transport host_tx{};
     bool has_host_tx = false;
-    // pinned bounce buffer of dx_h2d / dx_d2h
+    // pinned bounce buffer of dx_h2d / dx_d2h, and its device address (small
+    // read-backs are gathered into it by one kernel, dx_d2h_many)
     void* stage = nullptr;
+    void* stage_dev = nullptr;
     size_t stage_bytes = 0;
+    // 0, 1, 2, ... on the device, shared by the identity maps of one-rank
+    // grids (local position = leaf = slot); grown geometrically, the smaller
+    // arrays kept until the context goes (grids may still point into them)
+    uint32_t* ident = nullptr;
+    uint64_t ident_n = 0;
+    std::vector<uint32_t*> ident_old;
     // pinned upload slots of dx_h2d_async: slot k is reused once the event
     // recorded after its copy has passed
     static constexpr int UP_SLOTS = 16;
@@ -549,7 +557,9 @@ int dx_d2h(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st);
 // after it by the caller (the structural calls end in a synchronisation).
 // Larger copies and other streams take dx_h2d.
 int dx_h2d_async(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st);
-// several device -> host copies behind one synchronisation
+// several device -> host copies behind one synchronisation; small ones (at
+// most 16 ranges, 1 MiB together) are one gather kernel writing the pinned
+// stage (a runtime copy of pinned memory is a launch of its own per range)
 struct D2H {
     void* dst;
     const void* src;
@@ -565,6 +575,10 @@ struct Fill {
     uint8_t value;
 };
 int dx_fill_many(const Fill* v, int n, hipStream_t st);
+// the context's identity array, at least n entries (one launch when it grows)
+int ctx_identity(Ctx* c, uint64_t n, uint32_t** out, hipStream_t st);
+// p is (in) one of the context's identity arrays: not to be freed
+bool ctx_is_identity(const Ctx* c, const void* p);
 
 }  // namespace dccrgx
 
