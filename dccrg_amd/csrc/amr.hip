@@ -469,7 +469,9 @@ int rebuild_prepare(dccrgx_grid* grid, std::vector<uint64_t>& leaves, const std:
         if (launch_move_many(src.data(), np.data(), elem.data(), src.size(), d_from, ns, st) != DCCRGX_OK)
             return fail(DCCRGX_EHIP);
     }
-    if (hipStreamSynchronize(st) != hipSuccess) return fail(set_error(DCCRGX_EHIP, "moving field data failed"));
+    if (hipGetLastError() != hipSuccess) return fail(set_error(DCCRGX_EHIP, "moving field data failed"));
+    // no wait here: the moves stay queued before the commit's and the next
+    // call's work on the stream, and d_from's free below is fenced by events
     dx_free(d_from);
     // the new state goes aside; the grid is the old one until the commit
     t.ex = grid->ex;

@@ -301,19 +301,28 @@ __device__ inline bool a_item_blocks(const AView& a, const uint64_t pi[3], int p
         wi[d] = (uint64_t)x;
     }
     const uint64_t W = map_cell(mp, wi, pl);
-    if (ex_find(a.v, W) >= 0) return false;                                      // a leaf of the parent's level
-    if (pl > 0 && ex_find(a.v, map_cell(mp, wi, pl - 1)) >= 0) return false;  // coarser
+    // W and its parent looked up together, then W's eight children together
+    // and their flags together: three dependent lookups, not up to eighteen
+    const int64_t gw = ex_find(a.v, W);
+    const int64_t gp = pl > 0 ? ex_find(a.v, map_cell(mp, wi, pl - 1)) : -1;
+    if (gw >= 0) return false;  // a leaf of the parent's level
+    if (gp >= 0) return false;  // coarser
     for (int l = pl - 2; l >= 0; l--)  // covered by a coarser ancestor: no leaf inside W
         if (ex_find(a.v, map_cell(mp, wi, l)) >= 0) return false;
     if (pl >= M) return false;
     uint64_t ch[8];
     a_children(a, W, ch);
-    for (int j = 0; j < 8; j++) {
-        const int64_t gc = ex_find(a.v, ch[j]);
-        if (gc < 0) return true;                   // refined: leaves at plvl + 2 or finer
-        if (a.flags[gc] & RF_REFINE) return true;  // plvl + 1 and about to be refined
-    }
-    return false;
+    int64_t gc[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) gc[j] = ex_find(a.v, ch[j]);
+    bool refined = false;  // a child that is not a leaf: leaves at plvl + 2 or finer
+#pragma unroll
+    for (int j = 0; j < 8; j++) refined |= gc[j] < 0;
+    if (refined) return true;
+    uint32_t f = 0;  // plvl + 1 and about to be refined
+#pragma unroll
+    for (int j = 0; j < 8; j++) f |= a.flags[gc[j]];
+    return (f & RF_REFINE) != 0;
 }
 
 // unrefine_completely, dccrg.hpp:2596-2675, phase 1 (reads the flags only).
@@ -1338,13 +1347,22 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     uint64_t nk[2] = {0, 0}, first_leaf = 0;
     uint32_t ngone = 0;
     int e = DCCRGX_OK;
-    {
-        const D2H c2[3] = {{nk, d_cnt64, 16}, {&ngone, d_ngone, 4}, {&first_leaf, d_new, 8}};
+    const D2H c2[3] = {{nk, d_cnt64, 16}, {&ngone, d_ngone, 4}, {&first_leaf, d_new, 8}};
+    const D2H l1[4] = {{nr.data(), d_nr, cnt[4] * 8ull},
+                       {A.new_cells.data(), d_all + off_ls[0], cnt[1] * 8ull},
+                       {A.removed.data(), d_all + off_ls[1], cnt[2] * 8ull},
+                       {retired.data(), d_all + off_ls[2], cnt[3] * 8ull}};
+    if (!host_list) {  // one rank: the counts and the lists (sized by the first read-back) in one read-back
+        D2H all[7];
+        std::copy(c2, c2 + 3, all);
+        std::copy(l1, l1 + 4, all + 3);
+        e = dx_d2h_many(ctx, all, 7, st);
+    } else {
         e = dx_d2h_many(ctx, c2, 3, st);
     }
     std::vector<uint64_t> added(host_list ? nk[1] : 0);
     std::vector<uint32_t> gone(host_list ? ngone : 0);
-    if (e == DCCRGX_OK) {
+    if (e == DCCRGX_OK && host_list) {
         const D2H l2[6] = {{nr.data(), d_nr, cnt[4] * 8ull},
                            {A.new_cells.data(), d_all + off_ls[0], cnt[1] * 8ull},
                            {A.removed.data(), d_all + off_ls[1], cnt[2] * 8ull},
@@ -1513,57 +1531,53 @@ __global__ void __launch_bounds__(256) k_copy_from_parents(SlotView sv, MapParam
 
 // adapter.hpp:253-300: the parent of removed cells is 0, then += child / 8
 // over its removed children in ascending order (the first removed child of
-// each parent does the sum; `removed` ascending)
+// each parent does the sum; `removed` ascending).  Eight lanes per removed
+// cell, lane k on the parent's child k (x fastest: ascending ids): the
+// children's entries in the retired cells' table (removed cells are retired
+// and marked there) are probed together, the values gathered together and
+// summed by lane 0 of the group in child order, as the reference adds them.
 __global__ void __launch_bounds__(256) k_average_children(SlotView sv, MapParams mp, const uint64_t* __restrict__ removed,
                                                           uint64_t n, FieldSet fs, int32_t* __restrict__ err)
 {
 #pragma clang fp contract(off)
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t c = removed[i];
-        uint64_t idx[3];
-        int l;
-        map_indices(mp, c, idx, &l);
-        const uint64_t par = map_cell(mp, idx, l - 1);
-        uint64_t pi[3];
-        int pl;
-        map_indices(mp, par, pi, &pl);
-        const uint64_t h = (uint64_t)1 << (mp.max_lvl - l);
-        uint64_t ch[8];
-        for (int k = 0; k < 8; k++) {  // x fastest: ascending ids
+    const int lane = threadIdx.x & 63, k = lane & 7, g0 = lane & ~7;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    // wave-uniform trip count (the shuffles need every lane)
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x - lane); base < 8 * n; base += stride) {
+        const uint64_t i = (base + lane) >> 3;
+        const bool valid = i < n;
+        uint64_t c = 0, par = 0, ch = 0, ent = ~0ull;
+        if (valid) {
+            c = removed[i];
+            uint64_t idx[3];
+            int l;
+            map_indices(mp, c, idx, &l);
+            par = map_cell(mp, idx, l - 1);
+            uint64_t pi[3];
+            int pl;
+            map_indices(mp, par, pi, &pl);
+            const uint64_t h = (uint64_t)1 << (mp.max_lvl - l);
             const uint64_t ci[3] = {pi[0] + (k & 1) * h, pi[1] + ((k >> 1) & 1) * h, pi[2] + ((k >> 2) & 1) * h};
-            ch[k] = map_cell(mp, ci, l);
+            ch = map_cell(mp, ci, l);
+            ent = ret_entry(sv, ch);
         }
-        // the first removed child of the parent does the sum, over the
-        // parent's removed children in ascending order.  Membership in the
-        // removed list and the children's slots come from the retired cells'
-        // table (removed cells are retired and marked there): eight
-        // independent probes instead of binary searches of the list
-        uint64_t ent[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) ent[k] = ret_entry(sv, ch[k]);
-        bool first = true;
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (ch[k] < c && ent[k] != ~0ull && (ent[k] & RET_REMOVED)) first = false;
-        if (!first) continue;
-        const int64_t ps = slot_lookup(sv, par);
-        if (ps < 0) {
-            atomicOr(err, 1);
-            continue;
-        }
-        int64_t cs[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const bool in = ch[k] >= c && ent[k] != ~0ull && (ent[k] & RET_REMOVED);
-            cs[k] = in ? (int64_t)(ent[k] & ~RET_REMOVED) : -2;
-        }
+        const bool rem = ent != ~0ull && (ent & RET_REMOVED);
+        // the first removed child of the parent does the sum
+        const bool first = ((__ballot(valid && rem && ch < c) >> g0) & 0xffull) == 0 && valid;
+        const int64_t ps = first ? slot_lookup(sv, par) : -1;
+        if (first && ps < 0 && k == 0) atomicOr(err, 1);
+        const bool in = first && ps >= 0 && rem && ch >= c;
+        const int64_t cs = in ? (int64_t)(ent & ~RET_REMOVED) : -1;
+        const uint64_t inmask = (__ballot(in) >> g0) & 0xffull;
         for (int f = 0; f < fs.n; f++) {
             double* d = reinterpret_cast<double*>(fs.p[f]);
+            const double q = in ? d[cs] / 8 : 0.0;
             double acc = 0;
-            for (int k = 0; k < 8; k++)
-                if (cs[k] >= 0) acc += d[cs[k]] / 8;
-            d[ps] = acc;
+            for (int j = 0; j < 8; j++) {
+                const double v = __shfl(q, g0 + j, 64);
+                if (inmask >> j & 1) acc += v;
+            }
+            if (k == 0 && first && ps >= 0) d[ps] = acc;
         }
     }
 }
@@ -1611,7 +1625,7 @@ static int run_rules(dccrgx_grid* grid, const std::vector<uint64_t>* new_cells, 
         hipLaunchKernelGGL(k_copy_from_parents, dim3(blocks(nn)), dim3(256), 0, st, sv, grid->map,
                            (const uint64_t*)d_cells, (uint64_t)nn, fs, d_err);
     for (const FieldSet& fs : avg_sets)  // after the copies (the reference's order, adapter.hpp:229-300)
-        hipLaunchKernelGGL(k_average_children, dim3(blocks(nr)), dim3(256), 0, st, sv, grid->map,
+        hipLaunchKernelGGL(k_average_children, dim3(blocks(8 * (uint64_t)nr)), dim3(256), 0, st, sv, grid->map,
                            (const uint64_t*)d_cells + nn, (uint64_t)nr, fs, d_err);
     DX_HIP(hipGetLastError());
     int32_t err = 0;

@@ -899,8 +899,10 @@ class Dccrg:
     # ---- halo (dccrg.hpp:978-1014, 5046-5413) --------------------------------
     def update_copies_of_remote_neighbors(self, hood: int = DEFAULT_NEIGHBORHOOD_ID, fields=None):
         f = self._fids(fields)
+        # no device-wide wait: the ghosts' writes are queued on the library's
+        # compute stream (dccrgx_halo_wait orders it after the exchange), where
+        # every later read of the fields runs
         check(lib().dccrgx_halo_update(self._h, hood, f.ctypes.data_as(X._i32p), f.size))
-        self.ctx.synchronize()
         # quirk kept: with the default id the reference returns false (dccrg.hpp:1001-1003)
         return hood != DEFAULT_NEIGHBORHOOD_ID
 
