@@ -324,23 +324,28 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, dou
         for (uint64_t s = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < t1; s += stride) rho_out[s] = p.rho[s];
 }
 
-// check_for_adaptation, tests/advection/adapter.hpp:66-103: max relative
-// density difference over the adapter's face neighbors, maximised into both
-// cells of a pair when the neighbor is local (atomic max on the bit pattern
-// of a non-negative double)
+// check_for_adaptation, tests/advection/adapter.hpp:66-103, and the marks of
+// :114-118 in one pass.  The reference maximises each face pair's relative
+// density difference into both cells (the neighbor's when it is local); the
+// face test on the offsets and the difference are symmetric in the pair and
+// a face neighbor's row holds the cell too, so every local cell takes the
+// maximum over its own row's faces: no atomics, no cleared array, no second
+// launch.
 __global__ void __launch_bounds__(256) k_adapt_diff(const double* __restrict__ rho, const uint64_t* __restrict__ st_row,
                                                     const uint32_t* __restrict__ st_slot,
                                                     const int32_t* __restrict__ st_off,
                                                     const uint32_t* __restrict__ local_g,
-                                                    const uint8_t* __restrict__ level, int M, uint64_t n,
-                                                    const uint8_t* __restrict__ slot_local, double thr,
-                                                    unsigned long long* __restrict__ maxd)
+                                                    const uint8_t* __restrict__ level, int M, uint64_t n, double thr,
+                                                    double inc, double sens, int8_t* __restrict__ marks,
+                                                    double* __restrict__ out)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
         const uint32_t c = local_g[q];
-        const int64_t lc = 1ll << (M - level[c]);
+        const int lv = level[c];
+        const int64_t lc = 1ll << (M - lv);
         const double rc = rho[c];
+        double m = 0.0;  // max_diff = 0 (:62-64)
         // (rows of a few face entries: the four-wide row walk measured slower here)
         for (uint64_t e = st_row[q]; e < st_row[q + 1]; e++) {
             const uint32_t nb = st_slot[e];
@@ -351,29 +356,12 @@ __global__ void __launch_bounds__(256) k_adapt_diff(const double* __restrict__ r
             if (!face) continue;
             const double rn = rho[nb];
             const double diff = fabs(rc - rn) / ((rc < rn ? rc : rn) + thr);
-            // the bit pattern orders like the value only for diff >= 0; a
-            // non-positive diff never raises the reference's max from 0
-            if (!(diff > 0.0)) continue;
-            const unsigned long long k = (unsigned long long)__double_as_longlong(diff);
-            atomicMax(&maxd[c], k);
-            if (slot_local[nb]) atomicMax(&maxd[nb], k);
+            if (diff > m) m = diff;  // a non-positive or NaN diff never raises it
         }
-    }
-}
-
-__global__ void __launch_bounds__(256) k_adapt_marks(const unsigned long long* __restrict__ maxd,
-                                                     const uint32_t* __restrict__ local_g,
-                                                     const uint8_t* __restrict__ level, uint64_t n, double inc,
-                                                     double sens, int8_t* __restrict__ marks, double* __restrict__ out)
-{
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
-        const uint32_t c = local_g[q];
-        const double diff = __longlong_as_double((long long)maxd[c]);
         // adapter.hpp:114-118
-        const double refine_diff = (level[c] + 1) * inc, unrefine_diff = sens * refine_diff;
-        marks[q] = diff > refine_diff ? 2 : (diff >= unrefine_diff ? 1 : 0);
-        out[q] = diff;
+        const double refine_diff = (lv + 1) * inc, unrefine_diff = sens * refine_diff;
+        marks[q] = m > refine_diff ? 2 : (m >= unrefine_diff ? 1 : 0);
+        if (out) out[q] = m;
     }
 }
 
@@ -423,13 +411,6 @@ __global__ void __launch_bounds__(256) k_adapt_codes(ExView v, const uint64_t* _
         }
         code[q] = m == 2 ? 1 : (m == 1 ? ((!g_ref && !earlier_keep) ? 2 : 0) : ((!g_ref && !g_keep) ? 3 : 0));
     }
-}
-
-__global__ void __launch_bounds__(256) k_flag_slots(const uint32_t* __restrict__ local_g, uint64_t n,
-                                                    uint8_t* __restrict__ flag)
-{
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) flag[local_g[q]] = 1;
 }
 
 // uniform grids: the face neighbors present in the neighborhood (mask bit
@@ -833,29 +814,15 @@ int adapt_marks_device(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_f
     ExRegion R;
     DX_TRY(explicit_region(grid, *h, DCCRGX_REGION_ALL, &R));
     hipStream_t st = grid->ctx->compute;
-    unsigned long long* d_max = nullptr;
-    uint8_t* d_flag = nullptr;
     int8_t* d_marks = nullptr;
     double* d_diff = nullptr;
-    const uint64_t ns = grid->n_slots;
-    DX_HIP(dx_malloc(&d_max, ns * 8));
-    DX_HIP(dx_malloc(&d_flag, ns));
     DX_HIP(dx_malloc(&d_marks, n));
-    DX_HIP(dx_malloc(&d_diff, n * 8));
-    {
-        const Fill z[2] = {{d_max, ns * 8, 0}, {d_flag, ns, 0}};  // max_diff = 0 (:62-64)
-        DX_TRY(dx_fill_many(z, 2, st));
-    }
-    hipLaunchKernelGGL(k_flag_slots, dim3(grid_for(n)), dim3(256), 0, st, R.local_slot, n, d_flag);
+    if (max_diff_out) DX_HIP(dx_malloc(&d_diff, n * 8));
     hipLaunchKernelGGL(k_adapt_diff, dim3(grid_for(n)), dim3(256), 0, st, p.rho, h->d_st_row, h->d_st_slot,
-                       h->d_st_off, R.local_slot, R.level, grid->map.max_lvl, n, (const uint8_t*)d_flag,
-                       diff_threshold, d_max);
-    hipLaunchKernelGGL(k_adapt_marks, dim3(grid_for(n)), dim3(256), 0, st, (const unsigned long long*)d_max,
-                       R.local_slot, R.level, n, diff_increase, unrefine_sensitivity, d_marks, d_diff);
+                       h->d_st_off, R.local_slot, R.level, grid->map.max_lvl, n, diff_threshold, diff_increase,
+                       unrefine_sensitivity, d_marks, d_diff);
     DX_HIP(hipGetLastError());
     if (max_diff_out) DX_TRY(dx_d2h(grid->ctx, max_diff_out, d_diff, n * 8, st));
-    dx_free(d_max);  // dx_free waits for the kernels above
-    dx_free(d_flag);
     dx_free(d_diff);
     *d_marks_out = d_marks;
     return DCCRGX_OK;

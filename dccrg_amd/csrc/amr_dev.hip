@@ -39,7 +39,6 @@ enum : uint32_t {
     RF_NOT_REFINE = 8u,
     RF_GONE = 16u,   // execute: the leaf disappears
     RF_KEEP = 32u,   // override_unrefines: the walk of this group / cell passed
-    RF_FINAL = 64u,  // override_unrefines: the unrefinement happens
 };
 constexpr uint32_t RF_SETS = RF_REFINE | RF_UNREFINE | RF_NOT_UNREFINE | RF_NOT_REFINE;
 static_assert(RF_GONE == AMR_FLAG_GONE, "the rebuild reads the gone flag (grid.hpp)");
@@ -697,17 +696,6 @@ __global__ void __launch_bounds__(256) k_ou_check(AView a, const uint32_t* __res
     }
 }
 
-__global__ void __launch_bounds__(256) k_ou_final(AView a, const uint32_t* __restrict__ us, const uint32_t* __restrict__ nu,
-                                                  const uint32_t* __restrict__ key)
-{
-    const uint32_t n = *nu;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t g = us[i], k = key[i];
-        if (a.flags[k != NONE32 ? k : g] & RF_KEEP) atomicOr(&a.flags[g], RF_FINAL);
-    }
-}
-
 // execute_refines, dccrg.hpp:10243-10693: children of refined leaves and
 // parents of unrefined groups are added; refined leaves and every child of an
 // unrefined parent go.  Local ones are reported (new / removed / retired).
@@ -718,7 +706,8 @@ struct ExecOut {
     uint64_t* newc;
     uint64_t* removed;
     uint64_t* retired;
-    uint32_t* cnt;  // added, new, removed, retired
+    uint64_t* nr;
+    uint32_t* cnt;  // added, new, removed, retired, nr
 };
 
 __global__ void __launch_bounds__(256) k_exec(AView a, const uint32_t* __restrict__ grp, ExecOut o)
@@ -726,6 +715,10 @@ __global__ void __launch_bounds__(256) k_exec(AView a, const uint32_t* __restric
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
         const uint32_t f = a.flags[g];
+        const bool unref = (f & RF_UNREFINE) != 0, nr = (f & RF_NOT_REFINE) != 0;
+        // most waves hold no request at all (active lanes agree: the
+        // reservations below need every active lane)
+        if (!__ballot((f & RF_REFINE) || unref || nr)) continue;
         const uint64_t c = a.leaves[g];
         // what this leaf adds: children of a refined leaf; the parent of an
         // unrefined group (by its walker, or by a lone request)
@@ -733,14 +726,24 @@ __global__ void __launch_bounds__(256) k_exec(AView a, const uint32_t* __restric
         const bool ref_local = ref && a_owner(a, c) == a.rank;
         bool fin = false, fin_local = false;
         uint64_t par = 0, ch[8];
-        if (f & RF_FINAL) {
+        int64_t gc[8];
+        if (unref) {
+            // override_unrefines' outcome: k_ou_check / k_ou_walk kept the
+            // group (on its first child's flags when every child is a leaf)
+            // or the lone request (on its own)
             par = a_parent(a, c);
             a_children(a, par, ch);
-            const int64_t g0 = ch[0] ? ex_find(a.v, ch[0]) : -1;
             bool all = true;
-            for (int k = 0; k < 8 && all; k++) all = ch[k] && ex_find(a.v, ch[k]) >= 0;
-            fin = !(all && grp[(uint32_t)g0] != (uint32_t)g);  // the group's walker does it
-            fin_local = fin && a_owner(a, par) == a.rank;       // the children's process too
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                gc[k] = ch[k] ? ex_find(a.v, ch[k]) : -1;
+                all &= gc[k] >= 0;
+            }
+            const uint32_t g0 = (uint32_t)gc[0];
+            if (a.flags[all ? g0 : (uint32_t)g] & RF_KEEP) {
+                fin = !(all && grp[g0] != (uint32_t)g);        // the group's walker does it
+                fin_local = fin && a_owner(a, par) == a.rank;  // the children's process too
+            }
         }
         uint32_t nch = 0;
         if (fin_local)
@@ -749,6 +752,9 @@ __global__ void __launch_bounds__(256) k_exec(AView a, const uint32_t* __restric
         const uint32_t p_new = wave_reserve(&o.cnt[1], ref_local ? 8u : 0u);
         const uint32_t p_rem = wave_reserve(&o.cnt[2], nch);
         uint32_t p_ret = wave_reserve(&o.cnt[3], (ref_local ? 1u : 0u) + nch);
+        // dont_refine ids that persist (:10178): leaves with the flag
+        const uint32_t p_nr = wave_reserve(&o.cnt[4], nr ? 1u : 0u);
+        if (nr) o.nr[p_nr] = c;
         if (ref) {
             atomicOr(&a.flags[g], RF_GONE);
             uint64_t cc[8];
@@ -764,32 +770,13 @@ __global__ void __launch_bounds__(256) k_exec(AView a, const uint32_t* __restric
         uint32_t w = 0;
         for (int k = 0; k < 8; k++) {
             if (!ch[k]) continue;
-            const int64_t gc = ex_find(a.v, ch[k]);
-            if (gc >= 0) atomicOr(&a.flags[gc], RF_GONE);
+            if (gc[k] >= 0) atomicOr(&a.flags[gc[k]], RF_GONE);
             if (fin_local) {
                 o.removed[p_rem + w] = ch[k];
                 o.retired[p_ret + w] = ch[k];
                 w++;
             }
         }
-    }
-}
-
-__global__ void __launch_bounds__(256) k_kept_flags(AView a, uint8_t* __restrict__ keep)
-{
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride)
-        keep[g] = (a.flags[g] & RF_GONE) ? 0 : 1;
-}
-
-// dont_refine ids that persist (:10178): leaves with the flag
-__global__ void __launch_bounds__(256) k_nr_ids(AView a, uint64_t* __restrict__ out, uint32_t* __restrict__ cnt)
-{
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
-        const bool hit = (a.flags[g] & RF_NOT_REFINE) != 0;
-        const uint32_t p = wave_reserve(cnt, hit ? 1u : 0u);
-        if (hit) out[p] = a.leaves[g];
     }
 }
 
@@ -818,8 +805,12 @@ __global__ void __launch_bounds__(256) k_merge(const uint64_t* __restrict__ a, c
 }
 
 // a leaf goes: its keep flag is clear (the ordered selection of their indices)
-struct NotKept {
-    __host__ __device__ bool operator()(uint8_t k) const { return k == 0; }
+// the leaves that stay / go, read straight from the decision flags
+struct Kept {
+    __host__ __device__ bool operator()(uint32_t f) const { return (f & RF_GONE) == 0; }
+};
+struct Gone {
+    __host__ __device__ bool operator()(uint32_t f) const { return (f & RF_GONE) != 0; }
 };
 
 // new = (old without the leaves at `gone`, ascending) merged with `added`
@@ -1222,20 +1213,17 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
                                (uint32_t*)nullptr, (uint32_t*)nullptr, d_err);
         }
     }
-    hipLaunchKernelGGL(k_ou_final, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_fa, (const uint32_t*)cu,
-                       (const uint32_t*)d_key);
-    // execute_refines
+    // execute_refines (with override_unrefines' outcome and the persisting
+    // dont_refine ids)
     ExecOut o;
     DX_TRY(S.get(&o.added, 8 * N + 8));
     DX_TRY(S.get(&o.newc, 8 * N + 8));
     DX_TRY(S.get(&o.removed, 8 * N + 8));
     DX_TRY(S.get(&o.retired, 9 * N + 8));
-    o.cnt = d_cnt + 2 * (M + 2) + 1;  // 4 counters
+    DX_TRY(S.get(&o.nr, N));
+    uint64_t* d_nr = o.nr;
+    o.cnt = d_cnt + 2 * (M + 2) + 1;  // 5 counters
     hipLaunchKernelGGL(k_exec, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_grp, o);
-    uint64_t* d_nr;
-    DX_TRY(S.get(&d_nr, N));
-    uint32_t* nr_cnt = o.cnt + 4;
-    hipLaunchKernelGGL(k_nr_ids, dim3(bN), dim3(256), 0, st, a, d_nr, nr_cnt);
     DX_HIP(hipGetLastError());
     uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
     int32_t err = 0;
@@ -1270,9 +1258,7 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
         return DCCRGX_OK;
     }
     // the new leaf list: surviving leaves in order, merged with the sorted new ones
-    uint8_t* d_keep;
     uint64_t *d_kept, *d_cnt64;
-    DX_TRY(S.get(&d_keep, N));
     DX_TRY(S.get(&d_kept, N));
     DX_TRY(S.get(&d_cnt64, 2));
     // the new ids and the new / removed / retired lists sorted on the device
@@ -1299,9 +1285,9 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     uint32_t* d_gone;
     DX_TRY(S.get(&d_gone, N));
     uint32_t* d_ngone = d_cnt + NC - 3;
-    hipLaunchKernelGGL(k_kept_flags, dim3(bN), dim3(256), 0, st, a, d_keep);
+    const hipcub::TransformInputIterator<bool, Kept, const uint32_t*> d_keep(a.flags, Kept{});
     const hipcub::CountingInputIterator<uint32_t> leaf_idx(0);
-    const hipcub::TransformInputIterator<bool, NotKept, const uint8_t*> gone_flags(d_keep, NotKept{});
+    const hipcub::TransformInputIterator<bool, Gone, const uint32_t*> gone_flags(a.flags, Gone{});
     size_t tb[4] = {0, 0, 0, 0};
     DX_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb[0], a.leaves, d_keep, d_kept, d_cnt64, (int)N, st));
     DX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb[1], d_keys, d_all, (int)n_all, 0, sort_bits, st));
