@@ -84,6 +84,11 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $out/adapt_trace -o run -- python3 tools/adapt_loop.py > $out/adapt_trace.log 2>&1 || fail adapt_trace $? $out/adapt_trace.log
       python3 tools/api_census.py $out/adapt_trace > $out/adapt_census.txt 2>&1 || true
       head -n 30 $out/adapt_census.txt ;;
+    adaptbigprof)
+      # the 3.5 M-leaf loop: a kernel + HIP-runtime trace and its census
+      ADAPT_N=1600 ADAPT_REL=0.006 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $out/adapt_big_trace -o run -- python3 tools/adapt_loop.py > $out/adapt_big_trace.log 2>&1 || fail adapt_big_trace $? $out/adapt_big_trace.log
+      python3 tools/api_census.py $out/adapt_big_trace > $out/adapt_big_census.txt 2>&1 || true
+      head -n 30 $out/adapt_big_census.txt ;;
     adaptinc)
       # the 218k loop with the incremental list rebuild forced on, then off
       ADAPT_INCREMENTAL=1 timeout -k 10 300 python -u tools/adapt_loop.py > $out/adapt_inc1.log 2>&1 || fail adapt_inc1 $? $out/adapt_inc1.log
