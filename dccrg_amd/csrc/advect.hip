@@ -365,6 +365,63 @@ __global__ void __launch_bounds__(256) k_adapt_diff(const double* __restrict__ r
     }
 }
 
+// k_adapt_diff and k_face_build in one walk of the rows (the rows are most
+// of both kernels' bytes: 4 + 12 B per entry), when the solver's face lists
+// are stale -- after every rebuild of an adaptive run.  Each entry feeds the
+// face lists (face_dir: a shared face) and the adaptation maximum (the
+// reference's offset test, a subset of those) as the two kernels do.
+__global__ void __launch_bounds__(256) k_adapt_faces(const double* __restrict__ rho, const uint64_t* __restrict__ st_row,
+                                                     const uint32_t* __restrict__ st_slot,
+                                                     const int32_t* __restrict__ st_off,
+                                                     const uint32_t* __restrict__ local_g,
+                                                     const uint8_t* __restrict__ level, int M, uint64_t n, double thr,
+                                                     double inc, double sens, int8_t* __restrict__ marks,
+                                                     double* __restrict__ out, uint32_t* __restrict__ ell_slot,
+                                                     uint32_t* __restrict__ o_cnt, uint32_t* __restrict__ o_slot,
+                                                     int8_t* __restrict__ o_dir, uint32_t* __restrict__ over)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        const uint32_t c = local_g[q];
+        const int lv = level[c];
+        const int64_t lc = 1ll << (M - lv);
+        const double rc = rho[c];
+        double m = 0.0;  // max_diff = 0 (:62-64)
+        uint32_t used = 0, k = 0;
+        const uint64_t base = st_row[q];
+        row_walk4(base, st_row[q + 1], st_slot, st_off, [&](uint64_t, uint32_t nb, int32_t x, int32_t y, int32_t z) {
+            const int64_t ln = 1ll << (M - level[nb]);
+            const int32_t o[3] = {x, y, z};
+            const int dir = face_dir(lc, ln, o);
+            if (!dir) return;  // the adaptation's faces are face_dir faces too
+            const bool aface = ((x == lc || x == -ln) && y == 0 && z == 0) ||
+                               ((y == lc || y == -ln) && x == 0 && z == 0) || ((z == lc || z == -ln) && x == 0 && y == 0);
+            if (aface) {
+                const double rn = rho[nb];
+                const double diff = fabs(rc - rn) / ((rc < rn ? rc : rn) + thr);
+                if (diff > m) m = diff;
+            }
+            const int col = 2 * ((dir > 0 ? dir : -dir) - 1) + (dir > 0 ? 1 : 0);
+            if (!(used >> col & 1u)) {
+                used |= 1u << col;
+                ell_slot[col * n + q] = nb;
+                return;
+            }
+            o_slot[base + k] = nb;
+            o_dir[base + k] = (int8_t)dir;
+            k++;
+        });
+        for (int col = 0; col < 6; col++)
+            if (!(used >> col & 1u)) ell_slot[col * n + q] = 0xffffffffu;
+        o_cnt[q] = k;
+        if (__ballot(k > 0) && (threadIdx.x & 63) == 0) atomicOr(over, 1u);
+        // adapter.hpp:114-118
+        const double refine_diff = (lv + 1) * inc, unrefine_diff = sens * refine_diff;
+        marks[q] = m > refine_diff ? 2 : (m >= unrefine_diff ? 1 : 0);
+        if (out) out[q] = m;
+    }
+}
+
 // adapter.hpp:109-176 per sibling group.  The reference's loop inserts and
 // erases while it walks the local cells; its outcome per group is: refine
 // every cell marked 2; if any sibling is marked 2 nothing else; else keep
@@ -606,15 +663,11 @@ void uniform_local_run(const dccrgx_grid* grid, uint64_t* s0, uint64_t* n)
 }
 
 
-// build the face lists of a neighborhood's local cells (explicit grids):
-// one pass, no synchronisation
-int build_faces(const dccrgx_grid* grid, Hood& h)
+// the face lists' storage for n local cells of a neighborhood, the overflow
+// flag cleared (stream order)
+int alloc_faces(const Hood& h, uint64_t n, hipStream_t st, std::shared_ptr<FaceCache>& out)
 {
-    ExRegion R;
-    DX_TRY(explicit_region(grid, h, DCCRGX_REGION_ALL, &R));
-    hipStream_t st = grid->ctx->compute;
     auto fc = std::make_shared<FaceCache>();
-    const uint64_t n = R.n;
     fc->n = n;
     const size_t m = std::max<uint64_t>(n, 1), cap = std::max<uint64_t>(h.st_cap, 1);
     DX_HIP(dx_malloc(&fc->ell_slot, 6 * m * 4));
@@ -623,7 +676,22 @@ int build_faces(const dccrgx_grid* grid, Hood& h)
     DX_HIP(dx_malloc(&fc->o_dir, cap));
     DX_HIP(dx_malloc(&fc->d_over, 4));
     fc->o_base = h.d_st_row;
-    DX_HIP(hipMemsetAsync(fc->d_over, 0, 4, st));
+    const Fill z[1] = {{fc->d_over, 4, 0}};
+    DX_TRY(dx_fill_many(z, 1, st));
+    out = std::move(fc);
+    return DCCRGX_OK;
+}
+
+// build the face lists of a neighborhood's local cells (explicit grids):
+// one pass, no synchronisation
+int build_faces(const dccrgx_grid* grid, Hood& h)
+{
+    ExRegion R;
+    DX_TRY(explicit_region(grid, h, DCCRGX_REGION_ALL, &R));
+    hipStream_t st = grid->ctx->compute;
+    std::shared_ptr<FaceCache> fc;
+    const uint64_t n = R.n;
+    DX_TRY(alloc_faces(h, n, st, fc));
     const int M = grid->map.max_lvl;
     if (n)
         hipLaunchKernelGGL(k_face_build, dim3(grid_for(n)), dim3(256), 0, st, h.d_st_row, h.d_st_slot, h.d_st_off,
@@ -818,9 +886,19 @@ int adapt_marks_device(dccrgx_grid* grid, int32_t hood_id, const dccrgx_advect_f
     double* d_diff = nullptr;
     DX_HIP(dx_malloc(&d_marks, n));
     if (max_diff_out) DX_HIP(dx_malloc(&d_diff, n * 8));
-    hipLaunchKernelGGL(k_adapt_diff, dim3(grid_for(n)), dim3(256), 0, st, p.rho, h->d_st_row, h->d_st_slot,
-                       h->d_st_off, R.local_slot, R.level, grid->map.max_lvl, n, diff_threshold, diff_increase,
-                       unrefine_sensitivity, d_marks, d_diff);
+    if (!h->faces) {  // the solver's face lists are stale: built in the same walk of the rows
+        std::shared_ptr<FaceCache> fc;
+        DX_TRY(alloc_faces(*h, n, st, fc));
+        hipLaunchKernelGGL(k_adapt_faces, dim3(grid_for(n)), dim3(256), 0, st, p.rho, h->d_st_row, h->d_st_slot,
+                           h->d_st_off, R.local_slot, R.level, grid->map.max_lvl, n, diff_threshold, diff_increase,
+                           unrefine_sensitivity, d_marks, d_diff, fc->ell_slot, fc->o_cnt, fc->o_slot, fc->o_dir,
+                           fc->d_over);
+        const_cast<Hood*>(h)->faces = fc;  // written in stream order before the solver's kernels
+    } else {
+        hipLaunchKernelGGL(k_adapt_diff, dim3(grid_for(n)), dim3(256), 0, st, p.rho, h->d_st_row, h->d_st_slot,
+                           h->d_st_off, R.local_slot, R.level, grid->map.max_lvl, n, diff_threshold, diff_increase,
+                           unrefine_sensitivity, d_marks, d_diff);
+    }
     DX_HIP(hipGetLastError());
     if (max_diff_out) DX_TRY(dx_d2h(grid->ctx, max_diff_out, d_diff, n * 8, st));
     dx_free(d_diff);

@@ -325,18 +325,24 @@ __device__ inline bool a_item_blocks(const AView& a, const uint64_t pi[3], int p
 }
 
 // unrefine_completely, dccrg.hpp:2596-2675, phase 1 (reads the flags only).
-// One wave per request: lanes 0-7 test the siblings (their outcome in the
-// reference's order, :2617-2633, is the first sibling that stops the loop,
-// found by ballot), then the lanes share the parent's window items (a serial
-// walk of them was a chain of ~100 dependent lookups per request).
+// L lanes per request (L = 8 .. 64, the window items' count rounded up, at
+// least the 8 siblings): lanes 0-7 of the group test the siblings (their
+// outcome in the reference's order, :2617-2633, is the first sibling that
+// stops the loop, found by ballot), then the group's lanes share the
+// parent's window items (a serial walk of them was a chain of ~100 dependent
+// lookups per request).  A group's control flow is uniform (one request), so
+// its ballots are its own bits of the wave's.
+template <int L>
 __global__ void __launch_bounds__(256) k_req_unref_a(AView a, const uint64_t* __restrict__ ids, uint64_t n,
                                                      int32_t* __restrict__ res, uint32_t* __restrict__ grp,
                                                      uint32_t* __restrict__ key)
 {
-    const int lane = threadIdx.x & 63;
-    const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += nwave) {
-        const uint64_t c = ids[i];  // wave-uniform from here on
+    const int lane = threadIdx.x & 63, sl = lane % L, gb = lane - sl;
+    const uint64_t gmask = L == 64 ? ~0ull : ((1ull << L) - 1);
+    auto gballot = [&](bool x) { return (uint64_t)(__ballot(x) >> gb) & gmask; };
+    const uint64_t ngroup = (uint64_t)gridDim.x * (blockDim.x / L);
+    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x / L) + threadIdx.x / L; i < n; i += ngroup) {
+        const uint64_t c = ids[i];  // group-uniform from here on
         int32_t r = 0;
         uint32_t kk = NONE32;
         const int64_t g = ex_find(a.v, c);
@@ -349,9 +355,9 @@ __global__ void __launch_bounds__(256) k_req_unref_a(AView a, const uint64_t* __
                 const uint64_t h = (uint64_t)1 << (a.v.mp.max_lvl - pl - 1);
                 bool hc = false, fl = false, un = false;
                 int64_t gk = -1;
-                if (lane < 8) {  // sibling `lane` (x fastest, Mapping::get_all_children)
-                    const uint64_t ci[3] = {pi[0] + (lane & 1) * h, pi[1] + ((lane >> 1) & 1) * h,
-                                            pi[2] + ((lane >> 2) & 1) * h};
+                if (sl < 8) {  // sibling `sl` (x fastest, Mapping::get_all_children)
+                    const uint64_t ci[3] = {pi[0] + (sl & 1) * h, pi[1] + ((sl >> 1) & 1) * h,
+                                            pi[2] + ((sl >> 2) & 1) * h};
                     const uint64_t sk = map_cell(a.v.mp, ci, pl + 1);
                     hc = a_has_children(a, sk);
                     if (!hc) {  // no children: a leaf
@@ -361,25 +367,25 @@ __global__ void __launch_bounds__(256) k_req_unref_a(AView a, const uint64_t* __
                         un = (f & RF_UNREFINE) != 0;
                     }
                 }
-                const uint64_t stop1 = __ballot(hc || fl);
+                const uint64_t stop1 = gballot(hc || fl);
                 bool stop = stop1 != 0;
                 if (stop) {
-                    if ((__ballot(hc) >> (__ffsll((unsigned long long)stop1) - 1)) & 1) r = 0;  // first stop: children
+                    if ((gballot(hc) >> (__ffsll((unsigned long long)stop1) - 1)) & 1) r = 0;  // first stop: children
                 } else {
-                    stop = __ballot(un) != 0;  // a sibling already recorded (amr.hip)
+                    stop = gballot(un) != 0;  // a sibling already recorded (amr.hip)
                 }
                 if (!stop) {
                     bool blk = false;
-                    for (int k = lane; k < a.K; k += 64) blk |= a_item_blocks(a, pi, pl, k);
-                    if (!__ballot(blk)) {
-                        const uint32_t k0 = (uint32_t)__shfl(gk, 0, 64);  // sibling 0, a leaf
+                    for (int k = sl; k < a.K; k += L) blk |= a_item_blocks(a, pi, pl, k);
+                    if (!gballot(blk)) {
+                        const uint32_t k0 = (uint32_t)__shfl(gk, gb, 64);  // sibling 0, a leaf
                         kk = k0;
-                        if (lane == 0) atomicMin(&grp[k0], (uint32_t)i);
+                        if (sl == 0) atomicMin(&grp[k0], (uint32_t)i);
                     }
                 }
             }
         }
-        if (lane == 0) {
+        if (sl == 0) {
             key[i] = kk;
             if (res) res[i] = r;
         }
@@ -1100,8 +1106,21 @@ int amr_dev_requests_many(dccrgx_grid* grid, int nk, const int32_t* kinds, const
                                (const uint32_t*)b.grp, (const uint32_t*)b.key, erase);
             break;
         case DCCRGX_AMR_UNREFINE:
-            hipLaunchKernelGGL(k_req_unref_a, dim3(bw), dim3(256), 0, st, a, (const uint64_t*)b.ids, (uint64_t)n,
-                               b.res, b.grp, b.key);
+        {
+            const unsigned bu = blocks((uint64_t)n * (a.K <= 8 ? 8 : a.K <= 16 ? 16 : a.K <= 32 ? 32 : 64));
+            if (a.K <= 8)
+                hipLaunchKernelGGL(k_req_unref_a<8>, dim3(bu), dim3(256), 0, st, a, (const uint64_t*)b.ids,
+                                   (uint64_t)n, b.res, b.grp, b.key);
+            else if (a.K <= 16)
+                hipLaunchKernelGGL(k_req_unref_a<16>, dim3(bu), dim3(256), 0, st, a, (const uint64_t*)b.ids,
+                                   (uint64_t)n, b.res, b.grp, b.key);
+            else if (a.K <= 32)
+                hipLaunchKernelGGL(k_req_unref_a<32>, dim3(bu), dim3(256), 0, st, a, (const uint64_t*)b.ids,
+                                   (uint64_t)n, b.res, b.grp, b.key);
+            else
+                hipLaunchKernelGGL(k_req_unref_a<64>, dim3(bu), dim3(256), 0, st, a, (const uint64_t*)b.ids,
+                                   (uint64_t)n, b.res, b.grp, b.key);
+        }
             hipLaunchKernelGGL(k_req_unref_b, dim3(bl), dim3(256), 0, st, a, (const uint64_t*)b.ids, (uint64_t)n,
                                (const uint32_t*)b.grp, (const uint32_t*)b.key);
             break;
@@ -1391,7 +1410,7 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
 struct SlotView {
     ExView v;
     const uint32_t* slot_of_g;
-    const uint64_t* ret;   // retired ids ascending, then their slots
+    const uint64_t* ret;   // retired ids ascending, then their slots (RET_REMOVED set for removed cells)
     uint64_t n_ret;
     const uint64_t* hkey;  // id -> slot table of the retired cells (hcap keys, then hcap slots)
     uint64_t hmask;        // hcap - 1
@@ -1444,6 +1463,28 @@ static SlotView slot_view(const dccrgx_grid* grid)
     return SlotView{explicit_view(grid), E->d_slot_of_g, E->d_ret, E->n_ret, hk, E->ret_hcap ? E->ret_hcap - 1 : 0};
 }
 
+// the retired cells' table on the device: ids ascending, then their slots
+// (the removed cells marked), then the hash (hcap keys, hcap values) filled
+// by one insertion kernel -- the host only lists the ids and slots (the
+// table itself was 16 B per hash entry zeroed, filled and uploaded by the
+// host: ~0.5 ms at 77k retired cells)
+__global__ void __launch_bounds__(256) k_ret_insert(const uint64_t* __restrict__ ids, const uint64_t* __restrict__ val,
+                                                    uint64_t n, unsigned long long* __restrict__ hk,
+                                                    uint64_t* __restrict__ hv, uint64_t mask)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t id = ids[i];
+        for (uint64_t h = ret_hash(id) & mask;; h = (h + 1) & mask) {
+            const unsigned long long prev = atomicCAS(&hk[h], 0ull, (unsigned long long)id);
+            if (prev == 0ull || prev == id) {
+                hv[h] = val[i];
+                break;
+            }
+        }
+    }
+}
+
 int amr_dev_retired_table(dccrgx_grid* grid)
 {
     Explicit* E = grid->ex;
@@ -1453,29 +1494,29 @@ int amr_dev_retired_table(dccrgx_grid* grid)
     if (!n) return DCCRGX_OK;
     uint64_t cap = 64;
     while (cap < 2 * n) cap <<= 1;  // load factor <= 1/2
-    std::vector<uint64_t> t(2 * n + 2 * cap, 0);
-    uint64_t* hk = t.data() + 2 * n;
-    uint64_t* hv = hk + cap;
+    std::vector<uint64_t> t(2 * n);
     // the removed cells among them (both lists ascending): marked in the table
     static const std::vector<uint64_t> none;
     const std::vector<uint64_t>& rem = grid->amr ? grid->amr->removed : none;
     size_t r = 0;
     for (uint64_t i = 0; i < n; i++) {
         const uint64_t id = E->retired[i], slot = E->ret_slot0 + i;
-        t[i] = id;
-        t[n + i] = slot;
         while (r < rem.size() && rem[r] < id) r++;
         const bool removed = r < rem.size() && rem[r] == id;
-        uint64_t h = ret_hash(id) & (cap - 1);
-        while (hk[h]) h = (h + 1) & (cap - 1);
-        hk[h] = id;
-        hv[h] = slot | (removed ? RET_REMOVED : 0);
+        t[i] = id;
+        t[n + i] = slot | (removed ? RET_REMOVED : 0);
     }
     hipStream_t st = grid->ctx->compute;
     ds_free(E->d_ret, st);
     E->d_ret = nullptr;
-    DX_HIP(ds_malloc(&E->d_ret, t.size() * 8, st));
+    DX_HIP(ds_malloc(&E->d_ret, (2 * n + 2 * cap) * 8, st));
+    uint64_t* hk = E->d_ret + 2 * n;
+    const Fill z[1] = {{hk, cap * 8, 0}};
+    DX_TRY(dx_fill_many(z, 1, st));
     DX_TRY(dx_h2d_async(grid->ctx, E->d_ret, t.data(), t.size() * 8, st));
+    hipLaunchKernelGGL(k_ret_insert, dim3(blocks(n)), dim3(256), 0, st, (const uint64_t*)E->d_ret,
+                       (const uint64_t*)(E->d_ret + n), n, (unsigned long long*)hk, hk + cap, cap - 1);
+    DX_HIP(hipGetLastError());
     E->n_ret = n;
     E->ret_hcap = cap;
     return DCCRGX_OK;

@@ -10,10 +10,10 @@ d = sys.argv[1]
 tr = list(csv.DictReader(open(f"{d}/run_hip_api_trace.csv")))
 kt = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
 marks = sorted(int(r["Start_Timestamp"]) for r in tr if False)
-starts = sorted(int(k["Start_Timestamp"]) for k in kt if "k_adapt_diff" in k["Kernel_Name"])
+starts = sorted(int(k["Start_Timestamp"]) for k in kt if ("k_adapt_diff" in k["Kernel_Name"] or "k_adapt_faces" in k["Kernel_Name"]))
 # the API call that launched each k_adapt_diff (by correlation id) marks a step
 launch_of = {r["Correlation_Id"]: int(r["Start_Timestamp"]) for r in tr}
-bounds = sorted(launch_of[k["Correlation_Id"]] for k in kt if "k_adapt_diff" in k["Kernel_Name"]
+bounds = sorted(launch_of[k["Correlation_Id"]] for k in kt if ("k_adapt_diff" in k["Kernel_Name"] or "k_adapt_faces" in k["Kernel_Name"])
                 and k["Correlation_Id"] in launch_of)
 a = int(sys.argv[2]) if len(sys.argv) > 2 else len(bounds) - 9
 b = int(sys.argv[3]) if len(sys.argv) > 3 else len(bounds) - 1

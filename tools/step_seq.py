@@ -11,7 +11,7 @@ kt = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
 tr = list(csv.DictReader(open(f"{d}/run_hip_api_trace.csv")))
 api = {r["Correlation_Id"]: r["Function"] for r in tr}
 kt.sort(key=lambda k: int(k["Start_Timestamp"]))
-idx = [i for i, k in enumerate(kt) if "k_adapt_diff" in k["Kernel_Name"]]
+idx = [i for i, k in enumerate(kt) if ("k_adapt_diff" in k["Kernel_Name"] or "k_adapt_faces" in k["Kernel_Name"])]
 a, b = idx[-back], idx[-back + 1]
 prev = None
 busy = gaps = 0
