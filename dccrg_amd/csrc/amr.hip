@@ -572,12 +572,23 @@ int ensure_explicit(dccrgx_grid* grid)
         rebuild_commit(grid, t);
         return DCCRGX_OK;
     }
+    // several ranks: the device list is generated there too (no upload of
+    // 8 B per cell); the host copy is filled by the host threads meanwhile
+    // (the per-rank owner and local lists are made from it)
+    hipStream_t st = grid->ctx->compute;
+    uint64_t* d_leaves = nullptr;
+    DX_HIP(ds_malloc(&d_leaves, N * 8, st));
+    hipLaunchKernelGGL(k_level0_ids, dim3(grid_for(N)), dim3(256), 0, st, d_leaves, N);
+    if (hipGetLastError() != hipSuccess) {
+        ds_free(d_leaves, st);
+        return set_error(DCCRGX_EHIP, "level-0 leaf list launch failed");
+    }
     std::vector<uint64_t> leaves(N);
     uint64_t* lv = leaves.data();
     parallel_ranges(N, 1u << 20, [lv](size_t b, size_t e) {
         for (size_t i = b; i < e; i++) lv[i] = i + 1;
     });
-    return rebuild(grid, leaves, {});
+    return rebuild(grid, leaves, {}, d_leaves);  // adopts d_leaves
 }
 
 // test option fail_stop_refining = rank + 1: the decisions of that rank's
