@@ -22,6 +22,7 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+US_LIB = os.path.join(ROOT, "examples", "libuser_stencil.so")  # tools/user_stencil_bench.py A/B runs replace it
 sys.path.insert(0, ROOT)
 
 METRIC = "cell updates/sec incl. halo exchange (1/2/4/8 GPU) + % of HBM roofline"
@@ -567,7 +568,7 @@ def user_stencil_gol(ctx, D):
     window; the boundary shell walked in separate launches) and for_each_cell
     (every neighbor read through its slot)."""
     import ctypes as C
-    L = C.CDLL(os.path.join(ROOT, "examples", "libuser_stencil.so"))
+    L = C.CDLL(US_LIB)
     L.us_gol.argtypes = [C.c_void_p] + [C.c_int32] * 5
     L.us_gol_staged.argtypes = [C.c_void_p] + [C.c_int32] * 6
     n = 2048

@@ -151,17 +151,15 @@ int main(int argc, char** argv)
         printf("%-28s %8.3f ms  %7.1f GB/s (read 1 write 2 stream)\n", "copy3", ms / reps, 12.0 * tot / (ms / reps) / 1e6);
         CK(hipMemset(cnt, 0, tot * 4));
     }
-    for (int64_t want : {65536, 131072, 262144}) {
+    for (int64_t want : {131072, 262144, 524288, 1048576}) {
         char nm[64];
 #define V(NW, NB, PF)                                                      \
     snprintf(nm, sizeof nm, "NW%d NB%d PF%d want%lld", NW, NB, PF, (long long)want); \
     report(nm, run<NW, NB, PF>(g, fld, f, want, reps));
         V(4, 4, 1)
-        V(2, 4, 1)
-        V(4, 3, 1)
+        V(4, 6, 1)
         V(4, 5, 1)
-        V(4, 2, 1)
-        V(8, 2, 3)
+        V(8, 4, 1)
     }
     return 0;
 }

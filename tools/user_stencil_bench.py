@@ -5,6 +5,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
+
+if os.environ.get("US_LIB"):  # A/B runs against another build of the example library
+    bench.US_LIB = os.environ["US_LIB"]
 import dccrg_amd as D  # noqa: E402
 
 ctx = D.Context(0, 0, 1)
