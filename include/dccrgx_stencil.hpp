@@ -1229,7 +1229,10 @@ inline SideStream* side_stream()
 
 /* options of the staged launches */
 struct StagedOptions {
-    int64_t workgroups = 131072;  // target workgroups of the staged kernel (tiles x slice chunks)
+    // target workgroups of the staged kernel (tiles x slice chunks): 2^18 was
+    // 0.4-1.0 ms faster than 2^17 and 2^19 on 2048^3 in two sweeps
+    // (profiles/s32_us_sweep.log, s34_us_sweep.log)
+    int64_t workgroups = 262144;
     bool staged = true;          // false: every cell through the walk (for comparisons)
     bool side_stream = true;     // edge launches on a second stream beside the staged kernel
 };
