@@ -110,7 +110,9 @@ def test_gather_on_caller_stream_follows_library_writes():
             g.update_copies_of_remote_neighbors(fields=["v"])
             with torch.cuda.stream(torch.cuda.Stream(device=dev)):
                 row, out = g.gather_neighbors("v")
-            got = out.cpu().numpy().view(np.uint64)
+                # read on the stream the result was handed over to (torch's
+                # default stream is not ordered after a side stream)
+                got = out.cpu().numpy().view(np.uint64)
             rr, ids, _ = g.neighbors_of(np.arange(1, n0 + 1, dtype=np.uint64))
             assert np.array_equal(got, ids * np.uint64(rnd + 3))
     finally:
