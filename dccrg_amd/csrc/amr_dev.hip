@@ -523,10 +523,12 @@ __global__ void __launch_bounds__(256) k_spread_rows(AView a, uint32_t bit, int 
 
 // override_unrefines, dccrg.hpp:9935-10124 (amr.hip explains the
 // restatement): sibling groups whose children are all leaves walk once, from
-// their smallest requested leaf; other requests walk alone.  key[g] = the
-// group's first child's leaf index, or NONE32 for a lone request.
+// their smallest requested leaf; other requests walk alone.  key[i] (and
+// lkey[leaf], for execute_refines) = the group's first child's leaf index, or
+// NONE32 for a lone request.  The eight children are looked up together.
 __global__ void __launch_bounds__(256) k_ou_group(AView a, const uint32_t* __restrict__ us, const uint32_t* __restrict__ nu,
-                                                  uint32_t* __restrict__ grp, uint32_t* __restrict__ key)
+                                                  uint32_t* __restrict__ grp, uint32_t* __restrict__ key,
+                                                  uint32_t* __restrict__ lkey)
 {
     const uint32_t n = *nu;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -534,14 +536,16 @@ __global__ void __launch_bounds__(256) k_ou_group(AView a, const uint32_t* __res
         const uint32_t g = us[i];
         uint64_t ch[8];
         a_children(a, a_parent(a, a.leaves[g]), ch);
-        uint32_t k0 = NONE32;
+        int64_t gc[8];
         bool all = true;
-        for (int k = 0; k < 8 && all; k++) {
-            const int64_t gc = ch[k] ? ex_find(a.v, ch[k]) : -1;
-            all = gc >= 0;
-            if (k == 0) k0 = (uint32_t)gc;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            gc[k] = ch[k] ? ex_find(a.v, ch[k]) : -1;
+            all &= gc[k] >= 0;
         }
-        key[i] = all ? k0 : NONE32;
+        const uint32_t k0 = all ? (uint32_t)gc[0] : NONE32;
+        key[i] = k0;
+        lkey[g] = k0;
         if (all) atomicMin(&grp[k0], g);
     }
 }
@@ -716,7 +720,8 @@ struct ExecOut {
     uint32_t* cnt;  // added, new, removed, retired, nr
 };
 
-__global__ void __launch_bounds__(256) k_exec(AView a, const uint32_t* __restrict__ grp, ExecOut o)
+__global__ void __launch_bounds__(256) k_exec(AView a, const uint32_t* __restrict__ grp,
+                                              const uint32_t* __restrict__ lkey, ExecOut o)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.n; g += stride) {
@@ -735,20 +740,18 @@ __global__ void __launch_bounds__(256) k_exec(AView a, const uint32_t* __restric
         int64_t gc[8];
         if (unref) {
             // override_unrefines' outcome: k_ou_check / k_ou_walk kept the
-            // group (on its first child's flags when every child is a leaf)
-            // or the lone request (on its own)
-            par = a_parent(a, c);
-            a_children(a, par, ch);
-            bool all = true;
+            // group (on its first child's flags when every child is a leaf,
+            // k_ou_group's key) or the lone request (on its own)
+            const uint32_t k0 = lkey[g];
+            if (a.flags[k0 != NONE32 ? k0 : (uint32_t)g] & RF_KEEP) {
+                fin = !(k0 != NONE32 && grp[k0] != (uint32_t)g);  // the group's walker does it
+                if (fin) {
+                    par = a_parent(a, c);
+                    a_children(a, par, ch);
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                gc[k] = ch[k] ? ex_find(a.v, ch[k]) : -1;
-                all &= gc[k] >= 0;
-            }
-            const uint32_t g0 = (uint32_t)gc[0];
-            if (a.flags[all ? g0 : (uint32_t)g] & RF_KEEP) {
-                fin = !(all && grp[g0] != (uint32_t)g);        // the group's walker does it
-                fin_local = fin && a_owner(a, par) == a.rank;  // the children's process too
+                    for (int k = 0; k < 8; k++) gc[k] = ch[k] ? ex_find(a.v, ch[k]) : -1;
+                    fin_local = a_owner(a, par) == a.rank;  // the children's process too
+                }
             }
         }
         uint32_t nch = 0;
@@ -1190,8 +1193,10 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     // override_unrefines
     uint32_t* cu = d_cnt + 2 * (M + 2);
     hipLaunchKernelGGL(k_collect, dim3(bN), dim3(256), 0, st, a, RF_UNREFINE, d_fa, cu);
+    uint32_t* d_lkey;  // per leaf, read only at the unrefine requests
+    DX_TRY(S.get(&d_lkey, N));
     hipLaunchKernelGGL(k_ou_group, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_fa, (const uint32_t*)cu, d_grp,
-                       d_key);
+                       d_key, d_lkey);
     int32_t* d_err = (int32_t*)(d_cnt + NC - 2);  // zeroed with the counters (walk overflow)
     if (!test_opt(OPT_OU_WALK, 0)) {
         hipLaunchKernelGGL(k_ou_check, dim3(blocks(64 * N, 2048)), dim3(256), 0, st, a, (const uint32_t*)d_fa,
@@ -1242,7 +1247,7 @@ int amr_dev_decide(dccrgx_grid* grid, uint64_t** d_leaves_out, uint64_t* n_out, 
     DX_TRY(S.get(&o.nr, N));
     uint64_t* d_nr = o.nr;
     o.cnt = d_cnt + 2 * (M + 2) + 1;  // 5 counters
-    hipLaunchKernelGGL(k_exec, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_grp, o);
+    hipLaunchKernelGGL(k_exec, dim3(bN), dim3(256), 0, st, a, (const uint32_t*)d_grp, (const uint32_t*)d_lkey, o);
     DX_HIP(hipGetLastError());
     uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
     int32_t err = 0;
