@@ -299,13 +299,29 @@ __global__ void __launch_bounds__(256, WPE) k_ex_advect_faces_buf(AdvPtrs p, dou
             __builtin_amdgcn_sched_barrier(0);
         }
         if (oc) {  // further faces (finer neighbors), in row order after the six above
-            {
-                const int ax = (dir0 > 0 ? dir0 : -dir0) - 1;
-                const double ln0 = adv_ld(rl0, nb0), ln1 = adv_ld(rl1, nb0), ln2 = adv_ld(rl2, nb0);
-                const double vn = adv_ld(ax == 0 ? rv0 : ax == 1 ? rv1 : rv2, nb0), rn = adv_ld(rr, nb0);
-                acc += face_term_v(dir0, dt, vol, lc3, vc3, rho_c, ln0, ln1, ln2, vn, rn);
+            // the first four entries' slots, then their gathers, issued
+            // together (a cell next to finer cells has up to four in 2-D); the
+            // terms are added in row order
+            uint32_t nbo[4] = {nb0, c, c, c};
+            int dro[4] = {dir0, 1, 1, 1};
+#pragma unroll
+            for (int j = 1; j < 4; j++)
+                if ((uint32_t)j < oc) {
+                    nbo[j] = fc.o_slot[ob + j];
+                    dro[j] = fc.o_dir[ob + j];
+                }
+            double to[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int ax = (dro[j] > 0 ? dro[j] : -dro[j]) - 1;
+                const double ln0 = adv_ld(rl0, nbo[j]), ln1 = adv_ld(rl1, nbo[j]), ln2 = adv_ld(rl2, nbo[j]);
+                const double vn = adv_ld(ax == 0 ? rv0 : ax == 1 ? rv1 : rv2, nbo[j]), rn = adv_ld(rr, nbo[j]);
+                to[j] = face_term_v(dro[j], dt, vol, lc3, vc3, rho_c, ln0, ln1, ln2, vn, rn);
             }
-            for (uint64_t e = ob + 1, e1 = ob + oc; e < e1; e++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if ((uint32_t)j < oc) acc += to[j];
+            for (uint64_t e = ob + 4, e1 = ob + oc; e < e1; e++) {
                 const uint32_t nb = fc.o_slot[e];
                 const int dir = fc.o_dir[e], ax = (dir > 0 ? dir : -dir) - 1;
                 const double ln0 = adv_ld(rl0, nb), ln1 = adv_ld(rl1, nb), ln2 = adv_ld(rl2, nb);
