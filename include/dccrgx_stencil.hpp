@@ -868,6 +868,181 @@ __global__ void __launch_bounds__(64 * NW) k_staged(StagedGeo g, Fields<T, NF> f
     }
 }
 
+/* k_staged for 4-byte elements on rows of a multiple of 4 cells, its planes
+ * fetched by buffer loads that write LDS directly (no register staging): two
+ * planes in flight in three LDS buffers at no register cost (the register
+ * path's second plane in flight costs ~40 VGPRs and a wave per SIMD).  A
+ * field's plane image is the tile's WB rows of 64 cells, dense (a 64-lane
+ * 16-byte load writes 1 KiB contiguously: four rows), then its two apron
+ * columns as [WB][2].  Wave w issues the loads i = w, w + NW, ... of each
+ * field; the wave with one fewer also loads the aprons (4 bytes per lane).
+ * The next plane's loads are issued after the cells' stores, so a wave's own
+ * loads of plane q are the oldest of its memory operations but those of plane
+ * q + 1: `s_waitcnt vmcnt(G_w)` (G_w its loads per plane) leaves exactly
+ * plane q + 1 in flight; a raw s_barrier then publishes every wave's share
+ * (__syncthreads would wait for every load in flight). */
+template <class T, int NF, int NW, int NB>
+struct StagedTileG {
+    static_assert(sizeof(T) == 4, "LDS-DMA staging: 4-byte elements");
+    static constexpr int TB = NW * NB, WB = TB + 2;
+    static_assert(2 * WB <= 64, "the apron columns are one 64-lane load");
+    static constexpr int MAIN = WB * 64;         // elements of the dense rows
+    static constexpr int PLANE = MAIN + 2 * WB;  // + the apron columns
+    static constexpr int NCHUNK = MAIN / 4;      // 16-byte loads
+    static constexpr int NI = (NCHUNK + 63) / 64;
+    static constexpr int KI = (NI + NW - 1) / NW;
+    static constexpr int AW = NI % NW;  // the apron wave (0 when every wave issues KI)
+    __host__ __device__ static constexpr int loads(int w)
+    {
+        return NF * ((NI - w + NW - 1) / NW + (w == AW ? 1 : 0));
+    }
+
+    // byte offsets in the plane; a position outside the grid reads past the
+    // plane (the buffer returns zeros).  Every load a wave counts in loads(w)
+    // is issued whatever the grid holds: a skipped one would let the wait
+    // count a younger plane's load as this plane's
+    static constexpr uint32_t OUT = 0x80000000u;
+    uint32_t off[KI], aoff;
+    int w, lane;
+
+    __device__ inline void init(const StagedGeo& g, int64_t a0, int64_t b0, int t)
+    {
+        const int64_t LA = (int64_t)g.la, LB = (int64_t)g.lb;
+        w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: scalar branches on it
+        lane = t & 63;
+#pragma unroll
+        for (int k = 0; k < KI; k++) {
+            const int i = w + NW * k, e = 64 * i + lane;
+            const int row = e >> 4, q = e & 15;
+            const int64_t a = a0 + 4 * q, b = b0 - 1 + row;
+            const bool ok = i < NI && e < NCHUNK && a < LA && b >= 0 && b < LB;
+            off[k] = ok ? (uint32_t)((a + LA * b) * 4) : OUT;
+        }
+        aoff = OUT;
+        if (w == AW && lane < 2 * WB) {
+            const int row = lane >> 1;
+            const int64_t a = (lane & 1) ? a0 + 64 : a0 - 1, b = b0 - 1 + row;
+            if (a >= 0 && a < LA && b >= 0 && b < LB) aoff = (uint32_t)((a + LA * b) * 4);
+        }
+    }
+    // plane image of storage slice sc into LDS buffer img (NF planes of PLANE)
+    __device__ inline void issue(const Fields<T, NF>& fld, uint64_t S, int64_t sc, T* img) const
+    {
+#if defined(__HIP_DEVICE_COMPILE__)  // the LDS-DMA builtins exist for the device only
+#pragma unroll
+        for (int j = 0; j < NF; j++) {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<T*>(fld.p[j] + (uint64_t)sc * S), 0, (int)(S * sizeof(T)), 0x00020000);
+            T* l = img + j * PLANE;
+#pragma unroll
+            for (int k = 0; k < KI; k++)
+                if (w + NW * k < NI && 64 * (w + NW * k) + lane < NCHUNK)  // lane 0 always: the load is issued
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rs, (__attribute__((address_space(3))) void*)(l + 256 * (w + NW * k)), 16, off[k], 0, 0, 0);
+            if (w == AW && lane < 2 * WB)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(l + MAIN), 4,
+                                                         aoff, 0, 0, 0);
+        }
+#endif
+    }
+    // the lane's 3 x (NB + 2) values of image img into W[.][pl]
+    __device__ inline void window(const T* img, T (&W)[NF][3][NB + 2][3], int pl) const
+    {
+        const int il = lane == 0 ? MAIN : lane - 1, sl = lane == 0 ? 2 : 64;
+        const int ir = lane == 63 ? MAIN + 1 : lane + 1, sr = lane == 63 ? 2 : 64;
+#pragma unroll
+        for (int j = 0; j < NF; j++) {
+            const T* l = img + j * PLANE;
+#pragma unroll
+            for (int rr = 0; rr < NB + 2; rr++) {
+                const int row = w * NB + rr;
+                W[j][pl][rr][0] = l[il + sl * row];
+                W[j][pl][rr][1] = l[64 * row + lane];
+                W[j][pl][rr][2] = l[ir + sr * row];
+            }
+        }
+    }
+};
+
+template <int N>
+__device__ inline void vm_wait()
+{
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+/* s_waitcnt vmcnt(loads(w)) for this wave (the immediate is per wave) */
+template <class Tile, int W, int NW>
+struct WaitOwn {
+    __device__ static inline void run(int w)
+    {
+        if (w == W) {
+            vm_wait<Tile::loads(W)>();
+            return;
+        }
+        WaitOwn<Tile, W + 1, NW>::run(w);
+    }
+};
+template <class Tile, int NW>
+struct WaitOwn<Tile, NW, NW> {
+    __device__ static inline void run(int)
+    {
+        vm_wait<0>();
+    }
+};
+
+template <class T, int NF, int SHAPE, int NW, int NB, class F>
+__global__ void __launch_bounds__(64 * NW) k_staged_g(StagedGeo g, Fields<T, NF> fld, F f)
+{
+    typedef StagedTileG<T, NF, NW, NB> Tile;
+    constexpr int NBUF = 3;
+    __shared__ __attribute__((aligned(16))) T P[NBUF * NF * Tile::PLANE];
+
+    const int t = threadIdx.x;
+    const uint32_t wgid = xcd_wgid(g.nwg);
+    const uint32_t tiles = g.tiles_a * g.tiles_b;
+    const uint32_t tile_id = wgid % tiles;
+    const int64_t chunk_id = wgid / tiles;
+    const int64_t a0 = (int64_t)(tile_id % g.tiles_a) * 64;
+    const int64_t b0 = (int64_t)(tile_id / g.tiles_a) * Tile::TB;
+    const int64_t c0 = g.s0 + chunk_id * g.chunk;
+    const int64_t c1 = min(g.s1, c0 + g.chunk);
+    if (c0 >= c1) return;
+
+    Tile tile;
+    tile.init(g, a0, b0, t);
+    T W[NF][3][NB + 2][3];
+    // plane q = storage slice c0 - 1 + q, q in [0, Q), in buffer q % 3;
+    // computed: q in [2, Q) -> slice c0 + q - 2
+    const int64_t Q = c1 - c0 + 2;
+    tile.issue(fld, g.S, c0 - 1, P);
+    tile.issue(fld, g.S, c0, P + NF * Tile::PLANE);
+    const int64_t a = a0 + tile.lane, bw = b0 + tile.w * NB;
+    for (int64_t q = 0; q < Q; q++) {
+        // this wave's loads of plane q are done (those of q + 1 may fly)
+        if (q + 1 < Q) WaitOwn<Tile, 0, NW>::run(tile.w);
+        else vm_wait<0>();
+        asm volatile("s_barrier" ::: "memory");
+        const T* img = P + (int)(q % NBUF) * NF * Tile::PLANE;
+        tile.window(img, W, 2);
+        if (q >= 2) {
+            const int64_t c = c0 + q - 2;
+            const int64_t pls[3] = {c - 1, c, c + 1};
+            staged_cells<T, NF, SHAPE, NB, CLS_MID>(g, f, W, pls, c, a, bw);
+        }
+#pragma unroll
+        for (int jj = 0; jj < NF; jj++)
+#pragma unroll
+            for (int rr = 0; rr < NB + 2; rr++)
+#pragma unroll
+                for (int qq = 0; qq < 3; qq++) {
+                    W[jj][0][rr][qq] = W[jj][1][rr][qq];
+                    W[jj][1][rr][qq] = W[jj][2][rr][qq];
+                }
+        // plane q + 2 into the buffer every wave finished reading at q - 1
+        if (q + 2 < Q) tile.issue(fld, g.S, c0 + 1 + q, P + (int)((q + 2) % NBUF) * NF * Tile::PLANE);
+    }
+}
+
 /* The first (CLS_LOW) or last (CLS_HIGH) slice of a periodic C axis, storage
  * slice g.s0: the plane across the wrap is read from storage slice
  * g.wrap_lo / g.wrap_hi (the local slice itself when this rank holds it, as
@@ -1058,7 +1233,7 @@ struct StagedShape {
     static constexpr int NW = units <= 1 ? 4 : 8;
     static constexpr int TB = NW * NB;
     static constexpr int VEC = (int)(16 / sizeof(T));
-    static constexpr int PF = 1;  // planes in flight (deeper costs occupancy: tools/us_sweep.hip)
+    static constexpr int PF = 1;  // planes in flight (deeper costs occupancy: tools/us_sweep.hip; k_staged_g keeps two)
 };
 
 inline StagedGeo staged_geo(const dccrgx_stencil_view& v, int TB)
@@ -1084,6 +1259,9 @@ inline StagedGeo staged_geo(const dccrgx_stencil_view& v, int TB)
     return g;
 }
 
+#ifndef DCCRGX_STAGED_GLDS
+#define DCCRGX_STAGED_GLDS 1  // 0: the register-staged k_staged for every element size
+#endif
 template <class T, int NF, int SHAPE, class F>
 int launch_staged(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, int64_t s1, F f, hipStream_t st,
                   int64_t want)
@@ -1099,6 +1277,13 @@ int launch_staged(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, i
     const int64_t nwg = tiles * ((nsl + g.chunk - 1) / g.chunk);
     if (nwg >= (1ll << 31)) return DCCRGX_EINVAL;
     g.nwg = (uint32_t)nwg;
+    if constexpr (sizeof(T) == 4 && DCCRGX_STAGED_GLDS) {
+        if (v.la % 4 == 0 && g.S * 4 < (1ull << 31)) {
+            hipLaunchKernelGGL((k_staged_g<T, NF, SHAPE, Sh::NW, Sh::NB, F>), dim3(g.nwg), dim3(64 * Sh::NW), 0, st,
+                               g, fld, f);
+            return DCCRGX_OK;
+        }
+    }
     if (v.la % Sh::VEC == 0)
         hipLaunchKernelGGL((k_staged<T, NF, SHAPE, Sh::NW, Sh::NB, Sh::VEC, Sh::PF, F>), dim3(g.nwg),
                            dim3(64 * Sh::NW), 0, st, g, fld, f);

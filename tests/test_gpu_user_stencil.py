@@ -237,7 +237,7 @@ LARGER = [((70, 40, 9), (True, False, True), 1),
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("staged", [None, 0, 1, 2])
+@pytest.mark.parametrize("staged", [None, 0, 1, 2, 3])
 @pytest.mark.parametrize("P", [1, 3])
 @pytest.mark.parametrize("length,per,hood_len", LARGER)
 def test_gol_functor_larger_grids(length, per, hood_len, P, staged):
@@ -247,7 +247,9 @@ def test_gol_functor_larger_grids(length, per, hood_len, P, staged):
     reference's lists) on every rank.  staged: None = for_each_cell (slots),
     1 = for_each_cell_staged (the staged kernel for the cube / faces plus the
     boundary walks on a second stream), 2 = the same on the caller's stream
-    alone, 0 = for_each_cell_staged with every cell walked."""
+    alone, 3 = 1 with one workgroup per tile marching through every slice
+    (long marches: every plane after the second fetched while two are in
+    flight), 0 = for_each_cell_staged with every cell walked."""
     import torch
 
     import dccrg_amd as D
