@@ -502,6 +502,7 @@ struct StagedGeo {
     int32_t inv[3];    // x, y, z -> canonical axis
     int32_t scale;
     int64_t nslices;   // storage slices
+    int32_t cols_in;   // k_staged_g also takes the columns a = 0, LA - 1 (rows 1 .. LB - 2; A not periodic)
 };
 
 /* a cell of the staged kernels: values from the register window
@@ -990,11 +991,56 @@ struct WaitOwn<Tile, NW, NW> {
     }
 };
 
+/* a column cell a = 0 / LA - 1 (A not periodic, B and C inside) of a
+ * k_staged_g tile: the inner order with the neighbors past A's end dropped
+ * (the edge walk's order there), the values from the three plane images in
+ * LDS at the cell's row and column.  (The rows b = 0, LB - 1 taken the same
+ * way, 64 lanes a row, measured 0.5 ms per 2048^3 step slower than leaving
+ * them to the edge walk: the extra functor body cost the march its register
+ * schedule, profiles/s53_staged_rows_ab.log.) */
+template <class T, int NF, int SHAPE, int PLANE>
+struct ImgEdgeCell {
+    uint64_t slot, id;
+    const T* img[3];  // planes c - 1, c, c + 1
+    int64_t la, S;
+    int32_t inv[3], scale;
+    int row, col;
+    bool lo_end, hi_end;  // a = 0 / a = LA - 1
+
+    __host__ __device__ inline T value(int j) const { return img[1][j * PLANE + row * 64 + col]; }
+
+    template <class G>
+    __host__ __device__ inline void for_each_neighbor(G&& fn) const
+    {
+        typedef StagedItems<SHAPE> It;
+#pragma unroll
+        for (int k = 0; k < It::K; k++) {
+            const int da = It::d(k, 0), db = It::d(k, 1), dc = It::d(k, 2);
+            if ((da < 0 && lo_end) || (da > 0 && hi_end)) continue;
+            ValueNeighbor<T, NF> nb;
+            nb.slot = slot + (uint64_t)((int64_t)da + la * db + S * dc);
+            nb.x = (inv[0] == 0 ? da : (inv[0] == 1 ? db : dc)) * scale;
+            nb.y = (inv[1] == 0 ? da : (inv[1] == 1 ? db : dc)) * scale;
+            nb.z = (inv[2] == 0 ? da : (inv[2] == 1 ? db : dc)) * scale;
+#pragma unroll
+            for (int j = 0; j < NF; j++) nb.v[j] = img[dc + 1][j * PLANE + (row + db) * 64 + col + da];
+            fn(nb);
+        }
+    }
+};
+
+// four workgroups of four waves per CU (at most 128 VGPRs: the game-of-life
+// functor with the column cells needs 130 unbounded, and fits with no spill)
+#ifndef DCCRGX_STAGED_G_MINWG
+#define DCCRGX_STAGED_G_MINWG 4
+#endif
 template <class T, int NF, int SHAPE, int NW, int NB, class F>
-__global__ void __launch_bounds__(64 * NW) k_staged_g(StagedGeo g, Fields<T, NF> fld, F f)
+__global__ void __launch_bounds__(64 * NW, DCCRGX_STAGED_G_MINWG) k_staged_g(StagedGeo g, Fields<T, NF> fld, F f)
 {
     typedef StagedTileG<T, NF, NW, NB> Tile;
-    constexpr int NBUF = 3;
+    // planes q - 2 .. q read at step q (the column cells read all three),
+    // q + 1 and q + 2 in flight
+    constexpr int NBUF = 5;
     __shared__ __attribute__((aligned(16))) T P[NBUF * NF * Tile::PLANE];
 
     const int t = threadIdx.x;
@@ -1011,17 +1057,52 @@ __global__ void __launch_bounds__(64 * NW) k_staged_g(StagedGeo g, Fields<T, NF>
     Tile tile;
     tile.init(g, a0, b0, t);
     T W[NF][3][NB + 2][3];
-    // plane q = storage slice c0 - 1 + q, q in [0, Q), in buffer q % 3;
+    // plane q = storage slice c0 - 1 + q, q in [0, Q), in buffer q % NBUF;
     // computed: q in [2, Q) -> slice c0 + q - 2
     const int64_t Q = c1 - c0 + 2;
     tile.issue(fld, g.S, c0 - 1, P);
     tile.issue(fld, g.S, c0, P + NF * Tile::PLANE);
     const int64_t a = a0 + tile.lane, bw = b0 + tile.w * NB;
+    // the column cells: lanes [0, NB) take a = 0 in the first tile, lanes
+    // [NB, 2 NB) a = LA - 1 in the last (rows bw ..; wave-uniform test first)
+    const int64_t LA = (int64_t)g.la, LB = (int64_t)g.lb;
+    const bool col_tile = g.cols_in && (a0 == 0 || a0 + 64 >= LA);  // uniform
     for (int64_t q = 0; q < Q; q++) {
         // this wave's loads of plane q are done (those of q + 1 may fly)
         if (q + 1 < Q) WaitOwn<Tile, 0, NW>::run(tile.w);
         else vm_wait<0>();
         asm volatile("s_barrier" ::: "memory");
+        if (q >= 2) {
+            // the column cells first, from the images: plane q's window
+            // registers are not live yet
+            const int64_t c = c0 + q - 2;
+            // (the lane's column cell recomputed here: fewer registers live
+            // across the march)
+            const int cside = tile.lane < NB ? 0 : (tile.lane < 2 * NB ? 1 : -1);
+            const int64_t ca = cside == 0 ? 0 : LA - 1, cb = bw + tile.lane - (cside == 1 ? NB : 0);
+            if (col_tile && cside >= 0 && (cside == 0 ? a0 == 0 : a0 + 64 >= LA) && cb >= 1 && cb + 1 < LB) {
+                const int64_t cg = c + g.cbase;
+                const uint64_t lin = (uint64_t)ca + g.la * (uint64_t)cb + g.S * (uint64_t)cg;
+                if (lin >= g.lo && lin < g.hi) {
+                    ImgEdgeCell<T, NF, SHAPE, Tile::PLANE> cell;
+                    cell.slot = (uint64_t)ca + g.la * (uint64_t)cb + g.S * (uint64_t)c;
+                    cell.id = lin + 1;
+                    cell.la = (int64_t)g.la;
+                    cell.S = (int64_t)g.S;
+                    cell.lo_end = ca == 0;
+                    cell.hi_end = ca == LA - 1;
+                    cell.inv[0] = g.inv[0];
+                    cell.inv[1] = g.inv[1];
+                    cell.inv[2] = g.inv[2];
+                    cell.scale = g.scale;
+#pragma unroll
+                    for (int d = 0; d < 3; d++) cell.img[d] = P + (int)((q - 2 + d) % NBUF) * NF * Tile::PLANE;
+                    cell.row = (int)(cb - b0) + 1;
+                    cell.col = (int)(ca - a0);
+                    f(cell);
+                }
+            }
+        }
         const T* img = P + (int)(q % NBUF) * NF * Tile::PLANE;
         tile.window(img, W, 2);
         if (q >= 2) {
@@ -1038,7 +1119,7 @@ __global__ void __launch_bounds__(64 * NW) k_staged_g(StagedGeo g, Fields<T, NF>
                     W[jj][0][rr][qq] = W[jj][1][rr][qq];
                     W[jj][1][rr][qq] = W[jj][2][rr][qq];
                 }
-        // plane q + 2 into the buffer every wave finished reading at q - 1
+        // plane q + 2 into the buffer no wave reads after step q
         if (q + 2 < Q) tile.issue(fld, g.S, c0 + 1 + q, P + (int)((q + 2) % NBUF) * NF * Tile::PLANE);
     }
 }
@@ -1256,16 +1337,22 @@ inline StagedGeo staged_geo(const dccrgx_stencil_view& v, int TB)
     g.tiles_a = (uint32_t)((v.la + 63) / 64);
     g.tiles_b = (uint32_t)((v.lb + TB - 1) / TB);
     g.nwg = 0;
+    g.cols_in = 0;
     return g;
 }
 
 #ifndef DCCRGX_STAGED_GLDS
 #define DCCRGX_STAGED_GLDS 1  // 0: the register-staged k_staged for every element size
 #endif
+#ifndef DCCRGX_STAGED_COLS
+#define DCCRGX_STAGED_COLS 1  // 0: k_staged_g leaves the edge columns to k_staged_cols
+#endif
+/* *cols_done: the launch took the edge columns a = 0, LA - 1 too */
 template <class T, int NF, int SHAPE, class F>
 int launch_staged(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, int64_t s1, F f, hipStream_t st,
-                  int64_t want)
+                  int64_t want, bool* cols_done)
 {
+    *cols_done = false;
     typedef StagedShape<T, NF> Sh;
     StagedGeo g = staged_geo(v, Sh::TB);
     g.s0 = s0;
@@ -1279,6 +1366,8 @@ int launch_staged(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, i
     g.nwg = (uint32_t)nwg;
     if constexpr (sizeof(T) == 4 && DCCRGX_STAGED_GLDS) {
         if (v.la % 4 == 0 && g.S * 4 < (1ull << 31)) {
+            g.cols_in = DCCRGX_STAGED_COLS && !v.per[0];
+            *cols_done = g.cols_in != 0;
             hipLaunchKernelGGL((k_staged_g<T, NF, SHAPE, Sh::NW, Sh::NB, F>), dim3(g.nwg), dim3(64 * Sh::NW), 0, st,
                                g, fld, f);
             return DCCRGX_OK;
@@ -1317,14 +1406,15 @@ int launch_staged_wrap(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t 
 
 template <class T, int NF, int SHAPE, class F>
 int launch_edge(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, int64_t s1, bool whole, F f,
-                hipStream_t st)
+                hipStream_t st, bool cols_done = false)
 {
     if (s1 <= s0) return DCCRGX_OK;
     const StagedGeo g = staged_geo(v, 1);
     // the ring: rows b = 0 and LB - 1 by the edge walk, the columns staged
-    // (k_staged_cols) when their values fit LDS
-    const bool cols = !whole && v.lb >= 3 && sizeof(T) * NF * (COL_C + 2) * (COL_B + 2) * 3 <= 48 * 1024;
-    const int32_t mode = whole ? 1 : cols ? 2 : 0;
+    // (k_staged_cols) when their values fit LDS, or none when the staged
+    // kernel took them (cols_done)
+    const bool cols = !whole && !cols_done && v.lb >= 3 && sizeof(T) * NF * (COL_C + 2) * (COL_B + 2) * 3 <= 48 * 1024;
+    const int32_t mode = whole ? 1 : (cols || cols_done) ? 2 : 0;
     const uint64_t per = mode == 1 ? v.la * v.lb : mode == 2 ? 2 * v.la : 2 * v.la + 2 * (v.lb - 2);
     const uint64_t n = per * (uint64_t)(s1 - s0);
     uint64_t blocks = (n + 255) / 256;
@@ -1359,8 +1449,9 @@ int staged_range(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, in
     const int64_t m1 = s1 < lc - 1 - cb ? s1 : lc - 1 - cb;
     int e = DCCRGX_OK;
     if (m1 > m0) {
-        e = launch_staged<T, NF, SHAPE>(v, fld, m0, m1, f, st, want);
-        if (e == DCCRGX_OK) e = launch_edge<T, NF, SHAPE>(v, fld, m0, m1, false, f, se);
+        bool cols_done = false;
+        e = launch_staged<T, NF, SHAPE>(v, fld, m0, m1, f, st, want, &cols_done);
+        if (e == DCCRGX_OK) e = launch_edge<T, NF, SHAPE>(v, fld, m0, m1, false, f, se, cols_done);
         if (e != DCCRGX_OK) return e;
     }
     for (int side = 0; side < 2; side++) {

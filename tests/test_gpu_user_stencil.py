@@ -233,7 +233,12 @@ LARGER = [((70, 40, 9), (True, False, True), 1),
           # A % 4 == 0 (16-byte staged loads), several tiles along A and B
           ((132, 37, 12), (False, True, True), 1),
           ((128, 50, 7), (True, True, False), 0),
-          ((8, 20, 16), (True, False, False), 1)]
+          ((8, 20, 16), (True, False, False), 1),
+          # A and B not periodic, A % 4 == 0: the staged kernel takes the
+          # boundary columns and rows too (the edge walk none of the ring)
+          ((68, 29, 10), (False, False, True), 1),
+          ((64, 40, 9), (False, False, False), 0),
+          ((136, 18, 7), (False, True, False), 1)]
 
 
 @pytest.mark.gpu
