@@ -1305,6 +1305,116 @@ __global__ void __launch_bounds__(COL_B* COL_C) k_staged_cols(StagedGeo g, Field
     }
 }
 
+/* The edge rows b = 0 and LB - 1 of storage slices [s0, s1) whose canonical c
+ * is inside (A and B not periodic): a wave owns 64 cells of one row and
+ * marches along C through `chunk` slices; each plane's edge row and the
+ * inner row next to it are read once (a - 1, a, a + 1: three coalesced
+ * loads each) into a register window of three planes.  A cell's neighbors
+ * come in the inner order with those past the grid's ends dropped, as the
+ * edge walk gives them (ROW 0: b = 0, ROW 1: b = LB - 1).  (The edge walk,
+ * one thread per cell and every neighbor loaded at its slot: 0.52 ms per
+ * 2048^3 step.) */
+template <class T, int NF, int SHAPE, int ROW>
+struct RowCell {
+    uint64_t slot, id;
+    const T (*w)[3][2][3];  // [field][plane c - 1 .. c + 1][row: inner-order][a - 1 .. a + 1]
+    int64_t la, S;
+    int32_t inv[3], scale;
+    bool a_lo, a_hi;
+
+    __host__ __device__ inline T value(int j) const { return w[j][1][ROW == 0 ? 0 : 1][1]; }
+
+    template <class G>
+    __host__ __device__ inline void for_each_neighbor(G&& fn) const
+    {
+        typedef StagedItems<SHAPE> It;
+#pragma unroll
+        for (int k = 0; k < It::K; k++) {
+            const int da = It::d(k, 0), db = It::d(k, 1), dc = It::d(k, 2);
+            if ((ROW == 0 && db < 0) || (ROW == 1 && db > 0)) continue;
+            if ((da < 0 && a_lo) || (da > 0 && a_hi)) continue;
+            ValueNeighbor<T, NF> nb;
+            nb.slot = slot + (uint64_t)((int64_t)da + la * db + S * dc);
+            nb.x = (inv[0] == 0 ? da : (inv[0] == 1 ? db : dc)) * scale;
+            nb.y = (inv[1] == 0 ? da : (inv[1] == 1 ? db : dc)) * scale;
+            nb.z = (inv[2] == 0 ? da : (inv[2] == 1 ? db : dc)) * scale;
+#pragma unroll
+            for (int j = 0; j < NF; j++) nb.v[j] = w[j][dc + 1][ROW == 0 ? db : db + 1][da + 1];
+            fn(nb);
+        }
+    }
+};
+
+template <class T, int NF, int SHAPE, int ROW, class F>
+__device__ inline void staged_row_march(const StagedGeo& g, const Fields<T, NF>& fld, int64_t cs, int64_t ce,
+                                        int64_t a, F& f)
+{
+    const int64_t LA = (int64_t)g.la, LB = (int64_t)g.lb;
+    const int64_t r0 = ROW == 0 ? 0 : LB - 2;  // window rows r0, r0 + 1
+    const int64_t b = ROW == 0 ? 0 : LB - 1;
+    T W[NF][3][2][3];
+    auto load = [&](int64_t sl, int pl) {
+#pragma unroll
+        for (int j = 0; j < NF; j++) {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<T*>(fld.p[j] + (uint64_t)sl * g.S), 0, (int)(g.S * sizeof(T)), 0x00020000);
+#pragma unroll
+            for (int r = 0; r < 2; r++)
+#pragma unroll
+                for (int q = 0; q < 3; q++) {
+                    // a - 1 < 0 / a + 1 = LA read past the row (a neighbor
+                    // dropped anyway): the plane's bounds give 0 outside it
+                    const int64_t e = a + q - 1 + LA * (r0 + r);
+                    W[j][pl][r][q] = buffer_load<T>(rs, e < 0 ? 0x80000000u : (uint32_t)(e * (int64_t)sizeof(T)));
+                }
+        }
+    };
+    load(cs - 1, 0);
+    load(cs, 1);
+    RowCell<T, NF, SHAPE, ROW> cell;
+    cell.w = W;
+    cell.la = LA;
+    cell.S = (int64_t)g.S;
+    cell.inv[0] = g.inv[0];
+    cell.inv[1] = g.inv[1];
+    cell.inv[2] = g.inv[2];
+    cell.scale = g.scale;
+    cell.a_lo = a == 0;
+    cell.a_hi = a == LA - 1;
+    for (int64_t sl = cs; sl < ce; sl++) {
+        load(sl + 1, 2);
+        const uint64_t lin = (uint64_t)a + g.la * (uint64_t)b + g.S * (uint64_t)(sl + g.cbase);
+        if (a < LA && lin >= g.lo && lin < g.hi) {
+            cell.slot = (uint64_t)a + g.la * (uint64_t)b + g.S * (uint64_t)sl;
+            cell.id = lin + 1;
+            f(cell);
+        }
+#pragma unroll
+        for (int j = 0; j < NF; j++)
+#pragma unroll
+            for (int r = 0; r < 2; r++)
+#pragma unroll
+                for (int q = 0; q < 3; q++) {
+                    W[j][0][r][q] = W[j][1][r][q];
+                    W[j][1][r][q] = W[j][2][r][q];
+                }
+    }
+}
+
+template <class T, int NF, int SHAPE, class F>
+__global__ void __launch_bounds__(256) k_staged_rows(StagedGeo g, Fields<T, NF> fld, int64_t s0, int64_t s1,
+                                                      int64_t chunk, F f)
+{
+    const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const uint64_t ta = (g.la + 63) / 64, per = 2 * ta;
+    const uint64_t cid = wave / per, rem = wave - cid * per, side = rem / ta, at = rem - side * ta;
+    const int64_t cs = s0 + (int64_t)cid * chunk, ce = min(s1, cs + chunk);
+    if (cs >= ce) return;  // wave-uniform
+    const int64_t a = (int64_t)(at * 64) + (threadIdx.x & 63);
+    if (side == 0) staged_row_march<T, NF, SHAPE, 0>(g, fld, cs, ce, a, f);
+    else staged_row_march<T, NF, SHAPE, 1>(g, fld, cs, ce, a, f);
+}
+
 template <class T, int NF>
 struct StagedShape {
     // the register window holds 9 (NB + 2) elements per field: NB rows per
@@ -1404,22 +1514,39 @@ int launch_staged_wrap(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t 
     return DCCRGX_OK;
 }
 
+#ifndef DCCRGX_STAGED_ROWS
+#define DCCRGX_STAGED_ROWS 1  // 0: the edge rows of inner slices by the edge walk too
+#endif
+/* inner: [s0, s1) are slices whose canonical c is inside (planes c - 1 .. c +
+ * 1 are storage slices s - 1 .. s + 1) */
 template <class T, int NF, int SHAPE, class F>
 int launch_edge(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, int64_t s1, bool whole, F f,
-                hipStream_t st, bool cols_done = false)
+                hipStream_t st, bool cols_done = false, bool inner = false)
 {
     if (s1 <= s0) return DCCRGX_OK;
     const StagedGeo g = staged_geo(v, 1);
-    // the ring: rows b = 0 and LB - 1 by the edge walk, the columns staged
-    // (k_staged_cols) when their values fit LDS, or none when the staged
-    // kernel took them (cols_done)
-    const bool cols = !whole && !cols_done && v.lb >= 3 && sizeof(T) * NF * (COL_C + 2) * (COL_B + 2) * 3 <= 48 * 1024;
-    const int32_t mode = whole ? 1 : (cols || cols_done) ? 2 : 0;
+    // the ring: rows b = 0 and LB - 1 by the row march (inner slices, A and B
+    // not periodic) or the edge walk, the columns staged (k_staged_cols) when
+    // their values fit LDS, or none when the staged kernel took them
+    const bool fits = v.lb >= 3 && sizeof(T) * NF * (COL_C + 2) * (COL_B + 2) * 3 <= 48 * 1024;
+    // (columns that fit no LDS go with the rows in the ring walk)
+    const bool rows_march = DCCRGX_STAGED_ROWS && !whole && inner && !v.per[0] && !v.per[1] && (cols_done || fits);
+    if (rows_march) {
+        const uint64_t ta = (v.la + 63) / 64, nsl = (uint64_t)(s1 - s0);
+        uint64_t chunks = 16384 / (2 * ta);
+        chunks = chunks < 1 ? 1 : (chunks > nsl ? nsl : chunks);
+        const int64_t chunk = (int64_t)((nsl + chunks - 1) / chunks);
+        const uint64_t waves = 2 * ta * ((nsl + chunk - 1) / chunk);
+        hipLaunchKernelGGL((k_staged_rows<T, NF, SHAPE, F>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, g, fld,
+                           s0, s1, chunk, f);
+    }
+    const bool cols = !whole && !cols_done && fits;
+    const int32_t mode = whole ? 1 : (rows_march ? -1 : (cols || cols_done) ? 2 : 0);  // -1: no walk
     const uint64_t per = mode == 1 ? v.la * v.lb : mode == 2 ? 2 * v.la : 2 * v.la + 2 * (v.lb - 2);
     const uint64_t n = per * (uint64_t)(s1 - s0);
     uint64_t blocks = (n + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    if (blocks)
+    if (blocks && mode >= 0)
         hipLaunchKernelGGL((k_staged_edge<T, NF, SHAPE, F>), dim3((unsigned)blocks), dim3(256), 0, st, g, fld, s0, s1,
                            mode, f);
     if (cols) {
@@ -1451,7 +1578,7 @@ int staged_range(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, in
     if (m1 > m0) {
         bool cols_done = false;
         e = launch_staged<T, NF, SHAPE>(v, fld, m0, m1, f, st, want, &cols_done);
-        if (e == DCCRGX_OK) e = launch_edge<T, NF, SHAPE>(v, fld, m0, m1, false, f, se, cols_done);
+        if (e == DCCRGX_OK) e = launch_edge<T, NF, SHAPE>(v, fld, m0, m1, false, f, se, cols_done, true);
         if (e != DCCRGX_OK) return e;
     }
     for (int side = 0; side < 2; side++) {
