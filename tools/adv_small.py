@@ -9,6 +9,10 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402,F401
 
+from dccrg_amd import _capi  # noqa: E402
+
+if os.environ.get("MAP_LIB"):  # A/B runs against another build of the library
+    _capi.LIB_PATH = os.environ["MAP_LIB"]
 import dccrg_amd as D  # noqa: E402
 from dccrg_amd import advection as A  # noqa: E402
 
