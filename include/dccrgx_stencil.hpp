@@ -1420,7 +1420,10 @@ struct StagedShape {
     // the register window holds 9 (NB + 2) elements per field: NB rows per
     // lane for 4-byte data, fewer (and more waves) for more bytes
     static constexpr int units = (int)((NF * sizeof(T) + 3) / 4);
-    static constexpr int NB = units <= 1 ? 4 : (units == 2 ? 2 : 1);
+#ifndef DCCRGX_STAGED_NB1
+#define DCCRGX_STAGED_NB1 4
+#endif
+    static constexpr int NB = units <= 1 ? DCCRGX_STAGED_NB1 : (units == 2 ? 2 : 1);
     static constexpr int NW = units <= 1 ? 4 : 8;
     static constexpr int TB = NW * NB;
     static constexpr int VEC = (int)(16 / sizeof(T));
