@@ -136,6 +136,35 @@ int us_fsum_staged(const dccrgx_grid* grid, int32_t hood_id, int32_t fu, int32_t
         nullptr, opt);
 }
 
+// the same over two staged f32 fields (4-byte elements: the LDS-DMA staged
+// kernel with two fields)
+int us_fsum32_staged(const dccrgx_grid* grid, int32_t hood_id, int32_t fu, int32_t fw, int32_t fout, int32_t region,
+                     int32_t staged)
+{
+    const float *u, *wt;
+    float* out;
+    int e = field_ptr(grid, fu, &u);
+    if (!e) e = field_ptr(grid, fw, &wt);
+    if (!e) e = field_ptr(grid, fout, &out);
+    if (e) return e;
+    dccrgx_user::StagedOptions opt;
+    opt.staged = staged != 0;
+    if (staged == 3) opt.workgroups = 1;
+    return dccrgx_user::for_each_cell_staged(
+        grid, hood_id, region, dccrgx_user::Fields<float, 2>{{u, wt}},
+        [=] __device__(const auto& cell) {
+            // no contraction: the staged and walked instantiations of this
+            // body round alike (with contraction the compiler fused them
+            // differently, 1-2 ulp apart)
+#pragma clang fp contract(off)
+            const float me = cell.value(0);
+            float s = me;
+            cell.for_each_neighbor([&](const auto& nb) { s += nb.value(1) * nb.value(0) - 0.25f * me; });
+            out[cell.slot] = s;
+        },
+        nullptr, opt);
+}
+
 // per cell: cid = the cell's id as for_each_cell reports it, dig = a digest of
 // its neighbor sequence h = (h ^ (mix64(id) + x * K1 + y * K2 + z * K3)) * P
 // over the neighbors in order (ids read from field fids, whose ghosts must be

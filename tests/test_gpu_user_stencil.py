@@ -53,13 +53,15 @@ def lib():
     L.us_gol_staged.argtypes = [C.c_void_p] + [C.c_int32] * 6
     L.us_digest_staged.argtypes = [C.c_void_p] + [C.c_int32] * 6
     L.us_fsum_staged.argtypes = [C.c_void_p] + [C.c_int32] * 6
+    L.us_fsum32_staged.argtypes = [C.c_void_p] + [C.c_int32] * 6
     return L
 
 
 def test_example_library_exports():
     """CPU: build() made the user-stencil program and it exports its entry points."""
     L = C.CDLL(LIB)
-    for s in ("us_gol", "us_digest", "us_region_cells", "us_gol_staged", "us_digest_staged", "us_fsum_staged"):
+    for s in ("us_gol", "us_digest", "us_region_cells", "us_gol_staged", "us_digest_staged", "us_fsum_staged",
+              "us_fsum32_staged"):
         assert hasattr(L, s)
 
 
@@ -382,6 +384,81 @@ def test_staged_f64_order(length, per, hood_len, P):
                     s += w0[i - 1] * u0[i - 1] - 0.25 * me
                 want[k] = s
             assert np.allclose(got1, want, rtol=1e-12, atol=1e-12)
+    finally:
+        for g in grids:
+            g.close()
+        for ctx in ctxs:
+            ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("staged", [1, 3])
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("length,per,hood_len", [((68, 29, 10), (False, False, True), 1),
+                                                 ((64, 40, 9), (False, False, False), 0),
+                                                 ((132, 37, 12), (False, True, True), 1),
+                                                 ((72, 20, 8), (True, False, True), 1)])
+def test_staged_f32_two_fields(length, per, hood_len, P, staged):
+    """Two staged f32 fields (the LDS-DMA kernel with two fields, its edge
+    columns and the row march; staged 3: long marches): the staged launch
+    gives the same bits as the walk, and both are within 1e-4 of a float64
+    sum in the reference's iteration order over the oracle's lists."""
+    import torch
+
+    import dccrg_amd as D
+    from dccrg_amd import _capi as X
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    n = int(np.prod(length))
+    rng = np.random.default_rng(12)
+    u0 = rng.standard_normal(n).astype(np.float32)
+    w0 = rng.uniform(0.5, 1.5, n).astype(np.float32)
+    og = O.Grid(length, 0, per, hood_len, list(range(1, n + 1)))
+    L = lib()
+    hood = D.DEFAULT_NEIGHBORHOOD_ID
+    ctxs, grids = [], []
+    for r in range(P):
+        ctx = D.Context(0, r, P)
+        ctxs.append(ctx)
+        g = (D.Dccrg().set_initial_length(length).set_periodic(*per).set_neighborhood_length(hood_len)
+             .initialize(ctx))
+        for f in ("u", "w", "o1", "o0"):
+            g.add_field(f, np.float32)
+        idx = g.local_cells().astype(np.int64) - 1
+        g.write_local("u", u0[idx])
+        g.write_local("w", w0[idx])
+        grids.append(g)
+    try:
+        msgs = {}
+        for r, g in enumerate(grids):
+            for p in g.get_cells_to_send():
+                buf = torch.empty(1 << 22, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
+                msgs[(r, p)] = (buf, g.pack_to(p, buf.data_ptr(), buf.numel(), fields=["u", "w"]))
+                g.ctx.synchronize()
+        for r, g in enumerate(grids):
+            g.halo_self(fields=["u", "w"])
+            for p in g.get_cells_to_receive():
+                buf, nb = msgs[(p, r)]
+                g.unpack_from(p, buf.data_ptr(), nb, fields=["u", "w"])
+            g.ctx.synchronize()
+        for g in grids:
+            f = g.field_id
+            for region in (X.REGION_INNER, X.REGION_OUTER):
+                assert L.us_fsum32_staged(g._h, hood, f("u"), f("w"), f("o1"), region, staged) == 0
+                assert L.us_fsum32_staged(g._h, hood, f("u"), f("w"), f("o0"), region, 0) == 0
+            g.ctx.synchronize()
+            got1, got0 = g.read_local("o1"), g.read_local("o0")
+            assert np.array_equal(got1.view(np.uint32), got0.view(np.uint32))
+            loc = g.local_cells()
+            want = np.empty(loc.size)
+            for k, c in enumerate(loc):
+                c = int(c)
+                me = float(u0[c - 1])
+                s = me
+                for i, _ in O.iteration_cache_lists(og.find_neighbors_of(c), og.find_neighbors_to(c))[0]:
+                    s += float(w0[i - 1]) * float(u0[i - 1]) - 0.25 * me
+                want[k] = s
+            assert np.allclose(got1.astype(np.float64), want, rtol=1e-4, atol=1e-4)
     finally:
         for g in grids:
             g.close()
