@@ -610,7 +610,8 @@ def user_stencil_gol(ctx, D):
         staged["workload"] = ("headline grid (2048^3, hood 1, periodic z) stepped by the game of life written as a "
                               "device user functor over staged values (include/dccrgx_stencil.hpp "
                               "for_each_cell_staged, examples/user_stencil.hip us_gol_staged): the staged kernel "
-                              "for the interior plus the boundary-shell walks, launches of one step")
+                              "(LDS-DMA planes; the interior and the edge columns), the edge rows' march and the "
+                              "wrap slices on a second stream, every launch of one step")
         walk["workload"] = ("the same functor reading every neighbor through its slot (for_each_cell, "
                             "examples/user_stencil.hip us_gol)")
         staged["walk"] = walk
