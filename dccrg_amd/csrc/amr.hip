@@ -616,6 +616,7 @@ struct StopTxn {
     std::vector<uint64_t> nr;  // the new dont_refine closure
     bool hybrid = false;       // a refine in place of a uniform grid, done at the commit
     std::vector<uint64_t> hybrid_cells;
+    std::vector<uint64_t> hybrid_unrefine;  // level-0 parents of the unrefined groups
 };
 
 int amr_ensure_explicit(dccrgx_grid* grid) { return ensure_explicit(grid); }
@@ -706,11 +707,27 @@ int dccrgx_refine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 {
     DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
-    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     DX_TRY(explicit_host_leaves(grid));
     *result = 0;
     if (cell == 0) return DCCRGX_OK;
+    if (grid->hy) {
+        // dccrg.hpp:2596-2675 with leaves of levels 0 and 1 only: no sibling
+        // has children, no level-1 cell is to be refined, nothing in the
+        // parent's windows is finer than level 1
+        if (hybrid_slot(grid, cell) < 0) return DCCRGX_OK;  // not a leaf
+        *result = 1;
+        if (map_level(grid->map, cell) == 0) return DCCRGX_OK;
+        Amr* Ap = nullptr;
+        DX_TRY(host_sets(grid, &Ap));
+        Amr& A = *Ap;
+        uint64_t parent, sib[8];
+        hybrid_group(grid, cell, &parent, sib);
+        for (uint64_t s : sib)
+            if (A.to_refine.count(s) || A.not_to_unrefine.count(s) || A.to_unrefine.count(s)) return DCCRGX_OK;
+        A.to_unrefine.insert(cell);
+        return DCCRGX_OK;
+    }
     if (grid->uniform) {  // every cell is at level 0: true for existing local cells (:2600-2602)
         *result = map_level(grid->map, cell) == 0 && cell <= grid->g.N &&
                   part_owner(grid->g.part, cell) == grid->ctx->rank;
@@ -755,11 +772,25 @@ int dccrgx_unrefine_completely(dccrgx_grid* grid, uint64_t cell, int32_t* result
 int dccrgx_dont_unrefine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 {
     DX_CHECK(grid && result, DCCRGX_EINVAL, "null argument");
-    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     DX_TRY(explicit_host_leaves(grid));
     *result = 0;
     if (cell == 0) return DCCRGX_OK;
+    if (grid->hy) {  // dccrg.hpp:2715-2759 on the hybrid's leaves
+        if (hybrid_slot(grid, cell) < 0) return DCCRGX_OK;
+        *result = 1;
+        if (map_level(grid->map, cell) == 0) return DCCRGX_OK;
+        Amr* Ap = nullptr;
+        DX_TRY(host_sets(grid, &Ap));
+        Amr& A = *Ap;
+        uint64_t parent, sib[8];
+        hybrid_group(grid, cell, &parent, sib);
+        for (uint64_t s : sib)
+            if (A.not_to_unrefine.count(s)) return DCCRGX_OK;
+        for (uint64_t s : sib) A.to_unrefine.erase(s);
+        A.not_to_unrefine.insert(cell);
+        return DCCRGX_OK;
+    }
     if (grid->uniform) {  // level 0: true for any existing cell (:2731-2733)
         *result = map_level(grid->map, cell) == 0 && cell <= grid->g.N;
         return DCCRGX_OK;
@@ -808,7 +839,6 @@ int dccrgx_dont_refine(dccrgx_grid* grid, uint64_t cell, int32_t* result)
 int dccrgx_amr_request_cells(dccrgx_grid* grid, int32_t kind, const uint64_t* ids, size_t n, int32_t* results)
 {
     DX_CHECK(grid && (ids || !n) && kind >= 0 && kind < 4, DCCRGX_EINVAL, "bad argument");
-    DX_NO_HYBRID(grid);
     DX_NOT_PENDING(grid);
     if (!grid->uniform) {  // the batch on the device (amr_dev.hip), results as the calls in this order
         amr_of(grid);
@@ -885,16 +915,20 @@ int dccrgx_stop_refining_prepare(dccrgx_grid* grid, const uint64_t* const* sets,
         return code;
     };
     if (grid->uniform && use_hybrid(grid)) {
-        // level-0 refines only: between levels 0 and 1 nothing is induced or
-        // overridden (2:1 holds for any set), so the decision is the
-        // requested cells minus the dont_refine ones (dccrg.hpp:10130-10693);
+        // level-0 refines and unrefines of level-1 groups: between levels 0
+        // and 1 nothing is induced or overridden (2:1 holds for any set, and
+        // no parent window holds a leaf finer than level 1 or a level-1 leaf
+        // to be refined), so the decision is the requested cells minus the
+        // dont_refine ones and every pending group (dccrg.hpp:9935-10693);
         // level-0 unrefines are no-ops (:2610-2612)
-        for (uint64_t c : A.to_unrefine.sorted())
-            if (map_level(grid->map, c) > 0)
-                return unwind_sets(set_error(DCCRGX_ESTATE, "unrefining cells of a uniform grid with refined cells "
-                                                            "(hybrid layout) is not supported"));
         for (uint64_t c : A.to_refine.sorted())
             if (!A.not_to_refine.count(c)) X.hybrid_cells.push_back(c);
+        for (uint64_t c : A.to_unrefine.sorted()) {
+            if (map_level(grid->map, c) == 0) continue;
+            uint64_t parent, sib[8];
+            hybrid_group(grid, c, &parent, sib);
+            X.hybrid_unrefine.push_back(parent);
+        }
         X.hybrid = true;
         X.nr = A.not_to_refine.sorted();
         if (n_new) *n_new = 8 * X.hybrid_cells.size();
@@ -974,9 +1008,8 @@ int dccrgx_stop_refining_finish(dccrgx_grid* grid, int32_t commit)
     hipStream_t st = grid->ctx->compute;
     if (commit && X.hybrid) {
         // the refine in place; on failure the grid and the requests stay
-        const int e = hybrid_refine(grid, X.hybrid_cells, A.new_cells);
+        const int e = hybrid_adapt(grid, X.hybrid_cells, X.hybrid_unrefine, A.new_cells, A.removed);
         if (e != DCCRGX_OK) return e;
-        A.removed.clear();
         A.to_refine.clear();
         A.to_unrefine.clear();
         A.not_to_unrefine.clear();

@@ -331,7 +331,7 @@ struct Amr {
 #define DX_NO_HYBRID(grid)                                                                                   \
     DX_CHECK(!((grid) && (grid)->hy), DCCRGX_ESTATE,                                                         \
              "not supported on a uniform grid with refined cells (hybrid layout, first slice: game of life, " \
-             "cell data by id, neighbor queries, further level-0 refines)")
+             "cell data by id, neighbor queries, level-0 refines and unrefines back to level 0)")
 #define DX_NOT_PENDING(grid)                                                                           \
     DX_CHECK(!((grid) && (grid)->amr && (grid)->amr->pending), DCCRGX_ESTATE,                                      \
              "a prepared stop_refining awaits dccrgx_stop_refining_finish")
@@ -479,7 +479,13 @@ struct Hybrid {
 int grid_create_box(dccrgx_ctx* ctx, const dccrgx_grid_params* prm, const uint64_t* leaves, size_t n,
                     dccrgx_grid** out);
 // refine level-0 `cells` (ascending, unique leaves) of a uniform grid in place
-int hybrid_refine(dccrgx_grid* grid, const std::vector<uint64_t>& cells, std::vector<uint64_t>& new_cells);
+// level-0 refines (cells) and unrefines of level-1 groups (their level-0
+// parents) of a hybrid grid: new_cells the children made, removed the
+// children removed, both ascending
+int hybrid_adapt(dccrgx_grid* grid, const std::vector<uint64_t>& cells, const std::vector<uint64_t>& unrefine,
+                 std::vector<uint64_t>& new_cells, std::vector<uint64_t>& removed);
+// a level-1 cell's level-0 parent and its 8 children (x fastest)
+void hybrid_group(const dccrgx_grid* grid, uint64_t child, uint64_t* parent, uint64_t sib[8]);
 void hybrid_destroy(dccrgx_grid* grid);
 // storage slot of a leaf of a hybrid grid, -1 if the id is not a leaf
 int64_t hybrid_slot(const dccrgx_grid* grid, uint64_t id);

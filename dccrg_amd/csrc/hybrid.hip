@@ -23,10 +23,18 @@
 // slab, then rewrites the overlay cells from their stored rows (the
 // iteration cache's order, as k_ex_gol).
 //
+// Unrefines of level-1 groups back to their level-0 parent: with no leaf
+// finer than level 1 and no level-1 refine, override_unrefines cancels none
+// (dccrg.hpp:9935-10124: nothing in a parent's windows is finer than the
+// children or of their level and to be refined), so every pending group goes;
+// the parent is value-initialised (:10590) in its slab slot and the
+// children's slots stay unused.
+//
 // First slice, refused elsewhere with DCCRGX_ESTATE (DX_NO_HYBRID): one
-// process, the default neighborhood only, refines of level-0 cells (no
-// unrefines, no level-1 refines), and the calls the game of life and cell
-// data by id need.  A refined cell's data is not kept after the refine.
+// process, the default neighborhood only, refines of level-0 cells and
+// unrefines of their children (no level-1 refines), and the calls the game
+// of life and cell data by id need.  The data of a refined cell or of
+// unrefined children is not kept after the step.
 #include "grid.hpp"
 
 namespace dccrgx {
@@ -38,6 +46,17 @@ unsigned grid_for(uint64_t n)
     uint64_t b = (n + 255) / 256;
     if (b > 65536) b = 65536;
     return (unsigned)(b ? b : 1);
+}
+
+// zero one element of every listed slot (value-initialised parents)
+__global__ void __launch_bounds__(256) k_hy_zero(char* __restrict__ base, uint64_t elem,
+                                                 const uint64_t* __restrict__ slots, uint64_t n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n * elem; i += stride) {
+        const uint64_t k = i / elem, b = i - k * elem;
+        base[slots[k] * elem + b] = 0;
+    }
 }
 
 // the overlay's rows: out / cnt of each overlay cell from its stored row
@@ -220,82 +239,16 @@ int hybrid_local_copy(const dccrgx_grid* grid, const Field& F, void* host, bool 
     return DCCRGX_OK;
 }
 
-int hybrid_refine(dccrgx_grid* grid, const std::vector<uint64_t>& cells, std::vector<uint64_t>& new_cells)
+namespace {
+
+// the overlay cells' rows of H (refined set not empty): an explicit grid over
+// the box of leaves around the refined cells
+int overlay_rows(dccrgx_grid* grid, Hybrid& Hr, int reach, const int32_t per[3])
 {
+    Hybrid* H = &Hr;
     Ctx* ctx = grid->ctx;
     hipStream_t st = ctx->compute;
     const MapParams& mp = grid->map;
-    DX_CHECK(grid->uniform && ctx->comm_size == 1, DCCRGX_ESTATE, "hybrid refinement: one process, uniform grid");
-    DX_CHECK(mp.max_lvl >= 1, DCCRGX_ESTATE, "maximum refinement level 0");
-    DX_CHECK(grid->hoods.size() == 1, DCCRGX_ESTATE,
-             "hybrid refinement supports the default neighborhood only (%zu neighborhoods)", grid->hoods.size());
-    for (const Field& F : grid->fields)
-        DX_CHECK(!F.variable, DCCRGX_ESTATE, "hybrid refinement of a grid with variable-size fields");
-    const Hood& hood = grid->hoods.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
-    std::unique_ptr<Hybrid> H(new Hybrid());
-    if (grid->hy) {  // the earlier refines stay (no unrefines in this slice)
-        H->refined = grid->hy->refined;
-        H->children = grid->hy->children;
-        H->child_slot = grid->hy->child_slot;
-        H->uniform_slots = grid->hy->uniform_slots;
-    } else {
-        H->uniform_slots = grid->n_slots;
-    }
-    // the new refined cells and their children (slots after the existing ones)
-    new_cells.clear();
-    std::vector<uint64_t> add;
-    for (uint64_t c : cells) {
-        DX_CHECK(map_level(mp, c) == 0 && c >= 1 && c <= grid->g.N, DCCRGX_EINVAL, "%llu is not a level-0 cell",
-                 (unsigned long long)c);
-        if (!H->is_refined(c)) add.push_back(c);
-    }
-    if (add.empty()) return DCCRGX_OK;
-    uint64_t next_slot = H->uniform_slots + H->children.size();
-    std::vector<std::pair<uint64_t, uint64_t>> ch_slot;
-    for (size_t i = 0; i < H->children.size(); i++) ch_slot.push_back({H->children[i], H->child_slot[i]});
-    for (uint64_t c : add) {
-        uint64_t ch[8];
-        children_of(mp, c, ch);
-        for (uint64_t x : ch) {
-            ch_slot.push_back({x, next_slot++});
-            new_cells.push_back(x);
-        }
-    }
-    std::sort(ch_slot.begin(), ch_slot.end());
-    std::sort(new_cells.begin(), new_cells.end());
-    H->children.clear();
-    H->child_slot.clear();
-    for (const auto& p : ch_slot) {
-        H->children.push_back(p.first);
-        H->child_slot.push_back(p.second);
-    }
-    H->refined.insert(H->refined.end(), add.begin(), add.end());
-    std::sort(H->refined.begin(), H->refined.end());
-    DX_CHECK(next_slot < (1ull << 32), DCCRGX_EINVAL, "hybrid refinement: %llu slots exceed 32-bit slot ids",
-             (unsigned long long)next_slot);
-
-    // reach of the neighborhood in level-0 cells: the overlay's level-0 cells
-    // are the ones an item of a refined cell reaches (the items are symmetric,
-    // so these are also the cells whose items reach a refined cell); the box
-    // extends three reaches from the refined cells
-    int reach = 1;
-    for (int32_t v : hood.items) reach = std::max(reach, std::abs(v));
-    const int32_t per[3] = {grid->params.periodic[0] ? 1 : 0, grid->params.periodic[1] ? 1 : 0,
-                            grid->params.periodic[2] ? 1 : 0};
-    std::vector<uint64_t> ov0;
-    for (uint64_t r : H->refined) {
-        int64_t x[3];
-        l0_indices(mp, r, x);
-        for (size_t k = 0; k + 2 < hood.items.size(); k += 3) {
-            const int64_t y[3] = {x[0] + hood.items[k], x[1] + hood.items[k + 1], x[2] + hood.items[k + 2]};
-            const uint64_t c = l0_cell(mp, per, y);
-            if (c && !H->is_refined(c)) ov0.push_back(c);
-        }
-    }
-    std::sort(ov0.begin(), ov0.end());
-    ov0.erase(std::unique(ov0.begin(), ov0.end()), ov0.end());
-    H->overlay = ov0;
-    H->overlay.insert(H->overlay.end(), H->children.begin(), H->children.end());
     const std::vector<uint64_t> box0 = around(mp, per, H->refined, 3 * reach);
     std::vector<uint64_t> box;
     box.reserve(box0.size() + H->children.size());
@@ -371,27 +324,164 @@ int hybrid_refine(dccrgx_grid* grid, const std::vector<uint64_t>& cells, std::ve
         H->ov_slot[q] = (uint32_t)s;
     }
 
-    // the new field arrays: the old slots copied, the children zeroed
-    // (value-initialised, dccrg.hpp:10375)
+    return DCCRGX_OK;
+}
+
+}  // namespace
+
+void hybrid_group(const dccrgx_grid* grid, uint64_t child, uint64_t* parent, uint64_t sib[8])
+{
+    const MapParams& mp = grid->map;
+    uint64_t idx[3];
+    int l;
+    map_indices(mp, child, idx, &l);
+    *parent = map_cell(mp, idx, 0);
+    children_of(mp, *parent, sib);
+}
+
+int hybrid_adapt(dccrgx_grid* grid, const std::vector<uint64_t>& cells, const std::vector<uint64_t>& unrefine,
+                 std::vector<uint64_t>& new_cells, std::vector<uint64_t>& removed)
+{
+    Ctx* ctx = grid->ctx;
+    hipStream_t st = ctx->compute;
+    const MapParams& mp = grid->map;
+    DX_CHECK(grid->uniform && ctx->comm_size == 1, DCCRGX_ESTATE, "hybrid refinement: one process, uniform grid");
+    DX_CHECK(mp.max_lvl >= 1, DCCRGX_ESTATE, "maximum refinement level 0");
+    DX_CHECK(grid->hoods.size() == 1, DCCRGX_ESTATE,
+             "hybrid refinement supports the default neighborhood only (%zu neighborhoods)", grid->hoods.size());
+    for (const Field& F : grid->fields)
+        DX_CHECK(!F.variable, DCCRGX_ESTATE, "hybrid refinement of a grid with variable-size fields");
+    const Hood& hood = grid->hoods.at(DCCRGX_DEFAULT_NEIGHBORHOOD_ID);
+    std::unique_ptr<Hybrid> H(new Hybrid());
+    if (grid->hy) {  // the earlier refines stay, but for the unrefined groups
+        H->refined = grid->hy->refined;
+        H->children = grid->hy->children;
+        H->child_slot = grid->hy->child_slot;
+        H->uniform_slots = grid->hy->uniform_slots;
+    } else {
+        H->uniform_slots = grid->n_slots;
+    }
+    // the unrefined groups: their parents leave the refined set, the
+    // children go (their slots stay unused)
+    new_cells.clear();
+    removed.clear();
+    std::vector<uint64_t> gone;  // unrefined parents
+    for (uint64_t p : unrefine) {
+        DX_CHECK(map_level(mp, p) == 0 && H->is_refined(p), DCCRGX_EINTERNAL, "hybrid: %llu is not a refined cell",
+                 (unsigned long long)p);
+        gone.push_back(p);
+        uint64_t ch[8];
+        children_of(mp, p, ch);
+        removed.insert(removed.end(), ch, ch + 8);
+    }
+    std::sort(gone.begin(), gone.end());
+    gone.erase(std::unique(gone.begin(), gone.end()), gone.end());
+    std::sort(removed.begin(), removed.end());
+    removed.erase(std::unique(removed.begin(), removed.end()), removed.end());
+    // the new refined cells and their children (slots after the last one)
+    std::vector<uint64_t> add;
+    for (uint64_t c : cells) {
+        DX_CHECK(map_level(mp, c) == 0 && c >= 1 && c <= grid->g.N, DCCRGX_EINVAL, "%llu is not a level-0 cell",
+                 (unsigned long long)c);
+        if (!H->is_refined(c)) add.push_back(c);
+    }
+    if (add.empty() && gone.empty()) return DCCRGX_OK;
+    uint64_t next_slot = grid->n_slots;
+    std::vector<std::pair<uint64_t, uint64_t>> ch_slot;
+    for (size_t i = 0; i < H->children.size(); i++)
+        if (!std::binary_search(removed.begin(), removed.end(), H->children[i]))
+            ch_slot.push_back({H->children[i], H->child_slot[i]});
+    {
+        std::vector<uint64_t> keep;
+        for (uint64_t r : H->refined)
+            if (!std::binary_search(gone.begin(), gone.end(), r)) keep.push_back(r);
+        H->refined.swap(keep);
+    }
+    for (uint64_t c : add) {
+        uint64_t ch[8];
+        children_of(mp, c, ch);
+        for (uint64_t x : ch) {
+            ch_slot.push_back({x, next_slot++});
+            new_cells.push_back(x);
+        }
+    }
+    std::sort(ch_slot.begin(), ch_slot.end());
+    std::sort(new_cells.begin(), new_cells.end());
+    H->children.clear();
+    H->child_slot.clear();
+    for (const auto& p : ch_slot) {
+        H->children.push_back(p.first);
+        H->child_slot.push_back(p.second);
+    }
+    H->refined.insert(H->refined.end(), add.begin(), add.end());
+    std::sort(H->refined.begin(), H->refined.end());
+    DX_CHECK(next_slot < (1ull << 32), DCCRGX_EINVAL, "hybrid refinement: %llu slots exceed 32-bit slot ids",
+             (unsigned long long)next_slot);
+
+    // reach of the neighborhood in level-0 cells: the overlay's level-0 cells
+    // are the ones an item of a refined cell reaches (the items are symmetric,
+    // so these are also the cells whose items reach a refined cell); the box
+    // extends three reaches from the refined cells
+    int reach = 1;
+    for (int32_t v : hood.items) reach = std::max(reach, std::abs(v));
+    const int32_t per[3] = {grid->params.periodic[0] ? 1 : 0, grid->params.periodic[1] ? 1 : 0,
+                            grid->params.periodic[2] ? 1 : 0};
+    std::vector<uint64_t> ov0;
+    for (uint64_t r : H->refined) {
+        int64_t x[3];
+        l0_indices(mp, r, x);
+        for (size_t k = 0; k + 2 < hood.items.size(); k += 3) {
+            const int64_t y[3] = {x[0] + hood.items[k], x[1] + hood.items[k + 1], x[2] + hood.items[k + 2]};
+            const uint64_t c = l0_cell(mp, per, y);
+            if (c && !H->is_refined(c)) ov0.push_back(c);
+        }
+    }
+    std::sort(ov0.begin(), ov0.end());
+    ov0.erase(std::unique(ov0.begin(), ov0.end()), ov0.end());
+    H->overlay = ov0;
+    H->overlay.insert(H->overlay.end(), H->children.begin(), H->children.end());
+    H->nof_row.assign(H->overlay.size() + 1, 0);
+    H->nto_row.assign(H->overlay.size() + 1, 0);
+    H->st_row.assign(H->overlay.size() + 1, 0);
+    H->ov_slot.resize(H->overlay.size());
+    if (!H->refined.empty()) DX_TRY(overlay_rows(grid, *H, reach, per));
     const uint64_t old_slots = grid->n_slots, new_slots = next_slot;
+    // the slab slots of the unrefined parents, zeroed in the new arrays
+    std::vector<uint64_t> pslot;
+    for (uint64_t p : gone) pslot.push_back(p - 1 + (uint64_t)(-grid->g.cbase * (int64_t)grid->g.S));
+    uint64_t* d_pslot = nullptr;
+
+    // the new field arrays: the old slots copied, the children zeroed
+    // (value-initialised, dccrg.hpp:10375), the unrefined parents too (:10590)
     std::vector<void*> np(grid->fields.size(), nullptr);
     auto drop = [&](int code) {
         for (void* p : np) dx_free(p);
+        dx_free(d_pslot);
         free_device(H.get());
         return code;
     };
+    if (!pslot.empty() && upload_vec(pslot, &d_pslot, st) != DCCRGX_OK)
+        return drop(set_error(DCCRGX_EHIP, "hybrid unrefinement: uploading the parents' slots"));
     for (size_t i = 0; i < grid->fields.size(); i++) {
         const Field& F = grid->fields[i];
         if (dx_malloc(&np[i], new_slots * F.elem) != hipSuccess)
             return drop(set_error(DCCRGX_ENOMEM, "hybrid refinement: field %zu of %llu slots", i,
                                   (unsigned long long)new_slots));
         if (hipMemcpyAsync(np[i], F.ptr, old_slots * F.elem, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-            hipMemsetAsync((char*)np[i] + old_slots * F.elem, 0, (new_slots - old_slots) * F.elem, st) != hipSuccess)
+            (new_slots > old_slots &&
+             hipMemsetAsync((char*)np[i] + old_slots * F.elem, 0, (new_slots - old_slots) * F.elem, st) != hipSuccess))
             return drop(set_error(DCCRGX_EHIP, "hybrid refinement: moving field %zu", i));
+        if (!pslot.empty()) {
+            hipLaunchKernelGGL(k_hy_zero, dim3(grid_for(pslot.size() * F.elem)), dim3(256), 0, st, (char*)np[i],
+                               (uint64_t)F.elem, d_pslot, (uint64_t)pslot.size());
+            if (hipGetLastError() != hipSuccess)
+                return drop(set_error(DCCRGX_EHIP, "hybrid unrefinement: zeroing field %zu", i));
+        }
     }
     if (upload_vec(H->st_row, &H->d_st_row, st) != DCCRGX_OK || upload_vec(H->st_slot, &H->d_st_slot, st) != DCCRGX_OK ||
         upload_vec(H->ov_slot, &H->d_ov_slot, st) != DCCRGX_OK || hipStreamSynchronize(st) != hipSuccess)
         return drop(set_error(DCCRGX_EHIP, "hybrid refinement: uploading the overlay rows"));
+    dx_free(d_pslot);
     // adopt
     for (size_t i = 0; i < grid->fields.size(); i++) {
         dx_free(grid->fields[i].ptr);

@@ -7,9 +7,11 @@ explicit machinery over a box around them.
 
 Checks: (1) with the test option "hybrid" forcing the path on small grids,
 the hybrid grid equals the same grid refined through the explicit layout
-(itself oracle-checked in test_gpu_amr.py) -- leaves, new cells, every leaf's
-neighbors_of / neighbors_to and several game-of-life steps -- over two rounds
-of refines, periodic and not, hood lengths 0, 1, 2; (2) a 1024^3 grid (1.07e9
+(itself oracle-checked in test_gpu_amr.py) -- leaves, new and removed cells,
+request results, every leaf's neighbors_of / neighbors_to and several
+game-of-life steps -- over two rounds of refines, then two rounds of
+unrefines back to level 0 (one group kept by dont_unrefine, a new refine
+beside them), periodic and not, hood lengths 0, 1, 2; (2) a 1024^3 grid (1.07e9
 cells, over the explicit layout's ~2.4e8-cell limit) refines one cell: the
 lists and the game of life around it equal a small grid refined the same way,
 a patch far from it equals a small uniform grid, and a whole-grid checksum
@@ -60,20 +62,52 @@ def test_hybrid_equals_explicit_refinement(length, per, hood):
             g.write_local("a", alive)
             grids.append(g)
         hy, ex = grids
-        picks = rng.choice(np.arange(1, n0 + 1), size=(2, 4), replace=False)
-        for rnd in range(2):
-            cells = [int(c) for c in picks[rnd]]
-            if rnd == 1:  # a neighbor of an earlier refined cell too (adjacent refined blocks)
-                cells.append(int(picks[0][0]) + 1 if (int(picks[0][0]) % length[0]) else int(picks[0][0]) - 1)
-            for g in grids:
-                for c in cells:
-                    g.refine_completely(c)
+        picks = rng.choice(np.arange(1, n0 + 1), size=(3, 4), replace=False)
+        refined = []
+        for rnd in range(4):
+            if rnd < 2:
+                cells = [int(c) for c in picks[rnd]]
+                if rnd == 1:  # a neighbor of an earlier refined cell too (adjacent refined blocks)
+                    cells.append(int(picks[0][0]) + 1 if (int(picks[0][0]) % length[0]) else int(picks[0][0]) - 1)
+                for g in grids:
+                    for c in cells:
+                        assert g.refine_completely(c)
+                refined += cells
+            else:
+                # unrefines: one child of a group, every child of another, a
+                # group kept by dont_unrefine, and (round 2) a new refine
+                # beside them; round 3 unrefines what is left
+                groups = sorted(set(refined))
+                if rnd == 2:
+                    un, keep = groups[:3], groups[3]
+                else:
+                    un, keep = groups, None
+                for g in grids:
+                    res = []
+                    for k, p in enumerate(un):
+                        kids = [int(x) for x in g.mapping.get_all_children(p)]
+                        for c in (kids if k == 1 else kids[k % 8:k % 8 + 1]):
+                            res.append(g.unrefine_completely(c))
+                    if keep is not None:
+                        kids = [int(x) for x in g.mapping.get_all_children(keep)]
+                        res.append(g.unrefine_completely(kids[2]))
+                        res.append(g.dont_unrefine(kids[5]))
+                    if rnd == 2:
+                        res.append(g.refine_completely(int(picks[2][0])))
+                    g._res = res
+                assert hy._res == ex._res
+                refined = [c for c in groups if c not in un]
+                if rnd == 2:
+                    refined.append(int(picks[2][0]))
             set_test_option("hybrid", 1)
             new_h = hy.stop_refining()
             set_test_option("hybrid", None)
             new_e = ex.stop_refining()
             assert hy.info.uniform == 2 and ex.info.uniform == 0
             assert np.array_equal(np.sort(new_h), np.sort(new_e))
+            assert np.array_equal(np.sort(hy.get_removed_cells()), np.sort(ex.get_removed_cells()))
+            if rnd >= 2:
+                assert len(ex.get_removed_cells()) > 0
             leaves = ex.local_cells()
             assert np.array_equal(hy.local_cells(), leaves)
             assert hy.info.n_local == leaves.size
@@ -185,6 +219,26 @@ def test_refine_one_cell_of_a_grid_beyond_the_explicit_layout():
         sb = big.checksum(cb)
         s_r, s_u = small_r.checksum(cr), small_u.checksum(cu)
         assert sb[0] == s_r[0] + s_u[0]
+        # unrefine back to level 0 (one child's request takes the group): the
+        # children go, the parent comes back value-initialised, and a step of
+        # the game of life around it equals the small grid's
+        kb = [int(x) for x in mb.get_all_children(rc_big)]
+        ks = [int(x) for x in ms.get_all_children(rc_small)]
+        assert big.unrefine_completely(kb[3]) and small_r.unrefine_completely(ks[3])
+        assert big.stop_refining().size == 0
+        small_r.stop_refining()
+        assert np.array_equal(np.sort(big.get_removed_cells()), np.sort(np.array(kb, dtype=np.uint64)))
+        assert big.info.n_local == L ** 3
+        assert int(np.concatenate(big.read_cells(cb, np.array([rc_big], dtype=np.uint64)))[0]) == 0
+        nxt = "a" if cb == "b" else "b"
+        big.gol_step(cb, nxt, "n")
+        small_r.gol_step(cr, nxt, "n")
+        inner_r = small_r.local_cells()
+        assert inner_r.size == P ** 3
+        for name in (nxt, "n"):
+            want = np.concatenate(small_r.read_cells(name, inner_r))
+            got = np.concatenate(big.read_cells(name, tr(inner_r, o_at)))
+            assert np.array_equal(got, want), name
     finally:
         for g in (big, small_r, small_u):
             g.close()
