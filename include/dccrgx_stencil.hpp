@@ -412,9 +412,14 @@ int for_each_cell(const dccrgx_grid* grid, int32_t hood_id, int32_t region, F f,
  * (16-byte loads, +1 apron) into LDS, every lane reads the 3 x (NB + 2)
  * values around its column of NB cells into a register window of three
  * planes, and the functor's neighbor loop is unrolled over compile-time
- * offsets into that window.  The cells within reach of a grid boundary (the
- * ring of each slice, the slices next to a C boundary) run the exact-order
- * walk in separate launches; so do other neighborhoods and refined grids.
+ * offsets into that window.  4-byte fields on rows of a multiple of 4 cells
+ * run k_staged_g instead: the planes come into LDS by LDS-DMA buffer loads,
+ * two in flight, and with A not periodic the edge columns are its own cells.
+ * The other cells within reach of a grid boundary (the rest of the ring of
+ * each slice, the slices next to a C boundary) run in separate launches (the
+ * edge rows' march k_staged_rows, the exact-order walk); so do other
+ * neighborhoods and refined grids.  Build knobs (defaults measured fastest on
+ * 2048^3): DCCRGX_STAGED_GLDS, _COLS, _ROWS, _G_MINWG, _NB1, _PF.
  * ---------------------------------------------------------------------- */
 
 template <class T, int NF>
