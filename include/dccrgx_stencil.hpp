@@ -1034,13 +1034,16 @@ struct ImgEdgeCell {
     }
 };
 
-// four workgroups of four waves per CU (at most 128 VGPRs: the game-of-life
-// functor with the column cells needs 130 unbounded, and fits with no spill)
+// MINWG: the waves per SIMD the build must allow (HIP's second launch bound).
+// With 4 (at most 128 VGPRs) the game-of-life functor with the column cells
+// fits with no spill (130 VGPRs unbounded, 3 waves); a functor that would
+// spill under the bound runs the unbounded build (launch_staged asks the
+// runtime for the bounded build's scratch once)
 #ifndef DCCRGX_STAGED_G_MINWG
 #define DCCRGX_STAGED_G_MINWG 4
 #endif
-template <class T, int NF, int SHAPE, int NW, int NB, class F>
-__global__ void __launch_bounds__(64 * NW, DCCRGX_STAGED_G_MINWG) k_staged_g(StagedGeo g, Fields<T, NF> fld, F f)
+template <class T, int NF, int SHAPE, int NW, int NB, int MINWG, class F>
+__global__ void __launch_bounds__(64 * NW, MINWG) k_staged_g(StagedGeo g, Fields<T, NF> fld, F f)
 {
     typedef StagedTileG<T, NF, NW, NB> Tile;
     // planes q - 2 .. q read at step q (the column cells read all three),
@@ -1486,8 +1489,22 @@ int launch_staged(const dccrgx_stencil_view& v, Fields<T, NF> fld, int64_t s0, i
         if (v.la % 4 == 0 && g.S * 4 < (1ull << 31)) {
             g.cols_in = DCCRGX_STAGED_COLS && !v.per[0];
             *cols_done = g.cols_in != 0;
-            hipLaunchKernelGGL((k_staged_g<T, NF, SHAPE, Sh::NW, Sh::NB, F>), dim3(g.nwg), dim3(64 * Sh::NW), 0, st,
-                               g, fld, f);
+            // the bounded build unless it spills (scratch), asked once per
+            // instantiation
+            static const bool bounded = [] {
+                hipFuncAttributes at{};
+                return hipFuncGetAttributes(
+                           &at, reinterpret_cast<const void*>(
+                                    &k_staged_g<T, NF, SHAPE, Sh::NW, Sh::NB, DCCRGX_STAGED_G_MINWG, F>)) ==
+                           hipSuccess &&
+                       at.localSizeBytes == 0;
+            }();
+            if (bounded)
+                hipLaunchKernelGGL((k_staged_g<T, NF, SHAPE, Sh::NW, Sh::NB, DCCRGX_STAGED_G_MINWG, F>), dim3(g.nwg),
+                                   dim3(64 * Sh::NW), 0, st, g, fld, f);
+            else
+                hipLaunchKernelGGL((k_staged_g<T, NF, SHAPE, Sh::NW, Sh::NB, 1, F>), dim3(g.nwg), dim3(64 * Sh::NW), 0,
+                                   st, g, fld, f);
             return DCCRGX_OK;
         }
     }
